@@ -1,0 +1,223 @@
+"""cmsisdsp_amd — Python face of the MI355X CMSIS-DSP backend (libcmsisdsp_mi355x.so).
+
+Two layers, both thin over the C ABI (include/arm_math.h, include/arm_math_mi355x.h):
+
+* drop-in, numpy in / numpy out, named and shaped like the reference's PythonWrapper
+  (`cmsisdsp.arm_cfft_f32(inst, x, ifft, bitrev)` -> new array; PythonWrapper/cmsisdsp_pkg/
+  src/cmsisdsp_transform.c:2074):  arm_cfft_f32 / _q31 / _q15, arm_rfft_fast_f32,
+  arm_fir_f32 / _q15, arm_mat_mult_f32 with their *_init functions;
+* batched, torch device tensors in place on a HIP stream: cfft_batch, rfft_fast_batch,
+  fir_batch, mat_mult_batch.
+
+The library is REQUIRED: importing works without a GPU, but every compute call goes to
+the HIP kernels; there is no CPU fallback (a missing .so raises at import).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi
+from ._abi import (arm_cfft_instance_f32, arm_cfft_instance_q15, arm_cfft_instance_q31,  # noqa: F401
+                   arm_fir_instance_f32, arm_fir_instance_q15, arm_matrix_instance_f32,
+                   arm_rfft_fast_instance_f32, ARM_MATH_SUCCESS, ARM_MATH_ARGUMENT_ERROR,
+                   ARM_MATH_SIZE_MISMATCH)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CMSISDSP_MI355X_LIB",
+                          os.path.join(os.path.dirname(_HERE), "lib", "libcmsisdsp_mi355x.so"))
+
+
+def _load():
+    # One HIP runtime per process: torch bundles its own libamdhip64 (SONAME
+    # libamdhip64.so.7, same as ROCm's).  Loading torch first makes our library bind to
+    # that already-loaded runtime instead of pulling in a second ROCr instance (two in
+    # one process fail with "no ROCm-capable device").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"cmsisdsp_amd: native library missing at {LIB_PATH} "
+                          f"(build it with `make -C cmsis-dsp_amd` or __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    _abi.bind(lib, _abi.DROPIN)
+    _abi.bind(lib, _abi.BATCHED)
+    return lib
+
+
+lib = _load()
+
+
+def version():
+    return lib.arm_mi355x_version().decode()
+
+
+def last_error():
+    return lib.arm_mi355x_last_error(), lib.arm_mi355x_last_error_string().decode()
+
+
+def _check_void(what):
+    code, msg = last_error()
+    if code:
+        lib.arm_mi355x_clear_error()
+        raise RuntimeError(f"{what}: device error {code}: {msg}")
+
+
+def const_instance(name):
+    """A pre-initialised const instance exported by the library (arm_const_structs.h)."""
+    kind = {"f32": arm_cfft_instance_f32, "q31": arm_cfft_instance_q31, "q15": arm_cfft_instance_q15}
+    if name.startswith("arm_rfft_fast_sR_f32"):
+        return arm_rfft_fast_instance_f32.in_dll(lib, name)
+    return kind[name.split("_")[3]].in_dll(lib, name)
+
+
+# ------------------------------------------------------------------ drop-in (numpy)
+def arm_cfft_init_f32(S, n):
+    return lib.arm_cfft_init_f32(C.byref(S), n)
+
+
+def arm_cfft_init_q31(S, n):
+    return lib.arm_cfft_init_q31(C.byref(S), n)
+
+
+def arm_cfft_init_q15(S, n):
+    return lib.arm_cfft_init_q15(C.byref(S), n)
+
+
+def _cfft(fn, dtype, S, x, ifft, bitrev):
+    buf = np.ascontiguousarray(x, dtype=dtype).copy()
+    fn(C.byref(S), buf.ctypes.data, ifft, bitrev)
+    _check_void(fn.__name__)
+    return buf
+
+
+def arm_cfft_f32(S, x, ifftFlag, bitReverseFlag):
+    return _cfft(lib.arm_cfft_f32, np.float32, S, x, ifftFlag, bitReverseFlag)
+
+
+def arm_cfft_q31(S, x, ifftFlag, bitReverseFlag):
+    return _cfft(lib.arm_cfft_q31, np.int32, S, x, ifftFlag, bitReverseFlag)
+
+
+def arm_cfft_q15(S, x, ifftFlag, bitReverseFlag):
+    return _cfft(lib.arm_cfft_q15, np.int16, S, x, ifftFlag, bitReverseFlag)
+
+
+def arm_rfft_fast_init_f32(S, n):
+    return lib.arm_rfft_fast_init_f32(C.byref(S), n)
+
+
+def arm_rfft_fast_f32(S, x, ifftFlag):
+    """Returns the output; like the reference, the forward transform also destroys the
+    input buffer (here a private copy)."""
+    p = np.ascontiguousarray(x, dtype=np.float32).copy()
+    out = np.zeros(S.fftLenRFFT, dtype=np.float32)
+    lib.arm_rfft_fast_f32(C.byref(S), p.ctypes.data, out.ctypes.data, ifftFlag)
+    _check_void("arm_rfft_fast_f32")
+    return out
+
+
+class FirF32:
+    """Streaming FIR f32 (arm_fir_init_f32 + arm_fir_f32): state carried across calls."""
+
+    def __init__(self, coeffs, block_size):
+        self.coeffs = np.ascontiguousarray(coeffs, dtype=np.float32)
+        self.block_size = block_size
+        self.state = np.zeros(len(self.coeffs) + block_size - 1, dtype=np.float32)
+        self.S = arm_fir_instance_f32()
+        lib.arm_fir_init_f32(C.byref(self.S), len(self.coeffs), self.coeffs.ctypes.data,
+                             self.state.ctypes.data, block_size)
+
+    def __call__(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        assert len(x) <= self.block_size
+        y = np.empty_like(x)
+        lib.arm_fir_f32(C.byref(self.S), x.ctypes.data, y.ctypes.data, len(x))
+        _check_void("arm_fir_f32")
+        return y
+
+
+class FirQ15(FirF32):
+    def __init__(self, coeffs, block_size):
+        self.coeffs = np.ascontiguousarray(coeffs, dtype=np.int16)
+        self.block_size = block_size
+        self.state = np.zeros(len(self.coeffs) + block_size - 1, dtype=np.int16)
+        self.S = arm_fir_instance_q15()
+        lib.arm_fir_init_q15(C.byref(self.S), len(self.coeffs), self.coeffs.ctypes.data,
+                             self.state.ctypes.data, block_size)
+
+    def __call__(self, x):
+        x = np.ascontiguousarray(x, dtype=np.int16)
+        y = np.empty_like(x)
+        lib.arm_fir_q15(C.byref(self.S), x.ctypes.data, y.ctypes.data, len(x))
+        _check_void("arm_fir_q15")
+        return y
+
+
+def arm_mat_mult_f32(a, b):
+    """(status, C) = A @ B through arm_mat_mult_f32 (row-major f32)."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    c = np.zeros((a.shape[0], b.shape[1]), dtype=np.float32)
+    A, B, Cm = arm_matrix_instance_f32(), arm_matrix_instance_f32(), arm_matrix_instance_f32()
+    lib.arm_mat_init_f32(C.byref(A), a.shape[0], a.shape[1], a.ctypes.data)
+    lib.arm_mat_init_f32(C.byref(B), b.shape[0], b.shape[1], b.ctypes.data)
+    lib.arm_mat_init_f32(C.byref(Cm), c.shape[0], c.shape[1], c.ctypes.data)
+    st = lib.arm_mat_mult_f32(C.byref(A), C.byref(B), C.byref(Cm))
+    _check_void("arm_mat_mult_f32")
+    return st, c
+
+
+# ------------------------------------------------------------------ batched (torch, device)
+def _stream_ptr(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return C.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream))
+
+
+_CFFT_BATCH = {"f32": ("arm_cfft_f32_batch", 2), "q31": ("arm_cfft_q31_batch", 2),
+               "q15": ("arm_cfft_q15_batch", 2)}
+
+
+def cfft_batch(S, data, ifft, bitrev, stream=None, kind=None):
+    """In-place CFFT of every row of `data` (torch device tensor [batch, 2*N])."""
+    if kind is None:
+        kind = {arm_cfft_instance_f32: "f32", arm_cfft_instance_q31: "q31",
+                arm_cfft_instance_q15: "q15"}[type(S)]
+    fn = getattr(lib, _CFFT_BATCH[kind][0])
+    batch = data.numel() // (2 * S.fftLen)
+    st = fn(C.byref(S), C.c_void_p(data.data_ptr()), batch, ifft, bitrev, _stream_ptr(stream))
+    if st != ARM_MATH_SUCCESS:
+        raise RuntimeError(f"{fn.__name__} -> {st}: {last_error()[1]}")
+
+
+def rfft_fast_batch(S, p, out, ifft, stream=None):
+    batch = p.numel() // S.fftLenRFFT
+    st = lib.arm_rfft_fast_f32_batch(C.byref(S), C.c_void_p(p.data_ptr()), C.c_void_p(out.data_ptr()), batch,
+                                     ifft, _stream_ptr(stream))
+    if st != ARM_MATH_SUCCESS:
+        raise RuntimeError(f"arm_rfft_fast_f32_batch -> {st}: {last_error()[1]}")
+
+
+def fir_batch(S, src, dst, hist, stream=None, q15=False):
+    """src/dst: [batch, blockSize] device tensors; hist: [batch, numTaps-1] device state."""
+    batch, block = src.shape
+    fn = lib.arm_fir_q15_batch if q15 else lib.arm_fir_f32_batch
+    st = fn(C.byref(S), C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()), block, batch,
+            C.c_void_p(hist.data_ptr() if hist is not None and hist.numel() else 0), _stream_ptr(stream))
+    if st != ARM_MATH_SUCCESS:
+        raise RuntimeError(f"{fn.__name__} -> {st}: {last_error()[1]}")
+
+
+def mat_mult_batch(a, b, c, stream=None):
+    """c[i] = a[i] @ b[i] for device tensors [batch, M, K] x [batch, K, N] -> [batch, M, N]."""
+    batch, m, k = a.shape
+    n = b.shape[2]
+    A, B, Cm = arm_matrix_instance_f32(m, k, C.cast(a.data_ptr(), _abi.c_f32p)), \
+        arm_matrix_instance_f32(k, n, C.cast(b.data_ptr(), _abi.c_f32p)), \
+        arm_matrix_instance_f32(m, n, C.cast(c.data_ptr(), _abi.c_f32p))
+    st = lib.arm_mat_mult_f32_batch(C.byref(A), C.byref(B), C.byref(Cm), batch, _stream_ptr(stream))
+    if st != ARM_MATH_SUCCESS:
+        raise RuntimeError(f"arm_mat_mult_f32_batch -> {st}: {last_error()[1]}")

@@ -1,0 +1,116 @@
+"""ctypes mirror of include/arm_math.h (struct layouts + prototypes).
+
+The same declarations bind three libraries with the identical C ABI:
+  * libcmsisdsp_mi355x.so  — this backend (the product);
+  * oracle/_ref/libcmsisdsp_ref.so — the reference scalar C path (test infrastructure);
+  * oracle/_build/liboracle.so — the CPU restatement (test infrastructure, `oracle_` prefix).
+"""
+import ctypes as C
+
+c_f32p = C.POINTER(C.c_float)
+c_i32p = C.POINTER(C.c_int32)
+c_i16p = C.POINTER(C.c_int16)
+c_u16p = C.POINTER(C.c_uint16)
+
+ARM_MATH_SUCCESS = 0
+ARM_MATH_ARGUMENT_ERROR = -1
+ARM_MATH_SIZE_MISMATCH = -3
+
+
+def _cfft_struct(name, twp):
+    # Include/dsp/transform_functions.h:410-424 (scalar layout)
+    return type(name, (C.Structure,), {"_fields_": [
+        ("fftLen", C.c_uint16), ("pTwiddle", twp), ("pBitRevTable", c_u16p), ("bitRevLength", C.c_uint16)]})
+
+
+arm_cfft_instance_f32 = _cfft_struct("arm_cfft_instance_f32", c_f32p)
+arm_cfft_instance_q31 = _cfft_struct("arm_cfft_instance_q31", c_i32p)
+arm_cfft_instance_q15 = _cfft_struct("arm_cfft_instance_q15", c_i16p)
+
+
+class arm_rfft_fast_instance_f32(C.Structure):
+    # Include/dsp/transform_functions.h:813-818
+    _fields_ = [("Sint", arm_cfft_instance_f32), ("fftLenRFFT", C.c_uint16), ("pTwiddleRFFT", c_f32p)]
+
+
+class arm_fir_instance_f32(C.Structure):
+    # Include/dsp/filtering_functions.h:86-91
+    _fields_ = [("numTaps", C.c_uint16), ("pState", c_f32p), ("pCoeffs", c_f32p)]
+
+
+class arm_fir_instance_q15(C.Structure):
+    # Include/dsp/filtering_functions.h:66-71
+    _fields_ = [("numTaps", C.c_uint16), ("pState", c_i16p), ("pCoeffs", c_i16p)]
+
+
+class arm_matrix_instance_f32(C.Structure):
+    # Include/dsp/matrix_functions.h:118-123
+    _fields_ = [("numRows", C.c_uint16), ("numCols", C.c_uint16), ("pData", c_f32p)]
+
+
+P = C.POINTER
+SIZES = (16, 32, 64, 128, 256, 512, 1024, 2048, 4096)
+RFFT_SIZES = (32, 64, 128, 256, 512, 1024, 2048, 4096)
+
+# name -> (restype, argtypes): the drop-in surface of include/arm_math.h
+DROPIN = {
+    "arm_cfft_init_f32": (C.c_int, [P(arm_cfft_instance_f32), C.c_uint16]),
+    "arm_cfft_init_q31": (C.c_int, [P(arm_cfft_instance_q31), C.c_uint16]),
+    "arm_cfft_init_q15": (C.c_int, [P(arm_cfft_instance_q15), C.c_uint16]),
+    "arm_cfft_f32": (None, [P(arm_cfft_instance_f32), C.c_void_p, C.c_uint8, C.c_uint8]),
+    "arm_cfft_q31": (None, [P(arm_cfft_instance_q31), C.c_void_p, C.c_uint8, C.c_uint8]),
+    "arm_cfft_q15": (None, [P(arm_cfft_instance_q15), C.c_void_p, C.c_uint8, C.c_uint8]),
+    "arm_rfft_fast_init_f32": (C.c_int, [P(arm_rfft_fast_instance_f32), C.c_uint16]),
+    "arm_rfft_fast_f32": (None, [P(arm_rfft_fast_instance_f32), C.c_void_p, C.c_void_p, C.c_uint8]),
+    "arm_fir_init_f32": (None, [P(arm_fir_instance_f32), C.c_uint16, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "arm_fir_f32": (None, [P(arm_fir_instance_f32), C.c_void_p, C.c_void_p, C.c_uint32]),
+    "arm_fir_init_q15": (C.c_int, [P(arm_fir_instance_q15), C.c_uint16, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "arm_fir_q15": (None, [P(arm_fir_instance_q15), C.c_void_p, C.c_void_p, C.c_uint32]),
+    "arm_mat_init_f32": (None, [P(arm_matrix_instance_f32), C.c_uint16, C.c_uint16, C.c_void_p]),
+    "arm_mat_mult_f32": (C.c_int, [P(arm_matrix_instance_f32), P(arm_matrix_instance_f32),
+                                   P(arm_matrix_instance_f32)]),
+}
+for _t in ("f32", "q31", "q15"):
+    _inst = {"f32": arm_cfft_instance_f32, "q31": arm_cfft_instance_q31, "q15": arm_cfft_instance_q15}[_t]
+    for _n in SIZES:
+        DROPIN[f"arm_cfft_init_{_n}_{_t}"] = (C.c_int, [P(_inst)])
+for _n in RFFT_SIZES:
+    DROPIN[f"arm_rfft_fast_init_{_n}_f32"] = (C.c_int, [P(arm_rfft_fast_instance_f32)])
+
+# the additive batched device API of include/arm_math_mi355x.h
+BATCHED = {
+    "arm_cfft_f32_batch": (C.c_int, [P(arm_cfft_instance_f32), C.c_void_p, C.c_uint32, C.c_uint8, C.c_uint8,
+                                     C.c_void_p]),
+    "arm_cfft_q31_batch": (C.c_int, [P(arm_cfft_instance_q31), C.c_void_p, C.c_uint32, C.c_uint8, C.c_uint8,
+                                     C.c_void_p]),
+    "arm_cfft_q15_batch": (C.c_int, [P(arm_cfft_instance_q15), C.c_void_p, C.c_uint32, C.c_uint8, C.c_uint8,
+                                     C.c_void_p]),
+    "arm_rfft_fast_f32_batch": (C.c_int, [P(arm_rfft_fast_instance_f32), C.c_void_p, C.c_void_p, C.c_uint32,
+                                          C.c_uint8, C.c_void_p]),
+    "arm_fir_f32_batch": (C.c_int, [P(arm_fir_instance_f32), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                    C.c_void_p, C.c_void_p]),
+    "arm_fir_q15_batch": (C.c_int, [P(arm_fir_instance_q15), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                    C.c_void_p, C.c_void_p]),
+    "arm_mat_mult_f32_batch": (C.c_int, [P(arm_matrix_instance_f32), P(arm_matrix_instance_f32),
+                                         P(arm_matrix_instance_f32), C.c_uint32, C.c_void_p]),
+    "arm_mi355x_last_error": (C.c_int, []),
+    "arm_mi355x_last_error_string": (C.c_char_p, []),
+    "arm_mi355x_clear_error": (None, []),
+    "arm_mi355x_version": (C.c_char_p, []),
+}
+
+# exported data symbols (arm_const_structs.h / arm_common_tables.h)
+DATA = ([f"arm_cfft_sR_{t}_len{n}" for t in ("f32", "q31", "q15") for n in SIZES]
+        + [f"arm_rfft_fast_sR_f32_len{n}" for n in RFFT_SIZES]
+        + [f"twiddleCoef_{n}" for n in SIZES] + [f"twiddleCoef_{n}_q31" for n in SIZES]
+        + [f"twiddleCoef_{n}_q15" for n in SIZES] + [f"twiddleCoef_rfft_{n}" for n in RFFT_SIZES]
+        + [f"armBitRevIndexTable{n}" for n in SIZES] + [f"armBitRevIndexTable_fixed_{n}" for n in SIZES])
+
+
+def bind(lib, table, prefix=""):
+    """Attach restype/argtypes for every function of `table` (optionally name-prefixed)."""
+    for name, (res, args) in table.items():
+        fn = getattr(lib, prefix + name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib

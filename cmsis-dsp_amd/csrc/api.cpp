@@ -1,0 +1,310 @@
+// C ABI of libcmsisdsp_mi355x.so: the drop-in processing functions of arm_math.h and the
+// batched device API of arm_math_mi355x.h.  Every GPU failure is caught here and mapped
+// to the reference's status values (or the thread-local error channel for void functions);
+// nothing aborts.  There is no CPU fallback: all compute runs in the HIP kernels.
+#include <string.h>
+
+#include "../../include/arm_math.h"
+#include "../../include/arm_math_mi355x.h"
+#include "common.hpp"
+#include "kernels.hpp"
+#include "runtime.hpp"
+
+using namespace mi355x;
+
+namespace {
+
+bool cfft_len_ok(uint32_t n) {
+  return n == 16 || n == 32 || n == 64 || n == 128 || n == 256 || n == 512 || n == 1024 || n == 2048 || n == 4096;
+}
+
+#define MI_CHECK(expr, where)                        \
+  do {                                               \
+    hipError_t e_ = (expr);                          \
+    if (e_ != hipSuccess) { set_error(e_, where); return false; } \
+  } while (0)
+
+struct CfftPrep {
+  const void* tw = nullptr;
+  const uint16_t* perm = nullptr;
+  uint32_t flags = 0;
+};
+
+// kind: 0 f32, 1 q31, 2 q15
+bool cfft_prepare(uint32_t n, const void* pTwiddle, const uint16_t* pBitRev, uint16_t bitRevLen, int kind,
+                  uint8_t ifftFlag, uint8_t bitReverseFlag, CfftPrep& out) {
+  // twiddle words: f32 N complex (twiddleCoef_N[2N]); fixed-point 3N/4 complex
+  // (twiddleCoef_N_q31[3N/2], arm_common_tables.h:61-116)
+  const size_t twb = kind == 0 ? 8u * n : (kind == 1 ? 4u * 3u * n / 2u : 2u * 3u * n / 2u);
+  out.tw = device_table(pTwiddle, twb);
+  if (!out.tw) return false;   // device_table recorded the cause
+  out.flags = (ifftFlag == 1u ? kIfft : 0u) | (bitReverseFlag ? kBitrev : 0u);   // arm_cfft_f32.c:1252,1282
+  if (bitReverseFlag) {
+    bool canon = true, ok = true;
+    out.perm = device_perm((int)n, pBitRev, bitRevLen, kind == 0 ? 0 : 1, &canon, &ok);
+    if (!ok) { set_error(hipErrorInvalidValue, "bit-reversal table"); return false; }
+  }
+  return true;
+}
+
+hipError_t cfft_launch(int kind, uint32_t n, void* d, uint32_t batch, const CfftPrep& pr, hipStream_t st) {
+  switch (kind) {
+    case 0: return cfft_f32_launch((int)n, (float*)d, batch, (const float*)pr.tw, pr.perm, pr.flags, st);
+    case 1: return cfft_q31_launch((int)n, (int32_t*)d, batch, (const int32_t*)pr.tw, pr.perm, pr.flags, st);
+    default: return cfft_q15_launch((int)n, (int16_t*)d, batch, (const int16_t*)pr.tw, pr.perm, pr.flags, st);
+  }
+}
+
+// synchronous single-transform drop-in path (host or device buffer)
+template <typename Inst>
+void cfft_sync(const Inst* S, void* p1, uint8_t ifftFlag, uint8_t bitReverseFlag, int kind, size_t word) {
+  if (!S || !p1 || !cfft_len_ok(S->fftLen)) return;       // reference: silent no-op
+  const uint32_t n = S->fftLen;
+  CfftPrep pr;
+  if (!cfft_prepare(n, S->pTwiddle, S->pBitRevTable, S->bitRevLength, kind, ifftFlag, bitReverseFlag, pr)) return;
+  hipStream_t st = sync_stream();
+  const size_t bytes = 2 * word * n;
+  if (is_device_ptr(p1)) {
+    hipError_t e = cfft_launch(kind, n, p1, 1, pr, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) set_error(e, "arm_cfft");
+    return;
+  }
+  void* d = scratch(bytes, 0);
+  if (!d) { set_error(hipErrorOutOfMemory, "arm_cfft scratch"); return; }
+  hipError_t e = hipMemcpyAsync(d, p1, bytes, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = cfft_launch(kind, n, d, 1, pr, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(p1, d, bytes, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) set_error(e, "arm_cfft");
+}
+
+template <typename Inst>
+arm_status cfft_batch(const Inst* S, void* d_p1, uint32_t batch, uint8_t ifftFlag, uint8_t bitReverseFlag,
+                      void* stream, int kind) {
+  if (!S || (!d_p1 && batch) || !cfft_len_ok(S->fftLen)) return ARM_MATH_ARGUMENT_ERROR;
+  CfftPrep pr;
+  if (!cfft_prepare(S->fftLen, S->pTwiddle, S->pBitRevTable, S->bitRevLength, kind, ifftFlag, bitReverseFlag, pr))
+    return ARM_MATH_ARGUMENT_ERROR;
+  hipError_t e = cfft_launch(kind, S->fftLen, d_p1, batch, pr, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(e, "arm_cfft_batch"); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
+}
+
+bool rfft_len_ok(uint32_t n) { return n >= 32 && n <= 4096 && (n & (n - 1)) == 0; }
+
+// arm_rfft_fast_f32.c:675-699 on `batch` signals; d_p / d_out device pointers
+bool rfft_run(const arm_rfft_fast_instance_f32* S, float* d_p, float* d_out, uint32_t batch, uint8_t ifftFlag,
+              hipStream_t st) {
+  const uint32_t n = S->fftLenRFFT, h = S->Sint.fftLen;
+  if (h != n / 2 || !cfft_len_ok(h)) { set_error(hipErrorInvalidValue, "rfft instance"); return false; }
+  const void* twr = device_table(S->pTwiddleRFFT, sizeof(float) * n);
+  if (!twr) return false;
+  CfftPrep pr;
+  // the inner CFFT receives ifftFlag unchanged and bitReverseFlag = 1 (:689, :694)
+  if (!cfft_prepare(h, S->Sint.pTwiddle, S->Sint.pBitRevTable, S->Sint.bitRevLength, 0, ifftFlag, 1, pr))
+    return false;
+  if (ifftFlag) {
+    MI_CHECK(rfft_f32_merge_launch((int)n, d_p, d_out, batch, (const float*)twr, st), "rfft merge");
+    MI_CHECK(cfft_f32_launch((int)h, d_out, batch, (const float*)pr.tw, pr.perm, pr.flags, st), "rfft cfft");
+  } else {
+    MI_CHECK(cfft_f32_launch((int)h, d_p, batch, (const float*)pr.tw, pr.perm, pr.flags, st), "rfft cfft");
+    MI_CHECK(rfft_f32_stage_launch((int)n, d_p, d_out, batch, (const float*)twr, st), "rfft stage");
+  }
+  return true;
+}
+
+template <typename T>
+const T* device_coeffs(const T* c, int n, int slot, hipStream_t st, bool* ok) {
+  *ok = true;
+  if (is_device_ptr(c)) return c;
+  T* d = (T*)scratch(sizeof(T) * (size_t)n, slot);
+  if (!d || hipMemcpyAsync(d, c, sizeof(T) * (size_t)n, hipMemcpyHostToDevice, st) != hipSuccess) {
+    *ok = false;
+    return nullptr;
+  }
+  return d;
+}
+
+// drop-in FIR: state = [history(T-1) ; block(B)] on host or device (arm_fir_f32.c:911-1280).
+// After the call the state holds [new history ; block input], as the reference leaves it.
+template <typename T, typename Inst>
+void fir_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B) {
+  if (!S || !S->pState || !S->pCoeffs || S->numTaps == 0 || B == 0) return;
+  const int taps = S->numTaps, T1 = taps - 1;
+  hipStream_t st = sync_stream();
+  bool ok = true;
+  const T* dc = device_coeffs<T>(S->pCoeffs, taps, 1, st, &ok);
+  if (!ok) { set_error(hipErrorOutOfMemory, "arm_fir coeffs"); return; }
+  const bool dstate = is_device_ptr(S->pState), dsrc = is_device_ptr(pSrc), ddst = is_device_ptr(pDst);
+  const size_t sb = sizeof(T) * (size_t)B, hb = sizeof(T) * (size_t)T1;
+  T* dhist = dstate ? S->pState : (T*)scratch(hb + 16, 2);
+  const T* dsr = dsrc ? pSrc : (const T*)scratch(sb, 3);
+  T* dds = ddst ? pDst : (T*)scratch(sb, 4);
+  if (!dhist || !dsr || !dds) { set_error(hipErrorOutOfMemory, "arm_fir scratch"); return; }
+  hipError_t e = hipSuccess;
+  if (!dstate && T1 > 0) e = hipMemcpyAsync(dhist, S->pState, hb, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && !dsrc) e = hipMemcpyAsync((void*)dsr, pSrc, sb, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) {
+    if constexpr (sizeof(T) == 4) e = fir_f32_launch((const float*)dc, taps, (const float*)dsr, (float*)dds, B, 1, (float*)dhist, st);
+    else e = fir_q15_launch((const int16_t*)dc, taps, (const int16_t*)dsr, (int16_t*)dds, B, 1, (int16_t*)dhist, st);
+  }
+  if (e == hipSuccess && !ddst) e = hipMemcpyAsync(pDst, dds, sb, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && !dstate && T1 > 0) e = hipMemcpyAsync(S->pState, dhist, hb, hipMemcpyDeviceToHost, st);
+  // state tail keeps the block input (the reference copies it there, :947-975)
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(S->pState + T1, dsr, sb, dstate ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) set_error(e, "arm_fir");
+}
+
+template <typename T, typename Inst>
+arm_status fir_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uint32_t batch, T* d_hist, void* stream) {
+  if (!S || !S->pCoeffs || S->numTaps == 0 || (batch && B && (!d_src || !d_dst))) return ARM_MATH_ARGUMENT_ERROR;
+  if (S->numTaps > 1 && batch && !d_hist) return ARM_MATH_ARGUMENT_ERROR;
+  hipStream_t st = (hipStream_t)stream;
+  bool ok = true;
+  const T* dc = device_coeffs<T>(S->pCoeffs, S->numTaps, 5, st, &ok);
+  if (!ok) { set_error(hipErrorOutOfMemory, "arm_fir_batch coeffs"); return ARM_MATH_ARGUMENT_ERROR; }
+  hipError_t e;
+  if constexpr (sizeof(T) == 4) e = fir_f32_launch((const float*)dc, S->numTaps, (const float*)d_src, (float*)d_dst, B, batch, (float*)d_hist, st);
+  else e = fir_q15_launch((const int16_t*)dc, S->numTaps, (const int16_t*)d_src, (int16_t*)d_dst, B, batch, (int16_t*)d_hist, st);
+  if (e != hipSuccess) { set_error(e, "arm_fir_batch"); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
+}
+
+bool mat_shapes_ok(const arm_matrix_instance_f32* a, const arm_matrix_instance_f32* b,
+                   const arm_matrix_instance_f32* c) {
+  return a->numCols == b->numRows && a->numRows == c->numRows && b->numCols == c->numCols;
+}
+
+// FIR init: zero numTaps + blockSize - 1 state words (arm_fir_init_f32.c:74-95,
+// arm_fir_init_q15.c:119-139, the !ARM_MATH_DSP branch: no even-numTaps check).
+// The state buffer is caller memory, host or device.
+template <typename T, typename Inst>
+void fir_init(Inst* S, uint16_t numTaps, const T* pCoeffs, T* pState, uint32_t blockSize) {
+  S->numTaps = numTaps;
+  S->pCoeffs = pCoeffs;
+  S->pState = pState;
+  if (!pState) return;
+  const size_t bytes = sizeof(T) * ((size_t)numTaps + blockSize - 1);
+  if (is_device_ptr(pState)) {
+    hipError_t e = hipMemset(pState, 0, bytes);
+    if (e != hipSuccess) set_error(e, "arm_fir_init");
+  } else {
+    memset(pState, 0, bytes);
+  }
+}
+}  // namespace
+
+extern "C" {
+
+const char* arm_mi355x_version(void) { return "cmsisdsp-mi355x 0.1.0 gfx950"; }
+
+void arm_cfft_f32(const arm_cfft_instance_f32* S, float32_t* p1, uint8_t ifftFlag, uint8_t bitReverseFlag) {
+  cfft_sync(S, p1, ifftFlag, bitReverseFlag, 0, sizeof(float));
+}
+void arm_cfft_q31(const arm_cfft_instance_q31* S, q31_t* p1, uint8_t ifftFlag, uint8_t bitReverseFlag) {
+  cfft_sync(S, p1, ifftFlag, bitReverseFlag, 1, sizeof(int32_t));
+}
+void arm_cfft_q15(const arm_cfft_instance_q15* S, q15_t* p1, uint8_t ifftFlag, uint8_t bitReverseFlag) {
+  cfft_sync(S, p1, ifftFlag, bitReverseFlag, 2, sizeof(int16_t));
+}
+
+arm_status arm_cfft_f32_batch(const arm_cfft_instance_f32* S, float32_t* d_p1, uint32_t batch, uint8_t ifftFlag,
+                              uint8_t bitReverseFlag, void* stream) {
+  return cfft_batch(S, d_p1, batch, ifftFlag, bitReverseFlag, stream, 0);
+}
+arm_status arm_cfft_q31_batch(const arm_cfft_instance_q31* S, q31_t* d_p1, uint32_t batch, uint8_t ifftFlag,
+                              uint8_t bitReverseFlag, void* stream) {
+  return cfft_batch(S, d_p1, batch, ifftFlag, bitReverseFlag, stream, 1);
+}
+arm_status arm_cfft_q15_batch(const arm_cfft_instance_q15* S, q15_t* d_p1, uint32_t batch, uint8_t ifftFlag,
+                              uint8_t bitReverseFlag, void* stream) {
+  return cfft_batch(S, d_p1, batch, ifftFlag, bitReverseFlag, stream, 2);
+}
+
+void arm_rfft_fast_f32(const arm_rfft_fast_instance_f32* S, float32_t* p, float32_t* pOut, uint8_t ifftFlag) {
+  if (!S || !p || !pOut || !rfft_len_ok(S->fftLenRFFT)) return;
+  const size_t bytes = sizeof(float) * S->fftLenRFFT;
+  hipStream_t st = sync_stream();
+  const bool dp = is_device_ptr(p), dout = is_device_ptr(pOut);
+  float* d_p = dp ? p : (float*)scratch(bytes, 0);
+  float* d_o = dout ? pOut : (float*)scratch(bytes, 1);
+  if (!d_p || !d_o) { set_error(hipErrorOutOfMemory, "arm_rfft_fast scratch"); return; }
+  hipError_t e = hipSuccess;
+  if (!dp) e = hipMemcpyAsync(d_p, p, bytes, hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) { set_error(e, "arm_rfft_fast"); return; }
+  if (!rfft_run(S, d_p, d_o, 1, ifftFlag, st)) return;
+  if (!dp && !ifftFlag) e = hipMemcpyAsync(p, d_p, bytes, hipMemcpyDeviceToHost, st);   // forward overwrites p
+  if (e == hipSuccess && !dout) e = hipMemcpyAsync(pOut, d_o, bytes, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) set_error(e, "arm_rfft_fast");
+}
+
+arm_status arm_rfft_fast_f32_batch(const arm_rfft_fast_instance_f32* S, float32_t* d_p, float32_t* d_out,
+                                   uint32_t batch, uint8_t ifftFlag, void* stream) {
+  if (!S || !rfft_len_ok(S->fftLenRFFT) || (batch && (!d_p || !d_out))) return ARM_MATH_ARGUMENT_ERROR;
+  if (batch == 0) return ARM_MATH_SUCCESS;
+  return rfft_run(S, d_p, d_out, batch, ifftFlag, (hipStream_t)stream) ? ARM_MATH_SUCCESS : ARM_MATH_ARGUMENT_ERROR;
+}
+
+void arm_fir_init_f32(arm_fir_instance_f32* S, uint16_t numTaps, const float32_t* pCoeffs, float32_t* pState,
+                      uint32_t blockSize) {
+  if (S) fir_init<float>(S, numTaps, pCoeffs, pState, blockSize);
+}
+arm_status arm_fir_init_q15(arm_fir_instance_q15* S, uint16_t numTaps, const q15_t* pCoeffs, q15_t* pState,
+                            uint32_t blockSize) {
+  if (!S) return ARM_MATH_ARGUMENT_ERROR;
+  fir_init<int16_t>(S, numTaps, pCoeffs, pState, blockSize);
+  return ARM_MATH_SUCCESS;
+}
+
+void arm_fir_f32(const arm_fir_instance_f32* S, const float32_t* pSrc, float32_t* pDst, uint32_t blockSize) {
+  fir_sync<float>(S, pSrc, pDst, blockSize);
+}
+void arm_fir_q15(const arm_fir_instance_q15* S, const q15_t* pSrc, q15_t* pDst, uint32_t blockSize) {
+  fir_sync<int16_t>(S, pSrc, pDst, blockSize);
+}
+arm_status arm_fir_f32_batch(const arm_fir_instance_f32* S, const float32_t* d_src, float32_t* d_dst,
+                             uint32_t blockSize, uint32_t batch, float32_t* d_hist, void* stream) {
+  return fir_batch<float>(S, d_src, d_dst, blockSize, batch, d_hist, stream);
+}
+arm_status arm_fir_q15_batch(const arm_fir_instance_q15* S, const q15_t* d_src, q15_t* d_dst, uint32_t blockSize,
+                             uint32_t batch, q15_t* d_hist, void* stream) {
+  return fir_batch<int16_t>(S, d_src, d_dst, blockSize, batch, d_hist, stream);
+}
+
+arm_status arm_mat_mult_f32(const arm_matrix_instance_f32* pSrcA, const arm_matrix_instance_f32* pSrcB,
+                            arm_matrix_instance_f32* pDst) {
+  if (!pSrcA || !pSrcB || !pDst) return ARM_MATH_ARGUMENT_ERROR;
+  if (!mat_shapes_ok(pSrcA, pSrcB, pDst)) return ARM_MATH_SIZE_MISMATCH;
+  const int m = pSrcA->numRows, k = pSrcA->numCols, n = pSrcB->numCols;
+  const size_t ab = sizeof(float) * (size_t)m * k, bb = sizeof(float) * (size_t)k * n, cb = sizeof(float) * (size_t)m * n;
+  hipStream_t st = sync_stream();
+  const bool da = is_device_ptr(pSrcA->pData), db = is_device_ptr(pSrcB->pData), dc = is_device_ptr(pDst->pData);
+  float* A = da ? pSrcA->pData : (float*)scratch(ab + 16, 0);
+  float* B = db ? pSrcB->pData : (float*)scratch(bb + 16, 1);
+  float* C = dc ? pDst->pData : (float*)scratch(cb + 16, 2);
+  if (!A || !B || !C) { set_error(hipErrorOutOfMemory, "arm_mat_mult scratch"); return ARM_MATH_ARGUMENT_ERROR; }
+  hipError_t e = hipSuccess;
+  if (!da && ab) e = hipMemcpyAsync(A, pSrcA->pData, ab, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && !db && bb) e = hipMemcpyAsync(B, pSrcB->pData, bb, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = mat_mult_f32_launch(m, k, n, A, B, C, 1, st);
+  if (e == hipSuccess && !dc && cb) e = hipMemcpyAsync(pDst->pData, C, cb, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) { set_error(e, "arm_mat_mult_f32"); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
+}
+
+arm_status arm_mat_mult_f32_batch(const arm_matrix_instance_f32* pSrcA, const arm_matrix_instance_f32* pSrcB,
+                                  arm_matrix_instance_f32* pDst, uint32_t batch, void* stream) {
+  if (!pSrcA || !pSrcB || !pDst) return ARM_MATH_ARGUMENT_ERROR;
+  if (!mat_shapes_ok(pSrcA, pSrcB, pDst)) return ARM_MATH_SIZE_MISMATCH;
+  hipError_t e = mat_mult_f32_launch(pSrcA->numRows, pSrcA->numCols, pSrcB->numCols, pSrcA->pData, pSrcB->pData,
+                                     pDst->pData, batch, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(e, "arm_mat_mult_f32_batch"); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
+}
+
+}  // extern "C"

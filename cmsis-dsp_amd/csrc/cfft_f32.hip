@@ -1,0 +1,275 @@
+// Batched complex FFT, f32 — MI355X (gfx950) kernels.
+//
+// Replaces the scalar path of Source/TransformFunctions/arm_cfft_f32.c:1243-1298
+// (radix8by2 :846-958, radix8by4 :960-1201) and arm_cfft_radix8_f32.c:51-291, plus the
+// table-driven arm_bitreversal_32 (arm_bitreversal2.c:84-108).
+//
+// Design: one workgroup = 256 threads = TPB transforms, 32 KiB of
+// LDS.  Each transform is read from HBM once (16-B coalesced loads) and written once;
+// every butterfly pass runs LDS -> registers -> LDS.  Every floating-point operation is
+// the reference's, in the reference's association order, with contraction disabled —
+// the output is bit-identical to the host scalar C path, not merely within tolerance.
+// The bit-reversal table is applied as the permutation it induces (folded into the
+// store), computed analytically for the reference tables and taken from a device copy
+// for any other table.
+#include "common.hpp"
+#include "kernels.hpp"
+
+#pragma clang fp contract(off)
+
+namespace mi355x {
+
+constexpr float kC81 = 0.70710678118f;  // arm_cfft_radix8_f32.c:68
+
+// --- radix-8 DIF butterfly, arm_cfft_radix8_f32.c:188-281 (twiddled) and :87-138 (j==0).
+// v[m] = x[i1 + m*n2]; the reference's temporaries are reproduced one for one.
+template <bool TW>
+__device__ __forceinline__ void r8(float2 (&v)[8], const float2* __restrict__ w) {
+  float r1, r2, r3, r4, r5, r6, r7, r8v, t1, t2;
+  float s1, s2, s3, s4, s5, s6, s7, s8;
+  r1 = v[0].x + v[4].x;  r5 = v[0].x - v[4].x;
+  r2 = v[1].x + v[5].x;  r6 = v[1].x - v[5].x;
+  r3 = v[2].x + v[6].x;  r7 = v[2].x - v[6].x;
+  r4 = v[3].x + v[7].x;  r8v = v[3].x - v[7].x;
+  t1 = r1 - r3;  r1 = r1 + r3;
+  r3 = r2 - r4;  r2 = r2 + r4;
+  float o0x = r1 + r2;
+  r2 = r1 - r2;                      // (j==0: stored to i5 directly)
+  s1 = v[0].y + v[4].y;  s5 = v[0].y - v[4].y;
+  s2 = v[1].y + v[5].y;  s6 = v[1].y - v[5].y;
+  s3 = v[2].y + v[6].y;  s7 = v[2].y - v[6].y;
+  s4 = v[3].y + v[7].y;  s8 = v[3].y - v[7].y;
+  t2 = s1 - s3;  s1 = s1 + s3;
+  s3 = s2 - s4;  s2 = s2 + s4;
+  r1 = t1 + s3;  t1 = t1 - s3;
+  float o0y = s1 + s2;
+  s2 = s1 - s2;
+  s1 = t2 - r3;  t2 = t2 + r3;
+  // outputs i5 (r2,s2), i3 (r1,s1), i7 (t1,t2)
+  float2 o4, o2, o6;
+  if (TW) {
+    float2 c5 = w[3], c3 = w[1], c7 = w[5];
+    o4.x = c5.x * r2 + c5.y * s2;  o4.y = c5.x * s2 - c5.y * r2;
+    o2.x = c3.x * r1 + c3.y * s1;  o2.y = c3.x * s1 - c3.y * r1;
+    o6.x = c7.x * t1 + c7.y * t2;  o6.y = c7.x * t2 - c7.y * t1;
+  } else {
+    o4 = make_float2(r2, s2);  o2 = make_float2(r1, s1);  o6 = make_float2(t1, t2);
+  }
+  r1 = (r6 - r8v) * kC81;  r6 = (r6 + r8v) * kC81;
+  s1 = (s6 - s8) * kC81;   s6 = (s6 + s8) * kC81;
+  t1 = r5 - r1;  r5 = r5 + r1;
+  r8v = r7 - r6; r7 = r7 + r6;
+  t2 = s5 - s1;  s5 = s5 + s1;
+  s8 = s7 - s6;  s7 = s7 + s6;
+  r1 = r5 + s7;  r5 = r5 - s7;
+  r6 = t1 + s8;  t1 = t1 - s8;
+  s1 = s5 - r7;  s5 = s5 + r7;
+  s6 = t2 - r8v; t2 = t2 + r8v;
+  float2 o1, o7, o5, o3;
+  if (TW) {
+    float2 c2 = w[0], c8 = w[6], c6 = w[4], c4 = w[2];
+    o1.x = c2.x * r1 + c2.y * s1;  o1.y = c2.x * s1 - c2.y * r1;
+    o7.x = c8.x * r5 + c8.y * s5;  o7.y = c8.x * s5 - c8.y * r5;
+    o5.x = c6.x * r6 + c6.y * s6;  o5.y = c6.x * s6 - c6.y * r6;
+    o3.x = c4.x * t1 + c4.y * t2;  o3.y = c4.x * t2 - c4.y * t1;
+  } else {
+    o1 = make_float2(r1, s1);  o7 = make_float2(r5, s5);
+    o5 = make_float2(r6, s6);  o3 = make_float2(t1, t2);
+  }
+  v[0] = make_float2(o0x, o0y);
+  v[1] = o1; v[2] = o2; v[3] = o3; v[4] = o4; v[5] = o5; v[6] = o6; v[7] = o7;
+}
+
+template <int N> struct PlanF32 {
+  static constexpr int FIRST = (N == 16 || N == 128 || N == 1024) ? 2
+                             : (N == 32 || N == 256 || N == 2048) ? 4 : 1;
+  static constexpr int L = N / FIRST;              // length handed to the radix-8 core
+  static constexpr int STAGES = Log2<L>::v / 3;    // radix-8 stages
+  static constexpr int LPT = N / 16;               // lanes per transform
+  static constexpr int TPB = kBlock / LPT;         // transforms per workgroup
+};
+
+// position (before bit reversal) that holds frequency k: inverse of the mixed-radix digit
+// reversal [FIRST, 8, 8, ...] the reference tables encode (checked on the host).
+template <int N> __device__ __forceinline__ int f32_src(int k) {
+  constexpr int FIRST = PlanF32<N>::FIRST;
+  int p = 0, rem = N;
+  if (FIRST > 1) { rem /= FIRST; p += (k % FIRST) * rem; k /= FIRST; }
+#pragma unroll
+  for (int s = 0; s < PlanF32<N>::STAGES; ++s) { rem >>= 3; p += (k & 7) * rem; k >>= 3; }
+  return p;
+}
+
+template <int N>
+__global__ __launch_bounds__(kBlock) void cfft_f32_kernel(float2* __restrict__ data, uint32_t batch,
+                                                          const float2* __restrict__ tw,
+                                                          const uint16_t* __restrict__ perm,
+                                                          uint32_t flags) {
+  using P = PlanF32<N>;
+  __shared__ __attribute__((aligned(16))) float2 lds[P::TPB * N];
+  const int tid = threadIdx.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * P::TPB;
+  const int valid = (int)min<uint64_t>((uint64_t)P::TPB, batch - t0);
+  const bool ifft = flags & kIfft;
+
+  // ---- load: 16-B coalesced, conj on the fly (arm_cfft_f32.c:1252-1261)
+  {
+    const float4* src = reinterpret_cast<const float4*>(data + t0 * N);
+    float4* dst = reinterpret_cast<float4*>(lds);
+    const int n4 = valid * N / 2;
+#pragma unroll 4
+    for (int i = tid; i < n4; i += kBlock) {
+      float4 v = src[i];
+      if (ifft) { v.y = -v.y; v.w = -v.w; }
+      dst[i] = v;
+    }
+  }
+  __syncthreads();
+
+  const int tr = tid / P::LPT, lane = tid % P::LPT;
+  float2* x = lds + tr * N;
+
+  // ---- first pass
+  if constexpr (P::FIRST == 2) {
+    // arm_cfft_radix8by2_f32, arm_cfft_f32.c:867-951
+    constexpr int Q = N / 4, H = N / 2;
+#pragma unroll
+    for (int it = 0; it < Q / P::LPT; ++it) {
+      const int k = lane + it * P::LPT;
+      const float2 w = tw[k];
+      float2 a = x[k], b = x[k + H], c = x[k + Q], d = x[k + H + Q];
+      x[k] = make_float2(a.x + b.x, a.y + b.y);
+      float2 t2 = make_float2(a.x - b.x, a.y - b.y);
+      x[k + Q] = make_float2(c.x + d.x, c.y + d.y);
+      float2 t4 = make_float2(d.x - c.x, d.y - c.y);
+      x[k + H] = make_float2(t2.x * w.x + t2.y * w.y, t2.y * w.x - t2.x * w.y);
+      x[k + H + Q] = make_float2(t4.x * w.y - t4.y * w.x, t4.y * w.y + t4.x * w.x);
+    }
+    __syncthreads();
+  } else if constexpr (P::FIRST == 4) {
+    // arm_cfft_radix8by4_f32, arm_cfft_f32.c:992-1188.  Work item w <= N/8: "top" row k=w
+    // (k=0 untwiddled, k=N/8 the "middle" row); w > N/8: "bottom" row kb = Q - i.
+    constexpr int Q = N / 4, E = N / 8;
+#pragma unroll
+    for (int it = 0; it < Q / P::LPT; ++it) {
+      const int w = lane + it * P::LPT;
+      if (w <= E) {
+        const int k = w;
+        float2 A = x[k], B = x[k + Q], C = x[k + 2 * Q], D = x[k + 3 * Q];
+        float ap0 = A.x + C.x, as0 = A.x - C.x, ap1 = A.y + C.y, as1 = A.y - C.y;
+        float2 t2 = make_float2(as0 + B.y - D.y, as1 - B.x + D.x);
+        float2 t3 = make_float2(ap0 - B.x - D.x, ap1 - B.y - D.y);
+        float2 t4 = make_float2(as0 - B.y + D.y, as1 + B.x - D.x);
+        x[k] = make_float2(ap0 + B.x + D.x, ap1 + B.y + D.y);
+        if (k == 0) {
+          x[k + Q] = t2; x[k + 2 * Q] = t3; x[k + 3 * Q] = t4;
+        } else {
+          const float2 w2 = tw[k], w3 = tw[2 * k], w4 = tw[3 * k];
+          x[k + Q]     = make_float2(t2.x * w2.x + t2.y * w2.y, t2.y * w2.x - t2.x * w2.y);
+          x[k + 2 * Q] = make_float2(t3.x * w3.x + t3.y * w3.y, t3.y * w3.x - t3.x * w3.y);
+          x[k + 3 * Q] = make_float2(t4.x * w4.x + t4.y * w4.y, t4.y * w4.x - t4.x * w4.y);
+        }
+      } else {
+        const int i = w - E, kb = Q - i;
+        float2 A = x[kb], B = x[kb + Q], C = x[kb + 2 * Q], D = x[kb + 3 * Q];
+        float ap1 = A.x + C.x, as1 = A.x - C.x, ap0 = A.y + C.y, as0 = A.y - C.y;
+        float t22 = B.y - D.y + as1;
+        float t23 = A.y - C.y - B.x + D.x;
+        float t32 = ap1 - B.x - D.x;
+        float t33 = ap0 - B.y - D.y;
+        float t42 = B.y - D.y - as1;
+        float t43 = D.x - B.x - as0;
+        x[kb] = make_float2(ap1 + B.x + D.x, ap0 + B.y + D.y);
+        const float2 w2 = tw[i], w3 = tw[2 * i], w4 = tw[3 * i];
+        x[kb + Q]     = make_float2(t22 * w2.y + t23 * w2.x, t23 * w2.y - t22 * w2.x);
+        x[kb + 2 * Q] = make_float2(t33 * w3.y - t32 * w3.x, -t33 * w3.x - t32 * w3.y);
+        x[kb + 3 * Q] = make_float2(t42 * w4.y + t43 * w4.x, t43 * w4.y - t42 * w4.x);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- radix-8 stages (arm_cfft_radix8_f32.c:72-290), on FIRST sub-transforms of length L
+  constexpr int L = P::L;
+#pragma unroll
+  for (int s = 0; s < P::STAGES; ++s) {
+    const int n1 = L >> (3 * s), n2 = n1 >> 3;
+    const int mod = P::FIRST << (3 * s);
+#pragma unroll
+    for (int r = 0; r < (N / 8) / P::LPT; ++r) {
+      const int b = lane + r * P::LPT;
+      const int c = b / (L / 8), rr = b % (L / 8);
+      const int j = rr % n2, q = rr / n2;
+      float2* base = x + c * L + q * n1 + j;
+      float2 v[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) v[m] = base[m * n2];
+      if (j == 0) {
+        r8<false>(v, nullptr);
+      } else {
+        float2 w[7];
+#pragma unroll
+        for (int m = 0; m < 7; ++m) w[m] = tw[(m + 1) * j * mod];
+        r8<true>(v, w);
+      }
+#pragma unroll
+      for (int m = 0; m < 8; ++m) base[m * n2] = v[m];
+    }
+    __syncthreads();
+  }
+
+  // ---- store: bit reversal as a gather from LDS, conj + 1/N scale (arm_cfft_f32.c:1282-1297)
+  {
+    float4* dst = reinterpret_cast<float4*>(data + t0 * N);
+    const bool brev = flags & kBitrev;
+    const float invL = 1.0f / (float)N;
+    const int n4 = valid * N / 2;
+#pragma unroll 4
+    for (int i = tid; i < n4; i += kBlock) {
+      const int e = 2 * i, t = e / N, k = e % N;   // outputs k, k+1 of transform t
+      float2 a, b;
+      if (brev) {
+        const int sa = perm ? perm[k] : f32_src<N>(k);
+        const int sb = perm ? perm[k + 1] : f32_src<N>(k + 1);
+        a = lds[t * N + sa]; b = lds[t * N + sb];
+      } else {
+        a = lds[e]; b = lds[e + 1];
+      }
+      if (ifft) {
+        a.x = a.x * invL; a.y = -a.y * invL;
+        b.x = b.x * invL; b.y = -b.y * invL;
+      }
+      dst[i] = make_float4(a.x, a.y, b.x, b.y);
+    }
+  }
+}
+
+template <int N>
+static hipError_t launch_f32(float2* data, uint32_t batch, const float2* tw, const uint16_t* perm,
+                             uint32_t flags, hipStream_t st) {
+  using P = PlanF32<N>;
+  const uint32_t grid = (uint32_t)((batch + P::TPB - 1) / P::TPB);
+  hipLaunchKernelGGL(cfft_f32_kernel<N>, dim3(grid), dim3(kBlock), 0, st, data, batch, tw, perm, flags);
+  return hipGetLastError();
+}
+
+hipError_t cfft_f32_launch(int n, float* data, uint32_t batch, const float* tw, const uint16_t* perm,
+                           uint32_t flags, hipStream_t st) {
+  float2* d = reinterpret_cast<float2*>(data);
+  const float2* w = reinterpret_cast<const float2*>(tw);
+  if (batch == 0) return hipSuccess;
+  switch (n) {
+    case 16:   return launch_f32<16>(d, batch, w, perm, flags, st);
+    case 32:   return launch_f32<32>(d, batch, w, perm, flags, st);
+    case 64:   return launch_f32<64>(d, batch, w, perm, flags, st);
+    case 128:  return launch_f32<128>(d, batch, w, perm, flags, st);
+    case 256:  return launch_f32<256>(d, batch, w, perm, flags, st);
+    case 512:  return launch_f32<512>(d, batch, w, perm, flags, st);
+    case 1024: return launch_f32<1024>(d, batch, w, perm, flags, st);
+    case 2048: return launch_f32<2048>(d, batch, w, perm, flags, st);
+    case 4096: return launch_f32<4096>(d, batch, w, perm, flags, st);
+    default:   return hipSuccess;  // reference: unsupported length is a silent no-op
+  }
+}
+
+}  // namespace mi355x

@@ -1,0 +1,44 @@
+// Shared device/host helpers for the MI355X CMSIS-DSP backend (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mi355x {
+
+// Exact integer semantics of the reference's host scalar path (Include/dsp/none.h):
+// int32 arithmetic wraps (gcc on x86-64), right shifts of signed values are arithmetic.
+// Everything is done on uint32_t so the compiler cannot exploit signed-overflow UB.
+__device__ __forceinline__ int32_t wadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+__device__ __forceinline__ int32_t wsub(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
+__device__ __forceinline__ int32_t wshl(int32_t a, int s) { return (int32_t)((uint32_t)a << s); }
+// (int32_t)(((q63_t)a * b) >> 32): arm_cfft_radix4_q31.c:235 — exactly v_mul_hi_i32.
+__device__ __forceinline__ int32_t mulhi(int32_t a, int32_t b) { return __mulhi(a, b); }
+
+// none.h:184-206 rounding forms (SMMULR / SMMLAR / SMMLSR)
+__device__ __forceinline__ int32_t mult_R(int32_t x, int32_t y) {
+  return (int32_t)((uint64_t)((int64_t)x * y + 0x80000000LL) >> 32);
+}
+__device__ __forceinline__ int32_t multAcc_R(int32_t a, int32_t x, int32_t y) {
+  uint64_t v = ((uint64_t)(int64_t)a << 32) + (uint64_t)((int64_t)x * y) + 0x80000000ULL;
+  return (int32_t)(v >> 32);
+}
+__device__ __forceinline__ int32_t multSub_R(int32_t a, int32_t x, int32_t y) {
+  uint64_t v = ((uint64_t)(int64_t)a << 32) - (uint64_t)((int64_t)x * y) + 0x80000000ULL;
+  return (int32_t)(v >> 32);
+}
+// __SSAT(val, 16): none.h:78-94
+__device__ __forceinline__ int32_t ssat16(int32_t v) { return v > 32767 ? 32767 : (v < -32768 ? -32768 : v); }
+
+constexpr int kBlock = 256;   // 4 wave64 per workgroup
+
+template <int N> struct Log2 { static constexpr int v = 1 + Log2<N / 2>::v; };
+template <> struct Log2<1> { static constexpr int v = 0; };
+
+// Binary bit reversal over B bits: the effective permutation of the fixed-point tables
+// armBitRevIndexTable_fixed_N (verified against the table swaps on the host).
+template <int B> __device__ __forceinline__ int bitrev(int k) { return (int)(__brev((uint32_t)k) >> (32 - B)); }
+
+// Flags shared by every transform kernel.
+enum : uint32_t { kIfft = 1u, kBitrev = 2u };
+
+}  // namespace mi355x

@@ -1,0 +1,121 @@
+// Host-side instance initialisation and the pre-initialised const instances.
+//
+// Mirrors Source/TransformFunctions/arm_cfft_init_{f32,q31,q15}.c (per-size CFFTINIT
+// macros + the fftLen switch), arm_rfft_fast_init_f32.c, Source/FilteringFunctions/
+// arm_fir_init_{f32,q15}.c, Source/MatrixFunctions/arm_mat_init_f32.c and the const
+// structs of Source/CommonTables/arm_const_structs.c.  Pure host code: filling a struct
+// involves no device work (tables are uploaded lazily by the processing functions).
+#include <string.h>
+
+#include "../../include/arm_const_structs.h"
+#include "../../include/arm_math.h"
+
+extern "C" {
+
+// ---- pre-initialised CFFT / RFFT instances (arm_const_structs.c:79-300)
+#define MI_CFFT_CONSTS(N)                                                                              \
+  const arm_cfft_instance_f32 arm_cfft_sR_f32_len##N = {N, twiddleCoef_##N, armBitRevIndexTable##N,     \
+                                                        ARMBITREVINDEXTABLE_##N##_TABLE_LENGTH};        \
+  const arm_cfft_instance_q31 arm_cfft_sR_q31_len##N = {N, twiddleCoef_##N##_q31,                       \
+                                                        armBitRevIndexTable_fixed_##N,                  \
+                                                        ARMBITREVINDEXTABLE_FIXED_##N##_TABLE_LENGTH};  \
+  const arm_cfft_instance_q15 arm_cfft_sR_q15_len##N = {N, twiddleCoef_##N##_q15,                       \
+                                                        armBitRevIndexTable_fixed_##N,                  \
+                                                        ARMBITREVINDEXTABLE_FIXED_##N##_TABLE_LENGTH};
+MI_CFFT_CONSTS(16)
+MI_CFFT_CONSTS(32)
+MI_CFFT_CONSTS(64)
+MI_CFFT_CONSTS(128)
+MI_CFFT_CONSTS(256)
+MI_CFFT_CONSTS(512)
+MI_CFFT_CONSTS(1024)
+MI_CFFT_CONSTS(2048)
+MI_CFFT_CONSTS(4096)
+#undef MI_CFFT_CONSTS
+
+#define MI_RFFT_CONST(N, H)                                                                         \
+  const arm_rfft_fast_instance_f32 arm_rfft_fast_sR_f32_len##N = {                                 \
+      {H, twiddleCoef_##H, armBitRevIndexTable##H, ARMBITREVINDEXTABLE_##H##_TABLE_LENGTH}, N,      \
+      twiddleCoef_rfft_##N};
+MI_RFFT_CONST(32, 16)
+MI_RFFT_CONST(64, 32)
+MI_RFFT_CONST(128, 64)
+MI_RFFT_CONST(256, 128)
+MI_RFFT_CONST(512, 256)
+MI_RFFT_CONST(1024, 512)
+MI_RFFT_CONST(2048, 1024)
+MI_RFFT_CONST(4096, 2048)
+#undef MI_RFFT_CONST
+
+// ---- per-size CFFT init: copy the const instance (arm_cfft_init_f32.c:121-136)
+#define MI_CFFT_INIT(N, T)                                                     \
+  arm_status arm_cfft_init_##N##_##T(arm_cfft_instance_##T* S) {               \
+    if (!S) return ARM_MATH_ARGUMENT_ERROR;                                    \
+    *S = arm_cfft_sR_##T##_len##N;                                             \
+    return ARM_MATH_SUCCESS;                                                   \
+  }
+#define MI_CFFT_INIT_ALL(T)                                                    \
+  MI_CFFT_INIT(16, T) MI_CFFT_INIT(32, T) MI_CFFT_INIT(64, T)                  \
+  MI_CFFT_INIT(128, T) MI_CFFT_INIT(256, T) MI_CFFT_INIT(512, T)               \
+  MI_CFFT_INIT(1024, T) MI_CFFT_INIT(2048, T) MI_CFFT_INIT(4096, T)            \
+  arm_status arm_cfft_init_##T(arm_cfft_instance_##T* S, uint16_t fftLen) {    \
+    switch (fftLen) {                                                          \
+      case 16: return arm_cfft_init_16_##T(S);                                 \
+      case 32: return arm_cfft_init_32_##T(S);                                 \
+      case 64: return arm_cfft_init_64_##T(S);                                 \
+      case 128: return arm_cfft_init_128_##T(S);                               \
+      case 256: return arm_cfft_init_256_##T(S);                               \
+      case 512: return arm_cfft_init_512_##T(S);                               \
+      case 1024: return arm_cfft_init_1024_##T(S);                             \
+      case 2048: return arm_cfft_init_2048_##T(S);                             \
+      case 4096: return arm_cfft_init_4096_##T(S);                             \
+      default: return ARM_MATH_ARGUMENT_ERROR;                                 \
+    }                                                                          \
+  }
+MI_CFFT_INIT_ALL(f32)
+MI_CFFT_INIT_ALL(q31)
+MI_CFFT_INIT_ALL(q15)
+#undef MI_CFFT_INIT_ALL
+#undef MI_CFFT_INIT
+
+// ---- RFFT fast init (arm_rfft_fast_init_f32.c): inner CFFT of N/2 + RFFT twiddles
+#define MI_RFFT_INIT(N)                                                        \
+  arm_status arm_rfft_fast_init_##N##_f32(arm_rfft_fast_instance_f32* S) {     \
+    if (!S) return ARM_MATH_ARGUMENT_ERROR;                                    \
+    *S = arm_rfft_fast_sR_f32_len##N;                                          \
+    return ARM_MATH_SUCCESS;                                                   \
+  }
+MI_RFFT_INIT(32)
+MI_RFFT_INIT(64)
+MI_RFFT_INIT(128)
+MI_RFFT_INIT(256)
+MI_RFFT_INIT(512)
+MI_RFFT_INIT(1024)
+MI_RFFT_INIT(2048)
+MI_RFFT_INIT(4096)
+#undef MI_RFFT_INIT
+
+arm_status arm_rfft_fast_init_f32(arm_rfft_fast_instance_f32* S, uint16_t fftLen) {
+  switch (fftLen) {
+    case 32: return arm_rfft_fast_init_32_f32(S);
+    case 64: return arm_rfft_fast_init_64_f32(S);
+    case 128: return arm_rfft_fast_init_128_f32(S);
+    case 256: return arm_rfft_fast_init_256_f32(S);
+    case 512: return arm_rfft_fast_init_512_f32(S);
+    case 1024: return arm_rfft_fast_init_1024_f32(S);
+    case 2048: return arm_rfft_fast_init_2048_f32(S);
+    case 4096: return arm_rfft_fast_init_4096_f32(S);
+    default: return ARM_MATH_ARGUMENT_ERROR;
+  }
+}
+
+// (FIR init zeroes a state buffer that may be device memory: it lives in api.cpp.)
+
+// ---- matrix init (arm_mat_init_f32.c)
+void arm_mat_init_f32(arm_matrix_instance_f32* S, uint16_t nRows, uint16_t nColumns, float32_t* pData) {
+  S->numRows = nRows;
+  S->numCols = nColumns;
+  S->pData = pData;
+}
+
+}  // extern "C"

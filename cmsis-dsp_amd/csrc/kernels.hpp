@@ -1,0 +1,35 @@
+// Internal launch entry points of the HIP kernels (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mi355x {
+
+// In-place batched CFFT over `batch` contiguous transforms of n complex samples.
+// tw: device copy of the instance's twiddle table.  perm: optional device permutation
+// (nullptr = the reference tables' canonical digit reversal).  flags: kIfft | kBitrev.
+hipError_t cfft_f32_launch(int n, float* data, uint32_t batch, const float* tw, const uint16_t* perm,
+                           uint32_t flags, hipStream_t st);
+hipError_t cfft_q31_launch(int n, int32_t* data, uint32_t batch, const int32_t* tw, const uint16_t* perm,
+                           uint32_t flags, hipStream_t st);
+hipError_t cfft_q15_launch(int n, int16_t* data, uint32_t batch, const int16_t* tw, const uint16_t* perm,
+                           uint32_t flags, hipStream_t st);
+
+// Real FFT split (forward, after the N/2 CFFT) / merge (inverse, before it) passes.
+hipError_t rfft_f32_stage_launch(int n_real, const float* p, float* out, uint32_t batch,
+                                 const float* tw_rfft, hipStream_t st);
+hipError_t rfft_f32_merge_launch(int n_real, const float* p, float* out, uint32_t batch,
+                                 const float* tw_rfft, hipStream_t st);
+
+// FIR: `batch` independent filters sharing one coefficient set.
+// hist: [batch][numTaps-1] streaming state (read, then overwritten with the new tail).
+hipError_t fir_f32_launch(const float* coeffs, int num_taps, const float* src, float* dst,
+                          uint32_t block_size, uint32_t batch, float* hist, hipStream_t st);
+hipError_t fir_q15_launch(const int16_t* coeffs, int num_taps, const int16_t* src, int16_t* dst,
+                          uint32_t block_size, uint32_t batch, int16_t* hist, hipStream_t st);
+
+// Row-major C[b] = A[b] (m x k) * B[b] (k x n), contiguous batch.
+hipError_t mat_mult_f32_launch(int m, int k, int n, const float* a, const float* b, float* c,
+                               uint32_t batch, hipStream_t st);
+
+}  // namespace mi355x

@@ -1,0 +1,152 @@
+// Host runtime: device table cache, staging scratch, error channel.
+#include "runtime.hpp"
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/arm_math_mi355x.h"
+
+namespace mi355x {
+
+namespace {
+thread_local int g_err = 0;
+thread_local std::string g_err_msg;
+
+std::mutex g_table_mu;
+std::map<std::tuple<int, const void*, size_t>, void*> g_tables;
+std::map<std::tuple<int, const void*, uint16_t, int, int>, std::pair<void*, bool>> g_perms;
+
+struct Scratch { void* p = nullptr; size_t n = 0; };
+thread_local std::map<std::pair<int, int>, Scratch> g_scratch;
+thread_local std::map<int, hipStream_t> g_streams;
+
+int cur_dev() { int d = 0; (void)hipGetDevice(&d); return d; }
+
+// canonical permutations the reference tables induce (verified in tests/test_tables.py):
+// f32: position holding frequency k under the mixed-radix [FIRST, 8, 8, ...] DIF
+int f32_src(int n, int k) {
+  int first = (n == 16 || n == 128 || n == 1024) ? 2 : (n == 32 || n == 256 || n == 2048) ? 4 : 1;
+  int p = 0, rem = n;
+  if (first > 1) { rem /= first; p += (k % first) * rem; k /= first; }
+  while (rem > 1) { rem >>= 3; p += (k & 7) * rem; k >>= 3; }
+  return p;
+}
+int fixed_src(int n, int k) {
+  int bits = 0;
+  while ((1 << bits) < n) ++bits;
+  int r = 0;
+  for (int b = 0; b < bits; ++b) r |= ((k >> b) & 1) << (bits - 1 - b);
+  return r;
+}
+}  // namespace
+
+void set_error(hipError_t e, const char* where) {
+  g_err = (int)e;
+  g_err_msg = std::string(where) + ": " + hipGetErrorString(e);
+}
+void clear_error() { g_err = 0; g_err_msg.clear(); }
+
+bool is_device_ptr(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  hipError_t e = hipPointerGetAttributes(&a, p);
+  if (e != hipSuccess) { (void)hipGetLastError(); return false; }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+const void* device_table(const void* host, size_t bytes) {
+  if (!host || !bytes) { set_error(hipErrorInvalidValue, "device_table: null table"); return nullptr; }
+  const int dev = cur_dev();
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  auto key = std::make_tuple(dev, host, bytes);
+  auto it = g_tables.find(key);
+  if (it != g_tables.end()) return it->second;
+  void* d = nullptr;
+  hipError_t e = hipMalloc(&d, bytes);
+  if (e != hipSuccess) { set_error(e, "device_table: hipMalloc"); return nullptr; }
+  e = hipMemcpy(d, host, bytes, is_device_ptr(host) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    set_error(e, "device_table: hipMemcpy");
+    (void)hipFree(d);
+    return nullptr;
+  }
+  g_tables[key] = d;
+  return d;
+}
+
+const uint16_t* device_perm(int n, const uint16_t* table, uint16_t len, int kind, bool* canonical, bool* ok) {
+  *ok = true;
+  *canonical = true;
+  if (!table) { return nullptr; }
+  const int dev = cur_dev();
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  auto key = std::make_tuple(dev, (const void*)table, len, kind, n);
+  auto it = g_perms.find(key);
+  if (it != g_perms.end()) {
+    *canonical = it->second.second;
+    return (const uint16_t*)it->second.first;
+  }
+  // apply the reference's sequential swaps (arm_bitreversal2.c:84-108) to an identity
+  // array of complex indices: a[pos] = pre-reversal index that ends up at pos.
+  const uint16_t* host = table;
+  std::vector<uint16_t> tmp;
+  if (is_device_ptr(table)) {
+    tmp.resize(len);
+    if (hipMemcpy(tmp.data(), table, len * sizeof(uint16_t), hipMemcpyDeviceToHost) != hipSuccess) { *ok = false; return nullptr; }
+    host = tmp.data();
+  }
+  std::vector<uint16_t> a(n);
+  for (int i = 0; i < n; ++i) a[i] = (uint16_t)i;
+  for (int i = 0; i + 1 < len; i += 2) {
+    const int x = host[i] >> 3, y = host[i + 1] >> 3;
+    if (x >= n || y >= n) { *ok = false; return nullptr; }
+    std::swap(a[x], a[y]);
+  }
+  bool canon = true;
+  for (int k = 0; k < n && canon; ++k) canon = a[k] == (kind == 0 ? f32_src(n, k) : fixed_src(n, k));
+  void* d = nullptr;
+  if (!canon) {
+    if (hipMalloc(&d, n * sizeof(uint16_t)) != hipSuccess ||
+        hipMemcpy(d, a.data(), n * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess) {
+      *ok = false;
+      return nullptr;
+    }
+  }
+  g_perms[key] = {d, canon};
+  *canonical = canon;
+  return (const uint16_t*)d;
+}
+
+void* scratch(size_t bytes, int slot) {
+  const int dev = cur_dev();
+  Scratch& s = g_scratch[{dev, slot}];
+  if (s.n < bytes) {
+    if (s.p) (void)hipFree(s.p);
+    s.p = nullptr;
+    s.n = 0;
+    if (hipMalloc(&s.p, bytes) != hipSuccess) return nullptr;
+    s.n = bytes;
+  }
+  return s.p;
+}
+
+hipStream_t sync_stream() {
+  const int dev = cur_dev();
+  auto it = g_streams.find(dev);
+  if (it != g_streams.end()) return it->second;
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  g_streams[dev] = s;
+  return s;
+}
+
+}  // namespace mi355x
+
+extern "C" {
+int arm_mi355x_last_error(void) { return mi355x::g_err; }
+const char* arm_mi355x_last_error_string(void) { return mi355x::g_err_msg.c_str(); }
+void arm_mi355x_clear_error(void) { mi355x::clear_error(); }
+}

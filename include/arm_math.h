@@ -1,0 +1,205 @@
+/*
+ * arm_math.h — drop-in subset of the CMSIS-DSP public API, served by the MI355X backend
+ * (libcmsisdsp_mi355x.so).  Only the hot path named in BASELINE.json `north_star` lives
+ * here: complex FFT f32/q31/q15, real FFT (fast) f32, FIR f32/q15, matrix multiply f32.
+ *
+ * Every type and prototype keeps the reference's layout and signature so that existing
+ * C callers recompile unchanged.  Each declaration cites the reference interface it
+ * replaces (paths relative to the reference tree, xavierbrgt/CMSIS-DSP).
+ *
+ * Semantics contract:
+ *   - processing functions are synchronous: when they return, the result is in p1/pDst;
+ *   - buffers may be host memory (staged through pinned memory) or device memory
+ *     (hipMalloc'd; used in place, no copies);
+ *   - an unsupported fftLen is a silent no-op, exactly like the reference switch;
+ *   - no processing function aborts or throws: a device failure is reported through
+ *     arm_mi355x_last_error() (arm_math_mi355x.h).
+ * The batched, stream-ordered, device-pointer API lives in arm_math_mi355x.h.
+ */
+#ifndef ARM_MATH_MI355X_DROPIN_H
+#define ARM_MATH_MI355X_DROPIN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- scalar types: Include/arm_math_types.h:324-351 ---------------------------- */
+typedef int8_t   q7_t;
+typedef int16_t  q15_t;
+typedef int32_t  q31_t;
+typedef int64_t  q63_t;
+typedef float    float32_t;
+typedef double   float64_t;
+
+/* ---- status codes: Include/arm_math_types.h:603-613 ---------------------------- */
+typedef enum {
+  ARM_MATH_SUCCESS               =  0,
+  ARM_MATH_ARGUMENT_ERROR        = -1,
+  ARM_MATH_LENGTH_ERROR          = -2,
+  ARM_MATH_SIZE_MISMATCH         = -3,
+  ARM_MATH_NANINF                = -4,
+  ARM_MATH_SINGULAR              = -5,
+  ARM_MATH_TEST_FAILURE          = -6,
+  ARM_MATH_DECOMPOSITION_FAILURE = -7
+} arm_status;
+
+/* ---- complex FFT instances: Include/dsp/transform_functions.h:282-296,347-361,410-424
+ * (scalar/non-Helium layout: {fftLen, pTwiddle, pBitRevTable, bitRevLength}) -------- */
+typedef struct {
+        uint16_t   fftLen;
+  const float32_t *pTwiddle;
+  const uint16_t  *pBitRevTable;
+        uint16_t   bitRevLength;
+} arm_cfft_instance_f32;
+
+typedef struct {
+        uint16_t   fftLen;
+  const q31_t     *pTwiddle;
+  const uint16_t  *pBitRevTable;
+        uint16_t   bitRevLength;
+} arm_cfft_instance_q31;
+
+typedef struct {
+        uint16_t   fftLen;
+  const q15_t     *pTwiddle;
+  const uint16_t  *pBitRevTable;
+        uint16_t   bitRevLength;
+} arm_cfft_instance_q15;
+
+/* ---- real FFT (fast) instance: Include/dsp/transform_functions.h:813-818 ---------- */
+typedef struct {
+        arm_cfft_instance_f32 Sint;
+        uint16_t              fftLenRFFT;
+  const float32_t            *pTwiddleRFFT;
+} arm_rfft_fast_instance_f32;
+
+/* ---- FIR instances: Include/dsp/filtering_functions.h:66-71, 86-91 --------------- */
+typedef struct {
+        uint16_t   numTaps;
+        q15_t     *pState;
+  const q15_t     *pCoeffs;
+} arm_fir_instance_q15;
+
+typedef struct {
+        uint16_t   numTaps;
+        float32_t *pState;
+  const float32_t *pCoeffs;
+} arm_fir_instance_f32;
+
+/* ---- matrix instance: Include/dsp/matrix_functions.h:118-123 --------------------- */
+typedef struct {
+  uint16_t   numRows;
+  uint16_t   numCols;
+  float32_t *pData;
+} arm_matrix_instance_f32;
+
+/* ===================================================================================
+ * Complex FFT, f32.  Prototypes: Include/dsp/transform_functions.h:428-460
+ * Reference bodies: Source/TransformFunctions/arm_cfft_init_f32.c:121-136,291-354,
+ *                   Source/TransformFunctions/arm_cfft_f32.c:1243-1298
+ * =================================================================================== */
+arm_status arm_cfft_init_4096_f32(arm_cfft_instance_f32 *S);
+arm_status arm_cfft_init_2048_f32(arm_cfft_instance_f32 *S);
+arm_status arm_cfft_init_1024_f32(arm_cfft_instance_f32 *S);
+arm_status arm_cfft_init_512_f32(arm_cfft_instance_f32 *S);
+arm_status arm_cfft_init_256_f32(arm_cfft_instance_f32 *S);
+arm_status arm_cfft_init_128_f32(arm_cfft_instance_f32 *S);
+arm_status arm_cfft_init_64_f32(arm_cfft_instance_f32 *S);
+arm_status arm_cfft_init_32_f32(arm_cfft_instance_f32 *S);
+arm_status arm_cfft_init_16_f32(arm_cfft_instance_f32 *S);
+arm_status arm_cfft_init_f32(arm_cfft_instance_f32 *S, uint16_t fftLen);
+void arm_cfft_f32(const arm_cfft_instance_f32 *S, float32_t *p1,
+                  uint8_t ifftFlag, uint8_t bitReverseFlag);
+
+/* ===================================================================================
+ * Complex FFT, q31.  Prototypes: Include/dsp/transform_functions.h:364-394
+ * Reference bodies: Source/TransformFunctions/arm_cfft_init_q31.c,
+ *                   Source/TransformFunctions/arm_cfft_q31.c:704-755
+ * =================================================================================== */
+arm_status arm_cfft_init_4096_q31(arm_cfft_instance_q31 *S);
+arm_status arm_cfft_init_2048_q31(arm_cfft_instance_q31 *S);
+arm_status arm_cfft_init_1024_q31(arm_cfft_instance_q31 *S);
+arm_status arm_cfft_init_512_q31(arm_cfft_instance_q31 *S);
+arm_status arm_cfft_init_256_q31(arm_cfft_instance_q31 *S);
+arm_status arm_cfft_init_128_q31(arm_cfft_instance_q31 *S);
+arm_status arm_cfft_init_64_q31(arm_cfft_instance_q31 *S);
+arm_status arm_cfft_init_32_q31(arm_cfft_instance_q31 *S);
+arm_status arm_cfft_init_16_q31(arm_cfft_instance_q31 *S);
+arm_status arm_cfft_init_q31(arm_cfft_instance_q31 *S, uint16_t fftLen);
+void arm_cfft_q31(const arm_cfft_instance_q31 *S, q31_t *p1,
+                  uint8_t ifftFlag, uint8_t bitReverseFlag);
+
+/* ===================================================================================
+ * Complex FFT, q15.  Prototypes: Include/dsp/transform_functions.h:299-331
+ * Reference bodies: Source/TransformFunctions/arm_cfft_init_q15.c,
+ *                   Source/TransformFunctions/arm_cfft_q15.c:671-722
+ * =================================================================================== */
+arm_status arm_cfft_init_4096_q15(arm_cfft_instance_q15 *S);
+arm_status arm_cfft_init_2048_q15(arm_cfft_instance_q15 *S);
+arm_status arm_cfft_init_1024_q15(arm_cfft_instance_q15 *S);
+arm_status arm_cfft_init_512_q15(arm_cfft_instance_q15 *S);
+arm_status arm_cfft_init_256_q15(arm_cfft_instance_q15 *S);
+arm_status arm_cfft_init_128_q15(arm_cfft_instance_q15 *S);
+arm_status arm_cfft_init_64_q15(arm_cfft_instance_q15 *S);
+arm_status arm_cfft_init_32_q15(arm_cfft_instance_q15 *S);
+arm_status arm_cfft_init_16_q15(arm_cfft_instance_q15 *S);
+arm_status arm_cfft_init_q15(arm_cfft_instance_q15 *S, uint16_t fftLen);
+void arm_cfft_q15(const arm_cfft_instance_q15 *S, q15_t *p1,
+                  uint8_t ifftFlag, uint8_t bitReverseFlag);
+
+/* ===================================================================================
+ * Real FFT (fast), f32.  Prototypes: Include/dsp/transform_functions.h:820-849
+ * Reference bodies: Source/TransformFunctions/arm_rfft_fast_init_f32.c:228-244,
+ *                   Source/TransformFunctions/arm_rfft_fast_f32.c:675-699
+ * Note (reference behaviour kept): the forward transform overwrites p.
+ * =================================================================================== */
+arm_status arm_rfft_fast_init_32_f32(arm_rfft_fast_instance_f32 *S);
+arm_status arm_rfft_fast_init_64_f32(arm_rfft_fast_instance_f32 *S);
+arm_status arm_rfft_fast_init_128_f32(arm_rfft_fast_instance_f32 *S);
+arm_status arm_rfft_fast_init_256_f32(arm_rfft_fast_instance_f32 *S);
+arm_status arm_rfft_fast_init_512_f32(arm_rfft_fast_instance_f32 *S);
+arm_status arm_rfft_fast_init_1024_f32(arm_rfft_fast_instance_f32 *S);
+arm_status arm_rfft_fast_init_2048_f32(arm_rfft_fast_instance_f32 *S);
+arm_status arm_rfft_fast_init_4096_f32(arm_rfft_fast_instance_f32 *S);
+arm_status arm_rfft_fast_init_f32(arm_rfft_fast_instance_f32 *S, uint16_t fftLen);
+void arm_rfft_fast_f32(const arm_rfft_fast_instance_f32 *S, float32_t *p,
+                       float32_t *pOut, uint8_t ifftFlag);
+
+/* ===================================================================================
+ * FIR.  Prototypes: Include/dsp/filtering_functions.h:141-145,175-180,233-237,260-265
+ * Reference bodies: Source/FilteringFunctions/arm_fir_f32.c:911-1280,
+ *                   arm_fir_init_f32.c:74-95, arm_fir_q15.c:458-726, arm_fir_init_q15.c:86-139
+ * pState holds numTaps+blockSize-1 samples; the last numTaps-1 are carried to the
+ * next call (streaming state), as in the reference.
+ * =================================================================================== */
+void arm_fir_init_f32(arm_fir_instance_f32 *S, uint16_t numTaps,
+                      const float32_t *pCoeffs, float32_t *pState, uint32_t blockSize);
+void arm_fir_f32(const arm_fir_instance_f32 *S, const float32_t *pSrc,
+                 float32_t *pDst, uint32_t blockSize);
+arm_status arm_fir_init_q15(arm_fir_instance_q15 *S, uint16_t numTaps,
+                            const q15_t *pCoeffs, q15_t *pState, uint32_t blockSize);
+void arm_fir_q15(const arm_fir_instance_q15 *S, const q15_t *pSrc,
+                 q15_t *pDst, uint32_t blockSize);
+
+/* ===================================================================================
+ * Matrix multiply, f32.  Prototypes: Include/dsp/matrix_functions.h:341-344,630-634
+ * Reference bodies: Source/MatrixFunctions/arm_mat_mult_f32.c:600-730,
+ *                   Source/MatrixFunctions/arm_mat_init_f32.c
+ * Size check: always performed (the reference checks only under ARM_MATH_MATRIX_CHECK,
+ * arm_mat_mult_f32.c:618-630; a mismatched call is undefined there).
+ * =================================================================================== */
+void arm_mat_init_f32(arm_matrix_instance_f32 *S, uint16_t nRows, uint16_t nColumns,
+                      float32_t *pData);
+arm_status arm_mat_mult_f32(const arm_matrix_instance_f32 *pSrcA,
+                            const arm_matrix_instance_f32 *pSrcB,
+                            arm_matrix_instance_f32 *pDst);
+
+#ifdef __cplusplus
+}
+#endif
+
+#include "arm_const_structs.h"
+
+#endif /* ARM_MATH_MI355X_DROPIN_H */

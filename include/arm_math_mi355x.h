@@ -1,0 +1,73 @@
+/*
+ * arm_math_mi355x.h — additive batched API of the MI355X CMSIS-DSP backend.
+ *
+ * The drop-in functions of arm_math.h process one transform / block / matrix per call,
+ * synchronously.  These entry points are the path that can reach the HBM roofline:
+ *   - all data pointers are DEVICE pointers (hipMalloc'd, or managed memory);
+ *   - `batch` items are contiguous (stride = one item), processed in one launch;
+ *   - work is enqueued on `stream` (a hipStream_t passed as void*, NULL = legacy default
+ *     stream) and the call returns without synchronising;
+ *   - results are bit-identical to calling the reference scalar function on each item in
+ *     turn (f32 CFFT/RFFT/FIR and all fixed-point functions), or within the stated
+ *     tolerance (arm_mat_mult_f32_batch, MFMA accumulation — DESIGN.md §mat_mult);
+ *   - return ARM_MATH_SUCCESS, ARM_MATH_ARGUMENT_ERROR (unsupported length, NULL pointer,
+ *     launch failure; details in arm_mi355x_last_error_string()).
+ * Instance structs are the reference's own (arm_math.h); tables they point to are
+ * uploaded once per device and cached by address, so they must stay immutable.
+ * Multi-GPU: one process (or thread) per device, each calling these on its own shard;
+ * the current HIP device of the calling thread is used.
+ */
+#ifndef ARM_MATH_MI355X_BATCH_H
+#define ARM_MATH_MI355X_BATCH_H
+
+#include "arm_math.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Complex FFT over `batch` contiguous transforms of 2*fftLen words each, in place.
+ * Per-item semantics: arm_cfft_f32 / _q31 / _q15 (arm_cfft_f32.c:1243, arm_cfft_q31.c:704,
+ * arm_cfft_q15.c:671). */
+arm_status arm_cfft_f32_batch(const arm_cfft_instance_f32 *S, float32_t *d_p1, uint32_t batch,
+                              uint8_t ifftFlag, uint8_t bitReverseFlag, void *stream);
+arm_status arm_cfft_q31_batch(const arm_cfft_instance_q31 *S, q31_t *d_p1, uint32_t batch,
+                              uint8_t ifftFlag, uint8_t bitReverseFlag, void *stream);
+arm_status arm_cfft_q15_batch(const arm_cfft_instance_q15 *S, q15_t *d_p1, uint32_t batch,
+                              uint8_t ifftFlag, uint8_t bitReverseFlag, void *stream);
+
+/* Real FFT (fast) over `batch` contiguous signals of fftLenRFFT floats.
+ * Per-item semantics: arm_rfft_fast_f32 (arm_rfft_fast_f32.c:675-699), including the
+ * reference's overwrite of d_p on the forward transform. */
+arm_status arm_rfft_fast_f32_batch(const arm_rfft_fast_instance_f32 *S, float32_t *d_p,
+                                   float32_t *d_out, uint32_t batch, uint8_t ifftFlag, void *stream);
+
+/* FIR over `batch` independent filters sharing S->numTaps / S->pCoeffs (host or device
+ * pointer; S->pState is not used).  d_src/d_dst: [batch][blockSize].  d_hist:
+ * [batch][numTaps-1] streaming state, read as the history before the block and
+ * overwritten with the history after it, so consecutive calls equal one long call
+ * (arm_fir_f32.c:1242-1278).  Zero it to start a stream (arm_fir_init_f32). */
+arm_status arm_fir_f32_batch(const arm_fir_instance_f32 *S, const float32_t *d_src, float32_t *d_dst,
+                             uint32_t blockSize, uint32_t batch, float32_t *d_hist, void *stream);
+arm_status arm_fir_q15_batch(const arm_fir_instance_q15 *S, const q15_t *d_src, q15_t *d_dst,
+                             uint32_t blockSize, uint32_t batch, q15_t *d_hist, void *stream);
+
+/* Row-major C[b] = A[b] * B[b] for `batch` contiguous (numRows x numCols) matrices with
+ * the shapes of the three instances (their pData must be device pointers to the first
+ * item).  Returns ARM_MATH_SIZE_MISMATCH on incompatible shapes (arm_mat_mult_f32.c:618-630). */
+arm_status arm_mat_mult_f32_batch(const arm_matrix_instance_f32 *pSrcA, const arm_matrix_instance_f32 *pSrcB,
+                                  arm_matrix_instance_f32 *pDst, uint32_t batch, void *stream);
+
+/* Error channel for the void-returning drop-in functions: 0 = no error, otherwise the
+ * hipError_t of the last failure on this thread. */
+int arm_mi355x_last_error(void);
+const char *arm_mi355x_last_error_string(void);
+void arm_mi355x_clear_error(void);
+
+/* Library identification: "cmsisdsp-mi355x <version> gfx950". */
+const char *arm_mi355x_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,46 @@
+# Builds the REAL reference scalar path from /root/reference sources into oracle/_ref/.
+# Test infrastructure only: the product never links or loads anything built here.
+# Flags follow SURVEY.md §8c: the CMake HOST=ON equivalent (__GNUC_PYTHON__ -> scalar
+# branches, ARM_MATH_DSP undefined), LOOPUNROLL on (CMake default), no -march, no
+# -ffast-math (no FMA contraction on x86-64 baseline).
+# Usage:  make -f oracle/ref.mk            (from the repo root)
+REF     ?= /root/reference
+OUT     ?= oracle/_ref
+CC      ?= gcc
+CFLAGS  := -O2 -fPIC -D__GNUC_PYTHON__ -DARM_MATH_LOOPUNROLL -ffp-contract=off -w \
+           -I$(REF)/Include -I$(REF)/PrivateInclude
+
+T := $(REF)/Source/TransformFunctions
+F := $(REF)/Source/FilteringFunctions
+M := $(REF)/Source/MatrixFunctions
+C := $(REF)/Source/CommonTables
+
+SRCS := \
+  $(T)/arm_cfft_f32.c $(T)/arm_cfft_radix8_f32.c $(T)/arm_cfft_init_f32.c \
+  $(T)/arm_cfft_q31.c $(T)/arm_cfft_radix4_q31.c $(T)/arm_cfft_init_q31.c \
+  $(T)/arm_cfft_q15.c $(T)/arm_cfft_radix4_q15.c $(T)/arm_cfft_init_q15.c \
+  $(T)/arm_bitreversal2.c $(T)/arm_bitreversal.c \
+  $(T)/arm_rfft_fast_f32.c $(T)/arm_rfft_fast_init_f32.c \
+  $(F)/arm_fir_f32.c $(F)/arm_fir_init_f32.c $(F)/arm_fir_q15.c $(F)/arm_fir_init_q15.c \
+  $(M)/arm_mat_mult_f32.c $(M)/arm_mat_init_f32.c \
+  $(C)/arm_common_tables.c $(C)/arm_const_structs.c
+
+OBJS := $(patsubst $(REF)/Source/%.c,$(OUT)/obj/%.o,$(SRCS))
+
+all: $(OUT)/libcmsisdsp_ref.so $(OUT)/bench_ref
+
+$(OUT)/obj/%.o: $(REF)/Source/%.c
+	@mkdir -p $(dir $@)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(OUT)/libcmsisdsp_ref.so: $(OBJS)
+	$(CC) -shared -Wl,-Bsymbolic -o $@ $(OBJS) -lm
+
+# Timing driver (CPU baseline kind "reference"): our own source, linked to the reference objects.
+$(OUT)/bench_ref: oracle/bench_cpu.c $(OBJS)
+	$(CC) -O2 -D__GNUC_PYTHON__ -DARM_MATH_LOOPUNROLL -I$(REF)/Include -I$(REF)/PrivateInclude \
+	  -DBENCH_AGAINST_REFERENCE -o $@ oracle/bench_cpu.c $(OBJS) -lm -lpthread
+
+clean:
+	rm -rf $(OUT)/obj $(OUT)/libcmsisdsp_ref.so $(OUT)/bench_ref
+.PHONY: all clean

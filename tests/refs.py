@@ -1,0 +1,150 @@
+"""Test-side access to the two CPU checkers (test infrastructure only — never the product):
+
+* `ref_lib()`    — oracle/_ref/libcmsisdsp_ref.so: the reference's own scalar C, compiled
+                   from /root/reference by oracle/ref.mk (travels to the GPU box prebuilt);
+* `oracle_lib()` — oracle/_build/liboracle.so: our plain-C restatement (oracle/src/*.c),
+                   exported with an `oracle_` prefix and the same C ABI.
+
+Both are wrapped by `Host`, a numpy in / numpy out driver with the reference's call
+shapes, so a test reads `host.cfft("f32", n, x, ifft, bitrev)` for either checker.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from cmsisdsp_amd import _abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libcmsisdsp_ref.so")
+ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+
+_INST = {"f32": _abi.arm_cfft_instance_f32, "q31": _abi.arm_cfft_instance_q31, "q15": _abi.arm_cfft_instance_q15}
+DTYPE = {"f32": np.float32, "q31": np.int32, "q15": np.int16}
+
+
+class Host:
+    def __init__(self, lib, prefix):
+        self.lib, self.p = lib, prefix
+        _abi.bind(lib, _abi.DROPIN, prefix)
+
+    def fn(self, name):
+        return getattr(self.lib, self.p + name)
+
+    def cfft_instance(self, kind, n):
+        S = _INST[kind]()
+        st = self.fn(f"arm_cfft_init_{kind}")(C.byref(S), n)
+        assert st == 0, (kind, n, st)
+        return S
+
+    def cfft(self, kind, n, x, ifft, bitrev):
+        S = self.cfft_instance(kind, n)
+        buf = np.ascontiguousarray(x, dtype=DTYPE[kind]).copy()
+        assert buf.size == 2 * n
+        self.fn(f"arm_cfft_{kind}")(C.byref(S), buf.ctypes.data, ifft, bitrev)
+        return buf
+
+    def cfft_many(self, kind, n, x, ifft, bitrev):
+        """x: [batch, 2n] -> per-row transforms (a Python loop over the scalar call)."""
+        S = self.cfft_instance(kind, n)
+        out = np.ascontiguousarray(x, dtype=DTYPE[kind]).copy()
+        f = self.fn(f"arm_cfft_{kind}")
+        for r in range(out.shape[0]):
+            f(C.byref(S), out[r].ctypes.data, ifft, bitrev)
+        return out
+
+    def rfft(self, n, x, ifft):
+        S = _abi.arm_rfft_fast_instance_f32()
+        assert self.fn("arm_rfft_fast_init_f32")(C.byref(S), n) == 0
+        p = np.ascontiguousarray(x, dtype=np.float32).copy()
+        out = np.zeros(n, dtype=np.float32)
+        self.fn("arm_rfft_fast_f32")(C.byref(S), p.ctypes.data, out.ctypes.data, ifft)
+        return out, p
+
+    def fir(self, kind, coeffs, blocks):
+        """Stream `blocks` (list of 1-D arrays, each <= the block size) through one filter;
+        returns (outputs, final state buffer)."""
+        dt = np.float32 if kind == "f32" else np.int16
+        inst = _abi.arm_fir_instance_f32() if kind == "f32" else _abi.arm_fir_instance_q15()
+        c = np.ascontiguousarray(coeffs, dtype=dt)
+        bs = max(len(b) for b in blocks)
+        state = np.zeros(len(c) + bs - 1, dtype=dt)
+        self.fn(f"arm_fir_init_{kind}")(C.byref(inst), len(c), c.ctypes.data, state.ctypes.data, bs)
+        outs = []
+        for b in blocks:
+            b = np.ascontiguousarray(b, dtype=dt)
+            y = np.zeros_like(b)
+            self.fn(f"arm_fir_{kind}")(C.byref(inst), b.ctypes.data, y.ctypes.data, len(b))
+            outs.append(y)
+        self._keep = (c, state)
+        return outs, state.copy()
+
+    def mat_mult(self, a, b):
+        a = np.ascontiguousarray(a, dtype=np.float32)
+        b = np.ascontiguousarray(b, dtype=np.float32)
+        c = np.zeros((a.shape[0], b.shape[1]), dtype=np.float32)
+        A, B, Cm = (_abi.arm_matrix_instance_f32() for _ in range(3))
+        init = self.fn("arm_mat_init_f32")
+        init(C.byref(A), a.shape[0], a.shape[1], a.ctypes.data)
+        init(C.byref(B), b.shape[0], b.shape[1], b.ctypes.data)
+        init(C.byref(Cm), c.shape[0], c.shape[1], c.ctypes.data)
+        st = self.fn("arm_mat_mult_f32")(C.byref(A), C.byref(B), C.byref(Cm))
+        return st, c
+
+
+_cache = {}
+
+
+def ref_lib():
+    if "ref" not in _cache:
+        if not os.path.exists(REF_SO):
+            raise FileNotFoundError(f"{REF_SO} missing: build it with `make -f oracle/ref.mk` (needs /root/reference)")
+        _cache["ref"] = Host(C.CDLL(REF_SO), "")
+    return _cache["ref"]
+
+
+def oracle_lib():
+    if "oracle" not in _cache:
+        if not os.path.exists(ORACLE_SO):
+            raise FileNotFoundError(f"{ORACLE_SO} missing: build it with `make -C oracle`")
+        _cache["oracle"] = Host(C.CDLL(ORACLE_SO), "oracle_")
+    return _cache["oracle"]
+
+
+# ------------------------------------------------------------------ seeded inputs
+def splitmix64(seed, n):
+    """The SplitMix64 stream (Steele et al.); bench.py and tests share it for inputs."""
+    out = np.empty(n, dtype=np.uint64)
+    s = np.uint64(seed)
+    with np.errstate(over="ignore"):
+        for i in range(n):
+            s = s + np.uint64(0x9E3779B97F4A7C15)
+            z = s
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            out[i] = z ^ (z >> np.uint64(31))
+    return out
+
+
+def rand_input(kind, n_words, seed, dist="uniform"):
+    rng = np.random.default_rng(seed)
+    if kind == "f32":
+        if dist == "uniform":
+            return rng.uniform(-1.0, 1.0, n_words).astype(np.float32)
+        if dist == "large":
+            return (rng.standard_normal(n_words) * 1e4).astype(np.float32)
+        raise ValueError(dist)
+    info = np.iinfo(DTYPE[kind])
+    if dist == "uniform":           # full range: exercises wrap / saturation
+        return rng.integers(info.min, info.max, n_words, endpoint=True, dtype=np.int64).astype(DTYPE[kind])
+    if dist == "sine":              # reference-style noisy sine, cmsisdsp/fixedpoint.py round+saturate
+        t = np.arange(n_words // 2)
+        v = 0.7 * np.sin(2 * np.pi * 13 * t / max(1, n_words // 2)) + 0.05 * rng.standard_normal(n_words // 2)
+        z = np.empty(n_words)
+        z[0::2] = v
+        z[1::2] = 0.05 * rng.standard_normal(n_words // 2)
+        scale = 2.0 ** (31 if kind == "q31" else 15)
+        return np.clip(np.round(z * scale), info.min, info.max).astype(DTYPE[kind])
+    if dist == "extreme":           # all min / max words
+        return rng.choice(np.array([info.min, info.max, 0, -1], dtype=DTYPE[kind]), n_words)
+    raise ValueError(dist)

@@ -1,0 +1,157 @@
+"""GPU parity: real FFT (fast) f32, FIR f32/q15, matrix multiply f32 vs the reference.
+
+rfft / FIR: bit-exact against oracle/_ref.  mat_mult: MFMA f32 accumulates as an fmaf
+chain (one rounding per term fewer than the reference's mul-then-add), so the bar is the
+reference test's own tolerance (Testing/Source/Tests/BinaryTestsF32.cpp:5,13-17:
+rel 1e-6 / abs 1e-5 at dims <= 40) plus a normwise bound at large sizes:
+|C - C_ref|_max <= 4 * K * eps32 * max(|A| |B|).
+"""
+import numpy as np
+import pytest
+
+import refs
+
+pytestmark = pytest.mark.gpu
+
+
+# ------------------------------------------------------------------ RFFT fast
+@pytest.mark.parametrize("n", [32, 64, 128, 256, 512, 1024, 2048, 4096])
+@pytest.mark.parametrize("ifft", [0, 1])
+def test_rfft_batch_bitexact(dsp, torch_gpu, ref, n, ifft):
+    torch = torch_gpu
+    batch = 19
+    x = np.stack([refs.rand_input("f32", n, seed=n + r + 100 * ifft) for r in range(batch)])
+    want = np.stack([ref.rfft(n, x[r], ifft)[0] for r in range(batch)])
+    want_p = np.stack([ref.rfft(n, x[r], ifft)[1] for r in range(batch)])
+    S = dsp.const_instance(f"arm_rfft_fast_sR_f32_len{n}")
+    p = torch.from_numpy(x.copy()).cuda()
+    out = torch.zeros_like(p)
+    dsp.rfft_fast_batch(S, p, out, ifft)
+    torch.cuda.synchronize()
+    assert out.cpu().numpy().tobytes() == want.tobytes()
+    if not ifft:   # the forward transform overwrites its input, like the reference
+        assert p.cpu().numpy().tobytes() == want_p.tobytes()
+
+
+@pytest.mark.parametrize("n", [32, 1024, 4096])
+def test_rfft_dropin(dsp, torch_gpu, ref, n):
+    x = refs.rand_input("f32", n, seed=n)
+    for ifft in (0, 1):
+        S = dsp.arm_rfft_fast_instance_f32()
+        assert dsp.arm_rfft_fast_init_f32(S, n) == 0
+        assert dsp.arm_rfft_fast_f32(S, x, ifft).tobytes() == ref.rfft(n, x, ifft)[0].tobytes()
+
+
+# ------------------------------------------------------------------ FIR
+def _fir_batched(dsp, torch, kind, coeffs, blocks_per_filter):
+    """blocks_per_filter: [batch][calls] arrays; runs the batched API call by call."""
+    import ctypes as C
+    dt = np.float32 if kind == "f32" else np.int16
+    batch, calls = len(blocks_per_filter), len(blocks_per_filter[0])
+    c = np.ascontiguousarray(coeffs, dtype=dt)
+    S = dsp.arm_fir_instance_f32() if kind == "f32" else dsp.arm_fir_instance_q15()
+    S.numTaps = len(c)
+    dc = torch.from_numpy(c.copy()).cuda()
+    S.pCoeffs = C.cast(dc.data_ptr(), S._fields_[2][1])
+    hist = torch.zeros((batch, max(len(c) - 1, 0)), dtype=dc.dtype, device="cuda")
+    outs = []
+    for k in range(calls):
+        src = torch.from_numpy(np.stack([blocks_per_filter[f][k] for f in range(batch)]).astype(dt)).cuda()
+        dst = torch.empty_like(src)
+        dsp.fir_batch(S, src, dst, hist, q15=(kind == "q15"))
+        outs.append(dst.cpu().numpy())
+    torch.cuda.synchronize()
+    return outs, hist.cpu().numpy()
+
+
+@pytest.mark.parametrize("kind", ["f32", "q15"])
+@pytest.mark.parametrize("taps,block", [(128, 4096), (29, 32), (2, 7), (64, 100), (130, 2049), (1, 64)])
+def test_fir_batch_bitexact_two_calls(dsp, torch_gpu, ref, kind, taps, block):
+    """Each filter runs two consecutive blocks: the state carry must make them equal one
+    long call (FIRF32.cpp:116-124 does the same two-call split)."""
+    if kind == "q15" and taps % 2:
+        pytest.skip("q15 FIR requires an even numTaps (arm_fir_init_q15.c:95-106)")
+    rng = np.random.default_rng(taps * 7 + block)
+    batch = 5
+    if kind == "f32":
+        coeffs = (rng.standard_normal(taps) / np.sqrt(taps)).astype(np.float32)
+        blocks = [[rng.uniform(-1, 1, block).astype(np.float32) for _ in range(2)] for _ in range(batch)]
+    else:
+        coeffs = rng.integers(-32768, 32767, taps, endpoint=True).astype(np.int16)
+        blocks = [[rng.integers(-32768, 32767, block, endpoint=True).astype(np.int16) for _ in range(2)]
+                  for _ in range(batch)]
+    got, hist = _fir_batched(dsp, torch_gpu, kind, coeffs, blocks)
+    for f in range(batch):
+        want, state = ref.fir(kind, coeffs, blocks[f])
+        for k in range(2):
+            assert got[k][f].tobytes() == want[k].tobytes(), (f, k)
+        assert hist[f].tobytes() == state[:taps - 1].tobytes()
+
+
+def test_fir_q15_pairwrap_extreme(dsp, torch_gpu, ref):
+    """All -32768 input and taps: the __SMLALD pair sum wraps in int32 on the unrolled
+    outputs but not on the blockSize%4 tail (arm_fir_q15.c:482-640 vs :649-681)."""
+    taps, block = 8, 4099
+    coeffs = np.full(taps, -32768, dtype=np.int16)
+    blocks = [[np.full(block, -32768, dtype=np.int16)]]
+    got, _ = _fir_batched(dsp, torch_gpu, "q15", coeffs, blocks)
+    want, _ = ref.fir("q15", coeffs, blocks[0])
+    assert got[0][0].tobytes() == want[0].tobytes()
+
+
+@pytest.mark.parametrize("kind", ["f32", "q15"])
+def test_fir_dropin_state(dsp, torch_gpu, ref, kind):
+    rng = np.random.default_rng(4)
+    taps, block = 32, 256
+    if kind == "f32":
+        coeffs = rng.standard_normal(taps).astype(np.float32)
+        blocks = [rng.uniform(-1, 1, block).astype(np.float32) for _ in range(3)]
+        f = dsp.FirF32(coeffs, block)
+    else:
+        coeffs = rng.integers(-20000, 20000, taps).astype(np.int16)
+        blocks = [rng.integers(-32768, 32767, block).astype(np.int16) for _ in range(3)]
+        f = dsp.FirQ15(coeffs, block)
+    want, state = ref.fir(kind, coeffs, blocks)
+    for b, w in zip(blocks, want):
+        assert f(b).tobytes() == w.tobytes()
+    assert f.state.tobytes() == state.tobytes()   # history head AND the block copy in the tail
+
+
+# ------------------------------------------------------------------ mat mult
+@pytest.mark.parametrize("m,k,n", [(1, 1, 1), (4, 4, 4), (17, 33, 9), (40, 40, 40), (2, 129, 3)])
+def test_mat_mult_small_reference_tolerance(dsp, torch_gpu, ref, m, k, n):
+    rng = np.random.default_rng(m * 1000 + k * 10 + n)
+    a = rng.uniform(-1, 1, (m, k)).astype(np.float32)
+    b = rng.uniform(-1, 1, (k, n)).astype(np.float32)
+    st, got = dsp.arm_mat_mult_f32(a, b)
+    st_r, want = ref.mat_mult(a, b)
+    assert st == 0 and st_r == 0
+    np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-5)
+
+
+def test_mat_mult_size_mismatch(dsp, torch_gpu):
+    import ctypes as C
+    A, B, Cm = dsp.arm_matrix_instance_f32(), dsp.arm_matrix_instance_f32(), dsp.arm_matrix_instance_f32()
+    buf = np.zeros(64, dtype=np.float32)
+    dsp.lib.arm_mat_init_f32(C.byref(A), 2, 3, buf.ctypes.data)
+    dsp.lib.arm_mat_init_f32(C.byref(B), 4, 2, buf.ctypes.data)
+    dsp.lib.arm_mat_init_f32(C.byref(Cm), 2, 2, buf.ctypes.data)
+    assert dsp.lib.arm_mat_mult_f32(C.byref(A), C.byref(B), C.byref(Cm)) == dsp.ARM_MATH_SIZE_MISMATCH
+
+
+@pytest.mark.parametrize("m,k,n,batch", [(256, 256, 256, 3), (300, 130, 200, 2), (1024, 1024, 1024, 1)])
+def test_mat_mult_batch_normwise(dsp, torch_gpu, ref, m, k, n, batch):
+    torch = torch_gpu
+    rng = np.random.default_rng(m + k + n)
+    a = rng.uniform(-1, 1, (batch, m, k)).astype(np.float32)
+    b = rng.uniform(-1, 1, (batch, k, n)).astype(np.float32)
+    da, db = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+    dc = torch.empty((batch, m, n), dtype=torch.float32, device="cuda")
+    dsp.mat_mult_batch(da, db, dc)
+    got = dc.cpu().numpy()
+    exact = np.einsum("bmk,bkn->bmn", a.astype(np.float64), b.astype(np.float64))
+    bound = 4 * k * np.finfo(np.float32).eps * np.einsum("bmk,bkn->bmn", np.abs(a), np.abs(b)).max()
+    assert np.abs(got - exact).max() <= bound
+    if m * k * n <= 256 ** 3:   # the reference itself on one item (seconds on the host)
+        st, want = ref.mat_mult(a[0], b[0])
+        assert np.abs(got[0] - want).max() <= 2 * bound
