@@ -1,0 +1,327 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X CMSIS-DSP backend — the BASELINE.json headline.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload WL] [--batch B]
+
+Default workload (BASELINE.json configs[1]): batched arm_cfft_f32, fftLen 1024,
+2^20 transforms per GPU (8 GiB in HBM, in place), bitReverseFlag 1; a step is one pass
+of the hot path over the batch, alternating forward / inverse (the inverse rescales by
+1/N, so values stay bounded).  The metric is whole-job complex samples per second.
+The same line carries the q31 N=4096 bit-exact companion measurement, the roofline of
+the dominant kernel (HIP-event average launch duration on the launch stream) and the
+reference scalar C timed on this host's cores (cpu_baseline).
+
+N > 1: launched by torch.distributed.run, one process per GPU; every rank processes its
+own 2^20 transforms (weak scaling, no data-path collective), timed between barriers,
+MAX over ranks.  Other workloads: cfft_q31_4096, cfft_q15_4096, fir_f32, mat_mult_f32.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cmsis-dsp_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import cmsisdsp_amd as dsp  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3     # dense f32 MFMA / packed-FMA VALU peak
+FP32_NOFMA_TFLOPS = 78.6     # separate v_mul_f32 + v_add_f32 (bit-exact FIR)
+METRIC = "Gsamples/sec batched arm_cfft_f32 N=1024 (+ q31 bit-exact) at 1/2/4/8 GPU"
+
+WORKLOADS = {
+    # name: (kind, fftLen / taps, default batch per GPU, algorithmic bytes per sample)
+    "cfft_f32_1024": ("f32", 1024, 1 << 20, 16),
+    "cfft_q31_4096": ("q31", 4096, 1 << 18, 16),
+    "cfft_q15_4096": ("q15", 4096, 1 << 18, 8),
+    "fir_f32": ("fir_f32", 128, 1 << 16, 8),
+    "mat_mult_f32": ("mat", 1024, 256, None),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# ------------------------------------------------------------------ distributed plumbing
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank
+
+
+def barrier(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def allreduce_max(x, world):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allreduce_sum(x, world):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+# ------------------------------------------------------------------ data + checkers
+def synth(kind, n_words, rank, salt=0):
+    """Deterministic synthetic input, rank-local (no scatter): uniform[-0.5,0.5) f32 or
+    full-range integers from a per-rank generator seeded 0x5EED + rank."""
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED + 1000003 * rank + salt)
+    if kind == "f32":
+        return torch.rand(n_words, generator=g, device="cuda", dtype=torch.float32) - 0.5
+    hi = 1 << (31 if kind == "q31" else 15)
+    dt = torch.int32 if kind == "q31" else torch.int16
+    return torch.randint(-hi, hi, (n_words,), generator=g, device="cuda", dtype=torch.int64).to(dt)
+
+
+def cpu_checker():
+    """The reference scalar C (oracle/_ref) if present, else the restatement (oracle/_build)."""
+    import refs
+    try:
+        return refs.ref_lib(), "reference"
+    except (FileNotFoundError, OSError):
+        return refs.oracle_lib(), "port"
+
+
+def flag_sequence(steps):
+    return [s & 1 for s in range(steps)]            # fwd, inv, fwd, ...
+
+
+# ------------------------------------------------------------------ CPU baseline
+def cpu_baseline(workload, n):
+    """Reference C on this host's cores, bounded sample (~16 thread-seconds)."""
+    threads = min(16, os.cpu_count() or 1)
+    secs = 1.0
+    exe_ref = os.path.join(ROOT, "oracle", "_ref", "bench_ref")
+    exe_port = os.path.join(ROOT, "oracle", "_build", "bench_port")
+    exe, kind = (exe_ref, "reference") if os.path.exists(exe_ref) else (exe_port, "port")
+    if not os.path.exists(exe):
+        return None
+    wl = {"cfft_f32_1024": "cfft_f32", "cfft_q31_4096": "cfft_q31", "cfft_q15_4096": "cfft_q15",
+          "fir_f32": "fir_f32", "mat_mult_f32": "mat_mult_f32"}[workload]
+    nn = 256 if workload == "mat_mult_f32" else n      # 1024^3 takes seconds per matrix on one core
+    out = subprocess.run([exe, wl, str(nn), str(threads), str(secs)], capture_output=True, text=True,
+                         timeout=120)
+    r = json.loads(out.stdout)
+    if workload == "mat_mult_f32":
+        return {"value": round(r["gflops"] * 1e-3, 6), "unit": "TFLOP/s", "cores": threads, "kind": kind,
+                "sample": f"{threads} threads x {secs:.0f} s of arm_mat_mult_f32 {nn}^3 (reference scalar C)"}
+    return {"value": round(r["gsamples_per_s"], 6), "unit": "Gsamples/s", "cores": threads, "kind": kind,
+            "sample": f"{threads} threads x {secs:.0f} s, {wl} n={nn}, {int(r['samples'])} samples "
+                      f"(reference scalar C, gcc -O2)"}
+
+
+# ------------------------------------------------------------------ timed loops
+def time_launches(launch, steps, warmup, world):
+    """W untimed, then K timed launches between barriers; returns (wall s, avg kernel ms)."""
+    for s in range(warmup):
+        launch(s)
+    barrier(world)
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for s in range(steps):
+        evs[s][0].record(stream)
+        launch(warmup + s)
+        evs[s][1].record(stream)
+    barrier(world)
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    return wall, kern_ms
+
+
+def run_cfft(kind, n, batch, steps, warmup, world, rank, check=True):
+    S = dsp.const_instance(f"arm_cfft_sR_{kind}_len{n}")
+    data = synth(kind, batch * 2 * n, rank).view(batch, 2 * n)
+    rows = sorted({0, 1, batch // 2, batch - 1})
+    before = data[rows].cpu().numpy().copy()
+    flags = flag_sequence(warmup + steps)
+
+    def launch(s):
+        dsp.cfft_batch(S, data, flags[s], 1)
+
+    wall, kern_ms = time_launches(launch, steps, warmup, world)
+    parity = None
+    if check:
+        # replay the exact flag sequence on the sampled rows with the CPU checker
+        host, hk = cpu_checker()
+        want = before
+        for f in flags:
+            want = host.cfft_many(kind, n, want, f, 1)
+        got = data[rows].cpu().numpy()
+        # plus a fresh 64-transform batch through one launch
+        fresh = synth(kind, 64 * 2 * n, rank, salt=17).view(64, 2 * n)
+        fin = fresh.cpu().numpy()
+        dsp.cfft_batch(S, fresh, 0, 1)
+        torch.cuda.synchronize()
+        ok = got.tobytes() == want.tobytes() and \
+            fresh.cpu().numpy().tobytes() == host.cfft_many(kind, n, fin, 0, 1).tobytes()
+        parity = {"checker": hk, "bit_exact": bool(ok), "transforms_checked": len(rows) + 64,
+                  "timed_buffer_rows_replayed": len(rows), "steps_replayed": len(flags)}
+    return wall, kern_ms, parity
+
+
+def run_fir(taps, batch, steps, warmup, world, rank, block=4096):
+    S = dsp.arm_fir_instance_f32()
+    rng = np.random.default_rng(5)
+    c = torch.from_numpy((rng.standard_normal(taps) / np.sqrt(taps)).astype(np.float32)).cuda()
+    import ctypes as C
+    S.numTaps = taps
+    S.pCoeffs = C.cast(c.data_ptr(), C.POINTER(C.c_float))
+    src = synth("f32", batch * block, rank).view(batch, block)
+    dst = torch.empty_like(src)
+    hist = torch.zeros((batch, taps - 1), dtype=torch.float32, device="cuda")
+
+    def launch(s):
+        dsp.fir_batch(S, src, dst, hist)
+
+    wall, kern_ms = time_launches(launch, steps, warmup, world)
+    # parity: two filters, one block, from zero history, vs the checker
+    host, hk = cpu_checker()
+    h0 = torch.zeros((2, taps - 1), dtype=torch.float32, device="cuda")
+    d0 = torch.empty((2, block), dtype=torch.float32, device="cuda")
+    dsp.fir_batch(S, src[:2].contiguous(), d0, h0)
+    torch.cuda.synchronize()
+    ok = all(d0[f].cpu().numpy().tobytes() ==
+             host.fir("f32", c.cpu().numpy(), [src[f].cpu().numpy()])[0][0].tobytes() for f in range(2))
+    return wall, kern_ms, {"checker": hk, "bit_exact": bool(ok), "filters_checked": 2}
+
+
+def run_mat(dim, batch, steps, warmup, world, rank):
+    a = synth("f32", batch * dim * dim, rank).view(batch, dim, dim) * 2
+    b = synth("f32", batch * dim * dim, rank, salt=3).view(batch, dim, dim) * 2
+    c = torch.empty_like(a)
+
+    def launch(s):
+        dsp.mat_mult_batch(a, b, c)
+
+    wall, kern_ms = time_launches(launch, steps, warmup, world)
+    exact = (a[0].double() @ b[0].double())
+    err = (c[0].double() - exact).abs().max().item()
+    bound = 4 * dim * np.finfo(np.float32).eps * (a[0].double().abs() @ b[0].double().abs()).max().item()
+    return wall, kern_ms, {"checker": "float64 GEMM of matrix 0", "max_abs_err": err, "bound": bound,
+                           "within_bound": bool(err <= bound)}
+
+
+def pmc_traffic(workload):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, when present."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    return json.load(open(p)).get(workload, {}).get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="cfft_f32_1024", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=0, help="items per GPU (default: the BASELINE config)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-companion", action="store_true", help="skip the q31 companion measurement")
+    args = ap.parse_args()
+
+    world, rank = dist_setup()
+    kind, n, batch0, bps = WORKLOADS[args.workload]
+    batch = args.batch or batch0
+    if args.workload.startswith("cfft"):
+        wall, kern_ms, parity = run_cfft(kind, n, batch, args.steps, args.warmup, world, rank)
+        units = batch * n                                 # complex samples per launch per GPU
+        algo_bytes = units * bps
+    elif args.workload == "fir_f32":
+        wall, kern_ms, parity = run_fir(n, batch, args.steps, args.warmup, world, rank)
+        units = batch * 4096
+        algo_bytes = units * bps + batch * (n - 1) * 8    # in + out + history read/write
+    else:
+        wall, kern_ms, parity = run_mat(n, batch, args.steps, args.warmup, world, rank)
+        units = batch                                      # matrices
+        algo_bytes = None
+
+    wall = allreduce_max(wall, world)
+    kern_ms = allreduce_max(kern_ms, world)
+    total_units = units * world * args.steps
+
+    line = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "data": "synthetic (per-rank seeded generator, rank-local, no scatter)"}
+    if args.workload == "mat_mult_f32":
+        flops = 2.0 * n * n * n * batch
+        line.update(value=round(total_units * 2.0 * n ** 3 / wall * 1e-12, 4), unit="TFLOP/s", dtype="f32",
+                    config={"workload": f"arm_mat_mult_f32 {n}x{n}x{n} batch={batch}/GPU (BASELINE configs[4])",
+                            "dims": [n, n, n], "batch_per_gpu": batch, "parallelism": f"dp{world} shards"})
+        achieved = flops / (kern_ms * 1e-3) * 1e-12
+        line["roofline"] = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
+                            "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                            "traffic": pmc_traffic(args.workload)}
+    else:
+        line.update(value=round(total_units / wall * 1e-9, 3), unit="Gsamples/s",
+                    dtype={"f32": "f32", "q31": "q31 (int32)", "q15": "q15 (int16)", "fir_f32": "f32"}[kind])
+        if args.workload.startswith("cfft"):
+            line["config"] = {"workload": f"arm_cfft_{kind} N={n} batch={batch}/GPU in place, bitReverseFlag=1, "
+                                          f"alternating fwd/inv (BASELINE configs[{1 if kind == 'f32' else 3}])",
+                              "fftLen": n, "batch_per_gpu": batch, "parallelism": f"dp{world} shards"}
+        else:
+            line["config"] = {"workload": f"arm_fir_f32 numTaps={n} blockSize=4096 batch={batch}/GPU "
+                                          "(BASELINE configs[2])", "numTaps": n, "blockSize": 4096,
+                              "batch_per_gpu": batch, "parallelism": f"dp{world} shards"}
+        achieved = algo_bytes / (kern_ms * 1e-3) * 1e-9
+        line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.workload),
+                            "algorithmic_bytes_per_launch": algo_bytes, "avg_kernel_ms": round(kern_ms, 4)}
+        if args.workload == "fir_f32":
+            valu = units * n * 2 / (kern_ms * 1e-3) * 1e-12
+            line["roofline"]["valu_tflops_nofma"] = {"achieved": round(valu, 2), "peak": FP32_NOFMA_TFLOPS,
+                                                     "frac": round(valu / FP32_NOFMA_TFLOPS, 4)}
+    line["parity"] = parity
+
+    if args.workload == "cfft_f32_1024" and not args.no_companion:
+        qb = 1 << 18
+        w2, k2, p2 = run_cfft("q31", 4096, qb, args.steps, args.warmup, world, rank)
+        w2 = allreduce_max(w2, world)
+        k2 = allreduce_max(k2, world)
+        ach = qb * 4096 * 16 / (k2 * 1e-3) * 1e-9
+        line["companion_q31"] = {"workload": f"arm_cfft_q31 N=4096 batch={qb}/GPU in place, bitReverseFlag=1",
+                                 "value": round(qb * 4096 * world * args.steps / w2 * 1e-9, 3), "unit": "Gsamples/s",
+                                 "hbm_gbs": round(ach, 1), "hbm_frac": round(ach / HBM_PEAK_GBS, 4),
+                                 "avg_kernel_ms": round(k2, 4), "parity": p2}
+
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        try:
+            line["cpu_baseline"] = cpu_baseline(args.workload, n)
+        except Exception as e:  # a missing/failed baseline must not hide the GPU number
+            log("cpu_baseline failed:", e)
+            line["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

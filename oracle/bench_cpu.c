@@ -1,0 +1,118 @@
+/*
+ * ORACLE — test infrastructure: the CPU baseline timing driver (bench.py cpu_baseline).
+ * Built twice from this one file:
+ *   oracle/_ref/bench_ref   -DBENCH_AGAINST_REFERENCE: linked to the reference's own
+ *                           objects (oracle/ref.mk) -> cpu_baseline.kind "reference";
+ *   oracle/_build/bench_port -DBENCH_AGAINST_ORACLE: linked to the restatement -> "port".
+ * Usage: bench_xxx <workload> <n> <threads> <seconds>
+ *   workload: cfft_f32 | cfft_q31 | cfft_q15 (n = fftLen), fir_f32 (n = numTaps, block 4096),
+ *             mat_mult_f32 (n = square dimension)
+ * Each thread owns its own buffers (the library is reentrant) and runs until the time
+ * budget is spent; in-place transforms alternate forward / inverse to stay bounded.
+ * Prints one JSON object: samples processed, seconds, threads, rate.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#ifdef BENCH_AGAINST_REFERENCE
+#include "arm_math.h"
+#include "arm_const_structs.h"
+#define F(name) name
+#else
+#include "src/oracle.h"
+#define F(name) oracle_##name
+arm_status oracle_arm_cfft_init_f32(arm_cfft_instance_f32 *S, uint16_t n);
+arm_status oracle_arm_cfft_init_q31(arm_cfft_instance_q31 *S, uint16_t n);
+arm_status oracle_arm_cfft_init_q15(arm_cfft_instance_q15 *S, uint16_t n);
+void oracle_arm_fir_init_f32(arm_fir_instance_f32 *S, uint16_t numTaps, const float *pCoeffs, float *pState,
+                             uint32_t blockSize);
+void oracle_arm_mat_init_f32(arm_matrix_instance_f32 *S, uint16_t r, uint16_t c, float *p);
+#endif
+
+static double now(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+typedef struct { const char *wl; int n; double seconds; int tid; double samples; double flops; } job_t;
+
+static uint64_t sm(uint64_t *s) {   /* splitmix64 */
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static float uni(uint64_t *s) { return (float)((sm(s) >> 40) * (1.0 / 16777216.0)) - 0.5f; }
+
+static void *worker(void *arg) {
+  job_t *j = (job_t *)arg;
+  uint64_t seed = 0x5EEDull + 7919ull * (uint64_t)j->tid;
+  const double t0 = now();
+  double samples = 0;
+  if (!strncmp(j->wl, "cfft_", 5)) {
+    const int n = j->n;
+    float *xf = malloc(sizeof(float) * 2 * n);
+    int32_t *xi = malloc(sizeof(int32_t) * 2 * n);
+    int16_t *xs = malloc(sizeof(int16_t) * 2 * n);
+    for (int i = 0; i < 2 * n; ++i) { xf[i] = uni(&seed); xi[i] = (int32_t)sm(&seed); xs[i] = (int16_t)(sm(&seed) >> 7); }
+    arm_cfft_instance_f32 Sf; arm_cfft_instance_q31 S31; arm_cfft_instance_q15 S15;
+    F(arm_cfft_init_f32)(&Sf, n); F(arm_cfft_init_q31)(&S31, n); F(arm_cfft_init_q15)(&S15, n);
+    uint64_t it = 0;
+    do {
+      for (int r = 0; r < 16; ++r, ++it) {
+        if (!strcmp(j->wl, "cfft_f32")) F(arm_cfft_f32)(&Sf, xf, (uint8_t)(it & 1), 1);
+        else if (!strcmp(j->wl, "cfft_q31")) F(arm_cfft_q31)(&S31, xi, 0, 1);
+        else F(arm_cfft_q15)(&S15, xs, 0, 1);
+      }
+      samples += 16.0 * n;
+    } while (now() - t0 < j->seconds);
+    free(xf); free(xi); free(xs);
+  } else if (!strcmp(j->wl, "fir_f32")) {
+    const int taps = j->n, block = 4096;
+    float *c = malloc(sizeof(float) * taps), *st = malloc(sizeof(float) * (taps + block - 1));
+    float *in = malloc(sizeof(float) * block), *out = malloc(sizeof(float) * block);
+    for (int i = 0; i < taps; ++i) c[i] = uni(&seed) * 0.1f;
+    for (int i = 0; i < block; ++i) in[i] = uni(&seed);
+    arm_fir_instance_f32 S;
+    F(arm_fir_init_f32)(&S, (uint16_t)taps, c, st, block);
+    do { F(arm_fir_f32)(&S, in, out, block); samples += block; } while (now() - t0 < j->seconds);
+    free(c); free(st); free(in); free(out);
+  } else if (!strcmp(j->wl, "mat_mult_f32")) {
+    const int d = j->n;
+    float *a = malloc(sizeof(float) * d * d), *b = malloc(sizeof(float) * d * d), *o = malloc(sizeof(float) * d * d);
+    for (int i = 0; i < d * d; ++i) { a[i] = uni(&seed); b[i] = uni(&seed); }
+    arm_matrix_instance_f32 A, B, O;
+    F(arm_mat_init_f32)(&A, d, d, a); F(arm_mat_init_f32)(&B, d, d, b); F(arm_mat_init_f32)(&O, d, d, o);
+    do { F(arm_mat_mult_f32)(&A, &B, &O); samples += (double)d * d; j->flops += 2.0 * d * d * d; }
+    while (now() - t0 < j->seconds);
+    free(a); free(b); free(o);
+  }
+  j->samples = samples;
+  return NULL;
+}
+
+int main(int argc, char **argv) {
+  if (argc < 5) { fprintf(stderr, "usage: %s workload n threads seconds\n", argv[0]); return 2; }
+  const char *wl = argv[1];
+  const int n = atoi(argv[2]), threads = atoi(argv[3]);
+  const double secs = atof(argv[4]);
+  pthread_t th[512];
+  job_t jobs[512];
+  const double t0 = now();
+  for (int t = 0; t < threads && t < 512; ++t) {
+    jobs[t] = (job_t){wl, n, secs, t, 0, 0};
+    pthread_create(&th[t], NULL, worker, &jobs[t]);
+  }
+  double samples = 0, flops = 0;
+  for (int t = 0; t < threads && t < 512; ++t) { pthread_join(th[t], NULL); samples += jobs[t].samples; flops += jobs[t].flops; }
+  const double el = now() - t0;
+  printf("{\"workload\": \"%s\", \"n\": %d, \"threads\": %d, \"seconds\": %.4f, \"samples\": %.0f, "
+         "\"gsamples_per_s\": %.6f, \"gflops\": %.4f}\n", wl, n, threads, el, samples, samples / el * 1e-9,
+         flops / el * 1e-9);
+  return 0;
+}

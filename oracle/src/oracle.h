@@ -1,0 +1,16 @@
+/* ORACLE — test infrastructure only.  Prototypes of the CPU restatement; the instance
+ * types are the reference layouts (include/arm_math.h). */
+#ifndef ORACLE_H
+#define ORACLE_H
+#include "../../include/arm_math.h"
+#include "../../include/arm_const_structs.h"
+
+void oracle_arm_cfft_f32(const arm_cfft_instance_f32 *S, float *p1, uint8_t ifftFlag, uint8_t bitReverseFlag);
+void oracle_arm_cfft_q31(const arm_cfft_instance_q31 *S, int32_t *p1, uint8_t ifftFlag, uint8_t bitReverseFlag);
+void oracle_arm_cfft_q15(const arm_cfft_instance_q15 *S, int16_t *p1, uint8_t ifftFlag, uint8_t bitReverseFlag);
+void oracle_arm_rfft_fast_f32(const arm_rfft_fast_instance_f32 *S, float *p, float *pOut, uint8_t ifftFlag);
+void oracle_arm_fir_f32(const arm_fir_instance_f32 *S, const float *pSrc, float *pDst, uint32_t blockSize);
+void oracle_arm_fir_q15(const arm_fir_instance_q15 *S, const int16_t *pSrc, int16_t *pDst, uint32_t blockSize);
+arm_status oracle_arm_mat_mult_f32(const arm_matrix_instance_f32 *A, const arm_matrix_instance_f32 *B,
+                                   arm_matrix_instance_f32 *C);
+#endif

@@ -1,0 +1,71 @@
+/*
+ * ORACLE — test infrastructure only (tests/, __graft_entry__.smoke(), bench.py cpu_baseline).
+ *
+ * CPU restatement of the reference's host scalar FIR and matrix multiply:
+ *   arm_fir_f32  Source/FilteringFunctions/arm_fir_f32.c:911-1280: y[n] = sum_k s[n+k]*c[k],
+ *                the accumulator starts at +0.0f, mul then add (no FMA), k ascending; the
+ *                8-way unrolled and the tail loops give the same order.
+ *   arm_fir_q15  arm_fir_q15.c:458-726 with ARM_MATH_LOOPUNROLL: outputs in groups of four
+ *                accumulate tap PAIRS as an int32-wrapped sum (__SMLALD, none.h:497-506),
+ *                the blockSize%4 tail accumulates every product in int64 (:649-681);
+ *                y = __SSAT((int32)(acc >> 15), 16).
+ *   state        s = [history (numTaps-1) ; block]; afterwards the state holds
+ *                [last numTaps-1 samples of s ; block] (:1242-1278).
+ *   arm_mat_mult_f32  arm_mat_mult_f32.c:600-730: per element, k-ordered mul-then-add.
+ * Pinned by tests/test_oracle.py against oracle/_ref bit for bit.
+ */
+#include <stdint.h>
+#include <string.h>
+
+#include "oracle.h"
+
+void oracle_arm_fir_f32(const arm_fir_instance_f32 *S, const float *pSrc, float *pDst, uint32_t blockSize) {
+  const uint32_t taps = S->numTaps;
+  float *s = S->pState;
+  memcpy(s + taps - 1, pSrc, sizeof(float) * blockSize);      /* append the block */
+  for (uint32_t n = 0; n < blockSize; ++n) {
+    float acc = 0.0f;
+    for (uint32_t k = 0; k < taps; ++k) {
+      const float prod = s[n + k] * S->pCoeffs[k];
+      acc = acc + prod;
+    }
+    pDst[n] = acc;
+  }
+  memmove(s, s + blockSize, sizeof(float) * (taps - 1));     /* carry the history */
+}
+
+static int16_t oracle_sat_q15(int32_t v) { return (int16_t)(v > 32767 ? 32767 : v < -32768 ? -32768 : v); }
+
+void oracle_arm_fir_q15(const arm_fir_instance_q15 *S, const int16_t *pSrc, int16_t *pDst, uint32_t blockSize) {
+  const uint32_t taps = S->numTaps, pairs = taps >> 1;
+  int16_t *s = S->pState;
+  const int16_t *c = S->pCoeffs;
+  memcpy(s + taps - 1, pSrc, sizeof(int16_t) * blockSize);
+  const uint32_t grouped = blockSize & ~3u;
+  for (uint32_t n = 0; n < blockSize; ++n) {
+    int64_t acc = 0;
+    for (uint32_t m = 0; m < pairs; ++m) {
+      const int32_t p0 = (int32_t)s[n + 2 * m] * c[2 * m];
+      const int32_t p1 = (int32_t)s[n + 2 * m + 1] * c[2 * m + 1];
+      if (n < grouped) acc += (int32_t)((uint32_t)p0 + (uint32_t)p1);   /* int32 pair sum */
+      else             acc += (int64_t)p0 + (int64_t)p1;
+    }
+    pDst[n] = oracle_sat_q15((int32_t)(acc >> 15));
+  }
+  memmove(s, s + blockSize, sizeof(int16_t) * (taps - 1));
+}
+
+arm_status oracle_arm_mat_mult_f32(const arm_matrix_instance_f32 *A, const arm_matrix_instance_f32 *B,
+                                   arm_matrix_instance_f32 *Cm) {
+  const uint32_t M = A->numRows, K = A->numCols, N = B->numCols;
+  for (uint32_t i = 0; i < M; ++i)
+    for (uint32_t j = 0; j < N; ++j) {
+      float acc = 0.0f;
+      for (uint32_t k = 0; k < K; ++k) {
+        const float prod = A->pData[i * K + k] * B->pData[k * N + j];
+        acc = acc + prod;
+      }
+      Cm->pData[i * N + j] = acc;
+    }
+  return ARM_MATH_SUCCESS;
+}

@@ -1,0 +1,85 @@
+"""CPU: the harvested CommonTables blobs and the permutations they induce."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TAB = os.path.join(ROOT, "cmsis-dsp_amd", "tables")
+SIZES = [16, 32, 64, 128, 256, 512, 1024, 2048, 4096]
+
+
+def test_blobs_match_manifest():
+    man = json.load(open(os.path.join(TAB, "MANIFEST.json")))
+    assert len(man["tables"]) == 53
+    for name, meta in man["tables"].items():
+        raw = open(os.path.join(TAB, name + ".bin"), "rb").read()
+        assert len(raw) == meta["bytes"] and hashlib.sha256(raw).hexdigest() == meta["sha256"], name
+
+
+def test_library_tables_are_the_blobs(dsp):
+    import ctypes as C
+    man = json.load(open(os.path.join(TAB, "MANIFEST.json")))
+    for name, meta in man["tables"].items():
+        addr = C.addressof(C.c_uint8.in_dll(dsp.lib, name))
+        assert C.string_at(addr, meta["bytes"]) == open(os.path.join(TAB, name + ".bin"), "rb").read(), name
+
+
+def test_library_tables_equal_reference_tables(dsp, ref):
+    """The product's embedded words are the reference's (read out of oracle/_ref)."""
+    import ctypes as C
+    man = json.load(open(os.path.join(TAB, "MANIFEST.json")))
+    for name, meta in man["tables"].items():
+        ours = C.string_at(C.addressof(C.c_uint8.in_dll(dsp.lib, name)), meta["bytes"])
+        theirs = C.string_at(C.addressof(C.c_uint8.in_dll(ref.lib, name)), meta["bytes"])
+        assert ours == theirs, name
+
+
+def _perm(table, n):
+    a = np.arange(n)
+    for i in range(0, len(table) - 1, 2):
+        x, y = table[i] >> 3, table[i + 1] >> 3
+        a[x], a[y] = a[y], a[x]
+    return a
+
+
+def _mixed_radix_src(n):
+    first = 2 if n in (16, 128, 1024) else 4 if n in (32, 256, 2048) else 1
+    out = np.zeros(n, dtype=np.int64)
+    for k in range(n):
+        kk, p, rem = k, 0, n
+        if first > 1:
+            rem //= first
+            p += (kk % first) * rem
+            kk //= first
+        while rem > 1:
+            rem //= 8
+            p += (kk & 7) * rem
+            kk >>= 3
+        out[k] = p
+    return out
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_f32_bitrev_table_is_mixed_radix_digit_reversal(n):
+    """armBitRevIndexTableN applied as sequential swaps == the digit reversal of the
+    [2|4, 8, 8, ...] DIF the kernels compute on the fly (runtime.cpp f32_src)."""
+    t = np.fromfile(os.path.join(TAB, f"armBitRevIndexTable{n}.bin"), dtype=np.uint16)
+    assert np.array_equal(_perm(t, n), _mixed_radix_src(n))
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_fixed_bitrev_table_is_binary_bit_reversal(n):
+    t = np.fromfile(os.path.join(TAB, f"armBitRevIndexTable_fixed_{n}.bin"), dtype=np.uint16)
+    bits = n.bit_length() - 1
+    br = np.array([int(format(k, f"0{bits}b")[::-1], 2) for k in range(n)])
+    assert np.array_equal(_perm(t, n), br)
+
+
+def test_f32_1024_table_is_not_an_involution():
+    """the N=1024 table is a product of cycles, so swap order matters."""
+    t = np.fromfile(os.path.join(TAB, "armBitRevIndexTable1024.bin"), dtype=np.uint16)
+    a = _perm(t, 1024)
+    assert not np.array_equal(a[a], np.arange(1024))

@@ -1,0 +1,31 @@
+/* Prints the byte layout of the hot-path instance structs.  Compiled against the
+ * reference headers (tools/make_golden.py -> tests/golden/abi_layout.json) and against
+ * include/ (tests/test_abi.py); the two must agree for the drop-in promise. */
+#include <stddef.h>
+#include <stdio.h>
+#include "arm_math.h"
+
+#define S(T) printf("  \"" #T "\": {\"size\": %zu", sizeof(T));
+#define F(T, f) printf(", \"" #f "\": %zu", offsetof(T, f));
+#define E() printf("},\n");
+
+int main(void) {
+  printf("{\n");
+  S(arm_cfft_instance_f32) F(arm_cfft_instance_f32, fftLen) F(arm_cfft_instance_f32, pTwiddle)
+    F(arm_cfft_instance_f32, pBitRevTable) F(arm_cfft_instance_f32, bitRevLength) E()
+  S(arm_cfft_instance_q31) F(arm_cfft_instance_q31, fftLen) F(arm_cfft_instance_q31, pTwiddle)
+    F(arm_cfft_instance_q31, pBitRevTable) F(arm_cfft_instance_q31, bitRevLength) E()
+  S(arm_cfft_instance_q15) F(arm_cfft_instance_q15, fftLen) F(arm_cfft_instance_q15, pTwiddle)
+    F(arm_cfft_instance_q15, pBitRevTable) F(arm_cfft_instance_q15, bitRevLength) E()
+  S(arm_rfft_fast_instance_f32) F(arm_rfft_fast_instance_f32, Sint) F(arm_rfft_fast_instance_f32, fftLenRFFT)
+    F(arm_rfft_fast_instance_f32, pTwiddleRFFT) E()
+  S(arm_fir_instance_f32) F(arm_fir_instance_f32, numTaps) F(arm_fir_instance_f32, pState)
+    F(arm_fir_instance_f32, pCoeffs) E()
+  S(arm_fir_instance_q15) F(arm_fir_instance_q15, numTaps) F(arm_fir_instance_q15, pState)
+    F(arm_fir_instance_q15, pCoeffs) E()
+  S(arm_matrix_instance_f32) F(arm_matrix_instance_f32, numRows) F(arm_matrix_instance_f32, numCols)
+    F(arm_matrix_instance_f32, pData) E()
+  printf("  \"arm_status\": {\"size\": %zu, \"ARM_MATH_SIZE_MISMATCH\": %d}\n}\n", sizeof(arm_status),
+         (int)ARM_MATH_SIZE_MISMATCH);
+  return 0;
+}
