@@ -22,9 +22,10 @@ namespace mi355x {
 constexpr float kC81 = 0.70710678118f;  // arm_cfft_radix8_f32.c:68
 
 // --- radix-8 DIF butterfly, arm_cfft_radix8_f32.c:188-281 (twiddled) and :87-138 (j==0).
-// v[m] = x[i1 + m*n2]; the reference's temporaries are reproduced one for one.
-template <bool TW>
-__device__ __forceinline__ void r8(float2 (&v)[8], const float2* __restrict__ w) {
+// v[m] = x[i1 + m*n2].  The j==0 group stores exactly the values the twiddled groups feed
+// to their twiddle multiply, so the butterfly is: untwiddled core, then (optionally) the
+// reference's complex multiply (co*r + si*s, co*s - si*r) on outputs 1..7.
+__device__ __forceinline__ void r8_core(float2 (&v)[8]) {
   float r1, r2, r3, r4, r5, r6, r7, r8v, t1, t2;
   float s1, s2, s3, s4, s5, s6, s7, s8;
   r1 = v[0].x + v[4].x;  r5 = v[0].x - v[4].x;
@@ -33,8 +34,8 @@ __device__ __forceinline__ void r8(float2 (&v)[8], const float2* __restrict__ w)
   r4 = v[3].x + v[7].x;  r8v = v[3].x - v[7].x;
   t1 = r1 - r3;  r1 = r1 + r3;
   r3 = r2 - r4;  r2 = r2 + r4;
-  float o0x = r1 + r2;
-  r2 = r1 - r2;                      // (j==0: stored to i5 directly)
+  const float o0x = r1 + r2;
+  r2 = r1 - r2;
   s1 = v[0].y + v[4].y;  s5 = v[0].y - v[4].y;
   s2 = v[1].y + v[5].y;  s6 = v[1].y - v[5].y;
   s3 = v[2].y + v[6].y;  s7 = v[2].y - v[6].y;
@@ -42,19 +43,10 @@ __device__ __forceinline__ void r8(float2 (&v)[8], const float2* __restrict__ w)
   t2 = s1 - s3;  s1 = s1 + s3;
   s3 = s2 - s4;  s2 = s2 + s4;
   r1 = t1 + s3;  t1 = t1 - s3;
-  float o0y = s1 + s2;
+  const float o0y = s1 + s2;
   s2 = s1 - s2;
   s1 = t2 - r3;  t2 = t2 + r3;
-  // outputs i5 (r2,s2), i3 (r1,s1), i7 (t1,t2)
-  float2 o4, o2, o6;
-  if (TW) {
-    float2 c5 = w[3], c3 = w[1], c7 = w[5];
-    o4.x = c5.x * r2 + c5.y * s2;  o4.y = c5.x * s2 - c5.y * r2;
-    o2.x = c3.x * r1 + c3.y * s1;  o2.y = c3.x * s1 - c3.y * r1;
-    o6.x = c7.x * t1 + c7.y * t2;  o6.y = c7.x * t2 - c7.y * t1;
-  } else {
-    o4 = make_float2(r2, s2);  o2 = make_float2(r1, s1);  o6 = make_float2(t1, t2);
-  }
+  const float2 o4 = make_float2(r2, s2), o2 = make_float2(r1, s1), o6 = make_float2(t1, t2);
   r1 = (r6 - r8v) * kC81;  r6 = (r6 + r8v) * kC81;
   s1 = (s6 - s8) * kC81;   s6 = (s6 + s8) * kC81;
   t1 = r5 - r1;  r5 = r5 + r1;
@@ -65,19 +57,33 @@ __device__ __forceinline__ void r8(float2 (&v)[8], const float2* __restrict__ w)
   r6 = t1 + s8;  t1 = t1 - s8;
   s1 = s5 - r7;  s5 = s5 + r7;
   s6 = t2 - r8v; t2 = t2 + r8v;
-  float2 o1, o7, o5, o3;
-  if (TW) {
-    float2 c2 = w[0], c8 = w[6], c6 = w[4], c4 = w[2];
-    o1.x = c2.x * r1 + c2.y * s1;  o1.y = c2.x * s1 - c2.y * r1;
-    o7.x = c8.x * r5 + c8.y * s5;  o7.y = c8.x * s5 - c8.y * r5;
-    o5.x = c6.x * r6 + c6.y * s6;  o5.y = c6.x * s6 - c6.y * r6;
-    o3.x = c4.x * t1 + c4.y * t2;  o3.y = c4.x * t2 - c4.y * t1;
-  } else {
-    o1 = make_float2(r1, s1);  o7 = make_float2(r5, s5);
-    o5 = make_float2(r6, s6);  o3 = make_float2(t1, t2);
-  }
   v[0] = make_float2(o0x, o0y);
-  v[1] = o1; v[2] = o2; v[3] = o3; v[4] = o4; v[5] = o5; v[6] = o6; v[7] = o7;
+  v[1] = make_float2(r1, s1); v[2] = o2; v[3] = make_float2(t1, t2); v[4] = o4;
+  v[5] = make_float2(r6, s6); v[6] = o6; v[7] = make_float2(r5, s5);
+}
+
+// reference twiddle multiply: p1 = co*r, p2 = si*s, p3 = co*s, p4 = si*r -> (p1+p2, p3-p4)
+__device__ __forceinline__ float2 twmul(float2 o, float2 c) {
+  return make_float2(c.x * o.x + c.y * o.y, c.x * o.y - c.y * o.x);
+}
+
+template <bool TW>
+__device__ __forceinline__ void r8(float2 (&v)[8], const float2* __restrict__ w) {
+  r8_core(v);
+  if (TW) {
+#pragma unroll
+    for (int m = 1; m < 8; ++m) v[m] = twmul(v[m], w[m - 1]);
+  }
+}
+
+// lane-dependent j==0 without divergence: twiddle, then select (v_cndmask)
+__device__ __forceinline__ void r8_sel(float2 (&v)[8], const float2 (&w)[7], bool tw) {
+  r8_core(v);
+#pragma unroll
+  for (int m = 1; m < 8; ++m) {
+    const float2 t = twmul(v[m], w[m - 1]);
+    v[m] = make_float2(tw ? t.x : v[m].x, tw ? t.y : v[m].y);
+  }
 }
 
 template <int N> struct PlanF32 {
@@ -244,6 +250,126 @@ __global__ __launch_bounds__(kBlock) void cfft_f32_kernel(float2* __restrict__ d
   }
 }
 
+// ============================================================================================
+// N = 1024 specialist (the BASELINE headline).  One wave per transform, persistent over the
+// batch.  Reference pass order: radix-2 pre-pass (radix8by2), then 3 radix-8 stages on each
+// 512-half, then the mixed-radix [2,8,8,8] digit reversal.
+//   phase A (registers): lane l loads x[l+64m] and x[512+l+64m] (m = 0..7, 512-B coalesced
+//            loads), runs the radix-2 pass on those 8 pairs and stage 0 of both halves
+//            (its butterflies are exactly {l+64m} and {512+l+64m});
+//   phase B (LDS exchange): stage 1, lane l = (q, j) = (l/8, l%8), both halves;
+//   phase C (LDS exchange): stage 2, butterflies p = l and p = l+64.  Frequency of output
+//            (p, m) is k = (p>>6) + 2*((p>>3)&7) + 16*(p&7) + 128*m, so lane l holds bins k
+//            (from p=l) and k+1 (from p=l+64): each output row m is one 16-B store per lane,
+//            the 64 lanes covering one contiguous 1 KiB — the bit reversal costs nothing.
+// Twiddles are lane-constant across transforms and live in 36 VGPRs for the kernel's life.
+// LDS: 16 blocks of 64 complex padded to 72, low 3 index bits XOR-swizzled with the next 3:
+// every exchange access pattern above is bank-conflict free.
+__device__ __forceinline__ int s1024(int e) {
+  return (e >> 6) * 72 + (((e >> 3) & 7) << 3) + ((e & 7) ^ ((e >> 3) & 7));
+}
+
+__global__ __launch_bounds__(64) void cfft_f32_n1024_kernel(float2* __restrict__ data, uint32_t batch,
+                                                           const float2* __restrict__ tw, uint32_t flags) {
+  __shared__ __attribute__((aligned(16))) float2 lds[16 * 72];
+  const int l = threadIdx.x;
+  const bool ifft = flags & kIfft;
+  const bool brev = flags & kBitrev;
+  const float invL = 1.0f / 1024.0f;
+
+  // lane-constant twiddles (arm_cfft_f32.c:909-933; arm_cfft_radix8_f32.c:152-174)
+  float2 wb[4], w0[7], w1[7];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) wb[i] = tw[l + 64 * i];
+#pragma unroll
+  for (int m = 0; m < 7; ++m) w0[m] = tw[2 * (m + 1) * l];          // stage 0: j = l, modifier 2
+  const int j1 = l & 7;
+#pragma unroll
+  for (int m = 0; m < 7; ++m) w1[m] = tw[16 * (m + 1) * j1];        // stage 1: j = l%8, modifier 16
+
+  for (uint32_t t = blockIdx.x; t < batch; t += gridDim.x) {
+    float2* X = data + (size_t)t * 1024;
+    // ---------------- phase A
+    float2 a[8], b[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) { a[m] = X[l + 64 * m]; b[m] = X[512 + l + 64 * m]; }
+    if (ifft) {
+#pragma unroll
+      for (int m = 0; m < 8; ++m) { a[m].y = -a[m].y; b[m].y = -b[m].y; }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {       // radix8by2 pre-pass, arm_cfft_f32.c:867-951
+      const float2 w = wb[m];
+      const float2 p = a[m], q = b[m];
+      a[m] = make_float2(p.x + q.x, p.y + q.y);
+      const float2 t2 = make_float2(p.x - q.x, p.y - q.y);
+      b[m] = make_float2(t2.x * w.x + t2.y * w.y, t2.y * w.x - t2.x * w.y);
+      const float2 c = a[m + 4], d = b[m + 4];
+      a[m + 4] = make_float2(c.x + d.x, c.y + d.y);
+      const float2 t4 = make_float2(d.x - c.x, d.y - c.y);
+      b[m + 4] = make_float2(t4.x * w.y - t4.y * w.x, t4.y * w.y + t4.x * w.x);
+    }
+    r8_sel(a, w0, l != 0);
+    r8_sel(b, w0, l != 0);
+    __syncthreads();                    // previous transform's phase C reads are done
+#pragma unroll
+    for (int m = 0; m < 8; ++m) { lds[s1024(l + 64 * m)] = a[m]; lds[s1024(512 + l + 64 * m)] = b[m]; }
+    __syncthreads();
+    // ---------------- phase B: stage 1
+    {
+      const int base = 64 * (l >> 3) + j1;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float2 v[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) v[m] = lds[s1024(h * 512 + base + 8 * m)];
+        r8_sel(v, w1, j1 != 0);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) lds[s1024(h * 512 + base + 8 * m)] = v[m];
+      }
+    }
+    __syncthreads();
+    // ---------------- phase C: stage 2 + digit reversal folded into the store
+#pragma unroll
+    for (int m = 0; m < 8; ++m) { a[m] = lds[s1024(8 * l + m)]; b[m] = lds[s1024(8 * (l + 64) + m)]; }
+    r8_core(a);
+    r8_core(b);
+    if (ifft) {                          // arm_cfft_f32.c:1285-1297
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        a[m] = make_float2(a[m].x * invL, -a[m].y * invL);
+        b[m] = make_float2(b[m].x * invL, -b[m].y * invL);
+      }
+    }
+    float4* Y = reinterpret_cast<float4*>(X);
+    if (brev) {
+      const int kl = 2 * (l >> 3) + 16 * (l & 7);    // bin of (p = l, m = 0)
+#pragma unroll
+      for (int m = 0; m < 8; ++m) Y[(kl + 128 * m) >> 1] = make_float4(a[m].x, a[m].y, b[m].x, b[m].y);
+    } else {
+#pragma unroll
+      for (int m = 0; m < 8; m += 2) {
+        Y[(8 * l + m) >> 1] = make_float4(a[m].x, a[m].y, a[m + 1].x, a[m + 1].y);
+        Y[(8 * (l + 64) + m) >> 1] = make_float4(b[m].x, b[m].y, b[m + 1].x, b[m + 1].y);
+      }
+    }
+  }
+}
+
+static int persistent_grid(const void* kernel, int block, size_t lds, uint32_t batch) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess || per_cu <= 0) per_cu = 8;
+  const uint64_t g = (uint64_t)cus * per_cu;
+  return (int)(g < batch ? g : batch);
+}
+
 template <int N>
 static hipError_t launch_f32(float2* data, uint32_t batch, const float2* tw, const uint16_t* perm,
                              uint32_t flags, hipStream_t st) {
@@ -265,7 +391,13 @@ hipError_t cfft_f32_launch(int n, float* data, uint32_t batch, const float* tw, 
     case 128:  return launch_f32<128>(d, batch, w, perm, flags, st);
     case 256:  return launch_f32<256>(d, batch, w, perm, flags, st);
     case 512:  return launch_f32<512>(d, batch, w, perm, flags, st);
-    case 1024: return launch_f32<1024>(d, batch, w, perm, flags, st);
+    case 1024:
+      if (!perm) {   // the reference's own table (or no reversal): the specialist kernel
+        const int grid = persistent_grid((const void*)cfft_f32_n1024_kernel, 64, 0, batch);
+        hipLaunchKernelGGL(cfft_f32_n1024_kernel, dim3(grid), dim3(64), 0, st, d, batch, w, flags);
+        return hipGetLastError();
+      }
+      return launch_f32<1024>(d, batch, w, perm, flags, st);
     case 2048: return launch_f32<2048>(d, batch, w, perm, flags, st);
     case 4096: return launch_f32<4096>(d, batch, w, perm, flags, st);
     default:   return hipSuccess;  // reference: unsupported length is a silent no-op

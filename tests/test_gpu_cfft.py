@@ -103,3 +103,14 @@ def test_cfft_custom_bitrev_table(dsp, torch_gpu, ref):
     buf = x.copy()
     ref.fn("arm_cfft_f32")(C.byref(Sr), buf.ctypes.data, 0, 1)
     assert got.tobytes() == buf.tobytes()
+
+
+@pytest.mark.parametrize("kind,n", [("f32", 1024), ("q31", 4096), ("q15", 4096), ("f32", 4096)])
+def test_cfft_batch_larger_than_resident_grid(dsp, torch_gpu, ref, kind, n):
+    """Persistent kernels loop over the batch: a batch several times the resident grid."""
+    batch = 9000 if n == 1024 else 2500
+    x = np.stack([refs.rand_input(kind, 2 * n, seed=r) for r in range(batch)])
+    for ifft in (0, 1):
+        got = _batched(dsp, torch_gpu, kind, n, x, ifft, 1)
+        want = ref.cfft_many(kind, n, x, ifft, 1)
+        assert got.tobytes() == want.tobytes()
