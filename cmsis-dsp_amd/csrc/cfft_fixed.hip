@@ -291,6 +291,147 @@ __global__ __launch_bounds__(kBlock) void cfft_fx_kernel(typename Fx<T>::C* __re
   }
 }
 
+// ============================================================================================
+// N = 4096 specialist (BASELINE configs[3]).  4096 = 4^6: six radix-4 stages fused in
+// pairs (radix-16 register passes), one 256-thread workgroup per transform, persistent.
+//   pass 1: thread c holds e = c + 256a + 1024b   -> stage 1 (over b), stage 2 (over a)
+//   pass 2: thread (q, j) = (t/16, t%16) holds e = 256q + j + 64a + 16b
+//                                                   -> stage 3 (over a), stage 4 (over b)
+//   pass 3: thread t holds e = 16*rev8(t) + 4a + b  -> stage 5 (over a), stage 6 (over b)
+// Output position e = 16*rev8(t) + u goes to bin rev12(e) = rev4(u)*256 + t: for every u
+// the 256 threads store 256 consecutive bins, so the bit reversal is free.
+// LDS: 4096 complex padded s(e) = e + 8*(e>>7) + (e>>9) (4351 slots): every exchange
+// pattern above is bank-conflict free and, being additive, addressed as lane base +
+// immediate (found by exhaustive search over two-term paddings).
+__device__ __forceinline__ int s4096(int e) { return e + 8 * (e >> 7) + (e >> 9); }
+
+template <typename T, bool INV>
+__global__ __launch_bounds__(256) void cfft_fx4096_kernel(typename Fx<T>::C* __restrict__ data, uint32_t batch,
+                                                          const typename Fx<T>::C* __restrict__ tw, uint32_t flags) {
+  using F = Fx<T>;
+  using C = typename F::C;
+  __shared__ __attribute__((aligned(16))) C lds[4351];
+  const int t = threadIdx.x;
+  const bool brev = flags & kBitrev;
+  const int q2 = t >> 4, j2 = t & 15;
+  const int q3 = (int)(__brev((uint32_t)t) >> 24);        // rev8(t)
+
+  // Lane-constant twiddles, loaded once for the kernel's life (stored in the table's own
+  // word type: q15 keeps two per VGPR).  (w1, w2, w3) = table[ia], table[2ia], table[3ia].
+  C tw1[4][3], tw2[3], tw3[4][3], tw4[3], tw5[4][3];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int ia1 = t + 256 * a, ia3 = (j2 + 16 * a) * 16, ia5 = a * 256;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      tw1[a][k] = tw[(k + 1) * ia1];
+      tw3[a][k] = tw[(k + 1) * ia3];
+      tw5[a][k] = tw[(k + 1) * ia5];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { tw2[k] = tw[(k + 1) * 4 * t]; tw4[k] = tw[(k + 1) * 64 * j2]; }
+  auto W = [](C c) { return make_int2(c.x, c.y); };
+
+  int2 v[16], nv[16];
+  if (blockIdx.x < batch) {
+    const C* X0 = data + (size_t)blockIdx.x * 4096;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) nv[4 * a + b] = F::ld(X0 + t + 256 * a + 1024 * b);
+  }
+  for (uint32_t tr = blockIdx.x; tr < batch; tr += gridDim.x) {
+    C* X = data + (size_t)tr * 4096;
+    // ---------------- pass 1: stages 1 (first) and 2
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = nv[u];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+      bfly<T, INV, 0>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], W(tw1[a][0]), W(tw1[a][1]), W(tw1[a][2]));
+#pragma unroll
+    for (int b = 0; b < 4; ++b) bfly<T, INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], W(tw2[0]), W(tw2[1]), W(tw2[2]));
+    __syncthreads();                    // the previous transform's pass-3 reads are done
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) F::st(lds + s4096(t + 256 * a + 1024 * b), v[4 * a + b]);
+    if (tr + gridDim.x < batch) {       // next transform's loads fly under passes 2 and 3
+      const C* XN = data + (size_t)(tr + gridDim.x) * 4096;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) nv[4 * a + b] = F::ld(XN + t + 256 * a + 1024 * b);
+    }
+    __syncthreads();
+    // ---------------- pass 2: stages 3 and 4
+    {
+      const int base = 256 * q2 + j2;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) v[4 * a + b] = F::ld(lds + s4096(base + 64 * a + 16 * b));
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        bfly<T, INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], W(tw3[b][0]), W(tw3[b][1]), W(tw3[b][2]));
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        bfly<T, INV, 1>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], W(tw4[0]), W(tw4[1]), W(tw4[2]));
+      __syncthreads();
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) F::st(lds + s4096(base + 64 * a + 16 * b), v[4 * a + b]);
+    }
+    __syncthreads();
+    // ---------------- pass 3: stages 5 and 6 (last)
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) v[4 * a + b] = F::ld(lds + s4096(16 * q3 + 4 * a + b));
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      bfly<T, INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], W(tw5[b][0]), W(tw5[b][1]), W(tw5[b][2]));
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+      bfly<T, INV, 2>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], int2{}, int2{}, int2{});
+    if (brev) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) F::st(X + (int)(__brev((uint32_t)u) >> 28) * 256 + t, v[u]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) F::st(X + 16 * q3 + u, v[u]);
+    }
+  }
+}
+
+static int fx_persistent_grid(const void* kernel, uint32_t batch) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 2;
+  const uint64_t g = (uint64_t)cus * per_cu;
+  return (int)(g < batch ? g : batch);
+}
+
+template <typename T>
+static hipError_t launch_fx4096(void* data, uint32_t batch, const void* tw, uint32_t flags, hipStream_t st) {
+  using C = typename Fx<T>::C;
+  if (flags & kIfft) {
+    const int grid = fx_persistent_grid((const void*)cfft_fx4096_kernel<T, true>, batch);
+    hipLaunchKernelGGL((cfft_fx4096_kernel<T, true>), dim3(grid), dim3(256), 0, st, (C*)data, batch, (const C*)tw, flags);
+  } else {
+    const int grid = fx_persistent_grid((const void*)cfft_fx4096_kernel<T, false>, batch);
+    hipLaunchKernelGGL((cfft_fx4096_kernel<T, false>), dim3(grid), dim3(256), 0, st, (C*)data, batch, (const C*)tw, flags);
+  }
+  return hipGetLastError();
+}
+
 template <typename T, int N>
 static hipError_t launch_fx(void* data, uint32_t batch, const void* tw, const uint16_t* perm,
                             uint32_t flags, hipStream_t st) {
@@ -319,7 +460,9 @@ static hipError_t dispatch_fx(int n, void* data, uint32_t batch, const void* tw,
     case 512:  return launch_fx<T, 512>(data, batch, tw, perm, flags, st);
     case 1024: return launch_fx<T, 1024>(data, batch, tw, perm, flags, st);
     case 2048: return launch_fx<T, 2048>(data, batch, tw, perm, flags, st);
-    case 4096: return launch_fx<T, 4096>(data, batch, tw, perm, flags, st);
+    case 4096:
+      if (!perm) return launch_fx4096<T>(data, batch, tw, flags, st);   // reference table: specialist
+      return launch_fx<T, 4096>(data, batch, tw, perm, flags, st);
     default:   return hipSuccess;   // reference: unsupported length is a silent no-op
   }
 }
