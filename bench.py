@@ -28,7 +28,6 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
 import cmsisdsp_amd as dsp  # noqa: E402
 
@@ -52,46 +51,25 @@ def log(*a):
 
 
 # ------------------------------------------------------------------ distributed plumbing
-def dist_setup():
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return world, rank
+from cmsisdsp_amd import parallel  # noqa: E402
+
+WORLD = parallel.World()
 
 
 def barrier(world):
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    parallel.barrier(WORLD)
 
 
 def allreduce_max(x, world):
-    if world == 1:
-        return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def allreduce_sum(x, world):
-    if world == 1:
-        return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return parallel.reduce_max(WORLD, x)
 
 
 # ------------------------------------------------------------------ data + checkers
 def synth(kind, n_words, rank, salt=0):
     """Deterministic synthetic input, rank-local (no scatter): uniform[-0.5,0.5) f32 or
-    full-range integers from a per-rank generator seeded 0x5EED + rank."""
+    full-range integers from a per-rank generator (parallel.seed_for)."""
     g = torch.Generator(device="cuda")
-    g.manual_seed(0x5EED + 1000003 * rank + salt)
+    g.manual_seed(parallel.seed_for(rank, salt))
     if kind == "f32":
         return torch.rand(n_words, generator=g, device="cuda", dtype=torch.float32) - 0.5
     hi = 1 << (31 if kind == "q31" else 15)
@@ -179,10 +157,15 @@ def run_cfft(kind, n, batch, steps, warmup, world, rank, check=True):
         fin = fresh.cpu().numpy()
         dsp.cfft_batch(S, fresh, 0, 1)
         torch.cuda.synchronize()
-        ok = got.tobytes() == want.tobytes() and \
-            fresh.cpu().numpy().tobytes() == host.cfft_many(kind, n, fin, 0, 1).tobytes()
-        parity = {"checker": hk, "bit_exact": bool(ok), "transforms_checked": len(rows) + 64,
-                  "timed_buffer_rows_replayed": len(rows), "steps_replayed": len(flags)}
+        fresh_got = fresh.cpu().numpy()
+        fresh_want = host.cfft_many(kind, n, fin, 0, 1)
+        rec = {"rank": rank,
+               "gpu_digest": parallel.digest(np.concatenate([got.ravel(), fresh_got.ravel()]).view(np.uint8)),
+               "ref_digest": parallel.digest(np.concatenate([want.ravel(), fresh_want.ravel()]).view(np.uint8))}
+        all_ok, combined = parallel.checksum_of_checksums(parallel.gather_objects(WORLD, rec))
+        parity = {"checker": hk, "bit_exact": bool(all_ok), "transforms_checked_per_rank": len(rows) + 64,
+                  "timed_buffer_rows_replayed": len(rows), "steps_replayed": len(flags),
+                  "ranks_checked": world, "checksum_of_checksums": f"{combined:016x}"}
     return wall, kern_ms, parity
 
 
@@ -245,9 +228,12 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="items per GPU (default: the BASELINE config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-companion", action="store_true", help="skip the q31 companion measurement")
+    ap.add_argument("--dist-backend", default=None, help="nccl (default, RCCL) or gloo (rehearsal)")
     args = ap.parse_args()
 
-    world, rank = dist_setup()
+    global WORLD
+    WORLD = parallel.init(backend=args.dist_backend)
+    world, rank = WORLD.size, WORLD.rank
     kind, n, batch0, bps = WORKLOADS[args.workload]
     batch = args.batch or batch0
     if args.workload.startswith("cfft"):
@@ -309,7 +295,8 @@ def main():
         line["companion_q31"] = {"workload": f"arm_cfft_q31 N=4096 batch={qb}/GPU in place, bitReverseFlag=1",
                                  "value": round(qb * 4096 * world * args.steps / w2 * 1e-9, 3), "unit": "Gsamples/s",
                                  "hbm_gbs": round(ach, 1), "hbm_frac": round(ach / HBM_PEAK_GBS, 4),
-                                 "avg_kernel_ms": round(k2, 4), "parity": p2}
+                                 "avg_kernel_ms": round(k2, 4), "traffic": pmc_traffic("cfft_q31_4096"),
+                                 "parity": p2}
 
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         try:
@@ -319,8 +306,7 @@ def main():
             line["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    parallel.shutdown(WORLD)
 
 
 if __name__ == "__main__":
