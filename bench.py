@@ -206,8 +206,8 @@ def run_mat(dim, batch, steps, warmup, world, rank):
     wall, kern_ms = time_launches(launch, steps, warmup, world)
     exact = (a[0].double() @ b[0].double())
     err = (c[0].double() - exact).abs().max().item()
-    bound = 4 * dim * np.finfo(np.float32).eps * (a[0].double().abs() @ b[0].double().abs()).max().item()
-    return wall, kern_ms, {"checker": "float64 GEMM of matrix 0", "max_abs_err": err, "bound": bound,
+    bound = float(4 * dim * np.finfo(np.float32).eps * (a[0].double().abs() @ b[0].double().abs()).max().item())
+    return wall, kern_ms, {"checker": "float64 GEMM of matrix 0", "max_abs_err": float(err), "bound": bound,
                            "within_bound": bool(err <= bound)}
 
 
