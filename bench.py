@@ -13,7 +13,7 @@ reference scalar C timed on this host's cores (cpu_baseline).
 
 N > 1: launched by torch.distributed.run, one process per GPU; every rank processes its
 own 2^20 transforms (weak scaling, no data-path collective), timed between barriers,
-MAX over ranks.  Other workloads: cfft_q31_4096, cfft_q15_4096, fir_f32, mat_mult_f32.
+MAX over ranks.  Other workloads: cfft_q31_4096, cfft_q15_4096, fir_f32, fir_q15, mat_mult_f32.
 """
 import argparse
 import json
@@ -42,6 +42,7 @@ WORKLOADS = {
     "cfft_q31_4096": ("q31", 4096, 1 << 18, 16),
     "cfft_q15_4096": ("q15", 4096, 1 << 18, 8),
     "fir_f32": ("fir_f32", 128, 1 << 16, 8),
+    "fir_q15": ("fir_q15", 128, 1 << 16, 4),
     "mat_mult_f32": ("mat", 1024, 256, None),
 }
 
@@ -101,7 +102,7 @@ def cpu_baseline(workload, n):
     if not os.path.exists(exe):
         return None
     wl = {"cfft_f32_1024": "cfft_f32", "cfft_q31_4096": "cfft_q31", "cfft_q15_4096": "cfft_q15",
-          "fir_f32": "fir_f32", "mat_mult_f32": "mat_mult_f32"}[workload]
+          "fir_f32": "fir_f32", "fir_q15": "fir_q15", "mat_mult_f32": "mat_mult_f32"}[workload]
     nn = 256 if workload == "mat_mult_f32" else n      # 1024^3 takes seconds per matrix on one core
     out = subprocess.run([exe, wl, str(nn), str(threads), str(secs)], capture_output=True, text=True,
                          timeout=120)
@@ -169,29 +170,35 @@ def run_cfft(kind, n, batch, steps, warmup, world, rank, check=True):
     return wall, kern_ms, parity
 
 
-def run_fir(taps, batch, steps, warmup, world, rank, block=4096):
-    S = dsp.arm_fir_instance_f32()
-    rng = np.random.default_rng(5)
-    c = torch.from_numpy((rng.standard_normal(taps) / np.sqrt(taps)).astype(np.float32)).cuda()
+def run_fir(kind, taps, batch, steps, warmup, world, rank, block=4096):
     import ctypes as C
+    q15 = kind == "q15"
+    rng = np.random.default_rng(5)
+    if q15:
+        S = dsp.arm_fir_instance_q15()
+        c = torch.from_numpy(rng.integers(-32768, 32768, taps).astype(np.int16)).cuda()
+        src = synth("q15", batch * block, rank).view(batch, block)
+    else:
+        S = dsp.arm_fir_instance_f32()
+        c = torch.from_numpy((rng.standard_normal(taps) / np.sqrt(taps)).astype(np.float32)).cuda()
+        src = synth("f32", batch * block, rank).view(batch, block)
     S.numTaps = taps
-    S.pCoeffs = C.cast(c.data_ptr(), C.POINTER(C.c_float))
-    src = synth("f32", batch * block, rank).view(batch, block)
+    S.pCoeffs = C.cast(c.data_ptr(), S._fields_[2][1])
     dst = torch.empty_like(src)
-    hist = torch.zeros((batch, taps - 1), dtype=torch.float32, device="cuda")
+    hist = torch.zeros((batch, taps - 1), dtype=src.dtype, device="cuda")
 
     def launch(s):
-        dsp.fir_batch(S, src, dst, hist)
+        dsp.fir_batch(S, src, dst, hist, q15=q15)
 
     wall, kern_ms = time_launches(launch, steps, warmup, world)
     # parity: two filters, one block, from zero history, vs the checker
     host, hk = cpu_checker()
-    h0 = torch.zeros((2, taps - 1), dtype=torch.float32, device="cuda")
-    d0 = torch.empty((2, block), dtype=torch.float32, device="cuda")
-    dsp.fir_batch(S, src[:2].contiguous(), d0, h0)
+    h0 = torch.zeros((2, taps - 1), dtype=src.dtype, device="cuda")
+    d0 = torch.empty((2, block), dtype=src.dtype, device="cuda")
+    dsp.fir_batch(S, src[:2].contiguous(), d0, h0, q15=q15)
     torch.cuda.synchronize()
     ok = all(d0[f].cpu().numpy().tobytes() ==
-             host.fir("f32", c.cpu().numpy(), [src[f].cpu().numpy()])[0][0].tobytes() for f in range(2))
+             host.fir(kind, c.cpu().numpy(), [src[f].cpu().numpy()])[0][0].tobytes() for f in range(2))
     return wall, kern_ms, {"checker": hk, "bit_exact": bool(ok), "filters_checked": 2}
 
 
@@ -240,10 +247,10 @@ def main():
         wall, kern_ms, parity = run_cfft(kind, n, batch, args.steps, args.warmup, world, rank)
         units = batch * n                                 # complex samples per launch per GPU
         algo_bytes = units * bps
-    elif args.workload == "fir_f32":
-        wall, kern_ms, parity = run_fir(n, batch, args.steps, args.warmup, world, rank)
+    elif args.workload.startswith("fir"):
+        wall, kern_ms, parity = run_fir(kind[4:], n, batch, args.steps, args.warmup, world, rank)
         units = batch * 4096
-        algo_bytes = units * bps + batch * (n - 1) * 8    # in + out + history read/write
+        algo_bytes = units * bps + batch * (n - 1) * bps  # in + out + history read/write
     else:
         wall, kern_ms, parity = run_mat(n, batch, args.steps, args.warmup, world, rank)
         units = batch                                      # matrices
@@ -267,19 +274,26 @@ def main():
                             "traffic": pmc_traffic(args.workload)}
     else:
         line.update(value=round(total_units / wall * 1e-9, 3), unit="Gsamples/s",
-                    dtype={"f32": "f32", "q31": "q31 (int32)", "q15": "q15 (int16)", "fir_f32": "f32"}[kind])
+                    dtype={"f32": "f32", "q31": "q31 (int32)", "q15": "q15 (int16)", "fir_f32": "f32",
+                           "fir_q15": "q15 (int16 x int16 -> int64)"}[kind])
         if args.workload.startswith("cfft"):
             line["config"] = {"workload": f"arm_cfft_{kind} N={n} batch={batch}/GPU in place, bitReverseFlag=1, "
                                           f"alternating fwd/inv (BASELINE configs[{1 if kind == 'f32' else 3}])",
                               "fftLen": n, "batch_per_gpu": batch, "parallelism": f"dp{world} shards"}
         else:
-            line["config"] = {"workload": f"arm_fir_f32 numTaps={n} blockSize=4096 batch={batch}/GPU "
-                                          "(BASELINE configs[2])", "numTaps": n, "blockSize": 4096,
+            line["config"] = {"workload": f"arm_{kind} numTaps={n} blockSize=4096 batch={batch}/GPU "
+                                          + ("(BASELINE configs[2])" if kind == "fir_f32" else "(configs[2] shape, q15)"),
+                              "numTaps": n, "blockSize": 4096,
                               "batch_per_gpu": batch, "parallelism": f"dp{world} shards"}
         achieved = algo_bytes / (kern_ms * 1e-3) * 1e-9
         line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.workload),
                             "algorithmic_bytes_per_launch": algo_bytes, "avg_kernel_ms": round(kern_ms, 4)}
+        if args.workload == "fir_q15":
+            # one v_dot2_i32_i16 per tap pair per h/l half: T VALU ops per output sample
+            valu = units * n / (kern_ms * 1e-3) * 1e-12
+            line["roofline"]["valu_tops_dot2"] = {"achieved": round(valu, 2), "peak": FP32_NOFMA_TFLOPS,
+                                                  "frac": round(valu / FP32_NOFMA_TFLOPS, 4)}
         if args.workload == "fir_f32":
             valu = units * n * 2 / (kern_ms * 1e-3) * 1e-12
             line["roofline"]["valu_tflops_nofma"] = {"achieved": round(valu, 2), "peak": FP32_NOFMA_TFLOPS,

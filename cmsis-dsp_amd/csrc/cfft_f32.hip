@@ -410,20 +410,6 @@ __global__ __launch_bounds__(64, MI355X_N1024_WAVES) void cfft_f32_n1024_kernel(
   }
 }
 
-static int persistent_grid(const void* kernel, int block, size_t lds, uint32_t batch) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
-  }
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess || per_cu <= 0) per_cu = 8;
-  const uint64_t g = (uint64_t)cus * per_cu;
-  return (int)(g < batch ? g : batch);
-}
-
 template <int N>
 static hipError_t launch_f32(float2* data, uint32_t batch, const float2* tw, const uint16_t* perm,
                              uint32_t flags, hipStream_t st) {
@@ -447,7 +433,7 @@ hipError_t cfft_f32_launch(int n, float* data, uint32_t batch, const float* tw, 
     case 512:  return launch_f32<512>(d, batch, w, perm, flags, st);
     case 1024:
       if (!perm) {   // the reference's own table (or no reversal): the specialist kernel
-        const int grid = persistent_grid((const void*)cfft_f32_n1024_kernel, 64, 0, batch);
+        const int grid = persistent_grid((const void*)cfft_f32_n1024_kernel, 64, 0, batch, 8);
         hipLaunchKernelGGL(cfft_f32_n1024_kernel, dim3(grid), dim3(64), 0, st, d, batch, w, flags);
         return hipGetLastError();
       }

@@ -405,28 +405,14 @@ __global__ __launch_bounds__(256) void cfft_fx4096_kernel(typename Fx<T>::C* __r
   }
 }
 
-static int fx_persistent_grid(const void* kernel, uint32_t batch) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
-  }
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 2;
-  const uint64_t g = (uint64_t)cus * per_cu;
-  return (int)(g < batch ? g : batch);
-}
-
 template <typename T>
 static hipError_t launch_fx4096(void* data, uint32_t batch, const void* tw, uint32_t flags, hipStream_t st) {
   using C = typename Fx<T>::C;
   if (flags & kIfft) {
-    const int grid = fx_persistent_grid((const void*)cfft_fx4096_kernel<T, true>, batch);
+    const int grid = persistent_grid((const void*)cfft_fx4096_kernel<T, true>, 256, 0, batch);
     hipLaunchKernelGGL((cfft_fx4096_kernel<T, true>), dim3(grid), dim3(256), 0, st, (C*)data, batch, (const C*)tw, flags);
   } else {
-    const int grid = fx_persistent_grid((const void*)cfft_fx4096_kernel<T, false>, batch);
+    const int grid = persistent_grid((const void*)cfft_fx4096_kernel<T, false>, 256, 0, batch);
     hipLaunchKernelGGL((cfft_fx4096_kernel<T, false>), dim3(grid), dim3(256), 0, st, (C*)data, batch, (const C*)tw, flags);
   }
   return hipGetLastError();

@@ -24,91 +24,298 @@ constexpr int kFirR = 8;                       // outputs per lane
 constexpr int kFirChunk = kBlock * kFirR;      // outputs per workgroup (2048)
 constexpr int kFirMaxTaps = 1024;              // LDS budget: (2048 + 1023) * 4 B
 
-// LDS index with one pad word every 32 (lanes read at a stride of R words)
-__device__ __forceinline__ int padx(int i) { return i + (i >> 5); }
-
+// Work items are (filter, chunk) pairs, item = f * nchunks + chunk.  The kernels are
+// persistent (grid = what the CUs hold): while a workgroup filters item i from LDS, the
+// window of item i + gridDim.x is already in flight into registers, so the HBM latency of
+// the staging overlaps the MACs instead of stalling every co-resident workgroup at once.
+struct FirItem {
+  uint32_t f;
+  int n0, count, total;   // first output, outputs in the chunk, window samples (count + T - 1)
+};
+__device__ __forceinline__ FirItem fir_item(uint32_t item, uint32_t nchunks, uint32_t B, int T1) {
+  FirItem it;
+  it.f = item / nchunks;
+  it.n0 = (int)(item - it.f * nchunks) * kFirChunk;
+  it.count = min((int)B - it.n0, kFirChunk);
+  it.total = it.count + T1;
+  return it;
+}
+// window sample j of an item: s[n0 + j] with s = [history (T-1) ; block input], 0 past the
+// window.  Branch-free (pointer select, index clamped in bounds) so that a thread's loads
+// all issue back to back instead of each waiting at a divergent join.
 template <typename T>
-__device__ __forceinline__ void stage_window(T* win, const T* __restrict__ hist, const T* __restrict__ src,
-                                             int T1, int n0, int count) {
-  // window[j] = s[n0 + j], j < count + T1, where s = [hist(T1) ; src]
-  const int total = count + T1;
-  for (int j = threadIdx.x; j < total; j += kBlock) {
-    const int sidx = n0 + j;
-    win[padx(j)] = sidx < T1 ? hist[sidx] : src[sidx - T1];
+__device__ __forceinline__ T fir_sample(const T* __restrict__ hist, const T* __restrict__ src, const FirItem& it,
+                                        uint32_t B, int T1, int j) {
+  const int sidx = it.n0 + min(j, it.total - 1);
+  const T* p = sidx < T1 ? hist + ((uint64_t)it.f * T1 + sidx) : src + ((uint64_t)it.f * B + (sidx - T1));
+  const T v = *p;
+  return j < it.total ? v : (T)0;
+}
+
+// ---------------------------------------------------------------- f32
+constexpr int kFirPre = (kFirChunk + kFirMaxTaps - 1 + kBlock - 1) / kBlock;   // window samples per thread
+
+// LDS index with one pad word every 8: lanes read at a stride of R = 8 words from any
+// offset, and i + i/8 keeps every ds_read_b32 32-lane group on 32 distinct banks (one
+// pad per 32 words is conflict-free only at offsets that are multiples of 32).
+__device__ __forceinline__ int padx(int i) { return i + (i >> 3); }
+
+__device__ __forceinline__ void fir_f32_fetch(float (&pre)[kFirPre], const float* hist, const float* src,
+                                              const FirItem& it, uint32_t B, int T1) {
+#pragma unroll
+  for (int k = 0; k < kFirPre; ++k) {
+    const int j = threadIdx.x + k * kBlock;
+    pre[k] = fir_sample(hist, src, it, B, T1, j);
   }
 }
 
 __global__ __launch_bounds__(kBlock) void fir_f32_kernel(const float* __restrict__ coeffs, int T,
                                                          const float* __restrict__ src, float* __restrict__ dst,
-                                                         uint32_t B, const float* __restrict__ hist_in) {
-  __shared__ float win[(kFirChunk + kFirMaxTaps) * 33 / 32 + 32];
-  const uint32_t f = blockIdx.y;
-  const int n0 = blockIdx.x * kFirChunk;
-  const int count = min((int)B - n0, kFirChunk);
+                                                         uint32_t B, const float* __restrict__ hist_in,
+                                                         uint32_t nchunks, uint32_t items) {
+  __shared__ float win[(kFirChunk + kFirMaxTaps) * 9 / 8 + 32];
   const int T1 = T - 1;
-  const float* s_src = src + (uint64_t)f * B;
-  const float* s_hist = hist_in + (uint64_t)f * T1;
-  stage_window(win, s_hist, s_src, T1, n0, count);
-  __syncthreads();
+  uint32_t item = blockIdx.x;
+  if (item >= items) return;
+  float pre[kFirPre];
+  FirItem it = fir_item(item, nchunks, B, T1);
+  fir_f32_fetch(pre, hist_in, src, it, B, T1);
+  for (; item < items; item += gridDim.x) {
+    __syncthreads();                                // the previous item is done with win
+#pragma unroll
+    for (int k = 0; k < kFirPre; ++k) {
+      const int j = threadIdx.x + k * kBlock;
+      if (j < it.total) win[padx(j)] = pre[k];
+    }
+    __syncthreads();
+    const FirItem cur = it;
+    if (item + gridDim.x < items) {
+      it = fir_item(item + gridDim.x, nchunks, B, T1);
+      fir_f32_fetch(pre, hist_in, src, it, B, T1);  // in flight during the MACs below
+    }
 
-  const int base = threadIdx.x * kFirR;           // local output index of this lane
-  if (base < count) {
-    // w is a ring over s[base + k .. base + k + R-1]; k advances R taps per unrolled round,
-    // so every ring index is a compile-time constant (no register shuffling).
-    float acc[kFirR], w[kFirR];
+    const int base = threadIdx.x * kFirR;           // local output index of this lane
+    if (base < cur.count) {
+      // w is a ring over s[base + k .. base + k + R-1]; k advances R taps per unrolled round,
+      // so every ring index is a compile-time constant (no register shuffling).
+      float acc[kFirR], w[kFirR];
 #pragma unroll
-    for (int r = 0; r < kFirR; ++r) { acc[r] = 0.0f; w[r] = win[padx(base + r)]; }
-    int k = 0;
-    for (; k + kFirR <= T; k += kFirR) {
+      for (int r = 0; r < kFirR; ++r) { acc[r] = 0.0f; w[r] = win[padx(base + r)]; }
+      int k = 0;
+      for (; k + kFirR <= T; k += kFirR) {
 #pragma unroll
-      for (int u = 0; u < kFirR; ++u) {
-        const float c = coeffs[k + u];
+        for (int u = 0; u < kFirR; ++u) {
+          const float c = coeffs[k + u];
 #pragma unroll
-        for (int r = 0; r < kFirR; ++r) acc[r] = acc[r] + w[(r + u) % kFirR] * c;
-        w[u] = win[padx(base + k + u + kFirR)];
+          for (int r = 0; r < kFirR; ++r) acc[r] = acc[r] + w[(r + u) % kFirR] * c;
+          w[u] = win[padx(base + k + u + kFirR)];
+        }
+      }
+      for (; k < T; ++k) {
+        const float c = coeffs[k];
+#pragma unroll
+        for (int r = 0; r < kFirR; ++r) acc[r] = acc[r] + w[r] * c;
+#pragma unroll
+        for (int r = 0; r < kFirR - 1; ++r) w[r] = w[r + 1];
+        w[kFirR - 1] = win[padx(base + kFirR + k)];
+      }
+      float* o = dst + (uint64_t)cur.f * B + cur.n0 + base;
+      if ((B & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + kFirR <= cur.count) {
+        reinterpret_cast<float4*>(o)[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        reinterpret_cast<float4*>(o)[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < kFirR; ++r)
+          if (base + r < cur.count) o[r] = acc[r];
       }
     }
-    for (; k < T; ++k) {
-      const float c = coeffs[k];
-#pragma unroll
-      for (int r = 0; r < kFirR; ++r) acc[r] = acc[r] + w[r] * c;
-#pragma unroll
-      for (int r = 0; r < kFirR - 1; ++r) w[r] = w[r + 1];
-      w[kFirR - 1] = win[padx(base + kFirR + k)];
-    }
-    float* o = dst + (uint64_t)f * B + n0 + base;
-#pragma unroll
-    for (int r = 0; r < kFirR; ++r)
-      if (base + r < count) o[r] = acc[r];
   }
 }
 
-__global__ __launch_bounds__(kBlock) void fir_q15_kernel(const int16_t* __restrict__ coeffs, int T,
-                                                         const int16_t* __restrict__ src, int16_t* __restrict__ dst,
-                                                         uint32_t B, const int16_t* __restrict__ hist_in) {
-  __shared__ int16_t win[(kFirChunk + kFirMaxTaps) * 33 / 32 + 32];
-  const uint32_t f = blockIdx.y;
-  const int n0 = blockIdx.x * kFirChunk;
-  const int count = min((int)B - n0, kFirChunk);
-  const int T1 = T - 1;
-  stage_window(win, hist_in + (uint64_t)f * T1, src + (uint64_t)f * B, T1, n0, count);
-  __syncthreads();
-  const int unrolled_end = (int)(B - (B & 3u));   // outputs before this use the pair-wrap path
-  const int pairs = T >> 1;
-  const int base = threadIdx.x * kFirR;
-  for (int r = 0; r < kFirR; ++r) {
-    const int ln = base + r;
-    if (ln >= count) break;
-    const bool pairwrap = (n0 + ln) < unrolled_end;
-    int64_t acc = 0;
-    for (int m = 0; m < pairs; ++m) {
-      const int32_t x0 = win[padx(ln + 2 * m)], x1 = win[padx(ln + 2 * m + 1)];
-      const int32_t c0 = coeffs[2 * m], c1 = coeffs[2 * m + 1];
-      if (pairwrap) acc += (int32_t)((uint32_t)(x0 * c0) + (uint32_t)(x1 * c1));
-      else          acc += (int64_t)(x0 * c0) + (int64_t)(x1 * c1);
+// ---------------------------------------------------------------- q15
+// A tap pair (c[2m], c[2m+1]) times a sample pair is one v_dot2_i32_i16 whose int32 result
+// wraps exactly like __SMLALD's pair sum (none.h:497-506).  The window is staged as words of
+// two samples, in four LDS planes: even pairs E[i] = (x[2i], x[2i+1]) and odd pairs
+// O[i] = (x[2i+1], x[2i+2]), each split into x>>8 ("h") and x&255 ("l") halves.  A lane's
+// R = 8 outputs need words wb+m .. wb+m+3 of every plane at tap pair m: one ds_read_b128 per
+// plane per 4 pairs (lane stride 16 B: conflict-free) feeds 64 v_dot2.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+constexpr int kQ15W = (kFirChunk + kFirMaxTaps) / 2 + 16;   // words per plane (+ look-ahead)
+constexpr int kQ15Chunk = 120;                               // tap pairs per int32 flush
+
+__device__ __forceinline__ int32_t dot2(uint32_t x, uint32_t c, int32_t acc) {
+  return __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, x), __builtin_bit_cast(s16x2, c), acc, false);
+}
+__device__ __forceinline__ uint32_t hi8(uint32_t w) { return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, w) >> (short)8); }
+__device__ __forceinline__ uint32_t lo8(uint32_t w) { return w & 0x00FF00FFu; }
+__device__ __forceinline__ uint32_t join8(uint32_t h, uint32_t l) { return ((h << 8) & 0xFF00FF00u) | l; }
+__device__ __forceinline__ uint32_t lane_word(const uint4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+
+// Split accumulation, valid when no coefficient pair is (-32768, -32768) -- only then can an
+// int32 pair sum wrap, and without wraps the unrolled and tail outputs (arm_fir_q15.c:482-640
+// vs :649-681) both equal the exact sum:  sum = 256*H + L  with  H = sum(h*c), L = sum(l*c),
+// int32-exact over kQ15Chunk pairs (|H| <= 2^30, 0 <= L < 255*2^15*240 < 2^31), flushed to
+// int64 after each chunk.
+struct Q15Ring { uint4 eh[3], el[3], oh[3], ol[3]; };   // three 4-word quads per plane
+
+template <int S>
+__device__ __forceinline__ void q15_fetch(Q15Ring& r, const uint32_t* lds, int w) {
+  r.eh[S] = *reinterpret_cast<const uint4*>(lds + 0 * kQ15W + w);
+  r.el[S] = *reinterpret_cast<const uint4*>(lds + 1 * kQ15W + w);
+  r.oh[S] = *reinterpret_cast<const uint4*>(lds + 2 * kQ15W + w);
+  r.ol[S] = *reinterpret_cast<const uint4*>(lds + 3 * kQ15W + w);
+}
+
+// 4 tap pairs starting at a multiple of 4 held in slot P (the next quad in slot P+1); the
+// quad after that is fetched into the free slot first, one block ahead of its use.
+template <int P>
+__device__ __forceinline__ void q15_block(Q15Ring& r, const uint32_t* lds, int w_ahead, const uint4 c4,
+                                          int32_t (&H)[kFirR], int32_t (&L)[kFirR]) {
+  q15_fetch<(P + 2) % 3>(r, lds, w_ahead);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const uint32_t c = lane_word(c4, u);
+#pragma unroll
+    for (int j = 0; j < kFirR / 2; ++j) {
+      const int i = u + j, s = i < 4 ? P : (P + 1) % 3, e = i & 3;
+      H[2 * j] = dot2(lane_word(r.eh[s], e), c, H[2 * j]);
+      L[2 * j] = dot2(lane_word(r.el[s], e), c, L[2 * j]);
+      H[2 * j + 1] = dot2(lane_word(r.oh[s], e), c, H[2 * j + 1]);
+      L[2 * j + 1] = dot2(lane_word(r.ol[s], e), c, L[2 * j + 1]);
     }
-    // __SSAT takes an int32_t: (acc >> 15) is narrowed first (arm_fir_q15.c:674)
-    dst[(uint64_t)f * B + n0 + ln] = (int16_t)ssat16((int32_t)(acc >> 15));
+  }
+}
+
+template <bool kFlush>   // pairs > kQ15Chunk: fold H, L into int64 every kQ15Chunk pairs
+__device__ __forceinline__ void fir_q15_split(const uint32_t* lds, const uint32_t* cw, int pairs, int wb,
+                                              int64_t (&acc)[kFirR]) {
+  int32_t H[kFirR], L[kFirR];
+#pragma unroll
+  for (int r = 0; r < kFirR; ++r) { H[r] = 0; L[r] = 0; acc[r] = 0; }
+  const uint4* c4 = reinterpret_cast<const uint4*>(cw);
+  Q15Ring r;
+  q15_fetch<0>(r, lds, wb);
+  q15_fetch<1>(r, lds, wb + 4);
+  int m = 0, blocks = 0;
+  for (; m + 12 <= pairs; m += 12) {
+    q15_block<0>(r, lds, wb + m + 8, c4[m / 4], H, L);
+    q15_block<1>(r, lds, wb + m + 12, c4[m / 4 + 1], H, L);
+    q15_block<2>(r, lds, wb + m + 16, c4[m / 4 + 2], H, L);
+    if (kFlush && ++blocks == kQ15Chunk / 12) {
+      blocks = 0;
+#pragma unroll
+      for (int k = 0; k < kFirR; ++k) { acc[k] += (int64_t)H[k] * 256 + L[k]; H[k] = 0; L[k] = 0; }
+    }
+  }
+  if (m + 4 <= pairs) {
+    q15_block<0>(r, lds, wb + m + 8, c4[m / 4], H, L);
+    m += 4;
+    if (m + 4 <= pairs) {
+      q15_block<1>(r, lds, wb + m + 8, c4[m / 4], H, L);
+      m += 4;
+    }
+  }
+  for (; m < pairs; ++m) {                         // pairs % 4 leftovers, straight from LDS
+    const uint32_t c = cw[m];
+#pragma unroll
+    for (int j = 0; j < kFirR / 2; ++j) {
+      const int w = wb + m + j;
+      H[2 * j] = dot2(lds[w], c, H[2 * j]);
+      L[2 * j] = dot2(lds[kQ15W + w], c, L[2 * j]);
+      H[2 * j + 1] = dot2(lds[2 * kQ15W + w], c, H[2 * j + 1]);
+      L[2 * j + 1] = dot2(lds[3 * kQ15W + w], c, L[2 * j + 1]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kFirR; ++k) acc[k] += (int64_t)H[k] * 256 + L[k];
+}
+
+// General accumulation: int64 sum of int32 pair sums; outputs at or past `tail_from` (the
+// blockSize%4 tail, arm_fir_q15.c:649-681) add the unwrapped pair sum instead.  A pair sum
+// is INT32_MIN only when it wrapped from +2^31 (the most negative true pair sum is
+// -2147418112), so the tail correction is exact.
+__device__ __forceinline__ void fir_q15_wide(const uint32_t* lds, const uint32_t* cw, int pairs, int wb,
+                                             int tail_from, int64_t (&acc)[kFirR]) {
+#pragma unroll
+  for (int r = 0; r < kFirR; ++r) acc[r] = 0;
+  for (int m = 0; m < pairs; ++m) {
+    const uint32_t c = cw[m];
+#pragma unroll
+    for (int r = 0; r < kFirR; ++r) {
+      const int w = wb + m + r / 2, plane = (r & 1) ? 2 : 0;
+      const int32_t p = dot2(join8(lds[plane * kQ15W + w], lds[(plane + 1) * kQ15W + w]), c, 0);
+      acc[r] += (r >= tail_from && p == INT32_MIN) ? (int64_t)2147483648LL : (int64_t)p;
+    }
+  }
+}
+
+#ifndef MI355X_FIR_Q15_WAVES
+#define MI355X_FIR_Q15_WAVES 1   // minimum waves per SIMD the register allocation must allow
+#endif
+__global__ __launch_bounds__(kBlock, MI355X_FIR_Q15_WAVES) void fir_q15_kernel(const int16_t* __restrict__ coeffs, int T,
+                                                         const int16_t* __restrict__ src, int16_t* __restrict__ dst,
+                                                         uint32_t B, const int16_t* __restrict__ hist_in,
+                                                         uint32_t nchunks) {
+  __shared__ uint4 lds4[kQ15W];                    // 4 planes x kQ15W words
+  __shared__ uint4 cw4[kFirMaxTaps / 8];           // tap pairs as words
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cw = reinterpret_cast<uint32_t*>(cw4);
+  const int T1 = T - 1;
+  const int pairs = T >> 1;
+  const FirItem it = fir_item(blockIdx.x, nchunks, B, T1);
+  // staging: every load of this thread is issued before the first LDS write
+  const int words = min((it.total + 1) / 2 + 12, kQ15W);
+  constexpr int kPer = (kQ15W + kBlock - 1) / kBlock;
+  uint32_t x[kPer][3];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int j = threadIdx.x + k * kBlock;
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+      const int i = 2 * j + h;
+      x[k][h] = (uint16_t)fir_sample(hist_in, src, it, B, T1, i);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int j = threadIdx.x + k * kBlock;
+    if (j < words) {
+      const uint32_t e = x[k][0] | (x[k][1] << 16), o = x[k][1] | (x[k][2] << 16);
+      lds[j] = hi8(e);
+      lds[kQ15W + j] = lo8(e);
+      lds[2 * kQ15W + j] = hi8(o);
+      lds[3 * kQ15W + j] = lo8(o);
+    }
+  }
+  int wrap = 0;
+  for (int m = threadIdx.x; m < pairs; m += kBlock) {
+    const uint32_t c = (uint32_t)(uint16_t)coeffs[2 * m] | ((uint32_t)(uint16_t)coeffs[2 * m + 1] << 16);
+    cw[m] = c;
+    wrap |= c == 0x80008000u;
+  }
+  const bool split = !__syncthreads_or(wrap);
+
+  const int base = threadIdx.x * kFirR;
+  if (base >= it.count) return;
+  int64_t acc[kFirR];
+  if (split && pairs <= kQ15Chunk) {
+    fir_q15_split<false>(lds, cw, pairs, base >> 1, acc);
+  } else if (split) {
+    fir_q15_split<true>(lds, cw, pairs, base >> 1, acc);
+  } else {
+    const int unrolled_end = (int)(B - (B & 3u));  // outputs before this use the pair-wrap path
+    fir_q15_wide(lds, cw, pairs, base >> 1, unrolled_end - (it.n0 + base), acc);
+  }
+  int16_t y[kFirR];
+#pragma unroll
+  for (int r = 0; r < kFirR; ++r) y[r] = (int16_t)ssat16((int32_t)(acc[r] >> 15));   // arm_fir_q15.c:674
+  int16_t* o = dst + (uint64_t)it.f * B + it.n0 + base;
+  if ((B & 7u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + kFirR <= it.count) {
+    *reinterpret_cast<uint4*>(o) = *reinterpret_cast<const uint4*>(y);
+  } else {
+#pragma unroll
+    for (int r = 0; r < kFirR; ++r)
+      if (base + r < it.count) o[r] = y[r];
   }
 }
 
@@ -141,13 +348,18 @@ static hipError_t fir_launch(const T* coeffs, int T_, const T* src, T* dst, uint
     if (e != hipSuccess) return e;
     hist_in = tmp;
   }
-  dim3 grid((B + kFirChunk - 1) / kFirChunk, batch);
-  if constexpr (sizeof(T) == 4)
-    hipLaunchKernelGGL(fir_f32_kernel, grid, dim3(kBlock), 0, st, (const float*)coeffs, T_, (const float*)src,
-                       (float*)dst, B, (const float*)hist_in);
-  else
-    hipLaunchKernelGGL(fir_q15_kernel, grid, dim3(kBlock), 0, st, (const int16_t*)coeffs, T_,
-                       (const int16_t*)src, (int16_t*)dst, B, (const int16_t*)hist_in);
+  const uint32_t nchunks = (B + kFirChunk - 1) / kFirChunk;
+  const uint64_t items64 = (uint64_t)nchunks * batch;
+  if (items64 > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  const uint32_t items = (uint32_t)items64;
+  if constexpr (sizeof(T) == 4) {
+    const int grid = persistent_grid((const void*)fir_f32_kernel, kBlock, 0, items, 4);
+    hipLaunchKernelGGL(fir_f32_kernel, dim3(grid), dim3(kBlock), 0, st, (const float*)coeffs, T_, (const float*)src,
+                       (float*)dst, B, (const float*)hist_in, nchunks, items);
+  } else {
+    hipLaunchKernelGGL(fir_q15_kernel, dim3(items), dim3(kBlock), 0, st, (const int16_t*)coeffs, T_,
+                       (const int16_t*)src, (int16_t*)dst, B, (const int16_t*)hist_in, nchunks);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (T1 > 0) {

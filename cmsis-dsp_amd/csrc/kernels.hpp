@@ -5,6 +5,26 @@
 
 namespace mi355x {
 
+// Grid of a persistent kernel: every CU filled to the occupancy the compiled kernel allows
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor x CU count), never more blocks than items.
+// The CU count is per device (cached for the first 16 ordinals).
+inline int persistent_grid(const void* kernel, int block, size_t lds, uint64_t items, int fallback_per_cu = 2) {
+  static int cus_cache[16] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int cus = (dev >= 0 && dev < 16) ? cus_cache[dev] : 0;
+  if (!cus) {
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+    if (dev >= 0 && dev < 16) cus_cache[dev] = cus;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess || per_cu <= 0)
+    per_cu = fallback_per_cu;
+  const uint64_t g = (uint64_t)cus * per_cu;
+  return (int)(g < items ? g : items);
+}
+
 // In-place batched CFFT over `batch` contiguous transforms of n complex samples.
 // tw: device copy of the instance's twiddle table.  perm: optional device permutation
 // (nullptr = the reference tables' canonical digit reversal).  flags: kIfft | kBitrev.

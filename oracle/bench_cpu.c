@@ -5,7 +5,7 @@
  *                           objects (oracle/ref.mk) -> cpu_baseline.kind "reference";
  *   oracle/_build/bench_port -DBENCH_AGAINST_ORACLE: linked to the restatement -> "port".
  * Usage: bench_xxx <workload> <n> <threads> <seconds>
- *   workload: cfft_f32 | cfft_q31 | cfft_q15 (n = fftLen), fir_f32 (n = numTaps, block 4096),
+ *   workload: cfft_f32 | cfft_q31 | cfft_q15 (n = fftLen), fir_f32 | fir_q15 (n = numTaps, block 4096),
  *             mat_mult_f32 (n = square dimension)
  * Each thread owns its own buffers (the library is reentrant) and runs until the time
  * budget is spent; in-place transforms alternate forward / inverse to stay bounded.
@@ -30,6 +30,8 @@ arm_status oracle_arm_cfft_init_q31(arm_cfft_instance_q31 *S, uint16_t n);
 arm_status oracle_arm_cfft_init_q15(arm_cfft_instance_q15 *S, uint16_t n);
 void oracle_arm_fir_init_f32(arm_fir_instance_f32 *S, uint16_t numTaps, const float *pCoeffs, float *pState,
                              uint32_t blockSize);
+arm_status oracle_arm_fir_init_q15(arm_fir_instance_q15 *S, uint16_t numTaps, const int16_t *pCoeffs,
+                                   int16_t *pState, uint32_t blockSize);
 void oracle_arm_mat_init_f32(arm_matrix_instance_f32 *S, uint16_t r, uint16_t c, float *p);
 #endif
 
@@ -81,6 +83,16 @@ static void *worker(void *arg) {
     arm_fir_instance_f32 S;
     F(arm_fir_init_f32)(&S, (uint16_t)taps, c, st, block);
     do { F(arm_fir_f32)(&S, in, out, block); samples += block; } while (now() - t0 < j->seconds);
+    free(c); free(st); free(in); free(out);
+  } else if (!strcmp(j->wl, "fir_q15")) {
+    const int taps = j->n, block = 4096;
+    int16_t *c = malloc(sizeof(int16_t) * taps), *st = malloc(sizeof(int16_t) * (taps + block - 1));
+    int16_t *in = malloc(sizeof(int16_t) * block), *out = malloc(sizeof(int16_t) * block);
+    for (int i = 0; i < taps; ++i) c[i] = (int16_t)(sm(&seed) >> 52);
+    for (int i = 0; i < block; ++i) in[i] = (int16_t)(sm(&seed) >> 48);
+    arm_fir_instance_q15 S;
+    F(arm_fir_init_q15)(&S, (uint16_t)taps, c, st, block);
+    do { F(arm_fir_q15)(&S, in, out, block); samples += block; } while (now() - t0 < j->seconds);
     free(c); free(st); free(in); free(out);
   } else if (!strcmp(j->wl, "mat_mult_f32")) {
     const int d = j->n;

@@ -65,7 +65,8 @@ def _fir_batched(dsp, torch, kind, coeffs, blocks_per_filter):
 
 
 @pytest.mark.parametrize("kind", ["f32", "q15"])
-@pytest.mark.parametrize("taps,block", [(128, 4096), (29, 32), (2, 7), (64, 100), (130, 2049), (1, 64)])
+@pytest.mark.parametrize("taps,block", [(128, 4096), (29, 32), (2, 7), (64, 100), (130, 2049), (1, 64),
+                                        (6, 50), (240, 1000), (242, 777), (256, 4100), (1024, 3000), (518, 2048)])
 def test_fir_batch_bitexact_two_calls(dsp, torch_gpu, ref, kind, taps, block):
     """Each filter runs two consecutive blocks: the state carry must make them equal one
     long call (FIRF32.cpp:116-124 does the same two-call split)."""
@@ -96,6 +97,39 @@ def test_fir_q15_pairwrap_extreme(dsp, torch_gpu, ref):
     blocks = [[np.full(block, -32768, dtype=np.int16)]]
     got, _ = _fir_batched(dsp, torch_gpu, "q15", coeffs, blocks)
     want, _ = ref.fir("q15", coeffs, blocks[0])
+    assert got[0][0].tobytes() == want[0].tobytes()
+
+
+@pytest.mark.parametrize("taps", [8, 240, 256, 1024])
+@pytest.mark.parametrize("pattern", ["neg", "alt"])
+def test_fir_q15_extremes_split_path(dsp, torch_gpu, ref, taps, pattern):
+    """Largest magnitudes the split (256*H + L) accumulation sees without a wrapping tap
+    pair: -32768 samples against (-32768, 32767) / (-32768, -32767) coefficient pairs, across
+    the int32 flush boundary (120 tap pairs) and the blockSize%4 tail."""
+    block = 4099
+    c = np.empty(taps, dtype=np.int16)
+    c[0::2] = -32768
+    c[1::2] = 32767 if pattern == "alt" else -32767
+    x = np.full(block, -32768, dtype=np.int16)
+    if pattern == "alt":
+        x[1::2] = 32767
+    got, _ = _fir_batched(dsp, torch_gpu, "q15", c, [[x]])
+    want, _ = ref.fir("q15", c, [x])
+    assert got[0][0].tobytes() == want[0].tobytes()
+
+
+@pytest.mark.parametrize("taps", [6, 300])
+def test_fir_q15_wrapping_pair_random(dsp, torch_gpu, ref, taps):
+    """One (-32768, -32768) coefficient pair selects the exact int64 path; random data with
+    runs of -32768 makes some pair sums wrap (unrolled outputs) and not wrap (tail)."""
+    rng = np.random.default_rng(taps)
+    block = 1023
+    c = rng.integers(-32768, 32767, taps, endpoint=True).astype(np.int16)
+    c[2:4] = -32768
+    x = rng.integers(-32768, 32767, block, endpoint=True).astype(np.int16)
+    x[rng.random(block) < 0.5] = -32768
+    got, _ = _fir_batched(dsp, torch_gpu, "q15", c, [[x]])
+    want, _ = ref.fir("q15", c, [x])
     assert got[0][0].tobytes() == want[0].tobytes()
 
 
