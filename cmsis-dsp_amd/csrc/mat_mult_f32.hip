@@ -107,11 +107,113 @@ __global__ __launch_bounds__(256) void mat_mult_f32_kernel(const float* __restri
       }
 }
 
+// Full-tile fast path (M, N multiples of 128, K a multiple of 16, 16-byte aligned rows):
+// float4 global loads (2 of A and 2 of B per thread per K tile, no bounds checks), A written
+// transposed into a k-major LDS tile whose row pitch of 130 words puts each 32-lane group of
+// the transposing ds_write_b32 on 32 distinct banks, B written with ds_write_b128.  Half the
+// registers of the general kernel, so four workgroups fit per CU (LDS- and VGPR-wise).
+constexpr int kLdA4 = kBM + 2;
+
+__global__ __launch_bounds__(256) void mat_mult_f32_full_kernel(const float* __restrict__ A,
+                                                                const float* __restrict__ B,
+                                                                float* __restrict__ C, int M, int K, int N) {
+  __shared__ __attribute__((aligned(16))) float As[2][kBK][kLdA4];
+  __shared__ __attribute__((aligned(16))) float Bs[2][kBK][kBN];
+
+  const int tilesN = N / kBN, ntiles = tilesN * (M / kBM);
+  const int orig = blockIdx.x;
+  const int q = ntiles / 8, r = ntiles % 8, xcd = orig % 8;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  const int tm = tile / tilesN, tn = tile % tilesN;
+  const size_t bz = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int row0 = tm * kBM, col0 = tn * kBN;
+
+  // this thread's float4 slots: A rows (tid>>2) and 64 + (tid>>2), k quad (tid&3);
+  // B rows k = tid>>5 and 8 + (tid>>5), column quad (tid&31)
+  const int a_row = tid >> 2, a_kq = (tid & 3) * 4;
+  const int b_k = tid >> 5, b_c = (tid & 31) * 4;
+  const float* pa = A + bz * (size_t)M * K + (size_t)(row0 + a_row) * K + a_kq;
+  const float* pb = B + bz * (size_t)K * N + (size_t)b_k * N + col0 + b_c;
+  const size_t a_step2 = (size_t)64 * K, b_step2 = (size_t)8 * N, b_tile = (size_t)kBK * N;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+  float4 ra0, ra1, rb0, rb1;
+#define MM_LOAD(kt)                                                              \
+  do {                                                                           \
+    const float* a_ = pa + (size_t)(kt) * kBK;                                   \
+    const float* b_ = pb + (size_t)(kt) * b_tile;                                \
+    ra0 = *reinterpret_cast<const float4*>(a_);                                  \
+    ra1 = *reinterpret_cast<const float4*>(a_ + a_step2);                        \
+    rb0 = *reinterpret_cast<const float4*>(b_);                                  \
+    rb1 = *reinterpret_cast<const float4*>(b_ + b_step2);                        \
+  } while (0)
+#define MM_STORE(buf)                                                            \
+  do {                                                                           \
+    As[buf][a_kq + 0][a_row] = ra0.x; As[buf][a_kq + 0][a_row + 64] = ra1.x;      \
+    As[buf][a_kq + 1][a_row] = ra0.y; As[buf][a_kq + 1][a_row + 64] = ra1.y;      \
+    As[buf][a_kq + 2][a_row] = ra0.z; As[buf][a_kq + 2][a_row + 64] = ra1.z;      \
+    As[buf][a_kq + 3][a_row] = ra0.w; As[buf][a_kq + 3][a_row + 64] = ra1.w;      \
+    *reinterpret_cast<float4*>(&Bs[buf][b_k][b_c]) = rb0;                        \
+    *reinterpret_cast<float4*>(&Bs[buf][b_k + 8][b_c]) = rb1;                    \
+  } while (0)
+
+  const int nk = K / kBK;
+  MM_LOAD(0);
+  MM_STORE(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) MM_LOAD(kt + 1);
+#pragma unroll
+    for (int kk = 0; kk < kBK; kk += 2) {
+      const int ka = kk + (lane >> 5);
+      float a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = As[cur][ka][wm * 64 + i * 32 + (lane & 31)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = Bs[cur][ka][wn * 64 + j * 32 + (lane & 31)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) MM_STORE(cur ^ 1);
+    __syncthreads();
+  }
+#undef MM_LOAD
+#undef MM_STORE
+
+  float* c = C + bz * (size_t)M * N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int rr = row0 + wm * 64 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+        const int cc = col0 + wn * 64 + j * 32 + (lane & 31);
+        c[(size_t)rr * N + cc] = acc[i][j][reg];
+      }
+}
+
 hipError_t mat_mult_f32_launch(int m, int k, int n, const float* a, const float* b, float* c, uint32_t batch,
                                hipStream_t st) {
   if (batch == 0 || m == 0 || n == 0) return hipSuccess;
   if (k == 0) return hipMemsetAsync(c, 0, sizeof(float) * (size_t)m * n * batch, st);
   const int tiles = ((m + kBM - 1) / kBM) * ((n + kBN - 1) / kBN);
+  const bool full = m % kBM == 0 && n % kBN == 0 && k % kBK == 0 &&
+                    ((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0;
+  if (full) {
+    hipLaunchKernelGGL(mat_mult_f32_full_kernel, dim3(tiles, 1, batch), dim3(256), 0, st, a, b, c, m, k, n);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(mat_mult_f32_kernel, dim3(tiles, 1, batch), dim3(256), 0, st, a, b, c, m, k, n);
   return hipGetLastError();
 }

@@ -173,7 +173,8 @@ def test_mat_mult_size_mismatch(dsp, torch_gpu):
     assert dsp.lib.arm_mat_mult_f32(C.byref(A), C.byref(B), C.byref(Cm)) == dsp.ARM_MATH_SIZE_MISMATCH
 
 
-@pytest.mark.parametrize("m,k,n,batch", [(256, 256, 256, 3), (300, 130, 200, 2), (1024, 1024, 1024, 1)])
+@pytest.mark.parametrize("m,k,n,batch", [(256, 256, 256, 3), (300, 130, 200, 2), (1024, 1024, 1024, 1),
+                                          (128, 16, 384, 2), (384, 48, 128, 1), (128, 1000, 128, 1)])
 def test_mat_mult_batch_normwise(dsp, torch_gpu, ref, m, k, n, batch):
     torch = torch_gpu
     rng = np.random.default_rng(m + k + n)
