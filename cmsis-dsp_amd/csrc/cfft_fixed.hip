@@ -305,8 +305,15 @@ __global__ __launch_bounds__(kBlock) void cfft_fx_kernel(typename Fx<T>::C* __re
 // immediate (found by exhaustive search over two-term paddings).
 __device__ __forceinline__ int s4096(int e) { return e + 8 * (e >> 7) + (e >> 9); }
 
+#ifndef MI355X_FX_TW_REGS
+#define MI355X_FX_TW_REGS 1
+#endif
+
+#ifndef MI355X_FX_WAVES
+#define MI355X_FX_WAVES 1     // minimum waves per SIMD the register allocation must allow
+#endif
 template <typename T, bool INV>
-__global__ __launch_bounds__(256) void cfft_fx4096_kernel(typename Fx<T>::C* __restrict__ data, uint32_t batch,
+__global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typename Fx<T>::C* __restrict__ data, uint32_t batch,
                                                           const typename Fx<T>::C* __restrict__ tw, uint32_t flags) {
   using F = Fx<T>;
   using C = typename F::C;
@@ -318,19 +325,37 @@ __global__ __launch_bounds__(256) void cfft_fx4096_kernel(typename Fx<T>::C* __r
 
   // Lane-constant twiddles, loaded once for the kernel's life (stored in the table's own
   // word type: q15 keeps two per VGPR).  (w1, w2, w3) = table[ia], table[2ia], table[3ia].
-  C tw1[4][3], tw2[3], tw3[4][3], tw4[3], tw5[4][3];
+  // MI355X_FX_TW_REGS=0: stage-1 and stage-3 twiddles (24 words per lane) are re-read from
+  // the cache-resident table every transform instead of pinned in VGPRs.
+  C tw2[3], tw4[3], tw5[4][3];
+#if MI355X_FX_TW_REGS
+  C tw1[4][3], tw3[4][3];
+#endif
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
-    const int ia1 = t + 256 * a, ia3 = (j2 + 16 * a) * 16, ia5 = a * 256;
+    const int ia5 = a * 256;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      tw1[a][k] = tw[(k + 1) * ia1];
-      tw3[a][k] = tw[(k + 1) * ia3];
+#if MI355X_FX_TW_REGS
+      tw1[a][k] = tw[(k + 1) * (t + 256 * a)];
+      tw3[a][k] = tw[(k + 1) * (j2 + 16 * a) * 16];
+#endif
       tw5[a][k] = tw[(k + 1) * ia5];
     }
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k) { tw2[k] = tw[(k + 1) * 4 * t]; tw4[k] = tw[(k + 1) * 64 * j2]; }
+#if MI355X_FX_TW_REGS
+#define TW1(a, k) tw1[a][k]
+#define TW2(k) tw2[k]
+#define TW3(a, k) tw3[a][k]
+#define TW4(k) tw4[k]
+#else
+#define TW1(a, k) twl[((k) + 1) * (t + 256 * (a))]
+#define TW2(k) tw2[k]
+#define TW3(a, k) twl[((k) + 1) * (j2 + 16 * (a)) * 16]
+#define TW4(k) tw4[k]
+#endif
   auto W = [](C c) { return make_int2(c.x, c.y); };
 
   int2 v[16], nv[16];
@@ -343,14 +368,18 @@ __global__ __launch_bounds__(256) void cfft_fx4096_kernel(typename Fx<T>::C* __r
   }
   for (uint32_t tr = blockIdx.x; tr < batch; tr += gridDim.x) {
     C* X = data + (size_t)tr * 4096;
+#if !MI355X_FX_TW_REGS
+    const C* twl = tw;
+    asm volatile("" : "+s"(twl));      // opaque per transform: keeps the re-reads in the loop
+#endif
     // ---------------- pass 1: stages 1 (first) and 2
 #pragma unroll
     for (int u = 0; u < 16; ++u) v[u] = nv[u];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
-      bfly<T, INV, 0>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], W(tw1[a][0]), W(tw1[a][1]), W(tw1[a][2]));
+      bfly<T, INV, 0>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], W(TW1(a, 0)), W(TW1(a, 1)), W(TW1(a, 2)));
 #pragma unroll
-    for (int b = 0; b < 4; ++b) bfly<T, INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], W(tw2[0]), W(tw2[1]), W(tw2[2]));
+    for (int b = 0; b < 4; ++b) bfly<T, INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], W(TW2(0)), W(TW2(1)), W(TW2(2)));
     __syncthreads();                    // the previous transform's pass-3 reads are done
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -373,10 +402,10 @@ __global__ __launch_bounds__(256) void cfft_fx4096_kernel(typename Fx<T>::C* __r
         for (int b = 0; b < 4; ++b) v[4 * a + b] = F::ld(lds + s4096(base + 64 * a + 16 * b));
 #pragma unroll
       for (int b = 0; b < 4; ++b)
-        bfly<T, INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], W(tw3[b][0]), W(tw3[b][1]), W(tw3[b][2]));
+        bfly<T, INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], W(TW3(b, 0)), W(TW3(b, 1)), W(TW3(b, 2)));
 #pragma unroll
       for (int a = 0; a < 4; ++a)
-        bfly<T, INV, 1>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], W(tw4[0]), W(tw4[1]), W(tw4[2]));
+        bfly<T, INV, 1>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], W(TW4(0)), W(TW4(1)), W(TW4(2)));
       __syncthreads();
 #pragma unroll
       for (int a = 0; a < 4; ++a)
@@ -404,6 +433,11 @@ __global__ __launch_bounds__(256) void cfft_fx4096_kernel(typename Fx<T>::C* __r
     }
   }
 }
+
+#undef TW1
+#undef TW2
+#undef TW3
+#undef TW4
 
 template <typename T>
 static hipError_t launch_fx4096(void* data, uint32_t batch, const void* tw, uint32_t flags, hipStream_t st) {
