@@ -13,7 +13,8 @@ reference scalar C timed on this host's cores (cpu_baseline).
 
 N > 1: launched by torch.distributed.run, one process per GPU; every rank processes its
 own 2^20 transforms (weak scaling, no data-path collective), timed between barriers,
-MAX over ranks.  Other workloads: cfft_q31_4096, cfft_q15_4096, fir_f32, fir_q15, mat_mult_f32.
+MAX over ranks.  Other workloads: cfft_q31_4096, cfft_q15_4096, fir_f32, fir_q15, mat_mult_f32,
+mfcc_f32 (arm_mfcc_f32, fftLen 1024, the reference suite's 20-Mel/13-DCT tables).
 """
 import argparse
 import json
@@ -44,6 +45,7 @@ WORKLOADS = {
     "fir_f32": ("fir_f32", 128, 1 << 16, 8),
     "fir_q15": ("fir_q15", 128, 1 << 16, 4),
     "mat_mult_f32": ("mat", 1024, 256, None),
+    "mfcc_f32": ("mfcc", 1024, 1 << 18, 4),
 }
 
 
@@ -102,7 +104,8 @@ def cpu_baseline(workload, n):
     if not os.path.exists(exe):
         return None
     wl = {"cfft_f32_1024": "cfft_f32", "cfft_q31_4096": "cfft_q31", "cfft_q15_4096": "cfft_q15",
-          "fir_f32": "fir_f32", "fir_q15": "fir_q15", "mat_mult_f32": "mat_mult_f32"}[workload]
+          "fir_f32": "fir_f32", "fir_q15": "fir_q15", "mat_mult_f32": "mat_mult_f32",
+          "mfcc_f32": "mfcc_f32"}[workload]
     nn = 256 if workload == "mat_mult_f32" else n      # 1024^3 takes seconds per matrix on one core
     out = subprocess.run([exe, wl, str(nn), str(threads), str(secs)], capture_output=True, text=True,
                          timeout=120)
@@ -218,6 +221,30 @@ def run_mat(dim, batch, steps, warmup, world, rank):
                            "within_bound": bool(err <= bound)}
 
 
+def run_mfcc(n, batch, steps, warmup, world, rank):
+    import mfcc_cfg
+    g = mfcc_cfg.golden()
+    cfg = mfcc_cfg.suite_cfg(g, n)
+    m = dsp.MfccF32(n, cfg["dct"], cfg["pos"], cfg["len"], cfg["coefs"], cfg["window"])
+    frames = synth("f32", batch * n, rank).view(batch, n)
+    work = torch.empty_like(frames)
+    out = torch.empty((batch, m.nb_dct), dtype=torch.float32, device="cuda")
+
+    def launch(s):
+        m.batch(frames, out, work)
+
+    wall, kern_ms = time_launches(launch, steps, warmup, world)
+    host, hk = cpu_checker()
+    fresh = synth("f32", 64 * n, rank, salt=29).view(64, n)
+    want = host.mfcc(cfg, fresh.cpu().numpy())
+    got = m.batch(fresh.clone()).cpu().numpy()
+    err = np.abs(got.astype(np.float64) - want)
+    return wall, kern_ms, {"checker": hk, "frames_checked": 64, "max_abs_err": float(err.max()),
+                           "within_tolerance": bool(np.all(err <= 2e-5 + 1e-6 * np.abs(want))),
+                           "bit_exact_fraction": float(np.mean(got.view(np.uint32) == want.view(np.uint32))),
+                           "tolerance": "2e-5 + 1e-6*|ref| (device logf vs host libm logf; other stages exact)"}
+
+
 def pmc_traffic(workload):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, when present."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -251,6 +278,10 @@ def main():
         wall, kern_ms, parity = run_fir(kind[4:], n, batch, args.steps, args.warmup, world, rank)
         units = batch * 4096
         algo_bytes = units * bps + batch * (n - 1) * bps  # in + out + history read/write
+    elif args.workload == "mfcc_f32":
+        wall, kern_ms, parity = run_mfcc(n, batch, args.steps, args.warmup, world, rank)
+        units = batch * n                                  # input samples
+        algo_bytes = units * bps + batch * 13 * 4          # frames in + coefficients out
     else:
         wall, kern_ms, parity = run_mat(n, batch, args.steps, args.warmup, world, rank)
         units = batch                                      # matrices
@@ -275,11 +306,15 @@ def main():
     else:
         line.update(value=round(total_units / wall * 1e-9, 3), unit="Gsamples/s",
                     dtype={"f32": "f32", "q31": "q31 (int32)", "q15": "q15 (int16)", "fir_f32": "f32",
-                           "fir_q15": "q15 (int16 x int16 -> int64)"}[kind])
+                           "fir_q15": "q15 (int16 x int16 -> int64)", "mfcc": "f32"}[kind])
         if args.workload.startswith("cfft"):
             line["config"] = {"workload": f"arm_cfft_{kind} N={n} batch={batch}/GPU in place, bitReverseFlag=1, "
                                           f"alternating fwd/inv (BASELINE configs[{1 if kind == 'f32' else 3}])",
                               "fftLen": n, "batch_per_gpu": batch, "parallelism": f"dp{world} shards"}
+        elif kind == "mfcc":
+            line["config"] = {"workload": f"arm_mfcc_f32 fftLen={n} 20 Mel / 13 DCT (reference MFCC F32 suite "
+                                          f"tables) batch={batch} frames/GPU", "fftLen": n, "batch_per_gpu": batch,
+                              "parallelism": f"dp{world} shards"}
         else:
             line["config"] = {"workload": f"arm_{kind} numTaps={n} blockSize=4096 batch={batch}/GPU "
                                           + ("(BASELINE configs[2])" if kind == "fir_f32" else "(configs[2] shape, q15)"),

@@ -20,7 +20,7 @@ import numpy as np
 from . import _abi
 from ._abi import (arm_cfft_instance_f32, arm_cfft_instance_q15, arm_cfft_instance_q31,  # noqa: F401
                    arm_fir_instance_f32, arm_fir_instance_q15, arm_matrix_instance_f32,
-                   arm_rfft_fast_instance_f32, ARM_MATH_SUCCESS, ARM_MATH_ARGUMENT_ERROR,
+                   arm_rfft_fast_instance_f32, arm_mfcc_instance_f32, ARM_MATH_SUCCESS, ARM_MATH_ARGUMENT_ERROR,
                    ARM_MATH_SIZE_MISMATCH)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -42,6 +42,7 @@ def _load():
                           f"(build it with `make -C cmsis-dsp_amd` or __graft_entry__.build())")
     lib = C.CDLL(LIB_PATH)
     _abi.bind(lib, _abi.DROPIN)
+    _abi.bind(lib, _abi.MFCC_LEN)
     _abi.bind(lib, _abi.BATCHED)
     return lib
 
@@ -167,6 +168,51 @@ def arm_mat_mult_f32(a, b):
     st = lib.arm_mat_mult_f32(C.byref(A), C.byref(B), C.byref(Cm))
     _check_void("arm_mat_mult_f32")
     return st, c
+
+
+class MfccF32:
+    """arm_mfcc_init_f32 + arm_mfcc_f32 with the instance's tables kept alive.
+    dct: [nbDctOutputs, nbMelFilters]; pos/lengths: per Mel filter; coefs: concatenated
+    filter weights; window: fftLen.  Tables may be numpy arrays (host) or torch device
+    tensors (their data_ptr is used)."""
+
+    def __init__(self, fft_len, dct, pos, lengths, coefs, window):
+        def keep(a, dt):
+            if hasattr(a, "data_ptr"):
+                return a, a.data_ptr()
+            a = np.ascontiguousarray(a, dtype=dt)
+            return a, a.ctypes.data
+        self._t = [keep(dct, np.float32), keep(pos, np.uint32), keep(lengths, np.uint32), keep(coefs, np.float32),
+                   keep(window, np.float32)]
+        self.nb_mel = int(len(lengths))
+        self.nb_dct = int(dct.shape[0])
+        self.fft_len = int(fft_len)
+        self.S = arm_mfcc_instance_f32()
+        st = lib.arm_mfcc_init_f32(C.byref(self.S), self.fft_len, self.nb_mel, self.nb_dct,
+                                   *[p for _, p in self._t])
+        if st != ARM_MATH_SUCCESS:
+            raise ValueError(f"arm_mfcc_init_f32({fft_len}) -> {st}")
+
+    def __call__(self, x):
+        """One frame (numpy) -> nbDctOutputs coefficients (the reference's call shape)."""
+        src = np.ascontiguousarray(x, dtype=np.float32).copy()
+        dst = np.zeros(self.nb_dct, dtype=np.float32)
+        tmp = np.zeros(2 * self.fft_len, dtype=np.float32)
+        lib.arm_mfcc_f32(C.byref(self.S), src.ctypes.data, dst.ctypes.data, tmp.ctypes.data)
+        _check_void("arm_mfcc_f32")
+        return dst
+
+    def batch(self, frames, out=None, work=None, stream=None):
+        """frames: torch device tensor [batch, fftLen] (overwritten) -> [batch, nbDct]."""
+        import torch
+        b = frames.shape[0]
+        out = torch.empty((b, self.nb_dct), dtype=torch.float32, device=frames.device) if out is None else out
+        work = torch.empty_like(frames) if work is None else work
+        st = lib.arm_mfcc_f32_batch(C.byref(self.S), C.c_void_p(frames.data_ptr()), C.c_void_p(out.data_ptr()),
+                                    C.c_void_p(work.data_ptr()), b, _stream_ptr(stream))
+        if st != ARM_MATH_SUCCESS:
+            raise RuntimeError(f"arm_mfcc_f32_batch -> {st}: {last_error()[1]}")
+        return out
 
 
 # ------------------------------------------------------------------ batched (torch, device)

@@ -48,6 +48,14 @@ class arm_matrix_instance_f32(C.Structure):
     _fields_ = [("numRows", C.c_uint16), ("numCols", C.c_uint16), ("pData", c_f32p)]
 
 
+class arm_mfcc_instance_f32(C.Structure):
+    # Include/dsp/transform_functions.h:856-873 (RFFT-based default build)
+    _fields_ = [("dctCoefs", c_f32p), ("filterCoefs", c_f32p), ("windowCoefs", c_f32p),
+                ("filterPos", C.POINTER(C.c_uint32)), ("filterLengths", C.POINTER(C.c_uint32)),
+                ("fftLen", C.c_uint32), ("nbMelFilters", C.c_uint32), ("nbDctOutputs", C.c_uint32),
+                ("rfft", arm_rfft_fast_instance_f32)]
+
+
 P = C.POINTER
 SIZES = (16, 32, 64, 128, 256, 512, 1024, 2048, 4096)
 RFFT_SIZES = (32, 64, 128, 256, 512, 1024, 2048, 4096)
@@ -67,6 +75,9 @@ DROPIN = {
     "arm_fir_init_q15": (C.c_int, [P(arm_fir_instance_q15), C.c_uint16, C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_fir_q15": (None, [P(arm_fir_instance_q15), C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_mat_init_f32": (None, [P(arm_matrix_instance_f32), C.c_uint16, C.c_uint16, C.c_void_p]),
+    "arm_mfcc_init_f32": (C.c_int, [P(arm_mfcc_instance_f32), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "arm_mfcc_f32": (None, [P(arm_mfcc_instance_f32), C.c_void_p, C.c_void_p, C.c_void_p]),
     "arm_mat_mult_f32": (C.c_int, [P(arm_matrix_instance_f32), P(arm_matrix_instance_f32),
                                    P(arm_matrix_instance_f32)]),
 }
@@ -76,6 +87,12 @@ for _t in ("f32", "q31", "q15"):
         DROPIN[f"arm_cfft_init_{_n}_{_t}"] = (C.c_int, [P(_inst)])
 for _n in RFFT_SIZES:
     DROPIN[f"arm_rfft_fast_init_{_n}_f32"] = (C.c_int, [P(arm_rfft_fast_instance_f32)])
+
+# per-length MFCC init functions (the product and the reference build; the oracle has the
+# generic init only)
+MFCC_LEN = {f"arm_mfcc_init_{n}_f32": (C.c_int, [P(arm_mfcc_instance_f32), C.c_uint32, C.c_uint32, C.c_void_p,
+                                                 C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
+            for n in RFFT_SIZES}
 
 # the additive batched device API of include/arm_math_mi355x.h
 BATCHED = {
@@ -93,6 +110,8 @@ BATCHED = {
                                     C.c_void_p, C.c_void_p]),
     "arm_mat_mult_f32_batch": (C.c_int, [P(arm_matrix_instance_f32), P(arm_matrix_instance_f32),
                                          P(arm_matrix_instance_f32), C.c_uint32, C.c_void_p]),
+    "arm_mfcc_f32_batch": (C.c_int, [P(arm_mfcc_instance_f32), C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                     C.c_void_p]),
     "arm_mi355x_last_error": (C.c_int, []),
     "arm_mi355x_last_error_string": (C.c_char_p, []),
     "arm_mi355x_clear_error": (None, []),

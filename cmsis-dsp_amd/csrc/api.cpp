@@ -4,6 +4,8 @@
 // nothing aborts.  There is no CPU fallback: all compute runs in the HIP kernels.
 #include <string.h>
 
+#include <vector>
+
 #include "../../include/arm_math.h"
 #include "../../include/arm_math_mi355x.h"
 #include "common.hpp"
@@ -111,6 +113,82 @@ bool rfft_run(const arm_rfft_fast_instance_f32* S, float* d_p, float* d_out, uin
     MI_CHECK(cfft_f32_launch((int)h, d_p, batch, (const float*)pr.tw, pr.perm, pr.flags, st), "rfft cfft");
     MI_CHECK(rfft_f32_stage_launch((int)n, d_p, d_out, batch, (const float*)twr, st), "rfft stage");
   }
+  return true;
+}
+
+// ---- MFCC (arm_mfcc_f32.c:83-160): the instance's user tables packed into one
+// content-cached device blob: [dct | filter coefs | window | pos | len | coef offsets]
+struct MfccDev {
+  const float* dct = nullptr;
+  const float* coefs = nullptr;
+  const float* win = nullptr;
+  const uint32_t* pos = nullptr;
+  const uint32_t* len = nullptr;
+  const uint32_t* off = nullptr;
+};
+
+template <typename T>
+bool host_copy(const T* p, size_t count, std::vector<T>& out) {
+  out.resize(count);
+  if (!count) return true;
+  if (!p) return false;
+  if (is_device_ptr(p)) return hipMemcpy(out.data(), p, sizeof(T) * count, hipMemcpyDeviceToHost) == hipSuccess;
+  memcpy(out.data(), p, sizeof(T) * count);
+  return true;
+}
+
+bool mfcc_prepare(const arm_mfcc_instance_f32* S, MfccDev& d) {
+  const uint32_t n = S->fftLen, nm = S->nbMelFilters, nd = S->nbDctOutputs;
+  if (!rfft_len_ok(n) || S->rfft.fftLenRFFT != n) { set_error(hipErrorInvalidValue, "mfcc instance"); return false; }
+  if (mfcc_f32_post_lds((int)n, (int)nm) > 65536) { set_error(hipErrorInvalidValue, "mfcc: too many Mel filters"); return false; }
+  std::vector<uint32_t> pos, len;
+  if (!host_copy(S->filterPos, nm, pos) || !host_copy(S->filterLengths, nm, len)) {
+    set_error(hipErrorInvalidValue, "mfcc filter tables");
+    return false;
+  }
+  std::vector<uint32_t> off(nm);
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < nm; ++i) {
+    if ((uint64_t)pos[i] + len[i] > n) { set_error(hipErrorInvalidValue, "mfcc filter beyond fftLen"); return false; }
+    off[i] = (uint32_t)total;
+    total += len[i];
+  }
+  auto up16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  const size_t b_dct = up16(sizeof(float) * nm * nd), b_cf = up16(sizeof(float) * total), b_win = up16(sizeof(float) * n);
+  const size_t b_u = up16(sizeof(uint32_t) * nm);
+  std::vector<uint8_t> blob(b_dct + b_cf + b_win + 3 * b_u + 16, 0);
+  std::vector<float> tmp;
+  if (!host_copy(S->dctCoefs, (size_t)nm * nd, tmp)) { set_error(hipErrorInvalidValue, "mfcc dct"); return false; }
+  memcpy(blob.data(), tmp.data(), sizeof(float) * tmp.size());
+  if (!host_copy(S->filterCoefs, (size_t)total, tmp)) { set_error(hipErrorInvalidValue, "mfcc coefs"); return false; }
+  memcpy(blob.data() + b_dct, tmp.data(), sizeof(float) * tmp.size());
+  if (!host_copy(S->windowCoefs, (size_t)n, tmp)) { set_error(hipErrorInvalidValue, "mfcc window"); return false; }
+  memcpy(blob.data() + b_dct + b_cf, tmp.data(), sizeof(float) * tmp.size());
+  uint8_t* u = blob.data() + b_dct + b_cf + b_win;
+  memcpy(u, pos.data(), sizeof(uint32_t) * nm);
+  memcpy(u + b_u, len.data(), sizeof(uint32_t) * nm);
+  memcpy(u + 2 * b_u, off.data(), sizeof(uint32_t) * nm);
+  const uint8_t* dev = (const uint8_t*)device_blob(blob.data(), blob.size());
+  if (!dev) return false;
+  d.dct = (const float*)dev;
+  d.coefs = (const float*)(dev + b_dct);
+  d.win = (const float*)(dev + b_dct + b_cf);
+  d.pos = (const uint32_t*)(dev + b_dct + b_cf + b_win);
+  d.len = (const uint32_t*)(dev + b_dct + b_cf + b_win + b_u);
+  d.off = (const uint32_t*)(dev + b_dct + b_cf + b_win + 2 * b_u);
+  return true;
+}
+
+// x: [batch][n] frames (overwritten), y: [batch][n] work, dst: [batch][nbDct]; the frame
+// maxima ride in dst[frame][0] between the two passes (read before the row is written).
+bool mfcc_run(const arm_mfcc_instance_f32* S, const MfccDev& d, float* x, float* y, float* dst, uint32_t batch,
+              hipStream_t st) {
+  const int n = (int)S->fftLen, nd = (int)S->nbDctOutputs;
+  MI_CHECK(mfcc_f32_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc pre");
+  if (!rfft_run(&S->rfft, x, y, batch, 0, st)) return false;
+  MI_CHECK(mfcc_f32_post_launch(n, y, dst, nd, (int)S->nbMelFilters, d.pos, d.len, d.off, d.coefs, nd, d.dct, dst,
+                                batch, st),
+           "mfcc post");
   return true;
 }
 
@@ -305,6 +383,37 @@ arm_status arm_mat_mult_f32_batch(const arm_matrix_instance_f32* pSrcA, const ar
                                      pDst->pData, batch, (hipStream_t)stream);
   if (e != hipSuccess) { set_error(e, "arm_mat_mult_f32_batch"); return ARM_MATH_ARGUMENT_ERROR; }
   return ARM_MATH_SUCCESS;
+}
+
+// ---- MFCC f32 (drop-in + batched) ------------------------------------------------
+void arm_mfcc_f32(const arm_mfcc_instance_f32* S, float32_t* pSrc, float32_t* pDst, float32_t* pTmp) {
+  (void)pTmp;   // work space lives on the device; the reference's pTmp contents are not reproduced
+  if (!S || !pSrc || !pDst || S->nbDctOutputs == 0) return;
+  MfccDev d;
+  if (!mfcc_prepare(S, d)) return;
+  const uint32_t n = S->fftLen, nd = S->nbDctOutputs;
+  hipStream_t st = sync_stream();
+  float* x = (float*)scratch(sizeof(float) * n, 0);
+  float* y = (float*)scratch(sizeof(float) * n, 1);
+  const bool ddst = is_device_ptr(pDst);
+  float* o = ddst ? pDst : (float*)scratch(sizeof(float) * nd, 2);
+  if (!x || !y || !o) { set_error(hipErrorOutOfMemory, "arm_mfcc scratch"); return; }
+  hipError_t e = hipMemcpyAsync(x, pSrc, sizeof(float) * n,
+                                is_device_ptr(pSrc) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) { set_error(e, "arm_mfcc_f32"); return; }
+  if (!mfcc_run(S, d, x, y, o, 1, st)) return;
+  if (!ddst) e = hipMemcpyAsync(pDst, o, sizeof(float) * nd, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) set_error(e, "arm_mfcc_f32");
+}
+
+arm_status arm_mfcc_f32_batch(const arm_mfcc_instance_f32* S, float32_t* d_src, float32_t* d_dst, float32_t* d_tmp,
+                              uint32_t batch, void* stream) {
+  if (!S || (batch && (!d_src || !d_dst || !d_tmp))) return ARM_MATH_ARGUMENT_ERROR;
+  if (batch == 0 || S->nbDctOutputs == 0) return ARM_MATH_SUCCESS;
+  MfccDev d;
+  if (!mfcc_prepare(S, d)) return ARM_MATH_ARGUMENT_ERROR;
+  return mfcc_run(S, d, d_src, d_tmp, d_dst, batch, (hipStream_t)stream) ? ARM_MATH_SUCCESS : ARM_MATH_ARGUMENT_ERROR;
 }
 
 }  // extern "C"

@@ -109,6 +109,45 @@ arm_status arm_rfft_fast_init_f32(arm_rfft_fast_instance_f32* S, uint16_t fftLen
   }
 }
 
+// ---- MFCC init (arm_mfcc_init_f32.c): record the tables, initialise the inner RFFT
+static void mfcc_fields(arm_mfcc_instance_f32* S, uint32_t fftLen, uint32_t nbMelFilters, uint32_t nbDctOutputs,
+                        const float32_t* dctCoefs, const uint32_t* filterPos, const uint32_t* filterLengths,
+                        const float32_t* filterCoefs, const float32_t* windowCoefs) {
+  S->fftLen = fftLen;
+  S->nbMelFilters = nbMelFilters;
+  S->nbDctOutputs = nbDctOutputs;
+  S->dctCoefs = dctCoefs;
+  S->filterPos = filterPos;
+  S->filterLengths = filterLengths;
+  S->filterCoefs = filterCoefs;
+  S->windowCoefs = windowCoefs;
+}
+
+arm_status arm_mfcc_init_f32(arm_mfcc_instance_f32* S, uint32_t fftLen, uint32_t nbMelFilters, uint32_t nbDctOutputs,
+                             const float32_t* dctCoefs, const uint32_t* filterPos, const uint32_t* filterLengths,
+                             const float32_t* filterCoefs, const float32_t* windowCoefs) {
+  mfcc_fields(S, fftLen, nbMelFilters, nbDctOutputs, dctCoefs, filterPos, filterLengths, filterCoefs, windowCoefs);
+  return fftLen > 0xFFFFu ? ARM_MATH_ARGUMENT_ERROR : arm_rfft_fast_init_f32(&S->rfft, (uint16_t)fftLen);
+}
+
+#define MI_MFCC_INIT(N)                                                                                        \
+  arm_status arm_mfcc_init_##N##_f32(arm_mfcc_instance_f32* S, uint32_t nbMelFilters, uint32_t nbDctOutputs,   \
+                                     const float32_t* dctCoefs, const uint32_t* filterPos,                     \
+                                     const uint32_t* filterLengths, const float32_t* filterCoefs,              \
+                                     const float32_t* windowCoefs) {                                           \
+    mfcc_fields(S, N, nbMelFilters, nbDctOutputs, dctCoefs, filterPos, filterLengths, filterCoefs, windowCoefs); \
+    return arm_rfft_fast_init_##N##_f32(&S->rfft);                                                             \
+  }
+MI_MFCC_INIT(32)
+MI_MFCC_INIT(64)
+MI_MFCC_INIT(128)
+MI_MFCC_INIT(256)
+MI_MFCC_INIT(512)
+MI_MFCC_INIT(1024)
+MI_MFCC_INIT(2048)
+MI_MFCC_INIT(4096)
+#undef MI_MFCC_INIT
+
 // (FIR init zeroes a state buffer that may be device memory: it lives in api.cpp.)
 
 // ---- matrix init (arm_mat_init_f32.c)

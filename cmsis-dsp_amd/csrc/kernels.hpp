@@ -48,6 +48,17 @@ hipError_t fir_f32_launch(const float* coeffs, int num_taps, const float* src, f
 hipError_t fir_q15_launch(const int16_t* coeffs, int num_taps, const int16_t* src, int16_t* dst,
                           uint32_t block_size, uint32_t batch, int16_t* hist, hipStream_t st);
 
+// MFCC f32 around the batched RFFT (mfcc_f32.hip): frame normalisation + window, then the
+// spectrum -> Mel -> log -> DCT tail.  post needs mfcc_f32_post_lds(n, nb_mel) bytes of LDS.
+// The frame maximum of frame f is written to / read from maxv[f * maxv_stride].
+hipError_t mfcc_f32_pre_launch(int n, const float* src, const float* win, float* x, float* maxv, uint32_t batch,
+                               int maxv_stride, hipStream_t st);
+size_t mfcc_f32_post_lds(int n, int nb_mel);
+hipError_t mfcc_f32_post_launch(int n, const float* y, const float* maxv, int maxv_stride, int nb_mel,
+                                const uint32_t* pos,
+                                const uint32_t* len, const uint32_t* off, const float* coefs, int nb_dct,
+                                const float* dct, float* dst, uint32_t batch, hipStream_t st);
+
 // Row-major C[b] = A[b] (m x k) * B[b] (k x n), contiguous batch.
 hipError_t mat_mult_f32_launch(int m, int k, int n, const float* a, const float* b, float* c,
                                uint32_t batch, hipStream_t st);

@@ -1,6 +1,8 @@
 // Host runtime: device table cache, staging scratch, error channel.
 #include "runtime.hpp"
 
+#include <string.h>
+
 #include <map>
 #include <mutex>
 #include <string>
@@ -18,6 +20,15 @@ thread_local std::string g_err_msg;
 std::mutex g_table_mu;
 std::map<std::tuple<int, const void*, size_t>, void*> g_tables;
 std::map<std::tuple<int, const void*, uint16_t, int, int>, std::pair<void*, bool>> g_perms;
+
+struct Blob { std::vector<uint8_t> host; void* dev = nullptr; };
+std::map<std::tuple<int, uint64_t, size_t>, std::vector<Blob>> g_blobs;
+
+uint64_t fnv1a(const uint8_t* p, size_t n) {
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < n; ++i) { h ^= p[i]; h *= 1099511628211ull; }
+  return h;
+}
 
 struct Scratch { void* p = nullptr; size_t n = 0; };
 thread_local std::map<std::pair<int, int>, Scratch> g_scratch;
@@ -75,6 +86,29 @@ const void* device_table(const void* host, size_t bytes) {
   }
   g_tables[key] = d;
   return d;
+}
+
+const void* device_blob(const void* host, size_t bytes) {
+  if (!host || !bytes) { set_error(hipErrorInvalidValue, "device_blob: empty"); return nullptr; }
+  const uint8_t* h = (const uint8_t*)host;
+  const int dev = cur_dev();
+  const auto key = std::make_tuple(dev, fnv1a(h, bytes), bytes);
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  std::vector<Blob>& bucket = g_blobs[key];
+  for (const Blob& b : bucket)
+    if (memcmp(b.host.data(), h, bytes) == 0) return b.dev;
+  Blob b;
+  b.host.assign(h, h + bytes);
+  hipError_t e = hipMalloc(&b.dev, bytes);
+  if (e != hipSuccess) { set_error(e, "device_blob: hipMalloc"); return nullptr; }
+  e = hipMemcpy(b.dev, h, bytes, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    set_error(e, "device_blob: hipMemcpy");
+    (void)hipFree(b.dev);
+    return nullptr;
+  }
+  bucket.push_back(std::move(b));
+  return bucket.back().dev;
 }
 
 const uint16_t* device_perm(int n, const uint16_t* table, uint16_t len, int kind, bool* canonical, bool* ok) {

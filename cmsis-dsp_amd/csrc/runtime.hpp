@@ -20,6 +20,11 @@ bool is_device_ptr(const void* p);
 // (device, host pointer, size).  Returns nullptr on failure.
 const void* device_table(const void* host, size_t bytes);
 
+// Device copy of a host byte blob, cached by CONTENT (hash + full compare): uploaded once
+// per distinct contents and device, immune to a caller reusing a buffer for new values.
+// Used for user-supplied coefficient tables (MFCC).  Returns nullptr on failure.
+const void* device_blob(const void* host, size_t bytes);
+
 // Device permutation implementing a bit-reversal swap table of a non-canonical instance.
 // *canonical is set when the table induces the reference's own permutation (then the
 // kernels compute it on the fly and nullptr is returned).  kind: 0 = f32 tables

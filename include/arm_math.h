@@ -75,6 +75,19 @@ typedef struct {
   const float32_t            *pTwiddleRFFT;
 } arm_rfft_fast_instance_f32;
 
+/* ---- MFCC instance (RFFT-based default build): Include/dsp/transform_functions.h:856-873 */
+typedef struct {
+  const float32_t *dctCoefs;        /* nbDctOutputs x nbMelFilters, row-major */
+  const float32_t *filterCoefs;     /* concatenated Mel filters (sum of filterLengths) */
+  const float32_t *windowCoefs;     /* fftLen */
+  const uint32_t  *filterPos;       /* first FFT bin of each Mel filter */
+  const uint32_t  *filterLengths;   /* bins per Mel filter */
+        uint32_t   fftLen;
+        uint32_t   nbMelFilters;
+        uint32_t   nbDctOutputs;
+  arm_rfft_fast_instance_f32 rfft;
+} arm_mfcc_instance_f32;
+
 /* ---- FIR instances: Include/dsp/filtering_functions.h:66-71, 86-91 --------------- */
 typedef struct {
         uint16_t   numTaps;
@@ -166,6 +179,52 @@ arm_status arm_rfft_fast_init_4096_f32(arm_rfft_fast_instance_f32 *S);
 arm_status arm_rfft_fast_init_f32(arm_rfft_fast_instance_f32 *S, uint16_t fftLen);
 void arm_rfft_fast_f32(const arm_rfft_fast_instance_f32 *S, float32_t *p,
                        float32_t *pOut, uint8_t ifftFlag);
+
+/* ===================================================================================
+ * MFCC, f32.  Prototypes: Include/dsp/transform_functions.h:875-990
+ * Reference bodies: Source/TransformFunctions/arm_mfcc_init_f32.c (init by length and
+ * generic), Source/TransformFunctions/arm_mfcc_f32.c:83-160 (RFFT-based path).
+ * pTmp: 2*fftLen floats as in the reference.  After the call the contents of pSrc and
+ * pTmp are unspecified (the reference documents pSrc as modified); Mel filters must lie
+ * within bins [0, fftLen/2) -- the reference reads uninitialised pTmp words beyond them.
+ * =================================================================================== */
+arm_status arm_mfcc_init_32_f32(arm_mfcc_instance_f32 *S, uint32_t nbMelFilters, uint32_t nbDctOutputs,
+                                const float32_t *dctCoefs, const uint32_t *filterPos,
+                                const uint32_t *filterLengths, const float32_t *filterCoefs,
+                                const float32_t *windowCoefs);
+arm_status arm_mfcc_init_64_f32(arm_mfcc_instance_f32 *S, uint32_t nbMelFilters, uint32_t nbDctOutputs,
+                                const float32_t *dctCoefs, const uint32_t *filterPos,
+                                const uint32_t *filterLengths, const float32_t *filterCoefs,
+                                const float32_t *windowCoefs);
+arm_status arm_mfcc_init_128_f32(arm_mfcc_instance_f32 *S, uint32_t nbMelFilters, uint32_t nbDctOutputs,
+                                 const float32_t *dctCoefs, const uint32_t *filterPos,
+                                 const uint32_t *filterLengths, const float32_t *filterCoefs,
+                                 const float32_t *windowCoefs);
+arm_status arm_mfcc_init_256_f32(arm_mfcc_instance_f32 *S, uint32_t nbMelFilters, uint32_t nbDctOutputs,
+                                 const float32_t *dctCoefs, const uint32_t *filterPos,
+                                 const uint32_t *filterLengths, const float32_t *filterCoefs,
+                                 const float32_t *windowCoefs);
+arm_status arm_mfcc_init_512_f32(arm_mfcc_instance_f32 *S, uint32_t nbMelFilters, uint32_t nbDctOutputs,
+                                 const float32_t *dctCoefs, const uint32_t *filterPos,
+                                 const uint32_t *filterLengths, const float32_t *filterCoefs,
+                                 const float32_t *windowCoefs);
+arm_status arm_mfcc_init_1024_f32(arm_mfcc_instance_f32 *S, uint32_t nbMelFilters, uint32_t nbDctOutputs,
+                                  const float32_t *dctCoefs, const uint32_t *filterPos,
+                                  const uint32_t *filterLengths, const float32_t *filterCoefs,
+                                  const float32_t *windowCoefs);
+arm_status arm_mfcc_init_2048_f32(arm_mfcc_instance_f32 *S, uint32_t nbMelFilters, uint32_t nbDctOutputs,
+                                  const float32_t *dctCoefs, const uint32_t *filterPos,
+                                  const uint32_t *filterLengths, const float32_t *filterCoefs,
+                                  const float32_t *windowCoefs);
+arm_status arm_mfcc_init_4096_f32(arm_mfcc_instance_f32 *S, uint32_t nbMelFilters, uint32_t nbDctOutputs,
+                                  const float32_t *dctCoefs, const uint32_t *filterPos,
+                                  const uint32_t *filterLengths, const float32_t *filterCoefs,
+                                  const float32_t *windowCoefs);
+arm_status arm_mfcc_init_f32(arm_mfcc_instance_f32 *S, uint32_t fftLen, uint32_t nbMelFilters,
+                             uint32_t nbDctOutputs, const float32_t *dctCoefs, const uint32_t *filterPos,
+                             const uint32_t *filterLengths, const float32_t *filterCoefs,
+                             const float32_t *windowCoefs);
+void arm_mfcc_f32(const arm_mfcc_instance_f32 *S, float32_t *pSrc, float32_t *pDst, float32_t *pTmp);
 
 /* ===================================================================================
  * FIR.  Prototypes: Include/dsp/filtering_functions.h:141-145,175-180,233-237,260-265

@@ -42,6 +42,14 @@ arm_status arm_cfft_q15_batch(const arm_cfft_instance_q15 *S, q15_t *d_p1, uint3
 arm_status arm_rfft_fast_f32_batch(const arm_rfft_fast_instance_f32 *S, float32_t *d_p,
                                    float32_t *d_out, uint32_t batch, uint8_t ifftFlag, void *stream);
 
+/* MFCC over `batch` contiguous frames of S->fftLen samples (arm_mfcc_f32.c:83-160 per
+ * frame).  d_src: [batch][fftLen] input frames (used as work space: overwritten);
+ * d_tmp: [batch][fftLen] work space; d_dst: [batch][nbDctOutputs].  The instance's
+ * coefficient tables may be host or device pointers (host tables are uploaded on each
+ * call through the calling thread's staging buffers, in stream order). */
+arm_status arm_mfcc_f32_batch(const arm_mfcc_instance_f32 *S, float32_t *d_src, float32_t *d_dst,
+                              float32_t *d_tmp, uint32_t batch, void *stream);
+
 /* FIR over `batch` independent filters sharing S->numTaps / S->pCoeffs (host or device
  * pointer; S->pState is not used).  d_src/d_dst: [batch][blockSize].  d_hist:
  * [batch][numTaps-1] streaming state, read as the history before the block and

@@ -6,7 +6,8 @@
  *   oracle/_build/bench_port -DBENCH_AGAINST_ORACLE: linked to the restatement -> "port".
  * Usage: bench_xxx <workload> <n> <threads> <seconds>
  *   workload: cfft_f32 | cfft_q31 | cfft_q15 (n = fftLen), fir_f32 | fir_q15 (n = numTaps, block 4096),
- *             mat_mult_f32 (n = square dimension)
+ *             mat_mult_f32 (n = square dimension), mfcc_f32 (n = fftLen; 20 triangular Mel
+ *             filters, 13 DCT outputs, Hamming window -- the suite's shape)
  * Each thread owns its own buffers (the library is reentrant) and runs until the time
  * budget is spent; in-place transforms alternate forward / inverse to stay bounded.
  * Prints one JSON object: samples processed, seconds, threads, rate.
@@ -16,6 +17,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <math.h>
 #include <time.h>
 
 #ifdef BENCH_AGAINST_REFERENCE
@@ -94,6 +96,30 @@ static void *worker(void *arg) {
     F(arm_fir_init_q15)(&S, (uint16_t)taps, c, st, block);
     do { F(arm_fir_q15)(&S, in, out, block); samples += block; } while (now() - t0 < j->seconds);
     free(c); free(st); free(in); free(out);
+  } else if (!strcmp(j->wl, "mfcc_f32")) {
+    const int n = j->n, nm = 20, nd = 13;
+    uint32_t pos[20], len[20], total = 0;
+    float *coefs = malloc(sizeof(float) * n), dct[13 * 20];
+    float *win = malloc(sizeof(float) * n), *x = malloc(sizeof(float) * n), *src = malloc(sizeof(float) * n);
+    float *tmp = calloc(2 * n, sizeof(float)), out[13];
+    for (int i = 0; i < nm; ++i) {                   /* evenly spaced triangles below n/2 */
+      pos[i] = 1 + (uint32_t)i * (n / 2 - 2) / (nm + 1);
+      len[i] = 2 * ((n / 2 - 2) / (nm + 1)) + 1;
+      if (pos[i] + len[i] > (uint32_t)n / 2) len[i] = n / 2 - pos[i];
+      for (uint32_t k = 0; k < len[i]; ++k) coefs[total + k] = 1.0f - fabsf((float)k - len[i] / 2.0f) / len[i];
+      total += len[i];
+    }
+    for (int r = 0; r < nd; ++r)
+      for (int c = 0; c < nm; ++c) dct[r * nm + c] = (float)cos(3.14159265358979 / nm * (c + 0.5) * r);
+    for (int i = 0; i < n; ++i) { win[i] = 0.54f - 0.46f * (float)cos(6.283185307179586 * i / n); x[i] = uni(&seed); }
+    arm_mfcc_instance_f32 S;
+    F(arm_mfcc_init_f32)(&S, n, nm, nd, dct, pos, len, coefs, win);
+    do {
+      memcpy(src, x, sizeof(float) * n);
+      F(arm_mfcc_f32)(&S, src, out, tmp);
+      samples += n;
+    } while (now() - t0 < j->seconds);
+    free(coefs); free(win); free(x); free(src); free(tmp);
   } else if (!strcmp(j->wl, "mat_mult_f32")) {
     const int d = j->n;
     float *a = malloc(sizeof(float) * d * d), *b = malloc(sizeof(float) * d * d), *o = malloc(sizeof(float) * d * d);

@@ -14,6 +14,10 @@ T := $(REF)/Source/TransformFunctions
 F := $(REF)/Source/FilteringFunctions
 M := $(REF)/Source/MatrixFunctions
 C := $(REF)/Source/CommonTables
+B := $(REF)/Source/BasicMathFunctions
+X := $(REF)/Source/ComplexMathFunctions
+ST := $(REF)/Source/StatisticsFunctions
+FM := $(REF)/Source/FastMathFunctions
 
 SRCS := \
   $(T)/arm_cfft_f32.c $(T)/arm_cfft_radix8_f32.c $(T)/arm_cfft_init_f32.c \
@@ -22,7 +26,10 @@ SRCS := \
   $(T)/arm_bitreversal2.c $(T)/arm_bitreversal.c \
   $(T)/arm_rfft_fast_f32.c $(T)/arm_rfft_fast_init_f32.c \
   $(F)/arm_fir_f32.c $(F)/arm_fir_init_f32.c $(F)/arm_fir_q15.c $(F)/arm_fir_init_q15.c \
-  $(M)/arm_mat_mult_f32.c $(M)/arm_mat_init_f32.c \
+  $(M)/arm_mat_mult_f32.c $(M)/arm_mat_init_f32.c $(M)/arm_mat_vec_mult_f32.c \
+  $(T)/arm_mfcc_f32.c $(T)/arm_mfcc_init_f32.c $(ST)/arm_absmax_f32.c $(B)/arm_scale_f32.c \
+  $(B)/arm_mult_f32.c $(B)/arm_dot_prod_f32.c $(B)/arm_offset_f32.c $(X)/arm_cmplx_mag_f32.c \
+  $(FM)/arm_vlog_f32.c \
   $(C)/arm_common_tables.c $(C)/arm_const_structs.c
 
 OBJS := $(patsubst $(REF)/Source/%.c,$(OUT)/obj/%.o,$(SRCS))

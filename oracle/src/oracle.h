@@ -13,4 +13,9 @@ void oracle_arm_fir_f32(const arm_fir_instance_f32 *S, const float *pSrc, float 
 void oracle_arm_fir_q15(const arm_fir_instance_q15 *S, const int16_t *pSrc, int16_t *pDst, uint32_t blockSize);
 arm_status oracle_arm_mat_mult_f32(const arm_matrix_instance_f32 *A, const arm_matrix_instance_f32 *B,
                                    arm_matrix_instance_f32 *C);
+arm_status oracle_arm_mfcc_init_f32(arm_mfcc_instance_f32 *S, uint32_t fftLen, uint32_t nbMelFilters,
+                                    uint32_t nbDctOutputs, const float *dctCoefs, const uint32_t *filterPos,
+                                    const uint32_t *filterLengths, const float *filterCoefs,
+                                    const float *windowCoefs);
+void oracle_arm_mfcc_f32(const arm_mfcc_instance_f32 *S, float *pSrc, float *pDst, float *pTmp);
 #endif

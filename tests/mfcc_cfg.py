@@ -1,0 +1,45 @@
+"""MFCC test configurations: the reference suite's tables (tests/golden/mfcc_f32.npz, data of
+Testing/Source/Tests/mfccdata.c) and a small generator of further valid configurations
+(triangular Mel filters below fftLen/2, orthonormal DCT-II, Hamming window) for the sizes
+the suite does not cover.  The checkers receive the same tables, so any valid table set
+exercises the same arithmetic."""
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mfcc_f32.npz")
+
+
+def golden():
+    return dict(np.load(GOLDEN))
+
+
+def suite_cfg(g, n):
+    return {"fftLen": n, "dct": g["dct"], "pos": g[f"pos_{n}"], "len": g[f"len_{n}"], "coefs": g[f"coefs_{n}"],
+            "window": g[f"window_{n}"]}
+
+
+def make_cfg(n, nb_mel=20, nb_dct=13, fs=16000.0, fmin=64.0):
+    nb_mel = min(nb_mel, max(1, n // 4 - 2))
+    fmax = fs / 2
+    mel = lambda f: 1127.0 * np.log(1.0 + f / 700.0)       # noqa: E731
+    imel = lambda m: 700.0 * (np.exp(m / 1127.0) - 1.0)    # noqa: E731
+    pts = imel(np.linspace(mel(fmin), mel(fmax), nb_mel + 2))
+    bins = np.clip(np.floor(n * pts / fs).astype(int), 0, n // 2 - 1)
+    pos, lens, coefs = [], [], []
+    for i in range(nb_mel):
+        lo, mid, hi = bins[i], max(bins[i + 1], bins[i] + 1), max(bins[i + 2], bins[i] + 2)
+        hi = min(hi, n // 2 - 1)
+        mid = min(mid, hi)
+        k = np.arange(lo, hi + 1)
+        w = np.where(k <= mid, (k - lo + 1) / (mid - lo + 1), (hi - k + 1) / (hi - mid + 1))
+        pos.append(lo)
+        lens.append(len(k))
+        coefs.append(w)
+    r, c = np.meshgrid(np.arange(nb_dct), np.arange(nb_mel), indexing="ij")
+    dct = np.sqrt(2.0 / nb_mel) * np.cos(np.pi / nb_mel * (c + 0.5) * r)
+    dct[0] *= np.sqrt(0.5)
+    win = 0.54 - 0.46 * np.cos(2 * np.pi * np.arange(n) / n)
+    return {"fftLen": n, "dct": dct.astype(np.float32), "pos": np.array(pos, np.uint32),
+            "len": np.array(lens, np.uint32), "coefs": np.concatenate(coefs).astype(np.float32),
+            "window": win.astype(np.float32)}

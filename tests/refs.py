@@ -61,6 +61,26 @@ class Host:
         self.fn("arm_rfft_fast_f32")(C.byref(S), p.ctypes.data, out.ctypes.data, ifft)
         return out, p
 
+    def mfcc(self, cfg, frames):
+        """cfg: dict with fftLen, dct [nbDct x nbMel], pos, len, coefs, window; frames:
+        [batch, fftLen] -> [batch, nbDct] (one arm_mfcc_f32 call per frame, zeroed pTmp)."""
+        n = int(cfg["fftLen"])
+        keep = [np.ascontiguousarray(cfg["dct"], dtype=np.float32), np.ascontiguousarray(cfg["pos"], dtype=np.uint32),
+                np.ascontiguousarray(cfg["len"], dtype=np.uint32), np.ascontiguousarray(cfg["coefs"], dtype=np.float32),
+                np.ascontiguousarray(cfg["window"], dtype=np.float32)]
+        nb_mel, nb_dct = keep[1].size, keep[0].shape[0]
+        S = _abi.arm_mfcc_instance_f32()
+        st = self.fn("arm_mfcc_init_f32")(C.byref(S), n, nb_mel, nb_dct, *[k.ctypes.data for k in keep])
+        assert st == 0, st
+        frames = np.atleast_2d(np.asarray(frames, dtype=np.float32))
+        out = np.zeros((frames.shape[0], nb_dct), dtype=np.float32)
+        f = self.fn("arm_mfcc_f32")
+        for r in range(frames.shape[0]):
+            src = frames[r].copy()
+            tmp = np.zeros(2 * n, dtype=np.float32)
+            f(C.byref(S), src.ctypes.data, out[r].ctypes.data, tmp.ctypes.data)
+        return out
+
     def fir(self, kind, coeffs, blocks):
         """Stream `blocks` (list of 1-D arrays, each <= the block size) through one filter;
         returns (outputs, final state buffer)."""

@@ -25,6 +25,10 @@ int main(void) {
     F(arm_fir_instance_q15, pCoeffs) E()
   S(arm_matrix_instance_f32) F(arm_matrix_instance_f32, numRows) F(arm_matrix_instance_f32, numCols)
     F(arm_matrix_instance_f32, pData) E()
+  S(arm_mfcc_instance_f32) F(arm_mfcc_instance_f32, dctCoefs) F(arm_mfcc_instance_f32, filterCoefs)
+    F(arm_mfcc_instance_f32, windowCoefs) F(arm_mfcc_instance_f32, filterPos) F(arm_mfcc_instance_f32, filterLengths)
+    F(arm_mfcc_instance_f32, fftLen) F(arm_mfcc_instance_f32, nbMelFilters) F(arm_mfcc_instance_f32, nbDctOutputs)
+    F(arm_mfcc_instance_f32, rfft) E()
   printf("  \"arm_status\": {\"size\": %zu, \"ARM_MATH_SIZE_MISMATCH\": %d}\n}\n", sizeof(arm_status),
          (int)ARM_MATH_SIZE_MISMATCH);
   return 0;
