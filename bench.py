@@ -260,6 +260,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="cfft_f32_1024", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="items per GPU (default: the BASELINE config)")
+    ap.add_argument("--fftlen", type=int, default=0,
+                    help="cfft workloads: another fftLen (16..4096), batch scaled to the same bytes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-companion", action="store_true", help="skip the q31 companion measurement")
     ap.add_argument("--dist-backend", default=None, help="nccl (default, RCCL) or gloo (rehearsal)")
@@ -269,6 +271,9 @@ def main():
     WORLD = parallel.init(backend=args.dist_backend)
     world, rank = WORLD.size, WORLD.rank
     kind, n, batch0, bps = WORKLOADS[args.workload]
+    if args.fftlen and args.workload.startswith("cfft"):
+        batch0 = max(1, batch0 * n // args.fftlen)
+        n = args.fftlen
     batch = args.batch or batch0
     if args.workload.startswith("cfft"):
         wall, kern_ms, parity = run_cfft(kind, n, batch, args.steps, args.warmup, world, rank)

@@ -179,15 +179,28 @@ bool mfcc_prepare(const arm_mfcc_instance_f32* S, MfccDev& d) {
   return true;
 }
 
-// x: [batch][n] frames (overwritten), y: [batch][n] work, dst: [batch][nbDct]; the frame
-// maxima ride in dst[frame][0] between the two passes (read before the row is written).
+// x: [batch][n] frames, y: [batch][n] work, dst: [batch][nbDct].  The reference's own
+// (canonical) CFFT tables take the fused single-launch kernel (x read once, y unused);
+// otherwise three launches, x overwritten and the frame maxima carried in dst[frame][0]
+// between the passes (read before the row is written).
 bool mfcc_run(const arm_mfcc_instance_f32* S, const MfccDev& d, float* x, float* y, float* dst, uint32_t batch,
               hipStream_t st) {
-  const int n = (int)S->fftLen, nd = (int)S->nbDctOutputs;
+  const int n = (int)S->fftLen, nd = (int)S->nbDctOutputs, nm = (int)S->nbMelFilters;
+  const arm_cfft_instance_f32& in = S->rfft.Sint;
+  bool canon = true, ok = true;
+  if (in.pBitRevTable) (void)device_perm((int)in.fftLen, in.pBitRevTable, in.bitRevLength, 0, &canon, &ok);
+  if (ok && canon && nm <= n / 2 && in.fftLen == (uint32_t)n / 2) {
+    const void* tw = device_table(in.pTwiddle, 8u * in.fftLen);
+    const void* twr = device_table(S->rfft.pTwiddleRFFT, sizeof(float) * n);
+    if (!tw || !twr) return false;
+    MI_CHECK(mfcc_f32_fused_launch(n, x, d.win, (const float*)tw, (const float*)twr, nm, d.pos, d.len, d.off,
+                                   d.coefs, nd, d.dct, dst, batch, st),
+             "mfcc fused");
+    return true;
+  }
   MI_CHECK(mfcc_f32_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc pre");
   if (!rfft_run(&S->rfft, x, y, batch, 0, st)) return false;
-  MI_CHECK(mfcc_f32_post_launch(n, y, dst, nd, (int)S->nbMelFilters, d.pos, d.len, d.off, d.coefs, nd, d.dct, dst,
-                                batch, st),
+  MI_CHECK(mfcc_f32_post_launch(n, y, dst, nd, nm, d.pos, d.len, d.off, d.coefs, nd, d.dct, dst, batch, st),
            "mfcc post");
   return true;
 }

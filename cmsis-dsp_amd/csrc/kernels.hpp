@@ -50,6 +50,12 @@ hipError_t fir_q15_launch(const int16_t* coeffs, int num_taps, const int16_t* sr
 
 // MFCC f32 around the batched RFFT (mfcc_f32.hip): frame normalisation + window, then the
 // spectrum -> Mel -> log -> DCT tail.  post needs mfcc_f32_post_lds(n, nb_mel) bytes of LDS.
+// Fused single-launch MFCC for the reference's canonical CFFT tables (nb_mel <= n/2):
+// tw = the inner CFFT(n/2) twiddles, twr = the RFFT split twiddles (twiddleCoef_rfft_n).
+hipError_t mfcc_f32_fused_launch(int n, const float* src, const float* win, const float* tw, const float* twr,
+                                 int nb_mel, const uint32_t* pos, const uint32_t* len, const uint32_t* off,
+                                 const float* coefs, int nb_dct, const float* dct, float* dst, uint32_t batch,
+                                 hipStream_t st);
 // The frame maximum of frame f is written to / read from maxv[f * maxv_stride].
 hipError_t mfcc_f32_pre_launch(int n, const float* src, const float* win, float* x, float* maxv, uint32_t batch,
                                int maxv_stride, hipStream_t st);

@@ -1,7 +1,17 @@
 // Batched MFCC f32 — MI355X kernels around the batched real FFT.
 //
 // Replaces Source/TransformFunctions/arm_mfcc_f32.c:83-160 (RFFT-based default path) for
-// `batch` frames.  Three stream-ordered launches per batch:
+// `batch` frames.
+//
+// Fused path (mfcc_fused_kernel<H>, H = fftLen/2, the default for the reference's own
+// bit-reversal tables): one launch, each frame read from HBM once and only the DCT
+// outputs written.  A 256-thread workgroup holds TPB = 256/(H/16) frames in 32 KiB of LDS;
+// the H/16 lanes of a frame normalise + window it in LDS, run the shared bit-exact CFFT
+// core (cfft_f32_core.hpp), form the split spectrum (stage_rfft_f32) directly from the
+// digit-reversed CFFT output, and continue with magnitudes, Mel, log and DCT in LDS.
+//
+// Unfused path (custom CFFT bit-reversal tables, or more Mel filters than fftLen/2): three
+// stream-ordered launches per batch:
 //   mfcc_pre   frame max |x| (arm_absmax_f32), x*(1/max) (arm_scale_f32), x*window
 //              (arm_mult_f32) -> X, max -> M            [one wave per frame]
 //   rfft       arm_rfft_fast_f32 forward on X -> Y      [the bit-exact batched RFFT]
@@ -14,12 +24,20 @@
 // the host libm's by an ulp.
 #include "common.hpp"
 #include "kernels.hpp"
+#include "cfft_f32_core.hpp"
 
 #pragma clang fp contract(off)
 
 namespace mi355x {
 
 constexpr int kMfccWaves = 4;   // frames (waves) per 256-thread workgroup
+
+#ifndef MI355X_MFCC_UNROLL
+#define MI355X_MFCC_UNROLL 8        // Mel / DCT dot products: loads issued 8 taps ahead
+#endif
+#ifndef MI355X_MFCC_SKIP_TAIL
+#define MI355X_MFCC_SKIP_TAIL 0     // diagnostic only: stop after the spectrum (no Mel/log/DCT)
+#endif
 
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
@@ -105,12 +123,162 @@ __global__ __launch_bounds__(256) void mfcc_post_kernel(const float* __restrict_
     for (int r = lane; r < nb_dct; r += 64) {
       const float* d = dct + (size_t)r * nb_mel;
       float sum = 0.0f;
+#pragma unroll MI355X_MFCC_UNROLL
       for (int i = 0; i < nb_mel; ++i) {
         const float prod = d[i] * mel[i];
         sum = sum + prod;
       }
       o[r] = sum;
     }
+  }
+}
+
+template <int H>
+__global__ __launch_bounds__(kBlock) void mfcc_fused_kernel(const float* __restrict__ src, const float* __restrict__ win,
+                                                            const float2* __restrict__ tw,
+                                                            const float2* __restrict__ twr, int nb_mel,
+                                                            const uint32_t* __restrict__ pos,
+                                                            const uint32_t* __restrict__ len,
+                                                            const uint32_t* __restrict__ off,
+                                                            const float* __restrict__ coefs, int nb_dct,
+                                                            const float* __restrict__ dct, float* __restrict__ dst,
+                                                            uint32_t batch) {
+  using P = PlanF32<H>;
+  constexpr int NF = 2 * H, LPT = P::LPT, TPB = P::TPB;
+  __shared__ __attribute__((aligned(16))) float2 lds[TPB * H];
+  // the CFFT(H) and split twiddles, staged once per workgroup: every butterfly of every
+  // frame reads them from LDS instead of through the vector memory path
+  __shared__ __attribute__((aligned(16))) float2 tws[H], twrs[H];
+  __shared__ float wmax[kBlock / 64];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < H; i += kBlock) { tws[i] = tw[i]; twrs[i] = twr[i]; }
+  const uint64_t f0 = (uint64_t)blockIdx.x * TPB;
+  const int valid = (int)min<uint64_t>((uint64_t)TPB, batch - f0);
+  {  // frames -> LDS, 16-B coalesced; frames past the batch end are zero-filled
+    const float4* s4 = reinterpret_cast<const float4*>(src + f0 * NF);
+    float4* d4 = reinterpret_cast<float4*>(lds);
+    const int n_valid = valid * (NF / 4);
+#pragma unroll 4
+    for (int i = tid; i < TPB * (NF / 4); i += kBlock) d4[i] = i < n_valid ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+  const int tr = tid / LPT, lane = tid % LPT;
+  float2* x = lds + tr * H;
+  float* xf = reinterpret_cast<float*>(x);
+
+  // ---- max |x| over the frame's LPT lanes (arm_absmax_f32; order-free for the max value)
+  float m = 0.0f;
+#pragma unroll 4
+  for (int j = lane; j < NF; j += LPT) m = fmaxf(m, fabsf(xf[j]));
+  if constexpr (LPT <= 64) {
+#pragma unroll
+    for (int o = LPT / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  } else {
+    m = wave_max(m);
+    if ((tid & 63) == 0) wmax[tid >> 6] = m;
+    __syncthreads();
+    m = 0.0f;
+#pragma unroll
+    for (int w = 0; w < LPT / 64; ++w) m = fmaxf(m, wmax[tr * (LPT / 64) + w]);
+  }
+  const bool scale = m != 0.0f;
+  const float inv = scale ? 1.0f / m : 1.0f;          // arm_mfcc_f32.c:102-105
+#pragma unroll 4
+  for (int j = lane; j < NF; j += LPT) {
+    float v = xf[j];
+    if (scale) v = v * inv;
+    xf[j] = v * win[j];                               // arm_mult_f32
+  }
+  __syncthreads();
+
+  cfft_f32_lds_fwd<H>(x, lane, tws);                  // arm_rfft_fast_f32.c:689 (bitrev folded below)
+
+  // ---- stage_rfft_f32 (arm_rfft_fast_f32.c:316-402) + |.| (arm_cmplx_mag_f32) + *max
+  constexpr int KPL = H / LPT;                        // bins per lane (16)
+  float mg[KPL];
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) {
+    const int k = lane + i * LPT;
+    float re, im;
+    if (k == 0) {
+      const float2 a = x[f32_src<H>(0)];
+      const float t1a = a.x + a.x, t1b = a.y + a.y;
+      re = 0.5f * (t1a + t1b);
+      im = 0.0f;                                      // pTmp[1] = 0 (arm_mfcc_f32.c:125)
+    } else {
+      const float2 A = x[f32_src<H>(k)], B = x[f32_src<H>(H - k)], w = twrs[k];
+      const float t1a = B.x - A.x, t1b = B.y + A.y;
+      const float p0 = w.x * t1a, p1 = w.y * t1a, p2 = w.x * t1b, p3 = w.y * t1b;
+      re = 0.5f * (A.x + B.x + p0 + p3);
+      im = 0.5f * (A.y - B.y + p1 - p2);
+    }
+    const float rr = re * re, ii = im * im;
+    const float sq = rr + ii;
+    float v = sq >= 0.0f ? sqrtf(sq) : 0.0f;
+    if (scale) v = v * m;
+    mg[i] = v;
+  }
+  __syncthreads();                                    // every spectrum read is done
+  float* mag = xf;                                    // H magnitudes, then nb_mel log-Mel values
+  float* mel = xf + H;
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) mag[lane + i * LPT] = mg[i];
+  __syncthreads();
+#if MI355X_MFCC_SKIP_TAIL
+  if (tr < valid && lane == 0) dst[(f0 + tr) * (uint64_t)nb_dct] = mag[1] + mag[H - 1];
+  return;
+#endif
+  for (int i = lane; i < nb_mel; i += LPT) {
+    const uint32_t p = pos[i], l = len[i];
+    const float* c = coefs + off[i];
+    float sum = 0.0f;
+#pragma unroll MI355X_MFCC_UNROLL
+    for (uint32_t j = 0; j < l; ++j) {
+      const uint32_t k = p + j;
+      const float prod = (k < (uint32_t)H ? mag[k] : 0.0f) * c[j];
+      sum = sum + prod;
+    }
+    mel[i] = logf(sum + 1.0e-6f);
+  }
+  __syncthreads();
+  if (tr < valid) {
+    float* o = dst + (f0 + tr) * (uint64_t)nb_dct;
+    for (int r = lane; r < nb_dct; r += LPT) {
+      const float* d = dct + (size_t)r * nb_mel;
+      float sum = 0.0f;
+#pragma unroll MI355X_MFCC_UNROLL
+      for (int i = 0; i < nb_mel; ++i) {
+        const float prod = d[i] * mel[i];
+        sum = sum + prod;
+      }
+      o[r] = sum;
+    }
+  }
+}
+
+template <int H>
+static hipError_t launch_fused(const float* src, const float* win, const float* tw, const float* twr, int nb_mel,
+                               const uint32_t* pos, const uint32_t* len, const uint32_t* off, const float* coefs,
+                               int nb_dct, const float* dct, float* dst, uint32_t batch, hipStream_t st) {
+  constexpr int TPB = PlanF32<H>::TPB;
+  const uint32_t grid = (uint32_t)((batch + TPB - 1) / TPB);
+  hipLaunchKernelGGL(mfcc_fused_kernel<H>, dim3(grid), dim3(kBlock), 0, st, src, win, (const float2*)tw,
+                     (const float2*)twr, nb_mel, pos, len, off, coefs, nb_dct, dct, dst, batch);
+  return hipGetLastError();
+}
+
+hipError_t mfcc_f32_fused_launch(int n, const float* src, const float* win, const float* tw, const float* twr,
+                                 int nb_mel, const uint32_t* pos, const uint32_t* len, const uint32_t* off,
+                                 const float* coefs, int nb_dct, const float* dct, float* dst, uint32_t batch,
+                                 hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  if (nb_mel > n / 2) return hipErrorInvalidValue;
+  switch (n) {
+#define MI_FUSED(NF) \
+    case NF: return launch_fused<NF / 2>(src, win, tw, twr, nb_mel, pos, len, off, coefs, nb_dct, dct, dst, batch, st);
+    MI_FUSED(32) MI_FUSED(64) MI_FUSED(128) MI_FUSED(256) MI_FUSED(512) MI_FUSED(1024) MI_FUSED(2048) MI_FUSED(4096)
+#undef MI_FUSED
+    default: return hipErrorInvalidValue;
   }
 }
 

@@ -104,3 +104,19 @@ def test_gpu_batch_device_tables_and_content_cache(dsp, torch_gpu, ref):
     b = m2.batch(torch_gpu.from_numpy(frames.copy()).cuda()).cpu().numpy()
     assert _close(a, ref.mfcc(cfg, frames)).all() and _close(b, ref.mfcc(cfg2, frames)).all()
     assert not np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_gpu_unfused_path_more_filters_than_half_spectrum(dsp, torch_gpu, ref):
+    """nbMelFilters > fftLen/2 takes the three-launch path (pre, RFFT, post)."""
+    n, nb_mel = 64, 40
+    cfg = {"fftLen": n, "pos": np.array([i % 30 for i in range(nb_mel)], np.uint32),
+           "len": np.full(nb_mel, 2, np.uint32),
+           "coefs": np.random.default_rng(3).uniform(0, 1, 2 * nb_mel).astype(np.float32),
+           "dct": np.random.default_rng(4).uniform(-0.3, 0.3, (13, nb_mel)).astype(np.float32),
+           "window": np.hanning(n).astype(np.float32)}
+    frames = np.random.default_rng(5).uniform(-1, 1, (9, n)).astype(np.float32)
+    m = dsp.MfccF32(n, cfg["dct"], cfg["pos"], cfg["len"], cfg["coefs"], cfg["window"])
+    got = m.batch(torch_gpu.from_numpy(frames.copy()).cuda()).cpu().numpy()
+    want = ref.mfcc(cfg, frames)
+    assert _close(got, want).all(), np.abs(got - want).max()
