@@ -26,7 +26,11 @@ __global__ __launch_bounds__(kBlock) void cfft_f32_kernel(float2* __restrict__ d
                                                           const uint16_t* __restrict__ perm,
                                                           uint32_t flags) {
   using P = PlanF32<N>;
-  __shared__ __attribute__((aligned(16))) float2 lds[P::TPB * N];
+  // transforms sit SP complex apart in LDS: for N <= 64 (LPT <= 4: many transforms per
+  // 32-lane group, all at the same offset) one pad element keeps their lanes on distinct
+  // banks; larger N pay more in occupancy (LDS > 32 KiB) than they would gain (measured)
+  constexpr int SP = N + (P::LPT <= 4 ? 1 : 0);
+  __shared__ __attribute__((aligned(16))) float2 lds[P::TPB * SP];
   const int tid = threadIdx.x;
   const uint64_t t0 = (uint64_t)blockIdx.x * P::TPB;
   const int valid = (int)min<uint64_t>((uint64_t)P::TPB, batch - t0);
@@ -35,19 +39,20 @@ __global__ __launch_bounds__(kBlock) void cfft_f32_kernel(float2* __restrict__ d
   // ---- load: 16-B coalesced, conj on the fly (arm_cfft_f32.c:1252-1261)
   {
     const float4* src = reinterpret_cast<const float4*>(data + t0 * N);
-    float4* dst = reinterpret_cast<float4*>(lds);
     const int n4 = valid * N / 2;
 #pragma unroll 4
     for (int i = tid; i < n4; i += kBlock) {
       float4 v = src[i];
       if (ifft) { v.y = -v.y; v.w = -v.w; }
-      dst[i] = v;
+      const int e = 2 * i, t = e / N, k = e % N;
+      lds[t * SP + k] = make_float2(v.x, v.y);
+      lds[t * SP + k + 1] = make_float2(v.z, v.w);
     }
   }
   __syncthreads();
 
   const int tr = tid / P::LPT, lane = tid % P::LPT;
-  float2* x = lds + tr * N;
+  float2* x = lds + tr * SP;
 
   cfft_f32_lds_fwd<N>(x, lane, tw);
 
@@ -64,9 +69,9 @@ __global__ __launch_bounds__(kBlock) void cfft_f32_kernel(float2* __restrict__ d
       if (brev) {
         const int sa = perm ? perm[k] : f32_src<N>(k);
         const int sb = perm ? perm[k + 1] : f32_src<N>(k + 1);
-        a = lds[t * N + sa]; b = lds[t * N + sb];
+        a = lds[t * SP + sa]; b = lds[t * SP + sb];
       } else {
-        a = lds[e]; b = lds[e + 1];
+        a = lds[t * SP + k]; b = lds[t * SP + k + 1];
       }
       if (ifft) {
         a.x = a.x * invL; a.y = -a.y * invL;

@@ -209,22 +209,32 @@ __global__ __launch_bounds__(kBlock) void cfft_fx_kernel(typename Fx<T>::C* __re
   using P = PlanFx<N>;
   using F = Fx<T>;
   using C = typename F::C;
-  __shared__ __attribute__((aligned(16))) C lds[P::TPB * N];
+  // transforms sit SP complex apart in LDS: for N <= 64 (LPT <= 4: many transforms per
+  // 32-lane group, all at the same offset) one pad element keeps their lanes on distinct
+  // banks; larger N pay more in occupancy than they would gain (measured)
+  constexpr int SP = N + (P::LPT <= 4 ? 1 : 0);
+  __shared__ __attribute__((aligned(16))) C lds[P::TPB * SP];
   const int tid = threadIdx.x;
   const uint64_t t0 = (uint64_t)blockIdx.x * P::TPB;
   const int valid = (int)min<uint64_t>((uint64_t)P::TPB, batch - t0);
 
-  {  // coalesced 16-B load
+  {  // coalesced 16-B load, scattered to the padded LDS image
+    constexpr int PER16 = 16 / (int)sizeof(C);
     const int4* src = reinterpret_cast<const int4*>(data + t0 * N);
-    int4* dst = reinterpret_cast<int4*>(lds);
-    const int n16 = valid * N * (int)sizeof(C) / 16;
+    const int n16 = valid * N / PER16;
 #pragma unroll 4
-    for (int i = tid; i < n16; i += kBlock) dst[i] = src[i];
+    for (int i = tid; i < n16; i += kBlock) {
+      const int4 v = src[i];
+      const int e = i * PER16, t = e / N, k = e % N;
+      const C* c = reinterpret_cast<const C*>(&v);
+#pragma unroll
+      for (int u = 0; u < PER16; ++u) lds[t * SP + k + u] = c[u];
+    }
   }
   __syncthreads();
 
   const int tr = tid / P::LPT, lane = tid % P::LPT;
-  C* x = lds + tr * N;
+  C* x = lds + tr * SP;
 
   if constexpr (P::BY2) {
     // radix-2 pre-pass: arm_cfft_q31.c:774-794 / :835-855, arm_cfft_q15.c:782-800 / :881-899
@@ -271,7 +281,7 @@ __global__ __launch_bounds__(kBlock) void cfft_fx_kernel(typename Fx<T>::C* __re
       for (int u = 0; u < PER16; ++u) {
         const int k = k0 + u;
         const int src = brev ? (perm ? (int)perm[k] : bitrev<LOG>(k)) : k;
-        v[u] = F::ld(lds + t * N + src);
+        v[u] = F::ld(lds + t * SP + src);
         if constexpr (P::BY2) {
           if constexpr (sizeof(T) == 4) v[u] = make_int2(wshl(v[u].x, 1), wshl(v[u].y, 1));
           else v[u] = make_int2(t16(v[u].x << 1), t16(v[u].y << 1));
