@@ -44,6 +44,9 @@ WORKLOADS = {
     "cfft_q15_4096": ("q15", 4096, 1 << 18, 8),
     "fir_f32": ("fir_f32", 128, 1 << 16, 8),
     "fir_q15": ("fir_q15", 128, 1 << 16, 4),
+    "fir_q31": ("fir_q31", 128, 1 << 16, 8),
+    "fir_fast_q15": ("fir_fast_q15", 128, 1 << 16, 4),
+    "fir_fast_q31": ("fir_fast_q31", 128, 1 << 16, 8),
     "mat_mult_f32": ("mat", 1024, 256, None),
     "mfcc_f32": ("mfcc", 1024, 1 << 18, 4),
 }
@@ -104,7 +107,8 @@ def cpu_baseline(workload, n):
     if not os.path.exists(exe):
         return None
     wl = {"cfft_f32_1024": "cfft_f32", "cfft_q31_4096": "cfft_q31", "cfft_q15_4096": "cfft_q15",
-          "fir_f32": "fir_f32", "fir_q15": "fir_q15", "mat_mult_f32": "mat_mult_f32",
+          "fir_f32": "fir_f32", "fir_q15": "fir_q15", "fir_q31": "fir_q31", "fir_fast_q15": "fir_fast_q15",
+          "fir_fast_q31": "fir_fast_q31", "mat_mult_f32": "mat_mult_f32",
           "mfcc_f32": "mfcc_f32"}[workload]
     nn = 256 if workload == "mat_mult_f32" else n      # 1024^3 takes seconds per matrix on one core
     out = subprocess.run([exe, wl, str(nn), str(threads), str(secs)], capture_output=True, text=True,
@@ -174,31 +178,31 @@ def run_cfft(kind, n, batch, steps, warmup, world, rank, check=True):
 
 
 def run_fir(kind, taps, batch, steps, warmup, world, rank, block=4096):
+    """kind: f32 | q15 | q31 | fast_q15 | fast_q31 (arm_fir_<kind>), full-range fixed point."""
     import ctypes as C
-    q15 = kind == "q15"
+    base = kind[-3:]
     rng = np.random.default_rng(5)
-    if q15:
-        S = dsp.arm_fir_instance_q15()
-        c = torch.from_numpy(rng.integers(-32768, 32768, taps).astype(np.int16)).cuda()
-        src = synth("q15", batch * block, rank).view(batch, block)
-    else:
-        S = dsp.arm_fir_instance_f32()
+    S = {"f32": dsp.arm_fir_instance_f32, "q15": dsp.arm_fir_instance_q15, "q31": dsp.arm_fir_instance_q31}[base]()
+    if base == "f32":
         c = torch.from_numpy((rng.standard_normal(taps) / np.sqrt(taps)).astype(np.float32)).cuda()
-        src = synth("f32", batch * block, rank).view(batch, block)
+    else:
+        bits, dt = (15, np.int16) if base == "q15" else (31, np.int32)
+        c = torch.from_numpy(rng.integers(-(1 << bits), 1 << bits, taps).astype(dt)).cuda()
+    src = synth(base, batch * block, rank).view(batch, block)
     S.numTaps = taps
     S.pCoeffs = C.cast(c.data_ptr(), S._fields_[2][1])
     dst = torch.empty_like(src)
     hist = torch.zeros((batch, taps - 1), dtype=src.dtype, device="cuda")
 
     def launch(s):
-        dsp.fir_batch(S, src, dst, hist, q15=q15)
+        dsp.fir_batch(S, src, dst, hist, kind=kind)
 
     wall, kern_ms = time_launches(launch, steps, warmup, world)
     # parity: two filters, one block, from zero history, vs the checker
     host, hk = cpu_checker()
     h0 = torch.zeros((2, taps - 1), dtype=src.dtype, device="cuda")
     d0 = torch.empty((2, block), dtype=src.dtype, device="cuda")
-    dsp.fir_batch(S, src[:2].contiguous(), d0, h0, q15=q15)
+    dsp.fir_batch(S, src[:2].contiguous(), d0, h0, kind=kind)
     torch.cuda.synchronize()
     ok = all(d0[f].cpu().numpy().tobytes() ==
              host.fir(kind, c.cpu().numpy(), [src[f].cpu().numpy()])[0][0].tobytes() for f in range(2))
@@ -311,7 +315,9 @@ def main():
     else:
         line.update(value=round(total_units / wall * 1e-9, 3), unit="Gsamples/s",
                     dtype={"f32": "f32", "q31": "q31 (int32)", "q15": "q15 (int16)", "fir_f32": "f32",
-                           "fir_q15": "q15 (int16 x int16 -> int64)", "mfcc": "f32"}[kind])
+                           "fir_q15": "q15 (int16 x int16 -> int64)", "mfcc": "f32",
+                           "fir_q31": "q31 (int32 x int32 -> int64)", "fir_fast_q15": "q15 (int32 wrap accumulator)",
+                           "fir_fast_q31": "q31 (rounded high-word accumulator)"}[kind])
         if args.workload.startswith("cfft"):
             line["config"] = {"workload": f"arm_cfft_{kind} N={n} batch={batch}/GPU in place, bitReverseFlag=1, "
                                           f"alternating fwd/inv (BASELINE configs[{1 if kind == 'f32' else 3}])",
@@ -329,6 +335,10 @@ def main():
         line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.workload),
                             "algorithmic_bytes_per_launch": algo_bytes, "avg_kernel_ms": round(kern_ms, 4)}
+        if args.workload == "fir_fast_q15":
+            valu = units * n / 2 / (kern_ms * 1e-3) * 1e-12      # one accumulating v_dot2 per tap pair
+            line["roofline"]["valu_tops_dot2"] = {"achieved": round(valu, 2), "peak": FP32_NOFMA_TFLOPS,
+                                                  "frac": round(valu / FP32_NOFMA_TFLOPS, 4)}
         if args.workload == "fir_q15":
             # one v_dot2_i32_i16 per tap pair per h/l half: T VALU ops per output sample
             valu = units * n / (kern_ms * 1e-3) * 1e-12

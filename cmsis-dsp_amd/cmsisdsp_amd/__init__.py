@@ -19,7 +19,7 @@ import numpy as np
 
 from . import _abi
 from ._abi import (arm_cfft_instance_f32, arm_cfft_instance_q15, arm_cfft_instance_q31,  # noqa: F401
-                   arm_fir_instance_f32, arm_fir_instance_q15, arm_matrix_instance_f32,
+                   arm_fir_instance_f32, arm_fir_instance_q15, arm_fir_instance_q31, arm_matrix_instance_f32,
                    arm_rfft_fast_instance_f32, arm_mfcc_instance_f32, ARM_MATH_SUCCESS, ARM_MATH_ARGUMENT_ERROR,
                    ARM_MATH_SIZE_MISMATCH)
 
@@ -156,6 +156,37 @@ class FirQ15(FirF32):
         return y
 
 
+class FirQ31(FirF32):
+    """Streaming arm_fir_q31 (fast=False) or arm_fir_fast_q31 (fast=True)."""
+
+    def __init__(self, coeffs, block_size, fast=False):
+        self.coeffs = np.ascontiguousarray(coeffs, dtype=np.int32)
+        self.block_size = block_size
+        self.fn = lib.arm_fir_fast_q31 if fast else lib.arm_fir_q31
+        self.state = np.zeros(len(self.coeffs) + block_size - 1, dtype=np.int32)
+        self.S = arm_fir_instance_q31()
+        lib.arm_fir_init_q31(C.byref(self.S), len(self.coeffs), self.coeffs.ctypes.data,
+                             self.state.ctypes.data, block_size)
+
+    def __call__(self, x):
+        x = np.ascontiguousarray(x, dtype=np.int32)
+        y = np.empty_like(x)
+        self.fn(C.byref(self.S), x.ctypes.data, y.ctypes.data, len(x))
+        _check_void(self.fn.__name__)
+        return y
+
+
+class FirFastQ15(FirQ15):
+    """Streaming arm_fir_fast_q15."""
+
+    def __call__(self, x):
+        x = np.ascontiguousarray(x, dtype=np.int16)
+        y = np.empty_like(x)
+        lib.arm_fir_fast_q15(C.byref(self.S), x.ctypes.data, y.ctypes.data, len(x))
+        _check_void("arm_fir_fast_q15")
+        return y
+
+
 def arm_mat_mult_f32(a, b):
     """(status, C) = A @ B through arm_mat_mult_f32 (row-major f32)."""
     a = np.ascontiguousarray(a, dtype=np.float32)
@@ -247,10 +278,18 @@ def rfft_fast_batch(S, p, out, ifft, stream=None):
         raise RuntimeError(f"arm_rfft_fast_f32_batch -> {st}: {last_error()[1]}")
 
 
-def fir_batch(S, src, dst, hist, stream=None, q15=False):
-    """src/dst: [batch, blockSize] device tensors; hist: [batch, numTaps-1] device state."""
+_FIR_BATCH = {"f32": "arm_fir_f32_batch", "q15": "arm_fir_q15_batch", "q31": "arm_fir_q31_batch",
+              "fast_q15": "arm_fir_fast_q15_batch", "fast_q31": "arm_fir_fast_q31_batch"}
+
+
+def fir_batch(S, src, dst, hist, stream=None, q15=False, kind=None):
+    """src/dst: [batch, blockSize] device tensors; hist: [batch, numTaps-1] device state.
+    kind: f32 | q15 | q31 | fast_q15 | fast_q31 (default from the instance type / q15 flag)."""
+    if kind is None:
+        kind = "q15" if q15 else {arm_fir_instance_f32: "f32", arm_fir_instance_q15: "q15",
+                                  arm_fir_instance_q31: "q31"}[type(S)]
     batch, block = src.shape
-    fn = lib.arm_fir_q15_batch if q15 else lib.arm_fir_f32_batch
+    fn = getattr(lib, _FIR_BATCH[kind])
     st = fn(C.byref(S), C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()), block, batch,
             C.c_void_p(hist.data_ptr() if hist is not None and hist.numel() else 0), _stream_ptr(stream))
     if st != ARM_MATH_SUCCESS:

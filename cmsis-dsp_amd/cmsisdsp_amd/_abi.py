@@ -43,6 +43,11 @@ class arm_fir_instance_q15(C.Structure):
     _fields_ = [("numTaps", C.c_uint16), ("pState", c_i16p), ("pCoeffs", c_i16p)]
 
 
+class arm_fir_instance_q31(C.Structure):
+    # Include/dsp/filtering_functions.h:76-81
+    _fields_ = [("numTaps", C.c_uint16), ("pState", c_i32p), ("pCoeffs", c_i32p)]
+
+
 class arm_matrix_instance_f32(C.Structure):
     # Include/dsp/matrix_functions.h:118-123
     _fields_ = [("numRows", C.c_uint16), ("numCols", C.c_uint16), ("pData", c_f32p)]
@@ -74,6 +79,10 @@ DROPIN = {
     "arm_fir_f32": (None, [P(arm_fir_instance_f32), C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_fir_init_q15": (C.c_int, [P(arm_fir_instance_q15), C.c_uint16, C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_fir_q15": (None, [P(arm_fir_instance_q15), C.c_void_p, C.c_void_p, C.c_uint32]),
+    "arm_fir_fast_q15": (None, [P(arm_fir_instance_q15), C.c_void_p, C.c_void_p, C.c_uint32]),
+    "arm_fir_init_q31": (None, [P(arm_fir_instance_q31), C.c_uint16, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "arm_fir_q31": (None, [P(arm_fir_instance_q31), C.c_void_p, C.c_void_p, C.c_uint32]),
+    "arm_fir_fast_q31": (None, [P(arm_fir_instance_q31), C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_mat_init_f32": (None, [P(arm_matrix_instance_f32), C.c_uint16, C.c_uint16, C.c_void_p]),
     "arm_mfcc_init_f32": (C.c_int, [P(arm_mfcc_instance_f32), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -108,6 +117,12 @@ BATCHED = {
                                     C.c_void_p, C.c_void_p]),
     "arm_fir_q15_batch": (C.c_int, [P(arm_fir_instance_q15), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                     C.c_void_p, C.c_void_p]),
+    "arm_fir_fast_q15_batch": (C.c_int, [P(arm_fir_instance_q15), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                         C.c_void_p, C.c_void_p]),
+    "arm_fir_q31_batch": (C.c_int, [P(arm_fir_instance_q31), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                    C.c_void_p, C.c_void_p]),
+    "arm_fir_fast_q31_batch": (C.c_int, [P(arm_fir_instance_q31), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                         C.c_void_p, C.c_void_p]),
     "arm_mat_mult_f32_batch": (C.c_int, [P(arm_matrix_instance_f32), P(arm_matrix_instance_f32),
                                          P(arm_matrix_instance_f32), C.c_uint32, C.c_void_p]),
     "arm_mfcc_f32_batch": (C.c_int, [P(arm_mfcc_instance_f32), C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,

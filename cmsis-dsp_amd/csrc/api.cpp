@@ -220,7 +220,7 @@ const T* device_coeffs(const T* c, int n, int slot, hipStream_t st, bool* ok) {
 // drop-in FIR: state = [history(T-1) ; block(B)] on host or device (arm_fir_f32.c:911-1280).
 // After the call the state holds [new history ; block input], as the reference leaves it.
 template <typename T, typename Inst>
-void fir_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B) {
+void fir_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B, int kind) {
   if (!S || !S->pState || !S->pCoeffs || S->numTaps == 0 || B == 0) return;
   const int taps = S->numTaps, T1 = taps - 1;
   hipStream_t st = sync_stream();
@@ -237,8 +237,7 @@ void fir_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B) {
   if (!dstate && T1 > 0) e = hipMemcpyAsync(dhist, S->pState, hb, hipMemcpyHostToDevice, st);
   if (e == hipSuccess && !dsrc) e = hipMemcpyAsync((void*)dsr, pSrc, sb, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) {
-    if constexpr (sizeof(T) == 4) e = fir_f32_launch((const float*)dc, taps, (const float*)dsr, (float*)dds, B, 1, (float*)dhist, st);
-    else e = fir_q15_launch((const int16_t*)dc, taps, (const int16_t*)dsr, (int16_t*)dds, B, 1, (int16_t*)dhist, st);
+    e = fir_run(kind, dc, taps, dsr, dds, B, 1, dhist, st);
   }
   if (e == hipSuccess && !ddst) e = hipMemcpyAsync(pDst, dds, sb, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess && !dstate && T1 > 0) e = hipMemcpyAsync(S->pState, dhist, hb, hipMemcpyDeviceToHost, st);
@@ -250,16 +249,15 @@ void fir_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B) {
 }
 
 template <typename T, typename Inst>
-arm_status fir_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uint32_t batch, T* d_hist, void* stream) {
+arm_status fir_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uint32_t batch, T* d_hist, void* stream,
+                     int kind) {
   if (!S || !S->pCoeffs || S->numTaps == 0 || (batch && B && (!d_src || !d_dst))) return ARM_MATH_ARGUMENT_ERROR;
   if (S->numTaps > 1 && batch && !d_hist) return ARM_MATH_ARGUMENT_ERROR;
   hipStream_t st = (hipStream_t)stream;
   bool ok = true;
   const T* dc = device_coeffs<T>(S->pCoeffs, S->numTaps, 5, st, &ok);
   if (!ok) { set_error(hipErrorOutOfMemory, "arm_fir_batch coeffs"); return ARM_MATH_ARGUMENT_ERROR; }
-  hipError_t e;
-  if constexpr (sizeof(T) == 4) e = fir_f32_launch((const float*)dc, S->numTaps, (const float*)d_src, (float*)d_dst, B, batch, (float*)d_hist, st);
-  else e = fir_q15_launch((const int16_t*)dc, S->numTaps, (const int16_t*)d_src, (int16_t*)d_dst, B, batch, (int16_t*)d_hist, st);
+  hipError_t e = fir_run(kind, dc, S->numTaps, d_src, d_dst, B, batch, d_hist, st);
   if (e != hipSuccess) { set_error(e, "arm_fir_batch"); return ARM_MATH_ARGUMENT_ERROR; }
   return ARM_MATH_SUCCESS;
 }
@@ -351,19 +349,45 @@ arm_status arm_fir_init_q15(arm_fir_instance_q15* S, uint16_t numTaps, const q15
   return ARM_MATH_SUCCESS;
 }
 
+void arm_fir_init_q31(arm_fir_instance_q31* S, uint16_t numTaps, const q31_t* pCoeffs, q31_t* pState,
+                      uint32_t blockSize) {
+  if (S) fir_init<int32_t>(S, numTaps, pCoeffs, pState, blockSize);
+}
+
 void arm_fir_f32(const arm_fir_instance_f32* S, const float32_t* pSrc, float32_t* pDst, uint32_t blockSize) {
-  fir_sync<float>(S, pSrc, pDst, blockSize);
+  fir_sync<float>(S, pSrc, pDst, blockSize, kFirF32);
 }
 void arm_fir_q15(const arm_fir_instance_q15* S, const q15_t* pSrc, q15_t* pDst, uint32_t blockSize) {
-  fir_sync<int16_t>(S, pSrc, pDst, blockSize);
+  fir_sync<int16_t>(S, pSrc, pDst, blockSize, kFirQ15);
+}
+void arm_fir_fast_q15(const arm_fir_instance_q15* S, const q15_t* pSrc, q15_t* pDst, uint32_t blockSize) {
+  fir_sync<int16_t>(S, pSrc, pDst, blockSize, kFirFastQ15);
+}
+void arm_fir_q31(const arm_fir_instance_q31* S, const q31_t* pSrc, q31_t* pDst, uint32_t blockSize) {
+  fir_sync<int32_t>(S, pSrc, pDst, blockSize, kFirQ31);
+}
+void arm_fir_fast_q31(const arm_fir_instance_q31* S, const q31_t* pSrc, q31_t* pDst, uint32_t blockSize) {
+  fir_sync<int32_t>(S, pSrc, pDst, blockSize, kFirFastQ31);
 }
 arm_status arm_fir_f32_batch(const arm_fir_instance_f32* S, const float32_t* d_src, float32_t* d_dst,
                              uint32_t blockSize, uint32_t batch, float32_t* d_hist, void* stream) {
-  return fir_batch<float>(S, d_src, d_dst, blockSize, batch, d_hist, stream);
+  return fir_batch<float>(S, d_src, d_dst, blockSize, batch, d_hist, stream, kFirF32);
 }
 arm_status arm_fir_q15_batch(const arm_fir_instance_q15* S, const q15_t* d_src, q15_t* d_dst, uint32_t blockSize,
                              uint32_t batch, q15_t* d_hist, void* stream) {
-  return fir_batch<int16_t>(S, d_src, d_dst, blockSize, batch, d_hist, stream);
+  return fir_batch<int16_t>(S, d_src, d_dst, blockSize, batch, d_hist, stream, kFirQ15);
+}
+arm_status arm_fir_fast_q15_batch(const arm_fir_instance_q15* S, const q15_t* d_src, q15_t* d_dst, uint32_t blockSize,
+                                  uint32_t batch, q15_t* d_hist, void* stream) {
+  return fir_batch<int16_t>(S, d_src, d_dst, blockSize, batch, d_hist, stream, kFirFastQ15);
+}
+arm_status arm_fir_q31_batch(const arm_fir_instance_q31* S, const q31_t* d_src, q31_t* d_dst, uint32_t blockSize,
+                             uint32_t batch, q31_t* d_hist, void* stream) {
+  return fir_batch<int32_t>(S, d_src, d_dst, blockSize, batch, d_hist, stream, kFirQ31);
+}
+arm_status arm_fir_fast_q31_batch(const arm_fir_instance_q31* S, const q31_t* d_src, q31_t* d_dst, uint32_t blockSize,
+                                  uint32_t batch, q31_t* d_hist, void* stream) {
+  return fir_batch<int32_t>(S, d_src, d_dst, blockSize, batch, d_hist, stream, kFirFastQ31);
 }
 
 arm_status arm_mat_mult_f32(const arm_matrix_instance_f32* pSrcA, const arm_matrix_instance_f32* pSrcB,

@@ -16,6 +16,8 @@
 #include "common.hpp"
 #include "kernels.hpp"
 
+#include <type_traits>
+
 #pragma clang fp contract(off)
 
 namespace mi355x {
@@ -252,6 +254,66 @@ __device__ __forceinline__ void fir_q15_wide(const uint32_t* lds, const uint32_t
 #ifndef MI355X_FIR_Q15_WAVES
 #define MI355X_FIR_Q15_WAVES 1   // minimum waves per SIMD the register allocation must allow
 #endif
+// arm_fir_fast_q15: mod-2^32 sum over all tap pairs with one accumulating v_dot2 each,
+// planes 0/1 hold the raw even / odd sample-pair words; 4-word quads read one block ahead.
+struct Q15FastRing { uint4 e[3], o[3]; };
+template <int S>
+__device__ __forceinline__ void q15f_fetch(Q15FastRing& r, const uint32_t* lds, int w) {
+  r.e[S] = *reinterpret_cast<const uint4*>(lds + w);
+  r.o[S] = *reinterpret_cast<const uint4*>(lds + kQ15W + w);
+}
+template <int P>
+__device__ __forceinline__ void q15f_block(Q15FastRing& r, const uint32_t* lds, int w_ahead, const uint4 c4,
+                                           int32_t (&A)[kFirR]) {
+  q15f_fetch<(P + 2) % 3>(r, lds, w_ahead);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const uint32_t c = lane_word(c4, u);
+#pragma unroll
+    for (int j = 0; j < kFirR / 2; ++j) {
+      const int i = u + j, s = i < 4 ? P : (P + 1) % 3, e = i & 3;
+      A[2 * j] = dot2(lane_word(r.e[s], e), c, A[2 * j]);
+      A[2 * j + 1] = dot2(lane_word(r.o[s], e), c, A[2 * j + 1]);
+    }
+  }
+}
+__device__ __forceinline__ void fir_q15_fast(const uint32_t* lds, const uint32_t* cw, int pairs, int wb,
+                                             int32_t (&A)[kFirR]) {
+#pragma unroll
+  for (int k = 0; k < kFirR; ++k) A[k] = 0;
+  const uint4* c4 = reinterpret_cast<const uint4*>(cw);
+  Q15FastRing r;
+  q15f_fetch<0>(r, lds, wb);
+  q15f_fetch<1>(r, lds, wb + 4);
+  int m = 0;
+  for (; m + 12 <= pairs; m += 12) {
+    q15f_block<0>(r, lds, wb + m + 8, c4[m / 4], A);
+    q15f_block<1>(r, lds, wb + m + 12, c4[m / 4 + 1], A);
+    q15f_block<2>(r, lds, wb + m + 16, c4[m / 4 + 2], A);
+  }
+  if (m + 4 <= pairs) {
+    q15f_block<0>(r, lds, wb + m + 8, c4[m / 4], A);
+    m += 4;
+    if (m + 4 <= pairs) {
+      q15f_block<1>(r, lds, wb + m + 8, c4[m / 4], A);
+      m += 4;
+    }
+  }
+  for (; m < pairs; ++m) {
+    const uint32_t c = cw[m];
+#pragma unroll
+    for (int j = 0; j < kFirR / 2; ++j) {
+      A[2 * j] = dot2(lds[wb + m + j], c, A[2 * j]);
+      A[2 * j + 1] = dot2(lds[kQ15W + wb + m + j], c, A[2 * j + 1]);
+    }
+  }
+}
+
+// FAST = arm_fir_fast_q15 (arm_fir_fast_q15.c): the accumulator is a q31_t fed by __SMLAD /
+// __SMLADX and plain int32 adds (none.h) -- every partial sum wraps mod 2^32, so the result
+// is the mod-2^32 sum of the products in ANY order: one accumulating v_dot2 per tap pair on
+// the raw sample-pair words (planes 0/1 = even/odd pairs), y = __SSAT(acc >> 15, 16).
+template <bool FAST>
 __global__ __launch_bounds__(kBlock, MI355X_FIR_Q15_WAVES) void fir_q15_kernel(const int16_t* __restrict__ coeffs, int T,
                                                          const int16_t* __restrict__ src, int16_t* __restrict__ dst,
                                                          uint32_t B, const int16_t* __restrict__ hist_in,
@@ -281,10 +343,15 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_Q15_WAVES) void fir_q15_kernel(c
     const int j = threadIdx.x + k * kBlock;
     if (j < words) {
       const uint32_t e = x[k][0] | (x[k][1] << 16), o = x[k][1] | (x[k][2] << 16);
-      lds[j] = hi8(e);
-      lds[kQ15W + j] = lo8(e);
-      lds[2 * kQ15W + j] = hi8(o);
-      lds[3 * kQ15W + j] = lo8(o);
+      if constexpr (FAST) {
+        lds[j] = e;
+        lds[kQ15W + j] = o;
+      } else {
+        lds[j] = hi8(e);
+        lds[kQ15W + j] = lo8(e);
+        lds[2 * kQ15W + j] = hi8(o);
+        lds[3 * kQ15W + j] = lo8(o);
+      }
     }
   }
   int wrap = 0;
@@ -298,7 +365,12 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_Q15_WAVES) void fir_q15_kernel(c
   const int base = threadIdx.x * kFirR;
   if (base >= it.count) return;
   int64_t acc[kFirR];
-  if (split && pairs <= kQ15Chunk) {
+  if constexpr (FAST) {
+    int32_t a32[kFirR];
+    fir_q15_fast(lds, cw, pairs, base >> 1, a32);
+#pragma unroll
+    for (int r = 0; r < kFirR; ++r) acc[r] = a32[r];  // (acc >> 15) of the int32 sum below
+  } else if (split && pairs <= kQ15Chunk) {
     fir_q15_split<false>(lds, cw, pairs, base >> 1, acc);
   } else if (split) {
     fir_q15_split<true>(lds, cw, pairs, base >> 1, acc);
@@ -319,6 +391,77 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_Q15_WAVES) void fir_q15_kernel(c
   }
 }
 
+// ---------------------------------------------------------------- q31 (exact and fast)
+// arm_fir_q31 (arm_fir_q31.c, LOOPUNROLL by 3 and tail alike): q63 accumulator of exact
+// q31 x q31 products, y = (q31)(acc >> 31).  arm_fir_fast_q31 (arm_fir_fast_q31.c):
+// multAcc_32x32_keep32_R(acc, x, c) = (q31)(((q63)acc << 32) + x*c + 2^31) >> 32)
+// = acc + ((x*c + 2^31) >> 32) mod 2^32 (acc << 32 has a zero low word), y = (q31)(acc << 1).
+// Both accumulators only ever wrap (gcc x86-64 semantics of the reference build): the
+// results are mod-2^64 / mod-2^32 sums, the same in any order.  Structure as fir_f32.
+template <bool FAST>
+__global__ __launch_bounds__(kBlock) void fir_q31_kernel(const int32_t* __restrict__ coeffs, int T,
+                                                         const int32_t* __restrict__ src, int32_t* __restrict__ dst,
+                                                         uint32_t B, const int32_t* __restrict__ hist_in,
+                                                         uint32_t nchunks) {
+  __shared__ int32_t win[(kFirChunk + kFirMaxTaps) * 9 / 8 + 32];
+  const int T1 = T - 1;
+  const FirItem it = fir_item(blockIdx.x, nchunks, B, T1);
+  int32_t pre[kFirPre];
+#pragma unroll
+  for (int k = 0; k < kFirPre; ++k) pre[k] = fir_sample(hist_in, src, it, B, T1, (int)threadIdx.x + k * kBlock);
+#pragma unroll
+  for (int k = 0; k < kFirPre; ++k) {
+    const int j = threadIdx.x + k * kBlock;
+    if (j < it.total) win[padx(j)] = pre[k];
+  }
+  __syncthreads();
+  const int base = threadIdx.x * kFirR;
+  if (base >= it.count) return;
+  using Acc = typename std::conditional<FAST, uint32_t, uint64_t>::type;
+  Acc acc[kFirR];
+  int32_t w[kFirR];
+  auto mac = [](Acc a, int32_t x, int32_t c) -> Acc {
+    const int64_t p = (int64_t)x * c;
+    if constexpr (FAST) return a + (uint32_t)((p + 0x80000000LL) >> 32);
+    else return a + (uint64_t)p;
+  };
+#pragma unroll
+  for (int r = 0; r < kFirR; ++r) { acc[r] = 0; w[r] = win[padx(base + r)]; }
+  int k = 0;
+  for (; k + kFirR <= T; k += kFirR) {
+#pragma unroll
+    for (int u = 0; u < kFirR; ++u) {
+      const int32_t c = coeffs[k + u];
+#pragma unroll
+      for (int r = 0; r < kFirR; ++r) acc[r] = mac(acc[r], w[(r + u) % kFirR], c);
+      w[u] = win[padx(base + k + u + kFirR)];
+    }
+  }
+  for (; k < T; ++k) {
+    const int32_t c = coeffs[k];
+#pragma unroll
+    for (int r = 0; r < kFirR; ++r) acc[r] = mac(acc[r], w[r], c);
+#pragma unroll
+    for (int r = 0; r < kFirR - 1; ++r) w[r] = w[r + 1];
+    w[kFirR - 1] = win[padx(base + kFirR + k)];
+  }
+  int32_t y[kFirR];
+#pragma unroll
+  for (int r = 0; r < kFirR; ++r) {
+    if constexpr (FAST) y[r] = (int32_t)(acc[r] << 1);
+    else y[r] = (int32_t)((int64_t)acc[r] >> 31);
+  }
+  int32_t* o = dst + (uint64_t)it.f * B + it.n0 + base;
+  if ((B & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + kFirR <= it.count) {
+    reinterpret_cast<int4*>(o)[0] = make_int4(y[0], y[1], y[2], y[3]);
+    reinterpret_cast<int4*>(o)[1] = make_int4(y[4], y[5], y[6], y[7]);
+  } else {
+#pragma unroll
+    for (int r = 0; r < kFirR; ++r)
+      if (base + r < it.count) o[r] = y[r];
+  }
+}
+
 // new history = last T-1 samples of [hist ; src]  (arm_fir_f32.c:1242-1278)
 template <typename T>
 __global__ void fir_hist_kernel(const T* __restrict__ src, T* __restrict__ hist, const T* __restrict__ hist_in,
@@ -332,7 +475,7 @@ __global__ void fir_hist_kernel(const T* __restrict__ src, T* __restrict__ hist,
 }
 
 template <typename T>
-static hipError_t fir_launch(const T* coeffs, int T_, const T* src, T* dst, uint32_t B, uint32_t batch,
+static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T* dst, uint32_t B, uint32_t batch,
                              T* hist, hipStream_t st) {
   if (batch == 0 || B == 0) return hipSuccess;
   if (T_ < 1 || T_ > kFirMaxTaps) return hipErrorInvalidValue;
@@ -352,13 +495,25 @@ static hipError_t fir_launch(const T* coeffs, int T_, const T* src, T* dst, uint
   const uint64_t items64 = (uint64_t)nchunks * batch;
   if (items64 > 0xFFFFFFFFull) return hipErrorInvalidValue;
   const uint32_t items = (uint32_t)items64;
-  if constexpr (sizeof(T) == 4) {
-    const int grid = persistent_grid((const void*)fir_f32_kernel, kBlock, 0, items, 4);
-    hipLaunchKernelGGL(fir_f32_kernel, dim3(grid), dim3(kBlock), 0, st, (const float*)coeffs, T_, (const float*)src,
-                       (float*)dst, B, (const float*)hist_in, nchunks, items);
-  } else {
-    hipLaunchKernelGGL(fir_q15_kernel, dim3(items), dim3(kBlock), 0, st, (const int16_t*)coeffs, T_,
-                       (const int16_t*)src, (int16_t*)dst, B, (const int16_t*)hist_in, nchunks);
+  switch (kind) {
+    case kFirF32: {
+      const int grid = persistent_grid((const void*)fir_f32_kernel, kBlock, 0, items, 4);
+      hipLaunchKernelGGL(fir_f32_kernel, dim3(grid), dim3(kBlock), 0, st, (const float*)coeffs, T_,
+                         (const float*)src, (float*)dst, B, (const float*)hist_in, nchunks, items);
+      break;
+    }
+    case kFirQ15:
+    case kFirFastQ15: {
+      auto k = kind == kFirQ15 ? fir_q15_kernel<false> : fir_q15_kernel<true>;
+      hipLaunchKernelGGL(k, dim3(items), dim3(kBlock), 0, st, (const int16_t*)coeffs, T_, (const int16_t*)src,
+                         (int16_t*)dst, B, (const int16_t*)hist_in, nchunks);
+      break;
+    }
+    default: {
+      auto k = kind == kFirQ31 ? fir_q31_kernel<false> : fir_q31_kernel<true>;
+      hipLaunchKernelGGL(k, dim3(items), dim3(kBlock), 0, st, (const int32_t*)coeffs, T_, (const int32_t*)src,
+                         (int32_t*)dst, B, (const int32_t*)hist_in, nchunks);
+    }
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -373,13 +528,23 @@ static hipError_t fir_launch(const T* coeffs, int T_, const T* src, T* dst, uint
   return e;
 }
 
-hipError_t fir_f32_launch(const float* coeffs, int num_taps, const float* src, float* dst, uint32_t block_size,
-                          uint32_t batch, float* hist, hipStream_t st) {
-  return fir_launch<float>(coeffs, num_taps, src, dst, block_size, batch, hist, st);
-}
-hipError_t fir_q15_launch(const int16_t* coeffs, int num_taps, const int16_t* src, int16_t* dst,
-                          uint32_t block_size, uint32_t batch, int16_t* hist, hipStream_t st) {
-  return fir_launch<int16_t>(coeffs, num_taps, src, dst, block_size, batch, hist, st);
+hipError_t fir_run(int kind, const void* coeffs, int num_taps, const void* src, void* dst, uint32_t block_size,
+                   uint32_t batch, void* hist, hipStream_t st) {
+  switch (kind) {
+    case kFirF32:
+      return fir_launch<float>(kind, (const float*)coeffs, num_taps, (const float*)src, (float*)dst, block_size,
+                               batch, (float*)hist, st);
+    case kFirQ15:
+    case kFirFastQ15:
+      return fir_launch<int16_t>(kind, (const int16_t*)coeffs, num_taps, (const int16_t*)src, (int16_t*)dst,
+                                 block_size, batch, (int16_t*)hist, st);
+    case kFirQ31:
+    case kFirFastQ31:
+      return fir_launch<int32_t>(kind, (const int32_t*)coeffs, num_taps, (const int32_t*)src, (int32_t*)dst,
+                                 block_size, batch, (int32_t*)hist, st);
+    default:
+      return hipErrorInvalidValue;
+  }
 }
 
 }  // namespace mi355x

@@ -41,12 +41,12 @@ hipError_t rfft_f32_stage_launch(int n_real, const float* p, float* out, uint32_
 hipError_t rfft_f32_merge_launch(int n_real, const float* p, float* out, uint32_t batch,
                                  const float* tw_rfft, hipStream_t st);
 
-// FIR: `batch` independent filters sharing one coefficient set.
-// hist: [batch][numTaps-1] streaming state (read, then overwritten with the new tail).
-hipError_t fir_f32_launch(const float* coeffs, int num_taps, const float* src, float* dst,
-                          uint32_t block_size, uint32_t batch, float* hist, hipStream_t st);
-hipError_t fir_q15_launch(const int16_t* coeffs, int num_taps, const int16_t* src, int16_t* dst,
-                          uint32_t block_size, uint32_t batch, int16_t* hist, hipStream_t st);
+// FIR: `batch` independent filters sharing one coefficient set, any of the five reference
+// variants (kind).  hist: [batch][numTaps-1] streaming state (read, then overwritten with
+// the new tail).  Element type: f32 float, q15/fast_q15 int16, q31/fast_q31 int32.
+enum FirKind { kFirF32 = 0, kFirQ15 = 1, kFirQ31 = 2, kFirFastQ15 = 3, kFirFastQ31 = 4 };
+hipError_t fir_run(int kind, const void* coeffs, int num_taps, const void* src, void* dst, uint32_t block_size,
+                   uint32_t batch, void* hist, hipStream_t st);
 
 // MFCC f32 around the batched RFFT (mfcc_f32.hip): frame normalisation + window, then the
 // spectrum -> Mel -> log -> DCT tail.  post needs mfcc_f32_post_lds(n, nb_mel) bytes of LDS.

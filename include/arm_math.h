@@ -88,12 +88,18 @@ typedef struct {
   arm_rfft_fast_instance_f32 rfft;
 } arm_mfcc_instance_f32;
 
-/* ---- FIR instances: Include/dsp/filtering_functions.h:66-71, 86-91 --------------- */
+/* ---- FIR instances: Include/dsp/filtering_functions.h:66-71, 76-81, 86-91 -------- */
 typedef struct {
         uint16_t   numTaps;
         q15_t     *pState;
   const q15_t     *pCoeffs;
 } arm_fir_instance_q15;
+
+typedef struct {
+        uint16_t   numTaps;
+        q31_t     *pState;
+  const q31_t     *pCoeffs;
+} arm_fir_instance_q31;
 
 typedef struct {
         uint16_t   numTaps;
@@ -241,6 +247,21 @@ arm_status arm_fir_init_q15(arm_fir_instance_q15 *S, uint16_t numTaps,
                             const q15_t *pCoeffs, q15_t *pState, uint32_t blockSize);
 void arm_fir_q15(const arm_fir_instance_q15 *S, const q15_t *pSrc,
                  q15_t *pDst, uint32_t blockSize);
+
+/* Further FIR variants.  Prototypes: Include/dsp/filtering_functions.h
+ * :154-158 (fast q15), :189-193 (q31), :202-206 (fast q31), :219-224 (init q31).
+ * Reference bodies: Source/FilteringFunctions/arm_fir_fast_q15.c (q31_t accumulator, __SMLAD:
+ * mod-2^32 sum, __SSAT(acc >> 15, 16)), arm_fir_q31.c (q63 sum of exact products,
+ * (q31)(acc >> 31)), arm_fir_fast_q31.c (multAcc_32x32_keep32_R per tap, (q31)(acc << 1)),
+ * arm_fir_init_q31.c.  numTaps must be even for the q15 variants, as in the reference. */
+void arm_fir_init_q31(arm_fir_instance_q31 *S, uint16_t numTaps,
+                      const q31_t *pCoeffs, q31_t *pState, uint32_t blockSize);
+void arm_fir_q31(const arm_fir_instance_q31 *S, const q31_t *pSrc,
+                 q31_t *pDst, uint32_t blockSize);
+void arm_fir_fast_q31(const arm_fir_instance_q31 *S, const q31_t *pSrc,
+                      q31_t *pDst, uint32_t blockSize);
+void arm_fir_fast_q15(const arm_fir_instance_q15 *S, const q15_t *pSrc,
+                      q15_t *pDst, uint32_t blockSize);
 
 /* ===================================================================================
  * Matrix multiply, f32.  Prototypes: Include/dsp/matrix_functions.h:341-344,630-634

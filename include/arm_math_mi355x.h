@@ -59,6 +59,12 @@ arm_status arm_fir_f32_batch(const arm_fir_instance_f32 *S, const float32_t *d_s
                              uint32_t blockSize, uint32_t batch, float32_t *d_hist, void *stream);
 arm_status arm_fir_q15_batch(const arm_fir_instance_q15 *S, const q15_t *d_src, q15_t *d_dst,
                              uint32_t blockSize, uint32_t batch, q15_t *d_hist, void *stream);
+arm_status arm_fir_fast_q15_batch(const arm_fir_instance_q15 *S, const q15_t *d_src, q15_t *d_dst,
+                                  uint32_t blockSize, uint32_t batch, q15_t *d_hist, void *stream);
+arm_status arm_fir_q31_batch(const arm_fir_instance_q31 *S, const q31_t *d_src, q31_t *d_dst,
+                             uint32_t blockSize, uint32_t batch, q31_t *d_hist, void *stream);
+arm_status arm_fir_fast_q31_batch(const arm_fir_instance_q31 *S, const q31_t *d_src, q31_t *d_dst,
+                                  uint32_t blockSize, uint32_t batch, q31_t *d_hist, void *stream);
 
 /* Row-major C[b] = A[b] * B[b] for `batch` contiguous (numRows x numCols) matrices with
  * the shapes of the three instances (their pData must be device pointers to the first

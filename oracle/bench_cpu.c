@@ -32,6 +32,8 @@ arm_status oracle_arm_cfft_init_q31(arm_cfft_instance_q31 *S, uint16_t n);
 arm_status oracle_arm_cfft_init_q15(arm_cfft_instance_q15 *S, uint16_t n);
 void oracle_arm_fir_init_f32(arm_fir_instance_f32 *S, uint16_t numTaps, const float *pCoeffs, float *pState,
                              uint32_t blockSize);
+void oracle_arm_fir_init_q31(arm_fir_instance_q31 *S, uint16_t numTaps, const int32_t *pCoeffs, int32_t *pState,
+                             uint32_t blockSize);
 arm_status oracle_arm_fir_init_q15(arm_fir_instance_q15 *S, uint16_t numTaps, const int16_t *pCoeffs,
                                    int16_t *pState, uint32_t blockSize);
 void oracle_arm_mat_init_f32(arm_matrix_instance_f32 *S, uint16_t r, uint16_t c, float *p);
@@ -86,7 +88,20 @@ static void *worker(void *arg) {
     F(arm_fir_init_f32)(&S, (uint16_t)taps, c, st, block);
     do { F(arm_fir_f32)(&S, in, out, block); samples += block; } while (now() - t0 < j->seconds);
     free(c); free(st); free(in); free(out);
-  } else if (!strcmp(j->wl, "fir_q15")) {
+  } else if (!strcmp(j->wl, "fir_q31") || !strcmp(j->wl, "fir_fast_q31")) {
+    const int taps = j->n, block = 4096, fast = !strcmp(j->wl, "fir_fast_q31");
+    int32_t *c = malloc(sizeof(int32_t) * taps), *st = malloc(sizeof(int32_t) * (taps + block - 1));
+    int32_t *in = malloc(sizeof(int32_t) * block), *out = malloc(sizeof(int32_t) * block);
+    for (int i = 0; i < taps; ++i) c[i] = (int32_t)(sm(&seed) >> 36);
+    for (int i = 0; i < block; ++i) in[i] = (int32_t)sm(&seed);
+    arm_fir_instance_q31 S;
+    F(arm_fir_init_q31)(&S, (uint16_t)taps, c, st, block);
+    do {
+      if (fast) F(arm_fir_fast_q31)(&S, in, out, block); else F(arm_fir_q31)(&S, in, out, block);
+      samples += block;
+    } while (now() - t0 < j->seconds);
+    free(c); free(st); free(in); free(out);
+  } else if (!strcmp(j->wl, "fir_q15") || !strcmp(j->wl, "fir_fast_q15")) {
     const int taps = j->n, block = 4096;
     int16_t *c = malloc(sizeof(int16_t) * taps), *st = malloc(sizeof(int16_t) * (taps + block - 1));
     int16_t *in = malloc(sizeof(int16_t) * block), *out = malloc(sizeof(int16_t) * block);
@@ -94,7 +109,11 @@ static void *worker(void *arg) {
     for (int i = 0; i < block; ++i) in[i] = (int16_t)(sm(&seed) >> 48);
     arm_fir_instance_q15 S;
     F(arm_fir_init_q15)(&S, (uint16_t)taps, c, st, block);
-    do { F(arm_fir_q15)(&S, in, out, block); samples += block; } while (now() - t0 < j->seconds);
+    const int fast = !strcmp(j->wl, "fir_fast_q15");
+    do {
+      if (fast) F(arm_fir_fast_q15)(&S, in, out, block); else F(arm_fir_q15)(&S, in, out, block);
+      samples += block;
+    } while (now() - t0 < j->seconds);
     free(c); free(st); free(in); free(out);
   } else if (!strcmp(j->wl, "mfcc_f32")) {
     const int n = j->n, nm = 20, nd = 13;

@@ -11,6 +11,9 @@ void oracle_arm_cfft_q15(const arm_cfft_instance_q15 *S, int16_t *p1, uint8_t if
 void oracle_arm_rfft_fast_f32(const arm_rfft_fast_instance_f32 *S, float *p, float *pOut, uint8_t ifftFlag);
 void oracle_arm_fir_f32(const arm_fir_instance_f32 *S, const float *pSrc, float *pDst, uint32_t blockSize);
 void oracle_arm_fir_q15(const arm_fir_instance_q15 *S, const int16_t *pSrc, int16_t *pDst, uint32_t blockSize);
+void oracle_arm_fir_fast_q15(const arm_fir_instance_q15 *S, const int16_t *pSrc, int16_t *pDst, uint32_t blockSize);
+void oracle_arm_fir_q31(const arm_fir_instance_q31 *S, const int32_t *pSrc, int32_t *pDst, uint32_t blockSize);
+void oracle_arm_fir_fast_q31(const arm_fir_instance_q31 *S, const int32_t *pSrc, int32_t *pDst, uint32_t blockSize);
 arm_status oracle_arm_mat_mult_f32(const arm_matrix_instance_f32 *A, const arm_matrix_instance_f32 *B,
                                    arm_matrix_instance_f32 *C);
 arm_status oracle_arm_mfcc_init_f32(arm_mfcc_instance_f32 *S, uint32_t fftLen, uint32_t nbMelFilters,

@@ -55,6 +55,54 @@ void oracle_arm_fir_q15(const arm_fir_instance_q15 *S, const int16_t *pSrc, int1
   memmove(s, s + blockSize, sizeof(int16_t) * (taps - 1));
 }
 
+/* arm_fir_fast_q15.c: q31_t accumulator fed by __SMLAD/__SMLADX and int32 adds (none.h) —
+ * every partial sum wraps mod 2^32, pairs or not; y = __SSAT(acc >> 15, 16). */
+void oracle_arm_fir_fast_q15(const arm_fir_instance_q15 *S, const int16_t *pSrc, int16_t *pDst, uint32_t blockSize) {
+  const uint32_t taps = S->numTaps, used = taps & ~1u;
+  int16_t *s = S->pState;
+  const int16_t *c = S->pCoeffs;
+  memcpy(s + taps - 1, pSrc, sizeof(int16_t) * blockSize);
+  for (uint32_t n = 0; n < blockSize; ++n) {
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < used; ++k) acc += (uint32_t)((int32_t)s[n + k] * c[k]);
+    pDst[n] = oracle_sat_q15((int32_t)acc >> 15);
+  }
+  memmove(s, s + blockSize, sizeof(int16_t) * (taps - 1));
+}
+
+/* arm_fir_q31.c: q63 accumulator of exact products (wrapping, as gcc x86-64 adds do),
+ * y = (q31)(acc >> 31). */
+void oracle_arm_fir_q31(const arm_fir_instance_q31 *S, const int32_t *pSrc, int32_t *pDst, uint32_t blockSize) {
+  const uint32_t taps = S->numTaps;
+  int32_t *s = S->pState;
+  const int32_t *c = S->pCoeffs;
+  memcpy(s + taps - 1, pSrc, sizeof(int32_t) * blockSize);
+  for (uint32_t n = 0; n < blockSize; ++n) {
+    uint64_t acc = 0;
+    for (uint32_t k = 0; k < taps; ++k) acc += (uint64_t)((int64_t)s[n + k] * c[k]);
+    pDst[n] = (int32_t)((int64_t)acc >> 31);
+  }
+  memmove(s, s + blockSize, sizeof(int32_t) * (taps - 1));
+}
+
+/* arm_fir_fast_q31.c: multAcc_32x32_keep32_R (none.h:185-186) per tap, taps in order:
+ * acc = (q31)((((q63)acc << 32) + x*c + 0x80000000) >> 32); y = (q31)(acc << 1). */
+void oracle_arm_fir_fast_q31(const arm_fir_instance_q31 *S, const int32_t *pSrc, int32_t *pDst, uint32_t blockSize) {
+  const uint32_t taps = S->numTaps;
+  int32_t *s = S->pState;
+  const int32_t *c = S->pCoeffs;
+  memcpy(s + taps - 1, pSrc, sizeof(int32_t) * blockSize);
+  for (uint32_t n = 0; n < blockSize; ++n) {
+    int32_t acc = 0;
+    for (uint32_t k = 0; k < taps; ++k) {
+      const uint64_t wide = ((uint64_t)(int64_t)acc << 32) + (uint64_t)((int64_t)s[n + k] * c[k]) + 0x80000000ull;
+      acc = (int32_t)(uint32_t)((int64_t)wide >> 32);
+    }
+    pDst[n] = (int32_t)((uint32_t)acc << 1);
+  }
+  memmove(s, s + blockSize, sizeof(int32_t) * (taps - 1));
+}
+
 arm_status oracle_arm_mat_mult_f32(const arm_matrix_instance_f32 *A, const arm_matrix_instance_f32 *B,
                                    arm_matrix_instance_f32 *Cm) {
   const uint32_t M = A->numRows, K = A->numCols, N = B->numCols;

@@ -94,6 +94,11 @@ arm_status oracle_arm_fir_init_q15(arm_fir_instance_q15 *S, uint16_t numTaps, co
   memset(pState, 0, sizeof(int16_t) * ((size_t)numTaps + blockSize - 1));
   return ARM_MATH_SUCCESS;
 }
+void oracle_arm_fir_init_q31(arm_fir_instance_q31 *S, uint16_t numTaps, const int32_t *pCoeffs, int32_t *pState,
+                             uint32_t blockSize) {
+  S->numTaps = numTaps; S->pCoeffs = pCoeffs; S->pState = pState;
+  memset(pState, 0, sizeof(int32_t) * ((size_t)numTaps + blockSize - 1));
+}
 void oracle_arm_mat_init_f32(arm_matrix_instance_f32 *S, uint16_t r, uint16_t c, float *p) {
   S->numRows = r; S->numCols = c; S->pData = p;
 }

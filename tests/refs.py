@@ -83,13 +83,15 @@ class Host:
 
     def fir(self, kind, coeffs, blocks):
         """Stream `blocks` (list of 1-D arrays, each <= the block size) through one filter;
-        returns (outputs, final state buffer)."""
-        dt = np.float32 if kind == "f32" else np.int16
-        inst = _abi.arm_fir_instance_f32() if kind == "f32" else _abi.arm_fir_instance_q15()
+        returns (outputs, final state buffer).  kind: f32, q15, q31, fast_q15, fast_q31."""
+        base = kind[-3:]
+        dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32}[base]
+        inst = {"f32": _abi.arm_fir_instance_f32, "q15": _abi.arm_fir_instance_q15,
+                "q31": _abi.arm_fir_instance_q31}[base]()
         c = np.ascontiguousarray(coeffs, dtype=dt)
         bs = max(len(b) for b in blocks)
         state = np.zeros(len(c) + bs - 1, dtype=dt)
-        self.fn(f"arm_fir_init_{kind}")(C.byref(inst), len(c), c.ctypes.data, state.ctypes.data, bs)
+        self.fn(f"arm_fir_init_{base}")(C.byref(inst), len(c), c.ctypes.data, state.ctypes.data, bs)
         outs = []
         for b in blocks:
             b = np.ascontiguousarray(b, dtype=dt)

@@ -46,10 +46,11 @@ def test_rfft_dropin(dsp, torch_gpu, ref, n):
 def _fir_batched(dsp, torch, kind, coeffs, blocks_per_filter):
     """blocks_per_filter: [batch][calls] arrays; runs the batched API call by call."""
     import ctypes as C
-    dt = np.float32 if kind == "f32" else np.int16
+    base = kind[-3:]
+    dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32}[base]
     batch, calls = len(blocks_per_filter), len(blocks_per_filter[0])
     c = np.ascontiguousarray(coeffs, dtype=dt)
-    S = dsp.arm_fir_instance_f32() if kind == "f32" else dsp.arm_fir_instance_q15()
+    S = {"f32": dsp.arm_fir_instance_f32, "q15": dsp.arm_fir_instance_q15, "q31": dsp.arm_fir_instance_q31}[base]()
     S.numTaps = len(c)
     dc = torch.from_numpy(c.copy()).cuda()
     S.pCoeffs = C.cast(dc.data_ptr(), S._fields_[2][1])
@@ -58,19 +59,22 @@ def _fir_batched(dsp, torch, kind, coeffs, blocks_per_filter):
     for k in range(calls):
         src = torch.from_numpy(np.stack([blocks_per_filter[f][k] for f in range(batch)]).astype(dt)).cuda()
         dst = torch.empty_like(src)
-        dsp.fir_batch(S, src, dst, hist, q15=(kind == "q15"))
+        dsp.fir_batch(S, src, dst, hist, kind=kind)
         outs.append(dst.cpu().numpy())
     torch.cuda.synchronize()
     return outs, hist.cpu().numpy()
 
 
-@pytest.mark.parametrize("kind", ["f32", "q15"])
+FIR_KINDS = ["f32", "q15", "q31", "fast_q15", "fast_q31"]
+
+
+@pytest.mark.parametrize("kind", FIR_KINDS)
 @pytest.mark.parametrize("taps,block", [(128, 4096), (29, 32), (2, 7), (64, 100), (130, 2049), (1, 64),
                                         (6, 50), (240, 1000), (242, 777), (256, 4100), (1024, 3000), (518, 2048)])
 def test_fir_batch_bitexact_two_calls(dsp, torch_gpu, ref, kind, taps, block):
     """Each filter runs two consecutive blocks: the state carry must make them equal one
     long call (FIRF32.cpp:116-124 does the same two-call split)."""
-    if kind == "q15" and taps % 2:
+    if kind.endswith("q15") and taps % 2:
         pytest.skip("q15 FIR requires an even numTaps (arm_fir_init_q15.c:95-106)")
     rng = np.random.default_rng(taps * 7 + block)
     batch = 5
@@ -78,8 +82,10 @@ def test_fir_batch_bitexact_two_calls(dsp, torch_gpu, ref, kind, taps, block):
         coeffs = (rng.standard_normal(taps) / np.sqrt(taps)).astype(np.float32)
         blocks = [[rng.uniform(-1, 1, block).astype(np.float32) for _ in range(2)] for _ in range(batch)]
     else:
-        coeffs = rng.integers(-32768, 32767, taps, endpoint=True).astype(np.int16)
-        blocks = [[rng.integers(-32768, 32767, block, endpoint=True).astype(np.int16) for _ in range(2)]
+        bits, dt = (15, np.int16) if kind.endswith("q15") else (31, np.int32)
+        lo, hi = -(1 << bits), (1 << bits) - 1
+        coeffs = rng.integers(lo, hi, taps, endpoint=True).astype(dt)
+        blocks = [[rng.integers(lo, hi, block, endpoint=True).astype(dt) for _ in range(2)]
                   for _ in range(batch)]
     got, hist = _fir_batched(dsp, torch_gpu, kind, coeffs, blocks)
     for f in range(batch):
@@ -131,6 +137,33 @@ def test_fir_q15_wrapping_pair_random(dsp, torch_gpu, ref, taps):
     got, _ = _fir_batched(dsp, torch_gpu, "q15", c, [[x]])
     want, _ = ref.fir("q15", c, [x])
     assert got[0][0].tobytes() == want[0].tobytes()
+
+
+@pytest.mark.parametrize("kind,word", [("q31", -(1 << 31)), ("fast_q31", -(1 << 31)), ("fast_q15", -32768),
+                                       ("q31", (1 << 31) - 1), ("fast_q31", (1 << 31) - 1)])
+def test_fir_extreme_words(dsp, torch_gpu, ref, kind, word):
+    """All-extreme samples and taps: the q63 / q31 accumulators wrap exactly as the
+    reference build's do."""
+    dt = np.int16 if kind.endswith("q15") else np.int32
+    coeffs = np.full(6, word, dtype=dt)
+    blocks = [[np.full(4099, word, dtype=dt)]]
+    got, _ = _fir_batched(dsp, torch_gpu, kind, coeffs, blocks)
+    want, _ = ref.fir(kind, coeffs, blocks[0])
+    assert got[0][0].tobytes() == want[0].tobytes()
+
+
+@pytest.mark.parametrize("kind", ["q31", "fast_q31", "fast_q15"])
+def test_fir_dropin_state_fixed_variants(dsp, torch_gpu, ref, kind):
+    rng = np.random.default_rng(11)
+    taps, block = 32, 256
+    bits, dt = (15, np.int16) if kind.endswith("q15") else (31, np.int32)
+    coeffs = rng.integers(-(1 << bits), (1 << bits) - 1, taps).astype(dt)
+    blocks = [rng.integers(-(1 << bits), (1 << bits) - 1, block).astype(dt) for _ in range(3)]
+    f = dsp.FirFastQ15(coeffs, block) if kind == "fast_q15" else dsp.FirQ31(coeffs, block, fast=kind == "fast_q31")
+    want, state = ref.fir(kind, coeffs, blocks)
+    for b, w in zip(blocks, want):
+        assert f(b).tobytes() == w.tobytes()
+    assert f.state.tobytes() == state.tobytes()
 
 
 @pytest.mark.parametrize("kind", ["f32", "q15"])

@@ -43,19 +43,29 @@ def test_rfft_oracle_equals_reference(oracle, ref, n):
             assert a.tobytes() == b.tobytes() and pa.tobytes() == pb.tobytes()
 
 
-@pytest.mark.parametrize("kind", ["f32", "q15"])
+def fir_case(kind, taps, blocks, seed):
+    """Coefficients and blocks for a FIR kind: f32 normal/uniform, fixed point full range."""
+    rng = np.random.default_rng(seed)
+    if kind == "f32":
+        return (rng.standard_normal(taps).astype(np.float32),
+                [rng.uniform(-1, 1, b).astype(np.float32) for b in blocks])
+    bits = 15 if kind.endswith("q15") else 31
+    dt = np.int16 if bits == 15 else np.int32
+    lo, hi = -(1 << bits), (1 << bits) - 1
+    return (rng.integers(lo, hi, taps, endpoint=True).astype(dt),
+            [rng.integers(lo, hi, b, endpoint=True).astype(dt) for b in blocks])
+
+
+FIR_KINDS = ["f32", "q15", "q31", "fast_q15", "fast_q31"]
+
+
+@pytest.mark.parametrize("kind", FIR_KINDS)
 @pytest.mark.parametrize("taps,blocks", [(128, [4096, 4096]), (2, [1, 3, 5]), (29, [32] * 10), (64, [7, 100, 33]),
                                          (1, [16, 16]), (130, [2049, 3])])
 def test_fir_oracle_equals_reference(oracle, ref, kind, taps, blocks):
-    if kind == "q15" and taps % 2:
+    if kind.endswith("q15") and taps % 2:
         pytest.skip("q15: even numTaps only")
-    rng = np.random.default_rng(taps)
-    if kind == "f32":
-        c = rng.standard_normal(taps).astype(np.float32)
-        xs = [rng.uniform(-1, 1, b).astype(np.float32) for b in blocks]
-    else:
-        c = rng.integers(-32768, 32767, taps, endpoint=True).astype(np.int16)
-        xs = [rng.integers(-32768, 32767, b, endpoint=True).astype(np.int16) for b in blocks]
+    c, xs = fir_case(kind, taps, blocks, taps)
     (ya, sa), (yb, sb) = oracle.fir(kind, c, xs), ref.fir(kind, c, xs)
     for u, v in zip(ya, yb):
         assert u.tobytes() == v.tobytes()
@@ -68,6 +78,17 @@ def test_fir_q15_all_min_wraps_like_reference(oracle, ref):
     (ya, _), (yb, _) = oracle.fir("q15", c, x), ref.fir("q15", c, x)
     assert ya[0].tobytes() == yb[0].tobytes()
     assert len(np.unique(ya[0])) > 1      # the grouped outputs wrap, the tail does not
+
+
+@pytest.mark.parametrize("kind,word", [("q31", -(1 << 31)), ("fast_q31", -(1 << 31)), ("fast_q15", -32768),
+                                       ("q31", (1 << 31) - 1), ("fast_q31", (1 << 31) - 1)])
+def test_fir_extreme_words_wrap_like_reference(oracle, ref, kind, word):
+    """All-extreme samples and taps: the q63 / q31 accumulators wrap (gcc x86-64 adds)."""
+    dt = np.int16 if kind.endswith("q15") else np.int32
+    c = np.full(6, word, dtype=dt)
+    x = [np.full(37, word, dtype=dt)]
+    (ya, _), (yb, _) = oracle.fir(kind, c, x), ref.fir(kind, c, x)
+    assert ya[0].tobytes() == yb[0].tobytes()
 
 
 @pytest.mark.parametrize("m,k,n", [(1, 1, 1), (7, 13, 5), (40, 40, 40), (64, 3, 65)])
