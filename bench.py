@@ -49,6 +49,8 @@ WORKLOADS = {
     "fir_fast_q31": ("fir_fast_q31", 128, 1 << 16, 8),
     "mat_mult_f32": ("mat", 1024, 256, None),
     "mfcc_f32": ("mfcc", 1024, 1 << 18, 4),
+    "mat_mult_q15": ("matq15", 1024, 64, None),
+    "mat_mult_q31": ("matq31", 1024, 64, None),
 }
 
 
@@ -109,14 +111,15 @@ def cpu_baseline(workload, n):
     wl = {"cfft_f32_1024": "cfft_f32", "cfft_q31_4096": "cfft_q31", "cfft_q15_4096": "cfft_q15",
           "fir_f32": "fir_f32", "fir_q15": "fir_q15", "fir_q31": "fir_q31", "fir_fast_q15": "fir_fast_q15",
           "fir_fast_q31": "fir_fast_q31", "mat_mult_f32": "mat_mult_f32",
-          "mfcc_f32": "mfcc_f32"}[workload]
-    nn = 256 if workload == "mat_mult_f32" else n      # 1024^3 takes seconds per matrix on one core
+          "mfcc_f32": "mfcc_f32", "mat_mult_q15": "mat_mult_q15", "mat_mult_q31": "mat_mult_q31"}[workload]
+    nn = 256 if workload.startswith("mat_mult") else n  # 1024^3 takes seconds per matrix on one core
     out = subprocess.run([exe, wl, str(nn), str(threads), str(secs)], capture_output=True, text=True,
                          timeout=120)
     r = json.loads(out.stdout)
-    if workload == "mat_mult_f32":
-        return {"value": round(r["gflops"] * 1e-3, 6), "unit": "TFLOP/s", "cores": threads, "kind": kind,
-                "sample": f"{threads} threads x {secs:.0f} s of arm_mat_mult_f32 {nn}^3 (reference scalar C)"}
+    if workload.startswith("mat_mult"):
+        return {"value": round(r["gflops"] * 1e-3, 6), "unit": "TFLOP/s" if workload.endswith("f32") else "TOPS",
+                "cores": threads, "kind": kind,
+                "sample": f"{threads} threads x {secs:.0f} s of arm_{workload} {nn}^3 (reference scalar C)"}
     return {"value": round(r["gsamples_per_s"], 6), "unit": "Gsamples/s", "cores": threads, "kind": kind,
             "sample": f"{threads} threads x {secs:.0f} s, {wl} n={nn}, {int(r['samples'])} samples "
                       f"(reference scalar C, gcc -O2)"}
@@ -249,6 +252,23 @@ def run_mfcc(n, batch, steps, warmup, world, rank):
                            "tolerance": "2e-5 + 1e-6*|ref| (device logf vs host libm logf; other stages exact)"}
 
 
+def run_mat_fixed(kind, dim, batch, steps, warmup, world, rank):
+    """arm_mat_mult_q15 / _q31 (byte-sliced i8 MFMA), full-range operands, bit-exact check of
+    matrix 0 against the CPU checker."""
+    a = synth(kind, batch * dim * dim, rank).view(batch, dim, dim)
+    b = synth(kind, batch * dim * dim, rank, salt=3).view(batch, dim, dim)
+    c = torch.empty_like(a)
+
+    def launch(s):
+        dsp.mat_mult_batch(a, b, c)
+
+    wall, kern_ms = time_launches(launch, steps, warmup, world)
+    host, hk = cpu_checker()
+    st, want = host.mat_mult_fixed(kind, a[0].cpu().numpy(), b[0].cpu().numpy())
+    ok = st == 0 and c[0].cpu().numpy().tobytes() == want.tobytes()
+    return wall, kern_ms, {"checker": hk, "bit_exact": bool(ok), "matrices_checked": 1}
+
+
 def pmc_traffic(workload):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, when present."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -287,6 +307,10 @@ def main():
         wall, kern_ms, parity = run_fir(kind[4:], n, batch, args.steps, args.warmup, world, rank)
         units = batch * 4096
         algo_bytes = units * bps + batch * (n - 1) * bps  # in + out + history read/write
+    elif args.workload in ("mat_mult_q15", "mat_mult_q31"):
+        wall, kern_ms, parity = run_mat_fixed(kind[3:], n, batch, args.steps, args.warmup, world, rank)
+        units = batch
+        algo_bytes = None
     elif args.workload == "mfcc_f32":
         wall, kern_ms, parity = run_mfcc(n, batch, args.steps, args.warmup, world, rank)
         units = batch * n                                  # input samples
@@ -303,7 +327,18 @@ def main():
     line = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "data": "synthetic (per-rank seeded generator, rank-local, no scatter)"}
-    if args.workload == "mat_mult_f32":
+    if args.workload in ("mat_mult_q15", "mat_mult_q31"):
+        planes = 2 if args.workload.endswith("q15") else 4
+        ops = 2.0 * n * n * n * batch
+        line.update(value=round(total_units * 2.0 * n ** 3 / wall * 1e-12, 4), unit="TOPS (2*M*N*K int MAC)",
+                    dtype=f"{kind[3:]} (exact int64 sums via {planes}x{planes} i8 byte planes)",
+                    config={"workload": f"arm_mat_mult_{kind[3:]} {n}x{n}x{n} batch={batch}/GPU",
+                            "dims": [n, n, n], "batch_per_gpu": batch, "parallelism": f"dp{world} shards"})
+        i8 = ops * planes * planes / (kern_ms * 1e-3) * 1e-12
+        line["roofline"] = {"bound": "mfma", "achieved": round(i8, 2), "peak": 5000.0,
+                            "unit": "TOPS (i8 MFMA ops incl. the byte-plane products)", "frac": round(i8 / 5000.0, 4),
+                            "traffic": None, "avg_kernel_ms": round(kern_ms, 4)}
+    elif args.workload == "mat_mult_f32":
         flops = 2.0 * n * n * n * batch
         line.update(value=round(total_units * 2.0 * n ** 3 / wall * 1e-12, 4), unit="TFLOP/s", dtype="f32",
                     config={"workload": f"arm_mat_mult_f32 {n}x{n}x{n} batch={batch}/GPU (BASELINE configs[4])",

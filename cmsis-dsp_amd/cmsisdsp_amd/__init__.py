@@ -20,7 +20,8 @@ import numpy as np
 from . import _abi
 from ._abi import (arm_cfft_instance_f32, arm_cfft_instance_q15, arm_cfft_instance_q31,  # noqa: F401
                    arm_fir_instance_f32, arm_fir_instance_q15, arm_fir_instance_q31, arm_matrix_instance_f32,
-                   arm_rfft_fast_instance_f32, arm_mfcc_instance_f32, ARM_MATH_SUCCESS, ARM_MATH_ARGUMENT_ERROR,
+                   arm_rfft_fast_instance_f32, arm_mfcc_instance_f32, arm_matrix_instance_q15,
+                   arm_matrix_instance_q31, ARM_MATH_SUCCESS, ARM_MATH_ARGUMENT_ERROR,
                    ARM_MATH_SIZE_MISMATCH)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -296,13 +297,38 @@ def fir_batch(S, src, dst, hist, stream=None, q15=False, kind=None):
         raise RuntimeError(f"{fn.__name__} -> {st}: {last_error()[1]}")
 
 
+def arm_mat_mult_fixed(kind, a, b):
+    """(status, C) = A @ B through arm_mat_mult_q15 / arm_mat_mult_q31 (row-major)."""
+    dt = np.int16 if kind == "q15" else np.int32
+    inst = arm_matrix_instance_q15 if kind == "q15" else arm_matrix_instance_q31
+    a = np.ascontiguousarray(a, dtype=dt)
+    b = np.ascontiguousarray(b, dtype=dt)
+    c = np.zeros((a.shape[0], b.shape[1]), dtype=dt)
+    A, B, Cm = inst(), inst(), inst()
+    init = getattr(lib, f"arm_mat_init_{kind}")
+    init(C.byref(A), a.shape[0], a.shape[1], a.ctypes.data)
+    init(C.byref(B), b.shape[0], b.shape[1], b.ctypes.data)
+    init(C.byref(Cm), c.shape[0], c.shape[1], c.ctypes.data)
+    if kind == "q15":
+        st = lib.arm_mat_mult_q15(C.byref(A), C.byref(B), C.byref(Cm), None)
+    else:
+        st = lib.arm_mat_mult_q31(C.byref(A), C.byref(B), C.byref(Cm))
+    _check_void(f"arm_mat_mult_{kind}")
+    return st, c
+
+
 def mat_mult_batch(a, b, c, stream=None):
-    """c[i] = a[i] @ b[i] for device tensors [batch, M, K] x [batch, K, N] -> [batch, M, N]."""
+    """c[i] = a[i] @ b[i] for device tensors [batch, M, K] x [batch, K, N] -> [batch, M, N];
+    float32 -> arm_mat_mult_f32_batch, int16 -> _q15, int32 -> _q31."""
+    import torch
     batch, m, k = a.shape
     n = b.shape[2]
-    A, B, Cm = arm_matrix_instance_f32(m, k, C.cast(a.data_ptr(), _abi.c_f32p)), \
-        arm_matrix_instance_f32(k, n, C.cast(b.data_ptr(), _abi.c_f32p)), \
-        arm_matrix_instance_f32(m, n, C.cast(c.data_ptr(), _abi.c_f32p))
-    st = lib.arm_mat_mult_f32_batch(C.byref(A), C.byref(B), C.byref(Cm), batch, _stream_ptr(stream))
+    kind, inst, ptr = {torch.float32: ("f32", arm_matrix_instance_f32, _abi.c_f32p),
+                       torch.int16: ("q15", arm_matrix_instance_q15, _abi.c_i16p),
+                       torch.int32: ("q31", arm_matrix_instance_q31, _abi.c_i32p)}[a.dtype]
+    A, B, Cm = inst(m, k, C.cast(a.data_ptr(), ptr)), inst(k, n, C.cast(b.data_ptr(), ptr)), \
+        inst(m, n, C.cast(c.data_ptr(), ptr))
+    fn = getattr(lib, f"arm_mat_mult_{kind}_batch")
+    st = fn(C.byref(A), C.byref(B), C.byref(Cm), batch, _stream_ptr(stream))
     if st != ARM_MATH_SUCCESS:
-        raise RuntimeError(f"arm_mat_mult_f32_batch -> {st}: {last_error()[1]}")
+        raise RuntimeError(f"{fn.__name__} -> {st}: {last_error()[1]}")

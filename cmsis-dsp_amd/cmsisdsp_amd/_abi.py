@@ -61,6 +61,16 @@ class arm_mfcc_instance_f32(C.Structure):
                 ("rfft", arm_rfft_fast_instance_f32)]
 
 
+class arm_matrix_instance_q15(C.Structure):
+    # Include/dsp/matrix_functions.h:139-144
+    _fields_ = [("numRows", C.c_uint16), ("numCols", C.c_uint16), ("pData", c_i16p)]
+
+
+class arm_matrix_instance_q31(C.Structure):
+    # Include/dsp/matrix_functions.h:149-154
+    _fields_ = [("numRows", C.c_uint16), ("numCols", C.c_uint16), ("pData", c_i32p)]
+
+
 P = C.POINTER
 SIZES = (16, 32, 64, 128, 256, 512, 1024, 2048, 4096)
 RFFT_SIZES = (32, 64, 128, 256, 512, 1024, 2048, 4096)
@@ -84,6 +94,12 @@ DROPIN = {
     "arm_fir_q31": (None, [P(arm_fir_instance_q31), C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_fir_fast_q31": (None, [P(arm_fir_instance_q31), C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_mat_init_f32": (None, [P(arm_matrix_instance_f32), C.c_uint16, C.c_uint16, C.c_void_p]),
+    "arm_mat_init_q15": (None, [P(arm_matrix_instance_q15), C.c_uint16, C.c_uint16, C.c_void_p]),
+    "arm_mat_init_q31": (None, [P(arm_matrix_instance_q31), C.c_uint16, C.c_uint16, C.c_void_p]),
+    "arm_mat_mult_q15": (C.c_int, [P(arm_matrix_instance_q15), P(arm_matrix_instance_q15),
+                                   P(arm_matrix_instance_q15), C.c_void_p]),
+    "arm_mat_mult_q31": (C.c_int, [P(arm_matrix_instance_q31), P(arm_matrix_instance_q31),
+                                   P(arm_matrix_instance_q31)]),
     "arm_mfcc_init_f32": (C.c_int, [P(arm_mfcc_instance_f32), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "arm_mfcc_f32": (None, [P(arm_mfcc_instance_f32), C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -125,6 +141,10 @@ BATCHED = {
                                          C.c_void_p, C.c_void_p]),
     "arm_mat_mult_f32_batch": (C.c_int, [P(arm_matrix_instance_f32), P(arm_matrix_instance_f32),
                                          P(arm_matrix_instance_f32), C.c_uint32, C.c_void_p]),
+    "arm_mat_mult_q15_batch": (C.c_int, [P(arm_matrix_instance_q15), P(arm_matrix_instance_q15),
+                                         P(arm_matrix_instance_q15), C.c_uint32, C.c_void_p]),
+    "arm_mat_mult_q31_batch": (C.c_int, [P(arm_matrix_instance_q31), P(arm_matrix_instance_q31),
+                                         P(arm_matrix_instance_q31), C.c_uint32, C.c_void_p]),
     "arm_mfcc_f32_batch": (C.c_int, [P(arm_mfcc_instance_f32), C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                      C.c_void_p]),
     "arm_mi355x_last_error": (C.c_int, []),

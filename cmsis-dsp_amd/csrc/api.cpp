@@ -262,9 +262,35 @@ arm_status fir_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uint32
   return ARM_MATH_SUCCESS;
 }
 
-bool mat_shapes_ok(const arm_matrix_instance_f32* a, const arm_matrix_instance_f32* b,
-                   const arm_matrix_instance_f32* c) {
+template <typename M>
+bool mat_shapes_ok(const M* a, const M* b, const M* c) {
   return a->numCols == b->numRows && a->numRows == c->numRows && b->numCols == c->numCols;
+}
+
+// drop-in fixed-point matrix multiply (host or device operands), synchronous
+template <typename T, typename M>
+arm_status mat_mult_fixed_sync(const M* pSrcA, const M* pSrcB, M* pDst) {
+  if (!pSrcA || !pSrcB || !pDst) return ARM_MATH_ARGUMENT_ERROR;
+  if (!mat_shapes_ok(pSrcA, pSrcB, pDst)) return ARM_MATH_SIZE_MISMATCH;
+  const int m = pSrcA->numRows, k = pSrcA->numCols, n = pSrcB->numCols;
+  const size_t ab = sizeof(T) * (size_t)m * k, bb = sizeof(T) * (size_t)k * n, cb = sizeof(T) * (size_t)m * n;
+  hipStream_t st = sync_stream();
+  const bool da = is_device_ptr(pSrcA->pData), db = is_device_ptr(pSrcB->pData), dc = is_device_ptr(pDst->pData);
+  T* A = da ? pSrcA->pData : (T*)scratch(ab + 16, 0);
+  T* B = db ? pSrcB->pData : (T*)scratch(bb + 16, 1);
+  T* Cd = dc ? pDst->pData : (T*)scratch(cb + 16, 2);
+  if (!A || !B || !Cd) { set_error(hipErrorOutOfMemory, "arm_mat_mult scratch"); return ARM_MATH_ARGUMENT_ERROR; }
+  hipError_t e = hipSuccess;
+  if (!da && ab) e = hipMemcpyAsync(A, pSrcA->pData, ab, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && !db && bb) e = hipMemcpyAsync(B, pSrcB->pData, bb, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) {
+    if constexpr (sizeof(T) == 2) e = mat_mult_q15_launch(m, k, n, A, B, Cd, 1, st);
+    else e = mat_mult_q31_launch(m, k, n, A, B, Cd, 1, st);
+  }
+  if (e == hipSuccess && !dc && cb) e = hipMemcpyAsync(pDst->pData, Cd, cb, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) { set_error(e, "arm_mat_mult"); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
 }
 
 // FIR init: zero numTaps + blockSize - 1 state words (arm_fir_init_f32.c:74-95,
@@ -451,6 +477,35 @@ arm_status arm_mfcc_f32_batch(const arm_mfcc_instance_f32* S, float32_t* d_src, 
   MfccDev d;
   if (!mfcc_prepare(S, d)) return ARM_MATH_ARGUMENT_ERROR;
   return mfcc_run(S, d, d_src, d_tmp, d_dst, batch, (hipStream_t)stream) ? ARM_MATH_SUCCESS : ARM_MATH_ARGUMENT_ERROR;
+}
+
+// ---- matrix multiply q15 / q31 --------------------------------------------------
+arm_status arm_mat_mult_q15(const arm_matrix_instance_q15* pSrcA, const arm_matrix_instance_q15* pSrcB,
+                            arm_matrix_instance_q15* pDst, q15_t* pState) {
+  (void)pState;   // the reference's transpose buffer (ARM_MATH_DSP branch only)
+  return mat_mult_fixed_sync<int16_t>(pSrcA, pSrcB, pDst);
+}
+arm_status arm_mat_mult_q31(const arm_matrix_instance_q31* pSrcA, const arm_matrix_instance_q31* pSrcB,
+                            arm_matrix_instance_q31* pDst) {
+  return mat_mult_fixed_sync<int32_t>(pSrcA, pSrcB, pDst);
+}
+arm_status arm_mat_mult_q15_batch(const arm_matrix_instance_q15* pSrcA, const arm_matrix_instance_q15* pSrcB,
+                                  arm_matrix_instance_q15* pDst, uint32_t batch, void* stream) {
+  if (!pSrcA || !pSrcB || !pDst) return ARM_MATH_ARGUMENT_ERROR;
+  if (!mat_shapes_ok(pSrcA, pSrcB, pDst)) return ARM_MATH_SIZE_MISMATCH;
+  hipError_t e = mat_mult_q15_launch(pSrcA->numRows, pSrcA->numCols, pSrcB->numCols, pSrcA->pData, pSrcB->pData,
+                                     pDst->pData, batch, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(e, "arm_mat_mult_q15_batch"); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
+}
+arm_status arm_mat_mult_q31_batch(const arm_matrix_instance_q31* pSrcA, const arm_matrix_instance_q31* pSrcB,
+                                  arm_matrix_instance_q31* pDst, uint32_t batch, void* stream) {
+  if (!pSrcA || !pSrcB || !pDst) return ARM_MATH_ARGUMENT_ERROR;
+  if (!mat_shapes_ok(pSrcA, pSrcB, pDst)) return ARM_MATH_SIZE_MISMATCH;
+  hipError_t e = mat_mult_q31_launch(pSrcA->numRows, pSrcA->numCols, pSrcB->numCols, pSrcA->pData, pSrcB->pData,
+                                     pDst->pData, batch, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(e, "arm_mat_mult_q31_batch"); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
 }
 
 }  // extern "C"

@@ -150,7 +150,17 @@ MI_MFCC_INIT(4096)
 
 // (FIR init zeroes a state buffer that may be device memory: it lives in api.cpp.)
 
-// ---- matrix init (arm_mat_init_f32.c)
+// ---- matrix init (arm_mat_init_f32.c, arm_mat_init_q15.c, arm_mat_init_q31.c)
+void arm_mat_init_q15(arm_matrix_instance_q15* S, uint16_t nRows, uint16_t nColumns, q15_t* pData) {
+  S->numRows = nRows;
+  S->numCols = nColumns;
+  S->pData = pData;
+}
+void arm_mat_init_q31(arm_matrix_instance_q31* S, uint16_t nRows, uint16_t nColumns, q31_t* pData) {
+  S->numRows = nRows;
+  S->numCols = nColumns;
+  S->pData = pData;
+}
 void arm_mat_init_f32(arm_matrix_instance_f32* S, uint16_t nRows, uint16_t nColumns, float32_t* pData) {
   S->numRows = nRows;
   S->numCols = nColumns;

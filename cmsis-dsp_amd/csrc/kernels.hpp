@@ -69,4 +69,11 @@ hipError_t mfcc_f32_post_launch(int n, const float* y, const float* maxv, int ma
 hipError_t mat_mult_f32_launch(int m, int k, int n, const float* a, const float* b, float* c,
                                uint32_t batch, hipStream_t st);
 
+// Row-major q15 / q31 C[b] = A[b] * B[b] (arm_mat_mult_q15 / _q31 semantics, bit-exact):
+// byte-sliced planes on the i8 matrix cores (mat_mult_fixed.hip).
+hipError_t mat_mult_q15_launch(int m, int k, int n, const int16_t* a, const int16_t* b, int16_t* c, uint32_t batch,
+                               hipStream_t st);
+hipError_t mat_mult_q31_launch(int m, int k, int n, const int32_t* a, const int32_t* b, int32_t* c, uint32_t batch,
+                               hipStream_t st);
+
 }  // namespace mi355x

@@ -1,0 +1,204 @@
+// Batched q15 / q31 matrix multiply on the i8 matrix cores — MI355X, bit-exact.
+//
+// Replaces the host scalar paths of Source/MatrixFunctions/arm_mat_mult_q15.c (:741-912,
+// !ARM_MATH_DSP branch: q63 sum of exact q15 products, __SSAT((sum >> 15), 16)) and
+// arm_mat_mult_q31.c (:53-163: q63 sum of exact q31 products, wrapping as gcc's adds do,
+// (q31)(sum >> 31)).  Both are plain integer sums, so any evaluation order gives the
+// reference's bits.
+//
+// Byte slicing: a value v of P bytes is v = sum_p 256^p t_p + c0 with every t_p a SIGNED
+// byte (the top byte as is, lower bytes offset by -128) and c0 = 128 * sum_{p<P-1} 256^p.
+// Then, for C = A*B over K terms,
+//   C_ij = sum_{p,q} 256^(p+q) (T^A_p T^B_q)_ij + c0 (rowsum(A)_i + colsum(B)_j) - K c0^2,
+// where the P^2 plane products run on v_mfma_i32_32x32x32_i8 (exact int32 accumulation)
+// into 2P-1 accumulators by weight class p+q, and the row / column sums are exact integer
+// sums gathered while staging.  The result is formed in int64 (mod 2^64, as the reference
+// wraps).  Accumulator bound: a class holds at most P pairs of |t t'| <= 2^14 per k, so
+// K <= kMatI8MaxK keeps every int32 accumulator exact; longer K uses the VALU kernel.
+// Operand maps (verified with exact data, tools/probes/mfma_i8_layout.hip): lane l holds
+// A[row l&31][k = 16(l>>5) + j] and B[k = 16(l>>5) + j][col l&31] in byte j.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace mi355x {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kMT = 64, kNT = 64, kKT = 64;     // workgroup tile: 4 waves of 32x32, K step 64
+constexpr int kRowB = kKT + 16;                  // LDS row pitch in bytes (k-contiguous rows)
+constexpr int kMatI8MaxK = 32704;
+
+template <typename T> struct Slices;
+template <> struct Slices<int16_t> { static constexpr int P = 2; static constexpr int64_t C0 = 128; };
+template <> struct Slices<int32_t> { static constexpr int P = 4; static constexpr int64_t C0 = 128LL * (1 + 256 + 65536); };
+
+// Plane p of four values given as the low bytes p of four dwords: signed bytes, the lower
+// planes offset by -128 (x - 128 = x ^ 0x80 on a byte).
+template <int P>
+__device__ __forceinline__ uint32_t plane4(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3, int p) {
+  const uint32_t sel = 0x0c0c0400u + 0x0101u * (uint32_t)p;     // [v_lo.byte p, v_hi.byte p, 0, 0]
+  const uint32_t lo = __builtin_amdgcn_perm(v1, v0, sel), hi = __builtin_amdgcn_perm(v3, v2, sel);
+  const uint32_t w = lo | (hi << 16);
+  return p == P - 1 ? w : w ^ 0x80808080u;
+}
+
+// 16 consecutive elements of a row (zero past `valid`), as one raw dword per element.
+template <typename T>
+__device__ __forceinline__ void load_row16(const T* __restrict__ p, int valid, bool vec, uint32_t (&v)[16]) {
+  if (vec && valid >= 16) {
+    if constexpr (sizeof(T) == 2) {
+      const uint4 a = reinterpret_cast<const uint4*>(p)[0], b = reinterpret_cast<const uint4*>(p)[1];
+      const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { v[2 * i] = (uint32_t)(int32_t)(int16_t)(d[i] & 0xffffu); v[2 * i + 1] = (uint32_t)((int32_t)d[i] >> 16); }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint4 a = reinterpret_cast<const uint4*>(p)[i];
+        v[4 * i] = a.x; v[4 * i + 1] = a.y; v[4 * i + 2] = a.z; v[4 * i + 3] = a.w;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = j < valid ? (uint32_t)(int32_t)p[j] : 0u;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void mat_mult_i8_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                          T* __restrict__ C, int M, int K, int N) {
+  constexpr int P = Slices<T>::P, S = 2 * P - 1;
+  constexpr int64_t C0 = Slices<T>::C0;
+  __shared__ __attribute__((aligned(16))) int8_t As[P][kMT][kRowB];
+  __shared__ __attribute__((aligned(16))) int8_t Bs[P][kNT][kRowB];   // transposed: [col][k]
+  __shared__ int64_t rsum[4][kMT], csum[4][kNT];
+
+  const int tilesN = (N + kNT - 1) / kNT;
+  const int tm = blockIdx.x / tilesN, tn = blockIdx.x % tilesN;
+  const size_t bz = blockIdx.z;
+  A += bz * (size_t)M * K;
+  B += bz * (size_t)K * N;
+  C += bz * (size_t)M * N;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int row0 = tm * kMT, col0 = tn * kNT;
+
+  // staging roles: A row (tid>>2), k sub-range 16*(tid&3); B column (tid&63), k sub-range 16*(tid>>6)
+  const int ar = tid >> 2, ak = 16 * (tid & 3);
+  const int bc = tid & 63, bk = 16 * (tid >> 6);
+  const int gr = row0 + ar, gc = col0 + bc;
+  const bool vec = ((K * (int)sizeof(T)) % 16) == 0 && (((uintptr_t)A) & 15) == 0;
+  int64_t my_rsum = 0, my_csum = 0;
+
+  i32x16 acc[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) acc[s] = i32x16{};
+  const int wm = wid >> 1, wn = wid & 1;
+  const int r = lane & 31, h = lane >> 5;
+
+  const int nk = (K + kKT - 1) / kKT;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int k0 = kt * kKT;
+    uint32_t av[16], bv[16];
+    load_row16<T>(A + (size_t)gr * K + k0 + ak, gr < M ? K - (k0 + ak) : 0, vec, av);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int kb = k0 + bk + j;
+      bv[j] = (gc < N && kb < K) ? (uint32_t)(int32_t)B[(size_t)kb * N + gc] : 0u;
+    }
+    __syncthreads();                     // the previous step's fragments are consumed
+    int64_t ra = 0, cb = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { ra += (int32_t)av[j]; cb += (int32_t)bv[j]; }
+    my_rsum += ra;
+    my_csum += cb;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      uint4 pa, pb;
+      pa.x = plane4<P>(av[0], av[1], av[2], av[3], p);     pb.x = plane4<P>(bv[0], bv[1], bv[2], bv[3], p);
+      pa.y = plane4<P>(av[4], av[5], av[6], av[7], p);     pb.y = plane4<P>(bv[4], bv[5], bv[6], bv[7], p);
+      pa.z = plane4<P>(av[8], av[9], av[10], av[11], p);   pb.z = plane4<P>(bv[8], bv[9], bv[10], bv[11], p);
+      pa.w = plane4<P>(av[12], av[13], av[14], av[15], p); pb.w = plane4<P>(bv[12], bv[13], bv[14], bv[15], p);
+      *reinterpret_cast<uint4*>(&As[p][ar][ak]) = pa;
+      *reinterpret_cast<uint4*>(&Bs[p][bc][bk]) = pb;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < kKT / 32; ++kk) {
+      i32x4 fa[P], fb[P];
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        fa[p] = *reinterpret_cast<const i32x4*>(&As[p][wm * 32 + r][32 * kk + 16 * h]);
+        fb[p] = *reinterpret_cast<const i32x4*>(&Bs[p][wn * 32 + r][32 * kk + 16 * h]);
+      }
+#pragma unroll
+      for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int q = 0; q < P; ++q) acc[p + q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[p], fb[q], acc[p + q], 0, 0, 0);
+    }
+  }
+
+  // exact row / column sums of the original values
+  rsum[tid & 3][ar] = my_rsum;
+  csum[tid >> 6][bc] = my_csum;
+  __syncthreads();
+  const int64_t kpad = (int64_t)nk * kKT;   // padded k terms are zeros: the identity holds over kpad
+  const int cc = wn * 32 + r;
+  const int64_t cs = csum[0][cc] + csum[1][cc] + csum[2][cc] + csum[3][cc];
+  const int gcol = col0 + cc;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int rr = wm * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    const int grow = row0 + rr;
+    const int64_t rs = rsum[0][rr] + rsum[1][rr] + rsum[2][rr] + rsum[3][rr];
+    uint64_t v = (uint64_t)(C0 * (rs + cs)) - (uint64_t)kpad * (uint64_t)(C0 * C0);
+#pragma unroll
+    for (int s = 0; s < S; ++s) v += (uint64_t)(int64_t)acc[s][reg] << (8 * s);
+    if (grow < M && gcol < N) {
+      const int64_t sum = (int64_t)v;
+      if constexpr (sizeof(T) == 2) C[(size_t)grow * N + gcol] = (T)ssat16((int32_t)(sum >> 15));
+      else C[(size_t)grow * N + gcol] = (T)(int32_t)(sum >> 31);
+    }
+  }
+}
+
+// K beyond the i8 accumulators' exact range: one thread per output, int64 sum.
+template <typename T>
+__global__ __launch_bounds__(256) void mat_mult_fixed_valu_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                                  T* __restrict__ C, int M, int K, int N) {
+  const size_t bz = blockIdx.z;
+  const int i = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= N) return;
+  const T* a = A + bz * (size_t)M * K + (size_t)i * K;
+  const T* b = B + bz * (size_t)K * N + j;
+  uint64_t sum = 0;
+  for (int k = 0; k < K; ++k) sum += (uint64_t)((int64_t)a[k] * b[(size_t)k * N]);
+  const int64_t s = (int64_t)sum;
+  if constexpr (sizeof(T) == 2) C[bz * (size_t)M * N + (size_t)i * N + j] = (T)ssat16((int32_t)(s >> 15));
+  else C[bz * (size_t)M * N + (size_t)i * N + j] = (T)(int32_t)(s >> 31);
+}
+
+template <typename T>
+static hipError_t launch_fixed(int m, int k, int n, const T* a, const T* b, T* c, uint32_t batch, hipStream_t st) {
+  if (batch == 0 || m == 0 || n == 0) return hipSuccess;
+  if (k == 0) return hipMemsetAsync(c, 0, sizeof(T) * (size_t)m * n * batch, st);
+  if (k <= kMatI8MaxK) {
+    const int tiles = ((m + kMT - 1) / kMT) * ((n + kNT - 1) / kNT);
+    hipLaunchKernelGGL(mat_mult_i8_kernel<T>, dim3(tiles, 1, batch), dim3(256), 0, st, a, b, c, m, k, n);
+  } else {
+    hipLaunchKernelGGL(mat_mult_fixed_valu_kernel<T>, dim3((n + 255) / 256, m, batch), dim3(256), 0, st, a, b, c,
+                       m, k, n);
+  }
+  return hipGetLastError();
+}
+
+hipError_t mat_mult_q15_launch(int m, int k, int n, const int16_t* a, const int16_t* b, int16_t* c, uint32_t batch,
+                               hipStream_t st) {
+  return launch_fixed<int16_t>(m, k, n, a, b, c, batch, st);
+}
+hipError_t mat_mult_q31_launch(int m, int k, int n, const int32_t* a, const int32_t* b, int32_t* c, uint32_t batch,
+                               hipStream_t st) {
+  return launch_fixed<int32_t>(m, k, n, a, b, c, batch, st);
+}
+
+}  // namespace mi355x

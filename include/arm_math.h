@@ -107,12 +107,25 @@ typedef struct {
   const float32_t *pCoeffs;
 } arm_fir_instance_f32;
 
-/* ---- matrix instance: Include/dsp/matrix_functions.h:118-123 --------------------- */
+/* ---- matrix instances: Include/dsp/matrix_functions.h:118-123 (f32), :139-144 (q15),
+ * :149-154 (q31) */
 typedef struct {
   uint16_t   numRows;
   uint16_t   numCols;
   float32_t *pData;
 } arm_matrix_instance_f32;
+
+typedef struct {
+  uint16_t   numRows;
+  uint16_t   numCols;
+  q15_t     *pData;
+} arm_matrix_instance_q15;
+
+typedef struct {
+  uint16_t   numRows;
+  uint16_t   numCols;
+  q31_t     *pData;
+} arm_matrix_instance_q31;
 
 /* ===================================================================================
  * Complex FFT, f32.  Prototypes: Include/dsp/transform_functions.h:428-460
@@ -275,6 +288,18 @@ void arm_mat_init_f32(arm_matrix_instance_f32 *S, uint16_t nRows, uint16_t nColu
 arm_status arm_mat_mult_f32(const arm_matrix_instance_f32 *pSrcA,
                             const arm_matrix_instance_f32 *pSrcB,
                             arm_matrix_instance_f32 *pDst);
+
+/* Matrix multiply q15 / q31.  Prototypes: Include/dsp/matrix_functions.h
+ * (arm_mat_mult_q15 with its pState transpose buffer, arm_mat_mult_q31, arm_mat_init_q15/_q31).
+ * Reference bodies: Source/MatrixFunctions/arm_mat_mult_q15.c:741-912 (!ARM_MATH_DSP: q63
+ * sum of exact products, __SSAT(sum >> 15, 16)), arm_mat_mult_q31.c:53-163 (q63 sum,
+ * (q31)(sum >> 31)).  Bit-exact; pState is accepted and unused.  Size check always on. */
+void arm_mat_init_q15(arm_matrix_instance_q15 *S, uint16_t nRows, uint16_t nColumns, q15_t *pData);
+void arm_mat_init_q31(arm_matrix_instance_q31 *S, uint16_t nRows, uint16_t nColumns, q31_t *pData);
+arm_status arm_mat_mult_q15(const arm_matrix_instance_q15 *pSrcA, const arm_matrix_instance_q15 *pSrcB,
+                            arm_matrix_instance_q15 *pDst, q15_t *pState);
+arm_status arm_mat_mult_q31(const arm_matrix_instance_q31 *pSrcA, const arm_matrix_instance_q31 *pSrcB,
+                            arm_matrix_instance_q31 *pDst);
 
 #ifdef __cplusplus
 }

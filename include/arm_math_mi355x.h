@@ -71,6 +71,11 @@ arm_status arm_fir_fast_q31_batch(const arm_fir_instance_q31 *S, const q31_t *d_
  * item).  Returns ARM_MATH_SIZE_MISMATCH on incompatible shapes (arm_mat_mult_f32.c:618-630). */
 arm_status arm_mat_mult_f32_batch(const arm_matrix_instance_f32 *pSrcA, const arm_matrix_instance_f32 *pSrcB,
                                   arm_matrix_instance_f32 *pDst, uint32_t batch, void *stream);
+/* q15 / q31 analogues (bit-exact; byte-sliced planes on the i8 matrix cores). */
+arm_status arm_mat_mult_q15_batch(const arm_matrix_instance_q15 *pSrcA, const arm_matrix_instance_q15 *pSrcB,
+                                  arm_matrix_instance_q15 *pDst, uint32_t batch, void *stream);
+arm_status arm_mat_mult_q31_batch(const arm_matrix_instance_q31 *pSrcA, const arm_matrix_instance_q31 *pSrcB,
+                                  arm_matrix_instance_q31 *pDst, uint32_t batch, void *stream);
 
 /* Error channel for the void-returning drop-in functions: 0 = no error, otherwise the
  * hipError_t of the last failure on this thread. */

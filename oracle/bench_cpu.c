@@ -36,6 +36,8 @@ void oracle_arm_fir_init_q31(arm_fir_instance_q31 *S, uint16_t numTaps, const in
                              uint32_t blockSize);
 arm_status oracle_arm_fir_init_q15(arm_fir_instance_q15 *S, uint16_t numTaps, const int16_t *pCoeffs,
                                    int16_t *pState, uint32_t blockSize);
+void oracle_arm_mat_init_q15(arm_matrix_instance_q15 *S, uint16_t r, uint16_t c, int16_t *p);
+void oracle_arm_mat_init_q31(arm_matrix_instance_q31 *S, uint16_t r, uint16_t c, int32_t *p);
 void oracle_arm_mat_init_f32(arm_matrix_instance_f32 *S, uint16_t r, uint16_t c, float *p);
 #endif
 
@@ -139,6 +141,20 @@ static void *worker(void *arg) {
       samples += n;
     } while (now() - t0 < j->seconds);
     free(coefs); free(win); free(x); free(src); free(tmp);
+  } else if (!strcmp(j->wl, "mat_mult_q15") || !strcmp(j->wl, "mat_mult_q31")) {
+    const int d = j->n, q15 = !strcmp(j->wl, "mat_mult_q15");
+    int16_t *a16 = malloc(2 * d * d), *b16 = malloc(2 * d * d), *o16 = malloc(2 * d * d), *st16 = malloc(2 * d * d);
+    int32_t *a32 = malloc(4 * d * d), *b32 = malloc(4 * d * d), *o32 = malloc(4 * d * d);
+    for (int i = 0; i < d * d; ++i) { a16[i] = (int16_t)sm(&seed); b16[i] = (int16_t)sm(&seed); a32[i] = (int32_t)sm(&seed); b32[i] = (int32_t)sm(&seed); }
+    arm_matrix_instance_q15 A15, B15, O15;
+    arm_matrix_instance_q31 A31, B31, O31;
+    F(arm_mat_init_q15)(&A15, d, d, a16); F(arm_mat_init_q15)(&B15, d, d, b16); F(arm_mat_init_q15)(&O15, d, d, o16);
+    F(arm_mat_init_q31)(&A31, d, d, a32); F(arm_mat_init_q31)(&B31, d, d, b32); F(arm_mat_init_q31)(&O31, d, d, o32);
+    do {
+      if (q15) F(arm_mat_mult_q15)(&A15, &B15, &O15, st16); else F(arm_mat_mult_q31)(&A31, &B31, &O31);
+      samples += (double)d * d; j->flops += 2.0 * d * d * d;
+    } while (now() - t0 < j->seconds);
+    free(a16); free(b16); free(o16); free(st16); free(a32); free(b32); free(o32);
   } else if (!strcmp(j->wl, "mat_mult_f32")) {
     const int d = j->n;
     float *a = malloc(sizeof(float) * d * d), *b = malloc(sizeof(float) * d * d), *o = malloc(sizeof(float) * d * d);

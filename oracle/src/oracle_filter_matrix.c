@@ -117,3 +117,31 @@ arm_status oracle_arm_mat_mult_f32(const arm_matrix_instance_f32 *A, const arm_m
     }
   return ARM_MATH_SUCCESS;
 }
+
+/* arm_mat_mult_q15.c:741-912 (!ARM_MATH_DSP): q63 sum of exact q15 products in k order,
+ * __SSAT((sum >> 15), 16) with the shifted sum narrowed to int32 first. */
+arm_status oracle_arm_mat_mult_q15(const arm_matrix_instance_q15 *A, const arm_matrix_instance_q15 *B,
+                                   arm_matrix_instance_q15 *Cm, int16_t *pState) {
+  (void)pState;
+  const uint32_t M = A->numRows, K = A->numCols, N = B->numCols;
+  for (uint32_t i = 0; i < M; ++i)
+    for (uint32_t j = 0; j < N; ++j) {
+      int64_t sum = 0;
+      for (uint32_t k = 0; k < K; ++k) sum += (int32_t)A->pData[i * K + k] * B->pData[k * N + j];
+      Cm->pData[i * N + j] = oracle_sat_q15((int32_t)(sum >> 15));
+    }
+  return ARM_MATH_SUCCESS;
+}
+
+/* arm_mat_mult_q31.c:53-163: q63 sum of exact q31 products (wrapping), (q31)(sum >> 31). */
+arm_status oracle_arm_mat_mult_q31(const arm_matrix_instance_q31 *A, const arm_matrix_instance_q31 *B,
+                                   arm_matrix_instance_q31 *Cm) {
+  const uint32_t M = A->numRows, K = A->numCols, N = B->numCols;
+  for (uint32_t i = 0; i < M; ++i)
+    for (uint32_t j = 0; j < N; ++j) {
+      uint64_t sum = 0;
+      for (uint32_t k = 0; k < K; ++k) sum += (uint64_t)((int64_t)A->pData[i * K + k] * B->pData[k * N + j]);
+      Cm->pData[i * N + j] = (int32_t)((int64_t)sum >> 31);
+    }
+  return ARM_MATH_SUCCESS;
+}

@@ -99,6 +99,12 @@ void oracle_arm_fir_init_q31(arm_fir_instance_q31 *S, uint16_t numTaps, const in
   S->numTaps = numTaps; S->pCoeffs = pCoeffs; S->pState = pState;
   memset(pState, 0, sizeof(int32_t) * ((size_t)numTaps + blockSize - 1));
 }
+void oracle_arm_mat_init_q15(arm_matrix_instance_q15 *S, uint16_t r, uint16_t c, int16_t *p) {
+  S->numRows = r; S->numCols = c; S->pData = p;
+}
+void oracle_arm_mat_init_q31(arm_matrix_instance_q31 *S, uint16_t r, uint16_t c, int32_t *p) {
+  S->numRows = r; S->numCols = c; S->pData = p;
+}
 void oracle_arm_mat_init_f32(arm_matrix_instance_f32 *S, uint16_t r, uint16_t c, float *p) {
   S->numRows = r; S->numCols = c; S->pData = p;
 }

@@ -223,3 +223,44 @@ def test_mat_mult_batch_normwise(dsp, torch_gpu, ref, m, k, n, batch):
     if m * k * n <= 256 ** 3:   # the reference itself on one item (seconds on the host)
         st, want = ref.mat_mult(a[0], b[0])
         assert np.abs(got[0] - want).max() <= 2 * bound
+
+
+# ------------------------------------------------------------------ mat mult q15 / q31
+@pytest.mark.parametrize("kind", ["q15", "q31"])
+@pytest.mark.parametrize("m,k,n,fill", [(1, 1, 1, None), (5, 7, 3, None), (64, 64, 64, None), (65, 130, 67, None),
+                                        (128, 2000, 96, None), (40, 64, 40, "min"), (40, 64, 40, "max"),
+                                        (33, 100, 31, "mixed"), (3, 33000, 2, None)])
+def test_mat_mult_fixed_bitexact(dsp, torch_gpu, ref, kind, m, k, n, fill):
+    """Byte-sliced i8-MFMA kernel (K <= 32704) and the VALU kernel beyond, vs the reference
+    build bit for bit, including all-extreme operands (q63 wrap for q31, saturation for q15)."""
+    bits, dt = (15, np.int16) if kind == "q15" else (31, np.int32)
+    rng = np.random.default_rng(m + 7 * k + 13 * n)
+    lo, hi = -(1 << bits), (1 << bits) - 1
+    if fill is None:
+        a = rng.integers(lo, hi, (m, k), endpoint=True).astype(dt)
+        b = rng.integers(lo, hi, (k, n), endpoint=True).astype(dt)
+    elif fill == "mixed":
+        a = rng.choice(np.array([lo, hi, 0, -1, 1], dtype=np.int64), (m, k)).astype(dt)
+        b = rng.choice(np.array([lo, hi, 0, -1, 1], dtype=np.int64), (k, n)).astype(dt)
+    else:
+        v = lo if fill == "min" else hi
+        a, b = np.full((m, k), v, dt), np.full((k, n), v, dt)
+    st, got = dsp.arm_mat_mult_fixed(kind, a, b)
+    st_r, want = ref.mat_mult_fixed(kind, a, b)
+    assert st == 0 and st_r == 0
+    assert got.tobytes() == want.tobytes(), np.argwhere(got != want)[:5]
+
+
+@pytest.mark.parametrize("kind", ["q15", "q31"])
+def test_mat_mult_fixed_batch(dsp, torch_gpu, ref, kind):
+    bits, dt = (15, np.int16) if kind == "q15" else (31, np.int32)
+    tdt = torch_gpu.int16 if kind == "q15" else torch_gpu.int32
+    rng = np.random.default_rng(9)
+    a = rng.integers(-(1 << bits), 1 << bits, (3, 96, 200)).astype(dt)
+    b = rng.integers(-(1 << bits), 1 << bits, (3, 200, 80)).astype(dt)
+    A, B = torch_gpu.from_numpy(a).cuda(), torch_gpu.from_numpy(b).cuda()
+    Cm = torch_gpu.empty((3, 96, 80), dtype=tdt, device="cuda")
+    dsp.mat_mult_batch(A, B, Cm)
+    got = Cm.cpu().numpy()
+    for i in range(3):
+        assert got[i].tobytes() == ref.mat_mult_fixed(kind, a[i], b[i])[1].tobytes(), i

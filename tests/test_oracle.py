@@ -98,3 +98,19 @@ def test_mat_mult_oracle_equals_reference(oracle, ref, m, k, n):
     b = rng.uniform(-1, 1, (k, n)).astype(np.float32)
     (sa, ca), (sb, cb) = oracle.mat_mult(a, b), ref.mat_mult(a, b)
     assert sa == sb == 0 and ca.tobytes() == cb.tobytes()
+
+
+@pytest.mark.parametrize("kind", ["q15", "q31"])
+@pytest.mark.parametrize("m,k,n,fill", [(1, 1, 1, None), (7, 13, 5, None), (33, 70, 17, None), (8, 64, 9, "min"),
+                                        (8, 64, 9, "max")])
+def test_mat_mult_fixed_oracle_equals_reference(oracle, ref, kind, m, k, n, fill):
+    bits, dt = (15, np.int16) if kind == "q15" else (31, np.int32)
+    rng = np.random.default_rng(m * 31 + k + n)
+    if fill is None:
+        a = rng.integers(-(1 << bits), 1 << bits, (m, k)).astype(dt)
+        b = rng.integers(-(1 << bits), 1 << bits, (k, n)).astype(dt)
+    else:
+        v = -(1 << bits) if fill == "min" else (1 << bits) - 1
+        a, b = np.full((m, k), v, dt), np.full((k, n), v, dt)
+    (sa, ca), (sb, cb) = oracle.mat_mult_fixed(kind, a, b), ref.mat_mult_fixed(kind, a, b)
+    assert sa == sb == 0 and ca.tobytes() == cb.tobytes()

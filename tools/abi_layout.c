@@ -25,6 +25,12 @@ int main(void) {
     F(arm_fir_instance_q15, pCoeffs) E()
   S(arm_matrix_instance_f32) F(arm_matrix_instance_f32, numRows) F(arm_matrix_instance_f32, numCols)
     F(arm_matrix_instance_f32, pData) E()
+  S(arm_matrix_instance_q15) F(arm_matrix_instance_q15, numRows) F(arm_matrix_instance_q15, numCols)
+    F(arm_matrix_instance_q15, pData) E()
+  S(arm_matrix_instance_q31) F(arm_matrix_instance_q31, numRows) F(arm_matrix_instance_q31, numCols)
+    F(arm_matrix_instance_q31, pData) E()
+  S(arm_fir_instance_q31) F(arm_fir_instance_q31, numTaps) F(arm_fir_instance_q31, pState)
+    F(arm_fir_instance_q31, pCoeffs) E()
   S(arm_mfcc_instance_f32) F(arm_mfcc_instance_f32, dctCoefs) F(arm_mfcc_instance_f32, filterCoefs)
     F(arm_mfcc_instance_f32, windowCoefs) F(arm_mfcc_instance_f32, filterPos) F(arm_mfcc_instance_f32, filterLengths)
     F(arm_mfcc_instance_f32, fftLen) F(arm_mfcc_instance_f32, nbMelFilters) F(arm_mfcc_instance_f32, nbDctOutputs)
