@@ -1,0 +1,197 @@
+"""`cmsisdsp`-compatible Python module over the MI355X library.
+
+Same function names, argument order and return conventions as the reference's CPython
+extension (PythonWrapper/cmsisdsp_pkg/src/cmsisdsp_transform.c, _filtering.c, _matrix.c,
+as exercised by PythonWrapper/examples/testdsp*.py, testrfft_all.py, testmfcc.py) for the
+functions this backend provides: numpy (or list) in, a new numpy array out, instances as
+opaque objects.  Every call runs on the GPU through libcmsisdsp_mi355x.so (the drop-in C
+ABI, host buffers staged through device memory); there is no CPU implementation here.
+
+    import sys; sys.path.insert(0, "cmsis-dsp_amd")
+    import cmsisdsp as dsp
+    S = dsp.arm_cfft_instance_f32(); dsp.arm_cfft_init_f32(S, 1024)
+    y = dsp.arm_cfft_f32(S, x, 0, 1)
+"""
+import ctypes as _C
+
+import numpy as _np
+
+import cmsisdsp_amd as _amd
+from cmsisdsp_amd import _abi
+from . import datatype  # noqa: F401
+
+_lib = _amd.lib
+
+
+def has_neon():
+    return False
+
+
+# ------------------------------------------------------------------ instances
+class _Instance:
+    _struct = None
+
+    def __init__(self):
+        self._s = self._struct()
+        self._keep = []
+
+    def __getattr__(self, name):            # accessor methods: inst.fftLen(), inst.numTaps() ...
+        s = object.__getattribute__(self, "_s")
+        if any(f == name for f, _ in s._fields_):
+            return lambda: getattr(s, name)
+        raise AttributeError(name)
+
+
+def _make(name, struct):
+    return type(name, (_Instance,), {"_struct": struct})
+
+
+arm_cfft_instance_f32 = _make("arm_cfft_instance_f32", _abi.arm_cfft_instance_f32)
+arm_cfft_instance_q31 = _make("arm_cfft_instance_q31", _abi.arm_cfft_instance_q31)
+arm_cfft_instance_q15 = _make("arm_cfft_instance_q15", _abi.arm_cfft_instance_q15)
+arm_rfft_fast_instance_f32 = _make("arm_rfft_fast_instance_f32", _abi.arm_rfft_fast_instance_f32)
+arm_fir_instance_f32 = _make("arm_fir_instance_f32", _abi.arm_fir_instance_f32)
+arm_fir_instance_q31 = _make("arm_fir_instance_q31", _abi.arm_fir_instance_q31)
+arm_fir_instance_q15 = _make("arm_fir_instance_q15", _abi.arm_fir_instance_q15)
+arm_mfcc_instance_f32 = _make("arm_mfcc_instance_f32", _abi.arm_mfcc_instance_f32)
+
+_DT = {"f32": _np.float32, "q31": _np.int32, "q15": _np.int16}
+
+
+def _arr(x, dt):
+    return _np.ascontiguousarray(_np.asarray(x).astype(dt, copy=False))
+
+
+def _check(what):
+    code, msg = _amd.last_error()
+    if code:
+        _lib.arm_mi355x_clear_error()
+        raise RuntimeError(f"{what}: device error {code}: {msg}")
+
+
+# ------------------------------------------------------------------ complex FFT
+def _cfft_init(kind):
+    def init(inst, fftLen):
+        return getattr(_lib, f"arm_cfft_init_{kind}")(_C.byref(inst._s), int(fftLen))
+    init.__name__ = f"arm_cfft_init_{kind}"
+    return init
+
+
+def _cfft(kind):
+    def run(inst, p1, ifftFlag, bitReverseFlag=1, tmp=None):
+        buf = _arr(p1, _DT[kind]).copy()
+        getattr(_lib, f"arm_cfft_{kind}")(_C.byref(inst._s), buf.ctypes.data, int(ifftFlag), int(bitReverseFlag))
+        _check(f"arm_cfft_{kind}")
+        return buf
+    run.__name__ = f"arm_cfft_{kind}"
+    return run
+
+
+arm_cfft_init_f32, arm_cfft_init_q31, arm_cfft_init_q15 = (_cfft_init(k) for k in ("f32", "q31", "q15"))
+arm_cfft_f32, arm_cfft_q31, arm_cfft_q15 = (_cfft(k) for k in ("f32", "q31", "q15"))
+
+
+def arm_cfft_tmp_buffer_size(dt, nbSamples, buf_id, arch=None):
+    return 0                                  # no user temporary: work space lives on the device
+
+
+def arm_cfft_output_buffer_size(dt, nbSamples, arch=None):
+    return 2 * int(nbSamples)
+
+
+# ------------------------------------------------------------------ real FFT (fast)
+def arm_rfft_fast_init_f32(inst, fftLen):
+    return _lib.arm_rfft_fast_init_f32(_C.byref(inst._s), int(fftLen))
+
+
+def arm_rfft_fast_f32(inst, p, ifftFlag, tmp=None):
+    src = _arr(p, _np.float32).copy()
+    out = _np.zeros(inst._s.fftLenRFFT, dtype=_np.float32)
+    _lib.arm_rfft_fast_f32(_C.byref(inst._s), src.ctypes.data, out.ctypes.data, int(ifftFlag))
+    _check("arm_rfft_fast_f32")
+    return out
+
+
+def arm_rfft_tmp_buffer_size(dt, nbSamples, buf_id, arch=None):
+    return 0
+
+
+def arm_rfft_output_buffer_size(dt, nbSamples, arch=None):
+    return int(nbSamples)
+
+
+def arm_rifft_input_buffer_size(dt, nbSamples, arch=None):
+    return int(nbSamples)
+
+
+# ------------------------------------------------------------------ FIR
+def _fir_init(kind):
+    def init(inst, numTaps, pCoeffs, pState):
+        c = _arr(pCoeffs, _DT[kind])
+        state = _arr(pState, _DT[kind]).copy()
+        block = max(1, len(state) - int(numTaps) + 1)
+        inst._keep = [c, state]
+        inst._block = block
+        getattr(_lib, f"arm_fir_init_{kind}")(_C.byref(inst._s), int(numTaps), c.ctypes.data, state.ctypes.data, block)
+        _check(f"arm_fir_init_{kind}")
+        return 0
+    init.__name__ = f"arm_fir_init_{kind}"
+    return init
+
+
+def _fir(name, kind):
+    def run(inst, pSrc):
+        x = _arr(pSrc, _DT[kind])
+        if len(x) > inst._block:
+            raise ValueError(f"{name}: {len(x)} samples > the blockSize the state was sized for ({inst._block})")
+        y = _np.zeros_like(x)
+        getattr(_lib, name)(_C.byref(inst._s), x.ctypes.data, y.ctypes.data, len(x))
+        _check(name)
+        return y
+    run.__name__ = name
+    return run
+
+
+arm_fir_init_f32, arm_fir_init_q31, arm_fir_init_q15 = (_fir_init(k) for k in ("f32", "q31", "q15"))
+arm_fir_f32 = _fir("arm_fir_f32", "f32")
+arm_fir_q31 = _fir("arm_fir_q31", "q31")
+arm_fir_q15 = _fir("arm_fir_q15", "q15")
+arm_fir_fast_q31 = _fir("arm_fir_fast_q31", "q31")
+arm_fir_fast_q15 = _fir("arm_fir_fast_q15", "q15")
+
+
+# ------------------------------------------------------------------ matrix multiply
+def arm_mat_mult_f32(pSrcA, pSrcB):
+    """(status, A @ B) as in the reference binding."""
+    return _amd.arm_mat_mult_f32(_arr(pSrcA, _np.float32), _arr(pSrcB, _np.float32))
+
+
+def arm_mat_mult_q31(pSrcA, pSrcB):
+    return _amd.arm_mat_mult_fixed("q31", _arr(pSrcA, _np.int32), _arr(pSrcB, _np.int32))
+
+
+def arm_mat_mult_q15(pSrcA, pSrcB, pState=None):
+    return _amd.arm_mat_mult_fixed("q15", _arr(pSrcA, _np.int16), _arr(pSrcB, _np.int16))
+
+
+# ------------------------------------------------------------------ MFCC
+def arm_mfcc_init_f32(inst, fftLen, nbMelFilters, nbDctOutputs, dctCoefs, filterPos, filterLengths,
+                      filterCoefs, windowCoefs):
+    keep = [_arr(dctCoefs, _np.float32).reshape(-1), _arr(filterPos, _np.uint32), _arr(filterLengths, _np.uint32),
+            _arr(filterCoefs, _np.float32), _arr(windowCoefs, _np.float32)]
+    inst._keep = keep
+    return _lib.arm_mfcc_init_f32(_C.byref(inst._s), int(fftLen), int(nbMelFilters), int(nbDctOutputs),
+                                  *[k.ctypes.data for k in keep])
+
+
+def arm_mfcc_f32(inst, pSrc, pTmp, tmp2=None):
+    src = _arr(pSrc, _np.float32).copy()
+    out = _np.zeros(inst._s.nbDctOutputs, dtype=_np.float32)
+    tmp = _np.zeros(2 * inst._s.fftLen, dtype=_np.float32)
+    _lib.arm_mfcc_f32(_C.byref(inst._s), src.ctypes.data, out.ctypes.data, tmp.ctypes.data)
+    _check("arm_mfcc_f32")
+    return out
+
+
+def arm_mfcc_tmp_buffer_size(dt, fftLen, buf_id, arch=None, use_cfft=0):
+    return 2 * int(fftLen) if buf_id == 1 else 0
