@@ -368,13 +368,14 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 #endif
   auto W = [](C c) { return make_int2(c.x, c.y); };
 
-  int2 v[16], nv[16];
+  int2 v[16];
+  C nv[16];                             // prefetch in the storage type (q15: one VGPR per complex)
   if (blockIdx.x < batch) {
     const C* X0 = data + (size_t)blockIdx.x * 4096;
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) nv[4 * a + b] = F::ld(X0 + t + 256 * a + 1024 * b);
+      for (int b = 0; b < 4; ++b) nv[4 * a + b] = X0[t + 256 * a + 1024 * b];
   }
   for (uint32_t tr = blockIdx.x; tr < batch; tr += gridDim.x) {
     C* X = data + (size_t)tr * 4096;
@@ -384,7 +385,7 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 #endif
     // ---------------- pass 1: stages 1 (first) and 2
 #pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = nv[u];
+    for (int u = 0; u < 16; ++u) v[u] = W(nv[u]);
 #pragma unroll
     for (int a = 0; a < 4; ++a)
       bfly<T, INV, 0>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], W(TW1(a, 0)), W(TW1(a, 1)), W(TW1(a, 2)));
@@ -400,7 +401,7 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) nv[4 * a + b] = F::ld(XN + t + 256 * a + 1024 * b);
+        for (int b = 0; b < 4; ++b) nv[4 * a + b] = XN[t + 256 * a + 1024 * b];
     }
     __syncthreads();
     // ---------------- pass 2: stages 3 and 4
