@@ -49,6 +49,7 @@ WORKLOADS = {
     "fir_fast_q31": ("fir_fast_q31", 128, 1 << 16, 8),
     "mat_mult_f32": ("mat", 1024, 256, None),
     "mfcc_f32": ("mfcc", 1024, 1 << 18, 4),
+    "rfft_f32": ("rfft", 1024, 1 << 20, 8),
     "mat_mult_q15": ("matq15", 1024, 64, None),
     "mat_mult_q31": ("matq31", 1024, 64, None),
 }
@@ -111,7 +112,8 @@ def cpu_baseline(workload, n):
     wl = {"cfft_f32_1024": "cfft_f32", "cfft_q31_4096": "cfft_q31", "cfft_q15_4096": "cfft_q15",
           "fir_f32": "fir_f32", "fir_q15": "fir_q15", "fir_q31": "fir_q31", "fir_fast_q15": "fir_fast_q15",
           "fir_fast_q31": "fir_fast_q31", "mat_mult_f32": "mat_mult_f32",
-          "mfcc_f32": "mfcc_f32", "mat_mult_q15": "mat_mult_q15", "mat_mult_q31": "mat_mult_q31"}[workload]
+          "mfcc_f32": "mfcc_f32", "mat_mult_q15": "mat_mult_q15", "mat_mult_q31": "mat_mult_q31",
+          "rfft_f32": "rfft_f32"}[workload]
     nn = 256 if workload.startswith("mat_mult") else n  # 1024^3 takes seconds per matrix on one core
     out = subprocess.run([exe, wl, str(nn), str(threads), str(secs)], capture_output=True, text=True,
                          timeout=120)
@@ -228,6 +230,26 @@ def run_mat(dim, batch, steps, warmup, world, rank):
                            "within_bound": bool(err <= bound)}
 
 
+def run_rfft(n, batch, steps, warmup, world, rank):
+    """arm_rfft_fast_f32 forward over [batch][n] real frames -> [batch][n] packed spectra
+    (the forward transform also overwrites its input, as in the reference)."""
+    S = dsp.const_instance(f"arm_rfft_fast_sR_f32_len{n}")
+    p = synth("f32", batch * n, rank).view(batch, n)
+    out = torch.empty_like(p)
+    def launch(s):
+        dsp.rfft_fast_batch(S, p, out, 0)
+
+    wall, kern_ms = time_launches(launch, steps, warmup, world)
+    host, hk = cpu_checker()
+    fresh = synth("f32", 64 * n, rank, salt=41).view(64, n)
+    want = np.stack([host.rfft(n, r, 0)[0] for r in fresh.cpu().numpy()])
+    fo = torch.empty_like(fresh)
+    dsp.rfft_fast_batch(S, fresh.clone(), fo, 0)
+    torch.cuda.synchronize()
+    ok = fo.cpu().numpy().tobytes() == want.tobytes()
+    return wall, kern_ms, {"checker": hk, "bit_exact": bool(ok), "transforms_checked": 64}
+
+
 def run_mfcc(n, batch, steps, warmup, world, rank):
     import mfcc_cfg
     g = mfcc_cfg.golden()
@@ -295,7 +317,7 @@ def main():
     WORLD = parallel.init(backend=args.dist_backend)
     world, rank = WORLD.size, WORLD.rank
     kind, n, batch0, bps = WORKLOADS[args.workload]
-    if args.fftlen and args.workload.startswith("cfft"):
+    if args.fftlen and args.workload.startswith(("cfft", "rfft")):
         batch0 = max(1, batch0 * n // args.fftlen)
         n = args.fftlen
     batch = args.batch or batch0
@@ -311,6 +333,10 @@ def main():
         wall, kern_ms, parity = run_mat_fixed(kind[3:], n, batch, args.steps, args.warmup, world, rank)
         units = batch
         algo_bytes = None
+    elif args.workload == "rfft_f32":
+        wall, kern_ms, parity = run_rfft(n, batch, args.steps, args.warmup, world, rank)
+        units = batch * n                                  # real input samples
+        algo_bytes = units * bps                           # N floats in, N floats out
     elif args.workload == "mfcc_f32":
         wall, kern_ms, parity = run_mfcc(n, batch, args.steps, args.warmup, world, rank)
         units = batch * n                                  # input samples
@@ -352,11 +378,14 @@ def main():
                     dtype={"f32": "f32", "q31": "q31 (int32)", "q15": "q15 (int16)", "fir_f32": "f32",
                            "fir_q15": "q15 (int16 x int16 -> int64)", "mfcc": "f32",
                            "fir_q31": "q31 (int32 x int32 -> int64)", "fir_fast_q15": "q15 (int32 wrap accumulator)",
-                           "fir_fast_q31": "q31 (rounded high-word accumulator)"}[kind])
+                           "fir_fast_q31": "q31 (rounded high-word accumulator)", "rfft": "f32"}[kind])
         if args.workload.startswith("cfft"):
             line["config"] = {"workload": f"arm_cfft_{kind} N={n} batch={batch}/GPU in place, bitReverseFlag=1, "
                                           f"alternating fwd/inv (BASELINE configs[{1 if kind == 'f32' else 3}])",
                               "fftLen": n, "batch_per_gpu": batch, "parallelism": f"dp{world} shards"}
+        elif kind == "rfft":
+            line["config"] = {"workload": f"arm_rfft_fast_f32 N={n} forward, batch={batch}/GPU", "fftLen": n,
+                              "batch_per_gpu": batch, "parallelism": f"dp{world} shards"}
         elif kind == "mfcc":
             line["config"] = {"workload": f"arm_mfcc_f32 fftLen={n} 20 Mel / 13 DCT (reference MFCC F32 suite "
                                           f"tables) batch={batch} frames/GPU", "fftLen": n, "batch_per_gpu": batch,
@@ -370,6 +399,9 @@ def main():
         line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.workload),
                             "algorithmic_bytes_per_launch": algo_bytes, "avg_kernel_ms": round(kern_ms, 4)}
+        if args.workload == "rfft_f32":
+            # the forward transform also leaves the inner CFFT output in p (reference semantics)
+            line["roofline"]["bytes_moved_per_sample"] = 12
         if args.workload == "fir_fast_q15":
             valu = units * n / 2 / (kern_ms * 1e-3) * 1e-12      # one accumulating v_dot2 per tap pair
             line["roofline"]["valu_tops_dot2"] = {"achieved": round(valu, 2), "peak": FP32_NOFMA_TFLOPS,

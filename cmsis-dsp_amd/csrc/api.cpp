@@ -106,6 +106,13 @@ bool rfft_run(const arm_rfft_fast_instance_f32* S, float* d_p, float* d_out, uin
   // the inner CFFT receives ifftFlag unchanged and bitReverseFlag = 1 (:689, :694)
   if (!cfft_prepare(h, S->Sint.pTwiddle, S->Sint.pBitRevTable, S->Sint.bitRevLength, 0, ifftFlag, 1, pr))
     return false;
+  if (!pr.perm && ifftFlag <= 1) {   // the reference's own tables: one fused launch
+    // (ifftFlag > 1: merge + a FORWARD inner CFFT, arm_cfft_f32.c:1252 -- unfused path)
+    MI_CHECK(rfft_f32_fused_launch((int)n, ifftFlag != 0, d_p, ifftFlag ? nullptr : d_p, d_out, batch,
+                                   (const float*)pr.tw, (const float*)twr, st),
+             "rfft fused");
+    return true;
+  }
   if (ifftFlag) {
     MI_CHECK(rfft_f32_merge_launch((int)n, d_p, d_out, batch, (const float*)twr, st), "rfft merge");
     MI_CHECK(cfft_f32_launch((int)h, d_out, batch, (const float*)pr.tw, pr.perm, pr.flags, st), "rfft cfft");

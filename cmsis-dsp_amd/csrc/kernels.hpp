@@ -38,6 +38,11 @@ hipError_t cfft_q15_launch(int n, int16_t* data, uint32_t batch, const int16_t* 
 // Real FFT split (forward, after the N/2 CFFT) / merge (inverse, before it) passes.
 hipError_t rfft_f32_stage_launch(int n_real, const float* p, float* out, uint32_t batch,
                                  const float* tw_rfft, hipStream_t st);
+// Single-launch RFFT for the reference's canonical CFFT tables: tw = CFFT(n/2) twiddles,
+// tw_rfft = twiddleCoef_rfft_n.  Forward writes the spectrum to `out` and, when pcopy is
+// non-null, the inner CFFT output to pcopy (the reference leaves it in p).
+hipError_t rfft_f32_fused_launch(int n_real, bool inverse, const float* p, float* pcopy, float* out, uint32_t batch,
+                                 const float* tw, const float* tw_rfft, hipStream_t st);
 hipError_t rfft_f32_merge_launch(int n_real, const float* p, float* out, uint32_t batch,
                                  const float* tw_rfft, hipStream_t st);
 

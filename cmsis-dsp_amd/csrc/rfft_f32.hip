@@ -3,10 +3,17 @@
 // arm_rfft_fast_f32 (Source/TransformFunctions/arm_rfft_fast_f32.c:675-699) is
 //   forward: arm_cfft_f32(Sint, p, 0, 1) then stage_rfft_f32 (:316-402)
 //   inverse: merge_rfft_f32 (:405-462) then arm_cfft_f32(Sint, pOut, 1, 1).
-// The CFFT runs through cfft_f32_launch; these kernels are the O(N) passes, one thread
-// per output complex bin, with the reference's expression trees kept verbatim.
+// Fused path (rfft_fused_kernel<H, INV>, the reference's own CFFT tables): one launch per
+// batch.  Forward: frames -> LDS, the shared bit-exact CFFT(H) core (cfft_f32_core.hpp),
+// then the split evaluated straight from the digit-reversed CFFT image and stored with the
+// CFFT output itself (the reference leaves it in p) -- 12 B moved per real sample instead
+// of 16.  Inverse: the merge evaluated while loading, the inverse CFFT core, the reversal,
+// conjugate and 1/H scaling on the store -- 8 B per sample instead of 16.
+// Unfused path (custom CFFT tables): cfft_f32_launch plus the O(N) passes below, one
+// thread per output complex bin, with the reference's expression trees kept verbatim.
 #include "common.hpp"
 #include "kernels.hpp"
+#include "cfft_f32_core.hpp"
 
 #pragma clang fp contract(off)
 
@@ -50,6 +57,113 @@ __global__ __launch_bounds__(kBlock) void rfft_merge_kernel(const float2* __rest
   const float t1a = A.x - B.x, t1b = A.y + B.y;
   const float r = w.x * t1a, s = w.y * t1b, tt = w.y * t1a, u = w.x * t1b;
   out[t * H + i] = make_float2(0.5f * (A.x + B.x - r - s), 0.5f * (A.y - B.y + tt - u));
+}
+
+// forward split of bin i from the CFFT image x (frequency k at x[f32_src<H>(k)])
+template <int H>
+__device__ __forceinline__ float2 split_bin(const float2* x, int i, const float2* __restrict__ tw) {
+  if (i == 0) {                                       // arm_rfft_fast_f32.c:335-353
+    const float2 a = x[f32_src<H>(0)];
+    const float t1a = a.x + a.x, t1b = a.y + a.y;
+    return make_float2(0.5f * (t1a + t1b), 0.5f * (t1a - t1b));
+  }
+  const float2 A = x[f32_src<H>(i)], B = x[f32_src<H>(H - i)], w = tw[i];
+  const float t1a = B.x - A.x, t1b = B.y + A.y;
+  const float p0 = w.x * t1a, p1 = w.y * t1a, p2 = w.x * t1b, p3 = w.y * t1b;
+  return make_float2(0.5f * (A.x + B.x + p0 + p3), 0.5f * (A.y - B.y + p1 - p2));
+}
+
+// inverse merge of bin i from the packed half spectrum p (arm_rfft_fast_f32.c:405-462)
+__device__ __forceinline__ float2 merge_bin(const float2* __restrict__ x, int i, int H, const float2* __restrict__ tw) {
+  if (i == 0) {
+    const float2 a = x[0];
+    return make_float2(0.5f * (a.x + a.y), 0.5f * (a.x - a.y));
+  }
+  const float2 A = x[i], B = x[H - i], w = tw[i];
+  const float t1a = A.x - B.x, t1b = A.y + B.y;
+  const float r = w.x * t1a, s = w.y * t1b, tt = w.y * t1a, u = w.x * t1b;
+  return make_float2(0.5f * (A.x + B.x - r - s), 0.5f * (A.y - B.y + tt - u));
+}
+
+template <int H, bool INV>
+// src and pcopy may alias (forward: the CFFT output goes back to p): every frame is read
+// into LDS before the barrier and written after it, by the same workgroup.
+__global__ __launch_bounds__(kBlock) void rfft_fused_kernel(const float2* src, float2* pcopy,
+                                                            float2* __restrict__ dst, uint32_t batch,
+                                                            const float2* __restrict__ tw,
+                                                            const float2* __restrict__ twr) {
+  using P = PlanF32<H>;
+  constexpr int SP = H + (P::LPT <= 4 ? 1 : 0);      // as the batched CFFT's LDS image
+  __shared__ __attribute__((aligned(16))) float2 lds[P::TPB * SP];
+  const int tid = threadIdx.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * P::TPB;
+  const int valid = (int)min<uint64_t>((uint64_t)P::TPB, batch - t0);
+  const int n4 = valid * H / 2;                      // float4 (two bins) per item
+  {
+    const float4* s4 = reinterpret_cast<const float4*>(src + t0 * H);
+#pragma unroll 4
+    for (int i = tid; i < n4; i += kBlock) {
+      const int e = 2 * i, t = e / H, k = e % H;
+      float2 a, b;
+      if (INV) {                                      // merge, then conj for the inverse CFFT
+        const float2* x = src + (t0 + t) * H;
+        a = merge_bin(x, k, H, twr);
+        b = merge_bin(x, k + 1, H, twr);
+        a.y = -a.y; b.y = -b.y;
+      } else {
+        const float4 v = s4[i];
+        a = make_float2(v.x, v.y); b = make_float2(v.z, v.w);
+      }
+      lds[t * SP + k] = a;
+      lds[t * SP + k + 1] = b;
+    }
+  }
+  __syncthreads();
+  const int tr = tid / P::LPT, lane = tid % P::LPT;
+  cfft_f32_lds_fwd<H>(lds + tr * SP, lane, tw);
+  float4* d4 = reinterpret_cast<float4*>(dst + t0 * H);
+  float4* p4 = pcopy ? reinterpret_cast<float4*>(pcopy + t0 * H) : nullptr;
+  const float invL = 1.0f / (float)H;
+#pragma unroll 4
+  for (int i = tid; i < n4; i += kBlock) {
+    const int e = 2 * i, t = e / H, k = e % H;
+    const float2* x = lds + t * SP;
+    if (INV) {                                        // reversal, conj, 1/H (arm_cfft_f32.c:1282-1297)
+      float2 a = x[f32_src<H>(k)], b = x[f32_src<H>(k + 1)];
+      a.x = a.x * invL; a.y = -a.y * invL;
+      b.x = b.x * invL; b.y = -b.y * invL;
+      d4[i] = make_float4(a.x, a.y, b.x, b.y);
+    } else {
+      const float2 a = split_bin<H>(x, k, twr), b = split_bin<H>(x, k + 1, twr);
+      d4[i] = make_float4(a.x, a.y, b.x, b.y);
+      if (p4) {                                       // the reference leaves the CFFT output in p
+        const float2 ca = x[f32_src<H>(k)], cb = x[f32_src<H>(k + 1)];
+        p4[i] = make_float4(ca.x, ca.y, cb.x, cb.y);
+      }
+    }
+  }
+}
+
+template <int H>
+static hipError_t launch_fused(bool inv, const float* p, float* pcopy, float* out, uint32_t batch, const float* tw,
+                               const float* twr, hipStream_t st) {
+  using P = PlanF32<H>;
+  const uint32_t grid = (uint32_t)((batch + P::TPB - 1) / P::TPB);
+  auto k = inv ? rfft_fused_kernel<H, true> : rfft_fused_kernel<H, false>;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, st, (const float2*)p, (float2*)pcopy, (float2*)out, batch,
+                     (const float2*)tw, (const float2*)twr);
+  return hipGetLastError();
+}
+
+hipError_t rfft_f32_fused_launch(int n_real, bool inverse, const float* p, float* pcopy, float* out, uint32_t batch,
+                                 const float* tw, const float* tw_rfft, hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  switch (n_real) {
+#define MI_RF(N) case N: return launch_fused<N / 2>(inverse, p, pcopy, out, batch, tw, tw_rfft, st);
+    MI_RF(32) MI_RF(64) MI_RF(128) MI_RF(256) MI_RF(512) MI_RF(1024) MI_RF(2048) MI_RF(4096)
+#undef MI_RF
+    default: return hipErrorInvalidValue;
+  }
 }
 
 static hipError_t launch_pass(bool merge, int n_real, const float* p, float* out, uint32_t batch,

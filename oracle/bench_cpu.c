@@ -32,6 +32,7 @@ arm_status oracle_arm_cfft_init_q31(arm_cfft_instance_q31 *S, uint16_t n);
 arm_status oracle_arm_cfft_init_q15(arm_cfft_instance_q15 *S, uint16_t n);
 void oracle_arm_fir_init_f32(arm_fir_instance_f32 *S, uint16_t numTaps, const float *pCoeffs, float *pState,
                              uint32_t blockSize);
+arm_status oracle_arm_rfft_fast_init_f32(arm_rfft_fast_instance_f32 *S, uint16_t n);
 void oracle_arm_fir_init_q31(arm_fir_instance_q31 *S, uint16_t numTaps, const int32_t *pCoeffs, int32_t *pState,
                              uint32_t blockSize);
 arm_status oracle_arm_fir_init_q15(arm_fir_instance_q15 *S, uint16_t numTaps, const int16_t *pCoeffs,
@@ -117,6 +118,17 @@ static void *worker(void *arg) {
       samples += block;
     } while (now() - t0 < j->seconds);
     free(c); free(st); free(in); free(out);
+  } else if (!strcmp(j->wl, "rfft_f32")) {
+    const int n = j->n;
+    float *x = malloc(sizeof(float) * n), *p = malloc(sizeof(float) * n), *o = malloc(sizeof(float) * n);
+    for (int i = 0; i < n; ++i) x[i] = uni(&seed);
+    arm_rfft_fast_instance_f32 S;
+    F(arm_rfft_fast_init_f32)(&S, (uint16_t)n);
+    do {
+      for (int r = 0; r < 16; ++r) { memcpy(p, x, sizeof(float) * n); F(arm_rfft_fast_f32)(&S, p, o, 0); }
+      samples += 16.0 * n;
+    } while (now() - t0 < j->seconds);
+    free(x); free(p); free(o);
   } else if (!strcmp(j->wl, "mfcc_f32")) {
     const int n = j->n, nm = 20, nd = 13;
     uint32_t pos[20], len[20], total = 0;

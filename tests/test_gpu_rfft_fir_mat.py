@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 # ------------------------------------------------------------------ RFFT fast
 @pytest.mark.parametrize("n", [32, 64, 128, 256, 512, 1024, 2048, 4096])
-@pytest.mark.parametrize("ifft", [0, 1])
+@pytest.mark.parametrize("ifft", [0, 1, 2])   # 2: merge + forward inner CFFT (unfused path)
 def test_rfft_batch_bitexact(dsp, torch_gpu, ref, n, ifft):
     torch = torch_gpu
     batch = 19
