@@ -45,8 +45,8 @@ __global__ __launch_bounds__(kBlock) void cfft_f32_kernel(float2* __restrict__ d
       float4 v = src[i];
       if (ifft) { v.y = -v.y; v.w = -v.w; }
       const int e = 2 * i, t = e / N, k = e % N;
-      lds[t * SP + k] = make_float2(v.x, v.y);
-      lds[t * SP + k + 1] = make_float2(v.z, v.w);
+      lds[t * SP + swz<N>(k)] = make_float2(v.x, v.y);
+      lds[t * SP + swz<N>(k + 1)] = make_float2(v.z, v.w);
     }
   }
   __syncthreads();
@@ -69,9 +69,9 @@ __global__ __launch_bounds__(kBlock) void cfft_f32_kernel(float2* __restrict__ d
       if (brev) {
         const int sa = perm ? perm[k] : f32_src<N>(k);
         const int sb = perm ? perm[k + 1] : f32_src<N>(k + 1);
-        a = lds[t * SP + sa]; b = lds[t * SP + sb];
+        a = lds[t * SP + swz<N>(sa)]; b = lds[t * SP + swz<N>(sb)];
       } else {
-        a = lds[t * SP + k]; b = lds[t * SP + k + 1];
+        a = lds[t * SP + swz<N>(k)]; b = lds[t * SP + swz<N>(k + 1)];
       }
       if (ifft) {
         a.x = a.x * invL; a.y = -a.y * invL;

@@ -101,9 +101,21 @@ template <int N> __device__ __forceinline__ int f32_src(int k) {
 // digit-reversed order out: frequency k sits at x[f32_src<N>(k)]), computed by the LPT =
 // N/16 lanes `lane` = 0..LPT-1 of its group.  Every thread of the workgroup must call it
 // (it contains __syncthreads); the first pass and stages follow arm_cfft_f32.c:1263-1280.
+// LDS image index of element i of a length-N transform: for N >= 512 (whole waves inside
+// one transform) bits 1-4 are XORed with bits 4-7, which takes the radix-8 stages' strided
+// patterns from 4-8-way bank conflicts down to 1-2 (bijective on every aligned 256-block;
+// modelled over all stage access patterns).  Every LDS access to a
+// transform image -- here and in the kernels that load / store it -- goes through swz<N>.
+template <int N>
+__device__ __forceinline__ int swz(int i) {
+  if constexpr (N >= 512) return i ^ (((i >> 4) & 15) << 1);
+  else return i;
+}
+
 template <int N>
 __device__ __forceinline__ void cfft_f32_lds_fwd(float2* __restrict__ x, int lane, const float2* __restrict__ tw) {
   using P = PlanF32<N>;
+#define XS(i) x[swz<N>(i)]
   // ---- first pass
   if constexpr (P::FIRST == 2) {
     // arm_cfft_radix8by2_f32, arm_cfft_f32.c:867-951
@@ -112,13 +124,13 @@ __device__ __forceinline__ void cfft_f32_lds_fwd(float2* __restrict__ x, int lan
     for (int it = 0; it < Q / P::LPT; ++it) {
       const int k = lane + it * P::LPT;
       const float2 w = tw[k];
-      float2 a = x[k], b = x[k + H], c = x[k + Q], d = x[k + H + Q];
-      x[k] = make_float2(a.x + b.x, a.y + b.y);
+      float2 a = XS(k), b = XS(k + H), c = XS(k + Q), d = XS(k + H + Q);
+      XS(k) = make_float2(a.x + b.x, a.y + b.y);
       float2 t2 = make_float2(a.x - b.x, a.y - b.y);
-      x[k + Q] = make_float2(c.x + d.x, c.y + d.y);
+      XS(k + Q) = make_float2(c.x + d.x, c.y + d.y);
       float2 t4 = make_float2(d.x - c.x, d.y - c.y);
-      x[k + H] = make_float2(t2.x * w.x + t2.y * w.y, t2.y * w.x - t2.x * w.y);
-      x[k + H + Q] = make_float2(t4.x * w.y - t4.y * w.x, t4.y * w.y + t4.x * w.x);
+      XS(k + H) = make_float2(t2.x * w.x + t2.y * w.y, t2.y * w.x - t2.x * w.y);
+      XS(k + H + Q) = make_float2(t4.x * w.y - t4.y * w.x, t4.y * w.y + t4.x * w.x);
     }
     __syncthreads();
   } else if constexpr (P::FIRST == 4) {
@@ -130,23 +142,23 @@ __device__ __forceinline__ void cfft_f32_lds_fwd(float2* __restrict__ x, int lan
       const int w = lane + it * P::LPT;
       if (w <= E) {
         const int k = w;
-        float2 A = x[k], B = x[k + Q], C = x[k + 2 * Q], D = x[k + 3 * Q];
+        float2 A = XS(k), B = XS(k + Q), C = XS(k + 2 * Q), D = XS(k + 3 * Q);
         float ap0 = A.x + C.x, as0 = A.x - C.x, ap1 = A.y + C.y, as1 = A.y - C.y;
         float2 t2 = make_float2(as0 + B.y - D.y, as1 - B.x + D.x);
         float2 t3 = make_float2(ap0 - B.x - D.x, ap1 - B.y - D.y);
         float2 t4 = make_float2(as0 - B.y + D.y, as1 + B.x - D.x);
-        x[k] = make_float2(ap0 + B.x + D.x, ap1 + B.y + D.y);
+        XS(k) = make_float2(ap0 + B.x + D.x, ap1 + B.y + D.y);
         if (k == 0) {
-          x[k + Q] = t2; x[k + 2 * Q] = t3; x[k + 3 * Q] = t4;
+          XS(k + Q) = t2; XS(k + 2 * Q) = t3; XS(k + 3 * Q) = t4;
         } else {
           const float2 w2 = tw[k], w3 = tw[2 * k], w4 = tw[3 * k];
-          x[k + Q]     = make_float2(t2.x * w2.x + t2.y * w2.y, t2.y * w2.x - t2.x * w2.y);
-          x[k + 2 * Q] = make_float2(t3.x * w3.x + t3.y * w3.y, t3.y * w3.x - t3.x * w3.y);
-          x[k + 3 * Q] = make_float2(t4.x * w4.x + t4.y * w4.y, t4.y * w4.x - t4.x * w4.y);
+          XS(k + Q)     = make_float2(t2.x * w2.x + t2.y * w2.y, t2.y * w2.x - t2.x * w2.y);
+          XS(k + 2 * Q) = make_float2(t3.x * w3.x + t3.y * w3.y, t3.y * w3.x - t3.x * w3.y);
+          XS(k + 3 * Q) = make_float2(t4.x * w4.x + t4.y * w4.y, t4.y * w4.x - t4.x * w4.y);
         }
       } else {
         const int i = w - E, kb = Q - i;
-        float2 A = x[kb], B = x[kb + Q], C = x[kb + 2 * Q], D = x[kb + 3 * Q];
+        float2 A = XS(kb), B = XS(kb + Q), C = XS(kb + 2 * Q), D = XS(kb + 3 * Q);
         float ap1 = A.x + C.x, as1 = A.x - C.x, ap0 = A.y + C.y, as0 = A.y - C.y;
         float t22 = B.y - D.y + as1;
         float t23 = A.y - C.y - B.x + D.x;
@@ -154,11 +166,11 @@ __device__ __forceinline__ void cfft_f32_lds_fwd(float2* __restrict__ x, int lan
         float t33 = ap0 - B.y - D.y;
         float t42 = B.y - D.y - as1;
         float t43 = D.x - B.x - as0;
-        x[kb] = make_float2(ap1 + B.x + D.x, ap0 + B.y + D.y);
+        XS(kb) = make_float2(ap1 + B.x + D.x, ap0 + B.y + D.y);
         const float2 w2 = tw[i], w3 = tw[2 * i], w4 = tw[3 * i];
-        x[kb + Q]     = make_float2(t22 * w2.y + t23 * w2.x, t23 * w2.y - t22 * w2.x);
-        x[kb + 2 * Q] = make_float2(t33 * w3.y - t32 * w3.x, -t33 * w3.x - t32 * w3.y);
-        x[kb + 3 * Q] = make_float2(t42 * w4.y + t43 * w4.x, t43 * w4.y - t42 * w4.x);
+        XS(kb + Q)     = make_float2(t22 * w2.y + t23 * w2.x, t23 * w2.y - t22 * w2.x);
+        XS(kb + 2 * Q) = make_float2(t33 * w3.y - t32 * w3.x, -t33 * w3.x - t32 * w3.y);
+        XS(kb + 3 * Q) = make_float2(t42 * w4.y + t43 * w4.x, t43 * w4.y - t42 * w4.x);
       }
     }
     __syncthreads();
@@ -175,10 +187,10 @@ __device__ __forceinline__ void cfft_f32_lds_fwd(float2* __restrict__ x, int lan
       const int b = lane + r * P::LPT;
       const int c = b / (L / 8), rr = b % (L / 8);
       const int j = rr % n2, q = rr / n2;
-      float2* base = x + c * L + q * n1 + j;
+      const int bi = c * L + q * n1 + j;
       float2 v[8];
 #pragma unroll
-      for (int m = 0; m < 8; ++m) v[m] = base[m * n2];
+      for (int m = 0; m < 8; ++m) v[m] = XS(bi + m * n2);
       if (j == 0) {
         r8<false>(v, nullptr);
       } else {
@@ -188,11 +200,12 @@ __device__ __forceinline__ void cfft_f32_lds_fwd(float2* __restrict__ x, int lan
         r8<true>(v, w);
       }
 #pragma unroll
-      for (int m = 0; m < 8; ++m) base[m * n2] = v[m];
+      for (int m = 0; m < 8; ++m) XS(bi + m * n2) = v[m];
     }
     __syncthreads();
   }
 
+#undef XS
 }
 
 }  // namespace mi355x

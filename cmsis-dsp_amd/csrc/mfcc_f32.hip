@@ -154,12 +154,16 @@ __global__ __launch_bounds__(kBlock) void mfcc_fused_kernel(const float* __restr
   for (int i = tid; i < H; i += kBlock) { tws[i] = tw[i]; twrs[i] = twr[i]; }
   const uint64_t f0 = (uint64_t)blockIdx.x * TPB;
   const int valid = (int)min<uint64_t>((uint64_t)TPB, batch - f0);
-  {  // frames -> LDS, 16-B coalesced; frames past the batch end are zero-filled
+  {  // frames -> LDS (swizzled image), 16-B coalesced; frames past the batch end are zero-filled
     const float4* s4 = reinterpret_cast<const float4*>(src + f0 * NF);
-    float4* d4 = reinterpret_cast<float4*>(lds);
     const int n_valid = valid * (NF / 4);
 #pragma unroll 4
-    for (int i = tid; i < TPB * (NF / 4); i += kBlock) d4[i] = i < n_valid ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = tid; i < TPB * (NF / 4); i += kBlock) {
+      const float4 v = i < n_valid ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int e = 2 * i, t = e / H, k = e % H;
+      lds[t * H + swz<H>(k)] = make_float2(v.x, v.y);
+      lds[t * H + swz<H>(k + 1)] = make_float2(v.z, v.w);
+    }
   }
   __syncthreads();
   const int tr = tid / LPT, lane = tid % LPT;
@@ -169,7 +173,10 @@ __global__ __launch_bounds__(kBlock) void mfcc_fused_kernel(const float* __restr
   // ---- max |x| over the frame's LPT lanes (arm_absmax_f32; order-free for the max value)
   float m = 0.0f;
 #pragma unroll 4
-  for (int j = lane; j < NF; j += LPT) m = fmaxf(m, fabsf(xf[j]));
+  for (int j = lane; j < H; j += LPT) {
+    const float2 v = x[swz<H>(j)];
+    m = fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y)));
+  }
   if constexpr (LPT <= 64) {
 #pragma unroll
     for (int o = LPT / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
@@ -184,10 +191,11 @@ __global__ __launch_bounds__(kBlock) void mfcc_fused_kernel(const float* __restr
   const bool scale = m != 0.0f;
   const float inv = scale ? 1.0f / m : 1.0f;          // arm_mfcc_f32.c:102-105
 #pragma unroll 4
-  for (int j = lane; j < NF; j += LPT) {
-    float v = xf[j];
-    if (scale) v = v * inv;
-    xf[j] = v * win[j];                               // arm_mult_f32
+  for (int j = lane; j < H; j += LPT) {
+    float2 v = x[swz<H>(j)];
+    if (scale) { v.x = v.x * inv; v.y = v.y * inv; }
+    const float2 w = reinterpret_cast<const float2*>(win)[j];
+    x[swz<H>(j)] = make_float2(v.x * w.x, v.y * w.y);  // arm_mult_f32
   }
   __syncthreads();
 
@@ -201,12 +209,12 @@ __global__ __launch_bounds__(kBlock) void mfcc_fused_kernel(const float* __restr
     const int k = lane + i * LPT;
     float re, im;
     if (k == 0) {
-      const float2 a = x[f32_src<H>(0)];
+      const float2 a = x[swz<H>(f32_src<H>(0))];
       const float t1a = a.x + a.x, t1b = a.y + a.y;
       re = 0.5f * (t1a + t1b);
       im = 0.0f;                                      // pTmp[1] = 0 (arm_mfcc_f32.c:125)
     } else {
-      const float2 A = x[f32_src<H>(k)], B = x[f32_src<H>(H - k)], w = twrs[k];
+      const float2 A = x[swz<H>(f32_src<H>(k))], B = x[swz<H>(f32_src<H>(H - k))], w = twrs[k];
       const float t1a = B.x - A.x, t1b = B.y + A.y;
       const float p0 = w.x * t1a, p1 = w.y * t1a, p2 = w.x * t1b, p3 = w.y * t1b;
       re = 0.5f * (A.x + B.x + p0 + p3);

@@ -63,11 +63,11 @@ __global__ __launch_bounds__(kBlock) void rfft_merge_kernel(const float2* __rest
 template <int H>
 __device__ __forceinline__ float2 split_bin(const float2* x, int i, const float2* __restrict__ tw) {
   if (i == 0) {                                       // arm_rfft_fast_f32.c:335-353
-    const float2 a = x[f32_src<H>(0)];
+    const float2 a = x[swz<H>(f32_src<H>(0))];
     const float t1a = a.x + a.x, t1b = a.y + a.y;
     return make_float2(0.5f * (t1a + t1b), 0.5f * (t1a - t1b));
   }
-  const float2 A = x[f32_src<H>(i)], B = x[f32_src<H>(H - i)], w = tw[i];
+  const float2 A = x[swz<H>(f32_src<H>(i))], B = x[swz<H>(f32_src<H>(H - i))], w = tw[i];
   const float t1a = B.x - A.x, t1b = B.y + A.y;
   const float p0 = w.x * t1a, p1 = w.y * t1a, p2 = w.x * t1b, p3 = w.y * t1b;
   return make_float2(0.5f * (A.x + B.x + p0 + p3), 0.5f * (A.y - B.y + p1 - p2));
@@ -114,8 +114,8 @@ __global__ __launch_bounds__(kBlock) void rfft_fused_kernel(const float2* src, f
         const float4 v = s4[i];
         a = make_float2(v.x, v.y); b = make_float2(v.z, v.w);
       }
-      lds[t * SP + k] = a;
-      lds[t * SP + k + 1] = b;
+      lds[t * SP + swz<H>(k)] = a;
+      lds[t * SP + swz<H>(k + 1)] = b;
     }
   }
   __syncthreads();
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(kBlock) void rfft_fused_kernel(const float2* src, f
     const int e = 2 * i, t = e / H, k = e % H;
     const float2* x = lds + t * SP;
     if (INV) {                                        // reversal, conj, 1/H (arm_cfft_f32.c:1282-1297)
-      float2 a = x[f32_src<H>(k)], b = x[f32_src<H>(k + 1)];
+      float2 a = x[swz<H>(f32_src<H>(k))], b = x[swz<H>(f32_src<H>(k + 1))];
       a.x = a.x * invL; a.y = -a.y * invL;
       b.x = b.x * invL; b.y = -b.y * invL;
       d4[i] = make_float4(a.x, a.y, b.x, b.y);
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(kBlock) void rfft_fused_kernel(const float2* src, f
       const float2 a = split_bin<H>(x, k, twr), b = split_bin<H>(x, k + 1, twr);
       d4[i] = make_float4(a.x, a.y, b.x, b.y);
       if (p4) {                                       // the reference leaves the CFFT output in p
-        const float2 ca = x[f32_src<H>(k)], cb = x[f32_src<H>(k + 1)];
+        const float2 ca = x[swz<H>(f32_src<H>(k))], cb = x[swz<H>(f32_src<H>(k + 1))];
         p4[i] = make_float4(ca.x, ca.y, cb.x, cb.y);
       }
     }
