@@ -372,7 +372,7 @@ def main():
         achieved = flops / (kern_ms * 1e-3) * 1e-12
         line["roofline"] = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                             "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-                            "traffic": pmc_traffic(args.workload)}
+                            "traffic": pmc_traffic(args.workload), "avg_kernel_ms": round(kern_ms, 4)}
     else:
         line.update(value=round(total_units / wall * 1e-9, 3), unit="Gsamples/s",
                     dtype={"f32": "f32", "q31": "q31 (int32)", "q15": "q15 (int16)", "fir_f32": "f32",
