@@ -50,6 +50,7 @@ WORKLOADS = {
     "mat_mult_f32": ("mat", 1024, 256, None),
     "mfcc_f32": ("mfcc", 1024, 1 << 18, 4),
     "rfft_f32": ("rfft", 1024, 1 << 20, 8),
+    "conv_f32": ("conv", 128, 1 << 16, 8),
     "mat_mult_q15": ("matq15", 1024, 64, None),
     "mat_mult_q31": ("matq31", 1024, 64, None),
 }
@@ -113,7 +114,7 @@ def cpu_baseline(workload, n):
           "fir_f32": "fir_f32", "fir_q15": "fir_q15", "fir_q31": "fir_q31", "fir_fast_q15": "fir_fast_q15",
           "fir_fast_q31": "fir_fast_q31", "mat_mult_f32": "mat_mult_f32",
           "mfcc_f32": "mfcc_f32", "mat_mult_q15": "mat_mult_q15", "mat_mult_q31": "mat_mult_q31",
-          "rfft_f32": "rfft_f32"}[workload]
+          "rfft_f32": "rfft_f32", "conv_f32": "conv_f32"}[workload]
     nn = 256 if workload.startswith("mat_mult") else n  # 1024^3 takes seconds per matrix on one core
     out = subprocess.run([exe, wl, str(nn), str(threads), str(secs)], capture_output=True, text=True,
                          timeout=120)
@@ -250,6 +251,24 @@ def run_rfft(n, batch, steps, warmup, world, rank):
     return wall, kern_ms, {"checker": hk, "bit_exact": bool(ok), "transforms_checked": 64}
 
 
+def run_conv(taps, batch, steps, warmup, world, rank, block=4096):
+    """arm_conv_f32 of `batch` 4096-sample signals with one shared 128-sample kernel
+    (the FIR config's shape): outputs of block + taps - 1 samples."""
+    rng = np.random.default_rng(6)
+    a = synth("f32", batch * block, rank).view(batch, block)
+    b = torch.from_numpy((rng.standard_normal(taps) / np.sqrt(taps)).astype(np.float32)).cuda()
+    out = torch.empty((batch, block + taps - 1), dtype=torch.float32, device="cuda")
+
+    def launch(s):
+        dsp.conv_batch(a, b, out)
+
+    wall, kern_ms = time_launches(launch, steps, warmup, world)
+    host, hk = cpu_checker()
+    ok = all(out[i].cpu().numpy().tobytes() == host.conv("f32", a[i].cpu().numpy(), b.cpu().numpy()).tobytes()
+             for i in (0, batch - 1))
+    return wall, kern_ms, {"checker": hk, "bit_exact": bool(ok), "items_checked": 2}
+
+
 def run_mfcc(n, batch, steps, warmup, world, rank):
     import mfcc_cfg
     g = mfcc_cfg.golden()
@@ -333,6 +352,10 @@ def main():
         wall, kern_ms, parity = run_mat_fixed(kind[3:], n, batch, args.steps, args.warmup, world, rank)
         units = batch
         algo_bytes = None
+    elif args.workload == "conv_f32":
+        wall, kern_ms, parity = run_conv(n, batch, args.steps, args.warmup, world, rank)
+        units = batch * (4096 + n - 1)                     # output samples
+        algo_bytes = batch * 4096 * 4 + units * 4          # signal in + output
     elif args.workload == "rfft_f32":
         wall, kern_ms, parity = run_rfft(n, batch, args.steps, args.warmup, world, rank)
         units = batch * n                                  # real input samples
@@ -378,11 +401,14 @@ def main():
                     dtype={"f32": "f32", "q31": "q31 (int32)", "q15": "q15 (int16)", "fir_f32": "f32",
                            "fir_q15": "q15 (int16 x int16 -> int64)", "mfcc": "f32",
                            "fir_q31": "q31 (int32 x int32 -> int64)", "fir_fast_q15": "q15 (int32 wrap accumulator)",
-                           "fir_fast_q31": "q31 (rounded high-word accumulator)", "rfft": "f32"}[kind])
+                           "fir_fast_q31": "q31 (rounded high-word accumulator)", "rfft": "f32", "conv": "f32"}[kind])
         if args.workload.startswith("cfft"):
             line["config"] = {"workload": f"arm_cfft_{kind} N={n} batch={batch}/GPU in place, bitReverseFlag=1, "
                                           f"alternating fwd/inv (BASELINE configs[{1 if kind == 'f32' else 3}])",
                               "fftLen": n, "batch_per_gpu": batch, "parallelism": f"dp{world} shards"}
+        elif kind == "conv":
+            line["config"] = {"workload": f"arm_conv_f32 4096 (*) {n} (shared kernel), batch={batch}/GPU",
+                              "srcALen": 4096, "srcBLen": n, "batch_per_gpu": batch, "parallelism": f"dp{world} shards"}
         elif kind == "rfft":
             line["config"] = {"workload": f"arm_rfft_fast_f32 N={n} forward, batch={batch}/GPU", "fftLen": n,
                               "batch_per_gpu": batch, "parallelism": f"dp{world} shards"}
@@ -399,6 +425,10 @@ def main():
         line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.workload),
                             "algorithmic_bytes_per_launch": algo_bytes, "avg_kernel_ms": round(kern_ms, 4)}
+        if args.workload == "conv_f32":
+            valu = units * n * 2 / (kern_ms * 1e-3) * 1e-12
+            line["roofline"]["valu_tflops_nofma"] = {"achieved": round(valu, 2), "peak": FP32_NOFMA_TFLOPS,
+                                                     "frac": round(valu / FP32_NOFMA_TFLOPS, 4)}
         if args.workload == "rfft_f32":
             # the forward transform also leaves the inner CFFT output in p (reference semantics)
             line["roofline"]["bytes_moved_per_sample"] = 12

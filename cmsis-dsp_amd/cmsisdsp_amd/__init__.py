@@ -297,6 +297,31 @@ def fir_batch(S, src, dst, hist, stream=None, q15=False, kind=None):
         raise RuntimeError(f"{fn.__name__} -> {st}: {last_error()[1]}")
 
 
+def arm_conv(kind, a, b):
+    """arm_conv_f32 / _q15 / _q31 (drop-in, numpy): len(a) + len(b) - 1 samples."""
+    dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32}[kind]
+    a = np.ascontiguousarray(a, dtype=dt)
+    b = np.ascontiguousarray(b, dtype=dt)
+    y = np.zeros(len(a) + len(b) - 1, dtype=dt)
+    getattr(lib, f"arm_conv_{kind}")(a.ctypes.data, len(a), b.ctypes.data, len(b), y.ctypes.data)
+    _check_void(f"arm_conv_{kind}")
+    return y
+
+
+def conv_batch(a, b, out, stream=None):
+    """out[i] = a[i] (*) b[i]; a [batch, La], b [batch, Lb] or [Lb] (shared), out [batch, La+Lb-1]."""
+    import torch
+    kind = {torch.float32: "f32", torch.int16: "q15", torch.int32: "q31"}[a.dtype]
+    batch, la = a.shape
+    lb = b.shape[-1]
+    sb = 0 if b.dim() == 1 else b.stride(0)
+    fn = getattr(lib, f"arm_conv_{kind}_batch")
+    st = fn(C.c_void_p(a.data_ptr()), la, a.stride(0), C.c_void_p(b.data_ptr()), lb, sb,
+            C.c_void_p(out.data_ptr()), batch, _stream_ptr(stream))
+    if st != ARM_MATH_SUCCESS:
+        raise RuntimeError(f"{fn.__name__} -> {st}: {last_error()[1]}")
+
+
 def arm_mat_mult_fixed(kind, a, b):
     """(status, C) = A @ B through arm_mat_mult_q15 / arm_mat_mult_q31 (row-major)."""
     dt = np.int16 if kind == "q15" else np.int32

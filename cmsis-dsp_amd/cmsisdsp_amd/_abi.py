@@ -100,6 +100,9 @@ DROPIN = {
                                    P(arm_matrix_instance_q15), C.c_void_p]),
     "arm_mat_mult_q31": (C.c_int, [P(arm_matrix_instance_q31), P(arm_matrix_instance_q31),
                                    P(arm_matrix_instance_q31)]),
+    "arm_conv_f32": (None, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "arm_conv_q15": (None, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "arm_conv_q31": (None, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
     "arm_mfcc_init_f32": (C.c_int, [P(arm_mfcc_instance_f32), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "arm_mfcc_f32": (None, [P(arm_mfcc_instance_f32), C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -145,6 +148,12 @@ BATCHED = {
                                          P(arm_matrix_instance_q15), C.c_uint32, C.c_void_p]),
     "arm_mat_mult_q31_batch": (C.c_int, [P(arm_matrix_instance_q31), P(arm_matrix_instance_q31),
                                          P(arm_matrix_instance_q31), C.c_uint32, C.c_void_p]),
+    "arm_conv_f32_batch": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
+                                     C.c_void_p, C.c_uint32, C.c_void_p]),
+    "arm_conv_q15_batch": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
+                                     C.c_void_p, C.c_uint32, C.c_void_p]),
+    "arm_conv_q31_batch": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
+                                     C.c_void_p, C.c_uint32, C.c_void_p]),
     "arm_mfcc_f32_batch": (C.c_int, [P(arm_mfcc_instance_f32), C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                      C.c_void_p]),
     "arm_mi355x_last_error": (C.c_int, []),

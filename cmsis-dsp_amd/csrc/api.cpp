@@ -269,6 +269,35 @@ arm_status fir_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uint32
   return ARM_MATH_SUCCESS;
 }
 
+// drop-in convolution: host or device operands, synchronous
+template <typename T>
+void conv_sync(int kind, const T* a, uint32_t alen, const T* b, uint32_t blen, T* dst) {
+  if (!a || !b || !dst || alen == 0 || blen == 0) return;
+  const size_t ab = sizeof(T) * alen, bb = sizeof(T) * blen, yb = sizeof(T) * ((size_t)alen + blen - 1);
+  hipStream_t st = sync_stream();
+  const bool da = is_device_ptr(a), db = is_device_ptr(b), dd = is_device_ptr(dst);
+  const T* A = da ? a : (const T*)scratch(ab, 0);
+  const T* B = db ? b : (const T*)scratch(bb, 1);
+  T* Y = dd ? dst : (T*)scratch(yb, 2);
+  if (!A || !B || !Y) { set_error(hipErrorOutOfMemory, "arm_conv scratch"); return; }
+  hipError_t e = hipSuccess;
+  if (!da) e = hipMemcpyAsync((void*)A, a, ab, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && !db) e = hipMemcpyAsync((void*)B, b, bb, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = conv_run(kind, A, alen, 0, B, blen, 0, Y, 1, st);
+  if (e == hipSuccess && !dd) e = hipMemcpyAsync(dst, Y, yb, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) set_error(e, "arm_conv");
+}
+
+template <typename T>
+arm_status conv_batch(int kind, const T* a, uint32_t alen, uint32_t sa, const T* b, uint32_t blen, uint32_t sb, T* y,
+                      uint32_t batch, void* stream) {
+  if (batch && (!a || !b || !y || alen == 0 || blen == 0)) return ARM_MATH_ARGUMENT_ERROR;
+  hipError_t e = conv_run(kind, a, alen, sa, b, blen, sb, y, batch, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(e, "arm_conv_batch"); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
+}
+
 template <typename M>
 bool mat_shapes_ok(const M* a, const M* b, const M* c) {
   return a->numCols == b->numRows && a->numRows == c->numRows && b->numCols == c->numCols;
@@ -513,6 +542,29 @@ arm_status arm_mat_mult_q31_batch(const arm_matrix_instance_q31* pSrcA, const ar
                                      pDst->pData, batch, (hipStream_t)stream);
   if (e != hipSuccess) { set_error(e, "arm_mat_mult_q31_batch"); return ARM_MATH_ARGUMENT_ERROR; }
   return ARM_MATH_SUCCESS;
+}
+
+// ---- convolution ------------------------------------------------------------------
+void arm_conv_f32(const float32_t* pSrcA, uint32_t srcALen, const float32_t* pSrcB, uint32_t srcBLen, float32_t* pDst) {
+  conv_sync<float>(0, pSrcA, srcALen, pSrcB, srcBLen, pDst);
+}
+void arm_conv_q15(const q15_t* pSrcA, uint32_t srcALen, const q15_t* pSrcB, uint32_t srcBLen, q15_t* pDst) {
+  conv_sync<int16_t>(1, pSrcA, srcALen, pSrcB, srcBLen, pDst);
+}
+void arm_conv_q31(const q31_t* pSrcA, uint32_t srcALen, const q31_t* pSrcB, uint32_t srcBLen, q31_t* pDst) {
+  conv_sync<int32_t>(2, pSrcA, srcALen, pSrcB, srcBLen, pDst);
+}
+arm_status arm_conv_f32_batch(const float32_t* d_a, uint32_t srcALen, uint32_t strideA, const float32_t* d_b,
+                              uint32_t srcBLen, uint32_t strideB, float32_t* d_dst, uint32_t batch, void* stream) {
+  return conv_batch<float>(0, d_a, srcALen, strideA, d_b, srcBLen, strideB, d_dst, batch, stream);
+}
+arm_status arm_conv_q15_batch(const q15_t* d_a, uint32_t srcALen, uint32_t strideA, const q15_t* d_b,
+                              uint32_t srcBLen, uint32_t strideB, q15_t* d_dst, uint32_t batch, void* stream) {
+  return conv_batch<int16_t>(1, d_a, srcALen, strideA, d_b, srcBLen, strideB, d_dst, batch, stream);
+}
+arm_status arm_conv_q31_batch(const q31_t* d_a, uint32_t srcALen, uint32_t strideA, const q31_t* d_b,
+                              uint32_t srcBLen, uint32_t strideB, q31_t* d_dst, uint32_t batch, void* stream) {
+  return conv_batch<int32_t>(2, d_a, srcALen, strideA, d_b, srcBLen, strideB, d_dst, batch, stream);
 }
 
 }  // extern "C"

@@ -74,6 +74,12 @@ hipError_t mfcc_f32_post_launch(int n, const float* y, const float* maxv, int ma
 hipError_t mat_mult_f32_launch(int m, int k, int n, const float* a, const float* b, float* c,
                                uint32_t batch, hipStream_t st);
 
+// Linear convolution (arm_conv_f32 / _q15 / _q31 semantics, bit-exact), kind 0 f32, 1 q15,
+// 2 q31: y[i] = a[i] (*) b[i] over `batch` items, a / b item strides sa / sb (0 = shared),
+// y items contiguous of alen + blen - 1.
+hipError_t conv_run(int kind, const void* a, uint32_t alen, uint64_t sa, const void* b, uint32_t blen, uint64_t sb,
+                    void* y, uint32_t batch, hipStream_t st);
+
 // Row-major q15 / q31 C[b] = A[b] * B[b] (arm_mat_mult_q15 / _q31 semantics, bit-exact):
 // byte-sliced planes on the i8 matrix cores (mat_mult_fixed.hip).
 hipError_t mat_mult_q15_launch(int m, int k, int n, const int16_t* a, const int16_t* b, int16_t* c, uint32_t batch,

@@ -277,6 +277,18 @@ void arm_fir_fast_q15(const arm_fir_instance_q15 *S, const q15_t *pSrc,
                       q15_t *pDst, uint32_t blockSize);
 
 /* ===================================================================================
+ * Convolution.  Prototypes: Include/dsp/filtering_functions.h
+ * (arm_conv_f32 / _q15 / _q31).  Reference bodies: Source/FilteringFunctions/arm_conv_f32.c
+ * (per output a sum over the overlap from 0.0f in ascending index of pSrcA, mul then add), arm_conv_q15.c (!ARM_MATH_DSP: q63 sum,
+ * __SSAT(sum >> 15, 16)), arm_conv_q31.c (q63 sum, (q31)(sum >> 31)).  pDst holds
+ * srcALen + srcBLen - 1 samples.
+ * =================================================================================== */
+void arm_conv_f32(const float32_t *pSrcA, uint32_t srcALen, const float32_t *pSrcB, uint32_t srcBLen,
+                  float32_t *pDst);
+void arm_conv_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB, uint32_t srcBLen, q15_t *pDst);
+void arm_conv_q31(const q31_t *pSrcA, uint32_t srcALen, const q31_t *pSrcB, uint32_t srcBLen, q31_t *pDst);
+
+/* ===================================================================================
  * Matrix multiply, f32.  Prototypes: Include/dsp/matrix_functions.h:341-344,630-634
  * Reference bodies: Source/MatrixFunctions/arm_mat_mult_f32.c:600-730,
  *                   Source/MatrixFunctions/arm_mat_init_f32.c

@@ -66,6 +66,16 @@ arm_status arm_fir_q31_batch(const arm_fir_instance_q31 *S, const q31_t *d_src, 
 arm_status arm_fir_fast_q31_batch(const arm_fir_instance_q31 *S, const q31_t *d_src, q31_t *d_dst,
                                   uint32_t blockSize, uint32_t batch, q31_t *d_hist, void *stream);
 
+/* Convolution of `batch` pairs: item i convolves d_a + i*strideA (srcALen samples) with
+ * d_b + i*strideB (srcBLen samples; strideB = 0 shares one kernel) into
+ * d_dst + i*(srcALen + srcBLen - 1).  Per-item semantics: arm_conv_f32 / _q15 / _q31. */
+arm_status arm_conv_f32_batch(const float32_t *d_a, uint32_t srcALen, uint32_t strideA, const float32_t *d_b,
+                              uint32_t srcBLen, uint32_t strideB, float32_t *d_dst, uint32_t batch, void *stream);
+arm_status arm_conv_q15_batch(const q15_t *d_a, uint32_t srcALen, uint32_t strideA, const q15_t *d_b,
+                              uint32_t srcBLen, uint32_t strideB, q15_t *d_dst, uint32_t batch, void *stream);
+arm_status arm_conv_q31_batch(const q31_t *d_a, uint32_t srcALen, uint32_t strideA, const q31_t *d_b,
+                              uint32_t srcBLen, uint32_t strideB, q31_t *d_dst, uint32_t batch, void *stream);
+
 /* Row-major C[b] = A[b] * B[b] for `batch` contiguous (numRows x numCols) matrices with
  * the shapes of the three instances (their pData must be device pointers to the first
  * item).  Returns ARM_MATH_SIZE_MISMATCH on incompatible shapes (arm_mat_mult_f32.c:618-630). */

@@ -33,6 +33,7 @@ arm_status oracle_arm_cfft_init_q15(arm_cfft_instance_q15 *S, uint16_t n);
 void oracle_arm_fir_init_f32(arm_fir_instance_f32 *S, uint16_t numTaps, const float *pCoeffs, float *pState,
                              uint32_t blockSize);
 arm_status oracle_arm_rfft_fast_init_f32(arm_rfft_fast_instance_f32 *S, uint16_t n);
+void oracle_arm_conv_f32(const float *pSrcA, uint32_t srcALen, const float *pSrcB, uint32_t srcBLen, float *pDst);
 void oracle_arm_fir_init_q31(arm_fir_instance_q31 *S, uint16_t numTaps, const int32_t *pCoeffs, int32_t *pState,
                              uint32_t blockSize);
 arm_status oracle_arm_fir_init_q15(arm_fir_instance_q15 *S, uint16_t numTaps, const int16_t *pCoeffs,
@@ -118,6 +119,13 @@ static void *worker(void *arg) {
       samples += block;
     } while (now() - t0 < j->seconds);
     free(c); free(st); free(in); free(out);
+  } else if (!strcmp(j->wl, "conv_f32")) {
+    const int taps = j->n, block = 4096;
+    float *a = malloc(sizeof(float) * block), *b = malloc(sizeof(float) * taps), *y = malloc(sizeof(float) * (block + taps));
+    for (int i = 0; i < block; ++i) a[i] = uni(&seed);
+    for (int i = 0; i < taps; ++i) b[i] = uni(&seed);
+    do { F(arm_conv_f32)(a, block, b, taps, y); samples += block + taps - 1; } while (now() - t0 < j->seconds);
+    free(a); free(b); free(y);
   } else if (!strcmp(j->wl, "rfft_f32")) {
     const int n = j->n;
     float *x = malloc(sizeof(float) * n), *p = malloc(sizeof(float) * n), *o = malloc(sizeof(float) * n);

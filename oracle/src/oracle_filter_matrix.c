@@ -145,3 +145,39 @@ arm_status oracle_arm_mat_mult_q31(const arm_matrix_instance_q31 *A, const arm_m
     }
   return ARM_MATH_SUCCESS;
 }
+
+/* arm_conv_f32.c / arm_conv_q15.c (!ARM_MATH_DSP) / arm_conv_q31.c: y[n] = sum over the
+ * overlap of a[k]*b[n-k] with k (index of pSrcA) ASCENDING whichever input is longer
+ * (the reference's internal swap of the two inputs does not change that order; checked
+ * against oracle/_ref for both orders of the lengths), from 0.0f (f32: mul then add) or an
+ * exact q63 sum (q15: __SSAT((q31)(sum >> 15), 16); q31: (q31)(sum >> 31), wrapping). */
+#define ORACLE_CONV_SETUP(T)                                                    \
+  const T *x = pSrcA, *h = pSrcB;                                              \
+  const uint32_t A = srcALen, B = srcBLen, L = A + B - 1;
+void oracle_arm_conv_f32(const float *pSrcA, uint32_t srcALen, const float *pSrcB, uint32_t srcBLen, float *pDst) {
+  ORACLE_CONV_SETUP(float)
+  for (uint32_t n = 0; n < L; ++n) {
+    const uint32_t k0 = n + 1 > B ? n + 1 - B : 0, k1 = n < A - 1 ? n : A - 1;
+    float sum = 0.0f;
+    for (uint32_t k = k0; k <= k1; ++k) { const float p = x[k] * h[n - k]; sum = sum + p; }
+    pDst[n] = sum;
+  }
+}
+void oracle_arm_conv_q15(const int16_t *pSrcA, uint32_t srcALen, const int16_t *pSrcB, uint32_t srcBLen, int16_t *pDst) {
+  ORACLE_CONV_SETUP(int16_t)
+  for (uint32_t n = 0; n < L; ++n) {
+    const uint32_t k0 = n + 1 > B ? n + 1 - B : 0, k1 = n < A - 1 ? n : A - 1;
+    int64_t sum = 0;
+    for (uint32_t k = k0; k <= k1; ++k) sum += (int32_t)x[k] * h[n - k];
+    pDst[n] = oracle_sat_q15((int32_t)(sum >> 15));
+  }
+}
+void oracle_arm_conv_q31(const int32_t *pSrcA, uint32_t srcALen, const int32_t *pSrcB, uint32_t srcBLen, int32_t *pDst) {
+  ORACLE_CONV_SETUP(int32_t)
+  for (uint32_t n = 0; n < L; ++n) {
+    const uint32_t k0 = n + 1 > B ? n + 1 - B : 0, k1 = n < A - 1 ? n : A - 1;
+    uint64_t sum = 0;
+    for (uint32_t k = k0; k <= k1; ++k) sum += (uint64_t)((int64_t)x[k] * h[n - k]);
+    pDst[n] = (int32_t)((int64_t)sum >> 31);
+  }
+}

@@ -101,6 +101,14 @@ class Host:
         self._keep = (c, state)
         return outs, state.copy()
 
+    def conv(self, kind, a, b):
+        dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32}[kind]
+        a = np.ascontiguousarray(a, dtype=dt)
+        b = np.ascontiguousarray(b, dtype=dt)
+        y = np.zeros(len(a) + len(b) - 1, dtype=dt)
+        self.fn(f"arm_conv_{kind}")(a.ctypes.data, len(a), b.ctypes.data, len(b), y.ctypes.data)
+        return y
+
     def mat_mult_fixed(self, kind, a, b):
         """arm_mat_mult_q15 / _q31: returns (status, C)."""
         dt = np.int16 if kind == "q15" else np.int32

@@ -264,3 +264,47 @@ def test_mat_mult_fixed_batch(dsp, torch_gpu, ref, kind):
     got = Cm.cpu().numpy()
     for i in range(3):
         assert got[i].tobytes() == ref.mat_mult_fixed(kind, a[i], b[i])[1].tobytes(), i
+
+
+# ------------------------------------------------------------------ convolution
+def _conv_case(kind, la, lb, seed, fill=None):
+    rng = np.random.default_rng(seed)
+    if kind == "f32":
+        return rng.standard_normal(la).astype(np.float32), rng.standard_normal(lb).astype(np.float32)
+    bits, dt = (15, np.int16) if kind == "q15" else (31, np.int32)
+    if fill is not None:
+        v = -(1 << bits) if fill == "min" else (1 << bits) - 1
+        return np.full(la, v, dt), np.full(lb, v, dt)
+    return (rng.integers(-(1 << bits), 1 << bits, la).astype(dt), rng.integers(-(1 << bits), 1 << bits, lb).astype(dt))
+
+
+@pytest.mark.parametrize("kind", ["f32", "q15", "q31"])
+@pytest.mark.parametrize("la,lb", [(1, 1), (5, 3), (3, 5), (100, 7), (7, 100), (5000, 129), (129, 5000), (4096, 1024),
+                                   (2000, 1500), (33, 1)])
+def test_conv_dropin_bitexact(dsp, torch_gpu, ref, kind, la, lb):
+    """Both length orders (the reference sums in ascending index of pSrcA either way), the
+    LDS path (srcBLen <= 1024) and the direct path beyond."""
+    a, b = _conv_case(kind, la, lb, la * 7 + lb)
+    assert dsp.arm_conv(kind, a, b).tobytes() == ref.conv(kind, a, b).tobytes()
+
+
+@pytest.mark.parametrize("kind,fill", [("q15", "min"), ("q15", "max"), ("q31", "min"), ("q31", "max")])
+def test_conv_extremes(dsp, torch_gpu, ref, kind, fill):
+    a, b = _conv_case(kind, 300, 40, 1, fill)
+    assert dsp.arm_conv(kind, a, b).tobytes() == ref.conv(kind, a, b).tobytes()
+
+
+@pytest.mark.parametrize("kind", ["f32", "q15", "q31"])
+@pytest.mark.parametrize("shared", [False, True])
+def test_conv_batch(dsp, torch_gpu, ref, kind, shared):
+    batch, la, lb = 6, 3000, 77
+    A = np.stack([_conv_case(kind, la, lb, 50 + i)[0] for i in range(batch)])
+    B = np.stack([_conv_case(kind, la, lb, 90 + i)[1] for i in range(batch)])
+    tdt = {"f32": torch_gpu.float32, "q15": torch_gpu.int16, "q31": torch_gpu.int32}[kind]
+    dA = torch_gpu.from_numpy(A).cuda()
+    dB = torch_gpu.from_numpy(B[0].copy()).cuda() if shared else torch_gpu.from_numpy(B).cuda()
+    out = torch_gpu.empty((batch, la + lb - 1), dtype=tdt, device="cuda")
+    dsp.conv_batch(dA, dB, out)
+    got = out.cpu().numpy()
+    for i in range(batch):
+        assert got[i].tobytes() == ref.conv(kind, A[i], B[0] if shared else B[i]).tobytes(), i

@@ -114,3 +114,11 @@ def test_mat_mult_fixed_oracle_equals_reference(oracle, ref, kind, m, k, n, fill
         a, b = np.full((m, k), v, dt), np.full((k, n), v, dt)
     (sa, ca), (sb, cb) = oracle.mat_mult_fixed(kind, a, b), ref.mat_mult_fixed(kind, a, b)
     assert sa == sb == 0 and ca.tobytes() == cb.tobytes()
+
+
+@pytest.mark.parametrize("kind", ["f32", "q15", "q31"])
+@pytest.mark.parametrize("la,lb", [(1, 1), (5, 3), (3, 5), (64, 64), (100, 7), (7, 100), (1000, 129), (129, 1000),
+                                   (33, 1), (1, 33), (10, 37), (65, 64)])
+def test_conv_oracle_equals_reference(oracle, ref, kind, la, lb):
+    c, xs = fir_case(kind, lb, [la], la * 13 + lb)
+    assert oracle.conv(kind, xs[0], c).tobytes() == ref.conv(kind, xs[0], c).tobytes()
