@@ -174,6 +174,23 @@ def arm_mat_mult_q15(pSrcA, pSrcB, pState=None):
     return _amd.arm_mat_mult_fixed("q15", _arr(pSrcA, _np.int16), _arr(pSrcB, _np.int16))
 
 
+# ------------------------------------------------------------------ convolution
+def _conv(kind, dt):
+    def run(pSrcA, srcALen, pSrcB, srcBLen):
+        """Full linear convolution, srcALen + srcBLen - 1 samples (reference binding
+        PythonWrapper/cmsisdsp_pkg/src/cmsisdsp_filtering.c cmsis_arm_conv_*)."""
+        a = _arr(pSrcA, dt)[:int(srcALen)]
+        b = _arr(pSrcB, dt)[:int(srcBLen)]
+        return _amd.arm_conv(kind, a, b)
+    run.__name__ = f"arm_conv_{kind}"
+    return run
+
+
+arm_conv_f32 = _conv("f32", _np.float32)
+arm_conv_q15 = _conv("q15", _np.int16)
+arm_conv_q31 = _conv("q31", _np.int32)
+
+
 # ------------------------------------------------------------------ MFCC
 def arm_mfcc_init_f32(inst, fftLen, nbMelFilters, nbDctOutputs, dctCoefs, filterPos, filterLengths,
                       filterCoefs, windowCoefs):

@@ -37,7 +37,8 @@ def test_module_surface_without_gpu(cdsp):
     assert cdsp.arm_rfft_fast_init_f32(R, 128) == 0 and R.fftLenRFFT() == 128
     assert cdsp.arm_rfft_output_buffer_size(dt.F32, 128) == 128 and not cdsp.has_neon()
     for name in ("arm_cfft_q31", "arm_cfft_q15", "arm_fir_f32", "arm_fir_q15", "arm_fir_q31", "arm_fir_fast_q15",
-                 "arm_fir_fast_q31", "arm_mat_mult_f32", "arm_mat_mult_q15", "arm_mat_mult_q31", "arm_mfcc_f32"):
+                 "arm_fir_fast_q31", "arm_mat_mult_f32", "arm_mat_mult_q15", "arm_mat_mult_q31", "arm_mfcc_f32",
+                 "arm_conv_f32", "arm_conv_q15", "arm_conv_q31"):
         assert callable(getattr(cdsp, name))
 
 
@@ -128,3 +129,16 @@ def test_mfcc_f32(cdsp, torch_gpu, ref):
     x = g["input_Noise_512"]
     res = cdsp.arm_mfcc_f32(inst, x, np.zeros(cdsp.arm_mfcc_tmp_buffer_size(0, 512, 1), np.float32))
     np.testing.assert_allclose(res, ref.mfcc(cfg, x)[0], 3e-6, 3e-6)     # testmfcc.py tolerance
+
+
+@pytest.mark.gpu
+def test_conv(cdsp, torch_gpu, ref):
+    """testdsp.py-style conv: f32 against np.convolve (1e-6), fixed point bit-exact
+    against the reference build."""
+    rng = np.random.default_rng(5)
+    a, b = rng.uniform(-1, 1, 37), rng.uniform(-1, 1, 11)
+    np.testing.assert_allclose(cdsp.arm_conv_f32(a, len(a), b, len(b)), np.convolve(a, b), 1e-5, 1e-6)
+    for kind, conv in (("q15", toQ15), ("q31", toQ31)):
+        qa, qb = conv(a * 0.5), conv(b * 0.5)
+        got = getattr(cdsp, f"arm_conv_{kind}")(qa, len(qa), qb, len(qb))
+        assert got.tobytes() == ref.conv(kind, qa, qb).tobytes(), kind
