@@ -115,10 +115,36 @@ __device__ __forceinline__ int s1024(int e) {
 #ifndef MI355X_N1024_WAVES
 #define MI355X_N1024_WAVES 1
 #endif
-__global__ __launch_bounds__(64, MI355X_N1024_WAVES) void cfft_f32_n1024_kernel(float2* __restrict__ data, uint32_t batch,
+// Work mapping.  N1024_T = 0: persistent grid, wave g takes transforms g, g + G, g + 2G, ...
+// N1024_T = T > 0: grid = batch / (T * WPB) waves, wave g takes the T CONSECUTIVE transforms
+// gT .. gT+T-1 (the live HBM footprint stays a compact sliding window; measured by
+// tools/probes/hbm_inplace.hip).  N1024_WPB waves per workgroup, each with its own LDS image.
+// Default T = 4, WPB = 8, no software prefetch: 76 % of HBM peak against 66 % for the
+// persistent prefetching walk (profiles/r01/variants_n1024_mapping.txt).
+#ifndef MI355X_N1024_T
+#define MI355X_N1024_T 4
+#endif
+#ifndef MI355X_N1024_WPB
+#define MI355X_N1024_WPB 8
+#endif
+constexpr int kN1024T = MI355X_N1024_T, kN1024Wpb = MI355X_N1024_WPB;
+// Each wave owns its LDS image, so the exchanges need only a wave-level barrier: one
+// wave's LDS operations complete in issue order; the fences stop the compiler from moving
+// accesses across the exchange.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__global__ __launch_bounds__(64 * kN1024Wpb, MI355X_N1024_WAVES) void cfft_f32_n1024_kernel(float2* __restrict__ data, uint32_t batch,
                                                            const float2* __restrict__ tw, uint32_t flags) {
-  __shared__ __attribute__((aligned(16))) float2 lds[16 * 72];
-  const int l = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) float2 lds_all[kN1024Wpb][16 * 72];
+  const int l = threadIdx.x & 63;
+  float2* lds = lds_all[threadIdx.x >> 6];
+  const uint32_t wave = blockIdx.x * kN1024Wpb + (threadIdx.x >> 6);
+  const uint32_t t_begin = kN1024T ? wave * kN1024T : wave;
+  const uint32_t t_end = kN1024T ? min(batch, t_begin + kN1024T) : batch;
+  const uint32_t t_step = kN1024T ? 1u : gridDim.x * kN1024Wpb;
   const bool ifft = flags & kIfft;
   const bool brev = flags & kBitrev;
   const float invL = 1.0f / 1024.0f;
@@ -135,9 +161,11 @@ __global__ __launch_bounds__(64, MI355X_N1024_WAVES) void cfft_f32_n1024_kernel(
 
 // MI355X_PF: software-pipelined loads (the next transform's 16 loads are issued right
 // after phase A, in flight during phases B/C).  MI355X_NT: non-temporal loads/stores (the
-// batch is streamed once).  Both on: +4% over neither (profiles/r01/variants_n1024.txt).
+// batch is streamed once).  Both on: +4% over neither under the persistent walk
+// (profiles/r01/variants_n1024.txt); with T = 4 consecutive transforms per wave the prefetch
+// measured 1% slower and is off, NT stays (-13% without it).
 #ifndef MI355X_PF
-#define MI355X_PF 1
+#define MI355X_PF 0
 #endif
 #ifndef MI355X_NT
 #define MI355X_NT 1
@@ -150,13 +178,13 @@ __global__ __launch_bounds__(64, MI355X_N1024_WAVES) void cfft_f32_n1024_kernel(
   float2 a[8], b[8];
 #if MI355X_PF
   float2 na[8], nb[8];
-  if (blockIdx.x < batch) {
-    const float2* X0 = data + (size_t)blockIdx.x * 1024;
+  if (t_begin < t_end) {
+    const float2* X0 = data + (size_t)t_begin * 1024;
 #pragma unroll
     for (int m = 0; m < 8; ++m) { na[m] = LD(&X0[l + 64 * m]); nb[m] = LD(&X0[512 + l + 64 * m]); }
   }
 #endif
-  for (uint32_t t = blockIdx.x; t < batch; t += gridDim.x) {
+  for (uint32_t t = t_begin; t < t_end; t += t_step) {
     float2* X = data + (size_t)t * 1024;
     // ---------------- phase A
 #if MI355X_PF
@@ -184,17 +212,17 @@ __global__ __launch_bounds__(64, MI355X_N1024_WAVES) void cfft_f32_n1024_kernel(
     }
     r8_sel(a, w0, l != 0);
     r8_sel(b, w0, l != 0);
-    __syncthreads();                    // previous transform's phase C reads are done
+    wave_sync();                    // previous transform's phase C reads are done
 #pragma unroll
     for (int m = 0; m < 8; ++m) { lds[s1024(l + 64 * m)] = a[m]; lds[s1024(512 + l + 64 * m)] = b[m]; }
 #if MI355X_PF
-    if (t + gridDim.x < batch) {       // next transform's loads fly under phases B and C
-      const float2* XN = data + (size_t)(t + gridDim.x) * 1024;
+    if (t + t_step < t_end) {          // next transform's loads fly under phases B and C
+      const float2* XN = data + (size_t)(t + t_step) * 1024;
 #pragma unroll
       for (int m = 0; m < 8; ++m) { na[m] = LD(&XN[l + 64 * m]); nb[m] = LD(&XN[512 + l + 64 * m]); }
     }
 #endif
-    __syncthreads();
+    wave_sync();
     // ---------------- phase B: stage 1
     {
       const int base = 64 * (l >> 3) + j1;
@@ -208,7 +236,7 @@ __global__ __launch_bounds__(64, MI355X_N1024_WAVES) void cfft_f32_n1024_kernel(
         for (int m = 0; m < 8; ++m) lds[s1024(h * 512 + base + 8 * m)] = v[m];
       }
     }
-    __syncthreads();
+    wave_sync();
     // ---------------- phase C: stage 2 + digit reversal folded into the store
 #pragma unroll
     for (int m = 0; m < 8; ++m) { a[m] = lds[s1024(8 * l + m)]; b[m] = lds[s1024(8 * (l + 64) + m)]; }
@@ -265,8 +293,10 @@ hipError_t cfft_f32_launch(int n, float* data, uint32_t batch, const float* tw, 
     case 512:  return launch_f32<512>(d, batch, w, perm, flags, st);
     case 1024:
       if (!perm) {   // the reference's own table (or no reversal): the specialist kernel
-        const int grid = persistent_grid((const void*)cfft_f32_n1024_kernel, 64, 0, batch, 8);
-        hipLaunchKernelGGL(cfft_f32_n1024_kernel, dim3(grid), dim3(64), 0, st, d, batch, w, flags);
+        const int per_block = (kN1024T ? kN1024T : 1) * kN1024Wpb;
+        int grid = (int)((batch + per_block - 1) / per_block);
+        if (!kN1024T) grid = persistent_grid((const void*)cfft_f32_n1024_kernel, 64 * kN1024Wpb, 0, grid, 8);
+        hipLaunchKernelGGL(cfft_f32_n1024_kernel, dim3(grid), dim3(64 * kN1024Wpb), 0, st, d, batch, w, flags);
         return hipGetLastError();
       }
       return launch_f32<1024>(d, batch, w, perm, flags, st);

@@ -319,6 +319,10 @@ __device__ __forceinline__ int s4096(int e) { return e + 8 * (e >> 7) + (e >> 9)
 #define MI355X_FX_TW_REGS 1
 #endif
 
+#ifndef MI355X_FX_T
+#define MI355X_FX_T 0
+#endif
+constexpr uint32_t kFxT = MI355X_FX_T;
 #ifndef MI355X_FX_WAVES
 #define MI355X_FX_WAVES 1     // minimum waves per SIMD the register allocation must allow
 #endif
@@ -368,16 +372,21 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 #endif
   auto W = [](C c) { return make_int2(c.x, c.y); };
 
+  // Work mapping (as cfft_f32_n1024_kernel): MI355X_FX_T = 0 persistent grid-stride walk;
+  // T > 0: workgroup b takes the T consecutive transforms bT .. bT+T-1.
+  const uint32_t tr_begin = kFxT ? blockIdx.x * kFxT : blockIdx.x;
+  const uint32_t tr_end = kFxT ? min(batch, tr_begin + kFxT) : batch;
+  const uint32_t tr_step = kFxT ? 1u : gridDim.x;
   int2 v[16];
   C nv[16];                             // prefetch in the storage type (q15: one VGPR per complex)
-  if (blockIdx.x < batch) {
-    const C* X0 = data + (size_t)blockIdx.x * 4096;
+  if (tr_begin < tr_end) {
+    const C* X0 = data + (size_t)tr_begin * 4096;
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) nv[4 * a + b] = X0[t + 256 * a + 1024 * b];
   }
-  for (uint32_t tr = blockIdx.x; tr < batch; tr += gridDim.x) {
+  for (uint32_t tr = tr_begin; tr < tr_end; tr += tr_step) {
     C* X = data + (size_t)tr * 4096;
 #if !MI355X_FX_TW_REGS
     const C* twl = tw;
@@ -396,8 +405,8 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) F::st(lds + s4096(t + 256 * a + 1024 * b), v[4 * a + b]);
-    if (tr + gridDim.x < batch) {       // next transform's loads fly under passes 2 and 3
-      const C* XN = data + (size_t)(tr + gridDim.x) * 4096;
+    if (tr + tr_step < tr_end) {        // next transform's loads fly under passes 2 and 3
+      const C* XN = data + (size_t)(tr + tr_step) * 4096;
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -453,11 +462,12 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 template <typename T>
 static hipError_t launch_fx4096(void* data, uint32_t batch, const void* tw, uint32_t flags, hipStream_t st) {
   using C = typename Fx<T>::C;
+  const uint32_t blocks = kFxT ? (batch + kFxT - 1) / kFxT : batch;
   if (flags & kIfft) {
-    const int grid = persistent_grid((const void*)cfft_fx4096_kernel<T, true>, 256, 0, batch);
+    const int grid = kFxT ? (int)blocks : persistent_grid((const void*)cfft_fx4096_kernel<T, true>, 256, 0, batch);
     hipLaunchKernelGGL((cfft_fx4096_kernel<T, true>), dim3(grid), dim3(256), 0, st, (C*)data, batch, (const C*)tw, flags);
   } else {
-    const int grid = persistent_grid((const void*)cfft_fx4096_kernel<T, false>, 256, 0, batch);
+    const int grid = kFxT ? (int)blocks : persistent_grid((const void*)cfft_fx4096_kernel<T, false>, 256, 0, batch);
     hipLaunchKernelGGL((cfft_fx4096_kernel<T, false>), dim3(grid), dim3(256), 0, st, (C*)data, batch, (const C*)tw, flags);
   }
   return hipGetLastError();
