@@ -191,13 +191,15 @@ __device__ __forceinline__ void cfft_f32_lds_fwd(float2* __restrict__ x, int lan
       float2 v[8];
 #pragma unroll
       for (int m = 0; m < 8; ++m) v[m] = XS(bi + m * n2);
-      if (j == 0) {
+      if (n2 == 1) {                    // last stage: every group is the j == 0 group
         r8<false>(v, nullptr);
       } else {
+        // j == 0 lanes sit in every wave of the middle stages: twiddle everywhere and
+        // select (tw[0] is a valid load) instead of running both branch bodies
         float2 w[7];
 #pragma unroll
         for (int m = 0; m < 7; ++m) w[m] = tw[(m + 1) * j * mod];
-        r8<true>(v, w);
+        r8_sel(v, w, j != 0);
       }
 #pragma unroll
       for (int m = 0; m < 8; ++m) XS(bi + m * n2) = v[m];

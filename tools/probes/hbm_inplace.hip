@@ -106,6 +106,66 @@ __global__ void tstride_kernel(float* __restrict__ x, float s) {
   }
 }
 
+// Each workgroup T x W chunks; at step t its W waves take W ADJACENT chunks
+// ((b*T + t)*W + w), so the workgroup's live footprint is one contiguous W*8 KiB span.
+template <int T, bool PF>
+__global__ void wgil_kernel(float* __restrict__ x, float s) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, W = blockDim.x >> 6;
+  const long base = (long)blockIdx.x * T * W + w;
+  v4f r[8];
+  auto ld = [&](long c) {
+    const v4f* q = reinterpret_cast<const v4f*>(x + c * 2048) + lane;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) r[m] = __builtin_nontemporal_load(q + 64 * m);
+  };
+  if (PF) ld(base);
+  for (int t = 0; t < T; ++t) {
+    if (!PF) ld(base + (long)t * W);
+    v4f o[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) o[m] = r[m] * s;
+    if (PF && t + 1 < T) ld(base + (long)(t + 1) * W);
+    v4f* q = reinterpret_cast<v4f*>(x + (base + (long)t * W) * 2048) + lane;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) __builtin_nontemporal_store(o[m], q + 64 * m);
+  }
+}
+
+// tchunk with the 8 row loads/stores of a chunk issued in a per-wave rotated order
+// (row (m + R*wave) & 7), so concurrently issuing waves hit different 1 KiB rows.
+template <int T, int R>
+__global__ void trot_kernel(float* __restrict__ x, float s) {
+  const int lane = threadIdx.x & 63;
+  const long wv = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const long c0 = wv * T;
+  const int rot = (int)(wv * R) & 7;
+  v4f r[8];
+  for (int t = 0; t < T; ++t) {
+    const v4f* q = reinterpret_cast<const v4f*>(x + (c0 + t) * 2048) + lane;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) r[m] = __builtin_nontemporal_load(q + 64 * ((m + rot) & 7));
+    v4f* o = reinterpret_cast<v4f*>(x + (c0 + t) * 2048) + lane;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) __builtin_nontemporal_store(r[m] * s, o + 64 * ((m + rot) & 7));
+  }
+}
+
+// Cooperative flat access: a workgroup of W waves owns T x W consecutive chunks; at step t
+// its instruction m of thread j moves float4 m*64W + j of the step's W*8 KiB span (every
+// workgroup instruction covers W KiB contiguous).
+template <int T, int W>
+__global__ void coop_kernel(float* __restrict__ x, float s) {
+  const int j = threadIdx.x;
+  for (int t = 0; t < T; ++t) {
+    v4f* q = reinterpret_cast<v4f*>(x + ((long)blockIdx.x * T + t) * W * 2048) + j;
+    v4f r[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) r[m] = __builtin_nontemporal_load(q + m * 64 * W);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) __builtin_nontemporal_store(r[m] * s, q + m * 64 * W);
+  }
+}
+
 // torch-like flat elementwise: each thread U float4 at block-contiguous offsets.
 template <int U, bool NT>
 __global__ void flat_kernel(float* __restrict__ x, float s) {
@@ -166,13 +226,12 @@ int main() {
     char nm[64];
 #define TCH(T, WPB) snprintf(nm, 64, "tchunk T%d wpb%d", T, WPB); \
     timeit(nm, tchunk_kernel<T>, dim3(chunks / (T * WPB)), dim3(64 * WPB), x, bytes, e0, e1);
-    TCH(1, 4) TCH(2, 4) TCH(3, 4) TCH(4, 4) TCH(6, 4) TCH(8, 4) TCH(16, 4)
-    TCH(1, 8) TCH(2, 8) TCH(4, 8) TCH(8, 8)
-    TCH(2, 2) TCH(4, 2) TCH(8, 2)
-    TCH(2, 16) TCH(4, 16)
-    timeit("flat U1", flat_kernel<1, false>, dim3(bytes / 16 / 1 / 256), dim3(256), x, bytes, e0, e1);
+#define COOP(T, WPB) snprintf(nm, 64, "coop T%d wpb%d", T, WPB); \
+    timeit(nm, coop_kernel<T, WPB>, dim3(chunks / (T * WPB)), dim3(64 * WPB), x, bytes, e0, e1);
+    TCH(4, 8)
+    COOP(1, 1) COOP(1, 4) COOP(1, 8) COOP(2, 4) COOP(2, 8) COOP(4, 4) COOP(4, 8) COOP(8, 8) COOP(1, 16) COOP(2, 16)
     timeit("flat U1 nt", flat_kernel<1, true>, dim3(bytes / 16 / 1 / 256), dim3(256), x, bytes, e0, e1);
-    run<8, true, true, true>(x, chunks, 1, 8, cus, e0, e1);
+    timeit("flat U8 nt", flat_kernel<8, true>, dim3(bytes / 16 / 8 / 256), dim3(256), x, bytes, e0, e1);
   }
   hipFree(x);
   return 0;
