@@ -24,10 +24,14 @@ namespace mi355x {
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
+typedef short s2x __attribute__((ext_vector_type(2)));
 
 constexpr int kMT = 64, kNT = 64, kKT = 64;     // workgroup tile: 4 waves of 32x32, K step 64
 constexpr int kRowB = kKT + 16;                  // LDS row pitch in bytes (k-contiguous rows)
 constexpr int kMatI8MaxK = 32704;
+#ifndef MI355X_MATI8_V1
+#define MI355X_MATI8_V1 0
+#endif
 
 template <typename T> struct Slices;
 template <> struct Slices<int16_t> { static constexpr int P = 2; static constexpr int64_t C0 = 128; };
@@ -162,6 +166,245 @@ __global__ __launch_bounds__(256) void mat_mult_i8_kernel(const T* __restrict__ 
   }
 }
 
+// ---- v2 kernel: 128 x 128 (q15) / 128 x 64 (q31) workgroup tiles of 8 waves (4 x 2), wave
+// tiles 32 x 64 / 32 x 32 (accumulators fit two waves per SIMD, so one wave's MFMAs overlap
+// the other's staging), double-buffered LDS planes (one barrier per K step), step kt+2's
+// global loads in flight under step kt's MFMAs.  B arrives row-major [k][n]; the MFMA wants
+// 16 k-consecutive bytes per column, so staging transposes 4 k-rows x CW columns per thread
+// into k-contiguous dwords (v_perm) before the LDS write.
+template <typename T> struct I8Cfg;
+template <> struct I8Cfg<int16_t> { static constexpr int BM = 128, BN = 128, WBM = 1, WBN = 2; };
+template <> struct I8Cfg<int32_t> { static constexpr int BM = 128, BN = 64, WBM = 1, WBN = 1; };
+constexpr int kKT2 = 64, kPitch2 = kKT2 + 16;   // K step; LDS row pitch in bytes
+constexpr int kNT2 = 512, kWavesM = 4, kWavesN = 2;
+
+// plane p of the two q15 values in each of d0, d1: [d0.lo, d0.hi, d1.lo, d1.hi] byte p
+template <int P>
+__device__ __forceinline__ uint32_t plane_q15(uint32_t d0, uint32_t d1, int p) {
+  const uint32_t sel = (uint32_t)p | (uint32_t)(2 + p) << 8 | (uint32_t)(4 + p) << 16 | (uint32_t)(6 + p) << 24;
+  const uint32_t w = __builtin_amdgcn_perm(d1, d0, sel);
+  return p == P - 1 ? w : w ^ 0x80808080u;
+}
+// byte o of r0, r1, r2, r3 -> one dword (k-consecutive bytes of one column)
+__device__ __forceinline__ uint32_t gather4(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, int o) {
+  const uint32_t sel = (uint32_t)o | (uint32_t)(4 + o) << 8 | 0x0c0c0000u;
+  return __builtin_amdgcn_perm(r1, r0, sel) | (__builtin_amdgcn_perm(r3, r2, sel) << 16);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                             T* __restrict__ C, int M, int K, int N) {
+  using G = I8Cfg<T>;
+  constexpr int P = Slices<T>::P, S = 2 * P - 1;
+  constexpr int64_t C0 = Slices<T>::C0;
+  constexpr int BM = G::BM, BN = G::BN, WBM = G::WBM, WBN = G::WBN;
+  static_assert(BM == kWavesM * 32 * WBM && BN == kWavesN * 32 * WBN, "wave grid covers the tile");
+  constexpr int EPD = 4 / sizeof(T);             // elements per dword
+  constexpr int AK = BM * kKT2 / kNT2;           // A elements per staging thread (16)
+  constexpr int AKD = AK / EPD;                  // ... as dwords
+  constexpr int AQ = kKT2 / AK;                  // threads per A row (4)
+  constexpr int CW = BN / (kNT2 / 16);           // B columns per staging thread (4 q15 / 2 q31)
+  constexpr int BD = CW / EPD;                   // dwords per B k-row segment (2)
+  constexpr int BUF = P * (BM + BN) * kPitch2;   // one K step's planes; two buffers
+  __shared__ __attribute__((aligned(16))) int8_t lds[2 * BUF];
+
+  const int tilesN = (N + BN - 1) / BN;
+  const int tm = blockIdx.x / tilesN, tn = blockIdx.x % tilesN;
+  const size_t bz = blockIdx.z;
+  A += bz * (size_t)M * K;
+  B += bz * (size_t)K * N;
+  C += bz * (size_t)M * N;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int row0 = tm * BM, col0 = tn * BN;
+
+  // staging roles: A row ar, AK k from ak0; B k-quad bq (rows 4bq..4bq+3), columns bg*CW..+CW-1
+  const int ar = tid / AQ, ak0 = AK * (tid % AQ);
+  const int bq = tid & 15, bg = tid >> 4;
+  const int gr = row0 + ar, gc = col0 + bg * CW;
+  const bool vecA = ((K * (int)sizeof(T)) % 16) == 0 && (((uintptr_t)A) & 15) == 0;
+  const bool vecB = ((N * (int)sizeof(T)) % 8) == 0 && (((uintptr_t)B) & 7) == 0;
+
+  uint32_t ad[AKD], bd[4][BD];
+  auto load = [&](int k0) {
+    const int ka = k0 + ak0;
+    if (vecA && gr < M && ka + AK <= K) {
+      const uint4* p = reinterpret_cast<const uint4*>(A + (size_t)gr * K + ka);
+#pragma unroll
+      for (int i = 0; i < AKD / 4; ++i) {
+        const uint4 v = p[i];
+        ad[4 * i] = v.x; ad[4 * i + 1] = v.y; ad[4 * i + 2] = v.z; ad[4 * i + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < AKD; ++d) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int e = 0; e < EPD; ++e) {
+          const int k = ka + d * EPD + e;
+          const uint32_t v = (gr < M && k < K) ? (uint32_t)A[(size_t)gr * K + k] : 0u;
+          w |= (EPD == 2 ? (v & 0xffffu) : v) << (16 * e);
+        }
+        ad[d] = w;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int kb = k0 + 4 * bq + i;
+      if (vecB && kb < K && gc + CW <= N) {
+        const uint2 v = *reinterpret_cast<const uint2*>(B + (size_t)kb * N + gc);
+        bd[i][0] = v.x; bd[i][1] = v.y;
+      } else {
+#pragma unroll
+        for (int d = 0; d < BD; ++d) {
+          uint32_t w = 0;
+#pragma unroll
+          for (int e = 0; e < EPD; ++e) {
+            const int c = gc + d * EPD + e;
+            const uint32_t v = (kb < K && c < N) ? (uint32_t)B[(size_t)kb * N + c] : 0u;
+            w |= (EPD == 2 ? (v & 0xffffu) : v) << (16 * e);
+          }
+          bd[i][d] = w;
+        }
+      }
+    }
+  };
+
+  int64_t my_rsum = 0, my_csum[CW];
+#pragma unroll
+  for (int c = 0; c < CW; ++c) my_csum[c] = 0;
+  i32x16 acc[S][WBM][WBN];
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int i = 0; i < WBM; ++i)
+#pragma unroll
+      for (int j = 0; j < WBN; ++j) acc[s][i][j] = i32x16{};
+  const int wm = wid / kWavesN, wn = wid % kWavesN;
+  const int r = lane & 31, h = lane >> 5;
+
+  auto stage = [&](int buf) {
+    auto As = reinterpret_cast<int8_t (*)[BM][kPitch2]>(lds + buf * BUF);
+    auto Bs = reinterpret_cast<int8_t (*)[BN][kPitch2]>(lds + buf * BUF + P * BM * kPitch2);
+    // exact row / column sums of the original values
+    if constexpr (sizeof(T) == 2) {
+      int32_t ra = 0;
+#pragma unroll
+      for (int d = 0; d < AKD; ++d) ra = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2x, ad[d]), s2x{1, 1}, ra, false);
+      my_rsum += ra;
+#pragma unroll
+      for (int c = 0; c < CW; ++c) {
+        const s2x sel = (c & 1) ? s2x{0, 1} : s2x{1, 0};
+        int32_t cs = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cs = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2x, bd[i][c >> 1]), sel, cs, false);
+        my_csum[c] += cs;
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < AKD; ++d) my_rsum += (int32_t)ad[d];
+#pragma unroll
+      for (int c = 0; c < CW; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) my_csum[c] += (int32_t)bd[i][c];
+    }
+    // byte planes -> LDS
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      uint32_t w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (sizeof(T) == 2) w[q] = plane_q15<P>(ad[2 * q], ad[2 * q + 1], p);
+        else w[q] = plane4<P>(ad[4 * q], ad[4 * q + 1], ad[4 * q + 2], ad[4 * q + 3], p);
+      }
+      *reinterpret_cast<uint4*>(&As[p][ar][ak0]) = make_uint4(w[0], w[1], w[2], w[3]);
+#pragma unroll
+      for (int c = 0; c < CW; ++c) {
+        const int d = c / EPD, o = (c % EPD) * (int)sizeof(T) + p;
+        uint32_t g = gather4(bd[0][d], bd[1][d], bd[2][d], bd[3][d], o);
+        if (p != P - 1) g ^= 0x80808080u;
+        *reinterpret_cast<uint32_t*>(&Bs[p][bg * CW + c][4 * bq]) = g;
+      }
+    }
+  };
+  auto mma = [&](int buf) {
+    auto As = reinterpret_cast<const int8_t (*)[BM][kPitch2]>(lds + buf * BUF);
+    auto Bs = reinterpret_cast<const int8_t (*)[BN][kPitch2]>(lds + buf * BUF + P * BM * kPitch2);
+#pragma unroll
+    for (int kk = 0; kk < kKT2 / 32; ++kk) {
+      i32x4 fa[P][WBM], fb[P][WBN];
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+#pragma unroll
+        for (int i = 0; i < WBM; ++i)
+          fa[p][i] = *reinterpret_cast<const i32x4*>(&As[p][wm * 32 * WBM + i * 32 + r][32 * kk + 16 * h]);
+#pragma unroll
+        for (int j = 0; j < WBN; ++j)
+          fb[p][j] = *reinterpret_cast<const i32x4*>(&Bs[p][wn * 32 * WBN + j * 32 + r][32 * kk + 16 * h]);
+      }
+#pragma unroll
+      for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int q = 0; q < P; ++q)
+#pragma unroll
+          for (int i = 0; i < WBM; ++i)
+#pragma unroll
+            for (int j = 0; j < WBN; ++j)
+              acc[p + q][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[p][i], fb[q][j], acc[p + q][i][j], 0, 0, 0);
+    }
+  };
+
+  // Double-buffered K loop: step kt's MFMAs read buffer kt&1 while step kt+1's planes are
+  // staged into the other buffer and step kt+2's global loads are in flight; one barrier per step.
+  const int nk = (K + kKT2 - 1) / kKT2;
+  load(0);
+  stage(0);
+  if (nk > 1) load(kKT2);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1);
+    if (kt + 2 < nk) load((kt + 2) * kKT2);
+    mma(cur);
+    __syncthreads();
+  }
+
+  // ---- epilogue: exact sums through LDS (reusing the plane buffers), int64 combine
+  int64_t* rs = reinterpret_cast<int64_t*>(lds);            // [AQ][BM]
+  int64_t* cs = rs + AQ * BM;                               // [16][BN]
+  rs[(tid % AQ) * BM + ar] = my_rsum;
+#pragma unroll
+  for (int c = 0; c < CW; ++c) cs[bq * BN + bg * CW + c] = my_csum[c];
+  __syncthreads();
+  const int64_t kpad = (int64_t)nk * kKT2;   // padded k terms are zeros: the identity holds over kpad
+#pragma unroll
+  for (int j = 0; j < WBN; ++j) {
+    const int cc = wn * 32 * WBN + j * 32 + r;
+    int64_t csum = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) csum += cs[q * BN + cc];
+    const int gcol = col0 + cc;
+#pragma unroll
+    for (int i = 0; i < WBM; ++i) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int rr = wm * 32 * WBM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const int grow = row0 + rr;
+        int64_t rsum = 0;
+#pragma unroll
+        for (int q = 0; q < AQ; ++q) rsum += rs[q * BM + rr];
+        uint64_t v = (uint64_t)(C0 * (rsum + csum)) - (uint64_t)kpad * (uint64_t)(C0 * C0);
+#pragma unroll
+        for (int s = 0; s < S; ++s) v += (uint64_t)(int64_t)acc[s][i][j][reg] << (8 * s);
+        if (grow < M && gcol < N) {
+          const int64_t sum = (int64_t)v;
+          if constexpr (sizeof(T) == 2) C[(size_t)grow * N + gcol] = (T)ssat16((int32_t)(sum >> 15));
+          else C[(size_t)grow * N + gcol] = (T)(int32_t)(sum >> 31);
+        }
+      }
+    }
+  }
+}
+
 // K beyond the i8 accumulators' exact range: one thread per output, int64 sum.
 template <typename T>
 __global__ __launch_bounds__(256) void mat_mult_fixed_valu_kernel(const T* __restrict__ A, const T* __restrict__ B,
@@ -183,8 +426,14 @@ static hipError_t launch_fixed(int m, int k, int n, const T* a, const T* b, T* c
   if (batch == 0 || m == 0 || n == 0) return hipSuccess;
   if (k == 0) return hipMemsetAsync(c, 0, sizeof(T) * (size_t)m * n * batch, st);
   if (k <= kMatI8MaxK) {
+#if MI355X_MATI8_V1
     const int tiles = ((m + kMT - 1) / kMT) * ((n + kNT - 1) / kNT);
     hipLaunchKernelGGL(mat_mult_i8_kernel<T>, dim3(tiles, 1, batch), dim3(256), 0, st, a, b, c, m, k, n);
+#else
+    using G = I8Cfg<T>;
+    const int tiles = ((m + G::BM - 1) / G::BM) * ((n + G::BN - 1) / G::BN);
+    hipLaunchKernelGGL(mat_mult_i8v2_kernel<T>, dim3(tiles, 1, batch), dim3(kNT2), 0, st, a, b, c, m, k, n);
+#endif
   } else {
     hipLaunchKernelGGL(mat_mult_fixed_valu_kernel<T>, dim3((n + 255) / 256, m, batch), dim3(256), 0, st, a, b, c,
                        m, k, n);
