@@ -191,7 +191,10 @@ __device__ __forceinline__ uint32_t gather4(uint32_t r0, uint32_t r1, uint32_t r
   return __builtin_amdgcn_perm(r1, r0, sel) | (__builtin_amdgcn_perm(r3, r2, sel) << 16);
 }
 
-template <typename T>
+// FULL: M % BM == 0, N % BN == 0, K % 64 == 0 and 16-B / 8-B aligned rows -- no bounds
+// checks, so the K loop is one basic block the scheduler can interleave (loads, staging,
+// MFMAs); otherwise every load is guarded and zero-filled.
+template <typename T, bool FULL>
 __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                              T* __restrict__ C, int M, int K, int N) {
   using G = I8Cfg<T>;
@@ -221,13 +224,13 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
   const int ar = tid / AQ, ak0 = AK * (tid % AQ);
   const int bq = tid & 15, bg = tid >> 4;
   const int gr = row0 + ar, gc = col0 + bg * CW;
-  const bool vecA = ((K * (int)sizeof(T)) % 16) == 0 && (((uintptr_t)A) & 15) == 0;
-  const bool vecB = ((N * (int)sizeof(T)) % 8) == 0 && (((uintptr_t)B) & 7) == 0;
+  const bool vecA = FULL || (((K * (int)sizeof(T)) % 16) == 0 && (((uintptr_t)A) & 15) == 0);
+  const bool vecB = FULL || (((N * (int)sizeof(T)) % 8) == 0 && (((uintptr_t)B) & 7) == 0);
 
   uint32_t ad[AKD], bd[4][BD];
   auto load = [&](int k0) {
     const int ka = k0 + ak0;
-    if (vecA && gr < M && ka + AK <= K) {
+    if (FULL || (vecA && gr < M && ka + AK <= K)) {
       const uint4* p = reinterpret_cast<const uint4*>(A + (size_t)gr * K + ka);
 #pragma unroll
       for (int i = 0; i < AKD / 4; ++i) {
@@ -250,7 +253,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int kb = k0 + 4 * bq + i;
-      if (vecB && kb < K && gc + CW <= N) {
+      if (FULL || (vecB && kb < K && gc + CW <= N)) {
         const uint2 v = *reinterpret_cast<const uint2*>(B + (size_t)kb * N + gc);
         bd[i][0] = v.x; bd[i][1] = v.y;
       } else {
@@ -395,7 +398,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
         uint64_t v = (uint64_t)(C0 * (rsum + csum)) - (uint64_t)kpad * (uint64_t)(C0 * C0);
 #pragma unroll
         for (int s = 0; s < S; ++s) v += (uint64_t)(int64_t)acc[s][i][j][reg] << (8 * s);
-        if (grow < M && gcol < N) {
+        if (FULL || (grow < M && gcol < N)) {
           const int64_t sum = (int64_t)v;
           if constexpr (sizeof(T) == 2) C[(size_t)grow * N + gcol] = (T)ssat16((int32_t)(sum >> 15));
           else C[(size_t)grow * N + gcol] = (T)(int32_t)(sum >> 31);
@@ -432,7 +435,13 @@ static hipError_t launch_fixed(int m, int k, int n, const T* a, const T* b, T* c
 #else
     using G = I8Cfg<T>;
     const int tiles = ((m + G::BM - 1) / G::BM) * ((n + G::BN - 1) / G::BN);
-    hipLaunchKernelGGL(mat_mult_i8v2_kernel<T>, dim3(tiles, 1, batch), dim3(kNT2), 0, st, a, b, c, m, k, n);
+    const bool full = m % G::BM == 0 && n % G::BN == 0 && k % kKT2 == 0 &&
+                      ((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0 && (k * sizeof(T)) % 16 == 0 &&
+                      (n * sizeof(T)) % 16 == 0;
+    if (full)
+      hipLaunchKernelGGL((mat_mult_i8v2_kernel<T, true>), dim3(tiles, 1, batch), dim3(kNT2), 0, st, a, b, c, m, k, n);
+    else
+      hipLaunchKernelGGL((mat_mult_i8v2_kernel<T, false>), dim3(tiles, 1, batch), dim3(kNT2), 0, st, a, b, c, m, k, n);
 #endif
   } else {
     hipLaunchKernelGGL(mat_mult_fixed_valu_kernel<T>, dim3((n + 255) / 256, m, batch), dim3(256), 0, st, a, b, c,
