@@ -173,9 +173,11 @@ __global__ __launch_bounds__(256) void mat_mult_i8_kernel(const T* __restrict__ 
 // 16 k-consecutive bytes per column, so staging transposes 4 k-rows x CW columns per thread
 // into k-contiguous dwords (v_perm) before the LDS write.
 template <typename T> struct I8Cfg;
-template <> struct I8Cfg<int16_t> { static constexpr int BM = 128, BN = 128, WBM = 1, WBN = 2; };
-template <> struct I8Cfg<int32_t> { static constexpr int BM = 128, BN = 64, WBM = 1, WBN = 1; };
-constexpr int kKT2 = 64, kPitch2 = kKT2 + 16;   // K step; LDS row pitch in bytes
+#ifndef MI355X_I8_KT15
+#define MI355X_I8_KT15 64
+#endif
+template <> struct I8Cfg<int16_t> { static constexpr int BM = 128, BN = 128, WBM = 1, WBN = 2, KT = MI355X_I8_KT15; };
+template <> struct I8Cfg<int32_t> { static constexpr int BM = 128, BN = 64, WBM = 1, WBN = 1, KT = 64; };
 constexpr int kNT2 = 512, kWavesM = 4, kWavesN = 2;
 
 // plane p of the two q15 values in each of d0, d1: [d0.lo, d0.hi, d1.lo, d1.hi] byte p
@@ -200,20 +202,28 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
   using G = I8Cfg<T>;
   constexpr int P = Slices<T>::P, S = 2 * P - 1;
   constexpr int64_t C0 = Slices<T>::C0;
-  constexpr int BM = G::BM, BN = G::BN, WBM = G::WBM, WBN = G::WBN;
+  constexpr int BM = G::BM, BN = G::BN, WBM = G::WBM, WBN = G::WBN, kKT2 = G::KT, kPitch2 = kKT2 + 16;
   static_assert(BM == kWavesM * 32 * WBM && BN == kWavesN * 32 * WBN, "wave grid covers the tile");
   constexpr int EPD = 4 / sizeof(T);             // elements per dword
   constexpr int AK = BM * kKT2 / kNT2;           // A elements per staging thread (16)
   constexpr int AKD = AK / EPD;                  // ... as dwords
   constexpr int AQ = kKT2 / AK;                  // threads per A row (4)
-  constexpr int CW = BN / (kNT2 / 16);           // B columns per staging thread (4 q15 / 2 q31)
-  constexpr int BD = CW / EPD;                   // dwords per B k-row segment (2)
+  constexpr int NQ = kKT2 / 4;                   // k-quads per K step
+  constexpr int CW = BN / (kNT2 / NQ);           // B columns per staging thread (8 q15 / 2 q31)
+  constexpr int BD = CW / EPD;                   // dwords per B k-row segment (4 / 2)
   constexpr int BUF = P * (BM + BN) * kPitch2;   // one K step's planes; two buffers
   __shared__ __attribute__((aligned(16))) int8_t lds[2 * BUF];
 
-  const int tilesN = (N + BN - 1) / BN;
-  const int tm = blockIdx.x / tilesN, tn = blockIdx.x % tilesN;
-  const size_t bz = blockIdx.z;
+  // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs, so the linear id is
+  // permuted to give each XCD a contiguous run of (matrix, tile) pairs -- the tiles of one
+  // matrix then share their A row bands / B column bands in that XCD's L2.
+  const int tilesN = (N + BN - 1) / BN, tiles = tilesN * ((M + BM - 1) / BM);
+  const uint32_t total = gridDim.x;
+  uint32_t lin = blockIdx.x;
+  if (total % 8 == 0) lin = (lin % 8) * (total / 8) + lin / 8;
+  const int t = (int)(lin % (uint32_t)tiles);
+  const int tm = t / tilesN, tn = t % tilesN;
+  const size_t bz = lin / (uint32_t)tiles;
   A += bz * (size_t)M * K;
   B += bz * (size_t)K * N;
   C += bz * (size_t)M * N;
@@ -222,10 +232,10 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
 
   // staging roles: A row ar, AK k from ak0; B k-quad bq (rows 4bq..4bq+3), columns bg*CW..+CW-1
   const int ar = tid / AQ, ak0 = AK * (tid % AQ);
-  const int bq = tid & 15, bg = tid >> 4;
+  const int bq = tid % NQ, bg = tid / NQ;
   const int gr = row0 + ar, gc = col0 + bg * CW;
   const bool vecA = FULL || (((K * (int)sizeof(T)) % 16) == 0 && (((uintptr_t)A) & 15) == 0);
-  const bool vecB = FULL || (((N * (int)sizeof(T)) % 8) == 0 && (((uintptr_t)B) & 7) == 0);
+  const bool vecB = FULL || (((N * (int)sizeof(T)) % (4 * BD)) == 0 && (((uintptr_t)B) & (4 * BD - 1)) == 0);
 
   uint32_t ad[AKD], bd[4][BD];
   auto load = [&](int k0) {
@@ -254,8 +264,13 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
     for (int i = 0; i < 4; ++i) {
       const int kb = k0 + 4 * bq + i;
       if (FULL || (vecB && kb < K && gc + CW <= N)) {
-        const uint2 v = *reinterpret_cast<const uint2*>(B + (size_t)kb * N + gc);
-        bd[i][0] = v.x; bd[i][1] = v.y;
+        if constexpr (BD == 4) {
+          const uint4 v = *reinterpret_cast<const uint4*>(B + (size_t)kb * N + gc);
+          bd[i][0] = v.x; bd[i][1] = v.y; bd[i][2] = v.z; bd[i][3] = v.w;
+        } else {
+          const uint2 v = *reinterpret_cast<const uint2*>(B + (size_t)kb * N + gc);
+          bd[i][0] = v.x; bd[i][1] = v.y;
+        }
       } else {
 #pragma unroll
         for (int d = 0; d < BD; ++d) {
@@ -313,13 +328,15 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
     // byte planes -> LDS
 #pragma unroll
     for (int p = 0; p < P; ++p) {
-      uint32_t w[4];
+      uint32_t w[AK / 4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < AK / 4; ++q) {
         if constexpr (sizeof(T) == 2) w[q] = plane_q15<P>(ad[2 * q], ad[2 * q + 1], p);
         else w[q] = plane4<P>(ad[4 * q], ad[4 * q + 1], ad[4 * q + 2], ad[4 * q + 3], p);
       }
-      *reinterpret_cast<uint4*>(&As[p][ar][ak0]) = make_uint4(w[0], w[1], w[2], w[3]);
+#pragma unroll
+      for (int q = 0; q < AK / 16; ++q)
+        *reinterpret_cast<uint4*>(&As[p][ar][ak0 + 16 * q]) = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 #pragma unroll
       for (int c = 0; c < CW; ++c) {
         const int d = c / EPD, o = (c % EPD) * (int)sizeof(T) + p;
@@ -373,7 +390,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
 
   // ---- epilogue: exact sums through LDS (reusing the plane buffers), int64 combine
   int64_t* rs = reinterpret_cast<int64_t*>(lds);            // [AQ][BM]
-  int64_t* cs = rs + AQ * BM;                               // [16][BN]
+  int64_t* cs = rs + AQ * BM;                               // [NQ][BN]
   rs[(tid % AQ) * BM + ar] = my_rsum;
 #pragma unroll
   for (int c = 0; c < CW; ++c) cs[bq * BN + bg * CW + c] = my_csum[c];
@@ -384,7 +401,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
     const int cc = wn * 32 * WBN + j * 32 + r;
     int64_t csum = 0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) csum += cs[q * BN + cc];
+    for (int q = 0; q < NQ; ++q) csum += cs[q * BN + cc];
     const int gcol = col0 + cc;
 #pragma unroll
     for (int i = 0; i < WBM; ++i) {
@@ -435,13 +452,13 @@ static hipError_t launch_fixed(int m, int k, int n, const T* a, const T* b, T* c
 #else
     using G = I8Cfg<T>;
     const int tiles = ((m + G::BM - 1) / G::BM) * ((n + G::BN - 1) / G::BN);
-    const bool full = m % G::BM == 0 && n % G::BN == 0 && k % kKT2 == 0 &&
+    const bool full = m % G::BM == 0 && n % G::BN == 0 && k % G::KT == 0 &&
                       ((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0 && (k * sizeof(T)) % 16 == 0 &&
                       (n * sizeof(T)) % 16 == 0;
     if (full)
-      hipLaunchKernelGGL((mat_mult_i8v2_kernel<T, true>), dim3(tiles, 1, batch), dim3(kNT2), 0, st, a, b, c, m, k, n);
+      hipLaunchKernelGGL((mat_mult_i8v2_kernel<T, true>), dim3(tiles * batch), dim3(kNT2), 0, st, a, b, c, m, k, n);
     else
-      hipLaunchKernelGGL((mat_mult_i8v2_kernel<T, false>), dim3(tiles, 1, batch), dim3(kNT2), 0, st, a, b, c, m, k, n);
+      hipLaunchKernelGGL((mat_mult_i8v2_kernel<T, false>), dim3(tiles * batch), dim3(kNT2), 0, st, a, b, c, m, k, n);
 #endif
   } else {
     hipLaunchKernelGGL(mat_mult_fixed_valu_kernel<T>, dim3((n + 255) / 256, m, batch), dim3(256), 0, st, a, b, c,
