@@ -462,7 +462,7 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 template <typename T>
 static hipError_t launch_fx4096(void* data, uint32_t batch, const void* tw, uint32_t flags, hipStream_t st) {
   using C = typename Fx<T>::C;
-  const uint32_t blocks = kFxT ? (batch + kFxT - 1) / kFxT : batch;
+  const uint32_t blocks = kFxT ? (batch + kFxT - 1) / (kFxT ? kFxT : 1) : batch;
   if (flags & kIfft) {
     const int grid = kFxT ? (int)blocks : persistent_grid((const void*)cfft_fx4096_kernel<T, true>, 256, 0, batch);
     hipLaunchKernelGGL((cfft_fx4096_kernel<T, true>), dim3(grid), dim3(256), 0, st, (C*)data, batch, (const C*)tw, flags);

@@ -173,6 +173,9 @@ __global__ __launch_bounds__(256) void mat_mult_i8_kernel(const T* __restrict__ 
 // 16 k-consecutive bytes per column, so staging transposes 4 k-rows x CW columns per thread
 // into k-contiguous dwords (v_perm) before the LDS write.
 template <typename T> struct I8Cfg;
+#ifndef MI355X_I8_SCHED
+#define MI355X_I8_SCHED 6
+#endif
 #ifndef MI355X_I8_KT15
 #define MI355X_I8_KT15 64
 #endif
@@ -346,21 +349,26 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
       }
     }
   };
-  auto mma = [&](int buf) {
+  constexpr int KS = kKT2 / 32;                  // MFMA k-steps per K step
+  i32x4 fa[KS][P][WBM], fb[KS][P][WBN];
+  auto frags = [&](int buf) {
     auto As = reinterpret_cast<const int8_t (*)[BM][kPitch2]>(lds + buf * BUF);
     auto Bs = reinterpret_cast<const int8_t (*)[BN][kPitch2]>(lds + buf * BUF + P * BM * kPitch2);
 #pragma unroll
-    for (int kk = 0; kk < kKT2 / 32; ++kk) {
-      i32x4 fa[P][WBM], fb[P][WBN];
+    for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
       for (int p = 0; p < P; ++p) {
 #pragma unroll
         for (int i = 0; i < WBM; ++i)
-          fa[p][i] = *reinterpret_cast<const i32x4*>(&As[p][wm * 32 * WBM + i * 32 + r][32 * kk + 16 * h]);
+          fa[kk][p][i] = *reinterpret_cast<const i32x4*>(&As[p][wm * 32 * WBM + i * 32 + r][32 * kk + 16 * h]);
 #pragma unroll
         for (int j = 0; j < WBN; ++j)
-          fb[p][j] = *reinterpret_cast<const i32x4*>(&Bs[p][wn * 32 * WBN + j * 32 + r][32 * kk + 16 * h]);
+          fb[kk][p][j] = *reinterpret_cast<const i32x4*>(&Bs[p][wn * 32 * WBN + j * 32 + r][32 * kk + 16 * h]);
       }
+  };
+  auto mma = [&]() {
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
       for (int p = 0; p < P; ++p)
 #pragma unroll
@@ -369,22 +377,38 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
           for (int i = 0; i < WBM; ++i)
 #pragma unroll
             for (int j = 0; j < WBN; ++j)
-              acc[p + q][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[p][i], fb[q][j], acc[p + q][i][j], 0, 0, 0);
-    }
+              acc[p + q][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kk][p][i], fb[kk][q][j], acc[p + q][i][j], 0, 0, 0);
   };
 
-  // Double-buffered K loop: step kt's MFMAs read buffer kt&1 while step kt+1's planes are
-  // staged into the other buffer and step kt+2's global loads are in flight; one barrier per step.
+  // Double-buffered K loop: step kt's fragments are read from buffer kt&1 first, then step
+  // kt+1's planes are staged into the other buffer and step kt+2's global loads issued, and
+  // the MFMAs (register-only) can interleave with that staging work; one barrier per step.
   const int nk = (K + kKT2 - 1) / kKT2;
   load(0);
   stage(0);
   if (nk > 1) load(kKT2);
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) {                    // steady state: one basic block when FULL
     const int cur = kt & 1;
+    frags(cur);
+    stage(cur ^ 1);
+    load((kt + 2) * kKT2);
+    mma();
+#if MI355X_I8_SCHED
+#pragma unroll
+    for (int i = 0; i < KS * P * P * WBM * WBN; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                 // one MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, MI355X_I8_SCHED, 0);   // then VALU
+    }
+#endif
+    __syncthreads();
+  }
+  for (; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    frags(cur);
     if (kt + 1 < nk) stage(cur ^ 1);
-    if (kt + 2 < nk) load((kt + 2) * kKT2);
-    mma(cur);
+    mma();
     __syncthreads();
   }
 
