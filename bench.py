@@ -50,6 +50,10 @@ WORKLOADS = {
     "mat_mult_f32": ("mat", 1024, 256, None),
     "mfcc_f32": ("mfcc", 1024, 1 << 18, 4),
     "rfft_f32": ("rfft", 1024, 1 << 20, 8),
+    # real length 8192 (inner CFFT 4096 = the fixed-point specialist); bytes per sample:
+    # N words in, N words written back (the inner CFFT overwrites pSrc), 2N words out
+    "rfft_q31": ("rfftq31", 8192, 1 << 16, 16),
+    "rfft_q15": ("rfftq15", 8192, 1 << 16, 8),
     "conv_f32": ("conv", 128, 1 << 16, 8),
     "mat_mult_q15": ("matq15", 1024, 64, None),
     "mat_mult_q31": ("matq31", 1024, 64, None),
@@ -114,7 +118,7 @@ def cpu_baseline(workload, n):
           "fir_f32": "fir_f32", "fir_q15": "fir_q15", "fir_q31": "fir_q31", "fir_fast_q15": "fir_fast_q15",
           "fir_fast_q31": "fir_fast_q31", "mat_mult_f32": "mat_mult_f32",
           "mfcc_f32": "mfcc_f32", "mat_mult_q15": "mat_mult_q15", "mat_mult_q31": "mat_mult_q31",
-          "rfft_f32": "rfft_f32", "conv_f32": "conv_f32"}[workload]
+          "rfft_f32": "rfft_f32", "conv_f32": "conv_f32", "rfft_q31": "rfft_q31", "rfft_q15": "rfft_q15"}[workload]
     nn = 256 if workload.startswith("mat_mult") else n  # 1024^3 takes seconds per matrix on one core
     out = subprocess.run([exe, wl, str(nn), str(threads), str(secs)], capture_output=True, text=True,
                          timeout=120)
@@ -251,6 +255,30 @@ def run_rfft(n, batch, steps, warmup, world, rank):
     return wall, kern_ms, {"checker": hk, "bit_exact": bool(ok), "transforms_checked": 64}
 
 
+def run_rfft_fixed(kind, n, batch, steps, warmup, world, rank):
+    """arm_rfft_q31 / _q15 forward over [batch][n] full-range real signals -> [batch][2n]
+    spectra; bit-exact check of 16 fresh signals (spectrum and overwritten input)."""
+    S = dsp.arm_rfft_instance_q31() if kind == "q31" else dsp.arm_rfft_instance_q15()
+    assert getattr(dsp, f"arm_rfft_init_{kind}")(S, n, 0, 1) == 0
+    src = synth(kind, batch * n, rank).view(batch, n)
+    out = torch.empty((batch, 2 * n), dtype=src.dtype, device="cuda")
+
+    def launch(s):
+        dsp.rfft_fixed_batch(S, src, out)
+
+    wall, kern_ms = time_launches(launch, steps, warmup, world)
+    host, hk = cpu_checker()
+    fresh = synth(kind, 16 * n, rank, salt=43).view(16, n)
+    fin = fresh.cpu().numpy()
+    fo = torch.empty((16, 2 * n), dtype=src.dtype, device="cuda")
+    dsp.rfft_fixed_batch(S, fresh, fo)
+    torch.cuda.synchronize()
+    want = [host.rfft_fixed(kind, n, fin[r], 0, 1) for r in range(16)]
+    ok = (fo.cpu().numpy().tobytes() == np.stack([w[0] for w in want]).tobytes()
+          and fresh.cpu().numpy().tobytes() == np.stack([w[1] for w in want]).tobytes())
+    return wall, kern_ms, {"checker": hk, "bit_exact": bool(ok), "signals_checked": 16}
+
+
 def run_conv(taps, batch, steps, warmup, world, rank, block=4096):
     """arm_conv_f32 of `batch` 4096-sample signals with one shared 128-sample kernel
     (the FIR config's shape): outputs of block + taps - 1 samples."""
@@ -336,7 +364,7 @@ def main():
     WORLD = parallel.init(backend=args.dist_backend)
     world, rank = WORLD.size, WORLD.rank
     kind, n, batch0, bps = WORKLOADS[args.workload]
-    if args.fftlen and args.workload.startswith(("cfft", "rfft")):
+    if args.fftlen and args.workload.startswith(("cfft", "rfft")):   # same bytes per launch
         batch0 = max(1, batch0 * n // args.fftlen)
         n = args.fftlen
     batch = args.batch or batch0
@@ -360,6 +388,10 @@ def main():
         wall, kern_ms, parity = run_rfft(n, batch, args.steps, args.warmup, world, rank)
         units = batch * n                                  # real input samples
         algo_bytes = units * bps                           # N floats in, N floats out
+    elif args.workload in ("rfft_q31", "rfft_q15"):
+        wall, kern_ms, parity = run_rfft_fixed(kind[4:], n, batch, args.steps, args.warmup, world, rank)
+        units = batch * n                                  # real input samples
+        algo_bytes = units * bps                           # N in, N written back, 2N spectrum out
     elif args.workload == "mfcc_f32":
         wall, kern_ms, parity = run_mfcc(n, batch, args.steps, args.warmup, world, rank)
         units = batch * n                                  # input samples
@@ -401,7 +433,8 @@ def main():
                     dtype={"f32": "f32", "q31": "q31 (int32)", "q15": "q15 (int16)", "fir_f32": "f32",
                            "fir_q15": "q15 (int16 x int16 -> int64)", "mfcc": "f32",
                            "fir_q31": "q31 (int32 x int32 -> int64)", "fir_fast_q15": "q15 (int32 wrap accumulator)",
-                           "fir_fast_q31": "q31 (rounded high-word accumulator)", "rfft": "f32", "conv": "f32"}[kind])
+                           "fir_fast_q31": "q31 (rounded high-word accumulator)", "rfft": "f32", "conv": "f32",
+                           "rfftq31": "q31 (int32)", "rfftq15": "q15 (int16)"}[kind])
         if args.workload.startswith("cfft"):
             line["config"] = {"workload": f"arm_cfft_{kind} N={n} batch={batch}/GPU in place, bitReverseFlag=1, "
                                           f"alternating fwd/inv (BASELINE configs[{1 if kind == 'f32' else 3}])",
@@ -412,6 +445,10 @@ def main():
         elif kind == "rfft":
             line["config"] = {"workload": f"arm_rfft_fast_f32 N={n} forward, batch={batch}/GPU", "fftLen": n,
                               "batch_per_gpu": batch, "parallelism": f"dp{world} shards"}
+        elif kind in ("rfftq31", "rfftq15"):
+            line["config"] = {"workload": f"arm_rfft_{kind[4:]} N={n} forward (inner CFFT {n // 2}), "
+                                          f"batch={batch}/GPU", "fftLenReal": n, "batch_per_gpu": batch,
+                              "parallelism": f"dp{world} shards"}
         elif kind == "mfcc":
             line["config"] = {"workload": f"arm_mfcc_f32 fftLen={n} 20 Mel / 13 DCT (reference MFCC F32 suite "
                                           f"tables) batch={batch} frames/GPU", "fftLen": n, "batch_per_gpu": batch,

@@ -21,8 +21,8 @@ from . import _abi
 from ._abi import (arm_cfft_instance_f32, arm_cfft_instance_q15, arm_cfft_instance_q31,  # noqa: F401
                    arm_fir_instance_f32, arm_fir_instance_q15, arm_fir_instance_q31, arm_matrix_instance_f32,
                    arm_rfft_fast_instance_f32, arm_mfcc_instance_f32, arm_matrix_instance_q15,
-                   arm_matrix_instance_q31, ARM_MATH_SUCCESS, ARM_MATH_ARGUMENT_ERROR,
-                   ARM_MATH_SIZE_MISMATCH)
+                   arm_matrix_instance_q31, arm_rfft_instance_q31, arm_rfft_instance_q15, ARM_MATH_SUCCESS,
+                   ARM_MATH_ARGUMENT_ERROR, ARM_MATH_SIZE_MISMATCH)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CMSISDSP_MI355X_LIB",
@@ -44,6 +44,7 @@ def _load():
     lib = C.CDLL(LIB_PATH)
     _abi.bind(lib, _abi.DROPIN)
     _abi.bind(lib, _abi.MFCC_LEN)
+    _abi.bind(lib, _abi.RFFTQ_LEN)
     _abi.bind(lib, _abi.BATCHED)
     return lib
 
@@ -118,6 +119,45 @@ def arm_rfft_fast_f32(S, x, ifftFlag):
     lib.arm_rfft_fast_f32(C.byref(S), p.ctypes.data, out.ctypes.data, ifftFlag)
     _check_void("arm_rfft_fast_f32")
     return out
+
+
+def arm_rfft_init_q31(S, n, ifftFlagR, bitReverseFlag):
+    return lib.arm_rfft_init_q31(C.byref(S), n, ifftFlagR, bitReverseFlag)
+
+
+def arm_rfft_init_q15(S, n, ifftFlagR, bitReverseFlag):
+    return lib.arm_rfft_init_q15(C.byref(S), n, ifftFlagR, bitReverseFlag)
+
+
+def _rfft_fixed(kind, S, x):
+    dt = np.int32 if kind == "q31" else np.int16
+    src = np.ascontiguousarray(x, dtype=dt).copy()
+    n = S.fftLenReal
+    out = np.zeros(n if S.ifftFlagR == 1 else 2 * n, dtype=dt)
+    fn = getattr(lib, f"arm_rfft_{kind}")
+    fn(C.byref(S), src.ctypes.data, out.ctypes.data)
+    _check_void(fn.__name__)
+    return out
+
+
+def arm_rfft_q31(S, x):
+    """Forward: N samples -> 2N-word spectrum; inverse: spectrum (>= N+2 words) -> N samples
+    (arm_rfft_q31.c:148-183; the input copy is consumed as in the reference)."""
+    return _rfft_fixed("q31", S, x)
+
+
+def arm_rfft_q15(S, x):
+    return _rfft_fixed("q15", S, x)
+
+
+def rfft_fixed_batch(S, src, dst, stream=None):
+    """Batched arm_rfft_q31 / _q15 on device tensors: forward src [batch, N] (overwritten)
+    -> dst [batch, 2N]; inverse src [batch, 2N] -> dst [batch, N]."""
+    kind = "q31" if isinstance(S, arm_rfft_instance_q31) else "q15"
+    fn = getattr(lib, f"arm_rfft_{kind}_batch")
+    st = fn(C.byref(S), C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()), dst.shape[0], _stream_ptr(stream))
+    if st != ARM_MATH_SUCCESS:
+        raise RuntimeError(f"{fn.__name__} -> {st}: {last_error()[1]}")
 
 
 class FirF32:

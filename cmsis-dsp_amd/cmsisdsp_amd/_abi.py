@@ -33,6 +33,18 @@ class arm_rfft_fast_instance_f32(C.Structure):
     _fields_ = [("Sint", arm_cfft_instance_f32), ("fftLenRFFT", C.c_uint16), ("pTwiddleRFFT", c_f32p)]
 
 
+def _rfft_fixed_struct(name, twp, cfft):
+    # Include/dsp/transform_functions.h:636-649 (q31), :508-521 (q15): non-Neon, non-MVE layout
+    return type(name, (C.Structure,), {"_fields_": [
+        ("fftLenReal", C.c_uint32), ("ifftFlagR", C.c_uint8), ("bitReverseFlagR", C.c_uint8),
+        ("twidCoefRModifier", C.c_uint32), ("pTwiddleAReal", twp), ("pTwiddleBReal", twp),
+        ("pCfft", C.POINTER(cfft))]})
+
+
+arm_rfft_instance_q31 = _rfft_fixed_struct("arm_rfft_instance_q31", c_i32p, arm_cfft_instance_q31)
+arm_rfft_instance_q15 = _rfft_fixed_struct("arm_rfft_instance_q15", c_i16p, arm_cfft_instance_q15)
+
+
 class arm_fir_instance_f32(C.Structure):
     # Include/dsp/filtering_functions.h:86-91
     _fields_ = [("numTaps", C.c_uint16), ("pState", c_f32p), ("pCoeffs", c_f32p)]
@@ -85,6 +97,10 @@ DROPIN = {
     "arm_cfft_q15": (None, [P(arm_cfft_instance_q15), C.c_void_p, C.c_uint8, C.c_uint8]),
     "arm_rfft_fast_init_f32": (C.c_int, [P(arm_rfft_fast_instance_f32), C.c_uint16]),
     "arm_rfft_fast_f32": (None, [P(arm_rfft_fast_instance_f32), C.c_void_p, C.c_void_p, C.c_uint8]),
+    "arm_rfft_init_q31": (C.c_int, [P(arm_rfft_instance_q31), C.c_uint32, C.c_uint32, C.c_uint32]),
+    "arm_rfft_init_q15": (C.c_int, [P(arm_rfft_instance_q15), C.c_uint32, C.c_uint32, C.c_uint32]),
+    "arm_rfft_q31": (None, [P(arm_rfft_instance_q31), C.c_void_p, C.c_void_p]),
+    "arm_rfft_q15": (None, [P(arm_rfft_instance_q15), C.c_void_p, C.c_void_p]),
     "arm_fir_init_f32": (None, [P(arm_fir_instance_f32), C.c_uint16, C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_fir_f32": (None, [P(arm_fir_instance_f32), C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_fir_init_q15": (C.c_int, [P(arm_fir_instance_q15), C.c_uint16, C.c_void_p, C.c_void_p, C.c_uint32]),
@@ -122,6 +138,13 @@ MFCC_LEN = {f"arm_mfcc_init_{n}_f32": (C.c_int, [P(arm_mfcc_instance_f32), C.c_u
                                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
             for n in RFFT_SIZES}
 
+# per-length q31 / q15 RFFT init functions (product and reference build; the oracle has
+# the generic init only)
+RFFTQ_SIZES = (32, 64, 128, 256, 512, 1024, 2048, 4096, 8192)
+RFFTQ_LEN = {f"arm_rfft_init_{n}_{t}": (C.c_int, [P(arm_rfft_instance_q31 if t == "q31" else arm_rfft_instance_q15),
+                                                 C.c_uint32, C.c_uint32])
+             for n in RFFTQ_SIZES for t in ("q31", "q15")}
+
 # the additive batched device API of include/arm_math_mi355x.h
 BATCHED = {
     "arm_cfft_f32_batch": (C.c_int, [P(arm_cfft_instance_f32), C.c_void_p, C.c_uint32, C.c_uint8, C.c_uint8,
@@ -132,6 +155,8 @@ BATCHED = {
                                      C.c_void_p]),
     "arm_rfft_fast_f32_batch": (C.c_int, [P(arm_rfft_fast_instance_f32), C.c_void_p, C.c_void_p, C.c_uint32,
                                           C.c_uint8, C.c_void_p]),
+    "arm_rfft_q31_batch": (C.c_int, [P(arm_rfft_instance_q31), C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "arm_rfft_q15_batch": (C.c_int, [P(arm_rfft_instance_q15), C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
     "arm_fir_f32_batch": (C.c_int, [P(arm_fir_instance_f32), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                     C.c_void_p, C.c_void_p]),
     "arm_fir_q15_batch": (C.c_int, [P(arm_fir_instance_q15), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,

@@ -4,6 +4,7 @@
 // nothing aborts.  There is no CPU fallback: all compute runs in the HIP kernels.
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/arm_math.h"
@@ -121,6 +122,76 @@ bool rfft_run(const arm_rfft_fast_instance_f32* S, float* d_p, float* d_out, uin
     MI_CHECK(rfft_f32_stage_launch((int)n, d_p, d_out, batch, (const float*)twr, st), "rfft stage");
   }
   return true;
+}
+
+// ---- RFFT q31 / q15 (arm_rfft_q31.c:148-183, arm_rfft_q15.c): `batch` signals.
+// Forward: d_src [batch][N] (overwritten by the inner CFFT, as the reference leaves pSrc),
+// d_dst [batch][2N].  Inverse: d_src [batch][2N] spectrum rows (words 0 .. N+1 read),
+// d_dst [batch][N]; the final arm_shift(+1) is folded into the inverse CFFT's store.
+template <typename T, typename RInst>
+bool rfft_fixed_run(const RInst* S, T* d_src, T* d_dst, uint32_t batch, hipStream_t st) {
+  constexpr int kind = sizeof(T) == 4 ? 1 : 2;
+  const uint32_t n = S->fftLenReal, L = n / 2;
+  const auto* in = S->pCfft;
+  if (!in || in->fftLen != L || !cfft_len_ok(L) || n > 8192) { set_error(hipErrorInvalidValue, "rfft instance"); return false; }
+  // the split reads realCoef[2*mod*k + 1] for k < L: mod * N words cover it
+  const size_t words = std::max<size_t>(2, (size_t)S->twidCoefRModifier * n);
+  const T* ta = (const T*)device_table(S->pTwiddleAReal, sizeof(T) * words);
+  const T* tb = (const T*)device_table(S->pTwiddleBReal, sizeof(T) * words);
+  if (!ta || !tb) return false;
+  const bool inv = S->ifftFlagR == 1u;
+  CfftPrep pr;
+  if (!cfft_prepare(L, in->pTwiddle, in->pBitRevTable, in->bitRevLength, kind, inv ? 1 : 0, S->bitReverseFlagR, pr))
+    return false;
+  auto pass = [&](const T* a, T* b) {
+    if constexpr (kind == 1)
+      return rfft_q31_pass_launch(inv, (int)n, a, b, batch, ta, tb, S->twidCoefRModifier, st);
+    else
+      return rfft_q15_pass_launch(inv, (int)n, a, b, batch, ta, tb, S->twidCoefRModifier, st);
+  };
+  if (inv) {
+    MI_CHECK(pass(d_src, d_dst), "rfft merge");
+    pr.flags |= kSatShl1;
+    MI_CHECK(cfft_launch(kind, L, d_dst, batch, pr, st), "rfft cfft");
+  } else {
+    MI_CHECK(cfft_launch(kind, L, d_src, batch, pr, st), "rfft cfft");
+    MI_CHECK(pass(d_src, d_dst), "rfft split");
+  }
+  return true;
+}
+
+// drop-in arm_rfft_q31 / _q15: host or device buffers, synchronous
+template <typename T, typename RInst>
+void rfft_fixed_sync(const RInst* S, T* pSrc, T* pDst) {
+  if (!S || !pSrc || !pDst) return;
+  const uint32_t n = S->fftLenReal;
+  if (n < 32 || n > 8192 || (n & (n - 1))) return;   // reference: lengths of the init switch only
+  const bool inv = S->ifftFlagR == 1u;
+  // forward: src N words in/out, dst 2N out; inverse: src words 0..N+1 in, dst N out
+  const size_t sb = sizeof(T) * (inv ? (size_t)n + 2 : n), db = sizeof(T) * (inv ? n : 2 * (size_t)n);
+  hipStream_t st = sync_stream();
+  const bool ds = is_device_ptr(pSrc), dd = is_device_ptr(pDst);
+  // the batched inverse reads spectrum rows of 2N words: a host row is staged that wide
+  T* s = ds ? pSrc : (T*)scratch(sizeof(T) * 2 * (size_t)n, 0);
+  T* d = dd ? pDst : (T*)scratch(db, 1);
+  if (!s || !d) { set_error(hipErrorOutOfMemory, "arm_rfft scratch"); return; }
+  hipError_t e = hipSuccess;
+  if (!ds) e = hipMemcpyAsync(s, pSrc, sb, hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) { set_error(e, "arm_rfft"); return; }
+  if (!rfft_fixed_run<T>(S, s, d, 1, st)) return;
+  if (!ds && !inv) e = hipMemcpyAsync(pSrc, s, sb, hipMemcpyDeviceToHost, st);   // forward overwrites pSrc
+  if (e == hipSuccess && !dd) e = hipMemcpyAsync(pDst, d, db, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) set_error(e, "arm_rfft");
+}
+
+template <typename T, typename RInst>
+arm_status rfft_fixed_batch(const RInst* S, T* d_src, T* d_dst, uint32_t batch, void* stream) {
+  if (!S || (batch && (!d_src || !d_dst))) return ARM_MATH_ARGUMENT_ERROR;
+  const uint32_t n = S->fftLenReal;
+  if (n < 32 || n > 8192 || (n & (n - 1))) return ARM_MATH_ARGUMENT_ERROR;
+  if (batch == 0) return ARM_MATH_SUCCESS;
+  return rfft_fixed_run<T>(S, d_src, d_dst, batch, (hipStream_t)stream) ? ARM_MATH_SUCCESS : ARM_MATH_ARGUMENT_ERROR;
 }
 
 // ---- MFCC (arm_mfcc_f32.c:83-160): the instance's user tables packed into one
@@ -398,6 +469,17 @@ arm_status arm_rfft_fast_f32_batch(const arm_rfft_fast_instance_f32* S, float32_
   if (!S || !rfft_len_ok(S->fftLenRFFT) || (batch && (!d_p || !d_out))) return ARM_MATH_ARGUMENT_ERROR;
   if (batch == 0) return ARM_MATH_SUCCESS;
   return rfft_run(S, d_p, d_out, batch, ifftFlag, (hipStream_t)stream) ? ARM_MATH_SUCCESS : ARM_MATH_ARGUMENT_ERROR;
+}
+
+void arm_rfft_q31(const arm_rfft_instance_q31* S, q31_t* pSrc, q31_t* pDst) { rfft_fixed_sync<int32_t>(S, pSrc, pDst); }
+void arm_rfft_q15(const arm_rfft_instance_q15* S, q15_t* pSrc, q15_t* pDst) { rfft_fixed_sync<int16_t>(S, pSrc, pDst); }
+arm_status arm_rfft_q31_batch(const arm_rfft_instance_q31* S, q31_t* d_src, q31_t* d_dst, uint32_t batch,
+                              void* stream) {
+  return rfft_fixed_batch<int32_t>(S, d_src, d_dst, batch, stream);
+}
+arm_status arm_rfft_q15_batch(const arm_rfft_instance_q15* S, q15_t* d_src, q15_t* d_dst, uint32_t batch,
+                              void* stream) {
+  return rfft_fixed_batch<int16_t>(S, d_src, d_dst, batch, stream);
 }
 
 void arm_fir_init_f32(arm_fir_instance_f32* S, uint16_t numTaps, const float32_t* pCoeffs, float32_t* pState,

@@ -156,6 +156,12 @@ template <> struct Fx<int16_t> {   // q15: complex = short2
   __device__ static void st(C* p, int2 v) { *p = make_short2((short)v.x, (short)v.y); }
 };
 
+// the RFFT inverse's arm_shift_<q31|q15>(pDst, 1, ...) on a complex word pair
+template <typename T> __device__ __forceinline__ int2 sat_shl1(int2 v) {
+  if constexpr (sizeof(T) == 4) return make_int2(sat_shl1_q31(v.x), sat_shl1_q31(v.y));
+  else return make_int2(sat_shl1_q15(v.x), sat_shl1_q15(v.y));
+}
+
 template <int N> struct PlanFx {
   static constexpr bool BY2 = (Log2<N>::v & 1) != 0;       // 32,128,512,2048
   static constexpr int M = BY2 ? N / 2 : N;                 // radix-4 length
@@ -286,6 +292,7 @@ __global__ __launch_bounds__(kBlock) void cfft_fx_kernel(typename Fx<T>::C* __re
           if constexpr (sizeof(T) == 4) v[u] = make_int2(wshl(v[u].x, 1), wshl(v[u].y, 1));
           else v[u] = make_int2(t16(v[u].x << 1), t16(v[u].y << 1));
         }
+        if (flags & kSatShl1) v[u] = sat_shl1<T>(v[u]);
       }
       if constexpr (sizeof(T) == 4) {
         dst[i] = make_int4(v[0].x, v[0].y, v[1].x, v[1].y);
@@ -444,6 +451,10 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 #pragma unroll
     for (int a = 0; a < 4; ++a)
       bfly<T, INV, 2>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], int2{}, int2{}, int2{});
+    if (flags & kSatShl1) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = sat_shl1<T>(v[u]);
+    }
     if (brev) {
 #pragma unroll
       for (int u = 0; u < 16; ++u) F::st(X + (int)(__brev((uint32_t)u) >> 28) * 256 + t, v[u]);

@@ -38,7 +38,16 @@ template <> struct Log2<1> { static constexpr int v = 0; };
 // armBitRevIndexTable_fixed_N (verified against the table swaps on the host).
 template <int B> __device__ __forceinline__ int bitrev(int k) { return (int)(__brev((uint32_t)k) >> (32 - B)); }
 
-// Flags shared by every transform kernel.
-enum : uint32_t { kIfft = 1u, kBitrev = 2u };
+// Flags shared by every transform kernel.  kSatShl1 (fixed point only): every output word
+// is shifted left by one with saturation on store -- arm_shift_q31 / arm_shift_q15 by +1
+// (arm_shift_q31.c:143-146, arm_shift_q15.c:225), which the q31/q15 inverse RFFT applies
+// after its inner CFFT (arm_rfft_q31.c:164).
+enum : uint32_t { kIfft = 1u, kBitrev = 2u, kSatShl1 = 4u };
+
+__device__ __forceinline__ int32_t sat_shl1_q31(int32_t v) {
+  const int32_t o = (int32_t)((uint32_t)v << 1);
+  return (o >> 1) != v ? (int32_t)(0x7FFFFFFF ^ (v >> 31)) : o;
+}
+__device__ __forceinline__ int32_t sat_shl1_q15(int32_t v) { return ssat16(v << 1); }
 
 }  // namespace mi355x

@@ -1,7 +1,8 @@
 // Host-side instance initialisation and the pre-initialised const instances.
 //
 // Mirrors Source/TransformFunctions/arm_cfft_init_{f32,q31,q15}.c (per-size CFFTINIT
-// macros + the fftLen switch), arm_rfft_fast_init_f32.c, Source/FilteringFunctions/
+// macros + the fftLen switch), arm_rfft_fast_init_f32.c, arm_rfft_init_{q31,q15}.c,
+// Source/FilteringFunctions/
 // arm_fir_init_{f32,q15}.c, Source/MatrixFunctions/arm_mat_init_f32.c and the const
 // structs of Source/CommonTables/arm_const_structs.c.  Pure host code: filling a struct
 // involves no device work (tables are uploaded lazily by the processing functions).
@@ -108,6 +109,47 @@ arm_status arm_rfft_fast_init_f32(arm_rfft_fast_instance_f32* S, uint16_t fftLen
     default: return ARM_MATH_ARGUMENT_ERROR;
   }
 }
+
+// ---- RFFT q31 / q15 init (arm_rfft_init_q31.c:99-124 RFFTINIT_Q31 + the switch at
+// :429-478; arm_rfft_init_q15.c likewise): split tables realCoef{A,B}Q31 / Q15 shared by
+// every length with modifier 8192 / N, the inner CFFT of N/2 from the const instances.
+#define MI_RFFTQ_INIT(N, H, MOD, T, TAB)                                                           \
+  arm_status arm_rfft_init_##N##_##T(arm_rfft_instance_##T* S, uint32_t ifftFlagR, uint32_t bitReverseFlag) { \
+    if (!S) return ARM_MATH_ARGUMENT_ERROR;                                                         \
+    S->fftLenReal = N;                                                                              \
+    S->pTwiddleAReal = realCoefA##TAB;                                                              \
+    S->pTwiddleBReal = realCoefB##TAB;                                                              \
+    S->ifftFlagR = (uint8_t)ifftFlagR;                                                              \
+    S->bitReverseFlagR = (uint8_t)bitReverseFlag;                                                   \
+    S->twidCoefRModifier = MOD;                                                                     \
+    S->pCfft = &arm_cfft_sR_##T##_len##H;                                                           \
+    return ARM_MATH_SUCCESS;                                                                        \
+  }
+#define MI_RFFTQ_ALL(T, TAB)                                                                       \
+  MI_RFFTQ_INIT(8192, 4096, 1, T, TAB) MI_RFFTQ_INIT(4096, 2048, 2, T, TAB)                        \
+  MI_RFFTQ_INIT(2048, 1024, 4, T, TAB) MI_RFFTQ_INIT(1024, 512, 8, T, TAB)                         \
+  MI_RFFTQ_INIT(512, 256, 16, T, TAB) MI_RFFTQ_INIT(256, 128, 32, T, TAB)                          \
+  MI_RFFTQ_INIT(128, 64, 64, T, TAB) MI_RFFTQ_INIT(64, 32, 128, T, TAB)                            \
+  MI_RFFTQ_INIT(32, 16, 256, T, TAB)                                                               \
+  arm_status arm_rfft_init_##T(arm_rfft_instance_##T* S, uint32_t fftLenReal, uint32_t ifftFlagR,  \
+                               uint32_t bitReverseFlag) {                                          \
+    switch (fftLenReal) {                                                                          \
+      case 8192: return arm_rfft_init_8192_##T(S, ifftFlagR, bitReverseFlag);                      \
+      case 4096: return arm_rfft_init_4096_##T(S, ifftFlagR, bitReverseFlag);                      \
+      case 2048: return arm_rfft_init_2048_##T(S, ifftFlagR, bitReverseFlag);                      \
+      case 1024: return arm_rfft_init_1024_##T(S, ifftFlagR, bitReverseFlag);                      \
+      case 512: return arm_rfft_init_512_##T(S, ifftFlagR, bitReverseFlag);                        \
+      case 256: return arm_rfft_init_256_##T(S, ifftFlagR, bitReverseFlag);                        \
+      case 128: return arm_rfft_init_128_##T(S, ifftFlagR, bitReverseFlag);                        \
+      case 64: return arm_rfft_init_64_##T(S, ifftFlagR, bitReverseFlag);                          \
+      case 32: return arm_rfft_init_32_##T(S, ifftFlagR, bitReverseFlag);                          \
+      default: return ARM_MATH_ARGUMENT_ERROR;                                                     \
+    }                                                                                              \
+  }
+MI_RFFTQ_ALL(q31, Q31)
+MI_RFFTQ_ALL(q15, Q15)
+#undef MI_RFFTQ_ALL
+#undef MI_RFFTQ_INIT
 
 // ---- MFCC init (arm_mfcc_init_f32.c): record the tables, initialise the inner RFFT
 static void mfcc_fields(arm_mfcc_instance_f32* S, uint32_t fftLen, uint32_t nbMelFilters, uint32_t nbDctOutputs,

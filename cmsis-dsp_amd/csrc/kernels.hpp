@@ -27,7 +27,8 @@ inline int persistent_grid(const void* kernel, int block, size_t lds, uint64_t i
 
 // In-place batched CFFT over `batch` contiguous transforms of n complex samples.
 // tw: device copy of the instance's twiddle table.  perm: optional device permutation
-// (nullptr = the reference tables' canonical digit reversal).  flags: kIfft | kBitrev.
+// (nullptr = the reference tables' canonical digit reversal).  flags: kIfft | kBitrev
+// (| kSatShl1 for q31 / q15).
 hipError_t cfft_f32_launch(int n, float* data, uint32_t batch, const float* tw, const uint16_t* perm,
                            uint32_t flags, hipStream_t st);
 hipError_t cfft_q31_launch(int n, int32_t* data, uint32_t batch, const int32_t* tw, const uint16_t* perm,
@@ -45,6 +46,14 @@ hipError_t rfft_f32_fused_launch(int n_real, bool inverse, const float* p, float
                                  const float* tw, const float* tw_rfft, hipStream_t st);
 hipError_t rfft_f32_merge_launch(int n_real, const float* p, float* out, uint32_t batch,
                                  const float* tw_rfft, hipStream_t st);
+
+// RFFT q31 / q15 split (forward: src = [batch][N] CFFT(N/2) output -> dst [batch][2N]
+// spectrum) or merge (inverse: src = [batch][2N] spectrum rows -> dst [batch][N] inverse
+// CFFT input) pass.  ta / tb: device realCoef{A,B}; mod = the instance's modifier.
+hipError_t rfft_q31_pass_launch(bool inverse, int n, const int32_t* src, int32_t* dst, uint32_t batch,
+                                const int32_t* ta, const int32_t* tb, uint32_t mod, hipStream_t st);
+hipError_t rfft_q15_pass_launch(bool inverse, int n, const int16_t* src, int16_t* dst, uint32_t batch,
+                                const int16_t* ta, const int16_t* tb, uint32_t mod, hipStream_t st);
 
 // FIR: `batch` independent filters sharing one coefficient set, any of the five reference
 // variants (kind).  hist: [batch][numTaps-1] streaming state (read, then overwritten with

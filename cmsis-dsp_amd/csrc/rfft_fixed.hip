@@ -1,0 +1,148 @@
+// Real FFT, q31 and q15 — the split / merge passes around the batched fixed-point CFFT
+// (MI355X, gfx950), bit-exact.
+//
+// Replaces the host scalar path of
+//   q31: Source/TransformFunctions/arm_rfft_q31.c:148-183 (dispatch),
+//        arm_split_rfft_q31 :256-341, arm_split_rifft_q31 :397-476 (scalar branches);
+//   q15: arm_rfft_q15.c dispatch, arm_split_rfft_q15 / arm_split_rifft_q15
+//        (!ARM_MATH_DSP branches);
+//   the inverse's arm_shift_q31 / arm_shift_q15 by +1 is folded into the inverse CFFT's
+//   store (kSatShl1, cfft_fixed.hip).
+// L = N/2 complex bins of the inner CFFT.  One thread per (signal, k), k in [0, L):
+//   forward: reads bins k and L-k of the CFFT output, writes spectrum bin k and, for
+//            k >= 1, its mirror N-k (thread k = 0 writes bins 0 and L) -> 2N words out;
+//   inverse: reads bins k and L-k of the 2N-word spectrum row, writes bin k of the N-word
+//            CFFT input.
+// Twiddle c = 2*modifier*k into realCoef{A,B} (shared 8192-entry tables, L2-resident).
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace mi355x {
+
+namespace {
+
+// ((q63)x*y + 2^31) >> 32 forms of none.h:184-194 (SMMULR / SMMLAR / SMMLSR) -> common.hpp
+__device__ __forceinline__ int32_t wneg(int32_t a) { return (int32_t)(0u - (uint32_t)a); }
+// q15 x q15 product as a wrapping int32 term
+__device__ __forceinline__ uint32_t p16(int32_t a, int32_t b) { return (uint32_t)(a * b); }
+
+template <typename T> struct Cx;
+template <> struct Cx<int32_t> {
+  using C = int2;
+  __device__ static int2 ld(const int32_t* p) { return *reinterpret_cast<const int2*>(p); }
+  __device__ static void st(int32_t* p, int32_t re, int32_t im) { *reinterpret_cast<int2*>(p) = make_int2(re, im); }
+};
+template <> struct Cx<int16_t> {
+  __device__ static int2 ld(const int16_t* p) {
+    const short2 s = *reinterpret_cast<const short2*>(p);
+    return make_int2(s.x, s.y);
+  }
+  __device__ static void st(int16_t* p, int32_t re, int32_t im) {
+    *reinterpret_cast<short2*>(p) = make_short2((short)re, (short)im);
+  }
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void rfft_fx_split_kernel(const T* __restrict__ src, T* __restrict__ dst,
+                                                            uint64_t total, int n, int log2l,
+                                                            const T* __restrict__ ta, const T* __restrict__ tb,
+                                                            uint32_t mod) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const int L = n >> 1;
+  const uint64_t row = gid >> log2l;
+  const int k = (int)(gid & (uint64_t)(L - 1));
+  const T* x = src + row * (uint64_t)n;
+  T* y = dst + row * (uint64_t)(2 * n);
+  if (k == 0) {
+    const int2 v = Cx<T>::ld(x);
+    if constexpr (sizeof(T) == 4) {
+      Cx<T>::st(y + n, wsub(v.x, v.y) >> 1, 0);
+      Cx<T>::st(y, wadd(v.x, v.y) >> 1, 0);
+    } else {
+      Cx<T>::st(y + n, (v.x - v.y) >> 1, 0);
+      Cx<T>::st(y, (v.x + v.y) >> 1, 0);
+    }
+    return;
+  }
+  const int2 a = Cx<T>::ld(x + 2 * k), b = Cx<T>::ld(x + 2 * (L - k));
+  const uint32_t c = 2u * mod * (uint32_t)k;
+  const int32_t a1 = ta[c], a2 = ta[c + 1], b1 = tb[c];
+  if constexpr (sizeof(T) == 4) {
+    // arm_rfft_q31.c:293-326
+    int32_t re = mult_R(a.x, a1), im = mult_R(a.x, a2);
+    re = multSub_R(re, a.y, a2); im = multAcc_R(im, a.y, a1);
+    re = multSub_R(re, b.y, a2); im = multSub_R(im, b.y, b1);
+    re = multAcc_R(re, b.x, b1); im = multSub_R(im, b.x, a2);
+    Cx<T>::st(y + 2 * k, re, im);
+    Cx<T>::st(y + 2 * n - 2 * k, re, wneg(im));
+  } else {
+    // arm_rfft_q15.c scalar branch: wrapping int sums, >> 16, stores truncate to q15_t
+    const int32_t b2 = tb[c + 1];
+    const int32_t re = (int32_t)(p16(a.x, a1) - p16(a.y, a2) + p16(b.x, b1) + p16(b.y, b2)) >> 16;
+    const int32_t im = (int32_t)(p16(b.x, b2) - p16(b.y, b1) + p16(a.y, a1) + p16(a.x, a2)) >> 16;
+    Cx<T>::st(y + 2 * k, re, im);
+    Cx<T>::st(y + 2 * n - 2 * k, re, -im);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void rfft_fx_merge_kernel(const T* __restrict__ src, T* __restrict__ dst,
+                                                            uint64_t total, int n, int log2l,
+                                                            const T* __restrict__ ta, const T* __restrict__ tb,
+                                                            uint32_t mod) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const int L = n >> 1;
+  const uint64_t row = gid >> log2l;
+  const int k = (int)(gid & (uint64_t)(L - 1));
+  const T* x = src + row * (uint64_t)(2 * n);
+  T* y = dst + row * (uint64_t)n;
+  const int2 a = Cx<T>::ld(x + 2 * k), b = Cx<T>::ld(x + 2 * (L - k));
+  const uint32_t c = 2u * mod * (uint32_t)k;
+  const int32_t a1 = ta[c], a2 = ta[c + 1], b1 = tb[c];
+  if constexpr (sizeof(T) == 4) {
+    // arm_rfft_q31.c:430-466
+    int32_t re = mult_R(a.x, a1), im = mult_R(a.x, wneg(a2));
+    re = multAcc_R(re, a.y, a2); im = multAcc_R(im, a.y, a1);
+    re = multAcc_R(re, b.y, a2); im = multSub_R(im, b.y, b1);
+    re = multAcc_R(re, b.x, b1); im = multAcc_R(im, b.x, a2);
+    Cx<T>::st(y + 2 * k, re, im);
+  } else {
+    const int32_t b2 = tb[c + 1];
+    const int32_t re = (int32_t)(p16(b.x, b1) - p16(b.y, b2) + p16(a.x, a1) + p16(a.y, a2)) >> 16;
+    const int32_t im = (int32_t)(p16(a.y, a1) - p16(a.x, a2) - p16(b.x, b2) - p16(b.y, b1)) >> 16;
+    Cx<T>::st(y + 2 * k, re, im);
+  }
+}
+
+}  // namespace
+
+template <typename T>
+static hipError_t rfft_fx_pass(bool inverse, int n, const T* src, T* dst, uint32_t batch, const T* ta, const T* tb,
+                               uint32_t mod, hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  int log2l = 0;
+  while ((1 << log2l) < n / 2) ++log2l;
+  const uint64_t total = (uint64_t)batch << log2l;
+  const uint64_t blocks = (total + 255) / 256;
+  if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  if (inverse)
+    hipLaunchKernelGGL((rfft_fx_merge_kernel<T>), dim3((uint32_t)blocks), dim3(256), 0, st, src, dst, total, n, log2l,
+                       ta, tb, mod);
+  else
+    hipLaunchKernelGGL((rfft_fx_split_kernel<T>), dim3((uint32_t)blocks), dim3(256), 0, st, src, dst, total, n, log2l,
+                       ta, tb, mod);
+  return hipGetLastError();
+}
+
+hipError_t rfft_q31_pass_launch(bool inverse, int n, const int32_t* src, int32_t* dst, uint32_t batch,
+                                const int32_t* ta, const int32_t* tb, uint32_t mod, hipStream_t st) {
+  return rfft_fx_pass<int32_t>(inverse, n, src, dst, batch, ta, tb, mod, st);
+}
+hipError_t rfft_q15_pass_launch(bool inverse, int n, const int16_t* src, int16_t* dst, uint32_t batch,
+                                const int16_t* ta, const int16_t* tb, uint32_t mod, hipStream_t st) {
+  return rfft_fx_pass<int16_t>(inverse, n, src, dst, batch, ta, tb, mod, st);
+}
+
+}  // namespace mi355x

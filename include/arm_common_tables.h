@@ -39,6 +39,12 @@ extern const float twiddleCoef_rfft_1024[1024];
 extern const float twiddleCoef_rfft_2048[2048];
 extern const float twiddleCoef_rfft_4096[4096];
 
+/* real FFT split twiddles, q31 / q15 (Include/arm_common_tables.h:241-245) */
+extern const int32_t realCoefAQ31[8192];
+extern const int32_t realCoefBQ31[8192];
+extern const int16_t realCoefAQ15[8192];
+extern const int16_t realCoefBQ15[8192];
+
 /* bit-reversal table lengths: Include/arm_common_tables.h:181-235 */
 #define ARMBITREVINDEXTABLE_16_TABLE_LENGTH   ((uint16_t)20)
 #define ARMBITREVINDEXTABLE_32_TABLE_LENGTH   ((uint16_t)48)

@@ -75,6 +75,28 @@ typedef struct {
   const float32_t            *pTwiddleRFFT;
 } arm_rfft_fast_instance_f32;
 
+/* ---- real FFT instances, q31 / q15 (non-Neon, non-MVE build):
+ * Include/dsp/transform_functions.h:636-649 (q31), :508-521 (q15) */
+typedef struct {
+        uint32_t   fftLenReal;            /* real length N (32 ... 8192) */
+        uint8_t    ifftFlagR;             /* 0 forward, 1 inverse */
+        uint8_t    bitReverseFlagR;       /* passed to the inner CFFT */
+        uint32_t   twidCoefRModifier;     /* 8192 / N: stride into realCoefA/BQ31 */
+  const q31_t     *pTwiddleAReal;
+  const q31_t     *pTwiddleBReal;
+  const arm_cfft_instance_q31 *pCfft;     /* inner CFFT of N/2 */
+} arm_rfft_instance_q31;
+
+typedef struct {
+        uint32_t   fftLenReal;
+        uint8_t    ifftFlagR;
+        uint8_t    bitReverseFlagR;
+        uint32_t   twidCoefRModifier;
+  const q15_t     *pTwiddleAReal;
+  const q15_t     *pTwiddleBReal;
+  const arm_cfft_instance_q15 *pCfft;
+} arm_rfft_instance_q15;
+
 /* ---- MFCC instance (RFFT-based default build): Include/dsp/transform_functions.h:856-873 */
 typedef struct {
   const float32_t *dctCoefs;        /* nbDctOutputs x nbMelFilters, row-major */
@@ -198,6 +220,37 @@ arm_status arm_rfft_fast_init_4096_f32(arm_rfft_fast_instance_f32 *S);
 arm_status arm_rfft_fast_init_f32(arm_rfft_fast_instance_f32 *S, uint16_t fftLen);
 void arm_rfft_fast_f32(const arm_rfft_fast_instance_f32 *S, float32_t *p,
                        float32_t *pOut, uint8_t ifftFlag);
+
+/* ===================================================================================
+ * Real FFT, q31 / q15.  Prototypes: Include/dsp/transform_functions.h:695-749 (q31),
+ * :566-620 (q15).  Reference bodies: Source/TransformFunctions/arm_rfft_init_q31.c:99-124,
+ * :429-478, arm_rfft_q31.c:148-183 (+ arm_split_rfft_q31 / arm_split_rifft_q31, scalar
+ * branches), arm_rfft_init_q15.c, arm_rfft_q15.c (scalar, !ARM_MATH_DSP branches).
+ * Lengths 32 ... 8192.  Forward: pSrc (N words) is overwritten by the inner CFFT, pDst
+ * receives 2N words (the full conjugate-symmetric spectrum).  Inverse: pSrc holds the
+ * spectrum (words 0 .. N+1 are read), pDst receives N words (<< 1, saturated).
+ * =================================================================================== */
+#define ARM_MI355X_DECL_RFFT_INIT(N)                                                        \
+  arm_status arm_rfft_init_##N##_q31(arm_rfft_instance_q31 *S, uint32_t ifftFlagR,          \
+                                     uint32_t bitReverseFlag);                              \
+  arm_status arm_rfft_init_##N##_q15(arm_rfft_instance_q15 *S, uint32_t ifftFlagR,          \
+                                     uint32_t bitReverseFlag);
+ARM_MI355X_DECL_RFFT_INIT(32)
+ARM_MI355X_DECL_RFFT_INIT(64)
+ARM_MI355X_DECL_RFFT_INIT(128)
+ARM_MI355X_DECL_RFFT_INIT(256)
+ARM_MI355X_DECL_RFFT_INIT(512)
+ARM_MI355X_DECL_RFFT_INIT(1024)
+ARM_MI355X_DECL_RFFT_INIT(2048)
+ARM_MI355X_DECL_RFFT_INIT(4096)
+ARM_MI355X_DECL_RFFT_INIT(8192)
+#undef ARM_MI355X_DECL_RFFT_INIT
+arm_status arm_rfft_init_q31(arm_rfft_instance_q31 *S, uint32_t fftLenReal, uint32_t ifftFlagR,
+                             uint32_t bitReverseFlag);
+arm_status arm_rfft_init_q15(arm_rfft_instance_q15 *S, uint32_t fftLenReal, uint32_t ifftFlagR,
+                             uint32_t bitReverseFlag);
+void arm_rfft_q31(const arm_rfft_instance_q31 *S, q31_t *pSrc, q31_t *pDst);
+void arm_rfft_q15(const arm_rfft_instance_q15 *S, q15_t *pSrc, q15_t *pDst);
 
 /* ===================================================================================
  * MFCC, f32.  Prototypes: Include/dsp/transform_functions.h:875-990

@@ -42,6 +42,16 @@ arm_status arm_cfft_q15_batch(const arm_cfft_instance_q15 *S, q15_t *d_p1, uint3
 arm_status arm_rfft_fast_f32_batch(const arm_rfft_fast_instance_f32 *S, float32_t *d_p,
                                    float32_t *d_out, uint32_t batch, uint8_t ifftFlag, void *stream);
 
+/* Real FFT, q31 / q15, over `batch` signals (per item: arm_rfft_q31 / arm_rfft_q15,
+ * arm_rfft_q31.c:148-183).  Forward (S->ifftFlagR != 1): d_src [batch][N] is overwritten
+ * by the inner CFFT as in the reference, d_dst [batch][2N] receives the spectra.
+ * Inverse: d_src [batch][2N] spectrum rows (words 0 .. N+1 of each row are read; the
+ * layout of the forward output), d_dst [batch][N]. */
+arm_status arm_rfft_q31_batch(const arm_rfft_instance_q31 *S, q31_t *d_src, q31_t *d_dst, uint32_t batch,
+                              void *stream);
+arm_status arm_rfft_q15_batch(const arm_rfft_instance_q15 *S, q15_t *d_src, q15_t *d_dst, uint32_t batch,
+                              void *stream);
+
 /* MFCC over `batch` contiguous frames of S->fftLen samples (arm_mfcc_f32.c:83-160 per
  * frame).  d_src: [batch][fftLen] input frames (used as work space: overwritten);
  * d_tmp: [batch][fftLen] work space; d_dst: [batch][nbDctOutputs].  The instance's

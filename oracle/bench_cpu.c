@@ -6,6 +6,7 @@
  *   oracle/_build/bench_port -DBENCH_AGAINST_ORACLE: linked to the restatement -> "port".
  * Usage: bench_xxx <workload> <n> <threads> <seconds>
  *   workload: cfft_f32 | cfft_q31 | cfft_q15 (n = fftLen), fir_f32 | fir_q15 (n = numTaps, block 4096),
+ *             rfft_f32 | rfft_q31 | rfft_q15 (n = real length, forward),
  *             mat_mult_f32 (n = square dimension), mfcc_f32 (n = fftLen; 20 triangular Mel
  *             filters, 13 DCT outputs, Hamming window -- the suite's shape)
  * Each thread owns its own buffers (the library is reentrant) and runs until the time
@@ -137,6 +138,21 @@ static void *worker(void *arg) {
       samples += 16.0 * n;
     } while (now() - t0 < j->seconds);
     free(x); free(p); free(o);
+  } else if (!strcmp(j->wl, "rfft_q31") || !strcmp(j->wl, "rfft_q15")) {
+    const int n = j->n, q31 = !strcmp(j->wl, "rfft_q31");
+    int32_t *x31 = malloc(sizeof(int32_t) * n), *p31 = malloc(sizeof(int32_t) * n), *o31 = malloc(sizeof(int32_t) * 2 * n);
+    int16_t *x15 = malloc(sizeof(int16_t) * n), *p15 = malloc(sizeof(int16_t) * n), *o15 = malloc(sizeof(int16_t) * 2 * n);
+    for (int i = 0; i < n; ++i) { x31[i] = (int32_t)sm(&seed); x15[i] = (int16_t)(sm(&seed) >> 7); }
+    arm_rfft_instance_q31 S31; arm_rfft_instance_q15 S15;
+    F(arm_rfft_init_q31)(&S31, (uint32_t)n, 0, 1); F(arm_rfft_init_q15)(&S15, (uint32_t)n, 0, 1);
+    do {
+      for (int r = 0; r < 16; ++r) {
+        if (q31) { memcpy(p31, x31, sizeof(int32_t) * n); F(arm_rfft_q31)(&S31, p31, o31); }
+        else { memcpy(p15, x15, sizeof(int16_t) * n); F(arm_rfft_q15)(&S15, p15, o15); }
+      }
+      samples += 16.0 * n;
+    } while (now() - t0 < j->seconds);
+    free(x31); free(p31); free(o31); free(x15); free(p15); free(o15);
   } else if (!strcmp(j->wl, "mfcc_f32")) {
     const int n = j->n, nm = 20, nd = 13;
     uint32_t pos[20], len[20], total = 0;

@@ -25,6 +25,8 @@ SRCS := \
   $(T)/arm_cfft_q15.c $(T)/arm_cfft_radix4_q15.c $(T)/arm_cfft_init_q15.c \
   $(T)/arm_bitreversal2.c $(T)/arm_bitreversal.c \
   $(T)/arm_rfft_fast_f32.c $(T)/arm_rfft_fast_init_f32.c \
+  $(T)/arm_rfft_q31.c $(T)/arm_rfft_init_q31.c $(T)/arm_rfft_q15.c $(T)/arm_rfft_init_q15.c \
+  $(B)/arm_shift_q31.c $(B)/arm_shift_q15.c \
   $(F)/arm_fir_f32.c $(F)/arm_fir_init_f32.c $(F)/arm_fir_q15.c $(F)/arm_fir_init_q15.c \
   $(F)/arm_fir_q31.c $(F)/arm_fir_init_q31.c $(F)/arm_fir_fast_q15.c $(F)/arm_fir_fast_q31.c \
   $(F)/arm_conv_f32.c $(F)/arm_conv_q15.c $(F)/arm_conv_q31.c \

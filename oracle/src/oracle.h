@@ -9,6 +9,10 @@ void oracle_arm_cfft_f32(const arm_cfft_instance_f32 *S, float *p1, uint8_t ifft
 void oracle_arm_cfft_q31(const arm_cfft_instance_q31 *S, int32_t *p1, uint8_t ifftFlag, uint8_t bitReverseFlag);
 void oracle_arm_cfft_q15(const arm_cfft_instance_q15 *S, int16_t *p1, uint8_t ifftFlag, uint8_t bitReverseFlag);
 void oracle_arm_rfft_fast_f32(const arm_rfft_fast_instance_f32 *S, float *p, float *pOut, uint8_t ifftFlag);
+void oracle_arm_rfft_q31(const arm_rfft_instance_q31 *S, int32_t *pSrc, int32_t *pDst);
+void oracle_arm_rfft_q15(const arm_rfft_instance_q15 *S, int16_t *pSrc, int16_t *pDst);
+arm_status oracle_arm_rfft_init_q31(arm_rfft_instance_q31 *S, uint32_t n, uint32_t ifftFlagR, uint32_t bitReverseFlag);
+arm_status oracle_arm_rfft_init_q15(arm_rfft_instance_q15 *S, uint32_t n, uint32_t ifftFlagR, uint32_t bitReverseFlag);
 void oracle_arm_fir_f32(const arm_fir_instance_f32 *S, const float *pSrc, float *pDst, uint32_t blockSize);
 void oracle_arm_fir_q15(const arm_fir_instance_q15 *S, const int16_t *pSrc, int16_t *pDst, uint32_t blockSize);
 void oracle_arm_fir_fast_q15(const arm_fir_instance_q15 *S, const int16_t *pSrc, int16_t *pDst, uint32_t blockSize);

@@ -108,3 +108,27 @@ void oracle_arm_mat_init_q31(arm_matrix_instance_q31 *S, uint16_t r, uint16_t c,
 void oracle_arm_mat_init_f32(arm_matrix_instance_f32 *S, uint16_t r, uint16_t c, float *p) {
   S->numRows = r; S->numCols = c; S->pData = p;
 }
+
+/* RFFT q31 / q15 (arm_rfft_init_q31.c:99-124, :429-478; arm_rfft_init_q15.c): lengths
+ * 32 ... 8192, inner CFFT of N/2, twiddle modifier 8192 / N. */
+static arm_cfft_instance_q31 g_rfft_cfft_q31[9];
+static arm_cfft_instance_q15 g_rfft_cfft_q15[9];
+
+arm_status oracle_arm_rfft_init_q31(arm_rfft_instance_q31 *S, uint32_t n, uint32_t ifftFlagR, uint32_t bitReverseFlag) {
+  const int i = size_index(n / 2);
+  if (n < 32 || n > 8192 || i < 0 || (n & (n - 1))) return ARM_MATH_ARGUMENT_ERROR;
+  oracle_arm_cfft_init_q31(&g_rfft_cfft_q31[i], (uint16_t)(n / 2));
+  S->fftLenReal = n; S->ifftFlagR = (uint8_t)ifftFlagR; S->bitReverseFlagR = (uint8_t)bitReverseFlag;
+  S->twidCoefRModifier = 8192u / n; S->pTwiddleAReal = realCoefAQ31; S->pTwiddleBReal = realCoefBQ31;
+  S->pCfft = &g_rfft_cfft_q31[i];
+  return ARM_MATH_SUCCESS;
+}
+arm_status oracle_arm_rfft_init_q15(arm_rfft_instance_q15 *S, uint32_t n, uint32_t ifftFlagR, uint32_t bitReverseFlag) {
+  const int i = size_index(n / 2);
+  if (n < 32 || n > 8192 || i < 0 || (n & (n - 1))) return ARM_MATH_ARGUMENT_ERROR;
+  oracle_arm_cfft_init_q15(&g_rfft_cfft_q15[i], (uint16_t)(n / 2));
+  S->fftLenReal = n; S->ifftFlagR = (uint8_t)ifftFlagR; S->bitReverseFlagR = (uint8_t)bitReverseFlag;
+  S->twidCoefRModifier = 8192u / n; S->pTwiddleAReal = realCoefAQ15; S->pTwiddleBReal = realCoefBQ15;
+  S->pCfft = &g_rfft_cfft_q15[i];
+  return ARM_MATH_SUCCESS;
+}

@@ -11,6 +11,7 @@
  *             arm_cfft_radix4_q15.c:572-970, :1434-1813 (scalar branches)
  *   bit reversal  arm_bitreversal2.c:84-148 (sequential swaps of complex pairs)
  *   RFFT fast f32 arm_rfft_fast_f32.c:316-462, :675-699
+ *   RFFT q31/q15  arm_rfft_q31.c:148-183, :256-476; arm_rfft_q15.c (scalar branches)
  * Pinned by tests/test_oracle.py against oracle/_ref (the reference compiled from its
  * own sources) bit for bit, and against the reference's Testing/Patterns fixtures.
  * Build: make -C oracle  (gcc, -O2, -ffp-contract=off).
@@ -393,4 +394,88 @@ void oracle_arm_rfft_fast_f32(const arm_rfft_fast_instance_f32 *S, float *p, flo
       Y[i].im = 0.5f * (A.im - B.im + t[2 * i + 1] * d - t[2 * i] * s);
     }
   }
+}
+
+/* ------------------------------------------------------------------ RFFT q31 / q15
+ * arm_rfft_q31.c:148-183 (dispatch), arm_split_rfft_q31 :256-341, arm_split_rifft_q31
+ * :397-476 (scalar branches); arm_rfft_q15.c (dispatch), arm_split_rfft_q15 / _rifft_q15
+ * (!ARM_MATH_DSP branches); arm_shift_q31.c / arm_shift_q15.c (left shift by 1 with
+ * saturation).  L = N/2 complex bins of the inner CFFT; table stride c = 2*modifier*k.
+ * Forward: pSrc is transformed in place, pDst receives the full 2N-word spectrum (bins
+ * L+1 .. N-1 mirrored as conjugates).  Inverse: pSrc words 0 .. N+1 are read. */
+static int32_t rnd_mul(int32_t x, int32_t y) { return (int32_t)(((int64_t)x * y + 0x80000000LL) >> 32); }
+static int32_t rnd_acc(int32_t a, int32_t x, int32_t y) {
+  return (int32_t)((int64_t)(((uint64_t)(int64_t)a << 32) + (uint64_t)((int64_t)x * y) + 0x80000000ULL) >> 32);
+}
+static int32_t rnd_sub(int32_t a, int32_t x, int32_t y) {
+  return (int32_t)((int64_t)(((uint64_t)(int64_t)a << 32) - (uint64_t)((int64_t)x * y) + 0x80000000ULL) >> 32);
+}
+static int32_t sat_shl1_q31(int32_t v) {
+  const int32_t o = (int32_t)((uint32_t)v << 1);
+  return (o >> 1) != v ? (int32_t)(0x7FFFFFFF ^ (v >> 31)) : o;
+}
+
+void oracle_arm_rfft_q31(const arm_rfft_instance_q31 *S, int32_t *pSrc, int32_t *pDst) {
+  const uint32_t n = S->fftLenReal, L = n / 2, mod = S->twidCoefRModifier;
+  const int32_t *A = S->pTwiddleAReal, *B = S->pTwiddleBReal;
+  if (S->ifftFlagR == 1) {
+    for (uint32_t k = 0; k < L; ++k) {
+      const uint32_t c = 2 * mod * k;
+      const int32_t a1 = A[c], a2 = A[c + 1], b1 = B[c];
+      const int32_t xr = pSrc[2 * k], xi = pSrc[2 * k + 1], yr = pSrc[2 * (L - k)], yi = pSrc[2 * (L - k) + 1];
+      int32_t re = rnd_mul(xr, a1), im = rnd_mul(xr, (int32_t)(0u - (uint32_t)a2));
+      re = rnd_acc(re, xi, a2); im = rnd_acc(im, xi, a1);
+      re = rnd_acc(re, yi, a2); im = rnd_sub(im, yi, b1);
+      re = rnd_acc(re, yr, b1); im = rnd_acc(im, yr, a2);
+      pDst[2 * k] = re; pDst[2 * k + 1] = im;
+    }
+    oracle_arm_cfft_q31(S->pCfft, pDst, 1, S->bitReverseFlagR);
+    for (uint32_t i = 0; i < n; ++i) pDst[i] = sat_shl1_q31(pDst[i]);
+  } else {
+    oracle_arm_cfft_q31(S->pCfft, pSrc, S->ifftFlagR, S->bitReverseFlagR);
+    for (uint32_t k = 1; k < L; ++k) {
+      const uint32_t c = 2 * mod * k;
+      const int32_t a1 = A[c], a2 = A[c + 1], b1 = B[c];
+      const int32_t xr = pSrc[2 * k], xi = pSrc[2 * k + 1], yr = pSrc[2 * (L - k)], yi = pSrc[2 * (L - k) + 1];
+      int32_t re = rnd_mul(xr, a1), im = rnd_mul(xr, a2);
+      re = rnd_sub(re, xi, a2); im = rnd_acc(im, xi, a1);
+      re = rnd_sub(re, yi, a2); im = rnd_sub(im, yi, b1);
+      re = rnd_acc(re, yr, b1); im = rnd_sub(im, yr, a2);
+      pDst[2 * k] = re; pDst[2 * k + 1] = im;
+      pDst[2 * n - 2 * k] = re; pDst[2 * n - 2 * k + 1] = (int32_t)(0u - (uint32_t)im);
+    }
+    pDst[n] = wsub(pSrc[0], pSrc[1]) >> 1; pDst[n + 1] = 0;
+    pDst[0] = wadd(pSrc[0], pSrc[1]) >> 1; pDst[1] = 0;
+  }
+}
+
+void oracle_arm_rfft_q15(const arm_rfft_instance_q15 *S, int16_t *pSrc, int16_t *pDst) {
+  const uint32_t n = S->fftLenReal, L = n / 2, mod = S->twidCoefRModifier;
+  const int16_t *A = S->pTwiddleAReal, *B = S->pTwiddleBReal;
+  /* q15 x q15 products in int, sums wrap mod 2^32 (done in uint32_t), >> 16 arithmetic */
+#define P(a, b) ((uint32_t)((int32_t)(a) * (int32_t)(b)))
+  if (S->ifftFlagR == 1) {
+    for (uint32_t k = 0; k < L; ++k) {
+      const uint32_t c = 2 * mod * k;
+      const int16_t xr = pSrc[2 * k], xi = pSrc[2 * k + 1], yr = pSrc[2 * (L - k)], yi = pSrc[2 * (L - k) + 1];
+      const int32_t re = (int32_t)(P(yr, B[c]) - P(yi, B[c + 1]) + P(xr, A[c]) + P(xi, A[c + 1])) >> 16;
+      const int32_t im = (int32_t)(P(xi, A[c]) - P(xr, A[c + 1]) - P(yr, B[c + 1]) - P(yi, B[c]));
+      pDst[2 * k] = (int16_t)re; pDst[2 * k + 1] = (int16_t)(im >> 16);
+    }
+    oracle_arm_cfft_q15(S->pCfft, pDst, 1, S->bitReverseFlagR);
+    for (uint32_t i = 0; i < n; ++i) pDst[i] = (int16_t)sat16((int32_t)pDst[i] << 1);
+  } else {
+    oracle_arm_cfft_q15(S->pCfft, pSrc, S->ifftFlagR, S->bitReverseFlagR);
+    for (uint32_t k = 1; k < L; ++k) {
+      const uint32_t c = 2 * mod * k;
+      const int16_t xr = pSrc[2 * k], xi = pSrc[2 * k + 1], yr = pSrc[2 * (L - k)], yi = pSrc[2 * (L - k) + 1];
+      const int32_t re = (int32_t)(P(xr, A[c]) - P(xi, A[c + 1]) + P(yr, B[c]) + P(yi, B[c + 1])) >> 16;
+      const int32_t im = (int32_t)(P(yr, B[c + 1]) - P(yi, B[c]) + P(xi, A[c]) + P(xr, A[c + 1])) >> 16;
+      pDst[2 * k] = (int16_t)re; pDst[2 * k + 1] = (int16_t)im;
+      pDst[2 * n - 2 * k] = (int16_t)re; pDst[2 * n - 2 * k + 1] = (int16_t)(-im);
+    }
+    pDst[n] = (int16_t)((pSrc[0] - pSrc[1]) >> 1); pDst[n + 1] = 0;
+    pDst[0] = (int16_t)((pSrc[0] + pSrc[1]) >> 1); pDst[1] = 0;
+  }
+#undef P
 }

@@ -61,6 +61,19 @@ class Host:
         self.fn("arm_rfft_fast_f32")(C.byref(S), p.ctypes.data, out.ctypes.data, ifft)
         return out, p
 
+    def rfft_fixed(self, kind, n, x, ifft, bitrev=1):
+        """arm_rfft_q31 / _q15 on one signal: forward x = N words -> (2N-word spectrum, the
+        overwritten input); inverse x = spectrum (>= N+2 words) -> (N words, x)."""
+        inst = _abi.arm_rfft_instance_q31 if kind == "q31" else _abi.arm_rfft_instance_q15
+        dt = DTYPE[kind]
+        S = inst()
+        st = self.fn(f"arm_rfft_init_{kind}")(C.byref(S), n, ifft, bitrev)
+        assert st == 0, (kind, n, st)
+        src = np.ascontiguousarray(x, dtype=dt).copy()
+        out = np.zeros(2 * n if ifft != 1 else n, dtype=dt)
+        self.fn(f"arm_rfft_{kind}")(C.byref(S), src.ctypes.data, out.ctypes.data)
+        return out, src
+
     def mfcc(self, cfg, frames):
         """cfg: dict with fftLen, dct [nbDct x nbMel], pos, len, coefs, window; frames:
         [batch, fftLen] -> [batch, nbDct] (one arm_mfcc_f32 call per frame, zeroed pTmp)."""

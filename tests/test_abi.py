@@ -65,7 +65,8 @@ def test_ctypes_mirror_matches_headers(dsp):
     ref = json.load(open(os.path.join(ROOT, "tests", "golden", "abi_layout.json")))
     for name in ("arm_cfft_instance_f32", "arm_rfft_fast_instance_f32", "arm_fir_instance_f32",
                  "arm_fir_instance_q15", "arm_matrix_instance_f32", "arm_mfcc_instance_f32",
-                 "arm_matrix_instance_q15", "arm_matrix_instance_q31", "arm_fir_instance_q31"):
+                 "arm_matrix_instance_q15", "arm_matrix_instance_q31", "arm_fir_instance_q31",
+                 "arm_rfft_instance_q31", "arm_rfft_instance_q15"):
         st = getattr(_abi, name)
         assert C.sizeof(st) == ref[name]["size"], name
         for fname, _ in st._fields_:

@@ -1,0 +1,144 @@
+"""Real FFT q31 / q15 (arm_rfft_q31.c:148-183, arm_rfft_q15.c; SURVEY §8b "callers to keep
+working"): oracle pinning on CPU, bit-exact GPU parity.
+
+CPU (no GPU needed):
+* the oracle restatement equals the reference build (oracle/_ref) bit for bit on every
+  length 32 ... 8192, direction (ifftFlagR 0, 1 and 2 = "not 1", a forward), bit-reversal
+  flag and input distribution (full-range words exercise wrap and saturation);
+* the oracle meets the reference suites' own thresholds on their patterns
+  (TransformRQ31.cpp:7-10: |err| <= 33 forward, 52000 inverse, 209000 inverse N=4096;
+  TransformRQ15.cpp:1-4: SNR >= 40 dB / |err| <= 14 forward, SNR >= 25 dB / |err| <= 1250
+  inverse -- met by the reference scalar path itself only up to N = 128, see below),
+  replaying the suites' call sequence (inverse output << log2 N);
+* the oracle reproduces the committed reference vectors (tests/golden/rfft_fixed.npz).
+GPU (-m gpu): the batched and drop-in entry points equal the reference build bit for bit
+(forward spectrum AND the overwritten input), including ragged batch sizes.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import metrics
+import refs
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+SIZES = [32, 64, 128, 256, 512, 1024, 2048, 4096, 8192]
+DT = {"q31": np.int32, "q15": np.int16}
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return np.load(os.path.join(GOLD, "rfft_fixed.npz"))
+
+
+@pytest.mark.parametrize("kind", ["q31", "q15"])
+@pytest.mark.parametrize("n", SIZES)
+def test_rfft_fixed_oracle_equals_reference(oracle, ref, kind, n):
+    for d_i, dist in enumerate(("uniform", "sine", "extreme")):
+        for ifft in (0, 1, 2):
+            for bitrev in (0, 1):
+                x = refs.rand_input(kind, 2 * n if ifft == 1 else n, seed=n + 10 * d_i + ifft, dist=dist)
+                a, pa = oracle.rfft_fixed(kind, n, x, ifft, bitrev)
+                b, pb = ref.rfft_fixed(kind, n, x, ifft, bitrev)
+                assert a.tobytes() == b.tobytes(), (dist, ifft, bitrev)
+                assert pa.tobytes() == pb.tobytes(), (dist, ifft, bitrev)
+
+
+@pytest.mark.parametrize("kind", ["q31", "q15"])
+@pytest.mark.parametrize("dist", ["Noisy", "Step"])
+@pytest.mark.parametrize("n", [32, 64, 128, 256, 512, 1024, 2048, 4096])
+def test_rfft_fixed_oracle_reference_patterns(oracle, gold, kind, dist, n):
+    key = f"pat_{kind}_{dist}_{n}"
+    x, fft_ref, ifft_in = gold[key + "_in"], gold[key + "_fft"], gold[key + "_ifftin"]
+    out, _ = oracle.rfft_fixed(kind, n, x, 0)
+    got = out[:fft_ref.size]
+    inv, _ = oracle.rfft_fixed(kind, n, ifft_in, 1)
+    scaling = int(np.log2(n))
+    # the suite shifts the inverse output back by log2 N in the output word type
+    inv = (inv.astype(np.int64) << scaling).astype(DT[kind])
+    if kind == "q31":
+        assert metrics.near_eq(got, fft_ref, 33)                                   # ABS_RFFT_ERROR_Q31
+        assert metrics.near_eq(inv, x, 209000 if scaling == 12 else 52000)        # ABS_RIFFT_*_ERROR_Q31
+    else:
+        assert metrics.snr_db(fft_ref, got) >= 40 and metrics.near_eq(got, fft_ref, 14)
+        # q15 inverse: the reference scalar path itself meets RIFFT_SNR_THRESHOLD 25 dB /
+        # ABS_IFFT_ERROR_Q15 1250 only up to N = 128 (oracle/_ref, measured: 22 dB at 256,
+        # 10 dB at 1024, < 0 dB at 4096 -- the inverse output keeps log2 N fewer bits and
+        # the suite shifts it back); beyond that the bar is bit-equality with the
+        # reference (test_rfft_fixed_oracle_equals_reference).
+        if n <= 128:
+            assert metrics.snr_db(x, inv) >= 25 and metrics.near_eq(inv, x, 1250)
+
+
+@pytest.mark.parametrize("kind", ["q31", "q15"])
+def test_rfft_fixed_oracle_reference_vectors(oracle, gold, kind):
+    keys = sorted({k[: -len("_in")] for k in gold.files if k.startswith(f"ref_{kind}_") and k.endswith("_in")})
+    assert len(keys) >= 18
+    for key in keys:
+        n, flags = int(key.split("_")[2]), key.split("_")[3]
+        y, p = oracle.rfft_fixed(kind, n, gold[key + "_in"], int(flags[0]), int(flags[1]))
+        assert y.tobytes() == gold[key + "_out"].tobytes(), key
+        assert p.tobytes() == gold[key + "_src"].tobytes(), key
+
+
+# ------------------------------------------------------------------ GPU parity
+def _instance(dsp, kind, n, ifft, bitrev):
+    S = dsp.arm_rfft_instance_q31() if kind == "q31" else dsp.arm_rfft_instance_q15()
+    assert getattr(dsp, f"arm_rfft_init_{kind}")(S, n, ifft, bitrev) == 0
+    return S
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["q31", "q15"])
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("ifft", [0, 1, 2])
+def test_rfft_fixed_batch_bitexact(dsp, torch_gpu, ref, kind, n, ifft):
+    torch = torch_gpu
+    batch = 13
+    for bitrev, dist in ((1, "sine"), (0, "uniform")):
+        words = 2 * n if ifft == 1 else n
+        x = np.stack([refs.rand_input(kind, words, seed=n + r + 50 * ifft, dist=dist) for r in range(batch)])
+        outs = [ref.rfft_fixed(kind, n, x[r], ifft, bitrev) for r in range(batch)]
+        S = _instance(dsp, kind, n, ifft, bitrev)
+        src = torch.from_numpy(x.copy()).cuda()
+        dst = torch.zeros((batch, n if ifft == 1 else 2 * n), dtype=src.dtype, device="cuda")
+        dsp.rfft_fixed_batch(S, src, dst)
+        torch.cuda.synchronize()
+        assert dst.cpu().numpy().tobytes() == np.stack([o[0] for o in outs]).tobytes(), bitrev
+        if ifft != 1:   # the forward transform overwrites its input, like the reference
+            assert src.cpu().numpy().tobytes() == np.stack([o[1] for o in outs]).tobytes(), bitrev
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["q31", "q15"])
+def test_rfft_fixed_extremes_and_large_batch(dsp, torch_gpu, ref, kind):
+    """All-extreme words (wrap in the split sums, saturation in the inverse shift) and a
+    batch above one launch's persistent grid at N = 8192 (the inner CFFT is the 4096
+    specialist)."""
+    torch = torch_gpu
+    n, batch = 8192, 1100
+    for ifft in (0, 1):
+        words = 2 * n if ifft else n
+        x = np.stack([refs.rand_input(kind, words, seed=r, dist="extreme" if r % 2 else "uniform")
+                      for r in range(batch)])
+        S = _instance(dsp, kind, n, ifft, 1)
+        src = torch.from_numpy(x.copy()).cuda()
+        dst = torch.zeros((batch, n if ifft else 2 * n), dtype=src.dtype, device="cuda")
+        dsp.rfft_fixed_batch(S, src, dst)
+        torch.cuda.synchronize()
+        got = dst.cpu().numpy()
+        for r in list(range(4)) + [batch - 2, batch - 1]:
+            assert got[r].tobytes() == ref.rfft_fixed(kind, n, x[r], ifft, 1)[0].tobytes(), (ifft, r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["q31", "q15"])
+@pytest.mark.parametrize("n", [32, 1024, 8192])
+def test_rfft_fixed_dropin(dsp, torch_gpu, ref, kind, n):
+    """arm_rfft_q31 / _q15 with host buffers; the inverse reads only N+2 spectrum words."""
+    for ifft in (0, 1):
+        x = refs.rand_input(kind, n + 2 if ifft else n, seed=n + ifft, dist="sine")
+        S = _instance(dsp, kind, n, ifft, 1)
+        got = getattr(dsp, f"arm_rfft_{kind}")(S, x)
+        assert got.tobytes() == ref.rfft_fixed(kind, n, x, ifft, 1)[0].tobytes(), ifft

@@ -35,6 +35,12 @@ int main(void) {
     F(arm_mfcc_instance_f32, windowCoefs) F(arm_mfcc_instance_f32, filterPos) F(arm_mfcc_instance_f32, filterLengths)
     F(arm_mfcc_instance_f32, fftLen) F(arm_mfcc_instance_f32, nbMelFilters) F(arm_mfcc_instance_f32, nbDctOutputs)
     F(arm_mfcc_instance_f32, rfft) E()
+  S(arm_rfft_instance_q31) F(arm_rfft_instance_q31, fftLenReal) F(arm_rfft_instance_q31, ifftFlagR)
+    F(arm_rfft_instance_q31, bitReverseFlagR) F(arm_rfft_instance_q31, twidCoefRModifier)
+    F(arm_rfft_instance_q31, pTwiddleAReal) F(arm_rfft_instance_q31, pTwiddleBReal) F(arm_rfft_instance_q31, pCfft) E()
+  S(arm_rfft_instance_q15) F(arm_rfft_instance_q15, fftLenReal) F(arm_rfft_instance_q15, ifftFlagR)
+    F(arm_rfft_instance_q15, bitReverseFlagR) F(arm_rfft_instance_q15, twidCoefRModifier)
+    F(arm_rfft_instance_q15, pTwiddleAReal) F(arm_rfft_instance_q15, pTwiddleBReal) F(arm_rfft_instance_q15, pCfft) E()
   printf("  \"arm_status\": {\"size\": %zu, \"ARM_MATH_SIZE_MISMATCH\": %d}\n}\n", sizeof(arm_status),
          (int)ARM_MATH_SIZE_MISMATCH);
   return 0;
