@@ -54,6 +54,8 @@ arm_fir_instance_f32 = _make("arm_fir_instance_f32", _abi.arm_fir_instance_f32)
 arm_fir_instance_q31 = _make("arm_fir_instance_q31", _abi.arm_fir_instance_q31)
 arm_fir_instance_q15 = _make("arm_fir_instance_q15", _abi.arm_fir_instance_q15)
 arm_mfcc_instance_f32 = _make("arm_mfcc_instance_f32", _abi.arm_mfcc_instance_f32)
+arm_rfft_instance_q31 = _make("arm_rfft_instance_q31", _abi.arm_rfft_instance_q31)
+arm_rfft_instance_q15 = _make("arm_rfft_instance_q15", _abi.arm_rfft_instance_q15)
 
 _DT = {"f32": _np.float32, "q31": _np.int32, "q15": _np.int16}
 
@@ -112,16 +114,53 @@ def arm_rfft_fast_f32(inst, p, ifftFlag, tmp=None):
     return out
 
 
+# ------------------------------------------------------------------ real FFT, q31 / q15
+# cmsisdsp_transform.c:2275-2313 (init: "Oi|ii"), :2180-2273 / :2317-2405 (rfft: "OO|i$O",
+# the ifft / tmp arguments exist for the Neon API only): output fftLenReal words for an
+# inverse instance, 2*fftLenReal otherwise; the input is converted (copied) first.
+def _rfft_q_init(kind):
+    def init(inst, fftLenReal, ifftFlagR=0, bitReverseFlag=0):
+        return getattr(_lib, f"arm_rfft_init_{kind}")(_C.byref(inst._s), int(fftLenReal), int(ifftFlagR),
+                                                      int(bitReverseFlag))
+    init.__name__ = f"arm_rfft_init_{kind}"
+    return init
+
+
+def _rfft_q(kind):
+    def rfft(inst, pSrc, ifft=0, tmp=None):
+        s = inst._s
+        n = int(s.fftLenReal)
+        src = _np.zeros(2 * n, dtype=_DT[kind])           # room for the widest read (inverse: N+2)
+        x = _arr(pSrc, _DT[kind]).ravel()
+        src[:min(x.size, 2 * n)] = x[:2 * n]
+        out = _np.zeros(2 * n, dtype=_DT[kind])
+        getattr(_lib, f"arm_rfft_{kind}")(_C.byref(s), src.ctypes.data, out.ctypes.data)
+        _check(f"arm_rfft_{kind}")
+        return out[:n] if s.ifftFlagR else out
+    rfft.__name__ = f"arm_rfft_{kind}"
+    return rfft
+
+
+arm_rfft_init_q31 = _rfft_q_init("q31")
+arm_rfft_init_q15 = _rfft_q_init("q15")
+arm_rfft_q31 = _rfft_q("q31")
+arm_rfft_q15 = _rfft_q("q15")
+
+
 def arm_rfft_tmp_buffer_size(dt, nbSamples, buf_id, arch=None):
     return 0
 
 
 def arm_rfft_output_buffer_size(dt, nbSamples, arch=None):
-    return int(nbSamples)
+    """arm_transform_buffer_sizes.c:204-230 (generic arch): float N, fixed point 2N."""
+    from . import datatype as _dt
+    return 2 * int(nbSamples) if dt in (_dt.Q31, _dt.Q15) else int(nbSamples)
 
 
 def arm_rifft_input_buffer_size(dt, nbSamples, arch=None):
-    return int(nbSamples)
+    """arm_transform_buffer_sizes.c:245-263: float N, fixed point N + 2."""
+    from . import datatype as _dt
+    return int(nbSamples) + 2 if dt in (_dt.Q31, _dt.Q15) else int(nbSamples)
 
 
 # ------------------------------------------------------------------ FIR

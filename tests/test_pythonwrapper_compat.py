@@ -38,7 +38,7 @@ def test_module_surface_without_gpu(cdsp):
     assert cdsp.arm_rfft_output_buffer_size(dt.F32, 128) == 128 and not cdsp.has_neon()
     for name in ("arm_cfft_q31", "arm_cfft_q15", "arm_fir_f32", "arm_fir_q15", "arm_fir_q31", "arm_fir_fast_q15",
                  "arm_fir_fast_q31", "arm_mat_mult_f32", "arm_mat_mult_q15", "arm_mat_mult_q31", "arm_mfcc_f32",
-                 "arm_conv_f32", "arm_conv_q15", "arm_conv_q31"):
+                 "arm_conv_f32", "arm_conv_q15", "arm_conv_q31", "arm_rfft_q31", "arm_rfft_q15"):
         assert callable(getattr(cdsp, name))
 
 
@@ -142,3 +142,49 @@ def test_conv(cdsp, torch_gpu, ref):
         qa, qb = conv(a * 0.5), conv(b * 0.5)
         got = getattr(cdsp, f"arm_conv_{kind}")(qa, len(qa), qb, len(qb))
         assert got.tobytes() == ref.conv(kind, qa, qb).tobytes(), kind
+
+
+def _q31_to_f(x):
+    return np.asarray(x, np.float64) / Q31
+
+
+def _q15_to_f(x):
+    return np.asarray(x, np.float64) / Q15
+
+
+@pytest.mark.gpu
+def test_rfft_rifft_fixed(cdsp, torch_gpu, ref):
+    """testrfft_all.py test_rfft_q31 / test_rifft_q31 / test_rfft_q15 / test_rifft_q15
+    (non-Neon branch: init(S, nb, ifft, 1), output 2*nb with the conjugate half, inverse
+    input nb + 2) with their tolerances, plus bit-exact vs the reference build."""
+    import cmsisdsp.datatype as dt
+    import scipy.fft
+    nb = 32
+    t = np.arange(nb)
+    signal = np.cos(2 * np.pi * t / nb) * np.cos(0.2 * 2 * np.pi * t / nb)
+    sref = scipy.fft.rfft(signal)
+    invref = scipy.fft.irfft(sref)
+    fixed = np.zeros(2 * len(sref))
+    fixed[0::2], fixed[1::2] = np.real(sref), np.imag(sref)
+    assert cdsp.arm_rfft_output_buffer_size(dt.Q15, nb) == 2 * nb
+    assert cdsp.arm_rifft_input_buffer_size(dt.Q31, nb) == nb + 2
+    for kind, conv, back, atol_f, atol_i in (("q31", toQ31, _q31_to_f, 1e-6, 1e-6), ("q15", toQ15, _q15_to_f, 1e-2, 1e-3)):
+        inst = getattr(cdsp, f"arm_rfft_instance_{kind}")
+        init, rfft = getattr(cdsp, f"arm_rfft_init_{kind}"), getattr(cdsp, f"arm_rfft_{kind}")
+        S = inst()
+        assert init(S, nb, 0, 1) == 0
+        sq = conv(signal)
+        res = rfft(S, sq)
+        assert len(res) == 2 * nb
+        z = res[0::2] + 1j * res[1::2]                       # compareWithConjugatePart
+        assert np.array_equal(z[1:nb // 2], z[nb:nb // 2:-1].conj())
+        assert res.tobytes() == ref.rfft_fixed(kind, nb, sq, 0, 1)[0].tobytes()
+        np.testing.assert_allclose(back(res[:nb + 2]) * nb, fixed, rtol=1e-6, atol=atol_f)
+        Si = inst()
+        assert init(Si, nb, 1, 1) == 0
+        rq = conv(fixed / nb)
+        assert len(rq) == nb + 2
+        inv = rfft(Si, rq)
+        assert len(inv) == nb
+        assert inv.tobytes() == ref.rfft_fixed(kind, nb, rq, 1, 1)[0].tobytes()
+        np.testing.assert_allclose(invref / nb, back(inv), atol=atol_i)
