@@ -230,6 +230,29 @@ arm_conv_q15 = _conv("q15", _np.int16)
 arm_conv_q31 = _conv("q31", _np.int32)
 
 
+# cmsisdsp_filtering.c cmsis_arm_conv_fast_* ("OiOi", srcALen + srcBLen - 1 words),
+# cmsis_arm_correlate_* ("OiOi", 2 * max(srcALen, srcBLen) - 1 words, :6244-6276) and
+# cmsis_arm_conv_partial_* ("OiOiii" -> (status, srcALen + srcBLen - 1 words), :4313-4350).
+# The binding's output buffer is uninitialised where the C function does not write; here
+# those words are zero.
+def _conv_family(fn):
+    dt = _DT[fn[-3:]]
+
+    def run(pSrcA, srcALen, pSrcB, srcBLen, *partial):
+        a = _arr(pSrcA, dt)[:int(srcALen)]
+        b = _arr(pSrcB, dt)[:int(srcBLen)]
+        y, st = _amd.arm_conv_family(fn, a, b, *[int(v) for v in partial])
+        return (st, y) if partial else y
+    run.__name__ = f"arm_{fn}"
+    return run
+
+
+for _fn in ("conv_fast_q15", "conv_fast_q31", "correlate_f32", "correlate_q15", "correlate_q31", "correlate_fast_q15",
+            "correlate_fast_q31", "conv_partial_f32", "conv_partial_q15", "conv_partial_q31"):
+    globals()[f"arm_{_fn}"] = _conv_family(_fn)
+del _fn
+
+
 # ------------------------------------------------------------------ MFCC
 def arm_mfcc_init_f32(inst, fftLen, nbMelFilters, nbDctOutputs, dctCoefs, filterPos, filterLengths,
                       filterCoefs, windowCoefs):

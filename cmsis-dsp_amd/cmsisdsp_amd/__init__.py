@@ -362,6 +362,40 @@ def conv_batch(a, b, out, stream=None):
         raise RuntimeError(f"{fn.__name__} -> {st}: {last_error()[1]}")
 
 
+def arm_conv_family(fn, a, b, first=0, num=0, fill=0):
+    """Drop-in (numpy) call of arm_<fn>, fn in _abi.CONV_FULL + _abi.CONV_PARTIAL (e.g.
+    "correlate_q15", "conv_partial_f32", "conv_fast_q31"): returns (pDst, status); pDst is
+    pre-filled with `fill`, since partial / correlate leave the words they do not compute."""
+    dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32}[fn[-3:]]
+    a = np.ascontiguousarray(a, dtype=dt)
+    b = np.ascontiguousarray(b, dtype=dt)
+    n = 2 * max(len(a), len(b)) - 1 if fn.startswith("correlate") else len(a) + len(b) - 1
+    y = np.full(n, fill, dtype=dt)
+    f = getattr(lib, f"arm_{fn}")
+    if fn.startswith("conv_partial"):
+        st = f(a.ctypes.data, len(a), b.ctypes.data, len(b), y.ctypes.data, first, num)
+    else:
+        f(a.ctypes.data, len(a), b.ctypes.data, len(b), y.ctypes.data)
+        st = ARM_MATH_SUCCESS
+    _check_void(f"arm_{fn}")
+    return y, st
+
+
+def conv_family_batch(fn, a, b, out, first=0, num=0, stream=None):
+    """arm_<fn>_batch on torch device tensors: a [batch, La], b [batch, Lb] or [Lb] (shared),
+    out [batch, La+Lb-1] (conv), [batch, 2*max-1] (correlate) or [batch, num] (partial)."""
+    batch, la = a.shape
+    lb = b.shape[-1]
+    sb = 0 if b.dim() == 1 else b.stride(0)
+    fn_ = getattr(lib, f"arm_{fn}_batch")
+    args = [C.c_void_p(a.data_ptr()), la, a.stride(0), C.c_void_p(b.data_ptr()), lb, sb, C.c_void_p(out.data_ptr())]
+    if fn.startswith("conv_partial"):
+        args += [first, num]
+    st = fn_(*args, batch, _stream_ptr(stream))
+    if st != ARM_MATH_SUCCESS:
+        raise RuntimeError(f"arm_{fn}_batch -> {st}: {last_error()[1]}")
+
+
 def arm_mat_mult_fixed(kind, a, b):
     """(status, C) = A @ B through arm_mat_mult_q15 / arm_mat_mult_q31 (row-major)."""
     dt = np.int16 if kind == "q15" else np.int32

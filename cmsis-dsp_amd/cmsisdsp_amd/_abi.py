@@ -86,6 +86,10 @@ class arm_matrix_instance_q31(C.Structure):
 P = C.POINTER
 SIZES = (16, 32, 64, 128, 256, 512, 1024, 2048, 4096)
 RFFT_SIZES = (32, 64, 128, 256, 512, 1024, 2048, 4096)
+# convolution / correlation family (drop-in names without the arm_ prefix)
+CONV_FULL = ("conv_f32", "conv_q15", "conv_q31", "conv_fast_q15", "conv_fast_q31", "correlate_f32", "correlate_q15",
+             "correlate_q31", "correlate_fast_q15", "correlate_fast_q31")
+CONV_PARTIAL = ("conv_partial_f32", "conv_partial_q15", "conv_partial_q31")
 
 # name -> (restype, argtypes): the drop-in surface of include/arm_math.h
 DROPIN = {
@@ -119,6 +123,10 @@ DROPIN = {
     "arm_conv_f32": (None, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
     "arm_conv_q15": (None, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
     "arm_conv_q31": (None, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
+    **{f"arm_{f}": (None, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p])
+       for f in CONV_FULL if f not in ("conv_f32", "conv_q15", "conv_q31")},
+    **{f"arm_{f}": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32])
+       for f in CONV_PARTIAL},
     "arm_mfcc_init_f32": (C.c_int, [P(arm_mfcc_instance_f32), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "arm_mfcc_f32": (None, [P(arm_mfcc_instance_f32), C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -173,12 +181,10 @@ BATCHED = {
                                          P(arm_matrix_instance_q15), C.c_uint32, C.c_void_p]),
     "arm_mat_mult_q31_batch": (C.c_int, [P(arm_matrix_instance_q31), P(arm_matrix_instance_q31),
                                          P(arm_matrix_instance_q31), C.c_uint32, C.c_void_p]),
-    "arm_conv_f32_batch": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
-                                     C.c_void_p, C.c_uint32, C.c_void_p]),
-    "arm_conv_q15_batch": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
-                                     C.c_void_p, C.c_uint32, C.c_void_p]),
-    "arm_conv_q31_batch": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
-                                     C.c_void_p, C.c_uint32, C.c_void_p]),
+    **{f"arm_{f}_batch": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
+                                    C.c_void_p, C.c_uint32, C.c_void_p]) for f in CONV_FULL},
+    **{f"arm_{f}_batch": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
+                                    C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]) for f in CONV_PARTIAL},
     "arm_mfcc_f32_batch": (C.c_int, [P(arm_mfcc_instance_f32), C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                      C.c_void_p]),
     "arm_mi355x_last_error": (C.c_int, []),

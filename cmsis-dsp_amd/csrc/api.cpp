@@ -340,33 +340,91 @@ arm_status fir_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uint32
   return ARM_MATH_SUCCESS;
 }
 
-// drop-in convolution: host or device operands, synchronous
+// ---- convolution / correlation family ------------------------------------------------
+// How each reference function maps onto one ConvJob (conv.hip):
+//   conv (exact):      x = pSrcA, h = pSrcB, all srcALen + srcBLen - 1 outputs forward;
+//   conv (fast q15/q31): x = the longer input (arm_conv_fast_q15.c:83-103);
+//   conv_partial:      outputs [firstIndex, firstIndex + numPoints) at pDst[n];
+//   correlate (all):   x = the longer input, h = the shorter reversed; forward at
+//                      srcALen - srcBLen, or backward from srcALen + srcBLen - 2 when
+//                      srcALen < srcBLen (arm_correlate_f32.c:1040-1070).
+// Returns the job and the written output range [wlo, whi) of one item.
+enum ConvVariant { kVarConv = 0, kVarPartial = 1, kVarCorr = 2 };
+ConvJob conv_plan(int op, int variant, const void* a, uint32_t alen, const void* b, uint32_t blen, uint32_t first,
+                  uint32_t num, uint64_t* wlo, uint64_t* whi) {
+  ConvJob j{};
+  j.op = op;
+  j.corr = variant == kVarCorr;
+  const bool swap = (variant == kVarCorr || op == kConvFastQ15 || op == kConvFastQ31) && alen < blen;
+  j.x = swap ? b : a; j.A = swap ? blen : alen;
+  j.h = swap ? a : b; j.B = swap ? alen : blen;
+  const uint32_t L = alen + blen - 1;
+  j.ydir = 1; j.yoff = 0; j.first = 0; j.num = L;
+  *wlo = 0; *whi = L;
+  if (variant == kVarPartial) {
+    j.first = first; j.num = num;
+    *wlo = first; *whi = (uint64_t)first + num;
+  } else if (variant == kVarCorr) {
+    if (alen >= blen) { j.yoff = alen - blen; *wlo = alen - blen; *whi = (uint64_t)j.yoff + L; }
+    else { j.yoff = L - 1; j.ydir = -1; }
+  }
+  return j;
+}
+
+// drop-in: host or device operands, synchronous
 template <typename T>
-void conv_sync(int kind, const T* a, uint32_t alen, const T* b, uint32_t blen, T* dst) {
+void conv_family_sync(int op, int variant, const T* a, uint32_t alen, const T* b, uint32_t blen, T* dst,
+                      uint32_t first, uint32_t num, const char* what) {
   if (!a || !b || !dst || alen == 0 || blen == 0) return;
-  const size_t ab = sizeof(T) * alen, bb = sizeof(T) * blen, yb = sizeof(T) * ((size_t)alen + blen - 1);
+  uint64_t wlo, whi;
+  ConvJob j = conv_plan(op, variant, a, alen, b, blen, first, num, &wlo, &whi);
+  if (j.num == 0) return;
+  const size_t ab = sizeof(T) * alen, bb = sizeof(T) * blen;
   hipStream_t st = sync_stream();
   const bool da = is_device_ptr(a), db = is_device_ptr(b), dd = is_device_ptr(dst);
   const T* A = da ? a : (const T*)scratch(ab, 0);
   const T* B = db ? b : (const T*)scratch(bb, 1);
-  T* Y = dd ? dst : (T*)scratch(yb, 2);
-  if (!A || !B || !Y) { set_error(hipErrorOutOfMemory, "arm_conv scratch"); return; }
+  T* Y = dd ? dst : (T*)scratch(sizeof(T) * whi, 2);
+  if (!A || !B || !Y) { set_error(hipErrorOutOfMemory, what); return; }
   hipError_t e = hipSuccess;
   if (!da) e = hipMemcpyAsync((void*)A, a, ab, hipMemcpyHostToDevice, st);
   if (e == hipSuccess && !db) e = hipMemcpyAsync((void*)B, b, bb, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = conv_run(kind, A, alen, 0, B, blen, 0, Y, 1, st);
-  if (e == hipSuccess && !dd) e = hipMemcpyAsync(dst, Y, yb, hipMemcpyDeviceToHost, st);
+  const bool swapped = j.x != (const void*)a;
+  j.x = swapped ? (const void*)B : (const void*)A;
+  j.h = swapped ? (const void*)A : (const void*)B;
+  j.y = Y; j.sx = j.sh = j.sy = 0; j.batch = 1;
+  if (e == hipSuccess) e = conv_family_run(j, st);
+  // only the words the reference writes are copied back (partial / correlate leave the rest)
+  if (e == hipSuccess && !dd) e = hipMemcpyAsync(dst + wlo, Y + wlo, sizeof(T) * (whi - wlo), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e != hipSuccess) set_error(e, "arm_conv");
+  if (e != hipSuccess) set_error(e, what);
 }
 
+// batched device API: item i reads a + i*sa, b + i*sb (0 = shared) and writes y + i*sy at
+// the drop-in positions, except conv_partial, which writes its numPoints outputs compactly.
 template <typename T>
-arm_status conv_batch(int kind, const T* a, uint32_t alen, uint32_t sa, const T* b, uint32_t blen, uint32_t sb, T* y,
-                      uint32_t batch, void* stream) {
+arm_status conv_family_batch(int op, int variant, const T* a, uint32_t alen, uint32_t sa, const T* b, uint32_t blen,
+                             uint32_t sb, T* y, uint32_t first, uint32_t num, uint32_t batch, void* stream,
+                             const char* what) {
   if (batch && (!a || !b || !y || alen == 0 || blen == 0)) return ARM_MATH_ARGUMENT_ERROR;
-  hipError_t e = conv_run(kind, a, alen, sa, b, blen, sb, y, batch, (hipStream_t)stream);
-  if (e != hipSuccess) { set_error(e, "arm_conv_batch"); return ARM_MATH_ARGUMENT_ERROR; }
+  if (batch == 0) return ARM_MATH_SUCCESS;
+  uint64_t wlo, whi;
+  ConvJob j = conv_plan(op, variant, a, alen, b, blen, first, num, &wlo, &whi);
+  const bool swapped = j.x != (const void*)a;
+  j.sx = swapped ? sb : sa;
+  j.sh = swapped ? sa : sb;
+  j.y = y; j.batch = batch;
+  if (variant == kVarPartial) { j.sy = num; j.yoff = -(int64_t)first; }
+  else if (variant == kVarCorr) j.sy = 2ull * (alen > blen ? alen : blen) - 1;
+  else j.sy = (uint64_t)alen + blen - 1;
+  hipError_t e = conv_family_run(j, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(e, what); return ARM_MATH_ARGUMENT_ERROR; }
   return ARM_MATH_SUCCESS;
+}
+
+bool partial_range_ok(uint32_t alen, uint32_t blen, uint32_t first, uint32_t num) {
+  // arm_conv_partial_f32.c:644: (firstIndex + numPoints) > (srcALen + (srcBLen - 1))
+  return (uint64_t)first + num <= (uint64_t)alen + blen - 1;
 }
 
 template <typename M>
@@ -627,26 +685,45 @@ arm_status arm_mat_mult_q31_batch(const arm_matrix_instance_q31* pSrcA, const ar
 }
 
 // ---- convolution ------------------------------------------------------------------
-void arm_conv_f32(const float32_t* pSrcA, uint32_t srcALen, const float32_t* pSrcB, uint32_t srcBLen, float32_t* pDst) {
-  conv_sync<float>(0, pSrcA, srcALen, pSrcB, srcBLen, pDst);
-}
-void arm_conv_q15(const q15_t* pSrcA, uint32_t srcALen, const q15_t* pSrcB, uint32_t srcBLen, q15_t* pDst) {
-  conv_sync<int16_t>(1, pSrcA, srcALen, pSrcB, srcBLen, pDst);
-}
-void arm_conv_q31(const q31_t* pSrcA, uint32_t srcALen, const q31_t* pSrcB, uint32_t srcBLen, q31_t* pDst) {
-  conv_sync<int32_t>(2, pSrcA, srcALen, pSrcB, srcBLen, pDst);
-}
-arm_status arm_conv_f32_batch(const float32_t* d_a, uint32_t srcALen, uint32_t strideA, const float32_t* d_b,
-                              uint32_t srcBLen, uint32_t strideB, float32_t* d_dst, uint32_t batch, void* stream) {
-  return conv_batch<float>(0, d_a, srcALen, strideA, d_b, srcBLen, strideB, d_dst, batch, stream);
-}
-arm_status arm_conv_q15_batch(const q15_t* d_a, uint32_t srcALen, uint32_t strideA, const q15_t* d_b,
-                              uint32_t srcBLen, uint32_t strideB, q15_t* d_dst, uint32_t batch, void* stream) {
-  return conv_batch<int16_t>(1, d_a, srcALen, strideA, d_b, srcBLen, strideB, d_dst, batch, stream);
-}
-arm_status arm_conv_q31_batch(const q31_t* d_a, uint32_t srcALen, uint32_t strideA, const q31_t* d_b,
-                              uint32_t srcBLen, uint32_t strideB, q31_t* d_dst, uint32_t batch, void* stream) {
-  return conv_batch<int32_t>(2, d_a, srcALen, strideA, d_b, srcBLen, strideB, d_dst, batch, stream);
-}
+#define MI355X_CONV_FULL(NAME, T, CT, OP, VAR)                                                                  \
+  void NAME(const T* pSrcA, uint32_t srcALen, const T* pSrcB, uint32_t srcBLen, T* pDst) {                      \
+    conv_family_sync<CT>(OP, VAR, (const CT*)pSrcA, srcALen, (const CT*)pSrcB, srcBLen, (CT*)pDst, 0, 0, #NAME); \
+  }                                                                                                             \
+  arm_status NAME##_batch(const T* d_a, uint32_t srcALen, uint32_t strideA, const T* d_b, uint32_t srcBLen,     \
+                          uint32_t strideB, T* d_dst, uint32_t batch, void* stream) {                           \
+    return conv_family_batch<CT>(OP, VAR, (const CT*)d_a, srcALen, strideA, (const CT*)d_b, srcBLen, strideB,   \
+                                 (CT*)d_dst, 0, 0, batch, stream, #NAME "_batch");                              \
+  }
+MI355X_CONV_FULL(arm_conv_f32, float32_t, float, kConvF32, kVarConv)
+MI355X_CONV_FULL(arm_conv_q15, q15_t, int16_t, kConvQ15, kVarConv)
+MI355X_CONV_FULL(arm_conv_q31, q31_t, int32_t, kConvQ31, kVarConv)
+MI355X_CONV_FULL(arm_conv_fast_q15, q15_t, int16_t, kConvFastQ15, kVarConv)
+MI355X_CONV_FULL(arm_conv_fast_q31, q31_t, int32_t, kConvFastQ31, kVarConv)
+MI355X_CONV_FULL(arm_correlate_f32, float32_t, float, kConvF32, kVarCorr)
+MI355X_CONV_FULL(arm_correlate_q15, q15_t, int16_t, kConvQ15, kVarCorr)
+MI355X_CONV_FULL(arm_correlate_q31, q31_t, int32_t, kConvQ31, kVarCorr)
+MI355X_CONV_FULL(arm_correlate_fast_q15, q15_t, int16_t, kConvFastQ15, kVarCorr)
+MI355X_CONV_FULL(arm_correlate_fast_q31, q31_t, int32_t, kConvFastQ31, kVarCorr)
+#undef MI355X_CONV_FULL
+
+#define MI355X_CONV_PARTIAL(NAME, T, CT, OP)                                                                       \
+  arm_status NAME(const T* pSrcA, uint32_t srcALen, const T* pSrcB, uint32_t srcBLen, T* pDst, uint32_t firstIndex, \
+                  uint32_t numPoints) {                                                                            \
+    if (!partial_range_ok(srcALen, srcBLen, firstIndex, numPoints)) return ARM_MATH_ARGUMENT_ERROR;                \
+    conv_family_sync<CT>(OP, kVarPartial, (const CT*)pSrcA, srcALen, (const CT*)pSrcB, srcBLen, (CT*)pDst,         \
+                         firstIndex, numPoints, #NAME);                                                            \
+    return ARM_MATH_SUCCESS;                                                                                       \
+  }                                                                                                                \
+  arm_status NAME##_batch(const T* d_a, uint32_t srcALen, uint32_t strideA, const T* d_b, uint32_t srcBLen,        \
+                          uint32_t strideB, T* d_dst, uint32_t firstIndex, uint32_t numPoints, uint32_t batch,     \
+                          void* stream) {                                                                          \
+    if (!partial_range_ok(srcALen, srcBLen, firstIndex, numPoints)) return ARM_MATH_ARGUMENT_ERROR;                \
+    return conv_family_batch<CT>(OP, kVarPartial, (const CT*)d_a, srcALen, strideA, (const CT*)d_b, srcBLen,       \
+                                 strideB, (CT*)d_dst, firstIndex, numPoints, batch, stream, #NAME "_batch");       \
+  }
+MI355X_CONV_PARTIAL(arm_conv_partial_f32, float32_t, float, kConvF32)
+MI355X_CONV_PARTIAL(arm_conv_partial_q15, q15_t, int16_t, kConvQ15)
+MI355X_CONV_PARTIAL(arm_conv_partial_q31, q31_t, int32_t, kConvQ31)
+#undef MI355X_CONV_PARTIAL
 
 }  // extern "C"

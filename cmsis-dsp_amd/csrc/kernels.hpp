@@ -83,11 +83,21 @@ hipError_t mfcc_f32_post_launch(int n, const float* y, const float* maxv, int ma
 hipError_t mat_mult_f32_launch(int m, int k, int n, const float* a, const float* b, float* c,
                                uint32_t batch, hipStream_t st);
 
-// Linear convolution (arm_conv_f32 / _q15 / _q31 semantics, bit-exact), kind 0 f32, 1 q15,
-// 2 q31: y[i] = a[i] (*) b[i] over `batch` items, a / b item strides sa / sb (0 = shared),
-// y items contiguous of alen + blen - 1.
-hipError_t conv_run(int kind, const void* a, uint32_t alen, uint64_t sa, const void* b, uint32_t blen, uint64_t sb,
-                    void* y, uint32_t batch, hipStream_t st);
+// Convolution / correlation family (conv.hip), bit-exact per op:
+//   v[n] = sum_k x[k] * g[n-k], k ascending, g = h (convolution) or h time-reversed
+//   (corr: correlation), for n in [first, first + num), stored at
+//   y[item * sy + yoff + ydir * n].  x / h item strides sx / sh (0 = shared).
+// kConvFastQ15 requires A >= B (the reference's x is the longer input).
+enum ConvOp { kConvF32 = 0, kConvQ15 = 1, kConvQ31 = 2, kConvFastQ15 = 3, kConvFastQ31 = 4 };
+struct ConvJob {
+  int op;
+  bool corr;
+  const void* x; uint32_t A; uint64_t sx;
+  const void* h; uint32_t B; uint64_t sh;
+  void* y; uint64_t sy; int64_t yoff; int ydir;
+  uint32_t first, num, batch;
+};
+hipError_t conv_family_run(const ConvJob& job, hipStream_t st);
 
 // Row-major q15 / q31 C[b] = A[b] * B[b] (arm_mat_mult_q15 / _q31 semantics, bit-exact):
 // byte-sliced planes on the i8 matrix cores (mat_mult_fixed.hip).

@@ -341,6 +341,38 @@ void arm_conv_f32(const float32_t *pSrcA, uint32_t srcALen, const float32_t *pSr
 void arm_conv_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB, uint32_t srcBLen, q15_t *pDst);
 void arm_conv_q31(const q31_t *pSrcA, uint32_t srcALen, const q31_t *pSrcB, uint32_t srcBLen, q31_t *pDst);
 
+/* Fast fixed-point convolution (filtering_functions.h:503,555; arm_conv_fast_q15.c,
+ * arm_conv_fast_q31.c): modular q31_t accumulators.  q15: __SMLAD sums, (q15)(sum >> 15),
+ * including the reference's single-sample __SMLAD high-halfword term (+1 per MAC with both
+ * samples negative in its stage-1/stage-3 remainder loops); q31: sum of (x*y) >> 32, output
+ * sum << 1. */
+void arm_conv_fast_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB, uint32_t srcBLen, q15_t *pDst);
+void arm_conv_fast_q31(const q31_t *pSrcA, uint32_t srcALen, const q31_t *pSrcB, uint32_t srcBLen, q31_t *pDst);
+
+/* Partial convolution (filtering_functions.h:610,656,723; arm_conv_partial_{f32,q15,q31}.c
+ * !ARM_MATH_DSP branch): outputs firstIndex .. firstIndex + numPoints - 1 of arm_conv_*,
+ * written at pDst[firstIndex ...]; ARM_MATH_ARGUMENT_ERROR when firstIndex + numPoints >
+ * srcALen + srcBLen - 1. */
+arm_status arm_conv_partial_f32(const float32_t *pSrcA, uint32_t srcALen, const float32_t *pSrcB, uint32_t srcBLen,
+                                float32_t *pDst, uint32_t firstIndex, uint32_t numPoints);
+arm_status arm_conv_partial_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB, uint32_t srcBLen,
+                                q15_t *pDst, uint32_t firstIndex, uint32_t numPoints);
+arm_status arm_conv_partial_q31(const q31_t *pSrcA, uint32_t srcALen, const q31_t *pSrcB, uint32_t srcBLen,
+                                q31_t *pDst, uint32_t firstIndex, uint32_t numPoints);
+
+/* Correlation (filtering_functions.h:1873,1923,1939,1973,1989; arm_correlate_f32.c:1013-1096,
+ * arm_correlate_q15.c:814-895, arm_correlate_q31.c, arm_correlate_fast_q15.c,
+ * arm_correlate_fast_q31.c).  pDst has 2 * max(srcALen, srcBLen) - 1 words; the
+ * srcALen + srcBLen - 1 computed ones are written from pDst[srcALen - srcBLen] forward, or,
+ * when srcALen < srcBLen, from pDst[srcALen + srcBLen - 2] backward; the others are left
+ * untouched (the reference asks the caller to zero pDst). */
+void arm_correlate_f32(const float32_t *pSrcA, uint32_t srcALen, const float32_t *pSrcB, uint32_t srcBLen,
+                       float32_t *pDst);
+void arm_correlate_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB, uint32_t srcBLen, q15_t *pDst);
+void arm_correlate_q31(const q31_t *pSrcA, uint32_t srcALen, const q31_t *pSrcB, uint32_t srcBLen, q31_t *pDst);
+void arm_correlate_fast_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB, uint32_t srcBLen, q15_t *pDst);
+void arm_correlate_fast_q31(const q31_t *pSrcA, uint32_t srcALen, const q31_t *pSrcB, uint32_t srcBLen, q31_t *pDst);
+
 /* ===================================================================================
  * Matrix multiply, f32.  Prototypes: Include/dsp/matrix_functions.h:341-344,630-634
  * Reference bodies: Source/MatrixFunctions/arm_mat_mult_f32.c:600-730,

@@ -85,6 +85,39 @@ arm_status arm_conv_q15_batch(const q15_t *d_a, uint32_t srcALen, uint32_t strid
                               uint32_t srcBLen, uint32_t strideB, q15_t *d_dst, uint32_t batch, void *stream);
 arm_status arm_conv_q31_batch(const q31_t *d_a, uint32_t srcALen, uint32_t strideA, const q31_t *d_b,
                               uint32_t srcBLen, uint32_t strideB, q31_t *d_dst, uint32_t batch, void *stream);
+arm_status arm_conv_fast_q15_batch(const q15_t *d_a, uint32_t srcALen, uint32_t strideA, const q15_t *d_b,
+                                   uint32_t srcBLen, uint32_t strideB, q15_t *d_dst, uint32_t batch, void *stream);
+arm_status arm_conv_fast_q31_batch(const q31_t *d_a, uint32_t srcALen, uint32_t strideA, const q31_t *d_b,
+                                   uint32_t srcBLen, uint32_t strideB, q31_t *d_dst, uint32_t batch, void *stream);
+
+/* Partial convolution of `batch` pairs (strides as arm_conv_*_batch): item i's numPoints
+ * outputs firstIndex .. firstIndex + numPoints - 1 go COMPACTLY to d_dst + i*numPoints.
+ * ARM_MATH_ARGUMENT_ERROR when firstIndex + numPoints > srcALen + srcBLen - 1. */
+arm_status arm_conv_partial_f32_batch(const float32_t *d_a, uint32_t srcALen, uint32_t strideA,
+                                      const float32_t *d_b, uint32_t srcBLen, uint32_t strideB, float32_t *d_dst,
+                                      uint32_t firstIndex, uint32_t numPoints, uint32_t batch, void *stream);
+arm_status arm_conv_partial_q15_batch(const q15_t *d_a, uint32_t srcALen, uint32_t strideA, const q15_t *d_b,
+                                      uint32_t srcBLen, uint32_t strideB, q15_t *d_dst, uint32_t firstIndex,
+                                      uint32_t numPoints, uint32_t batch, void *stream);
+arm_status arm_conv_partial_q31_batch(const q31_t *d_a, uint32_t srcALen, uint32_t strideA, const q31_t *d_b,
+                                      uint32_t srcBLen, uint32_t strideB, q31_t *d_dst, uint32_t firstIndex,
+                                      uint32_t numPoints, uint32_t batch, void *stream);
+
+/* Correlation of `batch` pairs: item i writes d_dst + i*(2*max(srcALen, srcBLen) - 1) at the
+ * positions arm_correlate_* writes (the others are left untouched). */
+arm_status arm_correlate_f32_batch(const float32_t *d_a, uint32_t srcALen, uint32_t strideA, const float32_t *d_b,
+                                   uint32_t srcBLen, uint32_t strideB, float32_t *d_dst, uint32_t batch,
+                                   void *stream);
+arm_status arm_correlate_q15_batch(const q15_t *d_a, uint32_t srcALen, uint32_t strideA, const q15_t *d_b,
+                                   uint32_t srcBLen, uint32_t strideB, q15_t *d_dst, uint32_t batch, void *stream);
+arm_status arm_correlate_q31_batch(const q31_t *d_a, uint32_t srcALen, uint32_t strideA, const q31_t *d_b,
+                                   uint32_t srcBLen, uint32_t strideB, q31_t *d_dst, uint32_t batch, void *stream);
+arm_status arm_correlate_fast_q15_batch(const q15_t *d_a, uint32_t srcALen, uint32_t strideA, const q15_t *d_b,
+                                        uint32_t srcBLen, uint32_t strideB, q15_t *d_dst, uint32_t batch,
+                                        void *stream);
+arm_status arm_correlate_fast_q31_batch(const q31_t *d_a, uint32_t srcALen, uint32_t strideA, const q31_t *d_b,
+                                        uint32_t srcBLen, uint32_t strideB, q31_t *d_dst, uint32_t batch,
+                                        void *stream);
 
 /* Row-major C[b] = A[b] * B[b] for `batch` contiguous (numRows x numCols) matrices with
  * the shapes of the three instances (their pData must be device pointers to the first

@@ -30,6 +30,11 @@ SRCS := \
   $(F)/arm_fir_f32.c $(F)/arm_fir_init_f32.c $(F)/arm_fir_q15.c $(F)/arm_fir_init_q15.c \
   $(F)/arm_fir_q31.c $(F)/arm_fir_init_q31.c $(F)/arm_fir_fast_q15.c $(F)/arm_fir_fast_q31.c \
   $(F)/arm_conv_f32.c $(F)/arm_conv_q15.c $(F)/arm_conv_q31.c \
+  $(F)/arm_conv_fast_q15.c $(F)/arm_conv_fast_q31.c \
+  $(F)/arm_conv_partial_f32.c $(F)/arm_conv_partial_q15.c $(F)/arm_conv_partial_q31.c \
+  $(F)/arm_conv_partial_fast_q15.c $(F)/arm_conv_partial_fast_q31.c \
+  $(F)/arm_correlate_f32.c $(F)/arm_correlate_q15.c $(F)/arm_correlate_q31.c \
+  $(F)/arm_correlate_fast_q15.c $(F)/arm_correlate_fast_q31.c \
   $(M)/arm_mat_mult_f32.c $(M)/arm_mat_init_f32.c $(M)/arm_mat_vec_mult_f32.c \
   $(M)/arm_mat_mult_q15.c $(M)/arm_mat_mult_q31.c $(M)/arm_mat_init_q15.c $(M)/arm_mat_init_q31.c \
   $(T)/arm_mfcc_f32.c $(T)/arm_mfcc_init_f32.c $(ST)/arm_absmax_f32.c $(B)/arm_scale_f32.c \

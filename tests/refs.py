@@ -122,6 +122,20 @@ class Host:
         self.fn(f"arm_conv_{kind}")(a.ctypes.data, len(a), b.ctypes.data, len(b), y.ctypes.data)
         return y
 
+    def conv_family(self, fn, a, b, first=0, num=0, fill=0):
+        """arm_<fn> for fn in _abi.CONV_FULL + CONV_PARTIAL on one pair: returns (pDst, status)
+        with pDst pre-filled with `fill` (partial / correlate leave words untouched)."""
+        dt = DTYPE[fn[-3:]]
+        a = np.ascontiguousarray(a, dtype=dt)
+        b = np.ascontiguousarray(b, dtype=dt)
+        n = 2 * max(len(a), len(b)) - 1 if fn.startswith("correlate") else len(a) + len(b) - 1
+        y = np.full(n, fill, dtype=dt)
+        f = self.fn(f"arm_{fn}")
+        if fn.startswith("conv_partial"):
+            return y, f(a.ctypes.data, len(a), b.ctypes.data, len(b), y.ctypes.data, first, num)
+        f(a.ctypes.data, len(a), b.ctypes.data, len(b), y.ctypes.data)
+        return y, 0
+
     def mat_mult_fixed(self, kind, a, b):
         """arm_mat_mult_q15 / _q31: returns (status, C)."""
         dt = np.int16 if kind == "q15" else np.int32

@@ -38,7 +38,8 @@ def test_module_surface_without_gpu(cdsp):
     assert cdsp.arm_rfft_output_buffer_size(dt.F32, 128) == 128 and not cdsp.has_neon()
     for name in ("arm_cfft_q31", "arm_cfft_q15", "arm_fir_f32", "arm_fir_q15", "arm_fir_q31", "arm_fir_fast_q15",
                  "arm_fir_fast_q31", "arm_mat_mult_f32", "arm_mat_mult_q15", "arm_mat_mult_q31", "arm_mfcc_f32",
-                 "arm_conv_f32", "arm_conv_q15", "arm_conv_q31", "arm_rfft_q31", "arm_rfft_q15"):
+                 "arm_conv_f32", "arm_conv_q15", "arm_conv_q31", "arm_rfft_q31", "arm_rfft_q15",
+                 "arm_correlate_f32", "arm_correlate_fast_q15", "arm_conv_partial_q31", "arm_conv_fast_q31"):
         assert callable(getattr(cdsp, name))
 
 
@@ -188,3 +189,30 @@ def test_rfft_rifft_fixed(cdsp, torch_gpu, ref):
         assert len(inv) == nb
         assert inv.tobytes() == ref.rfft_fixed(kind, nb, rq, 1, 1)[0].tobytes()
         np.testing.assert_allclose(invref / nb, back(inv), atol=atol_i)
+
+
+@pytest.mark.gpu
+def test_correlate_and_partial(cdsp, torch_gpu, ref):
+    """cmsis_arm_correlate_* / cmsis_arm_conv_partial_* / cmsis_arm_conv_fast_* call shapes:
+    correlate f32 against np.correlate (full), fixed point bit-exact vs the reference build."""
+    rng = np.random.default_rng(4)
+    a, b = rng.uniform(-1, 1, 40), rng.uniform(-1, 1, 13)
+    # 2*max - 1 words: np.correlate(a, b, "full") after srcALen - srcBLen leading words when
+    # srcALen >= srcBLen, in the first srcALen + srcBLen - 1 words otherwise
+    y = cdsp.arm_correlate_f32(a, len(a), b, len(b))
+    assert len(y) == 79 and not y[:27].any()
+    np.testing.assert_allclose(y[27:], np.correlate(a, b, "full"), 1e-5, 1e-6)
+    y = cdsp.arm_correlate_f32(b, len(b), a, len(a))
+    assert len(y) == 79 and not y[52:].any()
+    np.testing.assert_allclose(y[:52], np.correlate(b, a, "full"), 1e-5, 1e-6)
+    st, y = cdsp.arm_conv_partial_f32(a, len(a), b, len(b), 5, 20)
+    assert st == 0
+    np.testing.assert_allclose(y[5:25], np.convolve(a, b)[5:25], 1e-5, 1e-6)
+    assert cdsp.arm_conv_partial_f32(a, len(a), b, len(b), 50, 20)[0] == -1
+    for kind, conv in (("q15", toQ15), ("q31", toQ31)):
+        qa, qb = conv(a * 0.5), conv(b * 0.5)
+        for fn in (f"correlate_{kind}", f"correlate_fast_{kind}", f"conv_fast_{kind}"):
+            got = getattr(cdsp, f"arm_{fn}")(qa, len(qa), qb, len(qb))
+            assert got.tobytes() == ref.conv_family(fn, qa, qb)[0].tobytes(), fn
+        st, got = getattr(cdsp, f"arm_conv_partial_{kind}")(qa, len(qa), qb, len(qb), 3, 30)
+        assert st == 0 and got[3:33].tobytes() == ref.conv_family(f"conv_partial_{kind}", qa, qb, 3, 30)[0][3:33].tobytes()
