@@ -248,7 +248,8 @@ def _conv_family(fn):
 
 
 for _fn in ("conv_fast_q15", "conv_fast_q31", "correlate_f32", "correlate_q15", "correlate_q31", "correlate_fast_q15",
-            "correlate_fast_q31", "conv_partial_f32", "conv_partial_q15", "conv_partial_q31"):
+            "correlate_fast_q31", "conv_partial_f32", "conv_partial_q15", "conv_partial_q31", "conv_partial_fast_q15",
+            "conv_partial_fast_q31"):
     globals()[f"arm_{_fn}"] = _conv_family(_fn)
 del _fn
 

@@ -45,6 +45,7 @@ def _load():
     _abi.bind(lib, _abi.DROPIN)
     _abi.bind(lib, _abi.MFCC_LEN)
     _abi.bind(lib, _abi.RFFTQ_LEN)
+    _abi.bind(lib, _abi.PARTIAL_FAST)
     _abi.bind(lib, _abi.BATCHED)
     return lib
 

@@ -90,6 +90,9 @@ RFFT_SIZES = (32, 64, 128, 256, 512, 1024, 2048, 4096)
 CONV_FULL = ("conv_f32", "conv_q15", "conv_q31", "conv_fast_q15", "conv_fast_q31", "correlate_f32", "correlate_q15",
              "correlate_q31", "correlate_fast_q15", "correlate_fast_q31")
 CONV_PARTIAL = ("conv_partial_f32", "conv_partial_q15", "conv_partial_q31")
+# product only (the oracle restates them as arm_conv_fast_* over the range; the reference's
+# own bodies are memory-unsafe for most ranges)
+CONV_PARTIAL_FAST = ("conv_partial_fast_q15", "conv_partial_fast_q31")
 
 # name -> (restype, argtypes): the drop-in surface of include/arm_math.h
 DROPIN = {
@@ -153,6 +156,9 @@ RFFTQ_LEN = {f"arm_rfft_init_{n}_{t}": (C.c_int, [P(arm_rfft_instance_q31 if t =
                                                  C.c_uint32, C.c_uint32])
              for n in RFFTQ_SIZES for t in ("q31", "q15")}
 
+PARTIAL_FAST = {f"arm_{f}": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
+                                       C.c_uint32]) for f in CONV_PARTIAL_FAST}
+
 # the additive batched device API of include/arm_math_mi355x.h
 BATCHED = {
     "arm_cfft_f32_batch": (C.c_int, [P(arm_cfft_instance_f32), C.c_void_p, C.c_uint32, C.c_uint8, C.c_uint8,
@@ -184,7 +190,8 @@ BATCHED = {
     **{f"arm_{f}_batch": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
                                     C.c_void_p, C.c_uint32, C.c_void_p]) for f in CONV_FULL},
     **{f"arm_{f}_batch": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
-                                    C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]) for f in CONV_PARTIAL},
+                                    C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p])
+       for f in CONV_PARTIAL + CONV_PARTIAL_FAST},
     "arm_mfcc_f32_batch": (C.c_int, [P(arm_mfcc_instance_f32), C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                      C.c_void_p]),
     "arm_mi355x_last_error": (C.c_int, []),

@@ -724,6 +724,12 @@ MI355X_CONV_FULL(arm_correlate_fast_q31, q31_t, int32_t, kConvFastQ31, kVarCorr)
 MI355X_CONV_PARTIAL(arm_conv_partial_f32, float32_t, float, kConvF32)
 MI355X_CONV_PARTIAL(arm_conv_partial_q15, q15_t, int16_t, kConvQ15)
 MI355X_CONV_PARTIAL(arm_conv_partial_q31, q31_t, int32_t, kConvQ31)
+// arm_conv_partial_fast_q15 / _q31: outputs firstIndex .. of arm_conv_fast_q15 / _q31.  The
+// reference's own bodies (arm_conv_partial_fast_q15.c:110-118 stage sizes) read outside the
+// inputs for most ranges (the host build segfaults: tools/probes/conv_family_model.py), so
+// the contract is the documented one: the fast convolution's words over the range.
+MI355X_CONV_PARTIAL(arm_conv_partial_fast_q15, q15_t, int16_t, kConvFastQ15)
+MI355X_CONV_PARTIAL(arm_conv_partial_fast_q31, q31_t, int32_t, kConvFastQ31)
 #undef MI355X_CONV_PARTIAL
 
 }  // extern "C"

@@ -359,6 +359,14 @@ arm_status arm_conv_partial_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_
                                 q15_t *pDst, uint32_t firstIndex, uint32_t numPoints);
 arm_status arm_conv_partial_q31(const q31_t *pSrcA, uint32_t srcALen, const q31_t *pSrcB, uint32_t srcBLen,
                                 q31_t *pDst, uint32_t firstIndex, uint32_t numPoints);
+/* filtering_functions.h:677,744 (arm_conv_partial_fast_q15.c / _q31.c): words firstIndex ..
+ * firstIndex + numPoints - 1 of arm_conv_fast_q15 / _q31.  The reference's bodies read
+ * outside the inputs for most ranges on the host build (segfault), so parity is pinned to
+ * arm_conv_fast_* over the range. */
+arm_status arm_conv_partial_fast_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB, uint32_t srcBLen,
+                                     q15_t *pDst, uint32_t firstIndex, uint32_t numPoints);
+arm_status arm_conv_partial_fast_q31(const q31_t *pSrcA, uint32_t srcALen, const q31_t *pSrcB, uint32_t srcBLen,
+                                     q31_t *pDst, uint32_t firstIndex, uint32_t numPoints);
 
 /* Correlation (filtering_functions.h:1873,1923,1939,1973,1989; arm_correlate_f32.c:1013-1096,
  * arm_correlate_q15.c:814-895, arm_correlate_q31.c, arm_correlate_fast_q15.c,

@@ -102,6 +102,12 @@ arm_status arm_conv_partial_q15_batch(const q15_t *d_a, uint32_t srcALen, uint32
 arm_status arm_conv_partial_q31_batch(const q31_t *d_a, uint32_t srcALen, uint32_t strideA, const q31_t *d_b,
                                       uint32_t srcBLen, uint32_t strideB, q31_t *d_dst, uint32_t firstIndex,
                                       uint32_t numPoints, uint32_t batch, void *stream);
+arm_status arm_conv_partial_fast_q15_batch(const q15_t *d_a, uint32_t srcALen, uint32_t strideA, const q15_t *d_b,
+                                           uint32_t srcBLen, uint32_t strideB, q15_t *d_dst, uint32_t firstIndex,
+                                           uint32_t numPoints, uint32_t batch, void *stream);
+arm_status arm_conv_partial_fast_q31_batch(const q31_t *d_a, uint32_t srcALen, uint32_t strideA, const q31_t *d_b,
+                                           uint32_t srcBLen, uint32_t strideB, q31_t *d_dst, uint32_t firstIndex,
+                                           uint32_t numPoints, uint32_t batch, void *stream);
 
 /* Correlation of `batch` pairs: item i writes d_dst + i*(2*max(srcALen, srcBLen) - 1) at the
  * positions arm_correlate_* writes (the others are left untouched). */

@@ -16,6 +16,7 @@ from cmsisdsp_amd import _abi
 
 FULL = list(_abi.CONV_FULL)
 PARTIAL = list(_abi.CONV_PARTIAL)
+PARTIAL_FAST = list(_abi.CONV_PARTIAL_FAST)
 DT = {"f32": np.float32, "q15": np.int16, "q31": np.int32}
 SMALL = [(a, b) for a in (1, 2, 3, 4, 5, 7, 8, 9, 13, 16, 17, 33) for b in (1, 2, 3, 4, 5, 6, 7, 9, 12, 13, 17, 33)]
 
@@ -147,3 +148,32 @@ def test_conv_family_batch(dsp, torch_gpu, ref, fn, la, lb):
             if fn in PARTIAL:
                 want = want[first:first + num]
             assert got[i].tobytes() == want.tobytes(), (shared, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fn", PARTIAL_FAST)
+def test_conv_partial_fast(dsp, torch_gpu, ref, fn):
+    """arm_conv_partial_fast_*: the words of arm_conv_fast_* over the range (the reference's
+    own partial-fast bodies read outside the inputs for most ranges on the host build, so
+    parity is pinned to the reference's arm_conv_fast_*), drop-in and batched."""
+    kind = fn[-3:]
+    full = fn.replace("partial_", "")
+    rng = np.random.default_rng(13)
+    for la, lb in [(5, 3), (3, 5), (300, 40), (40, 300), (5000, 129), (1500, 1100)]:
+        a, b = gen(kind, la, rng, "neg"), gen(kind, lb, rng, "full")
+        want, _ = ref.conv_family(full, a, b)
+        for first, num in partial_ranges(la, lb):
+            got, st = dsp.arm_conv_family(fn, a, b, first, num, fill=9)
+            assert st == 0 and got[first:first + num].tobytes() == want[first:first + num].tobytes(), (la, lb, first, num)
+            assert (got[:first] == 9).all() and (got[first + num:] == 9).all()
+        assert dsp.arm_conv_family(fn, a, b, la + lb - 2, 2)[1] == _abi.ARM_MATH_ARGUMENT_ERROR
+    la, lb, batch = 2500, 300, 4
+    A = np.stack([gen(kind, la, rng, "full") for _ in range(batch)])
+    B = gen(kind, lb, rng, "neg")
+    tdt = torch_gpu.int16 if kind == "q15" else torch_gpu.int32
+    first, num = 100, 2600
+    out = torch_gpu.zeros((batch, num), dtype=tdt, device="cuda")
+    dsp.conv_family_batch(fn, torch_gpu.from_numpy(A).cuda(), torch_gpu.from_numpy(B).cuda(), out, first, num)
+    got = out.cpu().numpy()
+    for i in range(batch):
+        assert got[i].tobytes() == ref.conv_family(full, A[i], B)[0][first:first + num].tobytes(), i
