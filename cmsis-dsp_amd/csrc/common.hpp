@@ -12,7 +12,14 @@ __device__ __forceinline__ int32_t wadd(int32_t a, int32_t b) { return (int32_t)
 __device__ __forceinline__ int32_t wsub(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
 __device__ __forceinline__ int32_t wshl(int32_t a, int s) { return (int32_t)((uint32_t)a << s); }
 // (int32_t)(((q63_t)a * b) >> 32): arm_cfft_radix4_q31.c:235 — exactly v_mul_hi_i32.
-__device__ __forceinline__ int32_t mulhi(int32_t a, int32_t b) { return __mulhi(a, b); }
+// Emitted directly: from __mulhi LLVM sometimes rebuilds the product as a general 64-bit
+// multiply of the sign-extended operands (v_mul_hi_u32 + v_mad_u64_u32 + v_mul_lo_u32 per
+// product instead of one v_mul_hi_i32; 30 % of the q31 N=4096 kernel's VALU instructions).
+__device__ __forceinline__ int32_t mulhi(int32_t a, int32_t b) {
+  int32_t r;
+  asm("v_mul_hi_i32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 
 // none.h:184-206 rounding forms (SMMULR / SMMLAR / SMMLSR)
 __device__ __forceinline__ int32_t mult_R(int32_t x, int32_t y) {
