@@ -470,9 +470,184 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 #undef TW3
 #undef TW4
 
+// ============================================================================================
+// q15 N = 4096 on packed 16-bit math: one VGPR holds a complex sample {re, im} and every
+// radix-4 butterfly of bfly_q15 is restated on v_pk_* / v_dot2 with identical bits:
+//   __SSAT(x + y, 16), __SSAT(x - y, 16)  -> v_pk_add_i16 / v_pk_sub_i16 with clamp
+//   t16((x >> 1) +- (y >> 1)) (never wraps) -> v_pk_ashrrev_i16 + v_pk_add/sub_u16
+//   (q15)((p*q +- r*s) >> 16) (int32 wrap)  -> v_dot2_i32_i16 (modular) and the high half;
+//     a difference uses the twiddle word ~w (= -w - 1) and adds the missing +R back through
+//     the dot's accumulator: w.x*R1 - w.y*R0 = dot2({~w.y, w.x}, R) + R0 (mod 2^32).
+// Each twiddle is held as the two packed words its products need (forward {w.x, w.y} and
+// {~w.y, w.x}; inverse {w.x, ~w.y} and {w.y, w.x}).  Same work mapping as
+// cfft_fx4096_kernel (three radix-16 register passes, s4096 LDS padding, free bit reversal).
+#ifndef MI355X_FX_Q15_PACKED
+#define MI355X_FX_Q15_PACKED 1
+#endif
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s16x2 pk(uint32_t u) { return __builtin_bit_cast(s16x2, u); }
+__device__ __forceinline__ uint32_t upk(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ s16x2 pk_sat_add(s16x2 a, s16x2 b) { return __builtin_elementwise_add_sat(a, b); }
+__device__ __forceinline__ s16x2 pk_sat_sub(s16x2 a, s16x2 b) { return __builtin_elementwise_sub_sat(a, b); }
+__device__ __forceinline__ s16x2 pk_swap(s16x2 v) { return __builtin_shufflevector(v, v, 1, 0); }
+
+struct TwP { s16x2 p, q; };      // the two packed twiddle words of one complex product
+template <bool INV> __device__ __forceinline__ TwP twp(short2 w) {
+  const short nx = (short)~w.y;   // ~w.y: forward imaginary / inverse real difference term
+  if (!INV) return TwP{s16x2{w.x, w.y}, s16x2{nx, w.x}};
+  return TwP{s16x2{w.x, nx}, s16x2{w.y, w.x}};
+}
+// forward: {hi(w.x R0 + w.y R1), hi(w.x R1 - w.y R0)}; inverse: {hi(w.x R0 - w.y R1),
+// hi(w.y R0 + w.x R1)} -- bfly_q15's q15mul pairs.
+template <bool INV> __device__ __forceinline__ s16x2 cmul_pk(TwP w, s16x2 R) {
+  const uint32_t u = upk(R);
+  int32_t x, y;
+  if (!INV) {
+    x = __builtin_amdgcn_sdot2(w.p, R, 0, false);
+    y = __builtin_amdgcn_sdot2(w.q, R, (int32_t)(int16_t)u, false);
+  } else {
+    x = __builtin_amdgcn_sdot2(w.p, R, (int32_t)u >> 16, false);
+    y = __builtin_amdgcn_sdot2(w.q, R, 0, false);
+  }
+  return pk(__builtin_amdgcn_perm((uint32_t)y, (uint32_t)x, 0x07060302u));
+}
+
+template <bool INV, int KIND>
+__device__ __forceinline__ void bfly_pk(s16x2& a, s16x2& b, s16x2& c, s16x2& d, TwP w1, TwP w2, TwP w3) {
+  constexpr short SH = KIND == 0 ? 2 : 0;
+  const s16x2 A = a >> SH, B = b >> SH, Cc = c >> SH, D = d >> SH;
+  s16x2 R = pk_sat_add(A, Cc), S = pk_sat_sub(A, Cc), T = pk_sat_add(B, D);
+  const s16x2 Rh = R >> (short)1, Th = T >> (short)1;
+  const s16x2 oa = KIND == 1 ? (s16x2)((Rh + Th) >> (short)1) : (s16x2)(Rh + Th);
+  R = KIND == 0 ? pk_sat_sub(R, T) : (s16x2)(Rh - Th);
+  const s16x2 ob = KIND == 2 ? R : cmul_pk<INV>(w2, R);
+  T = pk_sat_sub(B, D);
+  s16x2 nR, nS;                          // forward nR = {S0 - T1, S1 + T0}, nS = {S0 + T1, S1 - T0}
+  if constexpr (KIND == 0) {
+    const s16x2 Ts = pk_swap(T);
+    const s16x2 add = pk_sat_add(S, Ts), sub = pk_sat_sub(S, Ts);   // {S0+T1, S1+T0}, {S0-T1, S1-T0}
+    const s16x2 r = __builtin_shufflevector(sub, add, 0, 3), s = __builtin_shufflevector(add, sub, 0, 3);
+    nR = INV ? s : r; nS = INV ? r : s;
+  } else {
+    const s16x2 Sh = S >> (short)1;
+    const s16x2 Tn = pk_swap(T >> (short)1) * s16x2{1, -1};          // {T1', -T0'} (|T'| < 2^14)
+    const s16x2 r = Sh - Tn, s = Sh + Tn;
+    nR = INV ? s : r; nS = INV ? r : s;
+  }
+  if constexpr (KIND == 2) { c = nS; d = nR; }
+  else { c = cmul_pk<INV>(w1, nS); d = cmul_pk<INV>(w3, nR); }
+  a = oa; b = ob;
+}
+
+template <bool INV>
+__global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_q15_4096_pk_kernel(short2* __restrict__ data, uint32_t batch,
+                                                                    const short2* __restrict__ tw, uint32_t flags) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4351];
+  const int t = threadIdx.x;
+  const bool brev = flags & kBitrev;
+  const int q2 = t >> 4, j2 = t & 15;
+  const int q3 = (int)(__brev((uint32_t)t) >> 24);        // rev8(t)
+  TwP tw1[4][3], tw3[4][3], tw2[3], tw4[3], tw5[4][3];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      tw1[a][k] = twp<INV>(tw[(k + 1) * (t + 256 * a)]);
+      tw3[a][k] = twp<INV>(tw[(k + 1) * (j2 + 16 * a) * 16]);
+      tw5[a][k] = twp<INV>(tw[(k + 1) * a * 256]);
+    }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { tw2[k] = twp<INV>(tw[(k + 1) * 4 * t]); tw4[k] = twp<INV>(tw[(k + 1) * 64 * j2]); }
+  const TwP z{};
+
+  const uint32_t* D = reinterpret_cast<const uint32_t*>(data);
+  s16x2 v[16];
+  uint32_t nv[16];
+  if (blockIdx.x < batch) {
+    const uint32_t* X0 = D + (size_t)blockIdx.x * 4096;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) nv[4 * a + b] = X0[t + 256 * a + 1024 * b];
+  }
+  for (uint32_t tr = blockIdx.x; tr < batch; tr += gridDim.x) {
+    uint32_t* X = reinterpret_cast<uint32_t*>(data) + (size_t)tr * 4096;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = pk(nv[u]);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+      bfly_pk<INV, 0>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], tw1[a][0], tw1[a][1], tw1[a][2]);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) bfly_pk<INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], tw2[0], tw2[1], tw2[2]);
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) lds[s4096(t + 256 * a + 1024 * b)] = upk(v[4 * a + b]);
+    if (tr + gridDim.x < batch) {
+      const uint32_t* XN = D + (size_t)(tr + gridDim.x) * 4096;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) nv[4 * a + b] = XN[t + 256 * a + 1024 * b];
+    }
+    __syncthreads();
+    {
+      const int base = 256 * q2 + j2;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) v[4 * a + b] = pk(lds[s4096(base + 64 * a + 16 * b)]);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) bfly_pk<INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], tw3[b][0], tw3[b][1], tw3[b][2]);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        bfly_pk<INV, 1>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], tw4[0], tw4[1], tw4[2]);
+      __syncthreads();
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) lds[s4096(base + 64 * a + 16 * b)] = upk(v[4 * a + b]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) v[4 * a + b] = pk(lds[s4096(16 * q3 + 4 * a + b)]);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) bfly_pk<INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], tw5[b][0], tw5[b][1], tw5[b][2]);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) bfly_pk<INV, 2>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], z, z, z);
+    if (flags & kSatShl1) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = pk_sat_add(v[u], v[u]);    // arm_shift_q15(+1): __SSAT(x << 1, 16)
+    }
+    if (brev) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) X[(int)(__brev((uint32_t)u) >> 28) * 256 + t] = upk(v[u]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) X[16 * q3 + u] = upk(v[u]);
+    }
+  }
+}
+
 template <typename T>
 static hipError_t launch_fx4096(void* data, uint32_t batch, const void* tw, uint32_t flags, hipStream_t st) {
   using C = typename Fx<T>::C;
+  if constexpr (sizeof(T) == 2 && MI355X_FX_Q15_PACKED) {
+    if (flags & kIfft) {
+      const int grid = persistent_grid((const void*)cfft_q15_4096_pk_kernel<true>, 256, 0, batch);
+      hipLaunchKernelGGL(cfft_q15_4096_pk_kernel<true>, dim3(grid), dim3(256), 0, st, (short2*)data, batch,
+                         (const short2*)tw, flags);
+    } else {
+      const int grid = persistent_grid((const void*)cfft_q15_4096_pk_kernel<false>, 256, 0, batch);
+      hipLaunchKernelGGL(cfft_q15_4096_pk_kernel<false>, dim3(grid), dim3(256), 0, st, (short2*)data, batch,
+                         (const short2*)tw, flags);
+    }
+    return hipGetLastError();
+  }
   const uint32_t blocks = kFxT ? (batch + kFxT - 1) / (kFxT ? kFxT : 1) : batch;
   if (flags & kIfft) {
     const int grid = kFxT ? (int)blocks : persistent_grid((const void*)cfft_fx4096_kernel<T, true>, 256, 0, batch);
