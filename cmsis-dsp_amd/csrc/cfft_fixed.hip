@@ -143,6 +143,68 @@ __device__ __forceinline__ void bfly_q15(int2& a, int2& b, int2& c, int2& d,
   a = oa; b = ob; c = oc; d = od;
 }
 
+// ------------------------------------------------------------------ q15 butterflies, packed
+// (restated from bfly_q15, see cfft_q15_4096_pk_kernel for the mapping)
+#ifndef MI355X_FX_Q15_PACKED
+#define MI355X_FX_Q15_PACKED 1
+#endif
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s16x2 pk(uint32_t u) { return __builtin_bit_cast(s16x2, u); }
+__device__ __forceinline__ uint32_t upk(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ s16x2 pk_sat_add(s16x2 a, s16x2 b) { return __builtin_elementwise_add_sat(a, b); }
+__device__ __forceinline__ s16x2 pk_sat_sub(s16x2 a, s16x2 b) { return __builtin_elementwise_sub_sat(a, b); }
+__device__ __forceinline__ s16x2 pk_swap(s16x2 v) { return __builtin_shufflevector(v, v, 1, 0); }
+
+struct TwP { s16x2 p, q; };      // the two packed twiddle words of one complex product
+template <bool INV> __device__ __forceinline__ TwP twp(short2 w) {
+  const short nx = (short)~w.y;   // ~w.y: forward imaginary / inverse real difference term
+  if (!INV) return TwP{s16x2{w.x, w.y}, s16x2{nx, w.x}};
+  return TwP{s16x2{w.x, nx}, s16x2{w.y, w.x}};
+}
+// forward: {hi(w.x R0 + w.y R1), hi(w.x R1 - w.y R0)}; inverse: {hi(w.x R0 - w.y R1),
+// hi(w.y R0 + w.x R1)} -- bfly_q15's q15mul pairs.
+template <bool INV> __device__ __forceinline__ s16x2 cmul_pk(TwP w, s16x2 R) {
+  const uint32_t u = upk(R);
+  int32_t x, y;
+  if (!INV) {
+    x = __builtin_amdgcn_sdot2(w.p, R, 0, false);
+    y = __builtin_amdgcn_sdot2(w.q, R, (int32_t)(int16_t)u, false);
+  } else {
+    x = __builtin_amdgcn_sdot2(w.p, R, (int32_t)u >> 16, false);
+    y = __builtin_amdgcn_sdot2(w.q, R, 0, false);
+  }
+  return pk(__builtin_amdgcn_perm((uint32_t)y, (uint32_t)x, 0x07060302u));
+}
+
+template <bool INV, int KIND>
+__device__ __forceinline__ void bfly_pk(s16x2& a, s16x2& b, s16x2& c, s16x2& d, TwP w1, TwP w2, TwP w3) {
+  constexpr short SH = KIND == 0 ? 2 : 0;
+  const s16x2 A = a >> SH, B = b >> SH, Cc = c >> SH, D = d >> SH;
+  s16x2 R = pk_sat_add(A, Cc), S = pk_sat_sub(A, Cc), T = pk_sat_add(B, D);
+  const s16x2 Rh = R >> (short)1, Th = T >> (short)1;
+  const s16x2 oa = KIND == 1 ? (s16x2)((Rh + Th) >> (short)1) : (s16x2)(Rh + Th);
+  R = KIND == 0 ? pk_sat_sub(R, T) : (s16x2)(Rh - Th);
+  const s16x2 ob = KIND == 2 ? R : cmul_pk<INV>(w2, R);
+  T = pk_sat_sub(B, D);
+  s16x2 nR, nS;                          // forward nR = {S0 - T1, S1 + T0}, nS = {S0 + T1, S1 - T0}
+  if constexpr (KIND == 0) {
+    const s16x2 Ts = pk_swap(T);
+    const s16x2 add = pk_sat_add(S, Ts), sub = pk_sat_sub(S, Ts);   // {S0+T1, S1+T0}, {S0-T1, S1-T0}
+    const s16x2 r = __builtin_shufflevector(sub, add, 0, 3), s = __builtin_shufflevector(add, sub, 0, 3);
+    nR = INV ? s : r; nS = INV ? r : s;
+  } else {
+    const s16x2 Sh = S >> (short)1;
+    const s16x2 Tn = pk_swap(T >> (short)1) * s16x2{1, -1};          // {T1', -T0'} (|T'| < 2^14)
+    const s16x2 r = Sh - Tn, s = Sh + Tn;
+    nR = INV ? s : r; nS = INV ? r : s;
+  }
+  if constexpr (KIND == 2) { c = nS; d = nR; }
+  else { c = cmul_pk<INV>(w1, nS); d = cmul_pk<INV>(w3, nR); }
+  a = oa; b = ob;
+}
+
+
 // ------------------------------------------------------------------ element access
 template <typename T> struct Fx;
 template <> struct Fx<int32_t> {   // q31: complex = int2 in LDS and HBM
@@ -193,6 +255,21 @@ __device__ __forceinline__ void radix4_stages(typename Fx<T>::C* x, const typena
       const int c = bi / (M / 4), rr = bi % (M / 4);
       const int j = rr % n2, q = rr / n2;
       typename F::C* p = x + c * M + q * n1 + j;
+      if constexpr (sizeof(T) == 2 && MI355X_FX_Q15_PACKED) {
+        uint32_t* pu = reinterpret_cast<uint32_t*>(p);
+        s16x2 A = pk(pu[0]), B = pk(pu[n2]), C = pk(pu[2 * n2]), D = pk(pu[3 * n2]);
+        if (s == P::STAGES - 1) {
+          const TwP z{};
+          bfly_pk<INV, 2>(A, B, C, D, z, z, z);
+        } else {
+          const int ia = j * mod;
+          const TwP w1 = twp<INV>(tw[ia]), w2 = twp<INV>(tw[2 * ia]), w3 = twp<INV>(tw[3 * ia]);
+          if (s == 0) bfly_pk<INV, 0>(A, B, C, D, w1, w2, w3);
+          else        bfly_pk<INV, 1>(A, B, C, D, w1, w2, w3);
+        }
+        pu[0] = upk(A); pu[n2] = upk(B); pu[2 * n2] = upk(C); pu[3 * n2] = upk(D);
+        continue;
+      }
       int2 A = F::ld(p), B = F::ld(p + n2), C = F::ld(p + 2 * n2), D = F::ld(p + 3 * n2);
       if (s == P::STAGES - 1) {
         bfly<T, INV, 2>(A, B, C, D, int2{}, int2{}, int2{});
@@ -481,65 +558,6 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 // Each twiddle is held as the two packed words its products need (forward {w.x, w.y} and
 // {~w.y, w.x}; inverse {w.x, ~w.y} and {w.y, w.x}).  Same work mapping as
 // cfft_fx4096_kernel (three radix-16 register passes, s4096 LDS padding, free bit reversal).
-#ifndef MI355X_FX_Q15_PACKED
-#define MI355X_FX_Q15_PACKED 1
-#endif
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ s16x2 pk(uint32_t u) { return __builtin_bit_cast(s16x2, u); }
-__device__ __forceinline__ uint32_t upk(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
-__device__ __forceinline__ s16x2 pk_sat_add(s16x2 a, s16x2 b) { return __builtin_elementwise_add_sat(a, b); }
-__device__ __forceinline__ s16x2 pk_sat_sub(s16x2 a, s16x2 b) { return __builtin_elementwise_sub_sat(a, b); }
-__device__ __forceinline__ s16x2 pk_swap(s16x2 v) { return __builtin_shufflevector(v, v, 1, 0); }
-
-struct TwP { s16x2 p, q; };      // the two packed twiddle words of one complex product
-template <bool INV> __device__ __forceinline__ TwP twp(short2 w) {
-  const short nx = (short)~w.y;   // ~w.y: forward imaginary / inverse real difference term
-  if (!INV) return TwP{s16x2{w.x, w.y}, s16x2{nx, w.x}};
-  return TwP{s16x2{w.x, nx}, s16x2{w.y, w.x}};
-}
-// forward: {hi(w.x R0 + w.y R1), hi(w.x R1 - w.y R0)}; inverse: {hi(w.x R0 - w.y R1),
-// hi(w.y R0 + w.x R1)} -- bfly_q15's q15mul pairs.
-template <bool INV> __device__ __forceinline__ s16x2 cmul_pk(TwP w, s16x2 R) {
-  const uint32_t u = upk(R);
-  int32_t x, y;
-  if (!INV) {
-    x = __builtin_amdgcn_sdot2(w.p, R, 0, false);
-    y = __builtin_amdgcn_sdot2(w.q, R, (int32_t)(int16_t)u, false);
-  } else {
-    x = __builtin_amdgcn_sdot2(w.p, R, (int32_t)u >> 16, false);
-    y = __builtin_amdgcn_sdot2(w.q, R, 0, false);
-  }
-  return pk(__builtin_amdgcn_perm((uint32_t)y, (uint32_t)x, 0x07060302u));
-}
-
-template <bool INV, int KIND>
-__device__ __forceinline__ void bfly_pk(s16x2& a, s16x2& b, s16x2& c, s16x2& d, TwP w1, TwP w2, TwP w3) {
-  constexpr short SH = KIND == 0 ? 2 : 0;
-  const s16x2 A = a >> SH, B = b >> SH, Cc = c >> SH, D = d >> SH;
-  s16x2 R = pk_sat_add(A, Cc), S = pk_sat_sub(A, Cc), T = pk_sat_add(B, D);
-  const s16x2 Rh = R >> (short)1, Th = T >> (short)1;
-  const s16x2 oa = KIND == 1 ? (s16x2)((Rh + Th) >> (short)1) : (s16x2)(Rh + Th);
-  R = KIND == 0 ? pk_sat_sub(R, T) : (s16x2)(Rh - Th);
-  const s16x2 ob = KIND == 2 ? R : cmul_pk<INV>(w2, R);
-  T = pk_sat_sub(B, D);
-  s16x2 nR, nS;                          // forward nR = {S0 - T1, S1 + T0}, nS = {S0 + T1, S1 - T0}
-  if constexpr (KIND == 0) {
-    const s16x2 Ts = pk_swap(T);
-    const s16x2 add = pk_sat_add(S, Ts), sub = pk_sat_sub(S, Ts);   // {S0+T1, S1+T0}, {S0-T1, S1-T0}
-    const s16x2 r = __builtin_shufflevector(sub, add, 0, 3), s = __builtin_shufflevector(add, sub, 0, 3);
-    nR = INV ? s : r; nS = INV ? r : s;
-  } else {
-    const s16x2 Sh = S >> (short)1;
-    const s16x2 Tn = pk_swap(T >> (short)1) * s16x2{1, -1};          // {T1', -T0'} (|T'| < 2^14)
-    const s16x2 r = Sh - Tn, s = Sh + Tn;
-    nR = INV ? s : r; nS = INV ? r : s;
-  }
-  if constexpr (KIND == 2) { c = nS; d = nR; }
-  else { c = cmul_pk<INV>(w1, nS); d = cmul_pk<INV>(w3, nR); }
-  a = oa; b = ob;
-}
-
 template <bool INV>
 __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_q15_4096_pk_kernel(short2* __restrict__ data, uint32_t batch,
                                                                     const short2* __restrict__ tw, uint32_t flags) {
