@@ -57,6 +57,7 @@ WORKLOADS = {
     "conv_f32": ("conv", 128, 1 << 16, 8),
     "mat_mult_q15": ("matq15", 1024, 64, None),
     "mat_mult_q31": ("matq31", 1024, 64, None),
+    "mat_mult_fast_q31": ("matfast_q31", 1024, 64, None),
 }
 
 
@@ -118,7 +119,7 @@ def cpu_baseline(workload, n):
           "fir_f32": "fir_f32", "fir_q15": "fir_q15", "fir_q31": "fir_q31", "fir_fast_q15": "fir_fast_q15",
           "fir_fast_q31": "fir_fast_q31", "mat_mult_f32": "mat_mult_f32",
           "mfcc_f32": "mfcc_f32", "mat_mult_q15": "mat_mult_q15", "mat_mult_q31": "mat_mult_q31",
-          "rfft_f32": "rfft_f32", "conv_f32": "conv_f32", "rfft_q31": "rfft_q31", "rfft_q15": "rfft_q15"}[workload]
+          "mat_mult_fast_q31": "mat_mult_fast_q31", "rfft_f32": "rfft_f32", "conv_f32": "conv_f32", "rfft_q31": "rfft_q31", "rfft_q15": "rfft_q15"}[workload]
     nn = 256 if workload.startswith("mat_mult") else n  # 1024^3 takes seconds per matrix on one core
     out = subprocess.run([exe, wl, str(nn), str(threads), str(secs)], capture_output=True, text=True,
                          timeout=120)
@@ -322,14 +323,15 @@ def run_mfcc(n, batch, steps, warmup, world, rank):
 
 
 def run_mat_fixed(kind, dim, batch, steps, warmup, world, rank):
-    """arm_mat_mult_q15 / _q31 (byte-sliced i8 MFMA), full-range operands, bit-exact check of
-    matrix 0 against the CPU checker."""
-    a = synth(kind, batch * dim * dim, rank).view(batch, dim, dim)
-    b = synth(kind, batch * dim * dim, rank, salt=3).view(batch, dim, dim)
+    """arm_mat_mult_q15 / _q31 (byte-sliced i8 MFMA) or _fast_q31 (VALU), full-range operands,
+    bit-exact check of matrix 0 against the CPU checker."""
+    a = synth(kind[-3:], batch * dim * dim, rank).view(batch, dim, dim)
+    b = synth(kind[-3:], batch * dim * dim, rank, salt=3).view(batch, dim, dim)
     c = torch.empty_like(a)
+    fast = kind.startswith("fast")
 
     def launch(s):
-        dsp.mat_mult_batch(a, b, c)
+        dsp.mat_mult_batch(a, b, c, fast=fast)
 
     wall, kern_ms = time_launches(launch, steps, warmup, world)
     host, hk = cpu_checker()
@@ -376,7 +378,7 @@ def main():
         wall, kern_ms, parity = run_fir(kind[4:], n, batch, args.steps, args.warmup, world, rank)
         units = batch * 4096
         algo_bytes = units * bps + batch * (n - 1) * bps  # in + out + history read/write
-    elif args.workload in ("mat_mult_q15", "mat_mult_q31"):
+    elif args.workload in ("mat_mult_q15", "mat_mult_q31", "mat_mult_fast_q31"):
         wall, kern_ms, parity = run_mat_fixed(kind[3:], n, batch, args.steps, args.warmup, world, rank)
         units = batch
         algo_bytes = None
@@ -408,7 +410,18 @@ def main():
     line = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "data": "synthetic (per-rank seeded generator, rank-local, no scatter)"}
-    if args.workload in ("mat_mult_q15", "mat_mult_q31"):
+    if args.workload == "mat_mult_fast_q31":
+        ops = 2.0 * n * n * n * batch
+        line.update(value=round(total_units * 2.0 * n ** 3 / wall * 1e-12, 4), unit="TOPS (2*M*N*K int MAC)",
+                    dtype="q31 (per-product high word, modular q31 accumulator)",
+                    config={"workload": f"arm_mat_mult_fast_q31 {n}x{n}x{n} batch={batch}/GPU",
+                            "dims": [n, n, n], "batch_per_gpu": batch, "parallelism": f"dp{world} shards"})
+        # per MAC: one v_mul_hi_i32 + half a v_add3_u32 (two products summed per add3) = 1.5 lane-instr
+        lane_ops = 1.5 * (ops / 2) / (kern_ms * 1e-3) * 1e-12
+        line["roofline"] = {"bound": "valu", "achieved": round(lane_ops, 2), "peak": 39.3,
+                            "unit": "T VALU lane-instr/s (256 CU x 4 SIMD x 16 lanes x 2.4 GHz)",
+                            "frac": round(lane_ops / 39.3, 4), "traffic": None, "avg_kernel_ms": round(kern_ms, 4)}
+    elif args.workload in ("mat_mult_q15", "mat_mult_q31"):
         planes = 2 if args.workload.endswith("q15") else 4
         ops = 2.0 * n * n * n * batch
         line.update(value=round(total_units * 2.0 * n ** 3 / wall * 1e-12, 4), unit="TOPS (2*M*N*K int MAC)",

@@ -213,6 +213,15 @@ def arm_mat_mult_q15(pSrcA, pSrcB, pState=None):
     return _amd.arm_mat_mult_fixed("q15", _arr(pSrcA, _np.int16), _arr(pSrcB, _np.int16))
 
 
+def arm_mat_mult_fast_q31(pSrcA, pSrcB):
+    """cmsisdsp_matrix.c cmsis_arm_mat_mult_fast_q31: (status, C)."""
+    return _amd.arm_mat_mult_fixed("fast_q31", _arr(pSrcA, _np.int32), _arr(pSrcB, _np.int32))
+
+
+def arm_mat_mult_fast_q15(pSrcA, pSrcB, pState=None):
+    return _amd.arm_mat_mult_fixed("fast_q15", _arr(pSrcA, _np.int16), _arr(pSrcB, _np.int16))
+
+
 # ------------------------------------------------------------------ convolution
 def _conv(kind, dt):
     def run(pSrcA, srcALen, pSrcB, srcBLen):

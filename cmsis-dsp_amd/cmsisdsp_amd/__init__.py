@@ -398,28 +398,29 @@ def conv_family_batch(fn, a, b, out, first=0, num=0, stream=None):
 
 
 def arm_mat_mult_fixed(kind, a, b):
-    """(status, C) = A @ B through arm_mat_mult_q15 / arm_mat_mult_q31 (row-major)."""
-    dt = np.int16 if kind == "q15" else np.int32
-    inst = arm_matrix_instance_q15 if kind == "q15" else arm_matrix_instance_q31
+    """(status, C) = A @ B through arm_mat_mult_q15 / _q31 / _fast_q15 / _fast_q31 (kind
+    "q15", "q31", "fast_q15", "fast_q31"; row-major)."""
+    base = kind[-3:]
+    dt = np.int16 if base == "q15" else np.int32
+    inst = arm_matrix_instance_q15 if base == "q15" else arm_matrix_instance_q31
     a = np.ascontiguousarray(a, dtype=dt)
     b = np.ascontiguousarray(b, dtype=dt)
     c = np.zeros((a.shape[0], b.shape[1]), dtype=dt)
     A, B, Cm = inst(), inst(), inst()
-    init = getattr(lib, f"arm_mat_init_{kind}")
+    init = getattr(lib, f"arm_mat_init_{base}")
     init(C.byref(A), a.shape[0], a.shape[1], a.ctypes.data)
     init(C.byref(B), b.shape[0], b.shape[1], b.ctypes.data)
     init(C.byref(Cm), c.shape[0], c.shape[1], c.ctypes.data)
-    if kind == "q15":
-        st = lib.arm_mat_mult_q15(C.byref(A), C.byref(B), C.byref(Cm), None)
-    else:
-        st = lib.arm_mat_mult_q31(C.byref(A), C.byref(B), C.byref(Cm))
+    fn = getattr(lib, f"arm_mat_mult_{kind}")
+    st = fn(C.byref(A), C.byref(B), C.byref(Cm), None) if base == "q15" else fn(C.byref(A), C.byref(B), C.byref(Cm))
     _check_void(f"arm_mat_mult_{kind}")
     return st, c
 
 
-def mat_mult_batch(a, b, c, stream=None):
+def mat_mult_batch(a, b, c, stream=None, fast=False):
     """c[i] = a[i] @ b[i] for device tensors [batch, M, K] x [batch, K, N] -> [batch, M, N];
-    float32 -> arm_mat_mult_f32_batch, int16 -> _q15, int32 -> _q31."""
+    float32 -> arm_mat_mult_f32_batch, int16 -> _q15, int32 -> _q31 (fast=True: _fast_q15 /
+    _fast_q31)."""
     import torch
     batch, m, k = a.shape
     n = b.shape[2]
@@ -428,7 +429,7 @@ def mat_mult_batch(a, b, c, stream=None):
                        torch.int32: ("q31", arm_matrix_instance_q31, _abi.c_i32p)}[a.dtype]
     A, B, Cm = inst(m, k, C.cast(a.data_ptr(), ptr)), inst(k, n, C.cast(b.data_ptr(), ptr)), \
         inst(m, n, C.cast(c.data_ptr(), ptr))
-    fn = getattr(lib, f"arm_mat_mult_{kind}_batch")
+    fn = getattr(lib, f"arm_mat_mult_{'fast_' if fast and kind != 'f32' else ''}{kind}_batch")
     st = fn(C.byref(A), C.byref(B), C.byref(Cm), batch, _stream_ptr(stream))
     if st != ARM_MATH_SUCCESS:
         raise RuntimeError(f"{fn.__name__} -> {st}: {last_error()[1]}")

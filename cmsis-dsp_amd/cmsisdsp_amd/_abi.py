@@ -123,6 +123,10 @@ DROPIN = {
                                    P(arm_matrix_instance_q15), C.c_void_p]),
     "arm_mat_mult_q31": (C.c_int, [P(arm_matrix_instance_q31), P(arm_matrix_instance_q31),
                                    P(arm_matrix_instance_q31)]),
+    "arm_mat_mult_fast_q15": (C.c_int, [P(arm_matrix_instance_q15), P(arm_matrix_instance_q15),
+                                        P(arm_matrix_instance_q15), C.c_void_p]),
+    "arm_mat_mult_fast_q31": (C.c_int, [P(arm_matrix_instance_q31), P(arm_matrix_instance_q31),
+                                        P(arm_matrix_instance_q31)]),
     "arm_conv_f32": (None, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
     "arm_conv_q15": (None, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
     "arm_conv_q31": (None, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
@@ -187,6 +191,10 @@ BATCHED = {
                                          P(arm_matrix_instance_q15), C.c_uint32, C.c_void_p]),
     "arm_mat_mult_q31_batch": (C.c_int, [P(arm_matrix_instance_q31), P(arm_matrix_instance_q31),
                                          P(arm_matrix_instance_q31), C.c_uint32, C.c_void_p]),
+    "arm_mat_mult_fast_q15_batch": (C.c_int, [P(arm_matrix_instance_q15), P(arm_matrix_instance_q15),
+                                              P(arm_matrix_instance_q15), C.c_uint32, C.c_void_p]),
+    "arm_mat_mult_fast_q31_batch": (C.c_int, [P(arm_matrix_instance_q31), P(arm_matrix_instance_q31),
+                                              P(arm_matrix_instance_q31), C.c_uint32, C.c_void_p]),
     **{f"arm_{f}_batch": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
                                     C.c_void_p, C.c_uint32, C.c_void_p]) for f in CONV_FULL},
     **{f"arm_{f}_batch": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,

@@ -434,7 +434,7 @@ bool mat_shapes_ok(const M* a, const M* b, const M* c) {
 
 // drop-in fixed-point matrix multiply (host or device operands), synchronous
 template <typename T, typename M>
-arm_status mat_mult_fixed_sync(const M* pSrcA, const M* pSrcB, M* pDst) {
+arm_status mat_mult_fixed_sync(const M* pSrcA, const M* pSrcB, M* pDst, bool fast = false) {
   if (!pSrcA || !pSrcB || !pDst) return ARM_MATH_ARGUMENT_ERROR;
   if (!mat_shapes_ok(pSrcA, pSrcB, pDst)) return ARM_MATH_SIZE_MISMATCH;
   const int m = pSrcA->numRows, k = pSrcA->numCols, n = pSrcB->numCols;
@@ -449,8 +449,10 @@ arm_status mat_mult_fixed_sync(const M* pSrcA, const M* pSrcB, M* pDst) {
   if (!da && ab) e = hipMemcpyAsync(A, pSrcA->pData, ab, hipMemcpyHostToDevice, st);
   if (e == hipSuccess && !db && bb) e = hipMemcpyAsync(B, pSrcB->pData, bb, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) {
-    if constexpr (sizeof(T) == 2) e = mat_mult_q15_launch(m, k, n, A, B, Cd, 1, st);
-    else e = mat_mult_q31_launch(m, k, n, A, B, Cd, 1, st);
+    if constexpr (sizeof(T) == 2)
+      e = fast ? mat_mult_fast_q15_launch(m, k, n, A, B, Cd, 1, st) : mat_mult_q15_launch(m, k, n, A, B, Cd, 1, st);
+    else
+      e = fast ? mat_mult_fast_q31_launch(m, k, n, A, B, Cd, 1, st) : mat_mult_q31_launch(m, k, n, A, B, Cd, 1, st);
   }
   if (e == hipSuccess && !dc && cb) e = hipMemcpyAsync(pDst->pData, Cd, cb, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -664,6 +666,36 @@ arm_status arm_mat_mult_q15(const arm_matrix_instance_q15* pSrcA, const arm_matr
 arm_status arm_mat_mult_q31(const arm_matrix_instance_q31* pSrcA, const arm_matrix_instance_q31* pSrcB,
                             arm_matrix_instance_q31* pDst) {
   return mat_mult_fixed_sync<int32_t>(pSrcA, pSrcB, pDst);
+}
+// arm_mat_mult_fast_q15.c:351-401 (!ARM_MATH_DSP: q31_t modular sum, (q15)(sum >> 15)),
+// arm_mat_mult_fast_q31.c:152-166 (per-product high word, sum << 1); pState unused (the
+// reference's transpose buffer).
+arm_status arm_mat_mult_fast_q15(const arm_matrix_instance_q15* pSrcA, const arm_matrix_instance_q15* pSrcB,
+                                 arm_matrix_instance_q15* pDst, q15_t* pState) {
+  (void)pState;
+  return mat_mult_fixed_sync<int16_t>(pSrcA, pSrcB, pDst, true);
+}
+arm_status arm_mat_mult_fast_q31(const arm_matrix_instance_q31* pSrcA, const arm_matrix_instance_q31* pSrcB,
+                                 arm_matrix_instance_q31* pDst) {
+  return mat_mult_fixed_sync<int32_t>(pSrcA, pSrcB, pDst, true);
+}
+arm_status arm_mat_mult_fast_q15_batch(const arm_matrix_instance_q15* pSrcA, const arm_matrix_instance_q15* pSrcB,
+                                       arm_matrix_instance_q15* pDst, uint32_t batch, void* stream) {
+  if (!pSrcA || !pSrcB || !pDst) return ARM_MATH_ARGUMENT_ERROR;
+  if (!mat_shapes_ok(pSrcA, pSrcB, pDst)) return ARM_MATH_SIZE_MISMATCH;
+  hipError_t e = mat_mult_fast_q15_launch(pSrcA->numRows, pSrcA->numCols, pSrcB->numCols, pSrcA->pData,
+                                          pSrcB->pData, pDst->pData, batch, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(e, "arm_mat_mult_fast_q15_batch"); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
+}
+arm_status arm_mat_mult_fast_q31_batch(const arm_matrix_instance_q31* pSrcA, const arm_matrix_instance_q31* pSrcB,
+                                       arm_matrix_instance_q31* pDst, uint32_t batch, void* stream) {
+  if (!pSrcA || !pSrcB || !pDst) return ARM_MATH_ARGUMENT_ERROR;
+  if (!mat_shapes_ok(pSrcA, pSrcB, pDst)) return ARM_MATH_SIZE_MISMATCH;
+  hipError_t e = mat_mult_fast_q31_launch(pSrcA->numRows, pSrcA->numCols, pSrcB->numCols, pSrcA->pData,
+                                          pSrcB->pData, pDst->pData, batch, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(e, "arm_mat_mult_fast_q31_batch"); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
 }
 arm_status arm_mat_mult_q15_batch(const arm_matrix_instance_q15* pSrcA, const arm_matrix_instance_q15* pSrcB,
                                   arm_matrix_instance_q15* pDst, uint32_t batch, void* stream) {

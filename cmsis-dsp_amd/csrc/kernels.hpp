@@ -105,5 +105,11 @@ hipError_t mat_mult_q15_launch(int m, int k, int n, const int16_t* a, const int1
                                hipStream_t st);
 hipError_t mat_mult_q31_launch(int m, int k, int n, const int32_t* a, const int32_t* b, int32_t* c, uint32_t batch,
                                hipStream_t st);
+// arm_mat_mult_fast_q15 (exact i8-plane GEMM, modular q31 sum, (q15)(sum >> 15)) and
+// arm_mat_mult_fast_q31 (VALU: sum of per-product (a*b) >> 32, output << 1).
+hipError_t mat_mult_fast_q15_launch(int m, int k, int n, const int16_t* a, const int16_t* b, int16_t* c,
+                                    uint32_t batch, hipStream_t st);
+hipError_t mat_mult_fast_q31_launch(int m, int k, int n, const int32_t* a, const int32_t* b, int32_t* c,
+                                    uint32_t batch, hipStream_t st);
 
 }  // namespace mi355x

@@ -201,7 +201,7 @@ __device__ __forceinline__ uint32_t gather4(uint32_t r0, uint32_t r1, uint32_t r
 // MFMAs); otherwise every load is guarded and zero-filled.
 template <typename T, bool FULL>
 __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict__ A, const T* __restrict__ B,
-                                                             T* __restrict__ C, int M, int K, int N) {
+                                                             T* __restrict__ C, int M, int K, int N, int fast) {
   using G = I8Cfg<T>;
   constexpr int P = Slices<T>::P, S = 2 * P - 1;
   constexpr int64_t C0 = Slices<T>::C0;
@@ -441,7 +441,9 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
         for (int s = 0; s < S; ++s) v += (uint64_t)(int64_t)acc[s][i][j][reg] << (8 * s);
         if (FULL || (grow < M && gcol < N)) {
           const int64_t sum = (int64_t)v;
-          if constexpr (sizeof(T) == 2) C[(size_t)grow * N + gcol] = (T)ssat16((int32_t)(sum >> 15));
+          // fast q15 (arm_mat_mult_fast_q15.c:356-401 host branch): q31_t modular sum, (q15)(sum >> 15)
+          if constexpr (sizeof(T) == 2)
+            C[(size_t)grow * N + gcol] = fast ? (T)((int32_t)(uint32_t)v >> 15) : (T)ssat16((int32_t)(sum >> 15));
           else C[(size_t)grow * N + gcol] = (T)(int32_t)(sum >> 31);
         }
       }
@@ -452,7 +454,8 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
 // K beyond the i8 accumulators' exact range: one thread per output, int64 sum.
 template <typename T>
 __global__ __launch_bounds__(256) void mat_mult_fixed_valu_kernel(const T* __restrict__ A, const T* __restrict__ B,
-                                                                  T* __restrict__ C, int M, int K, int N) {
+                                                                  T* __restrict__ C, int M, int K, int N,
+                                                                  int fast) {
   const size_t bz = blockIdx.z;
   const int i = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
   if (j >= N) return;
@@ -461,15 +464,17 @@ __global__ __launch_bounds__(256) void mat_mult_fixed_valu_kernel(const T* __res
   uint64_t sum = 0;
   for (int k = 0; k < K; ++k) sum += (uint64_t)((int64_t)a[k] * b[(size_t)k * N]);
   const int64_t s = (int64_t)sum;
-  if constexpr (sizeof(T) == 2) C[bz * (size_t)M * N + (size_t)i * N + j] = (T)ssat16((int32_t)(s >> 15));
+  if constexpr (sizeof(T) == 2)
+    C[bz * (size_t)M * N + (size_t)i * N + j] = fast ? (T)((int32_t)(uint32_t)sum >> 15) : (T)ssat16((int32_t)(s >> 15));
   else C[bz * (size_t)M * N + (size_t)i * N + j] = (T)(int32_t)(s >> 31);
 }
 
 template <typename T>
-static hipError_t launch_fixed(int m, int k, int n, const T* a, const T* b, T* c, uint32_t batch, hipStream_t st) {
+static hipError_t launch_fixed(int m, int k, int n, const T* a, const T* b, T* c, uint32_t batch, hipStream_t st,
+                               int fast = 0) {
   if (batch == 0 || m == 0 || n == 0) return hipSuccess;
   if (k == 0) return hipMemsetAsync(c, 0, sizeof(T) * (size_t)m * n * batch, st);
-  if (k <= kMatI8MaxK) {
+  if (k <= kMatI8MaxK && !(MI355X_MATI8_V1 && fast)) {
 #if MI355X_MATI8_V1
     const int tiles = ((m + kMT - 1) / kMT) * ((n + kNT - 1) / kNT);
     hipLaunchKernelGGL(mat_mult_i8_kernel<T>, dim3(tiles, 1, batch), dim3(256), 0, st, a, b, c, m, k, n);
@@ -480,15 +485,85 @@ static hipError_t launch_fixed(int m, int k, int n, const T* a, const T* b, T* c
                       ((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0 && (k * sizeof(T)) % 16 == 0 &&
                       (n * sizeof(T)) % 16 == 0;
     if (full)
-      hipLaunchKernelGGL((mat_mult_i8v2_kernel<T, true>), dim3(tiles * batch), dim3(kNT2), 0, st, a, b, c, m, k, n);
+      hipLaunchKernelGGL((mat_mult_i8v2_kernel<T, true>), dim3(tiles * batch), dim3(kNT2), 0, st, a, b, c, m, k, n,
+                         fast);
     else
-      hipLaunchKernelGGL((mat_mult_i8v2_kernel<T, false>), dim3(tiles * batch), dim3(kNT2), 0, st, a, b, c, m, k, n);
+      hipLaunchKernelGGL((mat_mult_i8v2_kernel<T, false>), dim3(tiles * batch), dim3(kNT2), 0, st, a, b, c, m, k, n,
+                         fast);
 #endif
   } else {
     hipLaunchKernelGGL(mat_mult_fixed_valu_kernel<T>, dim3((n + 255) / 256, m, batch), dim3(256), 0, st, a, b, c,
-                       m, k, n);
+                       m, k, n, fast);
   }
   return hipGetLastError();
+}
+
+// ============================================================================================
+// arm_mat_mult_fast_q31 (arm_mat_mult_fast_q31.c:152-166 / :215-266, !ARM_MATH_DSP):
+// sum = (q31)(((q63)sum << 32 + a*b) >> 32) per product, i.e. sum += (a*b) >> 32 mod 2^32,
+// output sum << 1.  Not an exact-product GEMM (every product is floored on its own), so it
+// runs on the VALU: one v_mul_hi_i32 + one v_add per MAC, 64 x 64 tiles of 256 threads
+// (4 x 4 outputs per thread), 16-deep K steps staged in LDS (A k-major so each thread reads
+// its 4 rows as one 16-B word).
+constexpr int kFQ_T = 64, kFQ_K = 16;
+__global__ __launch_bounds__(256) void mat_mult_fast_q31_kernel(const int32_t* __restrict__ A,
+                                                                const int32_t* __restrict__ B,
+                                                                int32_t* __restrict__ C, int M, int K, int N,
+                                                                int tiles_n) {
+  __shared__ __attribute__((aligned(16))) int32_t As[kFQ_K][kFQ_T + 4];
+  __shared__ __attribute__((aligned(16))) int32_t Bs[kFQ_K][kFQ_T + 4];
+  const int tid = threadIdx.x;
+  const size_t bz = blockIdx.y;
+  const int row0 = (blockIdx.x / tiles_n) * kFQ_T, col0 = (blockIdx.x % tiles_n) * kFQ_T;
+  const int32_t* a = A + bz * (size_t)M * K;
+  const int32_t* b = B + bz * (size_t)K * N;
+  const int tr = (tid / 16) * 4, tc = (tid % 16) * 4;
+  uint32_t acc[4][4] = {};
+  // loaders: A tile 64 x 16 (thread -> row tid/4, k 4*(tid%4) .. +3), B tile 16 x 64
+  const int ar = tid / 4, ak = (tid % 4) * 4;
+  const int bk = tid / 16, bc = (tid % 16) * 4;
+  for (int k0 = 0; k0 < K; k0 += kFQ_K) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int gr = row0 + ar, gk = k0 + ak + u;
+      As[ak + u][ar] = (gr < M && gk < K) ? a[(size_t)gr * K + gk] : 0;
+      const int gk2 = k0 + bk, gc = col0 + bc + u;
+      Bs[bk][bc + u] = (gk2 < K && gc < N) ? b[(size_t)gk2 * N + gc] : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < kFQ_K; ++kk) {
+      const int4 av = *reinterpret_cast<const int4*>(&As[kk][tr]);
+      const int4 bv = *reinterpret_cast<const int4*>(&Bs[kk][tc]);
+      const int32_t ar4[4] = {av.x, av.y, av.z, av.w}, bc4[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += (uint32_t)mulhi(ar4[i], bc4[j]);
+    }
+    __syncthreads();
+  }
+  int32_t* c = C + bz * (size_t)M * N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int gr = row0 + tr + i, gc = col0 + tc + j;
+      if (gr < M && gc < N) c[(size_t)gr * N + gc] = (int32_t)(acc[i][j] << 1);
+    }
+}
+
+hipError_t mat_mult_fast_q31_launch(int m, int k, int n, const int32_t* a, const int32_t* b, int32_t* c,
+                                    uint32_t batch, hipStream_t st) {
+  if (batch == 0 || m == 0 || n == 0) return hipSuccess;
+  const int tn = (n + kFQ_T - 1) / kFQ_T, tm = (m + kFQ_T - 1) / kFQ_T;
+  if (batch > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mat_mult_fast_q31_kernel, dim3(tm * tn, batch), dim3(256), 0, st, a, b, c, m, k, n, tn);
+  return hipGetLastError();
+}
+hipError_t mat_mult_fast_q15_launch(int m, int k, int n, const int16_t* a, const int16_t* b, int16_t* c,
+                                    uint32_t batch, hipStream_t st) {
+  return launch_fixed<int16_t>(m, k, n, a, b, c, batch, st, 1);
 }
 
 hipError_t mat_mult_q15_launch(int m, int k, int n, const int16_t* a, const int16_t* b, int16_t* c, uint32_t batch,

@@ -405,6 +405,14 @@ arm_status arm_mat_mult_q15(const arm_matrix_instance_q15 *pSrcA, const arm_matr
                             arm_matrix_instance_q15 *pDst, q15_t *pState);
 arm_status arm_mat_mult_q31(const arm_matrix_instance_q31 *pSrcA, const arm_matrix_instance_q31 *pSrcB,
                             arm_matrix_instance_q31 *pDst);
+/* Fast fixed-point matrix multiply (matrix_functions.h:431-435,484-487):
+ * arm_mat_mult_fast_q15.c (!ARM_MATH_DSP): q31_t modular sum of q15 products, (q15)(sum >> 15);
+ * arm_mat_mult_fast_q31.c: sum = (q31)(((q63)sum << 32 + a*b) >> 32) per product, output
+ * sum << 1.  pState (the reference's transpose buffer) is not used. */
+arm_status arm_mat_mult_fast_q15(const arm_matrix_instance_q15 *pSrcA, const arm_matrix_instance_q15 *pSrcB,
+                                 arm_matrix_instance_q15 *pDst, q15_t *pState);
+arm_status arm_mat_mult_fast_q31(const arm_matrix_instance_q31 *pSrcA, const arm_matrix_instance_q31 *pSrcB,
+                                 arm_matrix_instance_q31 *pDst);
 
 #ifdef __cplusplus
 }

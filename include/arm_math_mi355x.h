@@ -135,6 +135,10 @@ arm_status arm_mat_mult_q15_batch(const arm_matrix_instance_q15 *pSrcA, const ar
                                   arm_matrix_instance_q15 *pDst, uint32_t batch, void *stream);
 arm_status arm_mat_mult_q31_batch(const arm_matrix_instance_q31 *pSrcA, const arm_matrix_instance_q31 *pSrcB,
                                   arm_matrix_instance_q31 *pDst, uint32_t batch, void *stream);
+arm_status arm_mat_mult_fast_q15_batch(const arm_matrix_instance_q15 *pSrcA, const arm_matrix_instance_q15 *pSrcB,
+                                       arm_matrix_instance_q15 *pDst, uint32_t batch, void *stream);
+arm_status arm_mat_mult_fast_q31_batch(const arm_matrix_instance_q31 *pSrcA, const arm_matrix_instance_q31 *pSrcB,
+                                       arm_matrix_instance_q31 *pDst, uint32_t batch, void *stream);
 
 /* Error channel for the void-returning drop-in functions: 0 = no error, otherwise the
  * hipError_t of the last failure on this thread. */

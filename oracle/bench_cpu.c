@@ -177,8 +177,8 @@ static void *worker(void *arg) {
       samples += n;
     } while (now() - t0 < j->seconds);
     free(coefs); free(win); free(x); free(src); free(tmp);
-  } else if (!strcmp(j->wl, "mat_mult_q15") || !strcmp(j->wl, "mat_mult_q31")) {
-    const int d = j->n, q15 = !strcmp(j->wl, "mat_mult_q15");
+  } else if (!strcmp(j->wl, "mat_mult_q15") || !strcmp(j->wl, "mat_mult_q31") || !strcmp(j->wl, "mat_mult_fast_q31")) {
+    const int d = j->n, q15 = !strcmp(j->wl, "mat_mult_q15"), fast = !strcmp(j->wl, "mat_mult_fast_q31");
     int16_t *a16 = malloc(2 * d * d), *b16 = malloc(2 * d * d), *o16 = malloc(2 * d * d), *st16 = malloc(2 * d * d);
     int32_t *a32 = malloc(4 * d * d), *b32 = malloc(4 * d * d), *o32 = malloc(4 * d * d);
     for (int i = 0; i < d * d; ++i) { a16[i] = (int16_t)sm(&seed); b16[i] = (int16_t)sm(&seed); a32[i] = (int32_t)sm(&seed); b32[i] = (int32_t)sm(&seed); }
@@ -187,7 +187,9 @@ static void *worker(void *arg) {
     F(arm_mat_init_q15)(&A15, d, d, a16); F(arm_mat_init_q15)(&B15, d, d, b16); F(arm_mat_init_q15)(&O15, d, d, o16);
     F(arm_mat_init_q31)(&A31, d, d, a32); F(arm_mat_init_q31)(&B31, d, d, b32); F(arm_mat_init_q31)(&O31, d, d, o32);
     do {
-      if (q15) F(arm_mat_mult_q15)(&A15, &B15, &O15, st16); else F(arm_mat_mult_q31)(&A31, &B31, &O31);
+      if (q15) F(arm_mat_mult_q15)(&A15, &B15, &O15, st16);
+      else if (fast) F(arm_mat_mult_fast_q31)(&A31, &B31, &O31);
+      else F(arm_mat_mult_q31)(&A31, &B31, &O31);
       samples += (double)d * d; j->flops += 2.0 * d * d * d;
     } while (now() - t0 < j->seconds);
     free(a16); free(b16); free(o16); free(st16); free(a32); free(b32); free(o32);

@@ -24,6 +24,10 @@ arm_status oracle_arm_mat_mult_q15(const arm_matrix_instance_q15 *A, const arm_m
                                    arm_matrix_instance_q15 *C, int16_t *pState);
 arm_status oracle_arm_mat_mult_q31(const arm_matrix_instance_q31 *A, const arm_matrix_instance_q31 *B,
                                    arm_matrix_instance_q31 *C);
+arm_status oracle_arm_mat_mult_fast_q15(const arm_matrix_instance_q15 *A, const arm_matrix_instance_q15 *B,
+                                        arm_matrix_instance_q15 *C, int16_t *pState);
+arm_status oracle_arm_mat_mult_fast_q31(const arm_matrix_instance_q31 *A, const arm_matrix_instance_q31 *B,
+                                        arm_matrix_instance_q31 *C);
 void oracle_arm_conv_f32(const float *pSrcA, uint32_t srcALen, const float *pSrcB, uint32_t srcBLen, float *pDst);
 void oracle_arm_conv_q15(const int16_t *pSrcA, uint32_t srcALen, const int16_t *pSrcB, uint32_t srcBLen, int16_t *pDst);
 void oracle_arm_conv_q31(const int32_t *pSrcA, uint32_t srcALen, const int32_t *pSrcB, uint32_t srcBLen, int32_t *pDst);

@@ -146,6 +146,33 @@ arm_status oracle_arm_mat_mult_q31(const arm_matrix_instance_q31 *A, const arm_m
   return ARM_MATH_SUCCESS;
 }
 
+/* arm_mat_mult_fast_q15.c:351-401 (!ARM_MATH_DSP): q31_t sum += a*b (wrapping), output
+ * (q15)(sum >> 15) -- truncation, no saturation.  arm_mat_mult_fast_q31.c:152-166, :215-266:
+ * sum = (q31)(((q63)sum << 32 + (q63)a*b) >> 32) per product (= sum + ((a*b) >> 32) mod 2^32),
+ * output sum << 1. */
+arm_status oracle_arm_mat_mult_fast_q15(const arm_matrix_instance_q15 *A, const arm_matrix_instance_q15 *B,
+                                        arm_matrix_instance_q15 *Cm, int16_t *pState) {
+  const uint32_t M = A->numRows, K = A->numCols, N = B->numCols;
+  for (uint32_t i = 0; i < M; ++i)
+    for (uint32_t j = 0; j < N; ++j) {
+      uint32_t sum = 0;
+      for (uint32_t k = 0; k < K; ++k) sum += (uint32_t)((int32_t)A->pData[i * K + k] * B->pData[k * N + j]);
+      Cm->pData[i * N + j] = (int16_t)((int32_t)sum >> 15);
+    }
+  return ARM_MATH_SUCCESS;
+}
+arm_status oracle_arm_mat_mult_fast_q31(const arm_matrix_instance_q31 *A, const arm_matrix_instance_q31 *B,
+                                        arm_matrix_instance_q31 *Cm) {
+  const uint32_t M = A->numRows, K = A->numCols, N = B->numCols;
+  for (uint32_t i = 0; i < M; ++i)
+    for (uint32_t j = 0; j < N; ++j) {
+      uint32_t sum = 0;
+      for (uint32_t k = 0; k < K; ++k) sum += (uint32_t)(int32_t)(((int64_t)A->pData[i * K + k] * B->pData[k * N + j]) >> 32);
+      Cm->pData[i * N + j] = (int32_t)(sum << 1);
+    }
+  return ARM_MATH_SUCCESS;
+}
+
 /* arm_conv_f32.c / arm_conv_q15.c (!ARM_MATH_DSP) / arm_conv_q31.c: y[n] = sum over the
  * overlap of a[k]*b[n-k] with k (index of pSrcA) ASCENDING whichever input is longer
  * (the reference's internal swap of the two inputs does not change that order; checked

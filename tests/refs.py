@@ -137,22 +137,23 @@ class Host:
         return y, 0
 
     def mat_mult_fixed(self, kind, a, b):
-        """arm_mat_mult_q15 / _q31: returns (status, C)."""
-        dt = np.int16 if kind == "q15" else np.int32
-        inst = _abi.arm_matrix_instance_q15 if kind == "q15" else _abi.arm_matrix_instance_q31
+        """arm_mat_mult_q15 / _q31 / _fast_q15 / _fast_q31: returns (status, C)."""
+        base = kind[-3:]
+        dt = np.int16 if base == "q15" else np.int32
+        inst = _abi.arm_matrix_instance_q15 if base == "q15" else _abi.arm_matrix_instance_q31
         a = np.ascontiguousarray(a, dtype=dt)
         b = np.ascontiguousarray(b, dtype=dt)
         c = np.zeros((a.shape[0], b.shape[1]), dtype=dt)
         A, B, Cm = inst(), inst(), inst()
-        init = self.fn(f"arm_mat_init_{kind}")
+        init = self.fn(f"arm_mat_init_{base}")
         init(C.byref(A), a.shape[0], a.shape[1], a.ctypes.data)
         init(C.byref(B), b.shape[0], b.shape[1], b.ctypes.data)
         init(C.byref(Cm), c.shape[0], c.shape[1], c.ctypes.data)
-        if kind == "q15":
+        if base == "q15":
             state = np.zeros(a.shape[1] * b.shape[1] + 16, dtype=np.int16)
-            st = self.fn("arm_mat_mult_q15")(C.byref(A), C.byref(B), C.byref(Cm), state.ctypes.data)
+            st = self.fn(f"arm_mat_mult_{kind}")(C.byref(A), C.byref(B), C.byref(Cm), state.ctypes.data)
         else:
-            st = self.fn("arm_mat_mult_q31")(C.byref(A), C.byref(B), C.byref(Cm))
+            st = self.fn(f"arm_mat_mult_{kind}")(C.byref(A), C.byref(B), C.byref(Cm))
         return st, c
 
     def mat_mult(self, a, b):

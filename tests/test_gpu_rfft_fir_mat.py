@@ -226,7 +226,7 @@ def test_mat_mult_batch_normwise(dsp, torch_gpu, ref, m, k, n, batch):
 
 
 # ------------------------------------------------------------------ mat mult q15 / q31
-@pytest.mark.parametrize("kind", ["q15", "q31"])
+@pytest.mark.parametrize("kind", ["q15", "q31", "fast_q15", "fast_q31"])
 @pytest.mark.parametrize("m,k,n,fill", [(1, 1, 1, None), (5, 7, 3, None), (64, 64, 64, None), (65, 130, 67, None),
                                         (128, 2000, 96, None), (40, 64, 40, "min"), (40, 64, 40, "max"),
                                         (33, 100, 31, "mixed"), (3, 33000, 2, None),
@@ -235,8 +235,9 @@ def test_mat_mult_batch_normwise(dsp, torch_gpu, ref, m, k, n, batch):
                                         (256, 64, 128, "max")])
 def test_mat_mult_fixed_bitexact(dsp, torch_gpu, ref, kind, m, k, n, fill):
     """Byte-sliced i8-MFMA kernel (K <= 32704) and the VALU kernel beyond, vs the reference
-    build bit for bit, including all-extreme operands (q63 wrap for q31, saturation for q15)."""
-    bits, dt = (15, np.int16) if kind == "q15" else (31, np.int32)
+    build bit for bit, including all-extreme operands (q63 wrap for q31, saturation for q15);
+    fast_q15 on the same kernels with the modular epilogue, fast_q31 on its VALU kernel."""
+    bits, dt = (15, np.int16) if kind.endswith("q15") else (31, np.int32)
     rng = np.random.default_rng(m + 7 * k + 13 * n)
     lo, hi = -(1 << bits), (1 << bits) - 1
     if fill is None:
@@ -254,17 +255,17 @@ def test_mat_mult_fixed_bitexact(dsp, torch_gpu, ref, kind, m, k, n, fill):
     assert got.tobytes() == want.tobytes(), np.argwhere(got != want)[:5]
 
 
-@pytest.mark.parametrize("kind", ["q15", "q31"])
+@pytest.mark.parametrize("kind", ["q15", "q31", "fast_q15", "fast_q31"])
 def test_mat_mult_fixed_batch(dsp, torch_gpu, ref, kind):
-    bits, dt = (15, np.int16) if kind == "q15" else (31, np.int32)
-    tdt = torch_gpu.int16 if kind == "q15" else torch_gpu.int32
+    bits, dt = (15, np.int16) if kind.endswith("q15") else (31, np.int32)
+    tdt = torch_gpu.int16 if kind.endswith("q15") else torch_gpu.int32
     rng = np.random.default_rng(9)
     for (m, k, n) in ((96, 200, 80), (128, 256, 128)):        # guarded and unguarded kernels
         a = rng.integers(-(1 << bits), 1 << bits, (3, m, k)).astype(dt)
         b = rng.integers(-(1 << bits), 1 << bits, (3, k, n)).astype(dt)
         A, B = torch_gpu.from_numpy(a).cuda(), torch_gpu.from_numpy(b).cuda()
         Cm = torch_gpu.empty((3, m, n), dtype=tdt, device="cuda")
-        dsp.mat_mult_batch(A, B, Cm)
+        dsp.mat_mult_batch(A, B, Cm, fast=kind.startswith("fast"))
         got = Cm.cpu().numpy()
         for i in range(3):
             assert got[i].tobytes() == ref.mat_mult_fixed(kind, a[i], b[i])[1].tobytes(), (m, i)

@@ -122,3 +122,20 @@ def test_mat_mult_fixed_oracle_equals_reference(oracle, ref, kind, m, k, n, fill
 def test_conv_oracle_equals_reference(oracle, ref, kind, la, lb):
     c, xs = fir_case(kind, lb, [la], la * 13 + lb)
     assert oracle.conv(kind, xs[0], c).tobytes() == ref.conv(kind, xs[0], c).tobytes()
+
+
+@pytest.mark.parametrize("kind", ["fast_q15", "fast_q31"])
+@pytest.mark.parametrize("m,k,n", [(1, 1, 1), (2, 3, 4), (5, 7, 3), (16, 16, 16), (33, 17, 9), (8, 100, 5)])
+def test_mat_mult_fast_oracle_equals_reference(oracle, ref, kind, m, k, n):
+    """arm_mat_mult_fast_q15 / _q31 (modular sums; odd shapes hit the reference's 2x2-block
+    remainder loops), full-range and all-minimum inputs."""
+    rng = np.random.default_rng(m * 100 + k * 10 + n)
+    dt, bits = (np.int16, 15) if kind.endswith("q15") else (np.int32, 31)
+    for fill in (None, "min"):
+        if fill is None:
+            a = rng.integers(-(1 << bits), 1 << bits, (m, k)).astype(dt)
+            b = rng.integers(-(1 << bits), 1 << bits, (k, n)).astype(dt)
+        else:
+            a, b = np.full((m, k), -(1 << bits), dt), np.full((k, n), -(1 << bits), dt)
+        (sa, ca), (sb, cb) = oracle.mat_mult_fixed(kind, a, b), ref.mat_mult_fixed(kind, a, b)
+        assert sa == sb == 0 and ca.tobytes() == cb.tobytes(), fill
