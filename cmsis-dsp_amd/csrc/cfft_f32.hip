@@ -270,6 +270,289 @@ __global__ __launch_bounds__(64 * kN1024Wpb, MI355X_N1024_WAVES) void cfft_f32_n
   }
 }
 
+// ============================================================================================
+// N = 4096 specialist.  The reference runs four radix-8 DIF stages (arm_cfft_f32.c:1278,
+// arm_radix8_butterfly_f32 with modifier 1: strides 512, 64, 8, 1) and the base-8 digit
+// reversal.  One 256-thread workgroup per transform, persistent, the next transform's 16
+// loads in flight under passes 2-4; every thread runs two radix-8 butterflies per stage:
+//   pass 1 (registers, from HBM): butterflies j = t + 256a of stage 0, elements j + 512m
+//          (each load instruction covers 512 consecutive bytes per wave);
+//   pass 2: stage 1, butterfly (block (t>>6) + 4a, j = t & 63), elements 512blk + j + 64m;
+//   pass 3: stage 2, butterfly (block (t>>3) + 32a, j = t & 7),  elements 64blk + j + 8m;
+//   pass 4: stage 3, butterfly q = rev3(t + 256a) (octal digit reversal), elements 8q + m:
+//          output m of that butterfly is frequency 512m + t + 256a, so each store
+//          instruction writes 512 consecutive bytes per wave -- the reversal costs nothing.
+// Stage twiddles depend only on the lane (j) and stay in 56 VGPRs for the kernel's life;
+// the j == 0 groups (no twiddle multiply in the reference) are selected, not branched.
+// LDS image s(e) = e + 8(e>>6) + (e>>9): every access pattern above is bank-conflict free
+// (modelled with the ds_read_b64 / ds_write_b64 banking of MI355X_MICROARCH.md §LDS) and
+// additive, so the eight accesses of a butterfly are one base + immediate offsets.
+__device__ __forceinline__ int s4096f(int e) { return e + 8 * (e >> 6) + (e >> 9); }
+__device__ __forceinline__ int rev3o(int t) { return ((t & 7) << 6) | (((t >> 3) & 7) << 3) | (t >> 6); }
+
+#ifndef MI355X_N4096_WAVES
+#define MI355X_N4096_WAVES 1
+#endif
+#ifndef MI355X_N4096_T
+#define MI355X_N4096_T 0
+#endif
+constexpr uint32_t kN4096T = MI355X_N4096_T;
+__global__ __launch_bounds__(256, MI355X_N4096_WAVES) void cfft_f32_n4096_kernel(float2* __restrict__ data, uint32_t batch,
+                                                             const float2* __restrict__ tw, uint32_t flags) {
+  __shared__ __attribute__((aligned(16))) float2 lds[4607];
+  const int t = threadIdx.x;
+  const bool ifft = flags & kIfft;
+  const bool brev = flags & kBitrev;
+  const float invL = 1.0f / 4096.0f;
+  const int j1 = t & 63, j2 = t & 7;
+  float2 w0[2][7], w1[7], w2[7];
+#pragma unroll
+  for (int m = 0; m < 7; ++m) {
+    w0[0][m] = tw[(m + 1) * t];
+    w0[1][m] = tw[(m + 1) * (t + 256)];
+    w1[m] = tw[(m + 1) * j1 * 8];
+    w2[m] = tw[(m + 1) * j2 * 64];
+  }
+  // work mapping: MI355X_N4096_T = 0 persistent grid-stride walk; T > 0: workgroup b takes
+  // the T consecutive transforms bT .. bT+T-1
+  const uint32_t tr_begin = kN4096T ? blockIdx.x * kN4096T : blockIdx.x;
+  const uint32_t tr_end = kN4096T ? min(batch, tr_begin + kN4096T) : batch;
+  const uint32_t tr_step = kN4096T ? 1u : gridDim.x;
+  float2 v[2][8], nv[2][8];
+  if (tr_begin < tr_end) {
+    const float2* X0 = data + (size_t)tr_begin * 4096;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int m = 0; m < 8; ++m) nv[a][m] = ldnt(&X0[t + 256 * a + 512 * m]);
+  }
+  for (uint32_t tr = tr_begin; tr < tr_end; tr += tr_step) {
+    float2* X = data + (size_t)tr * 4096;
+    // ---------------- pass 1: stage 0 (modifier 1)
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int m = 0; m < 8; ++m) v[a][m] = ifft ? make_float2(nv[a][m].x, -nv[a][m].y) : nv[a][m];
+      r8_sel(v[a], w0[a], t + 256 * a != 0);
+    }
+    __syncthreads();                    // the previous transform's pass-4 reads are done
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int m = 0; m < 8; ++m) lds[s4096f(t + 256 * a + 512 * m)] = v[a][m];
+    if (tr + tr_step < tr_end) {        // next transform's loads fly under passes 2-4
+      const float2* XN = data + (size_t)(tr + tr_step) * 4096;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int m = 0; m < 8; ++m) nv[a][m] = ldnt(&XN[t + 256 * a + 512 * m]);
+    }
+    __syncthreads();
+    // ---------------- pass 2: stage 1 (modifier 8)
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int base = 512 * ((t >> 6) + 4 * a) + j1;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) v[a][m] = lds[s4096f(base + 64 * m)];
+      r8_sel(v[a], w1, j1 != 0);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) lds[s4096f(base + 64 * m)] = v[a][m];
+    }
+    __syncthreads();
+    // ---------------- pass 3: stage 2 (modifier 64)
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int base = 64 * ((t >> 3) + 32 * a) + j2;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) v[a][m] = lds[s4096f(base + 8 * m)];
+      r8_sel(v[a], w2, j2 != 0);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) lds[s4096f(base + 8 * m)] = v[a][m];
+    }
+    __syncthreads();
+    // ---------------- pass 4: stage 3 (no twiddles) + digit reversal folded into the store
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int q = rev3o(t + 256 * a);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) v[a][m] = lds[s4096f(8 * q + m)];
+      r8_core(v[a]);
+      if (ifft) {                       // arm_cfft_f32.c:1285-1297
+#pragma unroll
+        for (int m = 0; m < 8; ++m) v[a][m] = make_float2(v[a][m].x * invL, -v[a][m].y * invL);
+      }
+      if (brev) {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const v2f o = {v[a][m].x, v[a][m].y};
+          __builtin_nontemporal_store(o, reinterpret_cast<v2f*>(&X[512 * m + t + 256 * a]));
+        }
+      } else {
+        float4* Y = reinterpret_cast<float4*>(X + 8 * q);
+#pragma unroll
+        for (int m = 0; m < 8; m += 2) Y[m >> 1] = make_float4(v[a][m].x, v[a][m].y, v[a][m + 1].x, v[a][m + 1].y);
+      }
+    }
+  }
+}
+
+#ifndef MI355X_F32_N4096
+#define MI355X_F32_N4096 1
+#endif
+
+// ============================================================================================
+// N = 2048 specialist.  Reference: arm_cfft_radix8by4_f32 (arm_cfft_f32.c:992-1188; rows
+// k <= N/8 "top", the others "bottom" with the mirrored twiddle index i = N/4 - k), then
+// 3 radix-8 stages on each 512-point quarter (modifier 4: strides 64, 8, 1), then the
+// mixed-radix [4, 8, 8, 8] digit reversal.  One wave per transform, as the N = 1024
+// kernel, with 32 complex per lane:
+//   phase A (registers): lane l loads x[l + 64m + 512c] (m, c: 32 loads of 512 B per
+//            wave), runs the radix-4 pass on its eight rows k = l + 64m, then stage 0 of
+//            all four quarters, whose butterflies are exactly {512c + l + 64m};
+//   phase B (LDS): stage 1, quarter c, butterfly (l >> 3, j = l & 7);
+//   phase C (LDS): stage 2, butterfly r = 0..3 of lane l is (c, p) = (l & 3,
+//            8((l >> 2) & 7) + (l >> 5) + 2r), whose output m is frequency
+//            c + 4(p >> 3) + 32(p & 7) + 256m = l + 64r + 256m: 512 consecutive bytes per
+//            store instruction, the reversal costs nothing.
+// LDS image (per wave) s(e) = e + 8(e >> 6) + (e >> 8): conflict free and additive for all
+// three patterns (same banking model as the N = 4096 kernel).
+__device__ __forceinline__ int s2048(int e) { return e + 8 * (e >> 6) + (e >> 8); }
+
+// radix8by4 top row (k <= N/8; k == 0 leaves the three products out), :1005-1060
+__device__ __forceinline__ void by4_top(float2& A, float2& B, float2& C, float2& D, float2 w2, float2 w3, float2 w4,
+                                        bool tw) {
+  const float ap0 = A.x + C.x, as0 = A.x - C.x, ap1 = A.y + C.y, as1 = A.y - C.y;
+  const float2 t2 = make_float2(as0 + B.y - D.y, as1 - B.x + D.x);
+  const float2 t3 = make_float2(ap0 - B.x - D.x, ap1 - B.y - D.y);
+  const float2 t4 = make_float2(as0 - B.y + D.y, as1 + B.x - D.x);
+  A = make_float2(ap0 + B.x + D.x, ap1 + B.y + D.y);
+  const float2 m2 = make_float2(t2.x * w2.x + t2.y * w2.y, t2.y * w2.x - t2.x * w2.y);
+  const float2 m3 = make_float2(t3.x * w3.x + t3.y * w3.y, t3.y * w3.x - t3.x * w3.y);
+  const float2 m4 = make_float2(t4.x * w4.x + t4.y * w4.y, t4.y * w4.x - t4.x * w4.y);
+  B = tw ? m2 : t2; C = tw ? m3 : t3; D = tw ? m4 : t4;
+}
+// radix8by4 bottom row kb = N/4 - i (twiddles tw[i], tw[2i], tw[3i]), :1061-1110
+__device__ __forceinline__ void by4_bot(float2& A, float2& B, float2& C, float2& D, float2 w2, float2 w3, float2 w4) {
+  const float ap1 = A.x + C.x, as1 = A.x - C.x, ap0 = A.y + C.y, as0 = A.y - C.y;
+  const float t22 = B.y - D.y + as1;
+  const float t23 = A.y - C.y - B.x + D.x;
+  const float t32 = ap1 - B.x - D.x;
+  const float t33 = ap0 - B.y - D.y;
+  const float t42 = B.y - D.y - as1;
+  const float t43 = D.x - B.x - as0;
+  A = make_float2(ap1 + B.x + D.x, ap0 + B.y + D.y);
+  B = make_float2(t22 * w2.y + t23 * w2.x, t23 * w2.y - t22 * w2.x);
+  C = make_float2(t33 * w3.y - t32 * w3.x, -t33 * w3.x - t32 * w3.y);
+  D = make_float2(t42 * w4.y + t43 * w4.x, t43 * w4.y - t42 * w4.x);
+}
+
+#ifndef MI355X_N2048_T
+#define MI355X_N2048_T 4
+#endif
+#ifndef MI355X_N2048_WPB
+#define MI355X_N2048_WPB 4
+#endif
+#ifndef MI355X_F32_N2048
+#define MI355X_F32_N2048 1
+#endif
+constexpr int kN2048T = MI355X_N2048_T, kN2048Wpb = MI355X_N2048_WPB;
+
+__global__ __launch_bounds__(64 * kN2048Wpb) void cfft_f32_n2048_kernel(float2* __restrict__ data, uint32_t batch,
+                                                                       const float2* __restrict__ tw,
+                                                                       uint32_t flags) {
+  __shared__ __attribute__((aligned(16))) float2 lds_all[kN2048Wpb][2303];
+  const int l = threadIdx.x & 63;
+  float2* lds = lds_all[threadIdx.x >> 6];
+  const uint32_t wave = blockIdx.x * kN2048Wpb + (threadIdx.x >> 6);
+  const uint32_t t_begin = wave * kN2048T;
+  const uint32_t t_end = min(batch, t_begin + kN2048T);
+  const bool ifft = flags & kIfft;
+  const bool brev = flags & kBitrev;
+  const float invL = 1.0f / 2048.0f;
+  // lane-constant twiddles: radix8by4 rows k = l + 64m (index k for top rows, 512 - k for
+  // bottom rows), stage 0 (j = l, modifier 4), stage 1 (j = l & 7, modifier 32)
+  float2 wq[8][3], w0[7], w1[7];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int k = l + 64 * m, i = k <= 256 ? k : 512 - k;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) wq[m][u] = tw[(u + 1) * i];
+  }
+  const int j1 = l & 7;
+#pragma unroll
+  for (int m = 0; m < 7; ++m) { w0[m] = tw[4 * (m + 1) * l]; w1[m] = tw[32 * (m + 1) * j1]; }
+
+  float2 R[4][8];
+  for (uint32_t t = t_begin; t < t_end; ++t) {
+    float2* X = data + (size_t)t * 2048;
+    // ---------------- phase A: radix-4 pass on rows l + 64m, stage 0 of the four quarters
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const float2 x = ldnt(&X[l + 64 * m + 512 * c]);
+        R[c][m] = ifft ? make_float2(x.x, -x.y) : x;
+      }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      if (m < 4) {
+        by4_top(R[0][m], R[1][m], R[2][m], R[3][m], wq[m][0], wq[m][1], wq[m][2], m != 0 || l != 0);
+      } else if (m > 4) {
+        by4_bot(R[0][m], R[1][m], R[2][m], R[3][m], wq[m][0], wq[m][1], wq[m][2]);
+      } else {                          // k = 256 + l: top for l == 0 (the middle row), else bottom
+        float2 a = R[0][m], b = R[1][m], c = R[2][m], d = R[3][m];
+        by4_top(a, b, c, d, wq[m][0], wq[m][1], wq[m][2], true);
+        by4_bot(R[0][m], R[1][m], R[2][m], R[3][m], wq[m][0], wq[m][1], wq[m][2]);
+        if (l == 0) { R[0][m] = a; R[1][m] = b; R[2][m] = c; R[3][m] = d; }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) r8_sel(R[c], w0, l != 0);
+    wave_sync();                        // previous transform's phase C reads are done
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int m = 0; m < 8; ++m) lds[s2048(512 * c + l + 64 * m)] = R[c][m];
+    wave_sync();
+    // ---------------- phase B: stage 1
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int base = 512 * c + 64 * (l >> 3) + j1;
+      float2 v[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) v[m] = lds[s2048(base + 8 * m)];
+      r8_sel(v, w1, j1 != 0);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) lds[s2048(base + 8 * m)] = v[m];
+    }
+    wave_sync();
+    // ---------------- phase C: stage 2 + digit reversal folded into the store
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = l & 3, p = 8 * ((l >> 2) & 7) + (l >> 5) + 2 * r;
+      float2 v[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) v[m] = lds[s2048(512 * c + 8 * p + m)];
+      r8_core(v);
+      if (ifft) {                       // arm_cfft_f32.c:1285-1297
+#pragma unroll
+        for (int m = 0; m < 8; ++m) v[m] = make_float2(v[m].x * invL, -v[m].y * invL);
+      }
+      if (brev) {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const v2f o = {v[m].x, v[m].y};
+          __builtin_nontemporal_store(o, reinterpret_cast<v2f*>(&X[l + 64 * r + 256 * m]));
+        }
+      } else {
+        float4* Y = reinterpret_cast<float4*>(X + 512 * c + 8 * p);
+#pragma unroll
+        for (int m = 0; m < 8; m += 2) Y[m >> 1] = make_float4(v[m].x, v[m].y, v[m + 1].x, v[m + 1].y);
+      }
+    }
+  }
+}
+
 template <int N>
 static hipError_t launch_f32(float2* data, uint32_t batch, const float2* tw, const uint16_t* perm,
                              uint32_t flags, hipStream_t st) {
@@ -300,8 +583,22 @@ hipError_t cfft_f32_launch(int n, float* data, uint32_t batch, const float* tw, 
         return hipGetLastError();
       }
       return launch_f32<1024>(d, batch, w, perm, flags, st);
-    case 2048: return launch_f32<2048>(d, batch, w, perm, flags, st);
-    case 4096: return launch_f32<4096>(d, batch, w, perm, flags, st);
+    case 2048:
+      if (!perm && MI355X_F32_N2048) {
+        const int per_block = kN2048T * kN2048Wpb;
+        const int grid = (int)((batch + per_block - 1) / per_block);
+        hipLaunchKernelGGL(cfft_f32_n2048_kernel, dim3(grid), dim3(64 * kN2048Wpb), 0, st, d, batch, w, flags);
+        return hipGetLastError();
+      }
+      return launch_f32<2048>(d, batch, w, perm, flags, st);
+    case 4096:
+      if (!perm && MI355X_F32_N4096) {   // the reference's own table: the specialist kernel
+        const int grid = kN4096T ? (int)((batch + kN4096T - 1) / kN4096T)
+                                 : persistent_grid((const void*)cfft_f32_n4096_kernel, 256, 0, batch);
+        hipLaunchKernelGGL(cfft_f32_n4096_kernel, dim3(grid), dim3(256), 0, st, d, batch, w, flags);
+        return hipGetLastError();
+      }
+      return launch_f32<4096>(d, batch, w, perm, flags, st);
     default:   return hipSuccess;  // reference: unsupported length is a silent no-op
   }
 }
