@@ -447,7 +447,7 @@ __device__ __forceinline__ void by4_bot(float2& A, float2& B, float2& C, float2&
 }
 
 #ifndef MI355X_N2048_T
-#define MI355X_N2048_T 4
+#define MI355X_N2048_T 2
 #endif
 #ifndef MI355X_N2048_WPB
 #define MI355X_N2048_WPB 4

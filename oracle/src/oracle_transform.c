@@ -358,7 +358,7 @@ void oracle_arm_cfft_q15(const arm_cfft_instance_q15 *S, int16_t *p1, uint8_t if
       }
       q15_radix4(w, h, S->pTwiddle, 2, inv);
       q15_radix4(w + h, h, S->pTwiddle, 2, inv);
-      for (uint32_t i = 0; i < n; ++i) { w[i].re = tr16(w[i].re << 1); w[i].im = tr16(w[i].im << 1); }
+      for (uint32_t i = 0; i < n; ++i) { w[i].re = tr16(wshl1(w[i].re)); w[i].im = tr16(wshl1(w[i].im)); }
     } else {
       q15_radix4(w, n, S->pTwiddle, 1, inv);
     }
@@ -463,7 +463,7 @@ void oracle_arm_rfft_q15(const arm_rfft_instance_q15 *S, int16_t *pSrc, int16_t 
       pDst[2 * k] = (int16_t)re; pDst[2 * k + 1] = (int16_t)(im >> 16);
     }
     oracle_arm_cfft_q15(S->pCfft, pDst, 1, S->bitReverseFlagR);
-    for (uint32_t i = 0; i < n; ++i) pDst[i] = (int16_t)sat16((int32_t)pDst[i] << 1);
+    for (uint32_t i = 0; i < n; ++i) pDst[i] = (int16_t)sat16((int32_t)pDst[i] * 2);   /* << 1 without UB */
   } else {
     oracle_arm_cfft_q15(S->pCfft, pSrc, S->ifftFlagR, S->bitReverseFlagR);
     for (uint32_t k = 1; k < L; ++k) {
