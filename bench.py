@@ -449,8 +449,11 @@ def main():
                            "fir_fast_q31": "q31 (rounded high-word accumulator)", "rfft": "f32", "conv": "f32",
                            "rfftq31": "q31 (int32)", "rfftq15": "q15 (int16)"}[kind])
         if args.workload.startswith("cfft"):
+            cfg_tag = ("BASELINE configs[1]" if (kind == "f32" and n == 1024) else
+                       "BASELINE configs[3]" if (kind != "f32" and n == 4096) else
+                       "size sweep, not a BASELINE config")
             line["config"] = {"workload": f"arm_cfft_{kind} N={n} batch={batch}/GPU in place, bitReverseFlag=1, "
-                                          f"alternating fwd/inv (BASELINE configs[{1 if kind == 'f32' else 3}])",
+                                          f"alternating fwd/inv ({cfg_tag})",
                               "fftLen": n, "batch_per_gpu": batch, "parallelism": f"dp{world} shards"}
         elif kind == "conv":
             line["config"] = {"workload": f"arm_conv_f32 4096 (*) {n} (shared kernel), batch={batch}/GPU",
