@@ -312,6 +312,26 @@ def cfft_batch(S, data, ifft, bitrev, stream=None, kind=None):
         raise RuntimeError(f"{fn.__name__} -> {st}: {last_error()[1]}")
 
 
+def cfft_batch_multi(S, shards, ifft, bitrev, kind=None):
+    """In-place CFFT of every row of every tensor in `shards` (torch tensors [batch_s, 2*N],
+    each on its own device) through one arm_cfft_*_batch_multi call (synchronous)."""
+    if kind is None:
+        kind = {arm_cfft_instance_f32: "f32", arm_cfft_instance_q31: "q31",
+                arm_cfft_instance_q15: "q15"}[type(S)]
+    k = len(shards)
+    devs = (C.c_int * k)(*[t.device.index for t in shards])
+    ptrs = (C.c_void_p * k)(*[t.data_ptr() for t in shards])
+    cnts = (C.c_uint32 * k)(*[t.numel() // (2 * S.fftLen) for t in shards])
+    fn = getattr(lib, f"arm_cfft_{kind}_batch_multi")
+    st = fn(C.byref(S), k, devs, ptrs, cnts, ifft, bitrev)
+    if st != ARM_MATH_SUCCESS:
+        raise RuntimeError(f"{fn.__name__} -> {st}: {last_error()[1]}")
+
+
+def device_count():
+    return lib.arm_mi355x_device_count()
+
+
 def rfft_fast_batch(S, p, out, ifft, stream=None):
     batch = p.numel() // S.fftLenRFFT
     st = lib.arm_rfft_fast_f32_batch(C.byref(S), C.c_void_p(p.data_ptr()), C.c_void_p(out.data_ptr()), batch,

@@ -202,6 +202,11 @@ BATCHED = {
        for f in CONV_PARTIAL + CONV_PARTIAL_FAST},
     "arm_mfcc_f32_batch": (C.c_int, [P(arm_mfcc_instance_f32), C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                      C.c_void_p]),
+    **{f"arm_cfft_{t}_batch_multi": (C.c_int, [P(inst), C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                               C.c_uint8, C.c_uint8])
+       for t, inst in (("f32", arm_cfft_instance_f32), ("q31", arm_cfft_instance_q31),
+                       ("q15", arm_cfft_instance_q15))},
+    "arm_mi355x_device_count": (C.c_int, []),
     "arm_mi355x_last_error": (C.c_int, []),
     "arm_mi355x_last_error_string": (C.c_char_p, []),
     "arm_mi355x_clear_error": (None, []),

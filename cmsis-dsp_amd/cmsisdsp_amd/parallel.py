@@ -37,12 +37,16 @@ def init(backend=None, device=True):
     size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_size = int(os.environ.get("LOCAL_WORLD_SIZE", str(size)))
+    ndev = torch.cuda.device_count() if device else 0
     if device:
-        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        torch.cuda.set_device(local % max(1, ndev))
     if size == 1:
         return World(rank, size, local, "none")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    backend = backend or ("nccl" if device else "gloo")
+    if backend is None:
+        # RCCL needs one GPU per rank; more local ranks than GPUs is a rehearsal -> gloo
+        backend = "nccl" if device and ndev >= local_size else "gloo"
     if backend == "nccl":
         dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
     else:
@@ -72,6 +76,12 @@ def weak_offset(per_rank, rank):
 def seed_for(rank, salt=0):
     """Per-rank generator seed: 0x5EED + a large prime stride (disjoint streams)."""
     return 0x5EED + 1000003 * rank + salt
+
+
+def block_seed(block, salt=0):
+    """Seed of global block `block` of a batch whose content must not depend on the world
+    size (strong scaling): every rank regenerates the blocks its slice overlaps."""
+    return 0x5EED0000 + 7919 * block + 1000003 * salt
 
 
 def _tensor_for(world, value, dtype):

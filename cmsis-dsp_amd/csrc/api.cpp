@@ -75,10 +75,11 @@ void cfft_sync(const Inst* S, void* p1, uint8_t ifftFlag, uint8_t bitReverseFlag
   }
   void* d = scratch(bytes, 0);
   if (!d) { set_error(hipErrorOutOfMemory, "arm_cfft scratch"); return; }
-  hipError_t e = hipMemcpyAsync(d, p1, bytes, hipMemcpyHostToDevice, st);
+  HostIO io(st);
+  hipError_t e = io.in(d, p1, bytes);
   if (e == hipSuccess) e = cfft_launch(kind, n, d, 1, pr, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(p1, d, bytes, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess) e = io.out(p1, d, bytes);
+  if (e == hipSuccess) e = io.finish();
   if (e != hipSuccess) set_error(e, "arm_cfft");
 }
 
@@ -92,6 +93,42 @@ arm_status cfft_batch(const Inst* S, void* d_p1, uint32_t batch, uint8_t ifftFla
   hipError_t e = cfft_launch(kind, S->fftLen, d_p1, batch, pr, (hipStream_t)stream);
   if (e != hipSuccess) { set_error(e, "arm_cfft_batch"); return ARM_MATH_ARGUMENT_ERROR; }
   return ARM_MATH_SUCCESS;
+}
+
+// multi-GPU: validate every shard, launch each on its device's internal stream, then wait
+template <typename Inst>
+arm_status cfft_batch_multi(const Inst* S, uint32_t nshards, const int* devices, void* const* d_p1,
+                            const uint32_t* batch, uint8_t ifftFlag, uint8_t bitReverseFlag, int kind) {
+  if (!S || !cfft_len_ok(S->fftLen) || (nshards && (!devices || !d_p1 || !batch))) return ARM_MATH_ARGUMENT_ERROR;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+  for (uint32_t s = 0; s < nshards; ++s)
+    if (devices[s] < 0 || devices[s] >= ndev || (batch[s] && !d_p1[s])) return ARM_MATH_ARGUMENT_ERROR;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  std::vector<int> used;
+  arm_status status = ARM_MATH_SUCCESS;
+  for (uint32_t s = 0; s < nshards && status == ARM_MATH_SUCCESS; ++s) {
+    if (!batch[s]) continue;
+    hipError_t e = hipSetDevice(devices[s]);
+    CfftPrep pr;
+    if (e != hipSuccess) { set_error(e, "arm_cfft_batch_multi: hipSetDevice"); status = ARM_MATH_ARGUMENT_ERROR; break; }
+    if (!cfft_prepare(S->fftLen, S->pTwiddle, S->pBitRevTable, S->bitRevLength, kind, ifftFlag, bitReverseFlag, pr)) {
+      status = ARM_MATH_ARGUMENT_ERROR;
+      break;
+    }
+    hipStream_t st = sync_stream();
+    e = st ? cfft_launch(kind, S->fftLen, d_p1[s], batch[s], pr, st) : hipErrorOutOfMemory;
+    if (e != hipSuccess) { set_error(e, "arm_cfft_batch_multi"); status = ARM_MATH_ARGUMENT_ERROR; }
+    if (std::find(used.begin(), used.end(), devices[s]) == used.end()) used.push_back(devices[s]);
+  }
+  for (int d : used) {   // drain every device that received work, also after a failure
+    hipError_t e = hipSetDevice(d);
+    if (e == hipSuccess) e = hipStreamSynchronize(sync_stream());
+    if (e != hipSuccess) { set_error(e, "arm_cfft_batch_multi: sync"); status = ARM_MATH_ARGUMENT_ERROR; }
+  }
+  (void)hipSetDevice(prev);
+  return status;
 }
 
 bool rfft_len_ok(uint32_t n) { return n >= 32 && n <= 4096 && (n & (n - 1)) == 0; }
@@ -175,13 +212,14 @@ void rfft_fixed_sync(const RInst* S, T* pSrc, T* pDst) {
   T* s = ds ? pSrc : (T*)scratch(sizeof(T) * 2 * (size_t)n, 0);
   T* d = dd ? pDst : (T*)scratch(db, 1);
   if (!s || !d) { set_error(hipErrorOutOfMemory, "arm_rfft scratch"); return; }
+  HostIO io(st);
   hipError_t e = hipSuccess;
-  if (!ds) e = hipMemcpyAsync(s, pSrc, sb, hipMemcpyHostToDevice, st);
+  if (!ds) e = io.in(s, pSrc, sb);
   if (e != hipSuccess) { set_error(e, "arm_rfft"); return; }
-  if (!rfft_fixed_run<T>(S, s, d, 1, st)) return;
-  if (!ds && !inv) e = hipMemcpyAsync(pSrc, s, sb, hipMemcpyDeviceToHost, st);   // forward overwrites pSrc
-  if (e == hipSuccess && !dd) e = hipMemcpyAsync(pDst, d, db, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (!rfft_fixed_run<T>(S, s, d, 1, st)) { (void)hipStreamSynchronize(st); return; }
+  if (!ds && !inv) e = io.out(pSrc, s, sb);   // forward overwrites pSrc
+  if (e == hipSuccess && !dd) e = io.out(pDst, d, db);
+  if (e == hipSuccess) e = io.finish();
   if (e != hipSuccess) set_error(e, "arm_rfft");
 }
 
@@ -283,16 +321,19 @@ bool mfcc_run(const arm_mfcc_instance_f32* S, const MfccDev& d, float* x, float*
   return true;
 }
 
+// FIR coefficients: device pointers in place, host sets through the content-keyed cache
+// (uploaded synchronously once per distinct set, so an asynchronous batch call never
+// shares a staging buffer with a later call on another stream)
 template <typename T>
-const T* device_coeffs(const T* c, int n, int slot, hipStream_t st, bool* ok) {
-  *ok = true;
-  if (is_device_ptr(c)) return c;
-  T* d = (T*)scratch(sizeof(T) * (size_t)n, slot);
-  if (!d || hipMemcpyAsync(d, c, sizeof(T) * (size_t)n, hipMemcpyHostToDevice, st) != hipSuccess) {
-    *ok = false;
-    return nullptr;
-  }
+const T* device_coeffs(const T* c, int n, bool* ok) {
+  const T* d = (const T*)device_table(c, sizeof(T) * (size_t)n);
+  *ok = d != nullptr;
   return d;
+}
+
+bool ranges_overlap(const void* a, const void* b, size_t bytes) {
+  const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+  return bytes && x < y + bytes && y < x + bytes;
 }
 
 // drop-in FIR: state = [history(T-1) ; block(B)] on host or device (arm_fir_f32.c:911-1280).
@@ -303,26 +344,33 @@ void fir_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B, int kind) {
   const int taps = S->numTaps, T1 = taps - 1;
   hipStream_t st = sync_stream();
   bool ok = true;
-  const T* dc = device_coeffs<T>(S->pCoeffs, taps, 1, st, &ok);
+  const T* dc = device_coeffs<T>(S->pCoeffs, taps, &ok);
   if (!ok) { set_error(hipErrorOutOfMemory, "arm_fir coeffs"); return; }
   const bool dstate = is_device_ptr(S->pState), dsrc = is_device_ptr(pSrc), ddst = is_device_ptr(pDst);
   const size_t sb = sizeof(T) * (size_t)B, hb = sizeof(T) * (size_t)T1;
+  // in place on the device (pSrc overlapping pDst): filter from a copy of the input, which
+  // also feeds the new history and the state tail (the reference copies each input into
+  // pState before writing pDst, arm_fir_f32.c:947-975)
+  const bool alias = dsrc && ddst && ranges_overlap(pSrc, pDst, sb);
   T* dhist = dstate ? S->pState : (T*)scratch(hb + 16, 2);
-  const T* dsr = dsrc ? pSrc : (const T*)scratch(sb, 3);
+  const T* dsr = (dsrc && !alias) ? pSrc : (const T*)scratch(sb, 3);
   T* dds = ddst ? pDst : (T*)scratch(sb, 4);
   if (!dhist || !dsr || !dds) { set_error(hipErrorOutOfMemory, "arm_fir scratch"); return; }
+  HostIO io(st);
   hipError_t e = hipSuccess;
-  if (!dstate && T1 > 0) e = hipMemcpyAsync(dhist, S->pState, hb, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess && !dsrc) e = hipMemcpyAsync((void*)dsr, pSrc, sb, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) {
-    e = fir_run(kind, dc, taps, dsr, dds, B, 1, dhist, st);
-  }
-  if (e == hipSuccess && !ddst) e = hipMemcpyAsync(pDst, dds, sb, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess && !dstate && T1 > 0) e = hipMemcpyAsync(S->pState, dhist, hb, hipMemcpyDeviceToHost, st);
+  if (!dstate && T1 > 0) e = io.in(dhist, S->pState, hb);
+  if (e == hipSuccess && alias) e = hipMemcpyAsync((void*)dsr, pSrc, sb, hipMemcpyDeviceToDevice, st);
+  else if (e == hipSuccess && !dsrc) e = io.in((void*)dsr, pSrc, sb);
+  if (e == hipSuccess) e = fir_run(kind, dc, taps, dsr, dds, B, 1, dhist, st);
+  if (e == hipSuccess && !ddst) e = io.out(pDst, dds, sb);
+  if (e == hipSuccess && !dstate && T1 > 0) e = io.out(S->pState, dhist, hb);
   // state tail keeps the block input (the reference copies it there, :947-975)
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(S->pState + T1, dsr, sb, dstate ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess) {
+    if (dstate) e = hipMemcpyAsync(S->pState + T1, dsr, sb, hipMemcpyDeviceToDevice, st);
+    else if (dsrc) e = io.out(S->pState + T1, dsr, sb);
+    else memcpy(S->pState + T1, pSrc, sb);     // host input, host state: the caller's words
+  }
+  if (e == hipSuccess) e = io.finish();
   if (e != hipSuccess) set_error(e, "arm_fir");
 }
 
@@ -333,7 +381,7 @@ arm_status fir_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uint32
   if (S->numTaps > 1 && batch && !d_hist) return ARM_MATH_ARGUMENT_ERROR;
   hipStream_t st = (hipStream_t)stream;
   bool ok = true;
-  const T* dc = device_coeffs<T>(S->pCoeffs, S->numTaps, 5, st, &ok);
+  const T* dc = device_coeffs<T>(S->pCoeffs, S->numTaps, &ok);
   if (!ok) { set_error(hipErrorOutOfMemory, "arm_fir_batch coeffs"); return ARM_MATH_ARGUMENT_ERROR; }
   hipError_t e = fir_run(kind, dc, S->numTaps, d_src, d_dst, B, batch, d_hist, st);
   if (e != hipSuccess) { set_error(e, "arm_fir_batch"); return ARM_MATH_ARGUMENT_ERROR; }
@@ -351,11 +399,12 @@ arm_status fir_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uint32
 // Returns the job and the written output range [wlo, whi) of one item.
 enum ConvVariant { kVarConv = 0, kVarPartial = 1, kVarCorr = 2 };
 ConvJob conv_plan(int op, int variant, const void* a, uint32_t alen, const void* b, uint32_t blen, uint32_t first,
-                  uint32_t num, uint64_t* wlo, uint64_t* whi) {
+                  uint32_t num, uint64_t* wlo, uint64_t* whi, bool* swapped) {
   ConvJob j{};
   j.op = op;
   j.corr = variant == kVarCorr;
   const bool swap = (variant == kVarCorr || op == kConvFastQ15 || op == kConvFastQ31) && alen < blen;
+  *swapped = swap;
   j.x = swap ? b : a; j.A = swap ? blen : alen;
   j.h = swap ? a : b; j.B = swap ? alen : blen;
   const uint32_t L = alen + blen - 1;
@@ -377,7 +426,8 @@ void conv_family_sync(int op, int variant, const T* a, uint32_t alen, const T* b
                       uint32_t first, uint32_t num, const char* what) {
   if (!a || !b || !dst || alen == 0 || blen == 0) return;
   uint64_t wlo, whi;
-  ConvJob j = conv_plan(op, variant, a, alen, b, blen, first, num, &wlo, &whi);
+  bool swapped = false;
+  ConvJob j = conv_plan(op, variant, a, alen, b, blen, first, num, &wlo, &whi, &swapped);
   if (j.num == 0) return;
   const size_t ab = sizeof(T) * alen, bb = sizeof(T) * blen;
   hipStream_t st = sync_stream();
@@ -386,17 +436,17 @@ void conv_family_sync(int op, int variant, const T* a, uint32_t alen, const T* b
   const T* B = db ? b : (const T*)scratch(bb, 1);
   T* Y = dd ? dst : (T*)scratch(sizeof(T) * whi, 2);
   if (!A || !B || !Y) { set_error(hipErrorOutOfMemory, what); return; }
+  HostIO io(st);
   hipError_t e = hipSuccess;
-  if (!da) e = hipMemcpyAsync((void*)A, a, ab, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess && !db) e = hipMemcpyAsync((void*)B, b, bb, hipMemcpyHostToDevice, st);
-  const bool swapped = j.x != (const void*)a;
+  if (!da) e = io.in((void*)A, a, ab);
+  if (e == hipSuccess && !db) e = io.in((void*)B, b, bb);
   j.x = swapped ? (const void*)B : (const void*)A;
   j.h = swapped ? (const void*)A : (const void*)B;
   j.y = Y; j.sx = j.sh = j.sy = 0; j.batch = 1;
   if (e == hipSuccess) e = conv_family_run(j, st);
   // only the words the reference writes are copied back (partial / correlate leave the rest)
-  if (e == hipSuccess && !dd) e = hipMemcpyAsync(dst + wlo, Y + wlo, sizeof(T) * (whi - wlo), hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess && !dd) e = io.out(dst + wlo, Y + wlo, sizeof(T) * (whi - wlo));
+  if (e == hipSuccess) e = io.finish();
   if (e != hipSuccess) set_error(e, what);
 }
 
@@ -409,8 +459,8 @@ arm_status conv_family_batch(int op, int variant, const T* a, uint32_t alen, uin
   if (batch && (!a || !b || !y || alen == 0 || blen == 0)) return ARM_MATH_ARGUMENT_ERROR;
   if (batch == 0) return ARM_MATH_SUCCESS;
   uint64_t wlo, whi;
-  ConvJob j = conv_plan(op, variant, a, alen, b, blen, first, num, &wlo, &whi);
-  const bool swapped = j.x != (const void*)a;
+  bool swapped = false;
+  ConvJob j = conv_plan(op, variant, a, alen, b, blen, first, num, &wlo, &whi, &swapped);
   j.sx = swapped ? sb : sa;
   j.sh = swapped ? sa : sb;
   j.y = y; j.batch = batch;
@@ -445,17 +495,18 @@ arm_status mat_mult_fixed_sync(const M* pSrcA, const M* pSrcB, M* pDst, bool fas
   T* B = db ? pSrcB->pData : (T*)scratch(bb + 16, 1);
   T* Cd = dc ? pDst->pData : (T*)scratch(cb + 16, 2);
   if (!A || !B || !Cd) { set_error(hipErrorOutOfMemory, "arm_mat_mult scratch"); return ARM_MATH_ARGUMENT_ERROR; }
+  HostIO io(st);
   hipError_t e = hipSuccess;
-  if (!da && ab) e = hipMemcpyAsync(A, pSrcA->pData, ab, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess && !db && bb) e = hipMemcpyAsync(B, pSrcB->pData, bb, hipMemcpyHostToDevice, st);
+  if (!da) e = io.in(A, pSrcA->pData, ab);
+  if (e == hipSuccess && !db) e = io.in(B, pSrcB->pData, bb);
   if (e == hipSuccess) {
     if constexpr (sizeof(T) == 2)
       e = fast ? mat_mult_fast_q15_launch(m, k, n, A, B, Cd, 1, st) : mat_mult_q15_launch(m, k, n, A, B, Cd, 1, st);
     else
       e = fast ? mat_mult_fast_q31_launch(m, k, n, A, B, Cd, 1, st) : mat_mult_q31_launch(m, k, n, A, B, Cd, 1, st);
   }
-  if (e == hipSuccess && !dc && cb) e = hipMemcpyAsync(pDst->pData, Cd, cb, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess && !dc) e = io.out(pDst->pData, Cd, cb);
+  if (e == hipSuccess) e = io.finish();
   if (e != hipSuccess) { set_error(e, "arm_mat_mult"); return ARM_MATH_ARGUMENT_ERROR; }
   return ARM_MATH_SUCCESS;
 }
@@ -506,6 +557,27 @@ arm_status arm_cfft_q15_batch(const arm_cfft_instance_q15* S, q15_t* d_p1, uint3
   return cfft_batch(S, d_p1, batch, ifftFlag, bitReverseFlag, stream, 2);
 }
 
+arm_status arm_cfft_f32_batch_multi(const arm_cfft_instance_f32* S, uint32_t nshards, const int* devices,
+                                    float32_t* const* d_p1, const uint32_t* batch, uint8_t ifftFlag,
+                                    uint8_t bitReverseFlag) {
+  return cfft_batch_multi(S, nshards, devices, (void* const*)d_p1, batch, ifftFlag, bitReverseFlag, 0);
+}
+arm_status arm_cfft_q31_batch_multi(const arm_cfft_instance_q31* S, uint32_t nshards, const int* devices,
+                                    q31_t* const* d_p1, const uint32_t* batch, uint8_t ifftFlag,
+                                    uint8_t bitReverseFlag) {
+  return cfft_batch_multi(S, nshards, devices, (void* const*)d_p1, batch, ifftFlag, bitReverseFlag, 1);
+}
+arm_status arm_cfft_q15_batch_multi(const arm_cfft_instance_q15* S, uint32_t nshards, const int* devices,
+                                    q15_t* const* d_p1, const uint32_t* batch, uint8_t ifftFlag,
+                                    uint8_t bitReverseFlag) {
+  return cfft_batch_multi(S, nshards, devices, (void* const*)d_p1, batch, ifftFlag, bitReverseFlag, 2);
+}
+int arm_mi355x_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) { (void)hipGetLastError(); return 0; }
+  return n;
+}
+
 void arm_rfft_fast_f32(const arm_rfft_fast_instance_f32* S, float32_t* p, float32_t* pOut, uint8_t ifftFlag) {
   if (!S || !p || !pOut || !rfft_len_ok(S->fftLenRFFT)) return;
   const size_t bytes = sizeof(float) * S->fftLenRFFT;
@@ -514,13 +586,14 @@ void arm_rfft_fast_f32(const arm_rfft_fast_instance_f32* S, float32_t* p, float3
   float* d_p = dp ? p : (float*)scratch(bytes, 0);
   float* d_o = dout ? pOut : (float*)scratch(bytes, 1);
   if (!d_p || !d_o) { set_error(hipErrorOutOfMemory, "arm_rfft_fast scratch"); return; }
+  HostIO io(st);
   hipError_t e = hipSuccess;
-  if (!dp) e = hipMemcpyAsync(d_p, p, bytes, hipMemcpyHostToDevice, st);
+  if (!dp) e = io.in(d_p, p, bytes);
   if (e != hipSuccess) { set_error(e, "arm_rfft_fast"); return; }
-  if (!rfft_run(S, d_p, d_o, 1, ifftFlag, st)) return;
-  if (!dp && !ifftFlag) e = hipMemcpyAsync(p, d_p, bytes, hipMemcpyDeviceToHost, st);   // forward overwrites p
-  if (e == hipSuccess && !dout) e = hipMemcpyAsync(pOut, d_o, bytes, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (!rfft_run(S, d_p, d_o, 1, ifftFlag, st)) { (void)hipStreamSynchronize(st); return; }
+  if (!dp && !ifftFlag) e = io.out(p, d_p, bytes);   // forward overwrites p
+  if (e == hipSuccess && !dout) e = io.out(pOut, d_o, bytes);
+  if (e == hipSuccess) e = io.finish();
   if (e != hipSuccess) set_error(e, "arm_rfft_fast");
 }
 
@@ -606,12 +679,13 @@ arm_status arm_mat_mult_f32(const arm_matrix_instance_f32* pSrcA, const arm_matr
   float* B = db ? pSrcB->pData : (float*)scratch(bb + 16, 1);
   float* C = dc ? pDst->pData : (float*)scratch(cb + 16, 2);
   if (!A || !B || !C) { set_error(hipErrorOutOfMemory, "arm_mat_mult scratch"); return ARM_MATH_ARGUMENT_ERROR; }
+  HostIO io(st);
   hipError_t e = hipSuccess;
-  if (!da && ab) e = hipMemcpyAsync(A, pSrcA->pData, ab, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess && !db && bb) e = hipMemcpyAsync(B, pSrcB->pData, bb, hipMemcpyHostToDevice, st);
+  if (!da) e = io.in(A, pSrcA->pData, ab);
+  if (e == hipSuccess && !db) e = io.in(B, pSrcB->pData, bb);
   if (e == hipSuccess) e = mat_mult_f32_launch(m, k, n, A, B, C, 1, st);
-  if (e == hipSuccess && !dc && cb) e = hipMemcpyAsync(pDst->pData, C, cb, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess && !dc) e = io.out(pDst->pData, C, cb);
+  if (e == hipSuccess) e = io.finish();
   if (e != hipSuccess) { set_error(e, "arm_mat_mult_f32"); return ARM_MATH_ARGUMENT_ERROR; }
   return ARM_MATH_SUCCESS;
 }
@@ -639,12 +713,13 @@ void arm_mfcc_f32(const arm_mfcc_instance_f32* S, float32_t* pSrc, float32_t* pD
   const bool ddst = is_device_ptr(pDst);
   float* o = ddst ? pDst : (float*)scratch(sizeof(float) * nd, 2);
   if (!x || !y || !o) { set_error(hipErrorOutOfMemory, "arm_mfcc scratch"); return; }
-  hipError_t e = hipMemcpyAsync(x, pSrc, sizeof(float) * n,
-                                is_device_ptr(pSrc) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st);
+  HostIO io(st);
+  hipError_t e = is_device_ptr(pSrc) ? hipMemcpyAsync(x, pSrc, sizeof(float) * n, hipMemcpyDeviceToDevice, st)
+                                     : io.in(x, pSrc, sizeof(float) * n);
   if (e != hipSuccess) { set_error(e, "arm_mfcc_f32"); return; }
-  if (!mfcc_run(S, d, x, y, o, 1, st)) return;
-  if (!ddst) e = hipMemcpyAsync(pDst, o, sizeof(float) * nd, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (!mfcc_run(S, d, x, y, o, 1, st)) { (void)hipStreamSynchronize(st); return; }
+  if (!ddst) e = io.out(pDst, o, sizeof(float) * nd);
+  if (e == hipSuccess) e = io.finish();
   if (e != hipSuccess) set_error(e, "arm_mfcc_f32");
 }
 

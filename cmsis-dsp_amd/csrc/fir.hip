@@ -480,6 +480,10 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
   if (batch == 0 || B == 0) return hipSuccess;
   if (T_ < 1 || T_ > kFirMaxTaps) return hipErrorInvalidValue;
   const int T1 = T_ - 1;
+  const uint32_t nchunks = (B + kFirChunk - 1) / kFirChunk;
+  const uint64_t items64 = (uint64_t)nchunks * batch;
+  if (items64 > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  const uint32_t items = (uint32_t)items64;
   // The history is read by the filter pass and rewritten afterwards; if the new tail
   // depends on old history (B < T1) keep a copy of the old one.
   const T* hist_in = hist;
@@ -491,10 +495,21 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
     if (e != hipSuccess) return e;
     hist_in = tmp;
   }
-  const uint32_t nchunks = (B + kFirChunk - 1) / kFirChunk;
-  const uint64_t items64 = (uint64_t)nchunks * batch;
-  if (items64 > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  const uint32_t items = (uint32_t)items64;
+  // In place (src overlapping dst): chunk c+1 stages its look-back window from src while
+  // chunk c may already be writing dst, and the new history is read from src after the
+  // pass; filter from a stream-ordered copy of the input instead.
+  T* src_copy = nullptr;
+  {
+    const size_t bytes = sizeof(T) * (size_t)batch * B;
+    const uintptr_t s0 = (uintptr_t)src, d0 = (uintptr_t)dst;
+    if (s0 < d0 + bytes && d0 < s0 + bytes) {
+      hipError_t e = hipMallocAsync((void**)&src_copy, bytes, st);
+      if (e != hipSuccess) return e;
+      e = hipMemcpyAsync(src_copy, src, bytes, hipMemcpyDeviceToDevice, st);
+      if (e != hipSuccess) return e;
+      src = src_copy;
+    }
+  }
   switch (kind) {
     case kFirF32: {
       const int grid = persistent_grid((const void*)fir_f32_kernel, kBlock, 0, items, 4);
@@ -525,6 +540,7 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
     e = hipGetLastError();
   }
   if (tmp) (void)hipFreeAsync(tmp, st);
+  if (src_copy) (void)hipFreeAsync(src_copy, st);
   return e;
 }
 

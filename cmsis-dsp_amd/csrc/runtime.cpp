@@ -1,6 +1,7 @@
 // Host runtime: device table cache, staging scratch, error channel.
 #include "runtime.hpp"
 
+#include <dlfcn.h>
 #include <string.h>
 
 #include <map>
@@ -32,6 +33,8 @@ uint64_t fnv1a(const uint8_t* p, size_t n) {
 
 struct Scratch { void* p = nullptr; size_t n = 0; };
 thread_local std::map<std::pair<int, int>, Scratch> g_scratch;
+struct Pinned { void* p = nullptr; size_t n = 0; };   // kept until process exit, like Scratch
+thread_local std::map<int, Pinned> g_pinned;
 thread_local std::map<int, hipStream_t> g_streams;
 
 int cur_dev() { int d = 0; (void)hipGetDevice(&d); return d; }
@@ -68,8 +71,19 @@ bool is_device_ptr(const void* p) {
   return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
+bool is_library_addr(const void* p) {
+  static const void* self = [] {
+    Dl_info i{};
+    return dladdr((const void*)&is_library_addr, &i) ? i.dli_fbase : (void*)nullptr;
+  }();
+  Dl_info i{};
+  return p && self && dladdr(p, &i) && i.dli_fbase == self;
+}
+
 const void* device_table(const void* host, size_t bytes) {
   if (!host || !bytes) { set_error(hipErrorInvalidValue, "device_table: null table"); return nullptr; }
+  if (is_device_ptr(host)) return host;
+  if (!is_library_addr(host)) return device_blob(host, bytes);
   const int dev = cur_dev();
   std::lock_guard<std::mutex> lk(g_table_mu);
   auto key = std::make_tuple(dev, host, bytes);
@@ -78,7 +92,7 @@ const void* device_table(const void* host, size_t bytes) {
   void* d = nullptr;
   hipError_t e = hipMalloc(&d, bytes);
   if (e != hipSuccess) { set_error(e, "device_table: hipMalloc"); return nullptr; }
-  e = hipMemcpy(d, host, bytes, is_device_ptr(host) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice);
+  e = hipMemcpy(d, host, bytes, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     set_error(e, "device_table: hipMemcpy");
     (void)hipFree(d);
@@ -116,12 +130,18 @@ const uint16_t* device_perm(int n, const uint16_t* table, uint16_t len, int kind
   *canonical = true;
   if (!table) { return nullptr; }
   const int dev = cur_dev();
-  std::lock_guard<std::mutex> lk(g_table_mu);
+  // the library's own tables are immutable: cache their verdict by address; any other
+  // table is re-derived from its current words on every call (O(len)) and a non-canonical
+  // permutation is uploaded through the content-keyed blob cache
+  const bool lib = is_library_addr(table);
   auto key = std::make_tuple(dev, (const void*)table, len, kind, n);
-  auto it = g_perms.find(key);
-  if (it != g_perms.end()) {
-    *canonical = it->second.second;
-    return (const uint16_t*)it->second.first;
+  if (lib) {
+    std::lock_guard<std::mutex> lk(g_table_mu);
+    auto it = g_perms.find(key);
+    if (it != g_perms.end()) {
+      *canonical = it->second.second;
+      return (const uint16_t*)it->second.first;
+    }
   }
   // apply the reference's sequential swaps (arm_bitreversal2.c:84-108) to an identity
   // array of complex indices: a[pos] = pre-reversal index that ends up at pos.
@@ -141,15 +161,15 @@ const uint16_t* device_perm(int n, const uint16_t* table, uint16_t len, int kind
   }
   bool canon = true;
   for (int k = 0; k < n && canon; ++k) canon = a[k] == (kind == 0 ? f32_src(n, k) : fixed_src(n, k));
-  void* d = nullptr;
+  const void* d = nullptr;
   if (!canon) {
-    if (hipMalloc(&d, n * sizeof(uint16_t)) != hipSuccess ||
-        hipMemcpy(d, a.data(), n * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess) {
-      *ok = false;
-      return nullptr;
-    }
+    d = device_blob(a.data(), n * sizeof(uint16_t));
+    if (!d) { *ok = false; return nullptr; }
   }
-  g_perms[key] = {d, canon};
+  if (lib) {
+    std::lock_guard<std::mutex> lk(g_table_mu);
+    g_perms[key] = {(void*)d, canon};
+  }
   *canonical = canon;
   return (const uint16_t*)d;
 }
@@ -165,6 +185,44 @@ void* scratch(size_t bytes, int slot) {
     s.n = bytes;
   }
   return s.p;
+}
+
+void* pinned(size_t bytes, int slot) {
+  Pinned& s = g_pinned[slot];
+  if (s.n < bytes) {
+    if (s.p) (void)hipHostFree(s.p);
+    s.p = nullptr;
+    s.n = 0;
+    if (hipHostMalloc(&s.p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    s.n = bytes;
+  }
+  return s.p;
+}
+
+hipError_t HostIO::in(void* dev, const void* host, size_t bytes) {
+  if (!bytes) return hipSuccess;
+  void* pin = pinned(bytes, slot_++);
+  if (!pin) return hipErrorOutOfMemory;
+  memcpy(pin, host, bytes);
+  return hipMemcpyAsync(dev, pin, bytes, hipMemcpyHostToDevice, st_);
+}
+
+hipError_t HostIO::out(void* host, const void* dev, size_t bytes) {
+  if (!bytes) return hipSuccess;
+  if (nouts_ == 4) return hipErrorInvalidValue;
+  void* pin = pinned(bytes, slot_++);
+  if (!pin) return hipErrorOutOfMemory;
+  hipError_t e = hipMemcpyAsync(pin, dev, bytes, hipMemcpyDeviceToHost, st_);
+  if (e == hipSuccess) outs_[nouts_++] = {host, pin, bytes};
+  return e;
+}
+
+hipError_t HostIO::finish() {
+  hipError_t e = hipStreamSynchronize(st_);
+  if (e != hipSuccess) return e;
+  for (int i = 0; i < nouts_; ++i) memcpy(outs_[i].host, outs_[i].pin, outs_[i].bytes);
+  nouts_ = 0;
+  return hipSuccess;
 }
 
 hipStream_t sync_stream() {

@@ -16,8 +16,16 @@ void clear_error();
 // including hipHostMalloc'd pinned memory, is staged through a device scratch buffer.
 bool is_device_ptr(const void* p);
 
-// Device copy of an immutable host table (twiddles, RFFT twiddles), uploaded once per
-// (device, host pointer, size).  Returns nullptr on failure.
+// True when p lies inside this library's own image (its CommonTables / const instances):
+// those words never change, so their device copies are cached by address.
+bool is_library_addr(const void* p);
+
+// Device view of a table (twiddles, RFFT twiddles, coefficients):
+//   * a device pointer is used in place (no copy; the caller keeps it alive);
+//   * the library's own tables are uploaded once per (device, address);
+//   * any other host table is cached by CONTENT (device_blob), so a caller that frees a
+//     table and reuses the address for new values never gets a stale copy.
+// Returns nullptr on failure.
 const void* device_table(const void* host, size_t bytes);
 
 // Device copy of a host byte blob, cached by CONTENT (hash + full compare): uploaded once
@@ -33,6 +41,28 @@ const uint16_t* device_perm(int n, const uint16_t* table, uint16_t len, int kind
 
 // Per-thread device scratch for the synchronous host-pointer path (grown on demand).
 void* scratch(size_t bytes, int slot);
+
+// Per-thread pinned (hipHostMalloc) bounce buffer, grown on demand.
+void* pinned(size_t bytes, int slot);
+
+// Host <-> device staging of one synchronous drop-in call: host words are copied into a
+// pinned bounce buffer and DMA'd from there (in), device results are DMA'd into a pinned
+// buffer and copied to the caller's memory after the stream has drained (finish).  One
+// pinned slot per transfer; every call ends with finish(), so slots are free again.
+class HostIO {
+ public:
+  explicit HostIO(hipStream_t st) : st_(st) {}
+  hipError_t in(void* dev, const void* host, size_t bytes);
+  hipError_t out(void* host, const void* dev, size_t bytes);
+  hipError_t finish();
+
+ private:
+  struct Pending { void* host; const void* pin; size_t bytes; };
+  hipStream_t st_;
+  int slot_ = 0;
+  Pending outs_[4];
+  int nouts_ = 0;
+};
 
 // The internal stream used by the synchronous drop-in API on the current device.
 hipStream_t sync_stream();

@@ -14,8 +14,10 @@
  *     launch failure; details in arm_mi355x_last_error_string()).
  * Instance structs are the reference's own (arm_math.h); tables they point to are
  * uploaded once per device and cached by address, so they must stay immutable.
- * Multi-GPU: one process (or thread) per device, each calling these on its own shard;
- * the current HIP device of the calling thread is used.
+ * Multi-GPU: either one process (or host thread) per device, each calling these on its
+ * own shard with that device current (the library's caches, scratch and internal streams
+ * are per device and per thread), or one call of the *_batch_multi entry points below,
+ * which enqueue every shard on its device before waiting for any.
  */
 #ifndef ARM_MATH_MI355X_BATCH_H
 #define ARM_MATH_MI355X_BATCH_H
@@ -139,6 +141,28 @@ arm_status arm_mat_mult_fast_q15_batch(const arm_matrix_instance_q15 *pSrcA, con
                                        arm_matrix_instance_q15 *pDst, uint32_t batch, void *stream);
 arm_status arm_mat_mult_fast_q31_batch(const arm_matrix_instance_q31 *pSrcA, const arm_matrix_instance_q31 *pSrcB,
                                        arm_matrix_instance_q31 *pDst, uint32_t batch, void *stream);
+
+/* Multi-GPU complex FFT (SURVEY §8b "a multi-GPU entry point"; per item: arm_cfft_f32 /
+ * _q31 / _q15, transform_functions.h:456-460).  Shard s of `nshards` is batch[s] contiguous
+ * transforms at DEVICE pointer d_p1[s] on HIP device devices[s] (a device may appear in
+ * several shards).  Every shard is launched on an internal stream of its device before any
+ * is waited for, so the devices run concurrently; the call returns when all shards are
+ * done (synchronous, like the drop-in API).  Input written on other streams must be
+ * complete before the call.  Arguments are validated before anything is launched:
+ * ARM_MATH_ARGUMENT_ERROR for a bad device index, NULL pointer or unsupported length.
+ * The calling thread's current device is restored. */
+arm_status arm_cfft_f32_batch_multi(const arm_cfft_instance_f32 *S, uint32_t nshards, const int *devices,
+                                    float32_t *const *d_p1, const uint32_t *batch, uint8_t ifftFlag,
+                                    uint8_t bitReverseFlag);
+arm_status arm_cfft_q31_batch_multi(const arm_cfft_instance_q31 *S, uint32_t nshards, const int *devices,
+                                    q31_t *const *d_p1, const uint32_t *batch, uint8_t ifftFlag,
+                                    uint8_t bitReverseFlag);
+arm_status arm_cfft_q15_batch_multi(const arm_cfft_instance_q15 *S, uint32_t nshards, const int *devices,
+                                    q15_t *const *d_p1, const uint32_t *batch, uint8_t ifftFlag,
+                                    uint8_t bitReverseFlag);
+
+/* Number of HIP devices visible to the process (0 when none). */
+int arm_mi355x_device_count(void);
 
 /* Error channel for the void-returning drop-in functions: 0 = no error, otherwise the
  * hipError_t of the last failure on this thread. */

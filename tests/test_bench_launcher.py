@@ -1,0 +1,49 @@
+"""CPU: bench.py's N-rank launch (SURVEY §8e / the bench contract).  `bench.py --gpus 2`
+without a torchrun environment must start two ranks as child processes (torch.distributed.run),
+shard the configs[3] global batch in contiguous slices and print one line with n_gpus 2; a
+world size that disagrees with --gpus must fail loudly instead of measuring fewer GPUs."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env=None, timeout=240):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, env=e, cwd=ROOT)
+
+
+def _line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_gpus2_launches_two_ranks_strong_spans():
+    r = _run(["--gpus", "2", "--dry-run", "--scaling", "strong", "--global-batch", "1048576"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _line(r.stdout)
+    assert line["n_gpus"] == 2 and line["ranks"] == 2 and line["dist_backend"] == "gloo"
+    assert len(set(line["pids"])) == 2 and os.getpid() not in line["pids"]
+    assert line["spans"] == [[0, 524288], [524288, 524288]]
+    assert line["max_wall_s"] == 0.002          # MAX over ranks (rank r reports 0.001 * (r + 1))
+
+
+def test_gpus3_ragged_global_batch():
+    r = _run(["--gpus", "3", "--dry-run", "--scaling", "strong", "--global-batch", "10"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _line(r.stdout)
+    assert line["n_gpus"] == 3
+    assert line["spans"] == [[0, 4], [4, 3], [7, 3]]
+
+
+def test_world_size_mismatch_fails_loudly():
+    r = _run(["--gpus", "2", "--dry-run"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE=1" in (r.stderr + r.stdout)

@@ -3,8 +3,9 @@
 rfft / FIR: bit-exact against oracle/_ref.  mat_mult: MFMA f32 accumulates as an fmaf
 chain (one rounding per term fewer than the reference's mul-then-add), so the bar is the
 reference test's own tolerance (Testing/Source/Tests/BinaryTestsF32.cpp:5,13-17:
-rel 1e-6 / abs 1e-5 at dims <= 40) plus a normwise bound at large sizes:
-|C - C_ref|_max <= 4 * K * eps32 * max(|A| |B|).
+rel 1e-6 / abs 1e-5 at dims <= 40) plus a per-element bound at large sizes:
+|C - C64|ij <= K * 2^-24 * (|A||B|)ij, 2x that against the reference build, and a bf16
+negative control that must fail it.
 """
 import numpy as np
 import pytest
@@ -206,9 +207,25 @@ def test_mat_mult_size_mismatch(dsp, torch_gpu):
     assert dsp.lib.arm_mat_mult_f32(C.byref(A), C.byref(B), C.byref(Cm)) == dsp.ARM_MATH_SIZE_MISMATCH
 
 
+def _elementwise_bound(a, b):
+    """|C - C64|ij <= K 2^-24 (|A||B|)ij: the recursive-summation bound of an f32 dot
+    product of length K (Higham, gamma_K), which the reference's own sequential sum
+    (arm_mat_mult_f32.c:635-722) and an fmaf chain both satisfy."""
+    k = a.shape[-1]
+    return k * 2.0 ** -24 * np.einsum("...mk,...kn->...mn", np.abs(a).astype(np.float64), np.abs(b).astype(np.float64))
+
+
+def _bf16(x):
+    import torch
+    return torch.from_numpy(x).bfloat16().double().numpy()
+
+
 @pytest.mark.parametrize("m,k,n,batch", [(256, 256, 256, 3), (300, 130, 200, 2), (1024, 1024, 1024, 1),
                                           (128, 16, 384, 2), (384, 48, 128, 1), (128, 1000, 128, 1)])
-def test_mat_mult_batch_normwise(dsp, torch_gpu, ref, m, k, n, batch):
+def test_mat_mult_batch_elementwise(dsp, torch_gpu, ref, m, k, n, batch):
+    """Per-element f32 bound against float64 over every item, and a negative control: the
+    product of bf16-rounded operands must violate the same bound (so the check tells f32
+    from bf16/tf32 inputs)."""
     torch = torch_gpu
     rng = np.random.default_rng(m + k + n)
     a = rng.uniform(-1, 1, (batch, m, k)).astype(np.float32)
@@ -216,13 +233,38 @@ def test_mat_mult_batch_normwise(dsp, torch_gpu, ref, m, k, n, batch):
     da, db = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
     dc = torch.empty((batch, m, n), dtype=torch.float32, device="cuda")
     dsp.mat_mult_batch(da, db, dc)
-    got = dc.cpu().numpy()
+    got = dc.cpu().numpy().astype(np.float64)
     exact = np.einsum("bmk,bkn->bmn", a.astype(np.float64), b.astype(np.float64))
-    bound = 4 * k * np.finfo(np.float32).eps * np.einsum("bmk,bkn->bmn", np.abs(a), np.abs(b)).max()
-    assert np.abs(got - exact).max() <= bound
+    bound = _elementwise_bound(a, b)
+    assert np.all(np.abs(got - exact) <= bound)
+    bf = np.einsum("bmk,bkn->bmn", _bf16(a), _bf16(b))     # negative control
+    assert np.mean(np.abs(bf - exact) > bound) > 0.1
     if m * k * n <= 256 ** 3:   # the reference itself on one item (seconds on the host)
         st, want = ref.mat_mult(a[0], b[0])
-        assert np.abs(got[0] - want).max() <= 2 * bound
+        assert np.all(np.abs(got[0] - want) <= 2 * bound[0])
+
+
+def test_mat_mult_1024_vs_reference_slice(dsp, torch_gpu, ref):
+    """BASELINE configs[4] shape (1024^3): a 16-row slice of A times all of B through the
+    reference's own arm_mat_mult_f32 (full K), held per element to 2 K 2^-24 (|A||B|)ij;
+    the whole product per element to K 2^-24 (|A||B|)ij vs float64; and the bf16 negative
+    control rejected."""
+    torch = torch_gpu
+    rng = np.random.default_rng(1024)
+    a = rng.uniform(-1, 1, (1024, 1024)).astype(np.float32)
+    b = rng.uniform(-1, 1, (1024, 1024)).astype(np.float32)
+    dc = torch.empty((1, 1024, 1024), dtype=torch.float32, device="cuda")
+    dsp.mat_mult_batch(torch.from_numpy(a).cuda()[None], torch.from_numpy(b).cuda()[None], dc)
+    got = dc[0].cpu().numpy().astype(np.float64)
+    at, bt = torch.from_numpy(a).double(), torch.from_numpy(b).double()
+    exact = (at @ bt).numpy()
+    bound = 1024 * 2.0 ** -24 * (at.abs() @ bt.abs()).numpy()
+    assert np.all(np.abs(got - exact) <= bound)
+    st, want = ref.mat_mult(a[:16], b)
+    assert st == 0
+    assert np.all(np.abs(got[:16] - want) <= 2 * bound[:16])
+    bf = (torch.from_numpy(_bf16(a)) @ torch.from_numpy(_bf16(b))).numpy()
+    assert np.mean(np.abs(bf - exact) > bound) > 0.1
 
 
 # ------------------------------------------------------------------ mat mult q15 / q31

@@ -1,0 +1,248 @@
+"""GPU: the host runtime around the kernels — the multi-GPU C entry point, several host
+threads sharing one device, in-place (aliased) FIR calls, aliased conv/correlate operands,
+user tables whose contents change at a reused address, and the pinned host staging of the
+drop-in API.  Every result is compared bit for bit with the reference scalar C
+(oracle/_ref).  Reference call shapes: transform_functions.h:456-460 (arm_cfft_*),
+filtering_functions.h:233-237 (arm_fir_f32), arm_correlate_f32.c:1013-1096."""
+import ctypes as C
+import threading
+
+import numpy as np
+import pytest
+
+import refs
+
+pytestmark = pytest.mark.gpu
+
+
+# ------------------------------------------------------------------ multi-GPU C entry point
+@pytest.mark.parametrize("kind,n", [("f32", 1024), ("q31", 4096), ("q15", 4096), ("f32", 256)])
+def test_cfft_batch_multi_bitexact(dsp, torch_gpu, ref, kind, n):
+    """Shards over every visible device (two shards per device, ragged sizes): each shard
+    equals the reference on its transforms."""
+    torch = torch_gpu
+    ndev = dsp.device_count()
+    assert ndev == torch.cuda.device_count() and ndev >= 1
+    counts = [5 + 3 * s for s in range(2 * ndev)]
+    devs = [s % ndev for s in range(2 * ndev)]
+    xs = [np.stack([refs.rand_input(kind, 2 * n, seed=100 * s + r) for r in range(c)]) for s, c in enumerate(counts)]
+    shards = [torch.from_numpy(x.copy()).to(f"cuda:{d}") for x, d in zip(xs, devs)]
+    S = dsp.const_instance(f"arm_cfft_sR_{kind}_len{n}")
+    for ifft in (0, 1):
+        for t, x in zip(shards, xs):
+            t.copy_(torch.from_numpy(x))
+        torch.cuda.synchronize()
+        dsp.cfft_batch_multi(S, shards, ifft, 1)
+        for t, x in zip(shards, xs):
+            assert t.cpu().numpy().tobytes() == ref.cfft_many(kind, n, x, ifft, 1).tobytes()
+
+
+def test_cfft_batch_multi_rejects_bad_shards(dsp, torch_gpu):
+    torch = torch_gpu
+    S = dsp.const_instance("arm_cfft_sR_f32_len1024")
+    t = torch.zeros((2, 2048), device="cuda")
+    ptrs = (C.c_void_p * 1)(t.data_ptr())
+    cnts = (C.c_uint32 * 1)(2)
+    bad = (C.c_int * 1)(dsp.device_count())                     # one past the last device
+    assert dsp.lib.arm_cfft_f32_batch_multi(C.byref(S), 1, bad, ptrs, cnts, 0, 1) == dsp.ARM_MATH_ARGUMENT_ERROR
+    null = (C.c_void_p * 1)(None)
+    ok_dev = (C.c_int * 1)(0)
+    assert dsp.lib.arm_cfft_f32_batch_multi(C.byref(S), 1, ok_dev, null, cnts, 0, 1) == dsp.ARM_MATH_ARGUMENT_ERROR
+    assert dsp.lib.arm_cfft_f32_batch_multi(C.byref(S), 0, None, None, None, 0, 1) == dsp.ARM_MATH_SUCCESS
+    assert torch.count_nonzero(t).item() == 0                   # nothing was launched
+
+
+# ------------------------------------------------------------------ host threads
+def test_four_host_threads_share_one_device(dsp, torch_gpu, ref):
+    """Four host threads, each on its own HIP stream, call arm_cfft_f32_batch and
+    arm_fir_f32_batch concurrently on device 0 (ctypes releases the GIL during the
+    calls): the table cache, the per-thread scratch and the coefficient cache under
+    contention.  Every thread's results stay bit-exact."""
+    torch = torch_gpu
+    n, batch, taps, block = 1024, 64, 32, 1000
+    coeffs = [refs.rand_input("f32", taps, seed=900 + t) for t in range(4)]   # distinct host coefficient sets
+    xs = [np.stack([refs.rand_input("f32", 2 * n, seed=40 * t + r) for r in range(batch)]) for t in range(4)]
+    sig = [np.stack([refs.rand_input("f32", block, seed=70 * t + r) for r in range(8)]) for t in range(4)]
+    want_fft = [ref.cfft_many("f32", n, x, 0, 1) for x in xs]
+    want_fir = [np.stack([ref.fir("f32", coeffs[t], [sig[t][r]])[0][0] for r in range(8)]) for t in range(4)]
+    errors, got_fft, got_fir = [], [None] * 4, [None] * 4
+    S = dsp.const_instance("arm_cfft_sR_f32_len1024")
+
+    def worker(t):
+        try:
+            torch.cuda.set_device(0)
+            st = torch.cuda.Stream()
+            fir = dsp.arm_fir_instance_f32()
+            fir.numTaps = taps
+            fir.pCoeffs = coeffs[t].ctypes.data_as(C.POINTER(C.c_float))   # host coefficients
+            with torch.cuda.stream(st):
+                d = torch.from_numpy(xs[t].copy()).cuda()
+                src = torch.from_numpy(sig[t].copy()).cuda()
+                dst = torch.empty_like(src)
+                hist = torch.zeros((8, taps - 1), device="cuda")
+                for _ in range(5):                                   # interleave many launches
+                    d.copy_(torch.from_numpy(xs[t]))
+                    dsp.cfft_batch(S, d, 0, 1, stream=st)
+                    hist.zero_()
+                    dsp.fir_batch(fir, src, dst, hist, stream=st)
+                st.synchronize()
+                got_fft[t] = d.cpu().numpy()
+                got_fir[t] = dst.cpu().numpy()
+        except Exception as e:   # noqa: BLE001 - reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not errors, errors
+    for t in range(4):
+        assert got_fft[t].tobytes() == want_fft[t].tobytes()
+        assert got_fir[t].tobytes() == want_fir[t].tobytes()
+
+
+# ------------------------------------------------------------------ aliasing
+def test_fir_dropin_in_place_on_device(dsp, torch_gpu, ref):
+    """arm_fir_f32 with pSrc == pDst on the device, two calls: outputs, carried history and
+    the state tail [history ; block input] equal the reference's (which copies each input
+    into pState before writing pDst)."""
+    torch = torch_gpu
+    taps, block = 29, 700
+    c = refs.rand_input("f32", taps, seed=1)
+    blocks = [refs.rand_input("f32", block, seed=2 + k) for k in range(2)]
+    want, want_state = ref.fir("f32", c, blocks)
+    S = dsp.arm_fir_instance_f32()
+    dc = torch.from_numpy(c).cuda()
+    state = torch.full((taps + block - 1,), 7.0, device="cuda")
+    dsp.lib.arm_fir_init_f32(C.byref(S), taps, C.c_void_p(dc.data_ptr()), C.c_void_p(state.data_ptr()), block)
+    for k in range(2):
+        buf = torch.from_numpy(blocks[k].copy()).cuda()
+        dsp.lib.arm_fir_f32(C.byref(S), C.c_void_p(buf.data_ptr()), C.c_void_p(buf.data_ptr()), block)
+        dsp._check_void("arm_fir_f32")
+        assert buf.cpu().numpy().tobytes() == want[k].tobytes()
+    assert state.cpu().numpy().tobytes() == want_state.tobytes()
+
+
+@pytest.mark.parametrize("kind", ["f32", "q15", "q31"])
+def test_fir_batch_in_place(dsp, torch_gpu, ref, kind):
+    """arm_fir_*_batch with d_src == d_dst over two calls (several chunks per filter)."""
+    torch = torch_gpu
+    taps = 40 if kind == "q15" else 37
+    block, batch = 5000, 6
+    c = refs.rand_input(kind, taps, seed=11)
+    blocks = [[refs.rand_input(kind, block, seed=50 * f + k) for k in range(2)] for f in range(batch)]
+    want = [ref.fir(kind, c, blocks[f])[0] for f in range(batch)]
+    S = getattr(dsp, f"arm_fir_instance_{kind}")()
+    S.numTaps = taps
+    dc = torch.from_numpy(c.copy()).cuda()
+    S.pCoeffs = C.cast(dc.data_ptr(), S._fields_[2][1])
+    hist = torch.zeros((batch, taps - 1), dtype=dc.dtype, device="cuda")
+    for k in range(2):
+        buf = torch.from_numpy(np.stack([blocks[f][k] for f in range(batch)])).cuda()
+        dsp.fir_batch(S, buf, buf, hist, kind=kind)
+        torch.cuda.synchronize()
+        got = buf.cpu().numpy()
+        for f in range(batch):
+            assert got[f].tobytes() == want[f][k].tobytes(), (k, f)
+
+
+@pytest.mark.parametrize("fn", ["correlate_f32", "correlate_q15", "correlate_q31", "conv_fast_q15",
+                                "conv_fast_q31", "correlate_fast_q31"])
+def test_conv_family_same_base_pointer_shorter_first(dsp, torch_gpu, ref, fn):
+    """pSrcA and pSrcB share one base address with srcALen < srcBLen (e.g.
+    arm_correlate_f32(x, 5, x, 10)): the operand swap must follow the lengths, not the
+    pointers.  Drop-in (host and device pointers) and batched."""
+    torch = torch_gpu
+    x = refs.rand_input(fn[-3:], 300, seed=3)
+    for la, lb in ((5, 10), (17, 250)):
+        want, _ = ref.conv_family(fn, x[:la], x[:lb], fill=0)
+        got, _ = dsp.arm_conv_family(fn, x[:la], x[:lb], fill=0)
+        assert got.tobytes() == want.tobytes(), (la, lb)
+        d = torch.from_numpy(x.copy()).cuda()
+        n = len(want)
+        out = torch.zeros(n, dtype=d.dtype, device="cuda")
+        getattr(dsp.lib, f"arm_{fn}")(C.c_void_p(d.data_ptr()), la, C.c_void_p(d.data_ptr()), lb,
+                                      C.c_void_p(out.data_ptr()))
+        dsp._check_void(fn)
+        assert out.cpu().numpy().tobytes() == want.tobytes(), (la, lb)
+        outb = torch.zeros((1, n), dtype=d.dtype, device="cuda")
+        dsp.conv_family_batch(fn, d[:la].view(1, la), d[:lb].view(1, lb), outb)
+        torch.cuda.synchronize()
+        assert outb[0].cpu().numpy().tobytes() == want.tobytes(), (la, lb)
+
+
+# ------------------------------------------------------------------ user tables by content
+def test_user_tables_follow_their_contents(dsp, torch_gpu, ref):
+    """A user twiddle table and a user bit-reversal table are rewritten IN PLACE between two
+    calls (same address, new words): the second call must use the new words."""
+    n = 64
+    tw = np.ctypeslib.as_array(C.cast(dsp.const_instance("arm_cfft_sR_f32_len64").pTwiddle,
+                                      C.POINTER(C.c_float)), (2 * n,)).copy()
+    tab = np.array([8 * 1, 8 * 5, 8 * 2, 8 * 9], dtype=np.uint16)
+    x = refs.rand_input("f32", 2 * n, seed=21)
+    for variant in range(2):
+        if variant:                       # new contents at the same addresses
+            tw[1::2] *= -1.0              # conjugate twiddles: a different (but valid) transform
+            tab[:] = [8 * 3, 8 * 7, 8 * 4, 8 * 60]
+        S = dsp.arm_cfft_instance_f32()
+        dsp.arm_cfft_init_f32(S, n)
+        S.pTwiddle = tw.ctypes.data_as(C.POINTER(C.c_float))
+        S.pBitRevTable = tab.ctypes.data_as(C.POINTER(C.c_uint16))
+        S.bitRevLength = len(tab)
+        got = dsp.arm_cfft_f32(S, x, 0, 1)
+        Sr = ref.cfft_instance("f32", n)
+        Sr.pTwiddle = tw.ctypes.data_as(C.POINTER(C.c_float))
+        Sr.pBitRevTable = tab.ctypes.data_as(C.POINTER(C.c_uint16))
+        Sr.bitRevLength = len(tab)
+        buf = x.copy()
+        ref.fn("arm_cfft_f32")(C.byref(Sr), buf.ctypes.data, 0, 1)
+        assert got.tobytes() == buf.tobytes(), variant
+
+
+def test_device_resident_twiddles_used_in_place(dsp, torch_gpu, ref):
+    """An instance whose twiddle table is a device pointer is used without a copy, and a
+    change of those device words is seen by the next call."""
+    torch = torch_gpu
+    import ctypes
+    n = 1024
+    base = dsp.const_instance("arm_cfft_sR_f32_len1024")
+    host_tw = np.ctypeslib.as_array(ctypes.cast(base.pTwiddle, ctypes.POINTER(ctypes.c_float)), (2 * n,)).copy()
+    dtw = torch.from_numpy(host_tw.copy()).cuda()
+    S = dsp.arm_cfft_instance_f32()
+    dsp.arm_cfft_init_f32(S, n)
+    S.pTwiddle = ctypes.cast(dtw.data_ptr(), ctypes.POINTER(ctypes.c_float))
+    x = np.stack([refs.rand_input("f32", 2 * n, seed=s) for s in range(3)])
+    for variant in range(2):
+        if variant:
+            dtw[1::2] *= -1.0
+            host_tw[1::2] *= -1.0
+        d = torch.from_numpy(x.copy()).cuda()
+        dsp.cfft_batch(S, d, 0, 1)
+        torch.cuda.synchronize()
+        Sr = ref.cfft_instance("f32", n)
+        Sr.pTwiddle = host_tw.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+        want = np.stack([_ref_cfft(ref, Sr, r) for r in x])
+        assert d.cpu().numpy().tobytes() == want.tobytes(), variant
+
+
+def _ref_cfft(ref, S, row):
+    buf = row.copy()
+    ref.fn("arm_cfft_f32")(C.byref(S), buf.ctypes.data, 0, 1)
+    return buf
+
+
+# ------------------------------------------------------------------ pinned staging
+def test_dropin_pinned_staging_repeated_sizes(dsp, torch_gpu, ref):
+    """The drop-in host path reuses its pinned bounce buffers across calls of growing and
+    shrinking sizes without mixing up words."""
+    for n in (4096, 16, 1024, 64, 4096):
+        x = refs.rand_input("q31", 2 * n, seed=n)
+        S = dsp.arm_cfft_instance_q31()
+        dsp.arm_cfft_init_q31(S, n)
+        assert dsp.arm_cfft_q31(S, x, 0, 1).tobytes() == ref.cfft("q31", n, x, 0, 1).tobytes()
+    a = refs.rand_input("f32", 40 * 33, seed=1).reshape(40, 33)
+    b = refs.rand_input("f32", 33 * 21, seed=2).reshape(33, 21)
+    st, c = dsp.arm_mat_mult_f32(a, b)
+    assert st == 0
+    np.testing.assert_allclose(c, a.astype(np.float64) @ b.astype(np.float64), rtol=1e-5, atol=1e-5)
