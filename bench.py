@@ -37,6 +37,7 @@ FP32_NOFMA_TFLOPS = 78.6     # separate v_mul_f32 + v_add_f32 (bit-exact FIR)
 METRIC = "Gsamples/sec batched arm_cfft_f32 N=1024 (+ q31 bit-exact) at 1/2/4/8 GPU"
 CONFIG3_GLOBAL_BATCH = 1 << 20   # BASELINE configs[3]: N=4096 batch=1M, sharded
 CPU_THREADS_MAX = 16             # the GPU box's CPU share per GPU
+SETTLE_MS = 40.0                 # device time of untimed launches before the W warmup steps
 
 WORKLOADS = {
     # name: (kind, fftLen / taps, default batch per GPU, algorithmic bytes per sample)
@@ -233,22 +234,43 @@ def main_rank(args):
     def flag_sequence(steps):
         return [s & 1 for s in range(steps)]            # fwd, inv, fwd, ...
 
+    settle = {"launches": 0}
+
     def time_launches(launch, steps, warmup):
-        """W untimed, then K timed launches between barriers; returns (wall s, avg kernel ms).
-        The HIP events are recorded on the stream the library launches on (torch's current)."""
-        for s in range(warmup):
-            launch(s)
-        parallel.barrier(world)
+        """Clock settle, W untimed, then K timed launches between barriers; returns (wall s,
+        avg kernel ms).  The settle phase repeats the launch until >= SETTLE_MS of device
+        time has passed (at most 64 launches): the GPU's power management dips the clock for
+        the first ~10-30 ms of a sustained load (kernel traces: the first launch is fast, the
+        next few 5-30 % slow, then steady), which W short warmup steps do not cover.  The
+        number of settle launches is reported (settle_launches) and every launch, settle
+        included, is replayed by the parity check.  The HIP events are recorded on the stream
+        the library launches on (torch's current stream)."""
         stream = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s = 0
+        e0.record(stream)
+        while s < 64:
+            launch(s)
+            s += 1
+            e1.record(stream)
+            e1.synchronize()
+            if e0.elapsed_time(e1) >= SETTLE_MS:
+                break
+        settle["launches"] = s
+        for w in range(warmup):
+            launch(s + w)
+        s += warmup
+        parallel.barrier(world)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
         t0 = time.perf_counter()
-        for s in range(steps):
-            evs[s][0].record(stream)
-            launch(warmup + s)
-            evs[s][1].record(stream)
+        for k in range(steps):
+            evs[k][0].record(stream)
+            launch(s + k)
+            evs[k][1].record(stream)
         parallel.barrier(world)
         wall = time.perf_counter() - t0
         kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        settle["total"] = s + steps
         return wall, kern_ms
 
     # ---------------------------------------------------------------- workloads
@@ -264,12 +286,12 @@ def main_rank(args):
             batch = strong_span[1]
         rows = sorted({0, 1, batch // 2, batch - 1})
         before = data[rows].cpu().numpy().copy()
-        flags = flag_sequence(warmup + steps)
 
         def launch(s):
-            dsp.cfft_batch(S, data, flags[s], 1)
+            dsp.cfft_batch(S, data, s & 1, 1)          # fwd, inv, fwd, ...
 
         wall, kern_ms = time_launches(launch, steps, warmup)
+        flags = flag_sequence(settle["total"])
         host, hk = cpu_checker()
         want = before
         for f in flags:
@@ -521,7 +543,8 @@ def main_rank(args):
     line = {"metric": METRIC, "n_gpus": world_n, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True, "scaling": scaling,
             "vs_baseline": None, "data": "synthetic (device generator seeded per rank / per global block; no scatter)",
-            "ranks": world_n, "devices_used": devices, "dist_backend": world.backend}
+            "ranks": world_n, "devices_used": devices, "dist_backend": world.backend,
+            "settle_launches": settle["launches"]}
     if args.workload == "mat_mult_fast_q31":
         ops = 2.0 * n * n * n * batch
         line.update(value=round(total_units * 2.0 * n ** 3 / wall * 1e-12, 4), unit="TOPS (2*M*N*K int MAC)",
@@ -552,8 +575,8 @@ def main_rank(args):
         achieved = flops / (kern_ms * 1e-3) * 1e-12
         line["roofline"] = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                             "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-                            "traffic": pmc_traffic(args.workload), "avg_kernel_ms": round(kern_ms, 4),
-                            "mfma_busy": pmc_field(args.workload, "mfma_busy_frac")}
+                            "traffic": pmc_traffic(args.workload, batch), "avg_kernel_ms": round(kern_ms, 4),
+                            "mfma_busy": pmc_field(args.workload, "mfma_busy_frac", batch)}
     else:
         line.update(value=round(total_units / wall * 1e-9, 3), unit="Gsamples/s",
                     dtype={"f32": "f32", "q31": "q31 (int32)", "q15": "q15 (int16)", "fir_f32": "f32",
@@ -595,8 +618,10 @@ def main_rank(args):
                               "numTaps": n, "blockSize": 4096,
                               "batch_per_gpu": batch, "parallelism": f"dp{world_n} shards"}
         achieved = algo_bytes / (kern_ms * 1e-3) * 1e-9
+        prof = (f"{args.workload}_strong{args.global_batch >> 20}M" if scaling == "strong" and args.global_batch % (1 << 20) == 0
+                else args.workload if not args.fftlen else f"cfft_{kind}_{n}")
         line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.workload),
+                            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(prof, batch),
                             "algorithmic_bytes_per_launch": algo_bytes, "avg_kernel_ms": round(kern_ms, 4)}
         if args.workload == "conv_f32":
             valu = units * n * 2 / (kern_ms * 1e-3) * 1e-12
@@ -630,10 +655,12 @@ def main_rank(args):
             biggest = max(r["span"][1] for r in p2["per_rank"])
             ach = biggest * 4096 * qbps / (k2 * 1e-3) * 1e-9
             c3[qk] = {"value": round(args.global_batch * 4096 * args.steps / w2 * 1e-9, 3), "unit": "Gsamples/s",
+                      "settle_launches": settle["launches"],
                       "ms_per_step": round(w2 / args.steps * 1e3, 4), "dtype": "q31 (int32)" if qk == "q31" else
                       "q15 (int16)", "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                                                   "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                                                  "traffic": pmc_traffic(f"cfft_{qk}_4096"),
+                                                  "traffic": pmc_traffic(f"cfft_{qk}_4096_strong1M", biggest)
+                                                  if args.global_batch == 1 << 20 else None,
                                                   "algorithmic_bytes_per_launch": biggest * 4096 * qbps,
                                                   "avg_kernel_ms": round(k2, 4)},
                       "parity": p2}
@@ -670,16 +697,25 @@ def dry_run(args, world, parallel):
     return 0
 
 
-def pmc_field(workload, field):
+def pmc_field(name, field, launch_items=None):
+    """A field of the committed rocprofv3 PMC record `name` (profiles/pmc_traffic.json,
+    written by tools/profile_collect.py), or None.  launch_items: the items (transforms,
+    filters, matrices) one launch of this run processes; the record is used only when its
+    profiled run launched the same number."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
-    return json.load(open(p)).get(workload, {}).get(field)
+    rec = json.load(open(p)).get(name, {})
+    cfg = rec.get("bench_config") or {}
+    items = cfg.get("batch_per_gpu", cfg.get("global_batch"))
+    if launch_items is not None and items != launch_items:
+        return None
+    return rec.get(field)
 
 
-def pmc_traffic(workload):
+def pmc_traffic(name, launch_items=None):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, when present."""
-    return pmc_field(workload, "hbm_bytes_per_launch")
+    return pmc_field(name, "hbm_bytes_per_launch", launch_items)
 
 
 def main(argv=None):

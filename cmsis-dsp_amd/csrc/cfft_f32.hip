@@ -127,7 +127,13 @@ __device__ __forceinline__ int s1024(int e) {
 #ifndef MI355X_N1024_WPB
 #define MI355X_N1024_WPB 8
 #endif
-constexpr int kN1024T = MI355X_N1024_T, kN1024Wpb = MI355X_N1024_WPB;
+// N1024_SPLIT = S > 1: workgroup b works in region b % S of the batch (S contiguous regions,
+// each S-th dispatched workgroup in the same region), so S address streams far apart are
+// live at once instead of one sliding window (grid % S != 0 falls back to S = 1).
+#ifndef MI355X_N1024_SPLIT
+#define MI355X_N1024_SPLIT 1
+#endif
+constexpr int kN1024T = MI355X_N1024_T, kN1024Wpb = MI355X_N1024_WPB, kN1024Split = MI355X_N1024_SPLIT;
 // Each wave owns its LDS image, so the exchanges need only a wave-level barrier: one
 // wave's LDS operations complete in issue order; the fences stop the compiler from moving
 // accesses across the exchange.
@@ -141,7 +147,10 @@ __global__ __launch_bounds__(64 * kN1024Wpb, MI355X_N1024_WAVES) void cfft_f32_n
   __shared__ __attribute__((aligned(16))) float2 lds_all[kN1024Wpb][16 * 72];
   const int l = threadIdx.x & 63;
   float2* lds = lds_all[threadIdx.x >> 6];
-  const uint32_t wave = blockIdx.x * kN1024Wpb + (threadIdx.x >> 6);
+  uint32_t vb = blockIdx.x;
+  if (kN1024Split > 1 && gridDim.x % kN1024Split == 0)
+    vb = (blockIdx.x % kN1024Split) * (gridDim.x / kN1024Split) + blockIdx.x / kN1024Split;
+  const uint32_t wave = vb * kN1024Wpb + (threadIdx.x >> 6);
   const uint32_t t_begin = kN1024T ? wave * kN1024T : wave;
   const uint32_t t_end = kN1024T ? min(batch, t_begin + kN1024T) : batch;
   const uint32_t t_step = kN1024T ? 1u : gridDim.x * kN1024Wpb;

@@ -22,7 +22,7 @@
 
 namespace mi355x {
 
-constexpr int kFirR = 8;                       // outputs per lane
+constexpr int kFirR = 8;                       // outputs per lane (fixed-point kernels)
 constexpr int kFirChunk = kBlock * kFirR;      // outputs per workgroup (2048)
 constexpr int kFirMaxTaps = 1024;              // LDS budget: (2048 + 1023) * 4 B
 
@@ -34,11 +34,12 @@ struct FirItem {
   uint32_t f;
   int n0, count, total;   // first output, outputs in the chunk, window samples (count + T - 1)
 };
-__device__ __forceinline__ FirItem fir_item(uint32_t item, uint32_t nchunks, uint32_t B, int T1) {
+__device__ __forceinline__ FirItem fir_item(uint32_t item, uint32_t nchunks, uint32_t B, int T1,
+                                            int chunk = kFirChunk) {
   FirItem it;
   it.f = item / nchunks;
-  it.n0 = (int)(item - it.f * nchunks) * kFirChunk;
-  it.count = min((int)B - it.n0, kFirChunk);
+  it.n0 = (int)(item - it.f * nchunks) * chunk;
+  it.count = min((int)B - it.n0, chunk);
   it.total = it.count + T1;
   return it;
 }
@@ -55,7 +56,19 @@ __device__ __forceinline__ T fir_sample(const T* __restrict__ hist, const T* __r
 }
 
 // ---------------------------------------------------------------- f32
-constexpr int kFirPre = (kFirChunk + kFirMaxTaps - 1 + kBlock - 1) / kBlock;   // window samples per thread
+#ifndef MI355X_FIR_F32_R
+#define MI355X_FIR_F32_R 8
+#endif
+// Coefficients: 1 = staged once per workgroup in LDS and read as wave-wide broadcasts (the
+// LDS queue is then the only lgkm traffic in the tap loop, so partial lgkmcnt waits work);
+// 0 = scalar loads from global memory (each s_load forces an lgkmcnt(0) that also drains
+// the window reads in flight).
+#ifndef MI355X_FIR_F32_COEF_LDS
+#define MI355X_FIR_F32_COEF_LDS 1
+#endif
+constexpr int kF32R = MI355X_FIR_F32_R;                 // outputs per lane
+constexpr int kF32Chunk = kBlock * kF32R;              // outputs per workgroup
+constexpr int kFirPre = (kF32Chunk + kFirMaxTaps - 1 + kBlock - 1) / kBlock;   // window samples per thread
 
 // LDS index with one pad word every 8: lanes read at a stride of R = 8 words from any
 // offset, and i + i/8 keeps every ds_read_b32 32-lane group on 32 distinct banks (one
@@ -75,12 +88,19 @@ __global__ __launch_bounds__(kBlock) void fir_f32_kernel(const float* __restrict
                                                          const float* __restrict__ src, float* __restrict__ dst,
                                                          uint32_t B, const float* __restrict__ hist_in,
                                                          uint32_t nchunks, uint32_t items) {
-  __shared__ float win[(kFirChunk + kFirMaxTaps) * 9 / 8 + 32];
+  __shared__ float win[(kF32Chunk + kFirMaxTaps) * 9 / 8 + 32];
   const int T1 = T - 1;
   uint32_t item = blockIdx.x;
   if (item >= items) return;
+#if MI355X_FIR_F32_COEF_LDS
+  __shared__ __attribute__((aligned(16))) float cl[kFirMaxTaps];
+  for (int i = threadIdx.x; i < T; i += kBlock) cl[i] = coeffs[i];   // visible after the loop's barriers
+  const float* cf = cl;
+#else
+  const float* cf = coeffs;
+#endif
   float pre[kFirPre];
-  FirItem it = fir_item(item, nchunks, B, T1);
+  FirItem it = fir_item(item, nchunks, B, T1, kF32Chunk);
   fir_f32_fetch(pre, hist_in, src, it, B, T1);
   for (; item < items; item += gridDim.x) {
     __syncthreads();                                // the previous item is done with win
@@ -92,42 +112,43 @@ __global__ __launch_bounds__(kBlock) void fir_f32_kernel(const float* __restrict
     __syncthreads();
     const FirItem cur = it;
     if (item + gridDim.x < items) {
-      it = fir_item(item + gridDim.x, nchunks, B, T1);
+      it = fir_item(item + gridDim.x, nchunks, B, T1, kF32Chunk);
       fir_f32_fetch(pre, hist_in, src, it, B, T1);  // in flight during the MACs below
     }
 
-    const int base = threadIdx.x * kFirR;           // local output index of this lane
+    const int base = threadIdx.x * kF32R;           // local output index of this lane
     if (base < cur.count) {
       // w is a ring over s[base + k .. base + k + R-1]; k advances R taps per unrolled round,
       // so every ring index is a compile-time constant (no register shuffling).
-      float acc[kFirR], w[kFirR];
+      float acc[kF32R], w[kF32R];
 #pragma unroll
-      for (int r = 0; r < kFirR; ++r) { acc[r] = 0.0f; w[r] = win[padx(base + r)]; }
+      for (int r = 0; r < kF32R; ++r) { acc[r] = 0.0f; w[r] = win[padx(base + r)]; }
       int k = 0;
-      for (; k + kFirR <= T; k += kFirR) {
+      for (; k + kF32R <= T; k += kF32R) {
 #pragma unroll
-        for (int u = 0; u < kFirR; ++u) {
-          const float c = coeffs[k + u];
+        for (int u = 0; u < kF32R; ++u) {
+          const float c = cf[k + u];
 #pragma unroll
-          for (int r = 0; r < kFirR; ++r) acc[r] = acc[r] + w[(r + u) % kFirR] * c;
-          w[u] = win[padx(base + k + u + kFirR)];
+          for (int r = 0; r < kF32R; ++r) acc[r] = acc[r] + w[(r + u) % kF32R] * c;
+          w[u] = win[padx(base + k + u + kF32R)];
         }
       }
       for (; k < T; ++k) {
-        const float c = coeffs[k];
+        const float c = cf[k];
 #pragma unroll
-        for (int r = 0; r < kFirR; ++r) acc[r] = acc[r] + w[r] * c;
+        for (int r = 0; r < kF32R; ++r) acc[r] = acc[r] + w[r] * c;
 #pragma unroll
-        for (int r = 0; r < kFirR - 1; ++r) w[r] = w[r + 1];
-        w[kFirR - 1] = win[padx(base + kFirR + k)];
+        for (int r = 0; r < kF32R - 1; ++r) w[r] = w[r + 1];
+        w[kF32R - 1] = win[padx(base + kF32R + k)];
       }
       float* o = dst + (uint64_t)cur.f * B + cur.n0 + base;
-      if ((B & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + kFirR <= cur.count) {
-        reinterpret_cast<float4*>(o)[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-        reinterpret_cast<float4*>(o)[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+      if ((B & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + kF32R <= cur.count) {
+#pragma unroll
+        for (int q = 0; q < kF32R / 4; ++q)
+          reinterpret_cast<float4*>(o)[q] = make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
       } else {
 #pragma unroll
-        for (int r = 0; r < kFirR; ++r)
+        for (int r = 0; r < kF32R; ++r)
           if (base + r < cur.count) o[r] = acc[r];
       }
     }
@@ -480,7 +501,8 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
   if (batch == 0 || B == 0) return hipSuccess;
   if (T_ < 1 || T_ > kFirMaxTaps) return hipErrorInvalidValue;
   const int T1 = T_ - 1;
-  const uint32_t nchunks = (B + kFirChunk - 1) / kFirChunk;
+  const int chunk = kind == kFirF32 ? kF32Chunk : kFirChunk;
+  const uint32_t nchunks = (B + chunk - 1) / chunk;
   const uint64_t items64 = (uint64_t)nchunks * batch;
   if (items64 > 0xFFFFFFFFull) return hipErrorInvalidValue;
   const uint32_t items = (uint32_t)items64;

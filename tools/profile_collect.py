@@ -1,0 +1,153 @@
+#!/usr/bin/env python3
+"""Collect tools/profile_round.sh output into profiles/<round>/<name>/ and
+profiles/pmc_traffic.json.
+
+Per workload:
+  * kernel_trace.json — every kernel's dispatches from the --kernel-trace pass, averaged
+    over the TIMED launches only (the dispatches with the kernel's largest grid: bench.py
+    also launches it on small parity batches), next to the bench line's live HIP-event
+    average of the same run (agreement ratio);
+  * pmc.json — per-dispatch counter averages of the dominant kernel over its largest-grid
+    dispatches, HBM bytes per launch (read = 2 x FETCH_SIZE: gfx950 tallies wide coalesced
+    reads at half, MI355X_MICROARCH.md §HBM, cross-checked with TCC_EA0_RDREQ x 128; write
+    = WRITE_SIZE), the effective clock (GRBM_GUI_ACTIVE per XCD over the kernel time) and,
+    for MFMA kernels, MFMA busy cycles as a fraction of the SIMD cycles of the launch;
+  * run_kernel_stats.csv — rocprofv3's own --stats summary (all dispatches).
+pmc_traffic.json keys: the profile name; bench.py uses a record only when its recorded
+bench config equals the line's config.
+Usage: profile_collect.py <round> [name ...]
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from profile_specs import SPECS  # noqa: E402
+
+N_XCD, N_SIMD = 8, 1024
+
+
+def _grid(row):
+    if "Grid_Size" in row and row["Grid_Size"]:
+        return int(row["Grid_Size"])
+    return int(row.get("Grid_Size_X", 0) or 0) * int(row.get("Grid_Size_Y", 1) or 1) * int(row.get("Grid_Size_Z", 1) or 1)
+
+
+def bench_line(path):
+    try:
+        for ln in open(path):
+            if ln.startswith("{"):
+                return json.loads(ln)
+    except OSError:
+        pass
+    return None
+
+
+def trace_summary(d):
+    ks = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            ks[row["Kernel_Name"]].append((_grid(row), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
+    out = {}
+    for k, v in ks.items():
+        g = max(x[0] for x in v)
+        timed = [x[1] for x in v if x[0] == g]
+        out[k] = {"dispatches": len(v), "timed_dispatches": len(timed), "timed_grid": g,
+                  "timed_avg_ms": sum(timed) / len(timed) * 1e-6, "all_avg_ms": sum(x[1] for x in v) / len(v) * 1e-6}
+    return out
+
+
+def pmc_summary(d, ksub):
+    per = defaultdict(lambda: defaultdict(float))     # (pass, dispatch) -> counter -> value
+    grids = {}
+    for f in glob.glob(os.path.join(d, "pmc_*", "**", "*counter_collection.csv"), recursive=True):
+        tag = os.path.relpath(f, d).split(os.sep)[0]
+        for row in csv.DictReader(open(f)):
+            if ksub not in row.get("Kernel_Name", ""):
+                continue
+            key = (tag, row["Dispatch_Id"])
+            grids[key] = _grid(row)
+            per[key][row["Counter_Name"]] += float(row["Counter_Value"])
+    if not per:
+        return None
+    gmax = max(grids.values())
+    acc = defaultdict(list)
+    for key, cs in per.items():
+        if grids[key] == gmax:
+            for name, v in cs.items():
+                acc[name].append(v)
+    return {name: sum(v) / len(v) for name, v in acc.items()}, gmax
+
+
+def main():
+    rnd = sys.argv[1]
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
+    names = sys.argv[2:] or sorted(n for n in os.listdir(src) if os.path.isdir(os.path.join(src, n)))
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
+    index = {}
+    for name in names:
+        d = os.path.join(src, name)
+        ksub = SPECS[name][1]
+        dest = os.path.join(ROOT, "profiles", rnd, name)
+        os.makedirs(dest, exist_ok=True)
+        line = bench_line(os.path.join(d, "bench_trace.json"))
+        tr = trace_summary(d)
+        dom = [k for k in tr if ksub in k]
+        rec = {"name": name, "bench_args": SPECS[name][0], "dominant_kernel_substring": ksub, "kernels": tr,
+               "bench_config": line.get("config") if line else None}
+        if dom:
+            k = max(dom, key=lambda k: tr[k]["timed_avg_ms"] * tr[k]["timed_dispatches"])
+            rec["dominant_kernel"] = k
+            rec["trace_timed_avg_ms"] = tr[k]["timed_avg_ms"]
+            if line and line.get("roofline", {}).get("avg_kernel_ms"):
+                rec["bench_hip_event_avg_ms"] = line["roofline"]["avg_kernel_ms"]
+                rec["trace_over_hip_event"] = tr[k]["timed_avg_ms"] / line["roofline"]["avg_kernel_ms"]
+        for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True):
+            shutil.copy(f, os.path.join(dest, "run_kernel_stats.csv"))
+        json.dump(rec, open(os.path.join(dest, "kernel_trace.json"), "w"), indent=1)
+        pm = pmc_summary(d, ksub)
+        if pm:
+            c, gmax = pm
+            ms = rec.get("trace_timed_avg_ms")
+            p = {"kernel_substring": ksub, "grid": gmax, "counters_per_dispatch": c}
+            if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+                p["read_bytes"] = c["FETCH_SIZE"] * 1024 * 2
+                p["write_bytes"] = c["WRITE_SIZE"] * 1024
+                p["hbm_bytes_per_launch"] = p["read_bytes"] + p["write_bytes"]
+            if "TCC_EA0_RDREQ_sum" in c:
+                p["read_bytes_from_rdreq_x128"] = c["TCC_EA0_RDREQ_sum"] * 128
+            if "GRBM_GUI_ACTIVE" in c and ms:
+                p["effective_clock_ghz"] = c["GRBM_GUI_ACTIVE"] / N_XCD / (ms * 1e6)
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in c and ms and "effective_clock_ghz" in p:
+                simd_cycles = N_SIMD * ms * 1e6 * p["effective_clock_ghz"]
+                p["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cycles
+            if line and line.get("roofline", {}).get("algorithmic_bytes_per_launch") and "hbm_bytes_per_launch" in p:
+                p["traffic_over_algorithmic"] = p["hbm_bytes_per_launch"] / line["roofline"]["algorithmic_bytes_per_launch"]
+            json.dump(p, open(os.path.join(dest, "pmc.json"), "w"), indent=1)
+            rec["pmc"] = {k: v for k, v in p.items() if k != "counters_per_dispatch"}
+            if "hbm_bytes_per_launch" in p or "mfma_busy_frac" in p:
+                traffic[name] = {"hbm_bytes_per_launch": round(p.get("hbm_bytes_per_launch", 0)) or None,
+                                 "read_bytes": round(p.get("read_bytes", 0)), "write_bytes": round(p.get("write_bytes", 0)),
+                                 "mfma_busy_frac": p.get("mfma_busy_frac"), "kernel": rec.get("dominant_kernel", ksub),
+                                 "avg_kernel_ms_trace": ms, "bench_config": rec["bench_config"], "round": rnd,
+                                 "source": f"profiles/{rnd}/{name}/pmc.json"}
+        index[name] = {k: rec.get(k) for k in ("dominant_kernel", "trace_timed_avg_ms", "bench_hip_event_avg_ms",
+                                               "trace_over_hip_event")}
+        index[name].update({k: rec.get("pmc", {}).get(k) for k in ("hbm_bytes_per_launch", "traffic_over_algorithmic",
+                                                                   "effective_clock_ghz", "mfma_busy_frac")})
+    json.dump(traffic, open(tpath, "w"), indent=1, sort_keys=True)
+    ipath = os.path.join(ROOT, "profiles", rnd, "INDEX.json")
+    old = json.load(open(ipath)) if os.path.exists(ipath) else {}
+    old.update(index)
+    json.dump(old, open(ipath, "w"), indent=1, sort_keys=True)
+    print(json.dumps(index, indent=1))
+
+
+if __name__ == "__main__":
+    main()

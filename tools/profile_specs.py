@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Bench command of every profiled workload (tools/profile_round.sh) and the kernel whose
+launches it measures (tools/profile_collect.py).  The timed launches are the dispatches of
+that kernel with the LARGEST grid: bench.py also launches it on small parity batches.
+Usage: profile_specs.py <name>  -> prints the bench.py arguments."""
+import sys
+
+# name: (bench.py arguments, kernel-name substring of the dominant kernel, unused)
+SPECS = {
+    "cfft_f32_1024": ("--workload cfft_f32_1024 --no-config3 --steps 10 --warmup 3", "n1024", ""),
+    "cfft_q31_4096_strong1M": ("--workload cfft_q31_4096 --scaling strong --global-batch 1048576 --steps 6 --warmup 2",
+                               "fx4096", ""),
+    "cfft_q15_4096_strong1M": ("--workload cfft_q15_4096 --scaling strong --global-batch 1048576 --steps 6 --warmup 2",
+                               "q15_4096_pk", ""),
+    "cfft_f32_2048": ("--fftlen 2048 --no-config3 --steps 10 --warmup 3", "n2048", ""),
+    "cfft_f32_4096": ("--fftlen 4096 --no-config3 --steps 10 --warmup 3", "n4096", ""),
+    "rfft_f32": ("--workload rfft_f32 --steps 10 --warmup 3", "rfft_fused", ""),
+    "rfft_q31": ("--workload rfft_q31 --steps 10 --warmup 3", "fx4096", ""),
+    "rfft_q15": ("--workload rfft_q15 --steps 10 --warmup 3", "q15_4096_pk", ""),
+    "fir_f32": ("--workload fir_f32 --steps 10 --warmup 3", "fir_f32_kernel", ""),
+    "fir_q15": ("--workload fir_q15 --steps 10 --warmup 3", "fir_q15_kernel", ""),
+    "fir_q31": ("--workload fir_q31 --steps 10 --warmup 3", "fir_q31_kernel", ""),
+    "fir_fast_q15": ("--workload fir_fast_q15 --steps 10 --warmup 3", "fir_q15_kernel", ""),
+    "fir_fast_q31": ("--workload fir_fast_q31 --steps 10 --warmup 3", "fir_q31_kernel", ""),
+    "conv_f32": ("--workload conv_f32 --steps 10 --warmup 3", "conv_kernel", ""),
+    "mfcc_f32": ("--workload mfcc_f32 --steps 10 --warmup 3", "mfcc_fused", ""),
+    "mat_mult_f32": ("--workload mat_mult_f32 --steps 6 --warmup 2", "mat_mult_f32_full", ""),
+    "mat_mult_q15": ("--workload mat_mult_q15 --steps 6 --warmup 2", "mat_mult_i8v2", ""),
+    "mat_mult_q31": ("--workload mat_mult_q31 --steps 6 --warmup 2", "mat_mult_i8v2", ""),
+    "mat_mult_fast_q31": ("--workload mat_mult_fast_q31 --steps 6 --warmup 2", "mat_mult_fast_q31", ""),
+}
+
+if __name__ == "__main__":
+    print(SPECS[sys.argv[1]][0])
