@@ -410,14 +410,28 @@ constexpr uint32_t kFxT = MI355X_FX_T;
 #ifndef MI355X_FX_WAVES
 #define MI355X_FX_WAVES 1     // minimum waves per SIMD the register allocation must allow
 #endif
-template <typename T, bool INV>
+// MI355X_FX_TW3_LDS = 1: the pass-2 (stage-3) twiddles tw[(k+1)*16m], m < 64, live in a
+// 1.5 KiB LDS table instead of 24 VGPRs per lane.  MI355X_FX_PF = 1: the next transform's
+// 16 loads are held in registers under passes 2-3 (32 VGPRs for q31).
+#ifndef MI355X_FX_TW3_LDS
+#define MI355X_FX_TW3_LDS 0
+#endif
+#ifndef MI355X_FX_PF
+#define MI355X_FX_PF 1
+#endif
+#ifndef MI355X_FX_TW4_LDS          // stage-4 twiddles tw[(k+1)*64*j2], j2 < 16: 384 B of LDS
+#define MI355X_FX_TW4_LDS 0
+#endif
+// BREV / SAT are the bitReverseFlag and the RFFT inverse's saturating <<1 (kSatShl1) as
+// template parameters: as run-time flags the compiler if-converted them into selects on
+// every output word and address.
+template <typename T, bool INV, bool BREV, bool SAT>
 __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typename Fx<T>::C* __restrict__ data, uint32_t batch,
-                                                          const typename Fx<T>::C* __restrict__ tw, uint32_t flags) {
+                                                          const typename Fx<T>::C* __restrict__ tw) {
   using F = Fx<T>;
   using C = typename F::C;
   __shared__ __attribute__((aligned(16))) C lds[4351];
   const int t = threadIdx.x;
-  const bool brev = flags & kBitrev;
   const int q2 = t >> 4, j2 = t & 15;
   const int q3 = (int)(__brev((uint32_t)t) >> 24);        // rev8(t)
 
@@ -427,7 +441,18 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
   // the cache-resident table every transform instead of pinned in VGPRs.
   C tw2[3], tw4[3], tw5[4][3];
 #if MI355X_FX_TW_REGS
-  C tw1[4][3], tw3[4][3];
+  C tw1[4][3];
+#if !MI355X_FX_TW3_LDS
+  C tw3[4][3];
+#endif
+#endif
+#if MI355X_FX_TW3_LDS
+  __shared__ __attribute__((aligned(16))) C tw3l[64 * 3];
+  if (t < 192) tw3l[t] = tw[(t % 3 + 1) * (t / 3) * 16];        // visible after the loop's barriers
+#endif
+#if MI355X_FX_TW4_LDS
+  __shared__ __attribute__((aligned(16))) C tw4l[16 * 3];
+  if (t < 48) tw4l[t] = tw[(t % 3 + 1) * 64 * (t / 3)];
 #endif
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
@@ -436,18 +461,33 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
     for (int k = 0; k < 3; ++k) {
 #if MI355X_FX_TW_REGS
       tw1[a][k] = tw[(k + 1) * (t + 256 * a)];
+#if !MI355X_FX_TW3_LDS
       tw3[a][k] = tw[(k + 1) * (j2 + 16 * a) * 16];
+#endif
 #endif
       tw5[a][k] = tw[(k + 1) * ia5];
     }
   }
 #pragma unroll
-  for (int k = 0; k < 3; ++k) { tw2[k] = tw[(k + 1) * 4 * t]; tw4[k] = tw[(k + 1) * 64 * j2]; }
+  for (int k = 0; k < 3; ++k) {
+    tw2[k] = tw[(k + 1) * 4 * t];
+#if !MI355X_FX_TW4_LDS
+    tw4[k] = tw[(k + 1) * 64 * j2];
+#endif
+  }
 #if MI355X_FX_TW_REGS
 #define TW1(a, k) tw1[a][k]
 #define TW2(k) tw2[k]
+#if MI355X_FX_TW3_LDS
+#define TW3(a, k) tw3l[(j2 + 16 * (a)) * 3 + (k)]
+#else
 #define TW3(a, k) tw3[a][k]
+#endif
+#if MI355X_FX_TW4_LDS
+#define TW4(k) tw4l[j2 * 3 + (k)]
+#else
 #define TW4(k) tw4[k]
+#endif
 #else
 #define TW1(a, k) twl[((k) + 1) * (t + 256 * (a))]
 #define TW2(k) tw2[k]
@@ -462,23 +502,42 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
   const uint32_t tr_end = kFxT ? min(batch, tr_begin + kFxT) : batch;
   const uint32_t tr_step = kFxT ? 1u : gridDim.x;
   int2 v[16];
-  C nv[16];                             // prefetch in the storage type (q15: one VGPR per complex)
-  if (tr_begin < tr_end) {
-    const C* X0 = data + (size_t)tr_begin * 4096;
+  // register prefetch MI355X_FX_PF transforms deep (0 = load at the top of each transform):
+  // nq[d] holds transform tr + (d+1) * step, in the storage type (q15: one VGPR per complex)
+  constexpr int PFD = MI355X_FX_PF > 0 ? MI355X_FX_PF : 1;
+  C nq[PFD][16];
+#if MI355X_FX_PF
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+  for (int d = 0; d < PFD; ++d) {
+    const uint32_t tp = tr_begin + d * tr_step;
+    if (tp < tr_end) {
+      const C* X0 = data + (size_t)tp * 4096;
 #pragma unroll
-      for (int b = 0; b < 4; ++b) nv[4 * a + b] = X0[t + 256 * a + 1024 * b];
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) nq[d][4 * a + b] = X0[t + 256 * a + 1024 * b];
+    }
   }
+#endif
   for (uint32_t tr = tr_begin; tr < tr_end; tr += tr_step) {
     C* X = data + (size_t)tr * 4096;
 #if !MI355X_FX_TW_REGS
     const C* twl = tw;
     asm volatile("" : "+s"(twl));      // opaque per transform: keeps the re-reads in the loop
 #endif
+#if !MI355X_FX_PF
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) nq[0][4 * a + b] = X[t + 256 * a + 1024 * b];
+#endif
     // ---------------- pass 1: stages 1 (first) and 2
 #pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = W(nv[u]);
+    for (int u = 0; u < 16; ++u) v[u] = W(nq[0][u]);
+#pragma unroll
+    for (int d = 0; d + 1 < PFD; ++d)
+#pragma unroll
+      for (int u = 0; u < 16; ++u) nq[d][u] = nq[d + 1][u];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
       bfly<T, INV, 0>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], W(TW1(a, 0)), W(TW1(a, 1)), W(TW1(a, 2)));
@@ -489,13 +548,15 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) F::st(lds + s4096(t + 256 * a + 1024 * b), v[4 * a + b]);
-    if (tr + tr_step < tr_end) {        // next transform's loads fly under passes 2 and 3
-      const C* XN = data + (size_t)(tr + tr_step) * 4096;
+#if MI355X_FX_PF
+    if (tr + PFD * tr_step < tr_end) {  // a later transform's loads fly under passes 2 and 3
+      const C* XN = data + (size_t)(tr + PFD * tr_step) * 4096;
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) nv[4 * a + b] = XN[t + 256 * a + 1024 * b];
+        for (int b = 0; b < 4; ++b) nq[PFD - 1][4 * a + b] = XN[t + 256 * a + 1024 * b];
     }
+#endif
     __syncthreads();
     // ---------------- pass 2: stages 3 and 4
     {
@@ -528,11 +589,11 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 #pragma unroll
     for (int a = 0; a < 4; ++a)
       bfly<T, INV, 2>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], int2{}, int2{}, int2{});
-    if (flags & kSatShl1) {
+    if constexpr (SAT) {
 #pragma unroll
       for (int u = 0; u < 16; ++u) v[u] = sat_shl1<T>(v[u]);
     }
-    if (brev) {
+    if constexpr (BREV) {
 #pragma unroll
       for (int u = 0; u < 16; ++u) F::st(X + (int)(__brev((uint32_t)u) >> 28) * 256 + t, v[u]);
     } else {
@@ -558,12 +619,14 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 // Each twiddle is held as the two packed words its products need (forward {w.x, w.y} and
 // {~w.y, w.x}; inverse {w.x, ~w.y} and {w.y, w.x}).  Same work mapping as
 // cfft_fx4096_kernel (three radix-16 register passes, s4096 LDS padding, free bit reversal).
-template <bool INV>
+#ifndef MI355X_FX_Q15_PFD
+#define MI355X_FX_Q15_PFD 2
+#endif
+template <bool INV, bool BREV, bool SAT>
 __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_q15_4096_pk_kernel(short2* __restrict__ data, uint32_t batch,
-                                                                    const short2* __restrict__ tw, uint32_t flags) {
+                                                                    const short2* __restrict__ tw) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4351];
   const int t = threadIdx.x;
-  const bool brev = flags & kBitrev;
   const int q2 = t >> 4, j2 = t & 15;
   const int q3 = (int)(__brev((uint32_t)t) >> 24);        // rev8(t)
   TwP tw1[4][3], tw3[4][3], tw2[3], tw4[3], tw5[4][3];
@@ -581,18 +644,30 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_q15_4096_pk_kernel(
 
   const uint32_t* D = reinterpret_cast<const uint32_t*>(data);
   s16x2 v[16];
-  uint32_t nv[16];
-  if (blockIdx.x < batch) {
-    const uint32_t* X0 = D + (size_t)blockIdx.x * 4096;
+  // Register prefetch MI355X_FX_Q15_PFD transforms deep: nq[d] holds transform tr + (d+1)G.
+  // q15 moves 4 B per load, so at the workgroups a CU holds one transform of look-ahead
+  // (16 KiB per workgroup) does not cover the HBM latency; two measured +8.5 %.
+  constexpr int PFD = MI355X_FX_Q15_PFD;
+  uint32_t nq[PFD][16];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+  for (int d = 0; d < PFD; ++d) {
+    const uint32_t tr = blockIdx.x + d * gridDim.x;
+    if (tr < batch) {
+      const uint32_t* X0 = D + (size_t)tr * 4096;
 #pragma unroll
-      for (int b = 0; b < 4; ++b) nv[4 * a + b] = X0[t + 256 * a + 1024 * b];
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) nq[d][4 * a + b] = X0[t + 256 * a + 1024 * b];
+    }
   }
   for (uint32_t tr = blockIdx.x; tr < batch; tr += gridDim.x) {
     uint32_t* X = reinterpret_cast<uint32_t*>(data) + (size_t)tr * 4096;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = pk(nv[u]);
+    for (int u = 0; u < 16; ++u) v[u] = pk(nq[0][u]);
+#pragma unroll
+    for (int d = 0; d + 1 < PFD; ++d)
+#pragma unroll
+      for (int u = 0; u < 16; ++u) nq[d][u] = nq[d + 1][u];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
       bfly_pk<INV, 0>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], tw1[a][0], tw1[a][1], tw1[a][2]);
@@ -603,12 +678,12 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_q15_4096_pk_kernel(
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) lds[s4096(t + 256 * a + 1024 * b)] = upk(v[4 * a + b]);
-    if (tr + gridDim.x < batch) {
-      const uint32_t* XN = D + (size_t)(tr + gridDim.x) * 4096;
+    if (tr + PFD * gridDim.x < batch) {
+      const uint32_t* XN = D + (size_t)(tr + PFD * gridDim.x) * 4096;
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) nv[4 * a + b] = XN[t + 256 * a + 1024 * b];
+        for (int b = 0; b < 4; ++b) nq[PFD - 1][4 * a + b] = XN[t + 256 * a + 1024 * b];
     }
     __syncthreads();
     {
@@ -637,11 +712,11 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_q15_4096_pk_kernel(
     for (int b = 0; b < 4; ++b) bfly_pk<INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], tw5[b][0], tw5[b][1], tw5[b][2]);
 #pragma unroll
     for (int a = 0; a < 4; ++a) bfly_pk<INV, 2>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], z, z, z);
-    if (flags & kSatShl1) {
+    if constexpr (SAT) {
 #pragma unroll
       for (int u = 0; u < 16; ++u) v[u] = pk_sat_add(v[u], v[u]);    // arm_shift_q15(+1): __SSAT(x << 1, 16)
     }
-    if (brev) {
+    if constexpr (BREV) {
 #pragma unroll
       for (int u = 0; u < 16; ++u) X[(int)(__brev((uint32_t)u) >> 28) * 256 + t] = upk(v[u]);
     } else {
@@ -651,29 +726,33 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_q15_4096_pk_kernel(
   }
 }
 
-template <typename T>
-static hipError_t launch_fx4096(void* data, uint32_t batch, const void* tw, uint32_t flags, hipStream_t st) {
+template <typename T, bool INV, bool BREV, bool SAT>
+static void launch_fx4096_t(void* data, uint32_t batch, const void* tw, hipStream_t st) {
   using C = typename Fx<T>::C;
   if constexpr (sizeof(T) == 2 && MI355X_FX_Q15_PACKED) {
-    if (flags & kIfft) {
-      const int grid = persistent_grid((const void*)cfft_q15_4096_pk_kernel<true>, 256, 0, batch);
-      hipLaunchKernelGGL(cfft_q15_4096_pk_kernel<true>, dim3(grid), dim3(256), 0, st, (short2*)data, batch,
-                         (const short2*)tw, flags);
-    } else {
-      const int grid = persistent_grid((const void*)cfft_q15_4096_pk_kernel<false>, 256, 0, batch);
-      hipLaunchKernelGGL(cfft_q15_4096_pk_kernel<false>, dim3(grid), dim3(256), 0, st, (short2*)data, batch,
-                         (const short2*)tw, flags);
-    }
-    return hipGetLastError();
-  }
-  const uint32_t blocks = kFxT ? (batch + kFxT - 1) / (kFxT ? kFxT : 1) : batch;
-  if (flags & kIfft) {
-    const int grid = kFxT ? (int)blocks : persistent_grid((const void*)cfft_fx4096_kernel<T, true>, 256, 0, batch);
-    hipLaunchKernelGGL((cfft_fx4096_kernel<T, true>), dim3(grid), dim3(256), 0, st, (C*)data, batch, (const C*)tw, flags);
+    auto k = cfft_q15_4096_pk_kernel<INV, BREV, SAT>;
+    const int grid = persistent_grid((const void*)k, 256, 0, batch);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (short2*)data, batch, (const short2*)tw);
   } else {
-    const int grid = kFxT ? (int)blocks : persistent_grid((const void*)cfft_fx4096_kernel<T, false>, 256, 0, batch);
-    hipLaunchKernelGGL((cfft_fx4096_kernel<T, false>), dim3(grid), dim3(256), 0, st, (C*)data, batch, (const C*)tw, flags);
+    auto k = cfft_fx4096_kernel<T, INV, BREV, SAT>;
+    const int grid = kFxT ? (int)((batch + kFxT - 1) / (kFxT ? kFxT : 1)) : persistent_grid((const void*)k, 256, 0, batch);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (C*)data, batch, (const C*)tw);
   }
+}
+
+template <typename T, bool INV>
+static void launch_fx4096_i(void* data, uint32_t batch, const void* tw, uint32_t flags, hipStream_t st) {
+  const bool brev = flags & kBitrev, sat = flags & kSatShl1;
+  if (brev && !sat) launch_fx4096_t<T, INV, true, false>(data, batch, tw, st);
+  else if (brev) launch_fx4096_t<T, INV, true, true>(data, batch, tw, st);
+  else if (!sat) launch_fx4096_t<T, INV, false, false>(data, batch, tw, st);
+  else launch_fx4096_t<T, INV, false, true>(data, batch, tw, st);
+}
+
+template <typename T>
+static hipError_t launch_fx4096(void* data, uint32_t batch, const void* tw, uint32_t flags, hipStream_t st) {
+  if (flags & kIfft) launch_fx4096_i<T, true>(data, batch, tw, flags, st);
+  else launch_fx4096_i<T, false>(data, batch, tw, flags, st);
   return hipGetLastError();
 }
 

@@ -79,6 +79,26 @@ __global__ void tchunk_kernel(float* __restrict__ x, float s) {
   }
 }
 
+// tchunk with the N=1024 FFT kernel's widths: 8-B loads (16 per chunk, 512 B per wave
+// instruction) and 16-B stores (8 per chunk), no prefetch.
+template <int T>
+__global__ void tchunk8_kernel(float* __restrict__ x, float s) {
+  const int lane = threadIdx.x & 63;
+  const long c0 = ((long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * T;
+  for (int t = 0; t < T; ++t) {
+    const v2f* q = reinterpret_cast<const v2f*>(x + (c0 + t) * 2048) + lane;
+    v2f r[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) r[m] = __builtin_nontemporal_load(q + 64 * m);
+    v4f* o = reinterpret_cast<v4f*>(x + (c0 + t) * 2048) + lane;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      v4f w = {r[2 * m].x, r[2 * m].y, r[2 * m + 1].x, r[2 * m + 1].y};
+      __builtin_nontemporal_store(w * s, o + 64 * m);
+    }
+  }
+}
+
 // Each wave T chunks interleaved by the grid (chunk = wave + t * waves), pipelined.
 template <int T>
 __global__ void tstride_kernel(float* __restrict__ x, float s) {
@@ -229,6 +249,10 @@ int main() {
 #define COOP(T, WPB) snprintf(nm, 64, "coop T%d wpb%d", T, WPB); \
     timeit(nm, coop_kernel<T, WPB>, dim3(chunks / (T * WPB)), dim3(64 * WPB), x, bytes, e0, e1);
     TCH(4, 8)
+    snprintf(nm, 64, "tchunk8 T4 wpb8");
+    timeit(nm, tchunk8_kernel<4>, dim3(chunks / 32), dim3(512), x, bytes, e0, e1);
+    snprintf(nm, 64, "tchunk8 T4 wpb4");
+    timeit(nm, tchunk8_kernel<4>, dim3(chunks / 16), dim3(256), x, bytes, e0, e1);
     COOP(1, 1) COOP(1, 4) COOP(1, 8) COOP(2, 4) COOP(2, 8) COOP(4, 4) COOP(4, 8) COOP(8, 8) COOP(1, 16) COOP(2, 16)
     timeit("flat U1 nt", flat_kernel<1, true>, dim3(bytes / 16 / 1 / 256), dim3(256), x, bytes, e0, e1);
     timeit("flat U8 nt", flat_kernel<8, true>, dim3(bytes / 16 / 8 / 256), dim3(256), x, bytes, e0, e1);
