@@ -282,8 +282,9 @@ __global__ __launch_bounds__(64 * kN1024Wpb, MI355X_N1024_WAVES) void cfft_f32_n
 // ============================================================================================
 // N = 4096 specialist.  The reference runs four radix-8 DIF stages (arm_cfft_f32.c:1278,
 // arm_radix8_butterfly_f32 with modifier 1: strides 512, 64, 8, 1) and the base-8 digit
-// reversal.  One 256-thread workgroup per transform, persistent, the next transform's 16
-// loads in flight under passes 2-4; every thread runs two radix-8 butterflies per stage:
+// reversal.  One 256-thread workgroup per transform (T consecutive transforms per
+// workgroup), the next transform's 16 loads in flight under passes 2-4; every thread runs
+// two radix-8 butterflies per stage:
 //   pass 1 (registers, from HBM): butterflies j = t + 256a of stage 0, elements j + 512m
 //          (each load instruction covers 512 consecutive bytes per wave);
 //   pass 2: stage 1, butterfly (block (t>>6) + 4a, j = t & 63), elements 512blk + j + 64m;
@@ -302,16 +303,19 @@ __device__ __forceinline__ int rev3o(int t) { return ((t & 7) << 6) | (((t >> 3)
 #ifndef MI355X_N4096_WAVES
 #define MI355X_N4096_WAVES 1
 #endif
+// Work mapping: T = 0 persistent grid-stride walk; T > 0: workgroup b takes the T consecutive
+// transforms bT .. bT+T-1 (as the fixed-point N = 4096 kernels, cfft_fixed.hip).
 #ifndef MI355X_N4096_T
-#define MI355X_N4096_T 0
+#define MI355X_N4096_T 8
 #endif
 constexpr uint32_t kN4096T = MI355X_N4096_T;
+// IFFT / BREV (ifftFlag, bitReverseFlag) are template parameters so that no output word or
+// address goes through a run-time select.
+template <bool IFFT, bool BREV>
 __global__ __launch_bounds__(256, MI355X_N4096_WAVES) void cfft_f32_n4096_kernel(float2* __restrict__ data, uint32_t batch,
-                                                             const float2* __restrict__ tw, uint32_t flags) {
+                                                             const float2* __restrict__ tw) {
   __shared__ __attribute__((aligned(16))) float2 lds[4607];
   const int t = threadIdx.x;
-  const bool ifft = flags & kIfft;
-  const bool brev = flags & kBitrev;
   const float invL = 1.0f / 4096.0f;
   const int j1 = t & 63, j2 = t & 7;
   float2 w0[2][7], w1[7], w2[7];
@@ -322,26 +326,32 @@ __global__ __launch_bounds__(256, MI355X_N4096_WAVES) void cfft_f32_n4096_kernel
     w1[m] = tw[(m + 1) * j1 * 8];
     w2[m] = tw[(m + 1) * j2 * 64];
   }
-  // work mapping: MI355X_N4096_T = 0 persistent grid-stride walk; T > 0: workgroup b takes
-  // the T consecutive transforms bT .. bT+T-1
   const uint32_t tr_begin = kN4096T ? blockIdx.x * kN4096T : blockIdx.x;
   const uint32_t tr_end = kN4096T ? min(batch, tr_begin + kN4096T) : batch;
   const uint32_t tr_step = kN4096T ? 1u : gridDim.x;
+  if (tr_begin >= tr_end) return;
   float2 v[2][8], nv[2][8];
-  if (tr_begin < tr_end) {
-    const float2* X0 = data + (size_t)tr_begin * 4096;
+  const int vin = t * 8;               // byte offset of element t (buffer I/O, SGPR soffsets)
+  auto fetch = [&](uint32_t tr) {
+    const __amdgpu_buffer_rsrc_t r = buf_rsrc(data + (size_t)tr * 4096, 4096 * 8);
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int m = 0; m < 8; ++m) nv[a][m] = ldnt(&X0[t + 256 * a + 512 * m]);
-  }
-  for (uint32_t tr = tr_begin; tr < tr_end; tr += tr_step) {
-    float2* X = data + (size_t)tr * 4096;
-    // ---------------- pass 1: stage 0 (modifier 1)
+      for (int m = 0; m < 8; ++m) nv[a][m] = buf_ld_f2(r, vin, (256 * a + 512 * m) * 8);
+  };
+  // pass 1: stage 0 (modifier 1) from the prefetched words, then the next transform's loads,
+  // which fly under passes 2-4.  The loop is entered after pass 1 (cfft_fx4096_kernel): the
+  // wait for the prefetched words then leaves the previous transform's stores in flight.
+  auto pass1 = [&](uint32_t tr) {
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
 #pragma unroll
-      for (int m = 0; m < 8; ++m) v[a][m] = ifft ? make_float2(nv[a][m].x, -nv[a][m].y) : nv[a][m];
+      for (int m = 0; m < 8; ++m) {
+        v[a][m] = nv[a][m];
+        // conj (arm_cfft_f32.c:1252-1261) as a sign-bit flip on the copy: written as a float
+        // negation the compiler split the prefetch registers and re-copied them at the back edge
+        if constexpr (IFFT) asm("v_xor_b32 %0, 0x80000000, %0" : "+v"(v[a][m].y));
+      }
       r8_sel(v[a], w0[a], t + 256 * a != 0);
     }
     __syncthreads();                    // the previous transform's pass-4 reads are done
@@ -349,14 +359,14 @@ __global__ __launch_bounds__(256, MI355X_N4096_WAVES) void cfft_f32_n4096_kernel
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int m = 0; m < 8; ++m) lds[s4096f(t + 256 * a + 512 * m)] = v[a][m];
-    if (tr + tr_step < tr_end) {        // next transform's loads fly under passes 2-4
-      const float2* XN = data + (size_t)(tr + tr_step) * 4096;
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int m = 0; m < 8; ++m) nv[a][m] = ldnt(&XN[t + 256 * a + 512 * m]);
-    }
+    if (tr + tr_step < tr_end) fetch(tr + tr_step);
     __syncthreads();
+  };
+  fetch(tr_begin);
+  pass1(tr_begin);
+  for (uint32_t tr = tr_begin;;) {
+    float2* X = data + (size_t)tr * 4096;
+    const __amdgpu_buffer_rsrc_t rx = buf_rsrc(X, 4096 * 8);
     // ---------------- pass 2: stage 1 (modifier 8)
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
@@ -386,22 +396,22 @@ __global__ __launch_bounds__(256, MI355X_N4096_WAVES) void cfft_f32_n4096_kernel
 #pragma unroll
       for (int m = 0; m < 8; ++m) v[a][m] = lds[s4096f(8 * q + m)];
       r8_core(v[a]);
-      if (ifft) {                       // arm_cfft_f32.c:1285-1297
+      if constexpr (IFFT) {             // arm_cfft_f32.c:1285-1297
 #pragma unroll
         for (int m = 0; m < 8; ++m) v[a][m] = make_float2(v[a][m].x * invL, -v[a][m].y * invL);
       }
-      if (brev) {
+      if constexpr (BREV) {
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          const v2f o = {v[a][m].x, v[a][m].y};
-          __builtin_nontemporal_store(o, reinterpret_cast<v2f*>(&X[512 * m + t + 256 * a]));
-        }
+        for (int m = 0; m < 8; ++m) buf_st_f2(rx, vin, (512 * m + 256 * a) * 8, v[a][m]);
       } else {
         float4* Y = reinterpret_cast<float4*>(X + 8 * q);
 #pragma unroll
         for (int m = 0; m < 8; m += 2) Y[m >> 1] = make_float4(v[a][m].x, v[a][m].y, v[a][m + 1].x, v[a][m + 1].y);
       }
     }
+    tr += tr_step;
+    if (tr >= tr_end) return;
+    pass1(tr);
   }
 }
 
@@ -602,9 +612,11 @@ hipError_t cfft_f32_launch(int n, float* data, uint32_t batch, const float* tw, 
       return launch_f32<2048>(d, batch, w, perm, flags, st);
     case 4096:
       if (!perm && MI355X_F32_N4096) {   // the reference's own table: the specialist kernel
-        const int grid = kN4096T ? (int)((batch + kN4096T - 1) / kN4096T)
-                                 : persistent_grid((const void*)cfft_f32_n4096_kernel, 256, 0, batch);
-        hipLaunchKernelGGL(cfft_f32_n4096_kernel, dim3(grid), dim3(256), 0, st, d, batch, w, flags);
+        const bool inv = flags & kIfft, brev = flags & kBitrev;
+        auto k = inv ? (brev ? cfft_f32_n4096_kernel<true, true> : cfft_f32_n4096_kernel<true, false>)
+                     : (brev ? cfft_f32_n4096_kernel<false, true> : cfft_f32_n4096_kernel<false, false>);
+        const int grid = kN4096T ? (int)((batch + kN4096T - 1) / kN4096T) : persistent_grid((const void*)k, 256, 0, batch);
+        hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, d, batch, w);
         return hipGetLastError();
       }
       return launch_f32<4096>(d, batch, w, perm, flags, st);

@@ -17,6 +17,12 @@
 
 namespace mi355x {
 
+// MI355X_FX_NULL = 1 (experiments only): butterflies do nothing, so a kernel keeps only its
+// memory traffic and LDS exchanges -- the ceiling of its access pattern (results are wrong).
+#ifndef MI355X_FX_NULL
+#define MI355X_FX_NULL 0
+#endif
+
 // ------------------------------------------------------------------ q31 butterflies
 // stage kinds: 0 = first (>>4 in, <<1 out), 1 = middle (>>2 / >>1), 2 = last (no twiddle)
 template <bool INV, int KIND>
@@ -179,6 +185,9 @@ template <bool INV> __device__ __forceinline__ s16x2 cmul_pk(TwP w, s16x2 R) {
 
 template <bool INV, int KIND>
 __device__ __forceinline__ void bfly_pk(s16x2& a, s16x2& b, s16x2& c, s16x2& d, TwP w1, TwP w2, TwP w3) {
+#if MI355X_FX_NULL
+  a ^= w1.p; b ^= w2.q; c ^= w3.p; return;
+#endif
   constexpr short SH = KIND == 0 ? 2 : 0;
   const s16x2 A = a >> SH, B = b >> SH, Cc = c >> SH, D = d >> SH;
   s16x2 R = pk_sat_add(A, Cc), S = pk_sat_sub(A, Cc), T = pk_sat_add(B, D);
@@ -209,11 +218,13 @@ __device__ __forceinline__ void bfly_pk(s16x2& a, s16x2& b, s16x2& c, s16x2& d, 
 template <typename T> struct Fx;
 template <> struct Fx<int32_t> {   // q31: complex = int2 in LDS and HBM
   using C = int2;
+  using S = int;
   __device__ static int2 ld(const C* p) { return *p; }
   __device__ static void st(C* p, int2 v) { *p = v; }
 };
 template <> struct Fx<int16_t> {   // q15: complex = short2
   using C = short2;
+  using S = short;
   __device__ static int2 ld(const C* p) { short2 s = *p; return make_int2(s.x, s.y); }
   __device__ static void st(C* p, int2 v) { *p = make_short2((short)v.x, (short)v.y); }
 };
@@ -234,6 +245,7 @@ template <int N> struct PlanFx {
 
 template <typename T, bool INV, int KIND>
 __device__ __forceinline__ void bfly(int2& a, int2& b, int2& c, int2& d, int2 w1, int2 w2, int2 w3) {
+  if constexpr (MI355X_FX_NULL) { a.x ^= w1.x; b.y ^= w2.y; c.x ^= w3.x; return; }
   if constexpr (sizeof(T) == 4) bfly_q31<INV, KIND>(a, b, c, d, w1, w2, w3);
   else bfly_q15<INV, KIND>(a, b, c, d, w1, w2, w3);
 }
@@ -394,33 +406,88 @@ __global__ __launch_bounds__(kBlock) void cfft_fx_kernel(typename Fx<T>::C* __re
 //   pass 3: thread t holds e = 16*rev8(t) + 4a + b  -> stage 5 (over a), stage 6 (over b)
 // Output position e = 16*rev8(t) + u goes to bin rev12(e) = rev4(u)*256 + t: for every u
 // the 256 threads store 256 consecutive bins, so the bit reversal is free.
-// LDS: 4096 complex padded s(e) = e + 8*(e>>7) + (e>>9) (4351 slots): every exchange
-// pattern above is bank-conflict free and, being additive, addressed as lane base +
-// immediate (found by exhaustive search over two-term paddings).
+// LDS paddings are additive (every access is lane base + immediate) and bank-conflict free
+// under the banking of the instructions the compiler emits (MI355X_MICROARCH.md §LDS):
+//  * 8-B complex (q31): reads pair into ds_read2_b64, writes are ds_write(2)_b64, all
+//    serviced in 16-lane groups on (dword mod 32) banks.  Passes 1-2 touch 16 consecutive e
+//    per group; pass 3's group reads e = 256*rev4(i) + K (i < 16), which s(e) = e + (e >> 8)
+//    puts on 16 distinct bank pairs.  The round-1 padding s4096 was chosen for ds_read_b64's
+//    32-lane / mod-64 banking and left pass 3 two-way conflicted under ds_read2_b64: 64
+//    extra LDS cycles per wave per transform (profiles/r02/cfft_q31_4096_strong1M/pmc.json).
+//  * 4-B complex (q15): ds_write_b32 / ds_read2_b32 in 32-lane groups on mod-32 banks; pass
+//    3's group reads e = 256*rev4(i) + 128g + K, which s4096 keeps conflict free (PMC: 0).
 __device__ __forceinline__ int s4096(int e) { return e + 8 * (e >> 7) + (e >> 9); }
+template <typename C> __device__ __forceinline__ int sfx(int e) {
+  if constexpr (sizeof(C) == 8) return e + (e >> 8);
+  else return s4096(e);
+}
+template <typename C> constexpr int kFxSlots = sizeof(C) == 8 ? 4096 + 16 : 4351;
 
-#ifndef MI355X_FX_TW_REGS
-#define MI355X_FX_TW_REGS 1
+// Global I/O through a buffer resource per transform (gfx9 raw buffer, dword 3 = 0x00020000):
+// one VGPR byte offset per lane, the (a, b) element offsets as SGPR soffsets, so no 64-bit
+// address arithmetic per access.  MI355X_FX_NT = 2 marks the streamed words nontemporal.
+#ifndef MI355X_FX_NT
+#define MI355X_FX_NT 2
 #endif
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t fx_rsrc(const void* p, uint32_t bytes) { return buf_rsrc(p, bytes); }
+template <typename C> struct FxIO;
+template <> struct FxIO<int2> {
+  __device__ static int2 ld(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+    const v2i v = __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, MI355X_FX_NT);
+    return make_int2(v.x, v.y);
+  }
+  __device__ static void st(__amdgpu_buffer_rsrc_t r, int vo, int so, int2 x) {
+    __builtin_amdgcn_raw_buffer_store_b64(v2i{x.x, x.y}, r, vo, so, MI355X_FX_NT);
+  }
+};
+template <> struct FxIO<short2> {
+  __device__ static short2 ld(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+    return __builtin_bit_cast(short2, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, MI355X_FX_NT));
+  }
+  __device__ static void st(__amdgpu_buffer_rsrc_t r, int vo, int so, short2 x) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, x), r, vo, so, MI355X_FX_NT);
+  }
+};
 
+// Work mapping of the N = 4096 kernels (q31: MI355X_FX_T, q15: MI355X_FXQ15_T).  T = 0:
+// persistent grid walking the batch with stride = grid; T > 0: workgroup b takes the T
+// consecutive transforms bT .. bT+T-1 (grid = batch / T; the prefetch runs inside the run).
+// Measured at 2^20 transforms (profiles/r02/variants_fx4096/): T = 8 ran at the ceiling of
+// the kernels' own access pattern (a build with the butterflies removed, MI355X_FX_NULL) on
+// every box, while the persistent walk ranged 316-354 Gsamples/s (q31) from box to box.
 #ifndef MI355X_FX_T
-#define MI355X_FX_T 0
+#define MI355X_FX_T 8
 #endif
-constexpr uint32_t kFxT = MI355X_FX_T;
+#ifndef MI355X_FXQ15_T
+#define MI355X_FXQ15_T 8
+#endif
+struct FxWalk { uint32_t begin, end, step; };
+template <uint32_t kT> __device__ __forceinline__ FxWalk fx_walk(uint32_t batch) {
+  if constexpr (kT == 0) return FxWalk{blockIdx.x, batch, gridDim.x};
+  const uint32_t b = blockIdx.x * kT;
+  return FxWalk{b, min(batch, b + kT), 1u};
+}
+template <uint32_t kT> __host__ __forceinline__ int fx_grid(const void* k, uint32_t batch) {
+  return kT ? (int)((batch + kT - 1) / kT) : persistent_grid(k, 256, 0, batch);
+}
+
 #ifndef MI355X_FX_WAVES
 #define MI355X_FX_WAVES 1     // minimum waves per SIMD the register allocation must allow
 #endif
-// MI355X_FX_TW3_LDS = 1: the pass-2 (stage-3) twiddles tw[(k+1)*16m], m < 64, live in a
-// 1.5 KiB LDS table instead of 24 VGPRs per lane.  MI355X_FX_PF = 1: the next transform's
-// 16 loads are held in registers under passes 2-3 (32 VGPRs for q31).
+// Twiddle placement.  Lane-distinct twiddles (stage 1: 12 words per lane, stage 2: 3) stay in
+// VGPRs for the kernel's life; stage 3 depends only on (t % 16, a) and stage 4 on t % 16, so
+// MI355X_FX_TW3_LDS / MI355X_FX_TW4_LDS keep them in small LDS tables (1.5 KiB / 384 B, read
+// as conflict-free broadcasts) instead of 24 / 6 VGPRs.  Stage 5 is lane-uniform (SGPRs).
 #ifndef MI355X_FX_TW3_LDS
 #define MI355X_FX_TW3_LDS 0
 #endif
+#ifndef MI355X_FX_TW4_LDS
+#define MI355X_FX_TW4_LDS 0
+#endif
+// MI355X_FX_PF = d >= 1: the next d transforms' 16 loads are held in registers (the first under
+// passes 2-3 of the current one), 32 VGPRs per transform for q31.
 #ifndef MI355X_FX_PF
 #define MI355X_FX_PF 1
-#endif
-#ifndef MI355X_FX_TW4_LDS          // stage-4 twiddles tw[(k+1)*64*j2], j2 < 16: 384 B of LDS
-#define MI355X_FX_TW4_LDS 0
 #endif
 // BREV / SAT are the bitReverseFlag and the RFFT inverse's saturating <<1 (kSatShl1) as
 // template parameters: as run-time flags the compiler if-converted them into selects on
@@ -430,42 +497,43 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
                                                           const typename Fx<T>::C* __restrict__ tw) {
   using F = Fx<T>;
   using C = typename F::C;
-  __shared__ __attribute__((aligned(16))) C lds[4351];
+  using IO = FxIO<C>;
+  constexpr int kC = (int)sizeof(C);
+  __shared__ __attribute__((aligned(16))) C lds[kFxSlots<C>];
   const int t = threadIdx.x;
   const int q2 = t >> 4, j2 = t & 15;
   const int q3 = (int)(__brev((uint32_t)t) >> 24);        // rev8(t)
+  const FxWalk wk = fx_walk<MI355X_FX_T>(batch);
+  const uint32_t tr0 = wk.begin, tend = wk.end, step = wk.step;
 
-  // Lane-constant twiddles, loaded once for the kernel's life (stored in the table's own
-  // word type: q15 keeps two per VGPR).  (w1, w2, w3) = table[ia], table[2ia], table[3ia].
-  // MI355X_FX_TW_REGS=0: stage-1 and stage-3 twiddles (24 words per lane) are re-read from
-  // the cache-resident table every transform instead of pinned in VGPRs.
-  C tw2[3], tw4[3], tw5[4][3];
-#if MI355X_FX_TW_REGS
-  C tw1[4][3];
-#if !MI355X_FX_TW3_LDS
-  C tw3[4][3];
-#endif
-#endif
+  // Lane-constant twiddles (stored in the table's word type).  (w1, w2, w3) = table[ia],
+  // table[2ia], table[3ia] of the butterfly's index ia.
+  C tw1[4][3], tw2[3], tw5[4][3];
 #if MI355X_FX_TW3_LDS
   __shared__ __attribute__((aligned(16))) C tw3l[64 * 3];
   if (t < 192) tw3l[t] = tw[(t % 3 + 1) * (t / 3) * 16];        // visible after the loop's barriers
+#define TW3(a, k) tw3l[(j2 + 16 * (a)) * 3 + (k)]
+#else
+  C tw3[4][3];
+#define TW3(a, k) tw3[a][k]
 #endif
 #if MI355X_FX_TW4_LDS
   __shared__ __attribute__((aligned(16))) C tw4l[16 * 3];
   if (t < 48) tw4l[t] = tw[(t % 3 + 1) * 64 * (t / 3)];
+#define TW4(k) tw4l[j2 * 3 + (k)]
+#else
+  C tw4[3];
+#define TW4(k) tw4[k]
 #endif
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
-    const int ia5 = a * 256;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-#if MI355X_FX_TW_REGS
       tw1[a][k] = tw[(k + 1) * (t + 256 * a)];
 #if !MI355X_FX_TW3_LDS
       tw3[a][k] = tw[(k + 1) * (j2 + 16 * a) * 16];
 #endif
-#endif
-      tw5[a][k] = tw[(k + 1) * ia5];
+      tw5[a][k] = tw[(k + 1) * a * 256];
     }
   }
 #pragma unroll
@@ -475,96 +543,60 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
     tw4[k] = tw[(k + 1) * 64 * j2];
 #endif
   }
-#if MI355X_FX_TW_REGS
-#define TW1(a, k) tw1[a][k]
-#define TW2(k) tw2[k]
-#if MI355X_FX_TW3_LDS
-#define TW3(a, k) tw3l[(j2 + 16 * (a)) * 3 + (k)]
-#else
-#define TW3(a, k) tw3[a][k]
-#endif
-#if MI355X_FX_TW4_LDS
-#define TW4(k) tw4l[j2 * 3 + (k)]
-#else
-#define TW4(k) tw4[k]
-#endif
-#else
-#define TW1(a, k) twl[((k) + 1) * (t + 256 * (a))]
-#define TW2(k) tw2[k]
-#define TW3(a, k) twl[((k) + 1) * (j2 + 16 * (a)) * 16]
-#define TW4(k) tw4[k]
-#endif
   auto W = [](C c) { return make_int2(c.x, c.y); };
 
-  // Work mapping (as cfft_f32_n1024_kernel): MI355X_FX_T = 0 persistent grid-stride walk;
-  // T > 0: workgroup b takes the T consecutive transforms bT .. bT+T-1.
-  const uint32_t tr_begin = kFxT ? blockIdx.x * kFxT : blockIdx.x;
-  const uint32_t tr_end = kFxT ? min(batch, tr_begin + kFxT) : batch;
-  const uint32_t tr_step = kFxT ? 1u : gridDim.x;
-  int2 v[16];
-  // register prefetch MI355X_FX_PF transforms deep (0 = load at the top of each transform):
-  // nq[d] holds transform tr + (d+1) * step, in the storage type (q15: one VGPR per complex)
+  // walk: nq[d] holds transform tr + (d + 1) * step (FxWalk)
   constexpr int PFD = MI355X_FX_PF > 0 ? MI355X_FX_PF : 1;
+  const int vin = t * kC;                                    // byte offset of element t
+  auto fetch = [&](C (&dst)[16], uint32_t tr) {
+    const __amdgpu_buffer_rsrc_t r = fx_rsrc(data + (size_t)tr * 4096, 4096 * kC);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) dst[4 * a + b] = IO::ld(r, vin, (256 * a + 1024 * b) * kC);
+  };
+  int2 v[16];
   C nq[PFD][16];
-#if MI355X_FX_PF
+  // Pass 1 of transform tr from nq[0]; then the prefetch of transform tr + PFD * step.
+  auto pass1 = [&](C (&buf)[16], uint32_t tr) {
 #pragma unroll
-  for (int d = 0; d < PFD; ++d) {
-    const uint32_t tp = tr_begin + d * tr_step;
-    if (tp < tr_end) {
-      const C* X0 = data + (size_t)tp * 4096;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) nq[d][4 * a + b] = X0[t + 256 * a + 1024 * b];
-    }
-  }
-#endif
-  for (uint32_t tr = tr_begin; tr < tr_end; tr += tr_step) {
-    C* X = data + (size_t)tr * 4096;
-#if !MI355X_FX_TW_REGS
-    const C* twl = tw;
-    asm volatile("" : "+s"(twl));      // opaque per transform: keeps the re-reads in the loop
-#endif
-#if !MI355X_FX_PF
+    for (int u = 0; u < 16; ++u) v[u] = W(buf[u]);
 #pragma unroll
     for (int a = 0; a < 4; ++a)
+      bfly<T, INV, 0>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], W(tw1[a][0]), W(tw1[a][1]), W(tw1[a][2]));
 #pragma unroll
-      for (int b = 0; b < 4; ++b) nq[0][4 * a + b] = X[t + 256 * a + 1024 * b];
-#endif
-    // ---------------- pass 1: stages 1 (first) and 2
-#pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = W(nq[0][u]);
-#pragma unroll
-    for (int d = 0; d + 1 < PFD; ++d)
-#pragma unroll
-      for (int u = 0; u < 16; ++u) nq[d][u] = nq[d + 1][u];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-      bfly<T, INV, 0>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], W(TW1(a, 0)), W(TW1(a, 1)), W(TW1(a, 2)));
-#pragma unroll
-    for (int b = 0; b < 4; ++b) bfly<T, INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], W(TW2(0)), W(TW2(1)), W(TW2(2)));
+    for (int b = 0; b < 4; ++b) bfly<T, INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], W(tw2[0]), W(tw2[1]), W(tw2[2]));
     __syncthreads();                    // the previous transform's pass-3 reads are done
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) F::st(lds + s4096(t + 256 * a + 1024 * b), v[4 * a + b]);
-#if MI355X_FX_PF
-    if (tr + PFD * tr_step < tr_end) {  // a later transform's loads fly under passes 2 and 3
-      const C* XN = data + (size_t)(tr + PFD * tr_step) * 4096;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) nq[PFD - 1][4 * a + b] = XN[t + 256 * a + 1024 * b];
-    }
-#endif
+      for (int b = 0; b < 4; ++b) F::st(lds + sfx<C>(t + 256 * a + 1024 * b), v[4 * a + b]);
+    if (tr + PFD * step < tend) fetch(buf, tr + PFD * step);   // flies under passes 2-3
     __syncthreads();
+  };
+  // The loop is entered after pass 1, so that at the point where pass 1 of the next
+  // transform waits for its prefetched words, the only younger vector-memory operations are
+  // the current transform's 16 stores and the deeper prefetches, on every path: the compiler
+  // then waits with vmcnt(16 * PFD) instead of draining the stores.  (With pass 1 at the
+  // loop head, the merge of the entry path -- prefetch loads youngest -- with the back edge
+  // made it wait for vmcnt(0), i.e. for the previous transform's stores to complete.)  The
+  // loop is unrolled PFD times so the prefetch buffers rotate by name: copying a buffer
+  // whose loads are in flight would wait for them.
+  if (tr0 >= tend) return;
+#pragma unroll
+  for (int d = 0; d < PFD; ++d)
+    if (tr0 + d * step < tend) fetch(nq[d], tr0 + d * step);
+  pass1(nq[0], tr0);
+  uint32_t tr = tr0;
+  auto pass23 = [&]() {
+    const __amdgpu_buffer_rsrc_t rx = fx_rsrc(data + (size_t)tr * 4096, 4096 * kC);
     // ---------------- pass 2: stages 3 and 4
     {
       const int base = 256 * q2 + j2;
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) v[4 * a + b] = F::ld(lds + s4096(base + 64 * a + 16 * b));
+        for (int b = 0; b < 4; ++b) v[4 * a + b] = F::ld(lds + sfx<C>(base + 64 * a + 16 * b));
 #pragma unroll
       for (int b = 0; b < 4; ++b)
         bfly<T, INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], W(TW3(b, 0)), W(TW3(b, 1)), W(TW3(b, 2)));
@@ -575,14 +607,14 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) F::st(lds + s4096(base + 64 * a + 16 * b), v[4 * a + b]);
+        for (int b = 0; b < 4; ++b) F::st(lds + sfx<C>(base + 64 * a + 16 * b), v[4 * a + b]);
     }
     __syncthreads();
     // ---------------- pass 3: stages 5 and 6 (last)
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) v[4 * a + b] = F::ld(lds + s4096(16 * q3 + 4 * a + b));
+      for (int b = 0; b < 4; ++b) v[4 * a + b] = F::ld(lds + sfx<C>(16 * q3 + 4 * a + b));
 #pragma unroll
     for (int b = 0; b < 4; ++b)
       bfly<T, INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], W(tw5[b][0]), W(tw5[b][1]), W(tw5[b][2]));
@@ -593,18 +625,28 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 #pragma unroll
       for (int u = 0; u < 16; ++u) v[u] = sat_shl1<T>(v[u]);
     }
+    C o[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) o[u] = C{(typename F::S)v[u].x, (typename F::S)v[u].y};
     if constexpr (BREV) {
 #pragma unroll
-      for (int u = 0; u < 16; ++u) F::st(X + (int)(__brev((uint32_t)u) >> 28) * 256 + t, v[u]);
+      for (int u = 0; u < 16; ++u) IO::st(rx, vin, (int)(__brev((uint32_t)u) >> 28) * 256 * kC, o[u]);
     } else {
 #pragma unroll
-      for (int u = 0; u < 16; ++u) F::st(X + 16 * q3 + u, v[u]);
+      for (int u = 0; u < 16; ++u) IO::st(rx, 16 * q3 * kC, u * kC, o[u]);
+    }
+  };
+  for (;;) {
+#pragma unroll
+    for (int d = 0; d < PFD; ++d) {
+      pass23();
+      tr += step;
+      if (tr >= tend) return;
+      pass1(nq[(d + 1) % PFD], tr);
     }
   }
 }
 
-#undef TW1
-#undef TW2
 #undef TW3
 #undef TW4
 
@@ -622,52 +664,78 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 #ifndef MI355X_FX_Q15_PFD
 #define MI355X_FX_Q15_PFD 2
 #endif
+// MI355X_FXQ15_TW34_LDS = 1: the stage-3/4 twiddle pairs (functions of t % 16 only) live in
+// LDS tables (1.5 KiB + 384 B) instead of 30 VGPRs; MI355X_FXQ15_WAVES = the minimum waves per
+// SIMD the register allocation must allow.
+#ifndef MI355X_FXQ15_TW34_LDS
+#define MI355X_FXQ15_TW34_LDS 0
+#endif
+#ifndef MI355X_FXQ15_WAVES
+#define MI355X_FXQ15_WAVES 1
+#endif
 template <bool INV, bool BREV, bool SAT>
-__global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_q15_4096_pk_kernel(short2* __restrict__ data, uint32_t batch,
+__global__ __launch_bounds__(256, MI355X_FXQ15_WAVES) void cfft_q15_4096_pk_kernel(short2* __restrict__ data, uint32_t batch,
                                                                     const short2* __restrict__ tw) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4351];
   const int t = threadIdx.x;
   const int q2 = t >> 4, j2 = t & 15;
   const int q3 = (int)(__brev((uint32_t)t) >> 24);        // rev8(t)
-  TwP tw1[4][3], tw3[4][3], tw2[3], tw4[3], tw5[4][3];
+  const FxWalk wk = fx_walk<MI355X_FXQ15_T>(batch);
+  const uint32_t tr0 = wk.begin, tend = wk.end, step = wk.step;
+  TwP tw1[4][3], tw2[3], tw5[4][3];
+#if MI355X_FXQ15_TW34_LDS
+  __shared__ TwP tw3l[64 * 3], tw4l[16 * 3];
+  if (t < 192) tw3l[t] = twp<INV>(tw[(t % 3 + 1) * (t / 3) * 16]);    // visible after the loop's barriers
+  else if (t < 240) tw4l[t - 192] = twp<INV>(tw[((t - 192) % 3 + 1) * 64 * ((t - 192) / 3)]);
+#define TW3Q(a, k) tw3l[(j2 + 16 * (a)) * 3 + (k)]
+#define TW4Q(k) tw4l[j2 * 3 + (k)]
+#else
+  TwP tw3[4][3], tw4[3];
+#define TW3Q(a, k) tw3[a][k]
+#define TW4Q(k) tw4[k]
+#endif
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       tw1[a][k] = twp<INV>(tw[(k + 1) * (t + 256 * a)]);
+#if !MI355X_FXQ15_TW34_LDS
       tw3[a][k] = twp<INV>(tw[(k + 1) * (j2 + 16 * a) * 16]);
+#endif
       tw5[a][k] = twp<INV>(tw[(k + 1) * a * 256]);
     }
 #pragma unroll
-  for (int k = 0; k < 3; ++k) { tw2[k] = twp<INV>(tw[(k + 1) * 4 * t]); tw4[k] = twp<INV>(tw[(k + 1) * 64 * j2]); }
+  for (int k = 0; k < 3; ++k) {
+    tw2[k] = twp<INV>(tw[(k + 1) * 4 * t]);
+#if !MI355X_FXQ15_TW34_LDS
+    tw4[k] = twp<INV>(tw[(k + 1) * 64 * j2]);
+#endif
+  }
   const TwP z{};
 
-  const uint32_t* D = reinterpret_cast<const uint32_t*>(data);
   s16x2 v[16];
-  // Register prefetch MI355X_FX_Q15_PFD transforms deep: nq[d] holds transform tr + (d+1)G.
+  const int vin = t * 4;                                   // byte offset of element t
+  auto fetch = [&](uint32_t (&dst)[16], uint32_t tr) {
+    const __amdgpu_buffer_rsrc_t r = fx_rsrc(data + (size_t)tr * 4096, 4096 * 4);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        dst[4 * a + b] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, vin, (256 * a + 1024 * b) * 4, MI355X_FX_NT);
+  };
+  // Register prefetch MI355X_FX_Q15_PFD transforms deep: nq[d] holds transform tr + (d+1)*step.
   // q15 moves 4 B per load, so at the workgroups a CU holds one transform of look-ahead
   // (16 KiB per workgroup) does not cover the HBM latency; two measured +8.5 %.
   constexpr int PFD = MI355X_FX_Q15_PFD;
   uint32_t nq[PFD][16];
 #pragma unroll
-  for (int d = 0; d < PFD; ++d) {
-    const uint32_t tr = blockIdx.x + d * gridDim.x;
-    if (tr < batch) {
-      const uint32_t* X0 = D + (size_t)tr * 4096;
+  for (int d = 0; d < PFD; ++d)
+    if (tr0 + d * step < tend) fetch(nq[d], tr0 + d * step);
+  // Loop entered after pass 1, as in cfft_fx4096_kernel: the wait for the prefetched words
+  // then covers only the older loads (vmcnt = the younger stores + deeper prefetches).
+  auto pass1 = [&](uint32_t (&buf)[16], uint32_t tr) {
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) nq[d][4 * a + b] = X0[t + 256 * a + 1024 * b];
-    }
-  }
-  for (uint32_t tr = blockIdx.x; tr < batch; tr += gridDim.x) {
-    uint32_t* X = reinterpret_cast<uint32_t*>(data) + (size_t)tr * 4096;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = pk(nq[0][u]);
-#pragma unroll
-    for (int d = 0; d + 1 < PFD; ++d)
-#pragma unroll
-      for (int u = 0; u < 16; ++u) nq[d][u] = nq[d + 1][u];
+    for (int u = 0; u < 16; ++u) v[u] = pk(buf[u]);
 #pragma unroll
     for (int a = 0; a < 4; ++a)
       bfly_pk<INV, 0>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], tw1[a][0], tw1[a][1], tw1[a][2]);
@@ -678,14 +746,14 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_q15_4096_pk_kernel(
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) lds[s4096(t + 256 * a + 1024 * b)] = upk(v[4 * a + b]);
-    if (tr + PFD * gridDim.x < batch) {
-      const uint32_t* XN = D + (size_t)(tr + PFD * gridDim.x) * 4096;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) nq[PFD - 1][4 * a + b] = XN[t + 256 * a + 1024 * b];
-    }
+    if (tr + PFD * step < tend) fetch(buf, tr + PFD * step);
     __syncthreads();
+  };
+  if (tr0 >= tend) return;
+  pass1(nq[0], tr0);
+  uint32_t tr = tr0;
+  auto pass23 = [&]() {
+    const __amdgpu_buffer_rsrc_t rx = fx_rsrc(data + (size_t)tr * 4096, 4096 * 4);
     {
       const int base = 256 * q2 + j2;
 #pragma unroll
@@ -693,10 +761,10 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_q15_4096_pk_kernel(
 #pragma unroll
         for (int b = 0; b < 4; ++b) v[4 * a + b] = pk(lds[s4096(base + 64 * a + 16 * b)]);
 #pragma unroll
-      for (int b = 0; b < 4; ++b) bfly_pk<INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], tw3[b][0], tw3[b][1], tw3[b][2]);
+      for (int b = 0; b < 4; ++b) bfly_pk<INV, 1>(v[b], v[4 + b], v[8 + b], v[12 + b], TW3Q(b, 0), TW3Q(b, 1), TW3Q(b, 2));
 #pragma unroll
       for (int a = 0; a < 4; ++a)
-        bfly_pk<INV, 1>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], tw4[0], tw4[1], tw4[2]);
+        bfly_pk<INV, 1>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], TW4Q(0), TW4Q(1), TW4Q(2));
       __syncthreads();
 #pragma unroll
       for (int a = 0; a < 4; ++a)
@@ -718,24 +786,37 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_q15_4096_pk_kernel(
     }
     if constexpr (BREV) {
 #pragma unroll
-      for (int u = 0; u < 16; ++u) X[(int)(__brev((uint32_t)u) >> 28) * 256 + t] = upk(v[u]);
+      for (int u = 0; u < 16; ++u)
+        __builtin_amdgcn_raw_buffer_store_b32((int)upk(v[u]), rx, vin, (int)(__brev((uint32_t)u) >> 28) * 1024, MI355X_FX_NT);
     } else {
 #pragma unroll
-      for (int u = 0; u < 16; ++u) X[16 * q3 + u] = upk(v[u]);
+      for (int u = 0; u < 16; ++u) __builtin_amdgcn_raw_buffer_store_b32((int)upk(v[u]), rx, 64 * q3, 4 * u, MI355X_FX_NT);
+    }
+  };
+  for (;;) {
+#pragma unroll
+    for (int d = 0; d < PFD; ++d) {
+      pass23();
+      tr += step;
+      if (tr >= tend) return;
+      pass1(nq[(d + 1) % PFD], tr);
     }
   }
 }
+
+#undef TW3Q
+#undef TW4Q
 
 template <typename T, bool INV, bool BREV, bool SAT>
 static void launch_fx4096_t(void* data, uint32_t batch, const void* tw, hipStream_t st) {
   using C = typename Fx<T>::C;
   if constexpr (sizeof(T) == 2 && MI355X_FX_Q15_PACKED) {
     auto k = cfft_q15_4096_pk_kernel<INV, BREV, SAT>;
-    const int grid = persistent_grid((const void*)k, 256, 0, batch);
+    const int grid = fx_grid<MI355X_FXQ15_T>((const void*)k, batch);
     hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (short2*)data, batch, (const short2*)tw);
   } else {
     auto k = cfft_fx4096_kernel<T, INV, BREV, SAT>;
-    const int grid = kFxT ? (int)((batch + kFxT - 1) / (kFxT ? kFxT : 1)) : persistent_grid((const void*)k, 256, 0, batch);
+    const int grid = fx_grid<MI355X_FX_T>((const void*)k, batch);
     hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (C*)data, batch, (const C*)tw);
   }
 }

@@ -38,6 +38,22 @@ __device__ __forceinline__ int32_t ssat16(int32_t v) { return v > 32767 ? 32767 
 
 constexpr int kBlock = 256;   // 4 wave64 per workgroup
 
+// Raw buffer resource over [p, p + bytes) (gfx9 descriptor dword 3 = 0x00020000): buffer
+// loads/stores take one VGPR byte offset plus an SGPR soffset, so the per-access 64-bit
+// address arithmetic of global_load/global_store disappears.  aux 2 = nontemporal.
+typedef int v2i __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+template <int AUX = 2>
+__device__ __forceinline__ float2 buf_ld_f2(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+  return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, AUX));
+}
+template <int AUX = 2>
+__device__ __forceinline__ void buf_st_f2(__amdgpu_buffer_rsrc_t r, int vo, int so, float2 x) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, x), r, vo, so, AUX);
+}
+
 template <int N> struct Log2 { static constexpr int v = 1 + Log2<N / 2>::v; };
 template <> struct Log2<1> { static constexpr int v = 0; };
 
