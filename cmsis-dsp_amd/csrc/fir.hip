@@ -56,17 +56,7 @@ __device__ __forceinline__ T fir_sample(const T* __restrict__ hist, const T* __r
 }
 
 // ---------------------------------------------------------------- f32
-#ifndef MI355X_FIR_F32_R
-#define MI355X_FIR_F32_R 8
-#endif
-// Coefficients: 1 = staged once per workgroup in LDS and read as wave-wide broadcasts (the
-// LDS queue is then the only lgkm traffic in the tap loop, so partial lgkmcnt waits work);
-// 0 = scalar loads from global memory (each s_load forces an lgkmcnt(0) that also drains
-// the window reads in flight).
-#ifndef MI355X_FIR_F32_COEF_LDS
-#define MI355X_FIR_F32_COEF_LDS 1
-#endif
-constexpr int kF32R = MI355X_FIR_F32_R;                 // outputs per lane
+constexpr int kF32R = 8;                                // outputs per lane (fir_f32_kernel)
 constexpr int kF32Chunk = kBlock * kF32R;              // outputs per workgroup
 constexpr int kFirPre = (kF32Chunk + kFirMaxTaps - 1 + kBlock - 1) / kBlock;   // window samples per thread
 
@@ -75,82 +65,143 @@ constexpr int kFirPre = (kF32Chunk + kFirMaxTaps - 1 + kBlock - 1) / kBlock;   /
 // pad per 32 words is conflict-free only at offsets that are multiples of 32).
 __device__ __forceinline__ int padx(int i) { return i + (i >> 3); }
 
-__device__ __forceinline__ void fir_f32_fetch(float (&pre)[kFirPre], const float* hist, const float* src,
-                                              const FirItem& it, uint32_t B, int T1) {
+// ---- fir_f32_kernel: a register-window formulation with no ring rotation.
+// A round is 8 consecutive taps k..k+7; output r of a lane needs window samples
+// base + r + k .. base + r + k + 7, i.e. the two 8-sample groups base + k and base + k + 8
+// (base = 8 * lane).  Four 8-register group buffers rotate by name over an unrolled block of
+// four rounds: round q computes from buffers (q, q+1) while group q + 2 is read from LDS,
+// one round (128 VALU) ahead of its use, so every operand index is a compile-time constant
+// and no register moves.  LDS window layout: 8-sample groups at a pitch of 10 words
+// (wpos), so each ds_read_b64 of a group (lanes 8 words apart in sample terms) lands its
+// 32-lane half on 64 distinct banks; coefficients are read as ds_read_b128 broadcasts.
+__host__ __device__ constexpr int wpos(int j) { return j + 2 * (j >> 3); }
+constexpr int kF32Win = kF32Chunk + kFirMaxTaps + 8;        // window samples incl. the read-ahead group
+
+struct F32Grp { float v[8]; };
+__device__ __forceinline__ void ld_grp(F32Grp& g, const float* win, int grp) {
+  const float2* p = reinterpret_cast<const float2*>(win + 10 * grp);
 #pragma unroll
-  for (int k = 0; k < kFirPre; ++k) {
-    const int j = threadIdx.x + k * kBlock;
-    pre[k] = fir_sample(hist, src, it, B, T1, j);
+  for (int i = 0; i < 4; ++i) {
+    const float2 x = p[i];
+    g.v[2 * i] = x.x;
+    g.v[2 * i + 1] = x.y;
   }
+}
+__device__ __forceinline__ void ld_coef(float (&c)[8], const float* cl, int k) {
+  const float4 a = *reinterpret_cast<const float4*>(cl + k), b = *reinterpret_cast<const float4*>(cl + k + 4);
+  c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w; c[4] = b.x; c[5] = b.y; c[6] = b.z; c[7] = b.w;
+}
+// one round: acc[r] += s[base + r + k + u] * c[k + u], u ascending (the reference's order)
+__device__ __forceinline__ void f32_round(float (&acc)[8], const F32Grp& A, const F32Grp& B, const float (&c)[8]) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] = acc[r] + (r + u < 8 ? A.v[r + u] : B.v[r + u - 8]) * c[u];
 }
 
 __global__ __launch_bounds__(kBlock) void fir_f32_kernel(const float* __restrict__ coeffs, int T,
                                                          const float* __restrict__ src, float* __restrict__ dst,
                                                          uint32_t B, const float* __restrict__ hist_in,
                                                          uint32_t nchunks, uint32_t items) {
-  __shared__ float win[(kF32Chunk + kFirMaxTaps) * 9 / 8 + 32];
+  __shared__ __attribute__((aligned(16))) float win[wpos(kF32Win) + 16];
+  __shared__ __attribute__((aligned(16))) float cl[kFirMaxTaps + 8];
   const int T1 = T - 1;
-  uint32_t item = blockIdx.x;
+  const uint32_t item = blockIdx.x;
   if (item >= items) return;
-#if MI355X_FIR_F32_COEF_LDS
-  __shared__ __attribute__((aligned(16))) float cl[kFirMaxTaps];
-  for (int i = threadIdx.x; i < T; i += kBlock) cl[i] = coeffs[i];   // visible after the loop's barriers
-  const float* cf = cl;
-#else
-  const float* cf = coeffs;
-#endif
-  float pre[kFirPre];
-  FirItem it = fir_item(item, nchunks, B, T1, kF32Chunk);
-  fir_f32_fetch(pre, hist_in, src, it, B, T1);
-  for (; item < items; item += gridDim.x) {
-    __syncthreads();                                // the previous item is done with win
+  for (int i = threadIdx.x; i < T; i += kBlock) cl[i] = coeffs[i];    // visible after the barrier
+  // Window staging through buffer resources sized to the item: reads past the window (or, in
+  // the first chunk, past the history / before the block) return 0 without index arithmetic.
+  // Window staging through buffer resources sized to the item: reads past the window return
+  // 0 without index arithmetic.  In the first chunk the window is [history (T1) ; block
+  // input]: the block part is read at offset max(j - T1, 0) and zeroed for j < T1, then OR-ed
+  // with the history word (history reads past T1 return 0).  Offsets are kept non-negative:
+  // the compiler moves constant parts of an offset into the instruction's immediate, and the
+  // hardware range check does not wrap a negative VGPR offset back into range.
+  // One item per workgroup: with 57 VGPRs and 19.6 KiB of LDS, eight workgroups share a CU
+  // and hide each other's staging (a persistent grid with a register prefetch of the next
+  // window measured neutral in round 1).
+  constexpr int kPre = (kF32Win + kBlock - 1) / kBlock;
+  constexpr int kPreH = (kFirMaxTaps - 1 + kBlock - 1) / kBlock;
+  const FirItem it = fir_item(item, nchunks, B, T1, kF32Chunk);
+  {
+    const int tid = threadIdx.x;
+    const int off = it.n0 - T1;                  // window sample j is block sample off + j
+    const float* p = src + (uint64_t)it.f * B + max(off, 0);
+    const __amdgpu_buffer_rsrc_t r = buf_rsrc(p, (uint32_t)min(it.total + min(off, 0), (int)B - max(off, 0)) * 4u);
+    int pre[kPre], preh[kPreH];
 #pragma unroll
-    for (int k = 0; k < kFirPre; ++k) {
-      const int j = threadIdx.x + k * kBlock;
-      if (j < it.total) win[padx(j)] = pre[k];
+    for (int k = 0; k < kPre; ++k) pre[k] = __builtin_amdgcn_raw_buffer_load_b32(r, max(tid + k * kBlock + min(off, 0), 0) * 4, 0, 0);
+#pragma unroll
+    for (int k = 0; k < kPreH; ++k) preh[k] = 0;
+    if (off < 0) {
+      const __amdgpu_buffer_rsrc_t rh = buf_rsrc(hist_in + (uint64_t)it.f * T1, (uint32_t)T1 * 4u);
+#pragma unroll
+      for (int k = 0; k < kPreH; ++k) preh[k] = __builtin_amdgcn_raw_buffer_load_b32(rh, (tid + k * kBlock) * 4, 0, 0);
     }
-    __syncthreads();
-    const FirItem cur = it;
-    if (item + gridDim.x < items) {
-      it = fir_item(item + gridDim.x, nchunks, B, T1, kF32Chunk);
-      fir_f32_fetch(pre, hist_in, src, it, B, T1);  // in flight during the MACs below
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+      const int j = tid + k * kBlock;
+      if (j < kF32Win) win[wpos(j)] = __builtin_bit_cast(float, k < kPreH ? (j + off >= 0 ? pre[k] : 0) | preh[k] : pre[k]);
     }
-
-    const int base = threadIdx.x * kF32R;           // local output index of this lane
-    if (base < cur.count) {
-      // w is a ring over s[base + k .. base + k + R-1]; k advances R taps per unrolled round,
-      // so every ring index is a compile-time constant (no register shuffling).
-      float acc[kF32R], w[kF32R];
+  }
+  __syncthreads();
+  const int rounds = T >> 3;
+  const int lane = threadIdx.x;
+  const int base = lane * kF32R;                    // local output index of this lane
+  if (base >= it.count) return;
+  {
+    const FirItem& cur = it;
+    float acc[8];
 #pragma unroll
-      for (int r = 0; r < kF32R; ++r) { acc[r] = 0.0f; w[r] = win[padx(base + r)]; }
-      int k = 0;
-      for (; k + kF32R <= T; k += kF32R) {
-#pragma unroll
-        for (int u = 0; u < kF32R; ++u) {
-          const float c = cf[k + u];
-#pragma unroll
-          for (int r = 0; r < kF32R; ++r) acc[r] = acc[r] + w[(r + u) % kF32R] * c;
-          w[u] = win[padx(base + k + u + kF32R)];
+    for (int r = 0; r < 8; ++r) acc[r] = 0.0f;
+    F32Grp X0, X1, X2, X3;
+    float c0[8], c1[8];
+    ld_grp(X0, win, lane);
+    ld_grp(X1, win, lane + 1);
+    int q = 0;
+    for (; q + 4 <= rounds; q += 4) {
+      ld_coef(c0, cl, 8 * q);
+      ld_grp(X2, win, lane + q + 2);
+      f32_round(acc, X0, X1, c0);
+      ld_coef(c1, cl, 8 * q + 8);
+      ld_grp(X3, win, lane + q + 3);
+      f32_round(acc, X1, X2, c1);
+      ld_coef(c0, cl, 8 * q + 16);
+      ld_grp(X0, win, lane + q + 4);
+      f32_round(acc, X2, X3, c0);
+      ld_coef(c1, cl, 8 * q + 24);
+      ld_grp(X1, win, lane + q + 5);
+      f32_round(acc, X3, X0, c1);
+    }
+    // 0..3 remaining whole rounds, same buffer order
+    if (q < rounds) {
+      ld_coef(c0, cl, 8 * q);
+      ld_grp(X2, win, lane + q + 2);
+      f32_round(acc, X0, X1, c0);
+      if (q + 1 < rounds) {
+        ld_coef(c1, cl, 8 * q + 8);
+        ld_grp(X3, win, lane + q + 3);
+        f32_round(acc, X1, X2, c1);
+        if (q + 2 < rounds) {
+          ld_coef(c0, cl, 8 * q + 16);
+          f32_round(acc, X2, X3, c0);
         }
       }
-      for (; k < T; ++k) {
-        const float c = cf[k];
+    }
+    // numTaps % 8 tail taps, straight from LDS
+    for (int k = 8 * rounds; k < T; ++k) {
+      const float c = cl[k];
 #pragma unroll
-        for (int r = 0; r < kF32R; ++r) acc[r] = acc[r] + w[r] * c;
+      for (int r = 0; r < 8; ++r) acc[r] = acc[r] + win[wpos(base + k + r)] * c;
+    }
+    float* o = dst + (uint64_t)cur.f * B + cur.n0 + base;
+    if ((B & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + 8 <= cur.count) {
+      reinterpret_cast<float4*>(o)[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      reinterpret_cast<float4*>(o)[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    } else {
 #pragma unroll
-        for (int r = 0; r < kF32R - 1; ++r) w[r] = w[r + 1];
-        w[kF32R - 1] = win[padx(base + kF32R + k)];
-      }
-      float* o = dst + (uint64_t)cur.f * B + cur.n0 + base;
-      if ((B & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + kF32R <= cur.count) {
-#pragma unroll
-        for (int q = 0; q < kF32R / 4; ++q)
-          reinterpret_cast<float4*>(o)[q] = make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
-      } else {
-#pragma unroll
-        for (int r = 0; r < kF32R; ++r)
-          if (base + r < cur.count) o[r] = acc[r];
-      }
+      for (int r = 0; r < 8; ++r)
+        if (base + r < cur.count) o[r] = acc[r];
     }
   }
 }
@@ -534,8 +585,7 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
   }
   switch (kind) {
     case kFirF32: {
-      const int grid = persistent_grid((const void*)fir_f32_kernel, kBlock, 0, items, 4);
-      hipLaunchKernelGGL(fir_f32_kernel, dim3(grid), dim3(kBlock), 0, st, (const float*)coeffs, T_,
+      hipLaunchKernelGGL(fir_f32_kernel, dim3(items), dim3(kBlock), 0, st, (const float*)coeffs, T_,
                          (const float*)src, (float*)dst, B, (const float*)hist_in, nchunks, items);
       break;
     }
