@@ -1,0 +1,351 @@
+// Batched complex FFT, q31 and q15, N = 256 / 512 / 1024 / 2048 — radix-16 register passes.
+//
+// Replaces the host scalar path of arm_cfft_q31 / arm_cfft_q15 (arm_cfft_q31.c:704-755,
+// radix4by2 :763-881; arm_cfft_q15.c:671-722, radix4by2 scalar :782-827 / :881-926;
+// arm_cfft_radix4_q31.c:153-473 / :524-834; arm_cfft_radix4_q15.c:572-970 / :1434-1813) and
+// arm_bitreversal_32 / _16 with armBitRevIndexTable_fixed_N, for the reference's own tables.
+// Same arithmetic as cfft_fx4096_kernel (cfft_fixed_core.hpp), generalised:
+//   * P = N/16 threads per transform, 16 complex per thread, 256 / P transforms per workgroup;
+//   * radix-4 stages fused in pairs (radix-16 register passes) with one LDS exchange between
+//     passes; N = 2M with M = 4^K odd powers of two (512, 2048) run the radix4by2 pre-pass and
+//     the first radix-4 stage of both halves in registers;
+//   * thread t' of a transform holds, per pass (stages s, s+1 of the radix-4 length M, group
+//     span L = M / 4^(s-1), strides d1 = L/4, d2 = L/16; j = t' mod d2, g = t' / d2):
+//       e(a, b) = h M + g L + j + d2 a + d1 b            (stage s over b, stage s+1 over a)
+//     with the first pass e = t' + P a + 4P b (coalesced loads) and the last pass on groups
+//     g = rev(t') -- 16-element groups for two stages, or four 4-element groups for one --
+//     so that the binary bit reversal of the output is free: every store instruction writes
+//     consecutive bins across the threads (by2 halves interleave: h = t' & 1);
+//   * LDS paddings s(e) = e + c1 (e >> k1) + c2 (e >> k2) and the per-transform stride found
+//     by tools/fx_r16_plan.py: conflict free under the ds_read2_b64 / ds_write_b64 (q31) and
+//     ds_read2_b32 / ds_write_b32 (q15) banking (N = 512: 1 extra cycle per 4 accesses);
+//   * buffer-resource I/O per group of transforms (out-of-range loads return 0 and stores are
+//     dropped, so a partial last group needs no bounds code), nontemporal; workgroup b takes
+//     the MI355X_FXR_T consecutive groups, the next group's words prefetched into registers
+//     under passes 2+, the loop entered after the first pass (see cfft_fx4096_kernel).
+#include "common.hpp"
+#include "kernels.hpp"
+#include "cfft_fixed_core.hpp"
+
+namespace mi355x {
+
+#ifndef MI355X_FXR_T
+#define MI355X_FXR_T 8
+#endif
+
+template <int N> struct R16 {
+  static constexpr int LOG = Log2<N>::v;
+  static constexpr bool BY2 = (LOG & 1) != 0;
+  static constexpr int M = BY2 ? N / 2 : N;      // radix-4 length
+  static constexpr int K = Log2<M>::v / 2;       // radix-4 stages
+  static constexpr int P = N / 16;               // threads per transform
+  static constexpr int PH = BY2 ? P / 2 : P;     // threads per radix-4 transform
+  static constexpr int TPW = kBlock / P;         // transforms per workgroup
+  static constexpr int MOD0 = BY2 ? 2 : 1;       // twiddle modifier of radix-4 stage 1
+  // stages handled by the first pass, then at most one middle pass, then the last pass
+  static constexpr int S_MID = BY2 ? 2 : 3;      // first stage of the middle pass
+  static constexpr bool HAS_MID = S_MID + 1 < K; // a two-stage middle pass before the last
+  static constexpr int S_LAST = HAS_MID ? S_MID + 2 : S_MID;
+  static constexpr bool LAST2 = S_LAST + 1 == K; // last pass holds two stages
+  static_assert(S_LAST == K || LAST2, "plan");
+};
+__device__ __forceinline__ constexpr int pow4(int s) { return 1 << (2 * s); }
+
+template <int N, bool Q31> struct R16Pad;   // tools/fx_r16_plan.py
+template <> struct R16Pad<256, true>   { static constexpr int k1 = 3, c1 = 0, k2 = 4, c2 = 1, stride = 271; };
+template <> struct R16Pad<256, false>  { static constexpr int k1 = 3, c1 = 0, k2 = 4, c2 = 1, stride = 272; };
+template <> struct R16Pad<512, true>   { static constexpr int k1 = 3, c1 = 0, k2 = 5, c2 = 1, stride = 527; };
+template <> struct R16Pad<512, false>  { static constexpr int k1 = 3, c1 = 0, k2 = 5, c2 = 1, stride = 527; };
+template <> struct R16Pad<1024, true>  { static constexpr int k1 = 6, c1 = 4, k2 = 8, c2 = 1, stride = 1087; };
+template <> struct R16Pad<1024, false> { static constexpr int k1 = 5, c1 = 2, k2 = 9, c2 = 1, stride = 1087; };
+template <> struct R16Pad<2048, true>  { static constexpr int k1 = 3, c1 = 0, k2 = 7, c2 = 1, stride = 2063; };
+template <> struct R16Pad<2048, false> { static constexpr int k1 = 3, c1 = 0, k2 = 6, c2 = 1, stride = 2079; };
+
+// Per-type register / LDS / global representations and the reference's butterflies.
+template <typename T, bool INV> struct R16Ops;
+template <bool INV> struct R16Ops<int32_t, INV> {
+  using V = int2;     // value in registers
+  using Tw = int2;    // twiddle operand
+  using W = int2;     // LDS word
+  using C = int2;     // global complex
+  static __device__ __forceinline__ V from_w(W w) { return w; }
+  static __device__ __forceinline__ W to_w(V v) { return v; }
+  static __device__ __forceinline__ Tw tw(const C* t, int i) { return t[i]; }
+  template <int KIND> static __device__ __forceinline__ void bf(V& a, V& b, V& c, V& d, Tw w1, Tw w2, Tw w3) {
+    bfly<int32_t, INV, KIND>(a, b, c, d, w1, w2, w3);
+  }
+  static __device__ __forceinline__ V ld(__amdgpu_buffer_rsrc_t r, int vo, int so) { return FxIO<int2>::ld(r, vo, so); }
+  static __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, int vo, int so, V v) { FxIO<int2>::st(r, vo, so, v); }
+  static __device__ __forceinline__ V by2_post(V v) { return make_int2(wshl(v.x, 1), wshl(v.y, 1)); }
+  static __device__ __forceinline__ V sat(V v) { return sat_shl1<int32_t>(v); }
+  // radix4by2 pre-pass pair (arm_cfft_q31.c:774-794 forward, :835-855 inverse)
+  static __device__ __forceinline__ void by2_pre(V& a, V& b, C w) {
+    const int32_t xt = wsub(a.x >> 2, b.x >> 2), yt = wsub(a.y >> 2, b.y >> 2);
+    a = make_int2(wadd(a.x >> 2, b.x >> 2), wadd(b.y >> 2, a.y >> 2));
+    int32_t p0 = mult_R(xt, w.x), p1 = mult_R(yt, w.x);
+    if (!INV) { p0 = multAcc_R(p0, yt, w.y); p1 = multSub_R(p1, xt, w.y); }
+    else      { p0 = multSub_R(p0, yt, w.y); p1 = multAcc_R(p1, xt, w.y); }
+    b = make_int2(wshl(p0, 1), wshl(p1, 1));
+  }
+};
+template <bool INV> struct R16Ops<int16_t, INV> {
+  using V = s16x2;    // one VGPR per complex (packed butterflies, cfft_fixed_core.hpp)
+  using Tw = TwP;
+  using W = uint32_t;
+  using C = short2;
+  static __device__ __forceinline__ V from_w(W w) { return pk(w); }
+  static __device__ __forceinline__ W to_w(V v) { return upk(v); }
+  static __device__ __forceinline__ Tw tw(const C* t, int i) { return twp<INV>(t[i]); }
+  template <int KIND> static __device__ __forceinline__ void bf(V& a, V& b, V& c, V& d, Tw w1, Tw w2, Tw w3) {
+    bfly_pk<INV, KIND>(a, b, c, d, w1, w2, w3);
+  }
+  static __device__ __forceinline__ V ld(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+    return pk((uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, vo, so, MI355X_FX_NT));
+  }
+  static __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, int vo, int so, V v) {
+    __builtin_amdgcn_raw_buffer_store_b32((int)upk(v), r, vo, so, MI355X_FX_NT);
+  }
+  static __device__ __forceinline__ V by2_post(V v) { return v << (short)1; }        // t16(x << 1)
+  static __device__ __forceinline__ V sat(V v) { return pk_sat_add(v, v); }          // __SSAT(x << 1, 16)
+  // radix4by2 pre-pass pair, scalar branch (arm_cfft_q15.c:782-800 forward, :881-899 inverse)
+  static __device__ __forceinline__ void by2_pre(V& A, V& B, C w) {
+    const int32_t ax = A.x, ay = A.y, bx = B.x, by = B.y;
+    const int32_t xt = t16((ax >> 1) - (bx >> 1)), yt = t16((ay >> 1) - (by >> 1));
+    A = s16x2{(short)(((ax >> 1) + (bx >> 1)) >> 1), (short)(((by >> 1) + (ay >> 1)) >> 1)};
+    const int32_t xc = t16((xt * w.x) >> 16), ys = t16((yt * w.y) >> 16);
+    const int32_t yc = t16((yt * w.x) >> 16), xs = t16((xt * w.y) >> 16);
+    if (!INV) B = s16x2{(short)(xc + ys), (short)(yc - xs)};
+    else      B = s16x2{(short)(xc - ys), (short)(yc + xs)};
+  }
+};
+
+template <typename T, int N, bool INV, bool BREV, bool SAT>
+__global__ __launch_bounds__(kBlock) void cfft_fx_r16_kernel(typename R16Ops<T, INV>::C* __restrict__ data,
+                                                             uint32_t batch,
+                                                             const typename R16Ops<T, INV>::C* __restrict__ tw) {
+  using R = R16<N>;
+  using O = R16Ops<T, INV>;
+  using V = typename O::V;
+  using Tw = typename O::Tw;
+  using W = typename O::W;
+  using C = typename O::C;
+  using PD = R16Pad<N, sizeof(T) == 4>;
+  constexpr int kC = (int)sizeof(C);
+  constexpr int P = R::P, M = R::M, K = R::K;
+  auto sfx = [](int e) { return e + PD::c1 * (e >> PD::k1) + PD::c2 * (e >> PD::k2); };
+
+  __shared__ __attribute__((aligned(16))) W lds_all[R::TPW * PD::stride];
+  const int t = threadIdx.x;
+  const int w = t / P, tp = t % P;                    // transform in the group, thread in it
+  W* lds = lds_all + w * PD::stride;
+  const int h = R::BY2 ? (tp & 1) : 0;                // by2 half of the later passes
+  const int tq = R::BY2 ? (tp >> 1) : tp;             // thread within that radix-4 transform
+
+  // ---- twiddles, lane-constant for the kernel's life
+  // first pass: non-by2 stage 1 (j = tp + P a) and stage 2 (j = tp); by2 pre-pass (i = tp + P u)
+  // and stage 1 of the halves (j = tp + P c, c < 2)
+  constexpr int NA0 = R::BY2 ? 2 : 4;
+  Tw tw0a[NA0][3], tw0b[3];
+  C twpre[R::BY2 ? 8 : 1];
+#pragma unroll
+  for (int a = 0; a < NA0; ++a)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) tw0a[a][k] = O::tw(tw, (k + 1) * (tp + P * a) * R::MOD0);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) tw0b[k] = O::tw(tw, (k + 1) * tp * 4 * R::MOD0);
+  if constexpr (R::BY2) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) twpre[u] = tw[tp + P * u];
+  }
+  // middle pass (stages S_MID, S_MID + 1): j = tq mod d2
+  constexpr int LM = M / pow4(R::S_MID - 1), D1M = LM / 4, D2M = LM / 16;
+  constexpr int MODM = R::MOD0 * pow4(R::S_MID - 1);
+  Tw twma[4][3], twmb[3];
+  if constexpr (R::HAS_MID) {
+    const int j = tq % D2M;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) twma[a][k] = O::tw(tw, (k + 1) * (j + D2M * a) * MODM);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) twmb[k] = O::tw(tw, (k + 1) * j * 4 * MODM);
+  }
+  // two-stage last pass: stage K-1 twiddles depend on a only
+  constexpr int MODL = R::MOD0 * pow4(K - 2);
+  Tw twl[4][3];
+  if constexpr (R::LAST2) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) twl[a][k] = O::tw(tw, (k + 1) * a * MODL);
+  }
+
+  // ---- work: groups of TPW transforms; workgroup b takes MI355X_FXR_T consecutive groups
+  const uint32_t ngroups = (batch + R::TPW - 1) / R::TPW;
+  const uint32_t g0 = blockIdx.x * MI355X_FXR_T;
+  const uint32_t gend = min(ngroups, g0 + MI355X_FXR_T);
+  if (g0 >= gend) return;
+  auto group_rsrc = [&](uint32_t g) {
+    const uint32_t first = g * R::TPW;
+    const uint32_t valid = min((uint32_t)R::TPW, batch - first);
+    return fx_rsrc(data + (size_t)first * N, valid * N * kC);
+  };
+  const int vin = (w * N + tp) * kC;                  // byte offset of the thread's first word
+  V nq[16];
+  auto fetch = [&](uint32_t g) {
+    const __amdgpu_buffer_rsrc_t r = group_rsrc(g);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) nq[u] = O::ld(r, vin, P * u * kC);   // e = tp + P u
+  };
+  V v[16];
+  // first pass from nq, then the next group's loads (they fly under the later passes)
+  auto pass0 = [&](uint32_t g) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = nq[u];
+    if constexpr (R::BY2) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) O::by2_pre(v[u], v[u + 8], twpre[u]);
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          O::template bf<0>(v[8 * hh + c], v[8 * hh + c + 2], v[8 * hh + c + 4], v[8 * hh + c + 6],
+                            tw0a[c][0], tw0a[c][1], tw0a[c][2]);
+    } else {
+      // v[4a + b] holds e = tp + P a + 4P b: stage 1 over b, stage 2 over a
+      V x[16];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) x[4 * a + b] = v[a + 4 * b];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        O::template bf<0>(x[4 * a], x[4 * a + 1], x[4 * a + 2], x[4 * a + 3], tw0a[a][0], tw0a[a][1], tw0a[a][2]);
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        O::template bf<K == 2 ? 2 : 1>(x[b], x[4 + b], x[8 + b], x[12 + b], tw0b[0], tw0b[1], tw0b[2]);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) v[a + 4 * b] = x[4 * a + b];
+    }
+    __syncthreads();                                  // the previous group's last reads are done
+#pragma unroll
+    for (int u = 0; u < 16; ++u) lds[sfx(tp + P * u)] = O::to_w(v[u]);
+    if (g + 1 < gend) fetch(g + 1);
+    __syncthreads();
+  };
+
+  fetch(g0);
+  pass0(g0);
+  for (uint32_t g = g0;;) {
+    // ---------------- middle pass: stages S_MID, S_MID + 1
+    if constexpr (R::HAS_MID) {
+      const int j = tq % D2M, gg = tq / D2M;
+      const int base = h * M + gg * LM + j;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) v[4 * a + b] = O::from_w(lds[sfx(base + D2M * a + D1M * b)]);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        O::template bf<1>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], twma[a][0], twma[a][1], twma[a][2]);
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        O::template bf<1>(v[b], v[4 + b], v[8 + b], v[12 + b], twmb[0], twmb[1], twmb[2]);
+      __syncthreads();
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) lds[sfx(base + D2M * a + D1M * b)] = O::to_w(v[4 * a + b]);
+      __syncthreads();
+    }
+    // ---------------- last pass, output with the bit reversal folded into the store
+    const __amdgpu_buffer_rsrc_t rx = group_rsrc(g);
+    int epos[16];                                     // element position of v[u] (bitReverseFlag 0)
+    int bin[16];                                      // output bin of v[u] minus tp (bitReverseFlag 1)
+    if constexpr (R::LAST2) {
+      const int gg = (int)(__brev((uint32_t)tq) >> (32 - Log2<M / 16>::v));
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          epos[4 * a + b] = h * M + 16 * gg + a + 4 * b;
+          v[4 * a + b] = O::from_w(lds[sfx(epos[4 * a + b])]);
+          bin[4 * a + b] = (int)(__brev((uint32_t)a) >> 30) * (N / 4) + (int)(__brev((uint32_t)b) >> 30) * (N / 16);
+        }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        O::template bf<1>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], twl[a][0], twl[a][1], twl[a][2]);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const Tw z{};
+        O::template bf<2>(v[b], v[4 + b], v[8 + b], v[12 + b], z, z, z);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int gc = (int)(__brev((uint32_t)(tq + R::PH * c)) >> (32 - Log2<M / 4>::v));
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          epos[4 * c + b] = h * M + 4 * gc + b;
+          v[4 * c + b] = O::from_w(lds[sfx(epos[4 * c + b])]);
+          bin[4 * c + b] = (int)(__brev((uint32_t)b) >> 30) * (N / 4) + P * c;
+        }
+        const Tw z{};
+        O::template bf<2>(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3], z, z, z);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if constexpr (R::BY2) v[u] = O::by2_post(v[u]);   // radix4by2 post-pass <<1
+      if constexpr (SAT) v[u] = O::sat(v[u]);
+      if constexpr (BREV) O::st(rx, vin, bin[u] * kC, v[u]);
+      else O::st(rx, (w * N + epos[u]) * kC, 0, v[u]);
+    }
+    if (++g >= gend) return;
+    pass0(g);
+  }
+}
+
+template <typename T, int N, bool INV, bool BREV, bool SAT>
+static void launch_r16_t(void* data, uint32_t batch, const void* tw, hipStream_t st) {
+  using C = typename R16Ops<T, INV>::C;
+  const uint32_t ngroups = (batch + R16<N>::TPW - 1) / R16<N>::TPW;
+  const uint32_t grid = (ngroups + MI355X_FXR_T - 1) / MI355X_FXR_T;
+  hipLaunchKernelGGL((cfft_fx_r16_kernel<T, N, INV, BREV, SAT>), dim3(grid), dim3(kBlock), 0, st, (C*)data, batch,
+                     (const C*)tw);
+}
+
+template <typename T, int N>
+static void launch_r16(void* data, uint32_t batch, const void* tw, uint32_t flags, hipStream_t st) {
+  const bool inv = flags & kIfft, brev = flags & kBitrev, sat = flags & kSatShl1;
+  if (inv) {
+    if (brev) sat ? launch_r16_t<T, N, true, true, true>(data, batch, tw, st) : launch_r16_t<T, N, true, true, false>(data, batch, tw, st);
+    else      sat ? launch_r16_t<T, N, true, false, true>(data, batch, tw, st) : launch_r16_t<T, N, true, false, false>(data, batch, tw, st);
+  } else {
+    if (brev) sat ? launch_r16_t<T, N, false, true, true>(data, batch, tw, st) : launch_r16_t<T, N, false, true, false>(data, batch, tw, st);
+    else      sat ? launch_r16_t<T, N, false, false, true>(data, batch, tw, st) : launch_r16_t<T, N, false, false, false>(data, batch, tw, st);
+  }
+}
+
+// Returns true if N is handled here (the reference's own bit-reversal table only).
+template <typename T>
+static bool dispatch_r16(int n, void* data, uint32_t batch, const void* tw, uint32_t flags, hipStream_t st) {
+  switch (n) {
+    case 256:  launch_r16<T, 256>(data, batch, tw, flags, st); return true;
+    case 512:  launch_r16<T, 512>(data, batch, tw, flags, st); return true;
+    case 1024: launch_r16<T, 1024>(data, batch, tw, flags, st); return true;
+    case 2048: launch_r16<T, 2048>(data, batch, tw, flags, st); return true;
+    default:   return false;
+  }
+}
+
+bool cfft_q31_r16_launch(int n, int32_t* data, uint32_t batch, const int32_t* tw, uint32_t flags, hipStream_t st) {
+  return dispatch_r16<int32_t>(n, data, batch, tw, flags, st);
+}
+bool cfft_q15_r16_launch(int n, int16_t* data, uint32_t batch, const int16_t* tw, uint32_t flags, hipStream_t st) {
+  return dispatch_r16<int16_t>(n, data, batch, tw, flags, st);
+}
+
+}  // namespace mi355x

@@ -128,20 +128,24 @@ __global__ __launch_bounds__(kBlock) void fir_f32_kernel(const float* __restrict
     const int off = it.n0 - T1;                  // window sample j is block sample off + j
     const float* p = src + (uint64_t)it.f * B + max(off, 0);
     const __amdgpu_buffer_rsrc_t r = buf_rsrc(p, (uint32_t)min(it.total + min(off, 0), (int)B - max(off, 0)) * 4u);
-    int pre[kPre], preh[kPreH];
+    // rows k < kPreH may lie in the history (offset clamped, word zeroed, OR-ed); later rows never do
+    const int o0 = min(off, 0);
+    int pre[kPre];
 #pragma unroll
-    for (int k = 0; k < kPre; ++k) pre[k] = __builtin_amdgcn_raw_buffer_load_b32(r, max(tid + k * kBlock + min(off, 0), 0) * 4, 0, 0);
-#pragma unroll
-    for (int k = 0; k < kPreH; ++k) preh[k] = 0;
+    for (int k = 0; k < kPre; ++k)
+      pre[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (k < kPreH ? max(tid + k * kBlock + o0, 0) : tid + k * kBlock + o0) * 4, 0, 0);
     if (off < 0) {
       const __amdgpu_buffer_rsrc_t rh = buf_rsrc(hist_in + (uint64_t)it.f * T1, (uint32_t)T1 * 4u);
 #pragma unroll
-      for (int k = 0; k < kPreH; ++k) preh[k] = __builtin_amdgcn_raw_buffer_load_b32(rh, (tid + k * kBlock) * 4, 0, 0);
+      for (int k = 0; k < kPreH; ++k) {
+        const int h = __builtin_amdgcn_raw_buffer_load_b32(rh, (tid + k * kBlock) * 4, 0, 0);
+        pre[k] = (tid + k * kBlock + off >= 0 ? pre[k] : 0) | h;
+      }
     }
 #pragma unroll
     for (int k = 0; k < kPre; ++k) {
       const int j = tid + k * kBlock;
-      if (j < kF32Win) win[wpos(j)] = __builtin_bit_cast(float, k < kPreH ? (j + off >= 0 ? pre[k] : 0) | preh[k] : pre[k]);
+      if (j < kF32Win) win[wpos(j)] = __builtin_bit_cast(float, pre[k]);
     }
   }
   __syncthreads();

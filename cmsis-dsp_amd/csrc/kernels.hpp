@@ -31,6 +31,10 @@ inline int persistent_grid(const void* kernel, int block, size_t lds, uint64_t i
 // (| kSatShl1 for q31 / q15).
 hipError_t cfft_f32_launch(int n, float* data, uint32_t batch, const float* tw, const uint16_t* perm,
                            uint32_t flags, hipStream_t st);
+// N = 256 / 512 / 1024 / 2048 with the reference's own bit-reversal table (cfft_fixed_r16.hip);
+// false if N is not one of those lengths.
+bool cfft_q31_r16_launch(int n, int32_t* data, uint32_t batch, const int32_t* tw, uint32_t flags, hipStream_t st);
+bool cfft_q15_r16_launch(int n, int16_t* data, uint32_t batch, const int16_t* tw, uint32_t flags, hipStream_t st);
 hipError_t cfft_q31_launch(int n, int32_t* data, uint32_t batch, const int32_t* tw, const uint16_t* perm,
                            uint32_t flags, hipStream_t st);
 hipError_t cfft_q15_launch(int n, int16_t* data, uint32_t batch, const int16_t* tw, const uint16_t* perm,

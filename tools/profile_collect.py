@@ -48,17 +48,24 @@ def bench_line(path):
     return None
 
 
-def trace_summary(d):
+def trace_summary(d, steps=None):
+    """Per kernel: the largest-grid dispatches; with `steps` (the bench line's timed step
+    count) only the LAST `steps` of them -- the timed region, after warmup and clock-settle
+    launches of the same grid."""
     ks = defaultdict(list)
     for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            ks[row["Kernel_Name"]].append((_grid(row), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
+            t0, t1 = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
+            ks[row["Kernel_Name"]].append((_grid(row), t1 - t0, t0))
     out = {}
     for k, v in ks.items():
         g = max(x[0] for x in v)
-        timed = [x[1] for x in v if x[0] == g]
-        out[k] = {"dispatches": len(v), "timed_dispatches": len(timed), "timed_grid": g,
-                  "timed_avg_ms": sum(timed) / len(timed) * 1e-6, "all_avg_ms": sum(x[1] for x in v) / len(v) * 1e-6}
+        big = sorted((x for x in v if x[0] == g), key=lambda x: x[2])
+        timed = [x[1] for x in (big[-steps:] if steps and len(big) >= steps else big)]
+        out[k] = {"dispatches": len(v), "largest_grid_dispatches": len(big), "timed_dispatches": len(timed),
+                  "timed_grid": g, "timed_avg_ms": sum(timed) / len(timed) * 1e-6,
+                  "largest_grid_avg_ms": sum(x[1] for x in big) / len(big) * 1e-6,
+                  "all_avg_ms": sum(x[1] for x in v) / len(v) * 1e-6}
     return out
 
 
@@ -97,7 +104,7 @@ def main():
         dest = os.path.join(ROOT, "profiles", rnd, name)
         os.makedirs(dest, exist_ok=True)
         line = bench_line(os.path.join(d, "bench_trace.json"))
-        tr = trace_summary(d)
+        tr = trace_summary(d, line.get("steps") if line else None)
         dom = [k for k in tr if ksub in k]
         rec = {"name": name, "bench_args": SPECS[name][0], "dominant_kernel_substring": ksub, "kernels": tr,
                "bench_config": line.get("config") if line else None}
