@@ -72,19 +72,24 @@ __device__ __forceinline__ int padx(int i) { return i + (i >> 3); }
 // four rounds: round q computes from buffers (q, q+1) while group q + 2 is read from LDS,
 // one round (128 VALU) ahead of its use, so every operand index is a compile-time constant
 // and no register moves.  LDS window layout: 8-sample groups at a pitch of 10 words
-// (wpos), so each ds_read_b64 of a group (lanes 8 words apart in sample terms) lands its
-// 32-lane half on 64 distinct banks; coefficients are read as ds_read_b128 broadcasts.
+// (wpos), so each ds_read2_b64 of a group (lanes 8 words apart in sample terms) lands each
+// 16-lane access on 32 distinct banks.  Coefficients are wave-uniform scalar loads into
+// SGPRs (the v_mul operand: no VGPRs, no LDS reads); the loop is 2 VALU per tap and output
+// plus 3 instructions per 512 (PMC: SQ_INSTS_VALU = 1.019 x the MAC minimum at 128 taps).
 __host__ __device__ constexpr int wpos(int j) { return j + 2 * (j >> 3); }
-constexpr int kF32Win = kF32Chunk + kFirMaxTaps + 8;        // window samples incl. the read-ahead group
 
+#ifndef MI355X_FIR_SCHED_BARRIER
+#define MI355X_FIR_SCHED_BARRIER 1
+#endif
 struct F32Grp { float v[8]; };
-__device__ __forceinline__ void ld_grp(F32Grp& g, const float* win, int grp) {
-  const float2* p = reinterpret_cast<const float2*>(win + 10 * grp);
+// group i after p (p + 10 i words): two ds_read2_b64 with immediate offsets
+__device__ __forceinline__ void ld_grp(F32Grp& g, const float* p, int i) {
+  const float2* q = reinterpret_cast<const float2*>(p + 10 * i);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float2 x = p[i];
-    g.v[2 * i] = x.x;
-    g.v[2 * i + 1] = x.y;
+  for (int h = 0; h < 4; ++h) {
+    const float2 x = q[h];
+    g.v[2 * h] = x.x;
+    g.v[2 * h + 1] = x.y;
   }
 }
 __device__ __forceinline__ void ld_coef(float (&c)[8], const float* cl, int k) {
@@ -97,116 +102,169 @@ __device__ __forceinline__ void f32_round(float (&acc)[8], const F32Grp& A, cons
   for (int u = 0; u < 8; ++u)
 #pragma unroll
     for (int r = 0; r < 8; ++r) acc[r] = acc[r] + (r + u < 8 ? A.v[r + u] : B.v[r + u - 8]) * c[u];
+#if MI355X_FIR_SCHED_BARRIER
+  __builtin_amdgcn_sched_barrier(0);   // keep each round's products next to their adds
+#endif
 }
 
-__global__ __launch_bounds__(kBlock) void fir_f32_kernel(const float* __restrict__ coeffs, int T,
+// Window rows staged per thread: KPRE * 256 >= chunk + T + 8 (the last block reads one group
+// past its taps), so the LDS image, the staging loads and the zero tail scale with numTaps.
+__host__ __device__ constexpr int fir_f32_kpre(int T) { return (kF32Chunk + T + 8 + kBlock - 1) / kBlock; }
+
+// Window staging of one item into registers, through buffer resources: window sample j is
+// block sample s = n0 - T1 + j, read from [0, n0 + count) of the filter's block (a negative
+// offset or one past the window is out of range and returns 0), OR-ed with history word
+// n0 + j, read from [0, T1) of the filter's history (only the first chunk, n0 < T1, reaches
+// it).  The per-row offsets pass through an empty asm so that the compiler cannot split a
+// constant part into the instruction's immediate: the range check takes the VGPR offset
+// alone, and a negative one would not be wrapped back into range by a positive immediate.
+__device__ __forceinline__ int opaque(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+// Rows k >= KPRE - 8 never reach the history (T1 < 256 (KPRE - 8)); the history words are
+// kept apart and OR-ed in when the window is written to LDS, so no wait is placed before the
+// MACs that the fetch is meant to overlap.
+template <int KPRE>
+struct F32Win {
+  int x[KPRE];
+  int h[KPRE - 8];
+};
+template <int KPRE>
+__device__ __forceinline__ void fir_f32_fetch(F32Win<KPRE>& w, const FirItem& it, const float* __restrict__ src,
+                                              const float* __restrict__ hist_in, uint32_t B, int T1, int tid) {
+  const __amdgpu_buffer_rsrc_t r = buf_rsrc(src + (uint64_t)it.f * B, (uint32_t)(it.n0 + it.count) * 4u);
+  const __amdgpu_buffer_rsrc_t rh = buf_rsrc(hist_in + (uint64_t)it.f * T1, (uint32_t)T1 * 4u);
+  const int v0 = (tid + it.n0 - T1) * 4, h0 = (tid + it.n0) * 4;
+#pragma unroll
+  for (int k = 0; k < KPRE; ++k) w.x[k] = __builtin_amdgcn_raw_buffer_load_b32(r, opaque(v0 + 1024 * k), 0, 0);
+#pragma unroll
+  for (int k = 0; k < KPRE - 8; ++k)
+    w.h[k] = __builtin_amdgcn_raw_buffer_load_b32(rh, opaque(h0 + 1024 * k), 0, 0);   // n0 >= T1: out of range, 0
+}
+template <int KPRE>
+__device__ __forceinline__ void fir_f32_put(float* wl, const F32Win<KPRE>& w) {
+#pragma unroll
+  for (int k = 0; k < KPRE; ++k)
+    wl[wpos(k * kBlock)] = __builtin_bit_cast(float, k < KPRE - 8 ? (w.x[k] | w.h[k < KPRE - 8 ? k : 0]) : w.x[k]);
+}
+
+// Items per workgroup.  Workgroups of identical work started together finish together, so with
+// one item each every generation of co-resident workgroups stages its window at the same time
+// and the SIMDs idle for the load latency (≈10 % of the launch, PMC: 89.5 % VALU busy).  A
+// workgroup instead walks ipw consecutive items with the next item's window in registers
+// while it filters the current one.  MI355X_FIR_IPW > 0: fixed ipw (default 16); 0: ipw =
+// items / (resident workgroups x CUs), one generation of persistent workgroups.  Measured at
+// 2^17 items (Gsamples/s): ipw 1 209, 2 214, 4 216, 8 219, 16 217-222, 32 210-215,
+// persistent (64) 206-208.
+#ifndef MI355X_FIR_IPW
+#define MI355X_FIR_IPW 16
+#endif
+
+#ifndef MI355X_FIR_F32_WAVES
+#define MI355X_FIR_F32_WAVES 8     // minimum waves per SIMD the register allocation must allow
+#endif
+template <int KPRE>
+__global__ __launch_bounds__(kBlock, MI355X_FIR_F32_WAVES) void fir_f32_kernel(const float* __restrict__ coeffs, int T,
                                                          const float* __restrict__ src, float* __restrict__ dst,
                                                          uint32_t B, const float* __restrict__ hist_in,
-                                                         uint32_t nchunks, uint32_t items) {
-  __shared__ __attribute__((aligned(16))) float win[wpos(kF32Win) + 16];
-  __shared__ __attribute__((aligned(16))) float cl[kFirMaxTaps + 8];
+                                                         uint32_t nchunks, uint32_t items, uint32_t ipw) {
+  constexpr int kWin = KPRE * kBlock;
+  __shared__ __attribute__((aligned(16))) float win[wpos(kWin) + 16];
   const int T1 = T - 1;
-  const uint32_t item = blockIdx.x;
-  if (item >= items) return;
-  for (int i = threadIdx.x; i < T; i += kBlock) cl[i] = coeffs[i];    // visible after the barrier
-  // Window staging through buffer resources sized to the item: reads past the window (or, in
-  // the first chunk, past the history / before the block) return 0 without index arithmetic.
-  // Window staging through buffer resources sized to the item: reads past the window return
-  // 0 without index arithmetic.  In the first chunk the window is [history (T1) ; block
-  // input]: the block part is read at offset max(j - T1, 0) and zeroed for j < T1, then OR-ed
-  // with the history word (history reads past T1 return 0).  Offsets are kept non-negative:
-  // the compiler moves constant parts of an offset into the instruction's immediate, and the
-  // hardware range check does not wrap a negative VGPR offset back into range.
-  // One item per workgroup: with 57 VGPRs and 19.6 KiB of LDS, eight workgroups share a CU
-  // and hide each other's staging (a persistent grid with a register prefetch of the next
-  // window measured neutral in round 1).
-  constexpr int kPre = (kF32Win + kBlock - 1) / kBlock;
-  constexpr int kPreH = (kFirMaxTaps - 1 + kBlock - 1) / kBlock;
-  const FirItem it = fir_item(item, nchunks, B, T1, kF32Chunk);
-  {
-    const int tid = threadIdx.x;
-    const int off = it.n0 - T1;                  // window sample j is block sample off + j
-    const float* p = src + (uint64_t)it.f * B + max(off, 0);
-    const __amdgpu_buffer_rsrc_t r = buf_rsrc(p, (uint32_t)min(it.total + min(off, 0), (int)B - max(off, 0)) * 4u);
-    // rows k < kPreH may lie in the history (offset clamped, word zeroed, OR-ed); later rows never do
-    const int o0 = min(off, 0);
-    int pre[kPre];
-#pragma unroll
-    for (int k = 0; k < kPre; ++k)
-      pre[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (k < kPreH ? max(tid + k * kBlock + o0, 0) : tid + k * kBlock + o0) * 4, 0, 0);
-    if (off < 0) {
-      const __amdgpu_buffer_rsrc_t rh = buf_rsrc(hist_in + (uint64_t)it.f * T1, (uint32_t)T1 * 4u);
-#pragma unroll
-      for (int k = 0; k < kPreH; ++k) {
-        const int h = __builtin_amdgcn_raw_buffer_load_b32(rh, (tid + k * kBlock) * 4, 0, 0);
-        pre[k] = (tid + k * kBlock + off >= 0 ? pre[k] : 0) | h;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kPre; ++k) {
-      const int j = tid + k * kBlock;
-      if (j < kF32Win) win[wpos(j)] = __builtin_bit_cast(float, pre[k]);
-    }
-  }
-  __syncthreads();
+  const uint32_t i0 = blockIdx.x * ipw;
+  if (i0 >= items) return;
+  const uint32_t i1 = min(items, i0 + ipw);
+  const int tid = threadIdx.x;
   const int rounds = T >> 3;
-  const int lane = threadIdx.x;
-  const int base = lane * kF32R;                    // local output index of this lane
-  if (base >= it.count) return;
-  {
-    const FirItem& cur = it;
+  const int base = tid * kF32R;                     // local output index of this lane
+  float* wl = win + wpos(tid);                      // wpos(tid + 256 k) = wpos(tid) + 320 k
+  F32Win<KPRE> pre;
+  FirItem cur = fir_item(i0, nchunks, B, T1, kF32Chunk);
+  fir_f32_fetch<KPRE>(pre, cur, src, hist_in, B, T1, tid);
+  fir_f32_put<KPRE>(wl, pre);
+  // Per item: barrier (window ready) -> next window's loads -> MACs -> barrier (window free)
+  // -> next window to LDS -> output stores.  The window write waits only for loads that had a
+  // whole item of MACs to land; the stores are issued after it, so no wait ever covers them.
+  for (uint32_t item = i0;;) {
+    __syncthreads();
+    const bool more = item + 1 < i1;
+    const FirItem nxt = more ? fir_item(item + 1, nchunks, B, T1, kF32Chunk) : cur;
+    if (more) fir_f32_fetch<KPRE>(pre, nxt, src, hist_in, B, T1, tid);
     float acc[8];
+    if (base < cur.count) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) acc[r] = 0.0f;
-    F32Grp X0, X1, X2, X3;
-    float c0[8], c1[8];
-    ld_grp(X0, win, lane);
-    ld_grp(X1, win, lane + 1);
-    int q = 0;
-    for (; q + 4 <= rounds; q += 4) {
-      ld_coef(c0, cl, 8 * q);
-      ld_grp(X2, win, lane + q + 2);
-      f32_round(acc, X0, X1, c0);
-      ld_coef(c1, cl, 8 * q + 8);
-      ld_grp(X3, win, lane + q + 3);
-      f32_round(acc, X1, X2, c1);
-      ld_coef(c0, cl, 8 * q + 16);
-      ld_grp(X0, win, lane + q + 4);
-      f32_round(acc, X2, X3, c0);
-      ld_coef(c1, cl, 8 * q + 24);
-      ld_grp(X1, win, lane + q + 5);
-      f32_round(acc, X3, X0, c1);
-    }
-    // 0..3 remaining whole rounds, same buffer order
-    if (q < rounds) {
-      ld_coef(c0, cl, 8 * q);
-      ld_grp(X2, win, lane + q + 2);
-      f32_round(acc, X0, X1, c0);
-      if (q + 1 < rounds) {
-        ld_coef(c1, cl, 8 * q + 8);
-        ld_grp(X3, win, lane + q + 3);
-        f32_round(acc, X1, X2, c1);
-        if (q + 2 < rounds) {
-          ld_coef(c0, cl, 8 * q + 16);
+      for (int r = 0; r < 8; ++r) acc[r] = 0.0f;
+      F32Grp X0, X1, X2, X3;
+      float c0[8], c1[8];
+      // Four group buffers rotate by name over a block of four rounds; the window pointer
+      // advances once per block, so every LDS read is base + immediate.  Coefficients are
+      // wave-uniform: scalar loads (s_load_dwordx8 per round) into SGPRs, the v_mul operand
+      // (no VGPRs, no LDS reads).
+      const float* wp = win + 10 * tid;
+      const float* cp = coeffs;
+      ld_grp(X0, wp, 0);
+      ld_grp(X1, wp, 1);
+      int nb = rounds >> 2;
+      if (nb > 0) {
+        do {
+          ld_coef(c0, cp, 0);
+          ld_grp(X2, wp, 2);
+          f32_round(acc, X0, X1, c0);
+          ld_coef(c1, cp, 8);
+          ld_grp(X3, wp, 3);
+          f32_round(acc, X1, X2, c1);
+          ld_coef(c0, cp, 16);
+          ld_grp(X0, wp, 4);
           f32_round(acc, X2, X3, c0);
+          ld_coef(c1, cp, 24);
+          ld_grp(X1, wp, 5);
+          f32_round(acc, X3, X0, c1);
+          wp += 40;
+          cp += 32;
+        } while (--nb);
+      }
+      // 0..3 remaining whole rounds, same buffer order
+      const int rem = rounds & 3;
+      if (rem > 0) {
+        ld_coef(c0, cp, 0);
+        ld_grp(X2, wp, 2);
+        f32_round(acc, X0, X1, c0);
+        if (rem > 1) {
+          ld_coef(c1, cp, 8);
+          ld_grp(X3, wp, 3);
+          f32_round(acc, X1, X2, c1);
+          if (rem > 2) {
+            ld_coef(c0, cp, 16);
+            f32_round(acc, X2, X3, c0);
+          }
         }
       }
-    }
-    // numTaps % 8 tail taps, straight from LDS
-    for (int k = 8 * rounds; k < T; ++k) {
-      const float c = cl[k];
+      // numTaps % 8 tail taps, straight from LDS
+      for (int k = 8 * rounds; k < T; ++k) {
+        const float c = coeffs[k];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) acc[r] = acc[r] + win[wpos(base + k + r)] * c;
+        for (int r = 0; r < 8; ++r) acc[r] = acc[r] + win[wpos(base + k + r)] * c;
+      }
     }
-    float* o = dst + (uint64_t)cur.f * B + cur.n0 + base;
-    if ((B & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + 8 <= cur.count) {
-      reinterpret_cast<float4*>(o)[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-      reinterpret_cast<float4*>(o)[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
-    } else {
+    if (more) {
+      __syncthreads();                              // every wave is done reading this window
+      fir_f32_put<KPRE>(wl, pre);
+    }
+    if (base < cur.count) {
+      float* o = dst + (uint64_t)cur.f * B + cur.n0 + base;
+      if ((B & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + 8 <= cur.count) {
+        reinterpret_cast<float4*>(o)[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        reinterpret_cast<float4*>(o)[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+      } else {
 #pragma unroll
-      for (int r = 0; r < 8; ++r)
-        if (base + r < cur.count) o[r] = acc[r];
+        for (int r = 0; r < 8; ++r)
+          if (base + r < cur.count) o[r] = acc[r];
+      }
     }
+    if (!more) break;
+    cur = nxt;
+    ++item;
   }
 }
 
@@ -589,8 +647,16 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
   }
   switch (kind) {
     case kFirF32: {
-      hipLaunchKernelGGL(fir_f32_kernel, dim3(items), dim3(kBlock), 0, st, (const float*)coeffs, T_,
-                         (const float*)src, (float*)dst, B, (const float*)hist_in, nchunks, items);
+      const int kpre = fir_f32_kpre(T_);
+      auto k = kpre <= 9 ? fir_f32_kernel<9> : kpre == 10 ? fir_f32_kernel<10> : kpre == 11 ? fir_f32_kernel<11>
+             : kpre == 12 ? fir_f32_kernel<12> : fir_f32_kernel<13>;
+      uint32_t ipw = MI355X_FIR_IPW;
+      if (!ipw) {
+        const uint32_t resident = (uint32_t)persistent_grid((const void*)k, kBlock, 0, items);
+        ipw = (items + resident - 1) / resident;
+      }
+      hipLaunchKernelGGL(k, dim3((items + ipw - 1) / ipw), dim3(kBlock), 0, st, (const float*)coeffs, T_,
+                         (const float*)src, (float*)dst, B, (const float*)hist_in, nchunks, items, ipw);
       break;
     }
     case kFirQ15:
