@@ -19,7 +19,8 @@ import numpy as np
 
 from . import _abi
 from ._abi import (arm_cfft_instance_f32, arm_cfft_instance_q15, arm_cfft_instance_q31,  # noqa: F401
-                   arm_fir_instance_f32, arm_fir_instance_q15, arm_fir_instance_q31, arm_matrix_instance_f32,
+                   arm_fir_instance_f32, arm_fir_instance_q15, arm_fir_instance_q31, arm_fir_instance_q7,
+                   arm_matrix_instance_f32,
                    arm_rfft_fast_instance_f32, arm_mfcc_instance_f32, arm_matrix_instance_q15,
                    arm_matrix_instance_q31, arm_rfft_instance_q31, arm_rfft_instance_q15, ARM_MATH_SUCCESS,
                    ARM_MATH_ARGUMENT_ERROR, ARM_MATH_SIZE_MISMATCH)
@@ -218,6 +219,25 @@ class FirQ31(FirF32):
         return y
 
 
+class FirQ7(FirF32):
+    """Streaming arm_fir_q7."""
+
+    def __init__(self, coeffs, block_size):
+        self.coeffs = np.ascontiguousarray(coeffs, dtype=np.int8)
+        self.block_size = block_size
+        self.state = np.zeros(len(self.coeffs) + block_size - 1, dtype=np.int8)
+        self.S = arm_fir_instance_q7()
+        lib.arm_fir_init_q7(C.byref(self.S), len(self.coeffs), self.coeffs.ctypes.data,
+                            self.state.ctypes.data, block_size)
+
+    def __call__(self, x):
+        x = np.ascontiguousarray(x, dtype=np.int8)
+        y = np.empty_like(x)
+        lib.arm_fir_q7(C.byref(self.S), x.ctypes.data, y.ctypes.data, len(x))
+        _check_void("arm_fir_q7")
+        return y
+
+
 class FirFastQ15(FirQ15):
     """Streaming arm_fir_fast_q15."""
 
@@ -341,15 +361,15 @@ def rfft_fast_batch(S, p, out, ifft, stream=None):
 
 
 _FIR_BATCH = {"f32": "arm_fir_f32_batch", "q15": "arm_fir_q15_batch", "q31": "arm_fir_q31_batch",
-              "fast_q15": "arm_fir_fast_q15_batch", "fast_q31": "arm_fir_fast_q31_batch"}
+              "fast_q15": "arm_fir_fast_q15_batch", "fast_q31": "arm_fir_fast_q31_batch", "q7": "arm_fir_q7_batch"}
 
 
 def fir_batch(S, src, dst, hist, stream=None, q15=False, kind=None):
     """src/dst: [batch, blockSize] device tensors; hist: [batch, numTaps-1] device state.
-    kind: f32 | q15 | q31 | fast_q15 | fast_q31 (default from the instance type / q15 flag)."""
+    kind: f32 | q15 | q31 | fast_q15 | fast_q31 | q7 (default from the instance type / q15 flag)."""
     if kind is None:
         kind = "q15" if q15 else {arm_fir_instance_f32: "f32", arm_fir_instance_q15: "q15",
-                                  arm_fir_instance_q31: "q31"}[type(S)]
+                                  arm_fir_instance_q31: "q31", arm_fir_instance_q7: "q7"}[type(S)]
     batch, block = src.shape
     fn = getattr(lib, _FIR_BATCH[kind])
     st = fn(C.byref(S), C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()), block, batch,
@@ -359,8 +379,8 @@ def fir_batch(S, src, dst, hist, stream=None, q15=False, kind=None):
 
 
 def arm_conv(kind, a, b):
-    """arm_conv_f32 / _q15 / _q31 (drop-in, numpy): len(a) + len(b) - 1 samples."""
-    dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32}[kind]
+    """arm_conv_f32 / _q15 / _q31 / _q7 (drop-in, numpy): len(a) + len(b) - 1 samples."""
+    dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32, "q7": np.int8}[kind]
     a = np.ascontiguousarray(a, dtype=dt)
     b = np.ascontiguousarray(b, dtype=dt)
     y = np.zeros(len(a) + len(b) - 1, dtype=dt)
@@ -372,7 +392,7 @@ def arm_conv(kind, a, b):
 def conv_batch(a, b, out, stream=None):
     """out[i] = a[i] (*) b[i]; a [batch, La], b [batch, Lb] or [Lb] (shared), out [batch, La+Lb-1]."""
     import torch
-    kind = {torch.float32: "f32", torch.int16: "q15", torch.int32: "q31"}[a.dtype]
+    kind = {torch.float32: "f32", torch.int16: "q15", torch.int32: "q31", torch.int8: "q7"}[a.dtype]
     batch, la = a.shape
     lb = b.shape[-1]
     sb = 0 if b.dim() == 1 else b.stride(0)
@@ -387,7 +407,7 @@ def arm_conv_family(fn, a, b, first=0, num=0, fill=0):
     """Drop-in (numpy) call of arm_<fn>, fn in _abi.CONV_FULL + _abi.CONV_PARTIAL (e.g.
     "correlate_q15", "conv_partial_f32", "conv_fast_q31"): returns (pDst, status); pDst is
     pre-filled with `fill`, since partial / correlate leave the words they do not compute."""
-    dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32}[fn[-3:]]
+    dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32, "q7": np.int8}[fn.split("_")[-1]]
     a = np.ascontiguousarray(a, dtype=dt)
     b = np.ascontiguousarray(b, dtype=dt)
     n = 2 * max(len(a), len(b)) - 1 if fn.startswith("correlate") else len(a) + len(b) - 1

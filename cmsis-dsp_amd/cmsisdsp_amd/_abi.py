@@ -50,6 +50,10 @@ class arm_fir_instance_f32(C.Structure):
     _fields_ = [("numTaps", C.c_uint16), ("pState", c_f32p), ("pCoeffs", c_f32p)]
 
 
+class arm_fir_instance_q7(C.Structure):
+    _fields_ = [("numTaps", C.c_uint16), ("pState", C.c_void_p), ("pCoeffs", C.c_void_p)]
+
+
 class arm_fir_instance_q15(C.Structure):
     # Include/dsp/filtering_functions.h:66-71
     _fields_ = [("numTaps", C.c_uint16), ("pState", c_i16p), ("pCoeffs", c_i16p)]
@@ -88,8 +92,8 @@ SIZES = (16, 32, 64, 128, 256, 512, 1024, 2048, 4096)
 RFFT_SIZES = (32, 64, 128, 256, 512, 1024, 2048, 4096)
 # convolution / correlation family (drop-in names without the arm_ prefix)
 CONV_FULL = ("conv_f32", "conv_q15", "conv_q31", "conv_fast_q15", "conv_fast_q31", "correlate_f32", "correlate_q15",
-             "correlate_q31", "correlate_fast_q15", "correlate_fast_q31")
-CONV_PARTIAL = ("conv_partial_f32", "conv_partial_q15", "conv_partial_q31")
+             "correlate_q31", "correlate_fast_q15", "correlate_fast_q31", "conv_q7", "correlate_q7")
+CONV_PARTIAL = ("conv_partial_f32", "conv_partial_q15", "conv_partial_q31", "conv_partial_q7")
 # product only (the oracle restates them as arm_conv_fast_* over the range; the reference's
 # own bodies are memory-unsafe for most ranges)
 CONV_PARTIAL_FAST = ("conv_partial_fast_q15", "conv_partial_fast_q31")
@@ -116,6 +120,8 @@ DROPIN = {
     "arm_fir_init_q31": (None, [P(arm_fir_instance_q31), C.c_uint16, C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_fir_q31": (None, [P(arm_fir_instance_q31), C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_fir_fast_q31": (None, [P(arm_fir_instance_q31), C.c_void_p, C.c_void_p, C.c_uint32]),
+    "arm_fir_init_q7": (None, [P(arm_fir_instance_q7), C.c_uint16, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "arm_fir_q7": (None, [P(arm_fir_instance_q7), C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_mat_init_f32": (None, [P(arm_matrix_instance_f32), C.c_uint16, C.c_uint16, C.c_void_p]),
     "arm_mat_init_q15": (None, [P(arm_matrix_instance_q15), C.c_uint16, C.c_uint16, C.c_void_p]),
     "arm_mat_init_q31": (None, [P(arm_matrix_instance_q31), C.c_uint16, C.c_uint16, C.c_void_p]),
@@ -185,6 +191,8 @@ BATCHED = {
                                     C.c_void_p, C.c_void_p]),
     "arm_fir_fast_q31_batch": (C.c_int, [P(arm_fir_instance_q31), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                          C.c_void_p, C.c_void_p]),
+    "arm_fir_q7_batch": (C.c_int, [P(arm_fir_instance_q7), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                   C.c_void_p, C.c_void_p]),
     "arm_mat_mult_f32_batch": (C.c_int, [P(arm_matrix_instance_f32), P(arm_matrix_instance_f32),
                                          P(arm_matrix_instance_f32), C.c_uint32, C.c_void_p]),
     "arm_mat_mult_q15_batch": (C.c_int, [P(arm_matrix_instance_q15), P(arm_matrix_instance_q15),

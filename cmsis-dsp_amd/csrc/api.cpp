@@ -631,8 +631,16 @@ void arm_fir_init_q31(arm_fir_instance_q31* S, uint16_t numTaps, const q31_t* pC
   if (S) fir_init<int32_t>(S, numTaps, pCoeffs, pState, blockSize);
 }
 
+void arm_fir_init_q7(arm_fir_instance_q7* S, uint16_t numTaps, const q7_t* pCoeffs, q7_t* pState,
+                     uint32_t blockSize) {
+  if (S) fir_init<int8_t>(S, numTaps, pCoeffs, pState, blockSize);
+}
+
 void arm_fir_f32(const arm_fir_instance_f32* S, const float32_t* pSrc, float32_t* pDst, uint32_t blockSize) {
   fir_sync<float>(S, pSrc, pDst, blockSize, kFirF32);
+}
+void arm_fir_q7(const arm_fir_instance_q7* S, const q7_t* pSrc, q7_t* pDst, uint32_t blockSize) {
+  fir_sync<int8_t>(S, pSrc, pDst, blockSize, kFirQ7);
 }
 void arm_fir_q15(const arm_fir_instance_q15* S, const q15_t* pSrc, q15_t* pDst, uint32_t blockSize) {
   fir_sync<int16_t>(S, pSrc, pDst, blockSize, kFirQ15);
@@ -665,6 +673,10 @@ arm_status arm_fir_q31_batch(const arm_fir_instance_q31* S, const q31_t* d_src, 
 arm_status arm_fir_fast_q31_batch(const arm_fir_instance_q31* S, const q31_t* d_src, q31_t* d_dst, uint32_t blockSize,
                                   uint32_t batch, q31_t* d_hist, void* stream) {
   return fir_batch<int32_t>(S, d_src, d_dst, blockSize, batch, d_hist, stream, kFirFastQ31);
+}
+arm_status arm_fir_q7_batch(const arm_fir_instance_q7* S, const q7_t* d_src, q7_t* d_dst, uint32_t blockSize,
+                            uint32_t batch, q7_t* d_hist, void* stream) {
+  return fir_batch<int8_t>(S, d_src, d_dst, blockSize, batch, d_hist, stream, kFirQ7);
 }
 
 arm_status arm_mat_mult_f32(const arm_matrix_instance_f32* pSrcA, const arm_matrix_instance_f32* pSrcB,
@@ -811,6 +823,8 @@ MI355X_CONV_FULL(arm_correlate_q15, q15_t, int16_t, kConvQ15, kVarCorr)
 MI355X_CONV_FULL(arm_correlate_q31, q31_t, int32_t, kConvQ31, kVarCorr)
 MI355X_CONV_FULL(arm_correlate_fast_q15, q15_t, int16_t, kConvFastQ15, kVarCorr)
 MI355X_CONV_FULL(arm_correlate_fast_q31, q31_t, int32_t, kConvFastQ31, kVarCorr)
+MI355X_CONV_FULL(arm_conv_q7, q7_t, int8_t, kConvQ7, kVarConv)
+MI355X_CONV_FULL(arm_correlate_q7, q7_t, int8_t, kConvQ7, kVarCorr)
 #undef MI355X_CONV_FULL
 
 #define MI355X_CONV_PARTIAL(NAME, T, CT, OP)                                                                       \
@@ -831,6 +845,7 @@ MI355X_CONV_FULL(arm_correlate_fast_q31, q31_t, int32_t, kConvFastQ31, kVarCorr)
 MI355X_CONV_PARTIAL(arm_conv_partial_f32, float32_t, float, kConvF32)
 MI355X_CONV_PARTIAL(arm_conv_partial_q15, q15_t, int16_t, kConvQ15)
 MI355X_CONV_PARTIAL(arm_conv_partial_q31, q31_t, int32_t, kConvQ31)
+MI355X_CONV_PARTIAL(arm_conv_partial_q7, q7_t, int8_t, kConvQ7)
 // arm_conv_partial_fast_q15 / _q31: outputs firstIndex .. of arm_conv_fast_q15 / _q31.  The
 // reference's own bodies (arm_conv_partial_fast_q15.c:110-118 stage sizes) read outside the
 // inputs for most ranges (the host build segfaults: tools/probes/conv_family_model.py), so

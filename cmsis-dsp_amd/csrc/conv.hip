@@ -5,6 +5,9 @@
 //   arm_conv_partial_f32.c / _q15.c / _q31.c (!ARM_MATH_DSP branch, :635-679 / :715-759)
 //   arm_correlate_f32.c / _q15.c / _q31.c   (!ARM_MATH_DSP branch, :1013-1096 / :814-895)
 //   arm_conv_fast_q15.c, arm_conv_fast_q31.c, arm_correlate_fast_q15.c, _fast_q31.c
+//   arm_conv_q7.c, arm_conv_partial_q7.c (!ARM_MATH_DSP, :688-735), arm_correlate_q7.c:
+//     q31_t sum of q7 x q7 products (int32 adds / __SMLAD pairs, both wrap: a modular sum,
+//     any order), output __SSAT(sum >> 7, 8)
 // Every exact variant sums each output over the overlap in ASCENDING index of the summed
 // input x (conv: pSrcA, whichever is longer; correlate: the longer input), f32 mul then add
 // from 0.0f, q15/q31 an exact q63 sum.  Correlation is the convolution of x with the time-
@@ -61,6 +64,14 @@ template <> struct ConvT<kConvFastQ15> {
   using T = int16_t; using Acc = uint32_t;
   static __device__ __forceinline__ Acc mac(Acc a, T w, T c) { return a + (uint32_t)((int32_t)w * (int32_t)c); }
   static __device__ __forceinline__ T out(Acc a) { return (T)((int32_t)a >> 15); }
+};
+template <> struct ConvT<kConvQ7> {
+  using T = int8_t; using Acc = uint32_t;
+  static __device__ __forceinline__ Acc mac(Acc a, T w, T c) { return a + (uint32_t)((int32_t)w * (int32_t)c); }
+  static __device__ __forceinline__ T out(Acc a) {
+    const int32_t v = (int32_t)a >> 7;
+    return (T)(v > 127 ? 127 : v < -128 ? -128 : v);
+  }
 };
 template <> struct ConvT<kConvFastQ31> {
   using T = int32_t; using Acc = uint32_t;
@@ -226,6 +237,7 @@ hipError_t conv_family_run(const ConvJob& j, hipStream_t st) {
     MI355X_CONV_CASE(kConvQ31)
     MI355X_CONV_CASE(kConvFastQ15)
     MI355X_CONV_CASE(kConvFastQ31)
+    MI355X_CONV_CASE(kConvQ7)
     default: return hipErrorInvalidValue;
   }
 #undef MI355X_CONV_CASE

@@ -596,6 +596,120 @@ __global__ __launch_bounds__(kBlock) void fir_q31_kernel(const int32_t* __restri
   }
 }
 
+// ---------------------------------------------------------------- q7
+// arm_fir_q7 (arm_fir_q7.c:446-560, LOOPUNROLL and tail alike): q31_t accumulator of q7 x q7
+// products with plain int32 adds (wrapping on the gcc x86-64 build: a modular sum, the same
+// in any order), y = __SSAT(acc >> 7, 8).  A tap quad c[4m..4m+3] times a sample quad is one
+// v_dot4_i32_i8 (no clamp: modular).  The window is staged as aligned byte-quad words W, then
+// as four LDS planes, plane p word i = (x[4i+p], .., x[4i+p+3]) = alignbyte(W[i+1], W[i], p);
+// output base + r at tap quad m reads plane r & 3, word base/4 + (r >> 2) + m.  Two quads per
+// block: each plane is read as an aligned 2-word pair one block ahead (3-slot ring).
+constexpr int kQ7W = (kFirChunk + kFirMaxTaps) / 4 + 16;   // words per plane (+ look-ahead)
+__device__ __forceinline__ int32_t dot4(uint32_t x, uint32_t c, int32_t acc) {
+  return __builtin_amdgcn_sdot4((int)x, (int)c, acc, false);
+}
+struct Q7Ring { uint2 p[4][3]; };
+template <int S>
+__device__ __forceinline__ void q7_fetch(Q7Ring& r, const uint32_t* lds, int w) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) r.p[q][S] = *reinterpret_cast<const uint2*>(lds + q * kQ7W + w);
+}
+template <int P>
+__device__ __forceinline__ void q7_block(Q7Ring& r, const uint32_t* lds, int w_ahead, const uint2 c2,
+                                         int32_t (&A)[kFirR]) {
+  q7_fetch<(P + 2) % 3>(r, lds, w_ahead);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const uint32_t c = u ? c2.y : c2.x;
+#pragma unroll
+    for (int rr = 0; rr < kFirR; ++rr) {
+      const int q = rr & 3, i = u + (rr >> 2), s = i < 2 ? P : (P + 1) % 3;
+      A[rr] = dot4((i & 1) ? r.p[q][s].y : r.p[q][s].x, c, A[rr]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void fir_q7_kernel(const int8_t* __restrict__ coeffs, int T,
+                                                        const int8_t* __restrict__ src, int8_t* __restrict__ dst,
+                                                        uint32_t B, const int8_t* __restrict__ hist_in,
+                                                        uint32_t nchunks) {
+  __shared__ uint32_t wq[kQ7W + 4];                 // aligned window words
+  __shared__ uint2 planes2[2 * kQ7W];              // 4 planes x kQ7W words
+  __shared__ uint2 cq2[kFirMaxTaps / 8 + 2];       // tap quads as words, zero past numTaps
+  uint32_t* lds = reinterpret_cast<uint32_t*>(planes2);
+  uint32_t* cq = reinterpret_cast<uint32_t*>(cq2);
+  const int T1 = T - 1;
+  const int quads = (T + 3) >> 2;
+  const FirItem it = fir_item(blockIdx.x, nchunks, B, T1);
+  const int nw = kFirChunk / 4 + quads + 1;        // plane words any lane reads (<= kQ7W)
+  for (int i = threadIdx.x; i <= nw; i += kBlock) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) w |= (uint32_t)(uint8_t)fir_sample(hist_in, src, it, B, T1, 4 * i + b) << (8 * b);
+    wq[i] = w;
+  }
+  for (int m = threadIdx.x; m < 2 * ((quads + 1) >> 1); m += kBlock) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int k = 4 * m + b;
+      w |= k < T ? (uint32_t)(uint8_t)coeffs[k] << (8 * b) : 0u;
+    }
+    cq[m] = w;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nw; i += kBlock) {
+    const uint32_t a = wq[i], b = wq[i + 1];
+    lds[i] = a;
+    lds[kQ7W + i] = __builtin_amdgcn_alignbyte(b, a, 1);
+    lds[2 * kQ7W + i] = __builtin_amdgcn_alignbyte(b, a, 2);
+    lds[3 * kQ7W + i] = __builtin_amdgcn_alignbyte(b, a, 3);
+  }
+  __syncthreads();
+  const int base = threadIdx.x * kFirR;
+  if (base >= it.count) return;
+  const int wb = base >> 2;
+  int32_t A[kFirR];
+#pragma unroll
+  for (int r = 0; r < kFirR; ++r) A[r] = 0;
+  Q7Ring ring;
+  q7_fetch<0>(ring, lds, wb);
+  q7_fetch<1>(ring, lds, wb + 2);
+  int m = 0;
+  for (; m + 6 <= quads; m += 6) {
+    q7_block<0>(ring, lds, wb + m + 4, cq2[m / 2], A);
+    q7_block<1>(ring, lds, wb + m + 6, cq2[m / 2 + 1], A);
+    q7_block<2>(ring, lds, wb + m + 8, cq2[m / 2 + 2], A);
+  }
+  if (m + 2 <= quads) {
+    q7_block<0>(ring, lds, wb + m + 4, cq2[m / 2], A);
+    m += 2;
+    if (m + 2 <= quads) {
+      q7_block<1>(ring, lds, wb + m + 4, cq2[m / 2], A);
+      m += 2;
+    }
+  }
+  if (m < quads) {                                  // odd quad count: the last one from LDS
+    const uint32_t c = cq[m];
+#pragma unroll
+    for (int r = 0; r < kFirR; ++r) A[r] = dot4(lds[(r & 3) * kQ7W + wb + (r >> 2) + m], c, A[r]);
+  }
+  int8_t y[kFirR];
+#pragma unroll
+  for (int r = 0; r < kFirR; ++r) {
+    const int32_t v = A[r] >> 7;
+    y[r] = (int8_t)(v > 127 ? 127 : v < -128 ? -128 : v);                   // arm_fir_q7.c:530
+  }
+  int8_t* o = dst + (uint64_t)it.f * B + it.n0 + base;
+  if ((B & 7u) == 0 && ((uintptr_t)dst & 7u) == 0 && base + kFirR <= it.count) {
+    *reinterpret_cast<uint2*>(o) = *reinterpret_cast<const uint2*>(y);
+  } else {
+#pragma unroll
+    for (int r = 0; r < kFirR; ++r)
+      if (base + r < it.count) o[r] = y[r];
+  }
+}
+
 // new history = last T-1 samples of [hist ; src]  (arm_fir_f32.c:1242-1278)
 template <typename T>
 __global__ void fir_hist_kernel(const T* __restrict__ src, T* __restrict__ hist, const T* __restrict__ hist_in,
@@ -666,6 +780,11 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
                          (int16_t*)dst, B, (const int16_t*)hist_in, nchunks);
       break;
     }
+    case kFirQ7: {
+      hipLaunchKernelGGL(fir_q7_kernel, dim3(items), dim3(kBlock), 0, st, (const int8_t*)coeffs, T_,
+                         (const int8_t*)src, (int8_t*)dst, B, (const int8_t*)hist_in, nchunks);
+      break;
+    }
     default: {
       auto k = kind == kFirQ31 ? fir_q31_kernel<false> : fir_q31_kernel<true>;
       hipLaunchKernelGGL(k, dim3(items), dim3(kBlock), 0, st, (const int32_t*)coeffs, T_, (const int32_t*)src,
@@ -700,6 +819,9 @@ hipError_t fir_run(int kind, const void* coeffs, int num_taps, const void* src, 
     case kFirFastQ31:
       return fir_launch<int32_t>(kind, (const int32_t*)coeffs, num_taps, (const int32_t*)src, (int32_t*)dst,
                                  block_size, batch, (int32_t*)hist, st);
+    case kFirQ7:
+      return fir_launch<int8_t>(kind, (const int8_t*)coeffs, num_taps, (const int8_t*)src, (int8_t*)dst,
+                                block_size, batch, (int8_t*)hist, st);
     default:
       return hipErrorInvalidValue;
   }

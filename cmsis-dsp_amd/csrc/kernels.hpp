@@ -61,8 +61,8 @@ hipError_t rfft_q15_pass_launch(bool inverse, int n, const int16_t* src, int16_t
 
 // FIR: `batch` independent filters sharing one coefficient set, any of the five reference
 // variants (kind).  hist: [batch][numTaps-1] streaming state (read, then overwritten with
-// the new tail).  Element type: f32 float, q15/fast_q15 int16, q31/fast_q31 int32.
-enum FirKind { kFirF32 = 0, kFirQ15 = 1, kFirQ31 = 2, kFirFastQ15 = 3, kFirFastQ31 = 4 };
+// the new tail).  Element type: f32 float, q15/fast_q15 int16, q31/fast_q31 int32, q7 int8.
+enum FirKind { kFirF32 = 0, kFirQ15 = 1, kFirQ31 = 2, kFirFastQ15 = 3, kFirFastQ31 = 4, kFirQ7 = 5 };
 hipError_t fir_run(int kind, const void* coeffs, int num_taps, const void* src, void* dst, uint32_t block_size,
                    uint32_t batch, void* hist, hipStream_t st);
 
@@ -92,7 +92,7 @@ hipError_t mat_mult_f32_launch(int m, int k, int n, const float* a, const float*
 //   (corr: correlation), for n in [first, first + num), stored at
 //   y[item * sy + yoff + ydir * n].  x / h item strides sx / sh (0 = shared).
 // kConvFastQ15 requires A >= B (the reference's x is the longer input).
-enum ConvOp { kConvF32 = 0, kConvQ15 = 1, kConvQ31 = 2, kConvFastQ15 = 3, kConvFastQ31 = 4 };
+enum ConvOp { kConvF32 = 0, kConvQ15 = 1, kConvQ31 = 2, kConvFastQ15 = 3, kConvFastQ31 = 4, kConvQ7 = 5 };
 struct ConvJob {
   int op;
   bool corr;

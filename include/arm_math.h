@@ -110,7 +110,13 @@ typedef struct {
   arm_rfft_fast_instance_f32 rfft;
 } arm_mfcc_instance_f32;
 
-/* ---- FIR instances: Include/dsp/filtering_functions.h:66-71, 76-81, 86-91 -------- */
+/* ---- FIR instances: Include/dsp/filtering_functions.h:56-61 (q7), 66-71, 76-81, 86-91 */
+typedef struct {
+        uint16_t   numTaps;
+        q7_t      *pState;
+  const q7_t      *pCoeffs;
+} arm_fir_instance_q7;
+
 typedef struct {
         uint16_t   numTaps;
         q15_t     *pState;
@@ -129,8 +135,14 @@ typedef struct {
   const float32_t *pCoeffs;
 } arm_fir_instance_f32;
 
-/* ---- matrix instances: Include/dsp/matrix_functions.h:118-123 (f32), :139-144 (q15),
- * :149-154 (q31) */
+/* ---- matrix instances: Include/dsp/matrix_functions.h:118-123 (f32), :139-143 (q7),
+ * :139-144 (q15), :149-154 (q31) */
+typedef struct {
+  uint16_t   numRows;
+  uint16_t   numCols;
+  q7_t      *pData;
+} arm_matrix_instance_q7;
+
 typedef struct {
   uint16_t   numRows;
   uint16_t   numCols;
@@ -328,6 +340,13 @@ void arm_fir_fast_q31(const arm_fir_instance_q31 *S, const q31_t *pSrc,
                       q31_t *pDst, uint32_t blockSize);
 void arm_fir_fast_q15(const arm_fir_instance_q15 *S, const q15_t *pSrc,
                       q15_t *pDst, uint32_t blockSize);
+/* q7 FIR.  Prototypes: Include/dsp/filtering_functions.h:110-114 (arm_fir_q7), :127-132
+ * (arm_fir_init_q7).  Reference bodies: Source/FilteringFunctions/arm_fir_q7.c:446-560 (q31_t
+ * accumulator of q7 x q7 products, wrapping int32 adds, __SSAT(acc >> 7, 8)),
+ * arm_fir_init_q7.c:67-85 (state numTaps + blockSize - 1 words, zeroed). */
+void arm_fir_init_q7(arm_fir_instance_q7 *S, uint16_t numTaps, const q7_t *pCoeffs, q7_t *pState,
+                     uint32_t blockSize);
+void arm_fir_q7(const arm_fir_instance_q7 *S, const q7_t *pSrc, q7_t *pDst, uint32_t blockSize);
 
 /* ===================================================================================
  * Convolution.  Prototypes: Include/dsp/filtering_functions.h
@@ -380,6 +399,16 @@ void arm_correlate_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB,
 void arm_correlate_q31(const q31_t *pSrcA, uint32_t srcALen, const q31_t *pSrcB, uint32_t srcBLen, q31_t *pDst);
 void arm_correlate_fast_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB, uint32_t srcBLen, q15_t *pDst);
 void arm_correlate_fast_q31(const q31_t *pSrcA, uint32_t srcALen, const q31_t *pSrcB, uint32_t srcBLen, q31_t *pDst);
+
+/* q7 convolution family.  Prototypes: Include/dsp/filtering_functions.h:591-596
+ * (arm_conv_q7), :790-797 (arm_conv_partial_q7), :2025-2030 (arm_correlate_q7).  Reference
+ * bodies: Source/FilteringFunctions/arm_conv_q7.c, arm_conv_partial_q7.c (!ARM_MATH_DSP,
+ * :688-735), arm_correlate_q7.c: q31_t sum of q7 x q7 products (int32 adds and __SMLAD pairs,
+ * both wrapping: a modular sum), __SSAT(sum >> 7, 8).  Output placement as the q15 forms. */
+void arm_conv_q7(const q7_t *pSrcA, uint32_t srcALen, const q7_t *pSrcB, uint32_t srcBLen, q7_t *pDst);
+arm_status arm_conv_partial_q7(const q7_t *pSrcA, uint32_t srcALen, const q7_t *pSrcB, uint32_t srcBLen,
+                               q7_t *pDst, uint32_t firstIndex, uint32_t numPoints);
+void arm_correlate_q7(const q7_t *pSrcA, uint32_t srcALen, const q7_t *pSrcB, uint32_t srcBLen, q7_t *pDst);
 
 /* ===================================================================================
  * Matrix multiply, f32.  Prototypes: Include/dsp/matrix_functions.h:341-344,630-634

@@ -77,6 +77,8 @@ arm_status arm_fir_q31_batch(const arm_fir_instance_q31 *S, const q31_t *d_src, 
                              uint32_t blockSize, uint32_t batch, q31_t *d_hist, void *stream);
 arm_status arm_fir_fast_q31_batch(const arm_fir_instance_q31 *S, const q31_t *d_src, q31_t *d_dst,
                                   uint32_t blockSize, uint32_t batch, q31_t *d_hist, void *stream);
+arm_status arm_fir_q7_batch(const arm_fir_instance_q7 *S, const q7_t *d_src, q7_t *d_dst,
+                            uint32_t blockSize, uint32_t batch, q7_t *d_hist, void *stream);
 
 /* Convolution of `batch` pairs: item i convolves d_a + i*strideA (srcALen samples) with
  * d_b + i*strideB (srcBLen samples; strideB = 0 shares one kernel) into
@@ -91,6 +93,8 @@ arm_status arm_conv_fast_q15_batch(const q15_t *d_a, uint32_t srcALen, uint32_t 
                                    uint32_t srcBLen, uint32_t strideB, q15_t *d_dst, uint32_t batch, void *stream);
 arm_status arm_conv_fast_q31_batch(const q31_t *d_a, uint32_t srcALen, uint32_t strideA, const q31_t *d_b,
                                    uint32_t srcBLen, uint32_t strideB, q31_t *d_dst, uint32_t batch, void *stream);
+arm_status arm_conv_q7_batch(const q7_t *d_a, uint32_t srcALen, uint32_t strideA, const q7_t *d_b,
+                             uint32_t srcBLen, uint32_t strideB, q7_t *d_dst, uint32_t batch, void *stream);
 
 /* Partial convolution of `batch` pairs (strides as arm_conv_*_batch): item i's numPoints
  * outputs firstIndex .. firstIndex + numPoints - 1 go COMPACTLY to d_dst + i*numPoints.
@@ -110,6 +114,9 @@ arm_status arm_conv_partial_fast_q15_batch(const q15_t *d_a, uint32_t srcALen, u
 arm_status arm_conv_partial_fast_q31_batch(const q31_t *d_a, uint32_t srcALen, uint32_t strideA, const q31_t *d_b,
                                            uint32_t srcBLen, uint32_t strideB, q31_t *d_dst, uint32_t firstIndex,
                                            uint32_t numPoints, uint32_t batch, void *stream);
+arm_status arm_conv_partial_q7_batch(const q7_t *d_a, uint32_t srcALen, uint32_t strideA, const q7_t *d_b,
+                                     uint32_t srcBLen, uint32_t strideB, q7_t *d_dst, uint32_t firstIndex,
+                                     uint32_t numPoints, uint32_t batch, void *stream);
 
 /* Correlation of `batch` pairs: item i writes d_dst + i*(2*max(srcALen, srcBLen) - 1) at the
  * positions arm_correlate_* writes (the others are left untouched). */
@@ -126,6 +133,8 @@ arm_status arm_correlate_fast_q15_batch(const q15_t *d_a, uint32_t srcALen, uint
 arm_status arm_correlate_fast_q31_batch(const q31_t *d_a, uint32_t srcALen, uint32_t strideA, const q31_t *d_b,
                                         uint32_t srcBLen, uint32_t strideB, q31_t *d_dst, uint32_t batch,
                                         void *stream);
+arm_status arm_correlate_q7_batch(const q7_t *d_a, uint32_t srcALen, uint32_t strideA, const q7_t *d_b,
+                                  uint32_t srcBLen, uint32_t strideB, q7_t *d_dst, uint32_t batch, void *stream);
 
 /* Row-major C[b] = A[b] * B[b] for `batch` contiguous (numRows x numCols) matrices with
  * the shapes of the three instances (their pData must be device pointers to the first

@@ -16,6 +16,9 @@ arm_status oracle_arm_rfft_init_q15(arm_rfft_instance_q15 *S, uint32_t n, uint32
 void oracle_arm_fir_f32(const arm_fir_instance_f32 *S, const float *pSrc, float *pDst, uint32_t blockSize);
 void oracle_arm_fir_q15(const arm_fir_instance_q15 *S, const int16_t *pSrc, int16_t *pDst, uint32_t blockSize);
 void oracle_arm_fir_fast_q15(const arm_fir_instance_q15 *S, const int16_t *pSrc, int16_t *pDst, uint32_t blockSize);
+void oracle_arm_fir_q7(const arm_fir_instance_q7 *S, const int8_t *pSrc, int8_t *pDst, uint32_t blockSize);
+void oracle_arm_fir_init_q7(arm_fir_instance_q7 *S, uint16_t numTaps, const int8_t *pCoeffs, int8_t *pState,
+                            uint32_t blockSize);
 void oracle_arm_fir_q31(const arm_fir_instance_q31 *S, const int32_t *pSrc, int32_t *pDst, uint32_t blockSize);
 void oracle_arm_fir_fast_q31(const arm_fir_instance_q31 *S, const int32_t *pSrc, int32_t *pDst, uint32_t blockSize);
 arm_status oracle_arm_mat_mult_f32(const arm_matrix_instance_f32 *A, const arm_matrix_instance_f32 *B,

@@ -16,6 +16,8 @@
  *       stage 2: none (pairs, or plain q31 sums in the remainder loops);
  *       stage 3: corr: the last count % 4 (:558-607); conv: the last count % 4 for the
  *       first (B-1)/4 outputs (:569-622), then every MAC (:629-656).
+ *   arm_conv_q7.c, arm_conv_partial_q7.c (!ARM_MATH_DSP :688-735), arm_correlate_q7.c: q31_t
+ *     sum of q7 x q7 products (int32 adds / __SMLAD pairs, wrapping), __SSAT(sum >> 7, 8).
  *   arm_conv_fast_q31.c / arm_correlate_fast_q31.c: sum = (q31)(((q63)sum << 32 + x*y) >> 32)
  *     per MAC (= sum + ((x*y) >> 32) mod 2^32), output sum << 1.
  * Pinned against oracle/_ref by tests/test_oracle.py::test_conv_family_oracle_equals_reference. */
@@ -24,7 +26,7 @@
 
 #include "oracle.h"
 
-enum { OP_F32, OP_Q15, OP_Q31, OP_FQ15, OP_FQ31 };
+enum { OP_F32, OP_Q15, OP_Q31, OP_FQ15, OP_FQ31, OP_Q7 };
 
 static int16_t sat16(int32_t v) { return (int16_t)(v > 32767 ? 32767 : v < -32768 ? -32768 : v); }
 
@@ -50,6 +52,12 @@ static void engine(int op, int corr, const void *xv, uint32_t A, const void *yv,
       uint64_t s = 0;
       for (uint32_t k = k0; k <= k1; ++k) s += (uint64_t)((int64_t)x[k] * G(int32_t));
       ((int32_t *)out)[pos] = (int32_t)((int64_t)s >> 31);
+    } else if (op == OP_Q7) {
+      const int8_t *x = xv;
+      uint32_t s = 0;
+      for (uint32_t k = k0; k <= k1; ++k) s += (uint32_t)((int32_t)x[k] * G(int8_t));
+      const int32_t v = (int32_t)s >> 7;
+      ((int8_t *)out)[pos] = (int8_t)(v > 127 ? 127 : v < -128 ? -128 : v);
     } else if (op == OP_FQ31) {
       const int32_t *x = xv;
       uint32_t s = 0;
@@ -107,3 +115,7 @@ arm_status oracle_arm_conv_partial_q15(const int16_t *a, uint32_t A, const int16
                                        uint32_t f, uint32_t n) { return partial(OP_Q15, a, A, b, B, d, f, n); }
 arm_status oracle_arm_conv_partial_q31(const int32_t *a, uint32_t A, const int32_t *b, uint32_t B, int32_t *d,
                                        uint32_t f, uint32_t n) { return partial(OP_Q31, a, A, b, B, d, f, n); }
+void oracle_arm_conv_q7(const int8_t *a, uint32_t A, const int8_t *b, uint32_t B, int8_t *d) { conv_fast(OP_Q7, a, A, b, B, d); }
+void oracle_arm_correlate_q7(const int8_t *a, uint32_t A, const int8_t *b, uint32_t B, int8_t *d) { correlate(OP_Q7, a, A, b, B, d); }
+arm_status oracle_arm_conv_partial_q7(const int8_t *a, uint32_t A, const int8_t *b, uint32_t B, int8_t *d,
+                                      uint32_t f, uint32_t n) { return partial(OP_Q7, a, A, b, B, d, f, n); }

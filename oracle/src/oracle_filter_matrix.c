@@ -70,6 +70,22 @@ void oracle_arm_fir_fast_q15(const arm_fir_instance_q15 *S, const int16_t *pSrc,
   memmove(s, s + blockSize, sizeof(int16_t) * (taps - 1));
 }
 
+/* arm_fir_q7.c:446-560 (LOOPUNROLL and tail alike): q31_t accumulator of q7 x q7 products,
+ * plain int32 adds (wrapping), y = __SSAT(acc >> 7, 8). */
+void oracle_arm_fir_q7(const arm_fir_instance_q7 *S, const int8_t *pSrc, int8_t *pDst, uint32_t blockSize) {
+  const uint32_t taps = S->numTaps;
+  int8_t *s = S->pState;
+  const int8_t *c = S->pCoeffs;
+  memcpy(s + taps - 1, pSrc, blockSize);
+  for (uint32_t n = 0; n < blockSize; ++n) {
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < taps; ++k) acc += (uint32_t)((int32_t)s[n + k] * c[k]);
+    const int32_t v = (int32_t)acc >> 7;
+    pDst[n] = (int8_t)(v > 127 ? 127 : v < -128 ? -128 : v);
+  }
+  memmove(s, s + blockSize, taps - 1);
+}
+
 /* arm_fir_q31.c: q63 accumulator of exact products (wrapping, as gcc x86-64 adds do),
  * y = (q31)(acc >> 31). */
 void oracle_arm_fir_q31(const arm_fir_instance_q31 *S, const int32_t *pSrc, int32_t *pDst, uint32_t blockSize) {

@@ -20,7 +20,7 @@ REF_SO = os.path.join(ROOT, "oracle", "_ref", "libcmsisdsp_ref.so")
 ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
 
 _INST = {"f32": _abi.arm_cfft_instance_f32, "q31": _abi.arm_cfft_instance_q31, "q15": _abi.arm_cfft_instance_q15}
-DTYPE = {"f32": np.float32, "q31": np.int32, "q15": np.int16}
+DTYPE = {"f32": np.float32, "q31": np.int32, "q15": np.int16, "q7": np.int8}
 
 
 class Host:
@@ -97,10 +97,10 @@ class Host:
     def fir(self, kind, coeffs, blocks):
         """Stream `blocks` (list of 1-D arrays, each <= the block size) through one filter;
         returns (outputs, final state buffer).  kind: f32, q15, q31, fast_q15, fast_q31."""
-        base = kind[-3:]
-        dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32}[base]
+        base = kind.split("_")[-1]
+        dt = DTYPE[base]
         inst = {"f32": _abi.arm_fir_instance_f32, "q15": _abi.arm_fir_instance_q15,
-                "q31": _abi.arm_fir_instance_q31}[base]()
+                "q31": _abi.arm_fir_instance_q31, "q7": _abi.arm_fir_instance_q7}[base]()
         c = np.ascontiguousarray(coeffs, dtype=dt)
         bs = max(len(b) for b in blocks)
         state = np.zeros(len(c) + bs - 1, dtype=dt)
@@ -115,7 +115,7 @@ class Host:
         return outs, state.copy()
 
     def conv(self, kind, a, b):
-        dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32}[kind]
+        dt = DTYPE[kind]
         a = np.ascontiguousarray(a, dtype=dt)
         b = np.ascontiguousarray(b, dtype=dt)
         y = np.zeros(len(a) + len(b) - 1, dtype=dt)
@@ -125,7 +125,7 @@ class Host:
     def conv_family(self, fn, a, b, first=0, num=0, fill=0):
         """arm_<fn> for fn in _abi.CONV_FULL + CONV_PARTIAL on one pair: returns (pDst, status)
         with pDst pre-filled with `fill` (partial / correlate leave words untouched)."""
-        dt = DTYPE[fn[-3:]]
+        dt = DTYPE[fn.split("_")[-1]]
         a = np.ascontiguousarray(a, dtype=dt)
         b = np.ascontiguousarray(b, dtype=dt)
         n = 2 * max(len(a), len(b)) - 1 if fn.startswith("correlate") else len(a) + len(b) - 1

@@ -17,7 +17,7 @@ from cmsisdsp_amd import _abi
 FULL = list(_abi.CONV_FULL)
 PARTIAL = list(_abi.CONV_PARTIAL)
 PARTIAL_FAST = list(_abi.CONV_PARTIAL_FAST)
-DT = {"f32": np.float32, "q15": np.int16, "q31": np.int32}
+DT = {"f32": np.float32, "q15": np.int16, "q31": np.int32, "q7": np.int8}
 SMALL = [(a, b) for a in (1, 2, 3, 4, 5, 7, 8, 9, 13, 16, 17, 33) for b in (1, 2, 3, 4, 5, 6, 7, 9, 12, 13, 17, 33)]
 
 
@@ -51,7 +51,7 @@ def partial_ranges(la, lb):
 # ------------------------------------------------------------------ CPU: oracle == reference
 @pytest.mark.parametrize("fn", FULL)
 def test_conv_family_oracle_equals_reference(oracle, ref, fn):
-    kind = fn[-3:]
+    kind = fn.split("_")[-1]
     rng = np.random.default_rng(len(fn))
     for la, lb in SMALL + [(200, 129), (129, 200), (1000, 64)]:
         for dist in dists(kind):
@@ -62,7 +62,7 @@ def test_conv_family_oracle_equals_reference(oracle, ref, fn):
 
 @pytest.mark.parametrize("fn", PARTIAL)
 def test_conv_partial_oracle_equals_reference(oracle, ref, fn):
-    kind = fn[-3:]
+    kind = fn.split("_")[-1]
     rng = np.random.default_rng(3)
     for la, lb in [(1, 1), (5, 3), (3, 5), (17, 9), (9, 17), (40, 40), (100, 7)]:
         for dist in dists(kind):
@@ -97,7 +97,7 @@ GPU_PAIRS = [(1, 1), (5, 3), (3, 5), (7, 100), (100, 7), (4100, 129), (129, 4100
 def test_conv_family_dropin_bitexact(dsp, torch_gpu, ref, fn):
     """Drop-in calls (host buffers), both length orders, the windowed kernel (srcBLen <= 1024)
     and the direct kernel beyond it; untouched correlate words keep the caller's fill."""
-    kind = fn[-3:]
+    kind = fn.split("_")[-1]
     rng = np.random.default_rng(11)
     for la, lb in GPU_PAIRS:
         for dist in dists(kind)[:3]:
@@ -110,7 +110,7 @@ def test_conv_family_dropin_bitexact(dsp, torch_gpu, ref, fn):
 @pytest.mark.gpu
 @pytest.mark.parametrize("fn", PARTIAL)
 def test_conv_partial_dropin_bitexact(dsp, torch_gpu, ref, fn):
-    kind = fn[-3:]
+    kind = fn.split("_")[-1]
     rng = np.random.default_rng(12)
     for la, lb in [(5, 3), (3, 5), (300, 40), (40, 300), (5000, 129), (1500, 1100)]:
         a, b = gen(kind, la, rng, "full" if kind != "f32" else "small"), gen(kind, lb, rng, "small")
@@ -128,12 +128,12 @@ def test_conv_partial_dropin_bitexact(dsp, torch_gpu, ref, fn):
 @pytest.mark.parametrize("la,lb", [(3000, 77), (77, 3000), (2048, 1300)])
 def test_conv_family_batch(dsp, torch_gpu, ref, fn, la, lb):
     """Batched device API: per-item operands and a shared pSrcB; partial outputs compact."""
-    kind = fn[-3:]
+    kind = fn.split("_")[-1]
     batch = 5
     rng = np.random.default_rng(la + lb)
     A = np.stack([gen(kind, la, rng, "full" if kind != "f32" else "small") for _ in range(batch)])
     B = np.stack([gen(kind, lb, rng, "neg" if kind == "q15" else "small") for _ in range(batch)])
-    tdt = {"f32": torch_gpu.float32, "q15": torch_gpu.int16, "q31": torch_gpu.int32}[kind]
+    tdt = {"f32": torch_gpu.float32, "q15": torch_gpu.int16, "q31": torch_gpu.int32, "q7": torch_gpu.int8}[kind]
     L = la + lb - 1
     first, num = (lb // 2, L - lb) if fn in PARTIAL else (0, 0)
     width = num if fn in PARTIAL else (2 * max(la, lb) - 1 if fn.startswith("correlate") else L)
@@ -156,7 +156,7 @@ def test_conv_partial_fast(dsp, torch_gpu, ref, fn):
     """arm_conv_partial_fast_*: the words of arm_conv_fast_* over the range (the reference's
     own partial-fast bodies read outside the inputs for most ranges on the host build, so
     parity is pinned to the reference's arm_conv_fast_*), drop-in and batched."""
-    kind = fn[-3:]
+    kind = fn.split("_")[-1]
     full = fn.replace("partial_", "")
     rng = np.random.default_rng(13)
     for la, lb in [(5, 3), (3, 5), (300, 40), (40, 300), (5000, 129), (1500, 1100)]:

@@ -47,11 +47,12 @@ def test_rfft_dropin(dsp, torch_gpu, ref, n):
 def _fir_batched(dsp, torch, kind, coeffs, blocks_per_filter):
     """blocks_per_filter: [batch][calls] arrays; runs the batched API call by call."""
     import ctypes as C
-    base = kind[-3:]
-    dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32}[base]
+    base = kind.split("_")[-1]
+    dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32, "q7": np.int8}[base]
     batch, calls = len(blocks_per_filter), len(blocks_per_filter[0])
     c = np.ascontiguousarray(coeffs, dtype=dt)
-    S = {"f32": dsp.arm_fir_instance_f32, "q15": dsp.arm_fir_instance_q15, "q31": dsp.arm_fir_instance_q31}[base]()
+    S = {"f32": dsp.arm_fir_instance_f32, "q15": dsp.arm_fir_instance_q15, "q31": dsp.arm_fir_instance_q31,
+         "q7": dsp.arm_fir_instance_q7}[base]()
     S.numTaps = len(c)
     dc = torch.from_numpy(c.copy()).cuda()
     S.pCoeffs = C.cast(dc.data_ptr(), S._fields_[2][1])
@@ -66,7 +67,7 @@ def _fir_batched(dsp, torch, kind, coeffs, blocks_per_filter):
     return outs, hist.cpu().numpy()
 
 
-FIR_KINDS = ["f32", "q15", "q31", "fast_q15", "fast_q31"]
+FIR_KINDS = ["f32", "q15", "q31", "fast_q15", "fast_q31", "q7"]
 
 
 @pytest.mark.parametrize("kind", FIR_KINDS)
@@ -83,7 +84,7 @@ def test_fir_batch_bitexact_two_calls(dsp, torch_gpu, ref, kind, taps, block):
         coeffs = (rng.standard_normal(taps) / np.sqrt(taps)).astype(np.float32)
         blocks = [[rng.uniform(-1, 1, block).astype(np.float32) for _ in range(2)] for _ in range(batch)]
     else:
-        bits, dt = (15, np.int16) if kind.endswith("q15") else (31, np.int32)
+        bits, dt = {"q15": (15, np.int16), "q31": (31, np.int32), "q7": (7, np.int8)}[kind.split("_")[-1]]
         lo, hi = -(1 << bits), (1 << bits) - 1
         coeffs = rng.integers(lo, hi, taps, endpoint=True).astype(dt)
         blocks = [[rng.integers(lo, hi, block, endpoint=True).astype(dt) for _ in range(2)]

@@ -49,14 +49,13 @@ def fir_case(kind, taps, blocks, seed):
     if kind == "f32":
         return (rng.standard_normal(taps).astype(np.float32),
                 [rng.uniform(-1, 1, b).astype(np.float32) for b in blocks])
-    bits = 15 if kind.endswith("q15") else 31
-    dt = np.int16 if bits == 15 else np.int32
+    bits, dt = {"q15": (15, np.int16), "q31": (31, np.int32), "q7": (7, np.int8)}[kind.split("_")[-1]]
     lo, hi = -(1 << bits), (1 << bits) - 1
     return (rng.integers(lo, hi, taps, endpoint=True).astype(dt),
             [rng.integers(lo, hi, b, endpoint=True).astype(dt) for b in blocks])
 
 
-FIR_KINDS = ["f32", "q15", "q31", "fast_q15", "fast_q31"]
+FIR_KINDS = ["f32", "q15", "q31", "fast_q15", "fast_q31", "q7"]
 
 
 @pytest.mark.parametrize("kind", FIR_KINDS)
@@ -80,12 +79,14 @@ def test_fir_q15_all_min_wraps_like_reference(oracle, ref):
     assert len(np.unique(ya[0])) > 1      # the grouped outputs wrap, the tail does not
 
 
-@pytest.mark.parametrize("kind,word", [("q31", -(1 << 31)), ("fast_q31", -(1 << 31)), ("fast_q15", -32768),
-                                       ("q31", (1 << 31) - 1), ("fast_q31", (1 << 31) - 1)])
-def test_fir_extreme_words_wrap_like_reference(oracle, ref, kind, word):
-    """All-extreme samples and taps: the q63 / q31 accumulators wrap (gcc x86-64 adds)."""
-    dt = np.int16 if kind.endswith("q15") else np.int32
-    c = np.full(6, word, dtype=dt)
+@pytest.mark.parametrize("kind,word,taps", [("q31", -(1 << 31), 6), ("fast_q31", -(1 << 31), 6),
+                                            ("fast_q15", -32768, 6), ("q31", (1 << 31) - 1, 6),
+                                            ("fast_q31", (1 << 31) - 1, 6), ("q7", -128, 6), ("q7", -128, 1000)])
+def test_fir_extreme_words_wrap_like_reference(oracle, ref, kind, word, taps):
+    """All-extreme samples and taps: the q63 / q31 accumulators wrap (gcc x86-64 adds); q7 at
+    1000 taps saturates (16384 * 1000 >> 7 > 127)."""
+    dt = {"q15": np.int16, "q31": np.int32, "q7": np.int8}[kind.split("_")[-1]]
+    c = np.full(taps, word, dtype=dt)
     x = [np.full(37, word, dtype=dt)]
     (ya, _), (yb, _) = oracle.fir(kind, c, x), ref.fir(kind, c, x)
     assert ya[0].tobytes() == yb[0].tobytes()
@@ -116,7 +117,7 @@ def test_mat_mult_fixed_oracle_equals_reference(oracle, ref, kind, m, k, n, fill
     assert sa == sb == 0 and ca.tobytes() == cb.tobytes()
 
 
-@pytest.mark.parametrize("kind", ["f32", "q15", "q31"])
+@pytest.mark.parametrize("kind", ["f32", "q15", "q31", "q7"])
 @pytest.mark.parametrize("la,lb", [(1, 1), (5, 3), (3, 5), (64, 64), (100, 7), (7, 100), (1000, 129), (129, 1000),
                                    (33, 1), (1, 33), (10, 37), (65, 64)])
 def test_conv_oracle_equals_reference(oracle, ref, kind, la, lb):
