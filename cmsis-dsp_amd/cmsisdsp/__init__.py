@@ -53,11 +53,18 @@ arm_rfft_fast_instance_f32 = _make("arm_rfft_fast_instance_f32", _abi.arm_rfft_f
 arm_fir_instance_f32 = _make("arm_fir_instance_f32", _abi.arm_fir_instance_f32)
 arm_fir_instance_q31 = _make("arm_fir_instance_q31", _abi.arm_fir_instance_q31)
 arm_fir_instance_q15 = _make("arm_fir_instance_q15", _abi.arm_fir_instance_q15)
+arm_fir_instance_q7 = _make("arm_fir_instance_q7", _abi.arm_fir_instance_q7)
 arm_mfcc_instance_f32 = _make("arm_mfcc_instance_f32", _abi.arm_mfcc_instance_f32)
+for _t in ("f32", "q31", "q15"):
+    globals()[f"arm_fir_decimate_instance_{_t}"] = _make(f"arm_fir_decimate_instance_{_t}",
+                                                         _abi.arm_fir_decimate_instance)
+    globals()[f"arm_fir_interpolate_instance_{_t}"] = _make(f"arm_fir_interpolate_instance_{_t}",
+                                                            _abi.arm_fir_interpolate_instance)
+del _t
 arm_rfft_instance_q31 = _make("arm_rfft_instance_q31", _abi.arm_rfft_instance_q31)
 arm_rfft_instance_q15 = _make("arm_rfft_instance_q15", _abi.arm_rfft_instance_q15)
 
-_DT = {"f32": _np.float32, "q31": _np.int32, "q15": _np.int16}
+_DT = {"f32": _np.float32, "q31": _np.int32, "q15": _np.int16, "q7": _np.int8}
 
 
 def _arr(x, dt):
@@ -191,12 +198,57 @@ def _fir(name, kind):
     return run
 
 
-arm_fir_init_f32, arm_fir_init_q31, arm_fir_init_q15 = (_fir_init(k) for k in ("f32", "q31", "q15"))
+arm_fir_init_f32, arm_fir_init_q31, arm_fir_init_q15, arm_fir_init_q7 = (_fir_init(k) for k in ("f32", "q31", "q15", "q7"))
+arm_fir_q7 = _fir("arm_fir_q7", "q7")
 arm_fir_f32 = _fir("arm_fir_f32", "f32")
 arm_fir_q31 = _fir("arm_fir_q31", "q31")
 arm_fir_q15 = _fir("arm_fir_q15", "q15")
 arm_fir_fast_q31 = _fir("arm_fir_fast_q31", "q31")
 arm_fir_fast_q15 = _fir("arm_fir_fast_q15", "q15")
+
+
+# ------------------------------------------------------------------ multirate FIR
+# cmsisdsp_filtering.c cmsis_arm_fir_decimate_init_* ("OhiOO": blockSize = len(pState) -
+# len(pCoeffs) + 1, :4742-4772) / cmsis_arm_fir_interpolate_init_* ("OihOO", same blockSize
+# rule, :5164-5190) return the status; cmsis_arm_fir_decimate_* returns len(pSrc) / M words,
+# cmsis_arm_fir_interpolate_* len(pSrc) * L words (:4706-4740, :5128-5160).
+def _mr_init(family, kind):
+    name = f"arm_fir_{family}_init_{kind}"
+
+    def init(inst, a, b, pCoeffs, pState):
+        c = _arr(pCoeffs, _DT[kind])
+        state = _arr(pState, _DT[kind]).copy()
+        block = len(state) - len(c) + 1
+        inst._keep = [c, state]
+        st = getattr(_lib, name)(_C.byref(inst._s), int(a), int(b), c.ctypes.data, state.ctypes.data, block)
+        _check(name)
+        return st
+    init.__name__ = name
+    return init
+
+
+def _mr(family, fn, kind):
+    name = f"arm_fir_{fn}"
+
+    def run(inst, pSrc):
+        x = _arr(pSrc, _DT[kind])
+        n = len(x) // inst._s.M if family == "decimate" else len(x) * inst._s.L
+        y = _np.zeros(n, dtype=_DT[kind])
+        getattr(_lib, name)(_C.byref(inst._s), x.ctypes.data, y.ctypes.data, len(x))
+        _check(name)
+        return y
+    run.__name__ = name
+    return run
+
+
+for _k in ("f32", "q31", "q15"):
+    globals()[f"arm_fir_decimate_init_{_k}"] = _mr_init("decimate", _k)
+    globals()[f"arm_fir_interpolate_init_{_k}"] = _mr_init("interpolate", _k)
+    globals()[f"arm_fir_decimate_{_k}"] = _mr("decimate", f"decimate_{_k}", _k)
+    globals()[f"arm_fir_interpolate_{_k}"] = _mr("interpolate", f"interpolate_{_k}", _k)
+arm_fir_decimate_fast_q15 = _mr("decimate", "decimate_fast_q15", "q15")
+arm_fir_decimate_fast_q31 = _mr("decimate", "decimate_fast_q31", "q31")
+del _k
 
 
 # ------------------------------------------------------------------ matrix multiply
@@ -237,6 +289,7 @@ def _conv(kind, dt):
 arm_conv_f32 = _conv("f32", _np.float32)
 arm_conv_q15 = _conv("q15", _np.int16)
 arm_conv_q31 = _conv("q31", _np.int32)
+arm_conv_q7 = _conv("q7", _np.int8)
 
 
 # cmsisdsp_filtering.c cmsis_arm_conv_fast_* ("OiOi", srcALen + srcBLen - 1 words),
@@ -245,7 +298,7 @@ arm_conv_q31 = _conv("q31", _np.int32)
 # The binding's output buffer is uninitialised where the C function does not write; here
 # those words are zero.
 def _conv_family(fn):
-    dt = _DT[fn[-3:]]
+    dt = _DT[fn.split("_")[-1]]
 
     def run(pSrcA, srcALen, pSrcB, srcBLen, *partial):
         a = _arr(pSrcA, dt)[:int(srcALen)]
@@ -258,7 +311,7 @@ def _conv_family(fn):
 
 for _fn in ("conv_fast_q15", "conv_fast_q31", "correlate_f32", "correlate_q15", "correlate_q31", "correlate_fast_q15",
             "correlate_fast_q31", "conv_partial_f32", "conv_partial_q15", "conv_partial_q31", "conv_partial_fast_q15",
-            "conv_partial_fast_q31"):
+            "conv_partial_fast_q31", "correlate_q7", "conv_partial_q7"):
     globals()[f"arm_{_fn}"] = _conv_family(_fn)
 del _fn
 

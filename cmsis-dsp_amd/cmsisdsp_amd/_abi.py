@@ -14,6 +14,7 @@ c_u16p = C.POINTER(C.c_uint16)
 
 ARM_MATH_SUCCESS = 0
 ARM_MATH_ARGUMENT_ERROR = -1
+ARM_MATH_LENGTH_ERROR = -2
 ARM_MATH_SIZE_MISMATCH = -3
 
 
@@ -52,6 +53,16 @@ class arm_fir_instance_f32(C.Structure):
 
 class arm_fir_instance_q7(C.Structure):
     _fields_ = [("numTaps", C.c_uint16), ("pState", C.c_void_p), ("pCoeffs", C.c_void_p)]
+
+
+# arm_fir_decimate_instance_{f32,q15,q31} / arm_fir_interpolate_instance_{f32,q15,q31}: one
+# layout per family (the element type only changes the pointees)
+class arm_fir_decimate_instance(C.Structure):
+    _fields_ = [("M", C.c_uint8), ("numTaps", C.c_uint16), ("pCoeffs", C.c_void_p), ("pState", C.c_void_p)]
+
+
+class arm_fir_interpolate_instance(C.Structure):
+    _fields_ = [("L", C.c_uint8), ("phaseLength", C.c_uint16), ("pCoeffs", C.c_void_p), ("pState", C.c_void_p)]
 
 
 class arm_fir_instance_q15(C.Structure):
@@ -121,6 +132,14 @@ DROPIN = {
     "arm_fir_q31": (None, [P(arm_fir_instance_q31), C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_fir_fast_q31": (None, [P(arm_fir_instance_q31), C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_fir_init_q7": (None, [P(arm_fir_instance_q7), C.c_uint16, C.c_void_p, C.c_void_p, C.c_uint32]),
+    **{f"arm_fir_decimate_init_{t}": (C.c_int, [P(arm_fir_decimate_instance), C.c_uint16, C.c_uint8, C.c_void_p,
+                                                C.c_void_p, C.c_uint32]) for t in ("f32", "q15", "q31")},
+    **{f"arm_fir_interpolate_init_{t}": (C.c_int, [P(arm_fir_interpolate_instance), C.c_uint8, C.c_uint16,
+                                                   C.c_void_p, C.c_void_p, C.c_uint32]) for t in ("f32", "q15", "q31")},
+    **{f"arm_fir_{k}": (None, [P(arm_fir_decimate_instance), C.c_void_p, C.c_void_p, C.c_uint32])
+       for k in ("decimate_f32", "decimate_q15", "decimate_fast_q15", "decimate_q31", "decimate_fast_q31")},
+    **{f"arm_fir_{k}": (None, [P(arm_fir_interpolate_instance), C.c_void_p, C.c_void_p, C.c_uint32])
+       for k in ("interpolate_f32", "interpolate_q15", "interpolate_q31")},
     "arm_fir_q7": (None, [P(arm_fir_instance_q7), C.c_void_p, C.c_void_p, C.c_uint32]),
     "arm_mat_init_f32": (None, [P(arm_matrix_instance_f32), C.c_uint16, C.c_uint16, C.c_void_p]),
     "arm_mat_init_q15": (None, [P(arm_matrix_instance_q15), C.c_uint16, C.c_uint16, C.c_void_p]),
@@ -193,6 +212,12 @@ BATCHED = {
                                          C.c_void_p, C.c_void_p]),
     "arm_fir_q7_batch": (C.c_int, [P(arm_fir_instance_q7), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                    C.c_void_p, C.c_void_p]),
+    **{f"arm_fir_{k}_batch": (C.c_int, [P(arm_fir_decimate_instance), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                        C.c_void_p, C.c_void_p])
+       for k in ("decimate_f32", "decimate_q15", "decimate_fast_q15", "decimate_q31", "decimate_fast_q31")},
+    **{f"arm_fir_{k}_batch": (C.c_int, [P(arm_fir_interpolate_instance), C.c_void_p, C.c_void_p, C.c_uint32,
+                                        C.c_uint32, C.c_void_p, C.c_void_p])
+       for k in ("interpolate_f32", "interpolate_q15", "interpolate_q31")},
     "arm_mat_mult_f32_batch": (C.c_int, [P(arm_matrix_instance_f32), P(arm_matrix_instance_f32),
                                          P(arm_matrix_instance_f32), C.c_uint32, C.c_void_p]),
     "arm_mat_mult_q15_batch": (C.c_int, [P(arm_matrix_instance_q15), P(arm_matrix_instance_q15),

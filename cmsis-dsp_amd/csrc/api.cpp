@@ -388,6 +388,113 @@ arm_status fir_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uint32
   return ARM_MATH_SUCCESS;
 }
 
+// zero a host or device buffer (the init functions' memset)
+void zero_words(void* p, size_t bytes, const char* what) {
+  if (is_device_ptr(p)) {
+    hipError_t e = hipMemset(p, 0, bytes);
+    if (e != hipSuccess) set_error(e, what);
+  } else {
+    memset(p, 0, bytes);
+  }
+}
+
+// ---- multirate FIR (decimator / interpolator) ----------------------------------------
+// Drop-in: state = [history (H) ; block (B)] on host or device; after the call it holds
+// [new history ; block input], as the reference leaves it (the block is copied into pState
+// before the pass, arm_fir_decimate_f32.c / arm_fir_interpolate_f32.c).  run(dc, src, dst,
+// hist, st) launches the batched pass for one stream.
+template <typename T, typename Run>
+void mr_sync(T* pState, const T* pCoeffs, int ncoef, int H, const T* pSrc, T* pDst, uint32_t B, size_t out_words,
+             const char* what, Run&& run) {
+  if (!pState || !pCoeffs || ncoef <= 0 || B == 0) return;
+  hipStream_t st = sync_stream();
+  bool ok = true;
+  const T* dc = device_coeffs<T>(pCoeffs, ncoef, &ok);
+  if (!ok) { set_error(hipErrorOutOfMemory, what); return; }
+  const bool dstate = is_device_ptr(pState), dsrc = is_device_ptr(pSrc), ddst = is_device_ptr(pDst);
+  const size_t sb = sizeof(T) * (size_t)B, hb = sizeof(T) * (size_t)H, ob = sizeof(T) * out_words;
+  const bool alias = dsrc && ddst && ranges_overlap(pSrc, pDst, sb > ob ? sb : ob);
+  T* dhist = dstate ? pState : (T*)scratch(hb + 16, 2);
+  const T* dsr = (dsrc && !alias) ? pSrc : (const T*)scratch(sb, 3);
+  T* dds = ddst ? pDst : (T*)scratch(ob + 16, 4);
+  if (!dhist || !dsr || !dds) { set_error(hipErrorOutOfMemory, what); return; }
+  HostIO io(st);
+  hipError_t e = hipSuccess;
+  if (!dstate && H > 0) e = io.in(dhist, pState, hb);
+  if (e == hipSuccess && alias) e = hipMemcpyAsync((void*)dsr, pSrc, sb, hipMemcpyDeviceToDevice, st);
+  else if (e == hipSuccess && !dsrc) e = io.in((void*)dsr, pSrc, sb);
+  if (e == hipSuccess) e = run(dc, dsr, dds, dhist, st);
+  if (e == hipSuccess && !ddst && ob) e = io.out(pDst, dds, ob);
+  if (e == hipSuccess && !dstate && H > 0) e = io.out(pState, dhist, hb);
+  if (e == hipSuccess) {
+    if (dstate) e = hipMemcpyAsync(pState + H, dsr, sb, hipMemcpyDeviceToDevice, st);
+    else if (dsrc) e = io.out(pState + H, dsr, sb);
+    else memcpy(pState + H, pSrc, sb);
+  }
+  if (e == hipSuccess) e = io.finish();
+  if (e != hipSuccess) set_error(e, what);
+}
+
+template <typename T, typename Inst>
+arm_status decimate_init(Inst* S, uint16_t numTaps, uint8_t M, const T* pCoeffs, T* pState, uint32_t blockSize) {
+  if (!S) return ARM_MATH_ARGUMENT_ERROR;
+  if (M == 0 || blockSize % M) return ARM_MATH_LENGTH_ERROR;       // arm_fir_decimate_init_f32.c
+  S->numTaps = numTaps; S->pCoeffs = pCoeffs; S->pState = pState; S->M = M;
+  if (pState) zero_words(pState, sizeof(T) * ((size_t)numTaps + blockSize - 1), "arm_fir_decimate_init");
+  return ARM_MATH_SUCCESS;
+}
+template <typename T, typename Inst>
+arm_status interpolate_init(Inst* S, uint8_t L, uint16_t numTaps, const T* pCoeffs, T* pState, uint32_t blockSize) {
+  if (!S) return ARM_MATH_ARGUMENT_ERROR;
+  if (L == 0 || numTaps % L) return ARM_MATH_LENGTH_ERROR;         // arm_fir_interpolate_init_f32.c
+  S->pCoeffs = pCoeffs; S->L = L; S->phaseLength = (uint16_t)(numTaps / L); S->pState = pState;
+  if (pState) zero_words(pState, sizeof(T) * ((size_t)blockSize + S->phaseLength - 1), "arm_fir_interpolate_init");
+  return ARM_MATH_SUCCESS;
+}
+template <typename T, typename Inst>
+void decimate_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B, int op, const char* what) {
+  if (!S || S->M == 0 || S->numTaps == 0) return;
+  const int M = S->M, taps = S->numTaps;
+  mr_sync<T>(S->pState, S->pCoeffs, taps, taps - 1, pSrc, pDst, B, B / M, what,
+             [&](const T* dc, const T* src, T* dst, T* hist, hipStream_t st) {
+               return fir_decimate_run(op, dc, taps, M, src, dst, B, 1, hist, st);
+             });
+}
+template <typename T, typename Inst>
+void interpolate_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B, int op, const char* what) {
+  if (!S || S->L == 0 || S->phaseLength == 0) return;
+  const int L = S->L, P = S->phaseLength;
+  mr_sync<T>(S->pState, S->pCoeffs, L * P, P - 1, pSrc, pDst, B, (size_t)B * L, what,
+             [&](const T* dc, const T* src, T* dst, T* hist, hipStream_t st) {
+               return fir_interpolate_run(op, dc, L, P, src, dst, B, 1, hist, st);
+             });
+}
+template <typename T, typename Inst>
+arm_status decimate_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uint32_t batch, T* d_hist,
+                          void* stream, int op, const char* what) {
+  if (!S || !S->pCoeffs || S->numTaps == 0 || S->M == 0) return ARM_MATH_ARGUMENT_ERROR;
+  if (batch && B && (!d_src || (B >= S->M && !d_dst) || (S->numTaps > 1 && !d_hist))) return ARM_MATH_ARGUMENT_ERROR;
+  bool ok = true;
+  const T* dc = device_coeffs<T>(S->pCoeffs, S->numTaps, &ok);
+  if (!ok) { set_error(hipErrorOutOfMemory, what); return ARM_MATH_ARGUMENT_ERROR; }
+  hipError_t e = fir_decimate_run(op, dc, S->numTaps, S->M, d_src, d_dst, B, batch, d_hist, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(e, what); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
+}
+template <typename T, typename Inst>
+arm_status interpolate_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uint32_t batch, T* d_hist,
+                             void* stream, int op, const char* what) {
+  if (!S || !S->pCoeffs || S->phaseLength == 0 || S->L == 0) return ARM_MATH_ARGUMENT_ERROR;
+  if (batch && B && (!d_src || !d_dst || (S->phaseLength > 1 && !d_hist))) return ARM_MATH_ARGUMENT_ERROR;
+  bool ok = true;
+  const T* dc = device_coeffs<T>(S->pCoeffs, (int)S->L * S->phaseLength, &ok);
+  if (!ok) { set_error(hipErrorOutOfMemory, what); return ARM_MATH_ARGUMENT_ERROR; }
+  hipError_t e = fir_interpolate_run(op, dc, S->L, S->phaseLength, d_src, d_dst, B, batch, d_hist,
+                                     (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(e, what); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
+}
+
 // ---- convolution / correlation family ------------------------------------------------
 // How each reference function maps onto one ConvJob (conv.hip):
 //   conv (exact):      x = pSrcA, h = pSrcB, all srcALen + srcBLen - 1 outputs forward;
@@ -853,5 +960,59 @@ MI355X_CONV_PARTIAL(arm_conv_partial_q7, q7_t, int8_t, kConvQ7)
 MI355X_CONV_PARTIAL(arm_conv_partial_fast_q15, q15_t, int16_t, kConvFastQ15)
 MI355X_CONV_PARTIAL(arm_conv_partial_fast_q31, q31_t, int32_t, kConvFastQ31)
 #undef MI355X_CONV_PARTIAL
+
+// ---- multirate FIR ---------------------------------------------------------------------
+arm_status arm_fir_decimate_init_f32(arm_fir_decimate_instance_f32* S, uint16_t numTaps, uint8_t M,
+                                     const float32_t* pCoeffs, float32_t* pState, uint32_t blockSize) {
+  return decimate_init<float>(S, numTaps, M, pCoeffs, pState, blockSize);
+}
+arm_status arm_fir_decimate_init_q15(arm_fir_decimate_instance_q15* S, uint16_t numTaps, uint8_t M,
+                                     const q15_t* pCoeffs, q15_t* pState, uint32_t blockSize) {
+  return decimate_init<int16_t>(S, numTaps, M, pCoeffs, pState, blockSize);
+}
+arm_status arm_fir_decimate_init_q31(arm_fir_decimate_instance_q31* S, uint16_t numTaps, uint8_t M,
+                                     const q31_t* pCoeffs, q31_t* pState, uint32_t blockSize) {
+  return decimate_init<int32_t>(S, numTaps, M, pCoeffs, pState, blockSize);
+}
+arm_status arm_fir_interpolate_init_f32(arm_fir_interpolate_instance_f32* S, uint8_t L, uint16_t numTaps,
+                                        const float32_t* pCoeffs, float32_t* pState, uint32_t blockSize) {
+  return interpolate_init<float>(S, L, numTaps, pCoeffs, pState, blockSize);
+}
+arm_status arm_fir_interpolate_init_q15(arm_fir_interpolate_instance_q15* S, uint8_t L, uint16_t numTaps,
+                                        const q15_t* pCoeffs, q15_t* pState, uint32_t blockSize) {
+  return interpolate_init<int16_t>(S, L, numTaps, pCoeffs, pState, blockSize);
+}
+arm_status arm_fir_interpolate_init_q31(arm_fir_interpolate_instance_q31* S, uint8_t L, uint16_t numTaps,
+                                        const q31_t* pCoeffs, q31_t* pState, uint32_t blockSize) {
+  return interpolate_init<int32_t>(S, L, numTaps, pCoeffs, pState, blockSize);
+}
+#define MI355X_DECIM(NAME, INST, T, CT, OP)                                                              \
+  void NAME(const INST* S, const T* pSrc, T* pDst, uint32_t blockSize) {                                \
+    decimate_sync<CT>(S, (const CT*)pSrc, (CT*)pDst, blockSize, OP, #NAME);                             \
+  }                                                                                                     \
+  arm_status NAME##_batch(const INST* S, const T* d_src, T* d_dst, uint32_t blockSize, uint32_t batch,  \
+                          T* d_hist, void* stream) {                                                    \
+    return decimate_batch<CT>(S, (const CT*)d_src, (CT*)d_dst, blockSize, batch, (CT*)d_hist, stream, OP, \
+                              #NAME "_batch");                                                          \
+  }
+MI355X_DECIM(arm_fir_decimate_f32, arm_fir_decimate_instance_f32, float32_t, float, kMrF32)
+MI355X_DECIM(arm_fir_decimate_q15, arm_fir_decimate_instance_q15, q15_t, int16_t, kMrQ15)
+MI355X_DECIM(arm_fir_decimate_fast_q15, arm_fir_decimate_instance_q15, q15_t, int16_t, kMrFastQ15)
+MI355X_DECIM(arm_fir_decimate_q31, arm_fir_decimate_instance_q31, q31_t, int32_t, kMrQ31)
+MI355X_DECIM(arm_fir_decimate_fast_q31, arm_fir_decimate_instance_q31, q31_t, int32_t, kMrFastQ31)
+#undef MI355X_DECIM
+#define MI355X_INTERP(NAME, INST, T, CT, OP)                                                             \
+  void NAME(const INST* S, const T* pSrc, T* pDst, uint32_t blockSize) {                                \
+    interpolate_sync<CT>(S, (const CT*)pSrc, (CT*)pDst, blockSize, OP, #NAME);                          \
+  }                                                                                                     \
+  arm_status NAME##_batch(const INST* S, const T* d_src, T* d_dst, uint32_t blockSize, uint32_t batch,  \
+                          T* d_hist, void* stream) {                                                    \
+    return interpolate_batch<CT>(S, (const CT*)d_src, (CT*)d_dst, blockSize, batch, (CT*)d_hist, stream, OP, \
+                                 #NAME "_batch");                                                       \
+  }
+MI355X_INTERP(arm_fir_interpolate_f32, arm_fir_interpolate_instance_f32, float32_t, float, kMrF32)
+MI355X_INTERP(arm_fir_interpolate_q15, arm_fir_interpolate_instance_q15, q15_t, int16_t, kMrQ15)
+MI355X_INTERP(arm_fir_interpolate_q31, arm_fir_interpolate_instance_q31, q31_t, int32_t, kMrQ31)
+#undef MI355X_INTERP
 
 }  // extern "C"

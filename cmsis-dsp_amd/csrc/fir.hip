@@ -710,15 +710,17 @@ __global__ __launch_bounds__(kBlock) void fir_q7_kernel(const int8_t* __restrict
   }
 }
 
-// new history = last T-1 samples of [hist ; src]  (arm_fir_f32.c:1242-1278)
+// new history = samples start .. start + T1 - 1 of s = [hist ; src]: the last T-1 for the FIR
+// (start = B, arm_fir_f32.c:1242-1278), from outBlockSize * M for the decimator
+// (arm_fir_decimate_f32.c), the last phaseLength - 1 for the interpolator (start = B)
 template <typename T>
 __global__ void fir_hist_kernel(const T* __restrict__ src, T* __restrict__ hist, const T* __restrict__ hist_in,
-                                uint32_t B, int T1, uint32_t batch) {
+                                uint32_t B, int T1, uint32_t batch, uint32_t start) {
   const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (g >= (uint64_t)batch * T1) return;
   const uint64_t f = g / T1;
   const int j = (int)(g % T1);
-  const int64_t sidx = (int64_t)B + j;              // index into s of the new history word j
+  const int64_t sidx = (int64_t)start + j;          // index into s of the new history word j
   hist[g] = sidx < T1 ? hist_in[f * T1 + sidx] : src[f * B + (sidx - T1)];
 }
 
@@ -797,7 +799,7 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
     const uint64_t n = (uint64_t)batch * T1;
     // stream order: the filter pass has read hist_in before it is overwritten here
     hipLaunchKernelGGL(fir_hist_kernel<T>, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
-                       src, hist, hist_in, B, T1, batch);
+                       src, hist, hist_in, B, T1, batch, B);
     e = hipGetLastError();
   }
   if (tmp) (void)hipFreeAsync(tmp, st);
@@ -824,6 +826,230 @@ hipError_t fir_run(int kind, const void* coeffs, int num_taps, const void* src, 
                                 block_size, batch, (int8_t*)hist, st);
     default:
       return hipErrorInvalidValue;
+  }
+}
+
+// ================================================================ multirate FIR
+// Decimator (arm_fir_decimate_{f32,q15,q31,fast_q15,fast_q31}.c, generic C paths): with
+// s = [history (numTaps-1) ; block], output j = sum_t s[M j + t] * h[t], t ascending from a
+// zero accumulator; outBlockSize = blockSize / M.  Interpolator
+// (arm_fir_interpolate_{f32,q15,q31}.c): s = [history (phaseLength-1) ; block], output
+// n L + q = sum_i s[n + i] * h[(L-1-q) + i L], i ascending.  Accumulators per op:
+//   f32: mul then add (bit-exact order);  q15: q63 sum of exact products, __SSAT(acc >> 15, 16);
+//   q31: q63 sum, (q31)(acc >> 31);  fast q15 (decimator): q31_t wrapping sum, __SSAT(acc >> 15, 16);
+//   fast q31 (decimator): acc = (q31)(((q63)acc << 32 + x*h) >> 32) = acc + floor(x*h / 2^32)
+//   mod 2^32 (no rounding term, unlike arm_fir_fast_q31), output acc << 1.
+// The integer sums are order-free, the f32 one is not.  One workgroup = one filter x a chunk of
+// outputs; the window is staged in LDS (the decimator's as M phases X_p[m] = s[M (j0 + m) + p]
+// so that lanes with consecutive outputs read consecutive words: bank-conflict free for any M);
+// coefficients are wave-uniform scalar loads.
+template <int OP> struct MrT;
+template <> struct MrT<kMrF32> {
+  using T = float; using Acc = float;
+  static __device__ __forceinline__ Acc mac(Acc a, T w, T c) { const float p = w * c; return a + p; }
+  static __device__ __forceinline__ T out(Acc a) { return a; }
+};
+template <> struct MrT<kMrQ15> {
+  using T = int16_t; using Acc = int64_t;
+  static __device__ __forceinline__ Acc mac(Acc a, T w, T c) { return a + (int32_t)w * (int32_t)c; }
+  static __device__ __forceinline__ T out(Acc a) { return (T)ssat16((int32_t)(a >> 15)); }
+};
+template <> struct MrT<kMrQ31> {
+  using T = int32_t; using Acc = uint64_t;
+  static __device__ __forceinline__ Acc mac(Acc a, T w, T c) { return a + (uint64_t)((int64_t)w * c); }
+  static __device__ __forceinline__ T out(Acc a) { return (T)(int32_t)((int64_t)a >> 31); }
+};
+template <> struct MrT<kMrFastQ15> {
+  using T = int16_t; using Acc = uint32_t;
+  static __device__ __forceinline__ Acc mac(Acc a, T w, T c) { return a + (uint32_t)((int32_t)w * (int32_t)c); }
+  static __device__ __forceinline__ T out(Acc a) { return (T)ssat16((int32_t)a >> 15); }
+};
+template <> struct MrT<kMrFastQ31> {
+  using T = int32_t; using Acc = uint32_t;
+  static __device__ __forceinline__ Acc mac(Acc a, T w, T c) { return a + (uint32_t)mulhi(w, c); }
+  static __device__ __forceinline__ T out(Acc a) { return (T)(a << 1); }
+};
+
+constexpr int kMrWin = 8192;               // LDS window elements per workgroup
+
+template <int OP>
+__global__ __launch_bounds__(kBlock) void fir_decimate_kernel(const typename MrT<OP>::T* __restrict__ coeffs, int T,
+                                                              int M, const typename MrT<OP>::T* __restrict__ src,
+                                                              typename MrT<OP>::T* __restrict__ dst, uint32_t B,
+                                                              const typename MrT<OP>::T* __restrict__ hist_in,
+                                                              uint32_t nchunks, int J, int Wp) {
+  using Op = MrT<OP>;
+  using E = typename Op::T;
+  __shared__ E win[kMrWin];
+  const uint32_t f = blockIdx.x / nchunks;
+  const int j0 = (int)(blockIdx.x - f * nchunks) * J;
+  const int outs = (int)(B / (uint32_t)M);
+  const int cnt = min(J, outs - j0);
+  FirItem it;
+  it.f = f; it.n0 = M * j0; it.count = cnt; it.total = M * (cnt - 1) + T;
+  for (int idx = threadIdx.x; idx < M * Wp; idx += kBlock) {
+    const int m = idx / M, p = idx - m * M;
+    win[p * Wp + m] = fir_sample(hist_in, src, it, B, T - 1, idx);
+  }
+  __syncthreads();
+  E* y = dst + (uint64_t)f * outs + j0;
+  for (int jl = threadIdx.x; jl < cnt; jl += kBlock) {
+    typename Op::Acc acc = 0;
+    if constexpr (OP == kMrF32) {
+      // t ascending: (i, p) = divmod(t, M), tap t reads X_p[jl + i]
+      const E* w = win + jl;
+      int t = 0;
+      for (int i = 0; t < T; ++i, ++w)
+        for (int p = 0; p < M && t < T; ++p, ++t) acc = Op::mac(acc, w[p * Wp], coeffs[t]);
+    } else {
+      // order-free sums: phase by phase, taps t = i M + p
+      for (int p = 0; p < M && p < T; ++p) {
+        const E* w = win + p * Wp + jl;
+        const int ni = (T - p + M - 1) / M;
+        for (int i = 0; i < ni; ++i) acc = Op::mac(acc, w[i], coeffs[i * M + p]);
+      }
+    }
+    y[jl] = Op::out(acc);
+  }
+}
+
+template <int OP>
+__global__ __launch_bounds__(kBlock) void fir_interpolate_kernel(const typename MrT<OP>::T* __restrict__ coeffs, int L,
+                                                                 int P, const typename MrT<OP>::T* __restrict__ src,
+                                                                 typename MrT<OP>::T* __restrict__ dst, uint32_t B,
+                                                                 const typename MrT<OP>::T* __restrict__ hist_in,
+                                                                 uint32_t nchunks, int N) {
+  using Op = MrT<OP>;
+  using E = typename Op::T;
+  __shared__ E win[kMrWin];
+  const uint32_t f = blockIdx.x / nchunks;
+  const int n0 = (int)(blockIdx.x - f * nchunks) * N;
+  const int cnt = min(N, (int)B - n0);
+  FirItem it;
+  it.f = f; it.n0 = n0; it.count = cnt; it.total = cnt + P - 1;
+  for (int idx = threadIdx.x; idx < it.total; idx += kBlock) win[idx] = fir_sample(hist_in, src, it, B, P - 1, idx);
+  __syncthreads();
+  E* y = dst + ((uint64_t)f * B + n0) * (uint32_t)L;
+  for (int nl = threadIdx.x; nl < cnt; nl += kBlock) {
+    const E* w = win + nl;
+    for (int q = 0; q < L; ++q) {
+      const E* h = coeffs + (L - 1 - q);
+      typename Op::Acc acc = 0;
+      int i = 0;
+      for (; i + 4 <= P; i += 4) {
+        acc = Op::mac(acc, w[i], h[i * L]);
+        acc = Op::mac(acc, w[i + 1], h[(i + 1) * L]);
+        acc = Op::mac(acc, w[i + 2], h[(i + 2) * L]);
+        acc = Op::mac(acc, w[i + 3], h[(i + 3) * L]);
+      }
+      for (; i < P; ++i) acc = Op::mac(acc, w[i], h[i * L]);
+      y[(uint64_t)nl * L + q] = Op::out(acc);
+    }
+  }
+}
+
+// Shared host part: history copy when the new history depends on the old one (the pass reads
+// hist_in, the history kernel rewrites hist), input copy when src overlaps dst, the filter
+// launch, then the history update from `start`.
+template <typename E, typename Launch>
+static hipError_t mr_launch(const E* src, E* dst, size_t out_words, uint32_t B, uint32_t batch, E* hist, int H,
+                            uint32_t start, hipStream_t st, Launch&& launch) {
+  const E* hist_in = hist;
+  E* tmp = nullptr;
+  if (H > 0 && (int64_t)start < H) {
+    hipError_t e = hipMallocAsync((void**)&tmp, sizeof(E) * (size_t)batch * H, st);
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(tmp, hist, sizeof(E) * (size_t)batch * H, hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) return e;
+    hist_in = tmp;
+  }
+  E* src_copy = nullptr;
+  {
+    const size_t ib = sizeof(E) * (size_t)batch * B, ob = sizeof(E) * out_words;
+    const uintptr_t s0 = (uintptr_t)src, d0 = (uintptr_t)dst;
+    if (s0 < d0 + ob && d0 < s0 + ib) {
+      hipError_t e = hipMallocAsync((void**)&src_copy, ib, st);
+      if (e != hipSuccess) return e;
+      e = hipMemcpyAsync(src_copy, src, ib, hipMemcpyDeviceToDevice, st);
+      if (e != hipSuccess) return e;
+      src = src_copy;
+    }
+  }
+  hipError_t e = launch(src, hist_in);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e == hipSuccess && H > 0) {
+    const uint64_t n = (uint64_t)batch * H;
+    hipLaunchKernelGGL(fir_hist_kernel<E>, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, src, hist,
+                       hist_in, B, H, batch, start);
+    e = hipGetLastError();
+  }
+  if (tmp) (void)hipFreeAsync(tmp, st);
+  if (src_copy) (void)hipFreeAsync(src_copy, st);
+  return e;
+}
+
+template <int OP>
+static hipError_t decimate_launch(const void* coeffs, int T, int M, const void* src, void* dst, uint32_t B,
+                                  uint32_t batch, void* hist, hipStream_t st) {
+  using E = typename MrT<OP>::T;
+  if (batch == 0 || B == 0) return hipSuccess;
+  if (T < 1 || M < 1) return hipErrorInvalidValue;
+  const int outs = (int)(B / (uint32_t)M);
+  const int per_phase = (T + M - 1) / M;
+  int J = kMrWin / M - per_phase - 1;               // M * (J + per_phase + 1) <= kMrWin
+  if (J < 1) return hipErrorInvalidValue;
+  J = J >= 2 * kBlock ? 4 * kBlock < J ? 4 * kBlock : (J / kBlock) * kBlock : J;
+  const int Wp = J + per_phase + 1;
+  const uint32_t nchunks = outs > 0 ? (uint32_t)((outs + J - 1) / J) : 0;
+  const uint64_t blocks = (uint64_t)nchunks * batch;
+  if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  return mr_launch<E>((const E*)src, (E*)dst, (size_t)batch * outs, B, batch, (E*)hist, T - 1, (uint32_t)(outs * M),
+                      st, [&](const E* s, const E* h) {
+                        if (blocks == 0) return hipSuccess;
+                        hipLaunchKernelGGL(fir_decimate_kernel<OP>, dim3((uint32_t)blocks), dim3(kBlock), 0, st,
+                                           (const E*)coeffs, T, M, s, (E*)dst, B, h, nchunks, J, Wp);
+                        return hipSuccess;
+                      });
+}
+
+template <int OP>
+static hipError_t interpolate_launch(const void* coeffs, int L, int P, const void* src, void* dst, uint32_t B,
+                                     uint32_t batch, void* hist, hipStream_t st) {
+  using E = typename MrT<OP>::T;
+  if (batch == 0 || B == 0) return hipSuccess;
+  if (L < 1 || P < 1 || P > kMrWin - kBlock) return hipErrorInvalidValue;
+  int N = kMrWin - (P - 1);
+  N = N >= 4 * kBlock ? 4 * kBlock : (N >= kBlock ? (N / kBlock) * kBlock : N);
+  const uint32_t nchunks = (B + N - 1) / N;
+  const uint64_t blocks = (uint64_t)nchunks * batch;
+  if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  return mr_launch<E>((const E*)src, (E*)dst, (size_t)batch * B * L, B, batch, (E*)hist, P - 1, B, st,
+                      [&](const E* s, const E* h) {
+                        hipLaunchKernelGGL(fir_interpolate_kernel<OP>, dim3((uint32_t)blocks), dim3(kBlock), 0, st,
+                                           (const E*)coeffs, L, P, s, (E*)dst, B, h, nchunks, N);
+                        return hipSuccess;
+                      });
+}
+
+hipError_t fir_decimate_run(int op, const void* coeffs, int num_taps, int M, const void* src, void* dst,
+                            uint32_t block_size, uint32_t batch, void* hist, hipStream_t st) {
+  switch (op) {
+    case kMrF32: return decimate_launch<kMrF32>(coeffs, num_taps, M, src, dst, block_size, batch, hist, st);
+    case kMrQ15: return decimate_launch<kMrQ15>(coeffs, num_taps, M, src, dst, block_size, batch, hist, st);
+    case kMrQ31: return decimate_launch<kMrQ31>(coeffs, num_taps, M, src, dst, block_size, batch, hist, st);
+    case kMrFastQ15: return decimate_launch<kMrFastQ15>(coeffs, num_taps, M, src, dst, block_size, batch, hist, st);
+    case kMrFastQ31: return decimate_launch<kMrFastQ31>(coeffs, num_taps, M, src, dst, block_size, batch, hist, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t fir_interpolate_run(int op, const void* coeffs, int L, int phase_len, const void* src, void* dst,
+                               uint32_t block_size, uint32_t batch, void* hist, hipStream_t st) {
+  switch (op) {
+    case kMrF32: return interpolate_launch<kMrF32>(coeffs, L, phase_len, src, dst, block_size, batch, hist, st);
+    case kMrQ15: return interpolate_launch<kMrQ15>(coeffs, L, phase_len, src, dst, block_size, batch, hist, st);
+    case kMrQ31: return interpolate_launch<kMrQ31>(coeffs, L, phase_len, src, dst, block_size, batch, hist, st);
+    default: return hipErrorInvalidValue;
   }
 }
 

@@ -66,6 +66,16 @@ enum FirKind { kFirF32 = 0, kFirQ15 = 1, kFirQ31 = 2, kFirFastQ15 = 3, kFirFastQ
 hipError_t fir_run(int kind, const void* coeffs, int num_taps, const void* src, void* dst, uint32_t block_size,
                    uint32_t batch, void* hist, hipStream_t st);
 
+// Multirate FIR (fir.hip): `batch` independent decimators / interpolators sharing one
+// coefficient set.  Decimator: outputs [batch][blockSize / M], hist [batch][numTaps - 1].
+// Interpolator (phase_len = numTaps / L): outputs [batch][blockSize * L], hist
+// [batch][phase_len - 1].  The interpolator takes kMrF32 / kMrQ15 / kMrQ31.
+enum MrOp { kMrF32 = 0, kMrQ15 = 1, kMrQ31 = 2, kMrFastQ15 = 3, kMrFastQ31 = 4 };
+hipError_t fir_decimate_run(int op, const void* coeffs, int num_taps, int M, const void* src, void* dst,
+                            uint32_t block_size, uint32_t batch, void* hist, hipStream_t st);
+hipError_t fir_interpolate_run(int op, const void* coeffs, int L, int phase_len, const void* src, void* dst,
+                               uint32_t block_size, uint32_t batch, void* hist, hipStream_t st);
+
 // MFCC f32 around the batched RFFT (mfcc_f32.hip): frame normalisation + window, then the
 // spectrum -> Mel -> log -> DCT tail.  post needs mfcc_f32_post_lds(n, nb_mel) bytes of LDS.
 // Fused single-launch MFCC for the reference's canonical CFFT tables (nb_mel <= n/2):

@@ -135,6 +135,50 @@ typedef struct {
   const float32_t *pCoeffs;
 } arm_fir_instance_f32;
 
+/* ---- multirate FIR instances: Include/dsp/filtering_functions.h:803-831 (decimators),
+ * :1012-1040 (interpolators) */
+typedef struct {
+        uint8_t    M;
+        uint16_t   numTaps;
+  const q15_t     *pCoeffs;
+        q15_t     *pState;
+} arm_fir_decimate_instance_q15;
+
+typedef struct {
+        uint8_t    M;
+        uint16_t   numTaps;
+  const q31_t     *pCoeffs;
+        q31_t     *pState;
+} arm_fir_decimate_instance_q31;
+
+typedef struct {
+        uint8_t    M;
+        uint16_t   numTaps;
+  const float32_t *pCoeffs;
+        float32_t *pState;
+} arm_fir_decimate_instance_f32;
+
+typedef struct {
+        uint8_t    L;
+        uint16_t   phaseLength;
+  const q15_t     *pCoeffs;
+        q15_t     *pState;
+} arm_fir_interpolate_instance_q15;
+
+typedef struct {
+        uint8_t    L;
+        uint16_t   phaseLength;
+  const q31_t     *pCoeffs;
+        q31_t     *pState;
+} arm_fir_interpolate_instance_q31;
+
+typedef struct {
+        uint8_t    L;
+        uint16_t   phaseLength;
+  const float32_t *pCoeffs;
+        float32_t *pState;
+} arm_fir_interpolate_instance_f32;
+
 /* ---- matrix instances: Include/dsp/matrix_functions.h:118-123 (f32), :139-143 (q7),
  * :139-144 (q15), :149-154 (q31) */
 typedef struct {
@@ -347,6 +391,49 @@ void arm_fir_fast_q15(const arm_fir_instance_q15 *S, const q15_t *pSrc,
 void arm_fir_init_q7(arm_fir_instance_q7 *S, uint16_t numTaps, const q7_t *pCoeffs, q7_t *pState,
                      uint32_t blockSize);
 void arm_fir_q7(const arm_fir_instance_q7 *S, const q7_t *pSrc, q7_t *pDst, uint32_t blockSize);
+
+/* ===================================================================================
+ * Multirate FIR.  Prototypes: Include/dsp/filtering_functions.h:886-1007 (decimators),
+ * :1050-1150 (interpolators).  Reference bodies: Source/FilteringFunctions/
+ * arm_fir_decimate_{f32,q15,fast_q15,q31,fast_q31}.c and arm_fir_interpolate_{f32,q15,q31}.c
+ * (generic C paths), arm_fir_decimate_init_*.c (ARM_MATH_LENGTH_ERROR unless blockSize % M
+ * == 0; state numTaps + blockSize - 1 words), arm_fir_interpolate_init_*.c
+ * (ARM_MATH_LENGTH_ERROR unless numTaps % L == 0; phaseLength = numTaps / L; state
+ * blockSize + phaseLength - 1 words).  Decimator output j = sum_t s[M j + t] h[t] (blockSize / M
+ * outputs); interpolator output n L + q = sum_i s[n + i] h[(L-1-q) + i L] (blockSize L outputs);
+ * s = [history ; block].  Accumulators: f32 mul then add, q15 / q31 q63 sums (__SSAT(>> 15) /
+ * >> 31), fast q15 a wrapping q31 sum with __SSAT(>> 15), fast q31 acc + floor(x h / 2^32)
+ * (no rounding term), output << 1.  M == 0 / L == 0 return ARM_MATH_LENGTH_ERROR (the
+ * reference divides by zero).
+ * =================================================================================== */
+arm_status arm_fir_decimate_init_f32(arm_fir_decimate_instance_f32 *S, uint16_t numTaps, uint8_t M,
+                                     const float32_t *pCoeffs, float32_t *pState, uint32_t blockSize);
+arm_status arm_fir_decimate_init_q15(arm_fir_decimate_instance_q15 *S, uint16_t numTaps, uint8_t M,
+                                     const q15_t *pCoeffs, q15_t *pState, uint32_t blockSize);
+arm_status arm_fir_decimate_init_q31(arm_fir_decimate_instance_q31 *S, uint16_t numTaps, uint8_t M,
+                                     const q31_t *pCoeffs, q31_t *pState, uint32_t blockSize);
+void arm_fir_decimate_f32(const arm_fir_decimate_instance_f32 *S, const float32_t *pSrc, float32_t *pDst,
+                          uint32_t blockSize);
+void arm_fir_decimate_q15(const arm_fir_decimate_instance_q15 *S, const q15_t *pSrc, q15_t *pDst,
+                          uint32_t blockSize);
+void arm_fir_decimate_fast_q15(const arm_fir_decimate_instance_q15 *S, const q15_t *pSrc, q15_t *pDst,
+                               uint32_t blockSize);
+void arm_fir_decimate_q31(const arm_fir_decimate_instance_q31 *S, const q31_t *pSrc, q31_t *pDst,
+                          uint32_t blockSize);
+void arm_fir_decimate_fast_q31(const arm_fir_decimate_instance_q31 *S, const q31_t *pSrc, q31_t *pDst,
+                               uint32_t blockSize);
+arm_status arm_fir_interpolate_init_f32(arm_fir_interpolate_instance_f32 *S, uint8_t L, uint16_t numTaps,
+                                        const float32_t *pCoeffs, float32_t *pState, uint32_t blockSize);
+arm_status arm_fir_interpolate_init_q15(arm_fir_interpolate_instance_q15 *S, uint8_t L, uint16_t numTaps,
+                                        const q15_t *pCoeffs, q15_t *pState, uint32_t blockSize);
+arm_status arm_fir_interpolate_init_q31(arm_fir_interpolate_instance_q31 *S, uint8_t L, uint16_t numTaps,
+                                        const q31_t *pCoeffs, q31_t *pState, uint32_t blockSize);
+void arm_fir_interpolate_f32(const arm_fir_interpolate_instance_f32 *S, const float32_t *pSrc, float32_t *pDst,
+                             uint32_t blockSize);
+void arm_fir_interpolate_q15(const arm_fir_interpolate_instance_q15 *S, const q15_t *pSrc, q15_t *pDst,
+                             uint32_t blockSize);
+void arm_fir_interpolate_q31(const arm_fir_interpolate_instance_q31 *S, const q31_t *pSrc, q31_t *pDst,
+                             uint32_t blockSize);
 
 /* ===================================================================================
  * Convolution.  Prototypes: Include/dsp/filtering_functions.h

@@ -80,6 +80,30 @@ arm_status arm_fir_fast_q31_batch(const arm_fir_instance_q31 *S, const q31_t *d_
 arm_status arm_fir_q7_batch(const arm_fir_instance_q7 *S, const q7_t *d_src, q7_t *d_dst,
                             uint32_t blockSize, uint32_t batch, q7_t *d_hist, void *stream);
 
+/* Multirate FIR over `batch` independent streams sharing one instance's coefficients (the
+ * instance's pState is not used): d_src [batch][blockSize]; decimators write
+ * d_dst [batch][blockSize / M] with d_hist [batch][numTaps - 1]; interpolators write
+ * d_dst [batch][blockSize * L] with d_hist [batch][phaseLength - 1].  Per-stream semantics:
+ * arm_fir_decimate_* / arm_fir_interpolate_*. */
+arm_status arm_fir_decimate_f32_batch(const arm_fir_decimate_instance_f32 *S, const float32_t *d_src,
+                                      float32_t *d_dst, uint32_t blockSize, uint32_t batch, float32_t *d_hist,
+                                      void *stream);
+arm_status arm_fir_decimate_q15_batch(const arm_fir_decimate_instance_q15 *S, const q15_t *d_src, q15_t *d_dst,
+                                      uint32_t blockSize, uint32_t batch, q15_t *d_hist, void *stream);
+arm_status arm_fir_decimate_fast_q15_batch(const arm_fir_decimate_instance_q15 *S, const q15_t *d_src, q15_t *d_dst,
+                                           uint32_t blockSize, uint32_t batch, q15_t *d_hist, void *stream);
+arm_status arm_fir_decimate_q31_batch(const arm_fir_decimate_instance_q31 *S, const q31_t *d_src, q31_t *d_dst,
+                                      uint32_t blockSize, uint32_t batch, q31_t *d_hist, void *stream);
+arm_status arm_fir_decimate_fast_q31_batch(const arm_fir_decimate_instance_q31 *S, const q31_t *d_src, q31_t *d_dst,
+                                           uint32_t blockSize, uint32_t batch, q31_t *d_hist, void *stream);
+arm_status arm_fir_interpolate_f32_batch(const arm_fir_interpolate_instance_f32 *S, const float32_t *d_src,
+                                         float32_t *d_dst, uint32_t blockSize, uint32_t batch, float32_t *d_hist,
+                                         void *stream);
+arm_status arm_fir_interpolate_q15_batch(const arm_fir_interpolate_instance_q15 *S, const q15_t *d_src, q15_t *d_dst,
+                                         uint32_t blockSize, uint32_t batch, q15_t *d_hist, void *stream);
+arm_status arm_fir_interpolate_q31_batch(const arm_fir_interpolate_instance_q31 *S, const q31_t *d_src, q31_t *d_dst,
+                                         uint32_t blockSize, uint32_t batch, q31_t *d_hist, void *stream);
+
 /* Convolution of `batch` pairs: item i convolves d_a + i*strideA (srcALen samples) with
  * d_b + i*strideB (srcBLen samples; strideB = 0 shares one kernel) into
  * d_dst + i*(srcALen + srcBLen - 1).  Per-item semantics: arm_conv_f32 / _q15 / _q31. */

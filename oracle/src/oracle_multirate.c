@@ -1,0 +1,117 @@
+/* ORACLE — test infrastructure only (never linked into the product).
+ *
+ * Plain-C restatement of the reference's multirate FIR paths (Source/FilteringFunctions,
+ * generic C branches, as the host build runs them):
+ *   arm_fir_decimate_{f32,q15,fast_q15,q31,fast_q31}.c: the block is appended to the state
+ *     s = [history (numTaps-1) ; block]; output j (j < blockSize / M) = sum over t ascending
+ *     of s[M j + t] * h[t] from a zero accumulator; then the numTaps - 1 words from
+ *     s[(blockSize / M) M] are moved to the front.  Accumulators: f32 mul then add; q15 q63
+ *     (__SSAT(acc >> 15, 16)); fast q15 q31_t with wrapping adds (__SSAT(acc >> 15, 16)); q31
+ *     q63 ((q31)(acc >> 31)); fast q31 acc = (q31)((((q63)acc << 32) + x*h) >> 32) with no
+ *     rounding term, output (q31)(acc << 1).
+ *   arm_fir_interpolate_{f32,q15,q31}.c: s = [history (phaseLength-1) ; block]; output
+ *     n L + q = sum over i ascending of s[n + i] * h[(L-1-q) + i L]; f32 mul then add, q15 q63
+ *     (__SSAT(acc >> 15, 16)), q31 q63 ((q31)(acc >> 31)); the last phaseLength - 1 words move
+ *     to the front.
+ *   arm_fir_decimate_init_*.c / arm_fir_interpolate_init_*.c: ARM_MATH_LENGTH_ERROR unless
+ *     blockSize % M == 0 / numTaps % L == 0; the state is zeroed.
+ * Pinned against oracle/_ref by tests/test_multirate.py. */
+#include <stdint.h>
+#include <string.h>
+
+#include "oracle.h"
+
+enum { MR_F32, MR_Q15, MR_FQ15, MR_Q31, MR_FQ31 };
+
+static int16_t sat16(int64_t v) { return (int16_t)(v > 32767 ? 32767 : v < -32768 ? -32768 : v); }
+
+/* one output: sum_{i < n} x[i * xs] * h[i * hs], ascending */
+static void mr_dot(int op, const void *x, int xs, const void *h, int hs, int n, void *out) {
+  if (op == MR_F32) {
+    const float *a = x, *b = h;
+    float s = 0.0f;
+    for (int i = 0; i < n; ++i) { const float p = a[i * xs] * b[i * hs]; s = s + p; }
+    *(float *)out = s;
+  } else if (op == MR_Q15 || op == MR_FQ15) {
+    const int16_t *a = x, *b = h;
+    if (op == MR_Q15) {
+      int64_t s = 0;
+      for (int i = 0; i < n; ++i) s += (int32_t)a[i * xs] * b[i * hs];
+      *(int16_t *)out = sat16(s >> 15);
+    } else {
+      uint32_t s = 0;
+      for (int i = 0; i < n; ++i) s += (uint32_t)((int32_t)a[i * xs] * b[i * hs]);
+      *(int16_t *)out = sat16((int32_t)s >> 15);
+    }
+  } else {
+    const int32_t *a = x, *b = h;
+    if (op == MR_Q31) {
+      uint64_t s = 0;
+      for (int i = 0; i < n; ++i) s += (uint64_t)((int64_t)a[i * xs] * b[i * hs]);
+      *(int32_t *)out = (int32_t)((int64_t)s >> 31);
+    } else {
+      int32_t s = 0;
+      for (int i = 0; i < n; ++i) {
+        const uint64_t wide = ((uint64_t)(int64_t)s << 32) + (uint64_t)((int64_t)a[i * xs] * b[i * hs]);
+        s = (int32_t)(uint32_t)((int64_t)wide >> 32);
+      }
+      *(int32_t *)out = (int32_t)((uint32_t)s << 1);
+    }
+  }
+}
+
+static void decimate(int op, size_t es, uint8_t M, uint16_t taps, const void *h, void *state, const void *src,
+                     void *dst, uint32_t B) {
+  char *s = state;
+  memcpy(s + es * (taps - 1), src, es * B);
+  const uint32_t outs = B / M;
+  for (uint32_t j = 0; j < outs; ++j) mr_dot(op, s + es * ((size_t)M * j), 1, h, 1, taps, (char *)dst + es * j);
+  memmove(s, s + es * ((size_t)outs * M), es * (taps - 1));
+}
+
+static void interpolate(int op, size_t es, uint8_t L, uint16_t P, const void *h, void *state, const void *src,
+                        void *dst, uint32_t B) {
+  char *s = state;
+  memcpy(s + es * (P - 1), src, es * B);
+  for (uint32_t n = 0; n < B; ++n)
+    for (uint32_t q = 0; q < L; ++q)
+      mr_dot(op, s + es * n, 1, (const char *)h + es * (L - 1 - q), L, P, (char *)dst + es * ((size_t)n * L + q));
+  memmove(s, s + es * B, es * (P - 1));
+}
+
+#define DECIM(NAME, INST, T, OP)                                                              \
+  void oracle_##NAME(const INST *S, const T *pSrc, T *pDst, uint32_t blockSize) {             \
+    decimate(OP, sizeof(T), S->M, S->numTaps, S->pCoeffs, S->pState, pSrc, pDst, blockSize); \
+  }
+DECIM(arm_fir_decimate_f32, arm_fir_decimate_instance_f32, float, MR_F32)
+DECIM(arm_fir_decimate_q15, arm_fir_decimate_instance_q15, int16_t, MR_Q15)
+DECIM(arm_fir_decimate_fast_q15, arm_fir_decimate_instance_q15, int16_t, MR_FQ15)
+DECIM(arm_fir_decimate_q31, arm_fir_decimate_instance_q31, int32_t, MR_Q31)
+DECIM(arm_fir_decimate_fast_q31, arm_fir_decimate_instance_q31, int32_t, MR_FQ31)
+
+#define INTERP(NAME, INST, T, OP)                                                                  \
+  void oracle_##NAME(const INST *S, const T *pSrc, T *pDst, uint32_t blockSize) {                  \
+    interpolate(OP, sizeof(T), S->L, S->phaseLength, S->pCoeffs, S->pState, pSrc, pDst, blockSize); \
+  }
+INTERP(arm_fir_interpolate_f32, arm_fir_interpolate_instance_f32, float, MR_F32)
+INTERP(arm_fir_interpolate_q15, arm_fir_interpolate_instance_q15, int16_t, MR_Q15)
+INTERP(arm_fir_interpolate_q31, arm_fir_interpolate_instance_q31, int32_t, MR_Q31)
+
+#define DINIT(T, ET)                                                                                          \
+  arm_status oracle_arm_fir_decimate_init_##T(arm_fir_decimate_instance_##T *S, uint16_t numTaps, uint8_t M,   \
+                                              const ET *pCoeffs, ET *pState, uint32_t blockSize) {             \
+    if (M == 0 || blockSize % M) return ARM_MATH_LENGTH_ERROR;                                                \
+    S->numTaps = numTaps; S->pCoeffs = pCoeffs; S->pState = pState; S->M = M;                                \
+    memset(pState, 0, sizeof(ET) * ((size_t)numTaps + blockSize - 1));                                        \
+    return ARM_MATH_SUCCESS;                                                                                  \
+  }                                                                                                           \
+  arm_status oracle_arm_fir_interpolate_init_##T(arm_fir_interpolate_instance_##T *S, uint8_t L, uint16_t numTaps, \
+                                                 const ET *pCoeffs, ET *pState, uint32_t blockSize) {         \
+    if (L == 0 || numTaps % L) return ARM_MATH_LENGTH_ERROR;                                                  \
+    S->pCoeffs = pCoeffs; S->L = L; S->phaseLength = numTaps / L; S->pState = pState;                         \
+    memset(pState, 0, sizeof(ET) * ((size_t)blockSize + S->phaseLength - 1));                                 \
+    return ARM_MATH_SUCCESS;                                                                                  \
+  }
+DINIT(f32, float)
+DINIT(q15, int16_t)
+DINIT(q31, int32_t)

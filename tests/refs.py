@@ -114,6 +114,37 @@ class Host:
         self._keep = (c, state)
         return outs, state.copy()
 
+    def multirate(self, fn, factor, coeffs, blocks, block_size=None):
+        """Stream `blocks` through one arm_fir_decimate_* / arm_fir_interpolate_* instance
+        (fn e.g. "decimate_fast_q15", "interpolate_f32"; factor = M or L): returns
+        (init status, outputs, final state buffer)."""
+        base = fn.split("_")[-1]
+        dt = DTYPE[base]
+        decim = fn.startswith("decimate")
+        c = np.ascontiguousarray(coeffs, dtype=dt)
+        bs = block_size or max(len(b) for b in blocks)
+        if decim:
+            inst = _abi.arm_fir_decimate_instance()
+            state = np.zeros(len(c) + bs - 1, dtype=dt)
+            st = self.fn(f"arm_fir_decimate_init_{base}")(C.byref(inst), len(c), factor, c.ctypes.data,
+                                                            state.ctypes.data, bs)
+        else:
+            inst = _abi.arm_fir_interpolate_instance()
+            state = np.zeros(bs + max(len(c) // max(factor, 1), 1) - 1, dtype=dt)
+            st = self.fn(f"arm_fir_interpolate_init_{base}")(C.byref(inst), factor, len(c), c.ctypes.data,
+                                                               state.ctypes.data, bs)
+        if st != 0:
+            return st, [], state
+        outs = []
+        f = self.fn(f"arm_fir_{fn}")
+        for b in blocks:
+            b = np.ascontiguousarray(b, dtype=dt)
+            y = np.zeros(len(b) // factor if decim else len(b) * factor, dtype=dt)
+            f(C.byref(inst), b.ctypes.data, y.ctypes.data, len(b))
+            outs.append(y)
+        self._keep = (c, state)
+        return st, outs, state.copy()
+
     def conv(self, kind, a, b):
         dt = DTYPE[kind]
         a = np.ascontiguousarray(a, dtype=dt)
