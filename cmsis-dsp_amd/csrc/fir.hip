@@ -161,6 +161,14 @@ __device__ __forceinline__ void fir_f32_put(float* wl, const F32Win<KPRE>& w) {
 #define MI355X_FIR_IPW 16
 #endif
 
+// Output lattice of fir_f32_kernel: plain (the FIR: y[f B + n]) or, for the multirate forms,
+// y[f per_filter + (n / M) L + q] for the outputs with n % M == 0 (decimator: L = 1, q = 0;
+// interpolator phase q: M = 1).
+struct FirOut {
+  uint32_t plain, M, L, q;
+  uint64_t per_filter;
+};
+
 #ifndef MI355X_FIR_F32_WAVES
 #define MI355X_FIR_F32_WAVES 8     // minimum waves per SIMD the register allocation must allow
 #endif
@@ -168,7 +176,8 @@ template <int KPRE>
 __global__ __launch_bounds__(kBlock, MI355X_FIR_F32_WAVES) void fir_f32_kernel(const float* __restrict__ coeffs, int T,
                                                          const float* __restrict__ src, float* __restrict__ dst,
                                                          uint32_t B, const float* __restrict__ hist_in,
-                                                         uint32_t nchunks, uint32_t items, uint32_t ipw) {
+                                                         uint32_t nchunks, uint32_t items, uint32_t ipw,
+                                                         FirOut fo) {
   constexpr int kWin = KPRE * kBlock;
   __shared__ __attribute__((aligned(16))) float win[wpos(kWin) + 16];
   const int T1 = T - 1;
@@ -251,7 +260,14 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_F32_WAVES) void fir_f32_kernel(c
       __syncthreads();                              // every wave is done reading this window
       fir_f32_put<KPRE>(wl, pre);
     }
-    if (base < cur.count) {
+    if (base < cur.count && !fo.plain) {             // decimator / interpolator phase
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const uint32_t n = (uint32_t)(cur.n0 + base + r);
+        if (base + r < cur.count && n % fo.M == 0)
+          dst[(uint64_t)cur.f * fo.per_filter + (uint64_t)(n / fo.M) * fo.L + fo.q] = acc[r];
+      }
+    } else if (base < cur.count) {
       float* o = dst + (uint64_t)cur.f * B + cur.n0 + base;
       if ((B & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + 8 <= cur.count) {
         reinterpret_cast<float4*>(o)[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
@@ -724,6 +740,23 @@ __global__ void fir_hist_kernel(const T* __restrict__ src, T* __restrict__ hist,
   hist[g] = sidx < T1 ? hist_in[f * T1 + sidx] : src[f * B + (sidx - T1)];
 }
 
+// One f32 FIR pass over `batch` filters (T <= kFirMaxTaps), outputs on the lattice `fo`.
+static void fir_f32_pass(const float* coeffs, int T, const float* src, float* dst, uint32_t B, uint32_t batch,
+                         const float* hist_in, FirOut fo, hipStream_t st) {
+  const uint32_t nchunks = (B + kF32Chunk - 1) / kF32Chunk;
+  const uint32_t items = nchunks * batch;
+  const int kpre = fir_f32_kpre(T);
+  auto k = kpre <= 9 ? fir_f32_kernel<9> : kpre == 10 ? fir_f32_kernel<10> : kpre == 11 ? fir_f32_kernel<11>
+         : kpre == 12 ? fir_f32_kernel<12> : fir_f32_kernel<13>;
+  uint32_t ipw = MI355X_FIR_IPW;
+  if (!ipw) {
+    const uint32_t resident = (uint32_t)persistent_grid((const void*)k, kBlock, 0, items);
+    ipw = (items + resident - 1) / resident;
+  }
+  hipLaunchKernelGGL(k, dim3((items + ipw - 1) / ipw), dim3(kBlock), 0, st, coeffs, T, src, dst, B, hist_in, nchunks,
+                     items, ipw, fo);
+}
+
 template <typename T>
 static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T* dst, uint32_t B, uint32_t batch,
                              T* hist, hipStream_t st) {
@@ -763,16 +796,8 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
   }
   switch (kind) {
     case kFirF32: {
-      const int kpre = fir_f32_kpre(T_);
-      auto k = kpre <= 9 ? fir_f32_kernel<9> : kpre == 10 ? fir_f32_kernel<10> : kpre == 11 ? fir_f32_kernel<11>
-             : kpre == 12 ? fir_f32_kernel<12> : fir_f32_kernel<13>;
-      uint32_t ipw = MI355X_FIR_IPW;
-      if (!ipw) {
-        const uint32_t resident = (uint32_t)persistent_grid((const void*)k, kBlock, 0, items);
-        ipw = (items + resident - 1) / resident;
-      }
-      hipLaunchKernelGGL(k, dim3((items + ipw - 1) / ipw), dim3(kBlock), 0, st, (const float*)coeffs, T_,
-                         (const float*)src, (float*)dst, B, (const float*)hist_in, nchunks, items, ipw);
+      fir_f32_pass((const float*)coeffs, T_, (const float*)src, (float*)dst, B, batch, (const float*)hist_in,
+                   FirOut{1u, 1u, 1u, 0u, (uint64_t)B}, st);
       break;
     }
     case kFirQ15:
@@ -913,12 +938,17 @@ __global__ __launch_bounds__(kBlock) void fir_decimate_kernel(const typename MrT
   }
 }
 
-template <int OP>
-__global__ __launch_bounds__(kBlock) void fir_interpolate_kernel(const typename MrT<OP>::T* __restrict__ coeffs, int L,
-                                                                 int P, const typename MrT<OP>::T* __restrict__ src,
-                                                                 typename MrT<OP>::T* __restrict__ dst, uint32_t B,
-                                                                 const typename MrT<OP>::T* __restrict__ hist_in,
-                                                                 uint32_t nchunks, int N) {
+// Interpolator, LG phases per launch in registers: one input position n per lane, each window
+// word s[n + i] read once and applied to the LG phases' accumulators (i ascending per output),
+// phase coefficients h_q[i] = h[(L-1-q) + i L] pre-permuted into contiguous rows (wave-uniform
+// scalar loads), the LG outputs y[n L + q0 .. q0 + LG - 1] stored together.
+template <int OP, int LG>
+__global__ __launch_bounds__(kBlock) void fir_interp_phases_kernel(const typename MrT<OP>::T* __restrict__ hq, int L,
+                                                                   int q0, int P,
+                                                                   const typename MrT<OP>::T* __restrict__ src,
+                                                                   typename MrT<OP>::T* __restrict__ dst, uint32_t B,
+                                                                   const typename MrT<OP>::T* __restrict__ hist_in,
+                                                                   uint32_t nchunks, int N) {
   using Op = MrT<OP>;
   using E = typename Op::T;
   __shared__ E win[kMrWin];
@@ -929,23 +959,40 @@ __global__ __launch_bounds__(kBlock) void fir_interpolate_kernel(const typename 
   it.f = f; it.n0 = n0; it.count = cnt; it.total = cnt + P - 1;
   for (int idx = threadIdx.x; idx < it.total; idx += kBlock) win[idx] = fir_sample(hist_in, src, it, B, P - 1, idx);
   __syncthreads();
-  E* y = dst + ((uint64_t)f * B + n0) * (uint32_t)L;
+  E* y = dst + ((uint64_t)f * B + n0) * (uint32_t)L + q0;
+  const E* h = hq + (size_t)q0 * P;
   for (int nl = threadIdx.x; nl < cnt; nl += kBlock) {
     const E* w = win + nl;
-    for (int q = 0; q < L; ++q) {
-      const E* h = coeffs + (L - 1 - q);
-      typename Op::Acc acc = 0;
-      int i = 0;
-      for (; i + 4 <= P; i += 4) {
-        acc = Op::mac(acc, w[i], h[i * L]);
-        acc = Op::mac(acc, w[i + 1], h[(i + 1) * L]);
-        acc = Op::mac(acc, w[i + 2], h[(i + 2) * L]);
-        acc = Op::mac(acc, w[i + 3], h[(i + 3) * L]);
+    typename Op::Acc acc[LG];
+#pragma unroll
+    for (int q = 0; q < LG; ++q) acc[q] = 0;
+    int i = 0;
+    for (; i + 4 <= P; i += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const E x = w[i + u];
+#pragma unroll
+        for (int q = 0; q < LG; ++q) acc[q] = Op::mac(acc[q], x, h[q * P + i + u]);
       }
-      for (; i < P; ++i) acc = Op::mac(acc, w[i], h[i * L]);
-      y[(uint64_t)nl * L + q] = Op::out(acc);
     }
+    for (; i < P; ++i) {
+      const E x = w[i];
+#pragma unroll
+      for (int q = 0; q < LG; ++q) acc[q] = Op::mac(acc[q], x, h[q * P + i]);
+    }
+    E* o = y + (uint64_t)nl * L;
+#pragma unroll
+    for (int q = 0; q < LG; ++q) o[q] = Op::out(acc[q]);
   }
+}
+
+// h_q[i] = h[(L-1-q) + i L]: the interpolator's phases as contiguous coefficient rows
+template <typename E>
+__global__ void mr_phase_coeffs_kernel(const E* __restrict__ h, E* __restrict__ hq, int L, int P) {
+  const int g = blockIdx.x * kBlock + threadIdx.x;
+  if (g >= L * P) return;
+  const int q = g / P, i = g - q * P;
+  hq[g] = h[(L - 1 - q) + i * L];
 }
 
 // Shared host part: history copy when the new history depends on the old one (the pass reads
@@ -1003,9 +1050,22 @@ static hipError_t decimate_launch(const void* coeffs, int T, int M, const void* 
   const uint32_t nchunks = outs > 0 ? (uint32_t)((outs + J - 1) / J) : 0;
   const uint64_t blocks = (uint64_t)nchunks * batch;
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  // f32 with M <= 4 and T within the FIR window: the register-window FIR pass over every
+  // input position, storing the outputs with n % M == 0 (M x the MACs at the FIR kernel's
+  // issue efficiency beats the one-output-per-lane kernel up to M = 4: tools/bench_filters.py)
+  const bool via_fir = OP == kMrF32 && M <= 4 && B % (uint32_t)M == 0 && T <= kFirMaxTaps &&
+                       (uint64_t)((B + kF32Chunk - 1) / kF32Chunk) * batch <= 0xFFFFFFFFull;
   return mr_launch<E>((const E*)src, (E*)dst, (size_t)batch * outs, B, batch, (E*)hist, T - 1, (uint32_t)(outs * M),
                       st, [&](const E* s, const E* h) {
                         if (blocks == 0) return hipSuccess;
+                        if constexpr (OP == kMrF32) {
+                          if (via_fir) {
+                            fir_f32_pass((const float*)coeffs, T, (const float*)s, (float*)dst, B, batch,
+                                         (const float*)h,
+                                         FirOut{0u, (uint32_t)M, 1u, 0u, (uint64_t)outs}, st);
+                            return hipSuccess;
+                          }
+                        }
                         hipLaunchKernelGGL(fir_decimate_kernel<OP>, dim3((uint32_t)blocks), dim3(kBlock), 0, st,
                                            (const E*)coeffs, T, M, s, (E*)dst, B, h, nchunks, J, Wp);
                         return hipSuccess;
@@ -1025,8 +1085,22 @@ static hipError_t interpolate_launch(const void* coeffs, int L, int P, const voi
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
   return mr_launch<E>((const E*)src, (E*)dst, (size_t)batch * B * L, B, batch, (E*)hist, P - 1, B, st,
                       [&](const E* s, const E* h) {
-                        hipLaunchKernelGGL(fir_interpolate_kernel<OP>, dim3((uint32_t)blocks), dim3(kBlock), 0, st,
-                                           (const E*)coeffs, L, P, s, (E*)dst, B, h, nchunks, N);
+                        E* hq = nullptr;
+                        hipError_t e = hipMallocAsync((void**)&hq, sizeof(E) * (size_t)L * P, st);
+                        if (e != hipSuccess) return e;
+                        const uint32_t nq = (uint32_t)L * P;
+                        hipLaunchKernelGGL(mr_phase_coeffs_kernel<E>, dim3((nq + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                                           st, (const E*)coeffs, hq, L, P);
+                        for (int q0 = 0; q0 < L; q0 += 8) {
+                          const int lg = L - q0 < 8 ? L - q0 : 8;
+                          auto k = lg == 1 ? fir_interp_phases_kernel<OP, 1> : lg == 2 ? fir_interp_phases_kernel<OP, 2>
+                                 : lg == 3 ? fir_interp_phases_kernel<OP, 3> : lg == 4 ? fir_interp_phases_kernel<OP, 4>
+                                 : lg == 5 ? fir_interp_phases_kernel<OP, 5> : lg == 6 ? fir_interp_phases_kernel<OP, 6>
+                                 : lg == 7 ? fir_interp_phases_kernel<OP, 7> : fir_interp_phases_kernel<OP, 8>;
+                          hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(kBlock), 0, st, (const E*)hq, L, q0, P, s,
+                                             (E*)dst, B, h, nchunks, N);
+                        }
+                        (void)hipFreeAsync(hq, st);
                         return hipSuccess;
                       });
 }
