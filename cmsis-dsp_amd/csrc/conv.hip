@@ -192,10 +192,39 @@ static hipError_t launch_direct(const ConvJob& j, uint32_t first, uint32_t num, 
   return hipGetLastError();
 }
 
+// c[t] = h[B-1-t] per item row (the convolution's taps in the FIR's order)
+__global__ void reverse_rows_kernel(const float* __restrict__ h, uint64_t sh, float* __restrict__ c, uint32_t B,
+                                    uint32_t rows) {
+  const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (g >= (uint64_t)rows * B) return;
+  const uint64_t r = g / B, t = g - r * B;
+  c[g] = h[r * sh + (B - 1 - t)];
+}
+
 template <int OP, bool CORR>
 static hipError_t launch_window(const ConvJob& j, uint32_t first, uint32_t num, hipStream_t st) {
   using T = typename ConvT<OP>::T;
   if (num == 0) return hipSuccess;
+  if constexpr (OP == kConvF32) {
+    // f32: the FIR kernel's register-window pass (fir.hip), taps in ascending index of x
+    const float* c = (const float*)j.h;
+    uint64_t cs = j.sh;
+    float* rev = nullptr;
+    if (!CORR) {
+      const uint32_t rows = j.sh ? j.batch : 1u;
+      hipError_t e = hipMallocAsync((void**)&rev, sizeof(float) * (size_t)rows * j.B, st);
+      if (e != hipSuccess) return e;
+      const uint64_t n = (uint64_t)rows * j.B;
+      hipLaunchKernelGGL(reverse_rows_kernel, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                         (const float*)j.h, j.sh, rev, j.B, rows);
+      c = rev;
+      cs = j.sh ? j.B : 0;
+    }
+    hipError_t e = fir_f32_conv_pass(c, cs, (int)j.B, (const float*)j.x, j.sx, j.A, first, (float*)j.y, j.sy,
+                                     j.yoff + (int64_t)j.ydir * first, j.ydir, num, j.batch, st);
+    if (rev) (void)hipFreeAsync(rev, st);
+    return e;
+  }
   const uint64_t nchunks = ((uint64_t)num + kConvChunk - 1) / kConvChunk;
   if (nchunks * j.batch > 0x7FFFFFFFull) return hipErrorInvalidValue;
   hipLaunchKernelGGL((conv_kernel<OP, CORR>), dim3((uint32_t)(nchunks * j.batch)), dim3(kBlock), 0, st,

@@ -130,12 +130,25 @@ struct F32Win {
   int x[KPRE];
   int h[KPRE - 8];
 };
+// Input addressing of fir_f32_kernel: filter f reads block samples from src + f * stride, of
+// which the first len are valid (beyond, and before 0, reads return 0), shifted by so (window
+// sample j of the chunk at n0 is block sample n0 - T1 + j + so), with the history (T1 words at
+// hist_in + f * T1) in front when hist != 0; coefficients at coeffs + f * cstride.
+//   FIR / multirate: {B, B, 0, 1, 0};  convolution family: x rows, so = first output, no history.
+struct FirIn {
+  uint64_t stride;
+  uint32_t len;
+  int so;
+  uint32_t hist;
+  uint64_t cstride;
+};
 template <int KPRE>
 __device__ __forceinline__ void fir_f32_fetch(F32Win<KPRE>& w, const FirItem& it, const float* __restrict__ src,
-                                              const float* __restrict__ hist_in, uint32_t B, int T1, int tid) {
-  const __amdgpu_buffer_rsrc_t r = buf_rsrc(src + (uint64_t)it.f * B, (uint32_t)(it.n0 + it.count) * 4u);
-  const __amdgpu_buffer_rsrc_t rh = buf_rsrc(hist_in + (uint64_t)it.f * T1, (uint32_t)T1 * 4u);
-  const int v0 = (tid + it.n0 - T1) * 4, h0 = (tid + it.n0) * 4;
+                                              const float* __restrict__ hist_in, const FirIn& in, int T1, int tid) {
+  const __amdgpu_buffer_rsrc_t r = buf_rsrc(src + it.f * in.stride, in.len * 4u);
+  const __amdgpu_buffer_rsrc_t rh = in.hist ? buf_rsrc(hist_in + (uint64_t)it.f * T1, (uint32_t)T1 * 4u)
+                                            : buf_rsrc(src, 0u);
+  const int v0 = (tid + it.n0 - T1 + in.so) * 4, h0 = (tid + it.n0) * 4;
 #pragma unroll
   for (int k = 0; k < KPRE; ++k) w.x[k] = __builtin_amdgcn_raw_buffer_load_b32(r, opaque(v0 + 1024 * k), 0, 0);
 #pragma unroll
@@ -161,11 +174,14 @@ __device__ __forceinline__ void fir_f32_put(float* wl, const F32Win<KPRE>& w) {
 #define MI355X_FIR_IPW 16
 #endif
 
-// Output lattice of fir_f32_kernel: plain (the FIR: y[f B + n]) or, for the multirate forms,
-// y[f per_filter + (n / M) L + q] for the outputs with n % M == 0 (decimator: L = 1, q = 0;
-// interpolator phase q: M = 1).
+// Output lattice of fir_f32_kernel: output n of filter f (n % M == 0 only) is stored at
+// y[f per_filter + off + dir ((n / M) L + q)]: the FIR {1, 1, 0, 1, 0, B}; the decimator
+// {M, 1, 0, 1, 0, B / M}; the convolution family {1, 1, 0, ydir, yoff + ydir first, sy}.
+// M = L = dir = 1 is a contiguous run (16-B stores when aligned).
 struct FirOut {
-  uint32_t plain, M, L, q;
+  uint32_t M, L, q;
+  int dir;
+  int64_t off;
   uint64_t per_filter;
 };
 
@@ -177,7 +193,7 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_F32_WAVES) void fir_f32_kernel(c
                                                          const float* __restrict__ src, float* __restrict__ dst,
                                                          uint32_t B, const float* __restrict__ hist_in,
                                                          uint32_t nchunks, uint32_t items, uint32_t ipw,
-                                                         FirOut fo) {
+                                                         FirIn in, FirOut fo) {
   constexpr int kWin = KPRE * kBlock;
   __shared__ __attribute__((aligned(16))) float win[wpos(kWin) + 16];
   const int T1 = T - 1;
@@ -190,7 +206,7 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_F32_WAVES) void fir_f32_kernel(c
   float* wl = win + wpos(tid);                      // wpos(tid + 256 k) = wpos(tid) + 320 k
   F32Win<KPRE> pre;
   FirItem cur = fir_item(i0, nchunks, B, T1, kF32Chunk);
-  fir_f32_fetch<KPRE>(pre, cur, src, hist_in, B, T1, tid);
+  fir_f32_fetch<KPRE>(pre, cur, src, hist_in, in, T1, tid);
   fir_f32_put<KPRE>(wl, pre);
   // Per item: barrier (window ready) -> next window's loads -> MACs -> barrier (window free)
   // -> next window to LDS -> output stores.  The window write waits only for loads that had a
@@ -199,7 +215,7 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_F32_WAVES) void fir_f32_kernel(c
     __syncthreads();
     const bool more = item + 1 < i1;
     const FirItem nxt = more ? fir_item(item + 1, nchunks, B, T1, kF32Chunk) : cur;
-    if (more) fir_f32_fetch<KPRE>(pre, nxt, src, hist_in, B, T1, tid);
+    if (more) fir_f32_fetch<KPRE>(pre, nxt, src, hist_in, in, T1, tid);
     float acc[8];
     if (base < cur.count) {
 #pragma unroll
@@ -211,7 +227,8 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_F32_WAVES) void fir_f32_kernel(c
       // wave-uniform: scalar loads (s_load_dwordx8 per round) into SGPRs, the v_mul operand
       // (no VGPRs, no LDS reads).
       const float* wp = win + 10 * tid;
-      const float* cp = coeffs;
+      const float* const ci = coeffs + cur.f * in.cstride;
+      const float* cp = ci;
       ld_grp(X0, wp, 0);
       ld_grp(X1, wp, 1);
       int nb = rounds >> 2;
@@ -251,7 +268,7 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_F32_WAVES) void fir_f32_kernel(c
       }
       // numTaps % 8 tail taps, straight from LDS
       for (int k = 8 * rounds; k < T; ++k) {
-        const float c = coeffs[k];
+        const float c = ci[k];
 #pragma unroll
         for (int r = 0; r < 8; ++r) acc[r] = acc[r] + win[wpos(base + k + r)] * c;
       }
@@ -260,22 +277,26 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_F32_WAVES) void fir_f32_kernel(c
       __syncthreads();                              // every wave is done reading this window
       fir_f32_put<KPRE>(wl, pre);
     }
-    if (base < cur.count && !fo.plain) {             // decimator / interpolator phase
+    if (base < cur.count) {
+      const bool run = fo.M == 1 && fo.L == 1 && fo.dir == 1;
+      if (run) {                                    // contiguous outputs
+        float* o = dst + cur.f * fo.per_filter + fo.off + cur.n0 + base;
+        if (((fo.per_filter | (uint64_t)fo.off) & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + 8 <= cur.count) {
+          reinterpret_cast<float4*>(o)[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+          reinterpret_cast<float4*>(o)[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+        } else {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const uint32_t n = (uint32_t)(cur.n0 + base + r);
-        if (base + r < cur.count && n % fo.M == 0)
-          dst[(uint64_t)cur.f * fo.per_filter + (uint64_t)(n / fo.M) * fo.L + fo.q] = acc[r];
-      }
-    } else if (base < cur.count) {
-      float* o = dst + (uint64_t)cur.f * B + cur.n0 + base;
-      if ((B & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + 8 <= cur.count) {
-        reinterpret_cast<float4*>(o)[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-        reinterpret_cast<float4*>(o)[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
-      } else {
+          for (int r = 0; r < 8; ++r)
+            if (base + r < cur.count) o[r] = acc[r];
+        }
+      } else {                                      // decimator / reversed runs
 #pragma unroll
-        for (int r = 0; r < 8; ++r)
-          if (base + r < cur.count) o[r] = acc[r];
+        for (int r = 0; r < 8; ++r) {
+          const uint32_t n = (uint32_t)(cur.n0 + base + r);
+          if (base + r < cur.count && n % fo.M == 0)
+            dst[(int64_t)(cur.f * fo.per_filter) + fo.off + (int64_t)fo.dir * ((int64_t)(n / fo.M) * fo.L + fo.q)] =
+                acc[r];
+        }
       }
     }
     if (!more) break;
@@ -742,7 +763,7 @@ __global__ void fir_hist_kernel(const T* __restrict__ src, T* __restrict__ hist,
 
 // One f32 FIR pass over `batch` filters (T <= kFirMaxTaps), outputs on the lattice `fo`.
 static void fir_f32_pass(const float* coeffs, int T, const float* src, float* dst, uint32_t B, uint32_t batch,
-                         const float* hist_in, FirOut fo, hipStream_t st) {
+                         const float* hist_in, FirIn in, FirOut fo, hipStream_t st) {
   const uint32_t nchunks = (B + kF32Chunk - 1) / kF32Chunk;
   const uint32_t items = nchunks * batch;
   const int kpre = fir_f32_kpre(T);
@@ -754,7 +775,21 @@ static void fir_f32_pass(const float* coeffs, int T, const float* src, float* ds
     ipw = (items + resident - 1) / resident;
   }
   hipLaunchKernelGGL(k, dim3((items + ipw - 1) / ipw), dim3(kBlock), 0, st, coeffs, T, src, dst, B, hist_in, nchunks,
-                     items, ipw, fo);
+                     items, ipw, in, fo);
+}
+
+// The f32 convolution family's windowed outputs as one FIR pass (conv.hip): taps c (row
+// stride cstride), x rows of A samples (stride sx), outputs n = first .. first + num - 1 of
+// v[n] = sum_t w[n + t] c[t], w[j] = x[j - (T-1)], stored at y[item sy + off + dir (n - first)].
+hipError_t fir_f32_conv_pass(const float* c, uint64_t cstride, int T, const float* x, uint64_t sx, uint32_t A,
+                             uint32_t first, float* y, uint64_t sy, int64_t off, int dir, uint32_t num, uint32_t batch,
+                             hipStream_t st) {
+  if (num == 0 || batch == 0) return hipSuccess;
+  if (T < 1 || T > kFirMaxTaps || (uint64_t)((num + kF32Chunk - 1) / kF32Chunk) * batch > 0xFFFFFFFFull)
+    return hipErrorInvalidValue;
+  fir_f32_pass(c, T, x, y, num, batch, nullptr, FirIn{sx, A, (int)first, 0u, cstride},
+               FirOut{1u, 1u, 0u, dir, off, sy}, st);
+  return hipGetLastError();
 }
 
 template <typename T>
@@ -797,7 +832,7 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
   switch (kind) {
     case kFirF32: {
       fir_f32_pass((const float*)coeffs, T_, (const float*)src, (float*)dst, B, batch, (const float*)hist_in,
-                   FirOut{1u, 1u, 1u, 0u, (uint64_t)B}, st);
+                   FirIn{B, B, 0, 1u, 0}, FirOut{1u, 1u, 0u, 1, 0, (uint64_t)B}, st);
       break;
     }
     case kFirQ15:
@@ -1061,8 +1096,8 @@ static hipError_t decimate_launch(const void* coeffs, int T, int M, const void* 
                         if constexpr (OP == kMrF32) {
                           if (via_fir) {
                             fir_f32_pass((const float*)coeffs, T, (const float*)s, (float*)dst, B, batch,
-                                         (const float*)h,
-                                         FirOut{0u, (uint32_t)M, 1u, 0u, (uint64_t)outs}, st);
+                                         (const float*)h, FirIn{B, B, 0, 1u, 0},
+                                         FirOut{(uint32_t)M, 1u, 0u, 1, 0, (uint64_t)outs}, st);
                             return hipSuccess;
                           }
                         }

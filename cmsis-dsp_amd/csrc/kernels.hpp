@@ -112,6 +112,11 @@ struct ConvJob {
   uint32_t first, num, batch;
 };
 hipError_t conv_family_run(const ConvJob& job, hipStream_t st);
+// f32 windowed outputs through the FIR kernel (fir.hip): v[n] = sum_t w[n + t] c[t],
+// w[j] = x[j - (T-1)], n = first .. first + num - 1, stored at y[item sy + off + dir (n - first)].
+hipError_t fir_f32_conv_pass(const float* c, uint64_t cstride, int T, const float* x, uint64_t sx, uint32_t A,
+                             uint32_t first, float* y, uint64_t sy, int64_t off, int dir, uint32_t num, uint32_t batch,
+                             hipStream_t st);
 
 // Row-major q15 / q31 C[b] = A[b] * B[b] (arm_mat_mult_q15 / _q31 semantics, bit-exact):
 // byte-sliced planes on the i8 matrix cores (mat_mult_fixed.hip).
