@@ -144,6 +144,104 @@ __global__ __launch_bounds__(kBlock) void rfft_fused_kernel(const float2* src, f
   }
 }
 
+// ============================================================================================
+// Forward N = 1024 specialist (inner CFFT H = 512 = 8^3: arm_radix8_butterfly_f32 with modifier
+// 1, then the base-8 digit reversal, then stage_rfft_f32): one wave per transform, as
+// cfft_f32_n1024_kernel (cfft_f32.hip) with one 512-point half.  Lane l loads x[l + 64m]
+// (512 B per load instruction) and runs radix-8 stage 0 (butterfly j = l) in registers;
+// stage 1 through LDS (butterfly (l >> 3, j = l & 7)); stage 2 on elements 8l + m, whose
+// output m is bin 64m + 8(l & 7) + (l >> 3): stored to p per m as a permutation of 64
+// consecutive bins and written to LDS in natural order; the split then reads bins k and
+// H - k for k = l + 64m and stores out[k] (512 B per store instruction).  LDS image: the
+// N = 1024 kernel's s1024 layout (blocks of 64 padded to 72, XOR-swizzled low bits: every
+// pattern above conflict free).  Twiddles are lane-constant (stage 0: 7, stage 1: 7, split: 8).
+// Mapping sweep (2^20 transforms, Gsamples/s): T consecutive transforms per wave x WPB waves per
+// workgroup: T1 433, T2 473, T4 460, T8 462, T2 x 4 waves 442; the generic fused kernel 441.
+#ifndef MI355X_RF1024_T
+#define MI355X_RF1024_T 2
+#endif
+#ifndef MI355X_RF1024_WPB
+#define MI355X_RF1024_WPB 8
+#endif
+constexpr int kRfT = MI355X_RF1024_T, kRfWpb = MI355X_RF1024_WPB;
+__device__ __forceinline__ int rf_s(int e) { return (e >> 6) * 72 + (((e >> 3) & 7) << 3) + ((e & 7) ^ ((e >> 3) & 7)); }
+__device__ __forceinline__ void rf_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+typedef float rf_v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void rf_st(float2* p, float2 v) {
+  __builtin_nontemporal_store(rf_v2f{v.x, v.y}, reinterpret_cast<rf_v2f*>(p));
+}
+
+__global__ __launch_bounds__(64 * kRfWpb) void rfft1024_fwd_kernel(float2* p, float2* __restrict__ out,
+                                                                   uint32_t batch, const float2* __restrict__ tw,
+                                                                   const float2* __restrict__ twr, int keep_p) {
+  __shared__ __attribute__((aligned(16))) float2 lds_all[kRfWpb][8 * 72];
+  const int l = threadIdx.x & 63;
+  float2* lds = lds_all[threadIdx.x >> 6];
+  const uint32_t wave = blockIdx.x * kRfWpb + (threadIdx.x >> 6);
+  const uint32_t t_begin = wave * kRfT, t_end = min(batch, t_begin + kRfT);
+  float2 w0[7], w1[7], ws[8];
+  const int j1 = l & 7;
+#pragma unroll
+  for (int m = 0; m < 7; ++m) { w0[m] = tw[(m + 1) * l]; w1[m] = tw[8 * (m + 1) * j1]; }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) ws[m] = twr[l + 64 * m];
+  const int kbin = 8 * (l & 7) + (l >> 3);            // stage-2 output m of lane l is bin kbin + 64 m
+  for (uint32_t t = t_begin; t < t_end; ++t) {
+    float2* X = p + (size_t)t * 512;
+    float2 a[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const rf_v2f v = __builtin_nontemporal_load(reinterpret_cast<const rf_v2f*>(&X[l + 64 * m]));
+      a[m] = make_float2(v.x, v.y);
+    }
+    r8_sel(a, w0, l != 0);                             // stage 0, arm_cfft_radix8_f32.c:152-174
+    rf_wave_sync();                                    // the previous transform's split reads are done
+#pragma unroll
+    for (int m = 0; m < 8; ++m) lds[rf_s(l + 64 * m)] = a[m];
+    rf_wave_sync();
+    {                                                  // stage 1
+      const int base = 64 * (l >> 3) + j1;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) a[m] = lds[rf_s(base + 8 * m)];
+      r8_sel(a, w1, j1 != 0);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) lds[rf_s(base + 8 * m)] = a[m];
+    }
+    rf_wave_sync();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) a[m] = lds[rf_s(8 * l + m)];
+    r8_core(a);                                        // stage 2 (no twiddles)
+    rf_wave_sync();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      lds[rf_s(kbin + 64 * m)] = a[m];                 // natural order for the split
+      if (keep_p) rf_st(&X[kbin + 64 * m], a[m]);      // the reference leaves the CFFT output in p
+    }
+    rf_wave_sync();
+    float2* Y = out + (size_t)t * 512;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {                      // stage_rfft_f32, arm_rfft_fast_f32.c:316-402
+      const int k = l + 64 * m;
+      float2 o;
+      if (k == 0) {
+        const float2 x0 = lds[rf_s(0)];
+        const float t1a = x0.x + x0.x, t1b = x0.y + x0.y;
+        o = make_float2(0.5f * (t1a + t1b), 0.5f * (t1a - t1b));
+      } else {
+        const float2 A = lds[rf_s(k)], B = lds[rf_s(512 - k)], w = ws[m];
+        const float t1a = B.x - A.x, t1b = B.y + A.y;
+        const float p0 = w.x * t1a, p1 = w.y * t1a, p2 = w.x * t1b, p3 = w.y * t1b;
+        o = make_float2(0.5f * (A.x + B.x + p0 + p3), 0.5f * (A.y - B.y + p1 - p2));
+      }
+      rf_st(&Y[k], o);
+    }
+  }
+}
+
 template <int H>
 static hipError_t launch_fused(bool inv, const float* p, float* pcopy, float* out, uint32_t batch, const float* tw,
                                const float* twr, hipStream_t st) {
@@ -155,9 +253,18 @@ static hipError_t launch_fused(bool inv, const float* p, float* pcopy, float* ou
   return hipGetLastError();
 }
 
+#ifndef MI355X_RF1024
+#define MI355X_RF1024 1
+#endif
 hipError_t rfft_f32_fused_launch(int n_real, bool inverse, const float* p, float* pcopy, float* out, uint32_t batch,
                                  const float* tw, const float* tw_rfft, hipStream_t st) {
   if (batch == 0) return hipSuccess;
+  if (MI355X_RF1024 && n_real == 1024 && !inverse && (!pcopy || pcopy == p)) {
+    const int per_block = kRfT * kRfWpb;
+    hipLaunchKernelGGL(rfft1024_fwd_kernel, dim3((batch + per_block - 1) / per_block), dim3(64 * kRfWpb), 0, st,
+                       (float2*)p, (float2*)out, batch, (const float2*)tw, (const float2*)tw_rfft, pcopy ? 1 : 0);
+    return hipGetLastError();
+  }
   switch (n_real) {
 #define MI_RF(N) case N: return launch_fused<N / 2>(inverse, p, pcopy, out, batch, tw, tw_rfft, st);
     MI_RF(32) MI_RF(64) MI_RF(128) MI_RF(256) MI_RF(512) MI_RF(1024) MI_RF(2048) MI_RF(4096)
