@@ -420,6 +420,81 @@ __global__ __launch_bounds__(256, MI355X_N4096_WAVES) void cfft_f32_n4096_kernel
 #endif
 
 // ============================================================================================
+// N = 512 specialist (arm_cfft_f32.c:1270: arm_radix8_butterfly_f32 with modifier 1, 512 = 8^3,
+// then the base-8 digit reversal): one wave per transform, the N = 1024 kernel's structure for
+// one 512-point half.  Lane l loads x[l + 64m] and runs stage 0 (butterfly j = l) in
+// registers; stage 1 through LDS (butterfly (l >> 3, j = l & 7)); stage 2 on elements
+// 8l + m, whose output m is bin 64m + 8(l & 7) + (l >> 3): with bitReverseFlag each store
+// instruction writes a permutation of 64 consecutive bins (512 B), without it the lane's 8
+// consecutive elements (two 16-B stores).  LDS image: s1024 (conflict free for these patterns).
+#ifndef MI355X_N512_T
+#define MI355X_N512_T 2
+#endif
+#ifndef MI355X_N512_WPB
+#define MI355X_N512_WPB 8
+#endif
+#ifndef MI355X_F32_N512
+#define MI355X_F32_N512 1
+#endif
+constexpr int kN512T = MI355X_N512_T, kN512Wpb = MI355X_N512_WPB;
+template <bool IFFT, bool BREV>
+__global__ __launch_bounds__(64 * kN512Wpb) void cfft_f32_n512_kernel(float2* __restrict__ data, uint32_t batch,
+                                                                     const float2* __restrict__ tw) {
+  __shared__ __attribute__((aligned(16))) float2 lds_all[kN512Wpb][8 * 72];
+  const int l = threadIdx.x & 63;
+  float2* lds = lds_all[threadIdx.x >> 6];
+  const uint32_t wave = blockIdx.x * kN512Wpb + (threadIdx.x >> 6);
+  const uint32_t t_begin = wave * kN512T, t_end = min(batch, t_begin + kN512T);
+  const float invL = 1.0f / 512.0f;
+  float2 w0[7], w1[7];
+  const int j1 = l & 7;
+#pragma unroll
+  for (int m = 0; m < 7; ++m) { w0[m] = tw[(m + 1) * l]; w1[m] = tw[8 * (m + 1) * j1]; }
+  const int kbin = 8 * (l & 7) + (l >> 3);
+  for (uint32_t t = t_begin; t < t_end; ++t) {
+    float2* X = data + (size_t)t * 512;
+    float2 a[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      a[m] = ldnt(&X[l + 64 * m]);
+      if (IFFT) a[m].y = -a[m].y;                      // arm_cfft_f32.c:1252-1261
+    }
+    r8_sel(a, w0, l != 0);
+    wave_sync();                                       // the previous transform's stage-2 reads are done
+#pragma unroll
+    for (int m = 0; m < 8; ++m) lds[s1024(l + 64 * m)] = a[m];
+    wave_sync();
+    {
+      const int base = 64 * (l >> 3) + j1;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) a[m] = lds[s1024(base + 8 * m)];
+      r8_sel(a, w1, j1 != 0);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) lds[s1024(base + 8 * m)] = a[m];
+    }
+    wave_sync();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) a[m] = lds[s1024(8 * l + m)];
+    r8_core(a);
+    if (IFFT) {                                        // arm_cfft_f32.c:1285-1297
+#pragma unroll
+      for (int m = 0; m < 8; ++m) a[m] = make_float2(a[m].x * invL, -a[m].y * invL);
+    }
+    if (BREV) {
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const v2f o = {a[m].x, a[m].y};
+        __builtin_nontemporal_store(o, reinterpret_cast<v2f*>(&X[kbin + 64 * m]));
+      }
+    } else {
+      float4* Y = reinterpret_cast<float4*>(X + 8 * l);
+#pragma unroll
+      for (int m = 0; m < 8; m += 2) stnt(&Y[m >> 1], make_float4(a[m].x, a[m].y, a[m + 1].x, a[m + 1].y));
+    }
+  }
+}
+
+// ============================================================================================
 // N = 2048 specialist.  Reference: arm_cfft_radix8by4_f32 (arm_cfft_f32.c:992-1188; rows
 // k <= N/8 "top", the others "bottom" with the mirrored twiddle index i = N/4 - k), then
 // 3 radix-8 stages on each 512-point quarter (modifier 4: strides 64, 8, 1), then the
@@ -592,7 +667,16 @@ hipError_t cfft_f32_launch(int n, float* data, uint32_t batch, const float* tw, 
     case 64:   return launch_f32<64>(d, batch, w, perm, flags, st);
     case 128:  return launch_f32<128>(d, batch, w, perm, flags, st);
     case 256:  return launch_f32<256>(d, batch, w, perm, flags, st);
-    case 512:  return launch_f32<512>(d, batch, w, perm, flags, st);
+    case 512:
+      if (!perm && MI355X_F32_N512) {   // the reference's own table: the specialist kernel
+        const bool inv = flags & kIfft, brev = flags & kBitrev;
+        auto k = inv ? (brev ? cfft_f32_n512_kernel<true, true> : cfft_f32_n512_kernel<true, false>)
+                     : (brev ? cfft_f32_n512_kernel<false, true> : cfft_f32_n512_kernel<false, false>);
+        const int per_block = kN512T * kN512Wpb;
+        hipLaunchKernelGGL(k, dim3((batch + per_block - 1) / per_block), dim3(64 * kN512Wpb), 0, st, d, batch, w);
+        return hipGetLastError();
+      }
+      return launch_f32<512>(d, batch, w, perm, flags, st);
     case 1024:
       if (!perm) {   // the reference's own table (or no reversal): the specialist kernel
         const int per_block = (kN1024T ? kN1024T : 1) * kN1024Wpb;
