@@ -12,9 +12,10 @@ SPECS = {
                                "fx4096", ""),
     "cfft_q15_4096_strong1M": ("--workload cfft_q15_4096 --scaling strong --global-batch 1048576 --steps 6 --warmup 2",
                                "q15_4096_pk", ""),
+    "cfft_f32_512": ("--fftlen 512 --no-config3 --steps 10 --warmup 3", "n512", ""),
     "cfft_f32_2048": ("--fftlen 2048 --no-config3 --steps 10 --warmup 3", "n2048", ""),
     "cfft_f32_4096": ("--fftlen 4096 --no-config3 --steps 10 --warmup 3", "n4096", ""),
-    "rfft_f32": ("--workload rfft_f32 --steps 10 --warmup 3", "rfft_fused", ""),
+    "rfft_f32": ("--workload rfft_f32 --steps 10 --warmup 3", "rfft1024_fwd", ""),
     "rfft_q31": ("--workload rfft_q31 --steps 10 --warmup 3", "fx4096", ""),
     "rfft_q15": ("--workload rfft_q15 --steps 10 --warmup 3", "q15_4096_pk", ""),
     "fir_f32": ("--workload fir_f32 --steps 10 --warmup 3", "fir_f32_kernel", ""),
@@ -22,7 +23,7 @@ SPECS = {
     "fir_q31": ("--workload fir_q31 --steps 10 --warmup 3", "fir_q31_kernel", ""),
     "fir_fast_q15": ("--workload fir_fast_q15 --steps 10 --warmup 3", "fir_q15_kernel", ""),
     "fir_fast_q31": ("--workload fir_fast_q31 --steps 10 --warmup 3", "fir_q31_kernel", ""),
-    "conv_f32": ("--workload conv_f32 --steps 10 --warmup 3", "conv_kernel", ""),
+    "conv_f32": ("--workload conv_f32 --steps 10 --warmup 3", "fir_f32_kernel", ""),
     "mfcc_f32": ("--workload mfcc_f32 --steps 10 --warmup 3", "mfcc_fused", ""),
     "mat_mult_f32": ("--workload mat_mult_f32 --steps 6 --warmup 2", "mat_mult_f32_full", ""),
     "mat_mult_q15": ("--workload mat_mult_q15 --steps 6 --warmup 2", "mat_mult_i8v2", ""),
