@@ -32,6 +32,12 @@ namespace mi355x {
 #ifndef MI355X_FXR_T
 #define MI355X_FXR_T 8
 #endif
+// MI355X_FXR_SMALL = 1: N = 32 / 64 / 128 on this kernel as well (bit-exact, but with 2-8
+// threads per transform each load instruction scatters over 32-8 transforms: q31 32/64/128
+// 42 / 201 / 254 Gsamples/s against 342 / 334 / 324 for the generic kernel; off).
+#ifndef MI355X_FXR_SMALL
+#define MI355X_FXR_SMALL 0
+#endif
 
 template <int N> struct R16 {
   static constexpr int LOG = Log2<N>::v;
@@ -52,6 +58,12 @@ template <int N> struct R16 {
 __device__ __forceinline__ constexpr int pow4(int s) { return 1 << (2 * s); }
 
 template <int N, bool Q31> struct R16Pad;   // tools/fx_r16_plan.py
+template <> struct R16Pad<32, true>    { static constexpr int k1 = 3, c1 = 0, k2 = 4, c2 = 1, stride = 34; };
+template <> struct R16Pad<32, false>   { static constexpr int k1 = 3, c1 = 0, k2 = 4, c2 = 1, stride = 34; };
+template <> struct R16Pad<64, true>    { static constexpr int k1 = 3, c1 = 0, k2 = 4, c2 = 1, stride = 68; };
+template <> struct R16Pad<64, false>   { static constexpr int k1 = 3, c1 = 0, k2 = 4, c2 = 1, stride = 68; };
+template <> struct R16Pad<128, true>   { static constexpr int k1 = 3, c1 = 0, k2 = 4, c2 = 1, stride = 136; };
+template <> struct R16Pad<128, false>  { static constexpr int k1 = 3, c1 = 0, k2 = 4, c2 = 1, stride = 136; };
 template <> struct R16Pad<256, true>   { static constexpr int k1 = 3, c1 = 0, k2 = 4, c2 = 1, stride = 271; };
 template <> struct R16Pad<256, false>  { static constexpr int k1 = 3, c1 = 0, k2 = 4, c2 = 1, stride = 272; };
 template <> struct R16Pad<512, true>   { static constexpr int k1 = 3, c1 = 0, k2 = 5, c2 = 1, stride = 527; };
@@ -333,6 +345,11 @@ static void launch_r16(void* data, uint32_t batch, const void* tw, uint32_t flag
 template <typename T>
 static bool dispatch_r16(int n, void* data, uint32_t batch, const void* tw, uint32_t flags, hipStream_t st) {
   switch (n) {
+#if MI355X_FXR_SMALL
+    case 32:   launch_r16<T, 32>(data, batch, tw, flags, st); return true;
+    case 64:   launch_r16<T, 64>(data, batch, tw, flags, st); return true;
+    case 128:  launch_r16<T, 128>(data, batch, tw, flags, st); return true;
+#endif
     case 256:  launch_r16<T, 256>(data, batch, tw, flags, st); return true;
     case 512:  launch_r16<T, 512>(data, batch, tw, flags, st); return true;
     case 1024: launch_r16<T, 1024>(data, batch, tw, flags, st); return true;
