@@ -962,11 +962,20 @@ __global__ __launch_bounds__(kBlock) void fir_decimate_kernel(const typename MrT
       for (int i = 0; t < T; ++i, ++w)
         for (int p = 0; p < M && t < T; ++p, ++t) acc = Op::mac(acc, w[p * Wp], coeffs[t]);
     } else {
-      // order-free sums: phase by phase, taps t = i M + p
+      // order-free sums: phase by phase over the pre-permuted phase rows hp[p I + i] =
+      // h[i M + p] (zero past numTaps), I = ceil(T / M): contiguous wave-uniform taps
+      const int I = (T + M - 1) / M;
       for (int p = 0; p < M && p < T; ++p) {
         const E* w = win + p * Wp + jl;
-        const int ni = (T - p + M - 1) / M;
-        for (int i = 0; i < ni; ++i) acc = Op::mac(acc, w[i], coeffs[i * M + p]);
+        const E* hp = coeffs + p * I;
+        int i = 0;
+        for (; i + 4 <= I; i += 4) {
+          acc = Op::mac(acc, w[i], hp[i]);
+          acc = Op::mac(acc, w[i + 1], hp[i + 1]);
+          acc = Op::mac(acc, w[i + 2], hp[i + 2]);
+          acc = Op::mac(acc, w[i + 3], hp[i + 3]);
+        }
+        for (; i < I; ++i) acc = Op::mac(acc, w[i], hp[i]);
       }
     }
     y[jl] = Op::out(acc);
@@ -1070,6 +1079,15 @@ static hipError_t mr_launch(const E* src, E* dst, size_t out_words, uint32_t B, 
   return e;
 }
 
+// hp[p I + i] = h[i M + p] (0 past numTaps): the decimator's taps as M contiguous phase rows
+template <typename E>
+__global__ void mr_decim_rows_kernel(const E* __restrict__ h, E* __restrict__ hp, int T, int M, int I) {
+  const int g = blockIdx.x * kBlock + threadIdx.x;
+  if (g >= M * I) return;
+  const int p = g / I, i = g - p * I, t = i * M + p;
+  hp[g] = t < T ? h[t] : (E)0;
+}
+
 template <int OP>
 static hipError_t decimate_launch(const void* coeffs, int T, int M, const void* src, void* dst, uint32_t B,
                                   uint32_t batch, void* hist, hipStream_t st) {
@@ -1101,8 +1119,19 @@ static hipError_t decimate_launch(const void* coeffs, int T, int M, const void* 
                             return hipSuccess;
                           }
                         }
+                        E* hp = nullptr;
+                        if constexpr (OP != kMrF32) {     // phase rows for the order-free sums
+                          const int I = (T + M - 1) / M;
+                          hipError_t e = hipMallocAsync((void**)&hp, sizeof(E) * (size_t)M * I, st);
+                          if (e != hipSuccess) return e;
+                          const uint32_t n = (uint32_t)(M * I);
+                          hipLaunchKernelGGL(mr_decim_rows_kernel<E>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                                             st, (const E*)coeffs, hp, T, M, I);
+                        }
                         hipLaunchKernelGGL(fir_decimate_kernel<OP>, dim3((uint32_t)blocks), dim3(kBlock), 0, st,
-                                           (const E*)coeffs, T, M, s, (E*)dst, B, h, nchunks, J, Wp);
+                                           hp ? (const E*)hp : (const E*)coeffs, T, M, s, (E*)dst, B, h, nchunks, J,
+                                           Wp);
+                        if (hp) (void)hipFreeAsync(hp, st);
                         return hipSuccess;
                       });
 }
