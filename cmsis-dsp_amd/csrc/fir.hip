@@ -953,32 +953,38 @@ __global__ __launch_bounds__(kBlock) void fir_decimate_kernel(const typename MrT
   }
   __syncthreads();
   E* y = dst + (uint64_t)f * outs + j0;
-  for (int jl = threadIdx.x; jl < cnt; jl += kBlock) {
-    typename Op::Acc acc = 0;
-    if constexpr (OP == kMrF32) {
+  if constexpr (OP == kMrF32) {
+    for (int jl = threadIdx.x; jl < cnt; jl += kBlock) {
       // t ascending: (i, p) = divmod(t, M), tap t reads X_p[jl + i]
+      typename Op::Acc acc = 0;
       const E* w = win + jl;
       int t = 0;
       for (int i = 0; t < T; ++i, ++w)
         for (int p = 0; p < M && t < T; ++p, ++t) acc = Op::mac(acc, w[p * Wp], coeffs[t]);
-    } else {
-      // order-free sums: phase by phase over the pre-permuted phase rows hp[p I + i] =
-      // h[i M + p] (zero past numTaps), I = ceil(T / M): contiguous wave-uniform taps
-      const int I = (T + M - 1) / M;
-      for (int p = 0; p < M && p < T; ++p) {
-        const E* w = win + p * Wp + jl;
-        const E* hp = coeffs + p * I;
-        int i = 0;
-        for (; i + 4 <= I; i += 4) {
-          acc = Op::mac(acc, w[i], hp[i]);
-          acc = Op::mac(acc, w[i + 1], hp[i + 1]);
-          acc = Op::mac(acc, w[i + 2], hp[i + 2]);
-          acc = Op::mac(acc, w[i + 3], hp[i + 3]);
-        }
-        for (; i < I; ++i) acc = Op::mac(acc, w[i], hp[i]);
-      }
+      y[jl] = Op::out(acc);
     }
-    y[jl] = Op::out(acc);
+  } else {
+    // order-free sums: phase by phase over the pre-permuted phase rows hp[p I + i] =
+    // h[i M + p] (zero past numTaps), I = ceil(T / M): contiguous wave-uniform taps, each
+    // applied to R = 4 outputs per lane (jl + 256 r) so one scalar-load wait covers 4R MACs
+    // (R = 1 and 2 measured slower for every op)
+    constexpr int R = 4;
+    const int I = (T + M - 1) / M;
+    for (int j0 = threadIdx.x; j0 < cnt; j0 += R * kBlock) {
+      typename Op::Acc acc[R] = {};
+      for (int p = 0; p < M && p < T; ++p) {
+        const E* w = win + p * Wp + j0;
+        const int32_t* hp = reinterpret_cast<const int32_t*>(coeffs) + p * I;   // dword rows
+        for (int i = 0; i < I; ++i) {
+          const E c = (E)hp[i];
+#pragma unroll
+          for (int r = 0; r < R; ++r) acc[r] = Op::mac(acc[r], w[i + r * kBlock], c);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (j0 + r * kBlock < cnt) y[j0 + r * kBlock] = Op::out(acc[r]);
+    }
   }
 }
 
@@ -1079,13 +1085,14 @@ static hipError_t mr_launch(const E* src, E* dst, size_t out_words, uint32_t B, 
   return e;
 }
 
-// hp[p I + i] = h[i M + p] (0 past numTaps): the decimator's taps as M contiguous phase rows
+// hp[p I + i] = h[i M + p] (0 past numTaps), widened to dwords: the decimator's taps as M
+// contiguous phase rows that scalar loads fetch four at a time
 template <typename E>
-__global__ void mr_decim_rows_kernel(const E* __restrict__ h, E* __restrict__ hp, int T, int M, int I) {
+__global__ void mr_decim_rows_kernel(const E* __restrict__ h, int32_t* __restrict__ hp, int T, int M, int I) {
   const int g = blockIdx.x * kBlock + threadIdx.x;
   if (g >= M * I) return;
   const int p = g / I, i = g - p * I, t = i * M + p;
-  hp[g] = t < T ? h[t] : (E)0;
+  hp[g] = t < T ? (int32_t)h[t] : 0;
 }
 
 template <int OP>
@@ -1119,10 +1126,10 @@ static hipError_t decimate_launch(const void* coeffs, int T, int M, const void* 
                             return hipSuccess;
                           }
                         }
-                        E* hp = nullptr;
+                        int32_t* hp = nullptr;
                         if constexpr (OP != kMrF32) {     // phase rows for the order-free sums
                           const int I = (T + M - 1) / M;
-                          hipError_t e = hipMallocAsync((void**)&hp, sizeof(E) * (size_t)M * I, st);
+                          hipError_t e = hipMallocAsync((void**)&hp, sizeof(int32_t) * (size_t)M * I, st);
                           if (e != hipSuccess) return e;
                           const uint32_t n = (uint32_t)(M * I);
                           hipLaunchKernelGGL(mr_decim_rows_kernel<E>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,

@@ -27,6 +27,7 @@ CASES = {
     "fir_decimate_f32_m4": ("decimate_f32", 4, "f32"),
     "fir_decimate_q15_m4": ("decimate_q15", 4, "q15"),
     "fir_decimate_fast_q31_m4": ("decimate_fast_q31", 4, "q31"),
+    "fir_decimate_q31_m4": ("decimate_q31", 4, "q31"),
     "fir_interpolate_f32_l4": ("interpolate_f32", 4, "f32"),
     "fir_interpolate_q31_l4": ("interpolate_q31", 4, "q31"),
 }
