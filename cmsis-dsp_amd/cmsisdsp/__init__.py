@@ -60,6 +60,8 @@ for _t in ("f32", "q31", "q15"):
                                                          _abi.arm_fir_decimate_instance)
     globals()[f"arm_fir_interpolate_instance_{_t}"] = _make(f"arm_fir_interpolate_instance_{_t}",
                                                             _abi.arm_fir_interpolate_instance)
+for _t in ("f32", "q31", "q15", "q7"):
+    globals()[f"arm_fir_sparse_instance_{_t}"] = _make(f"arm_fir_sparse_instance_{_t}", _abi.arm_fir_sparse_instance)
 del _t
 arm_rfft_instance_q31 = _make("arm_rfft_instance_q31", _abi.arm_rfft_instance_q31)
 arm_rfft_instance_q15 = _make("arm_rfft_instance_q15", _abi.arm_rfft_instance_q15)
@@ -248,6 +250,51 @@ for _k in ("f32", "q31", "q15"):
     globals()[f"arm_fir_interpolate_{_k}"] = _mr("interpolate", f"interpolate_{_k}", _k)
 arm_fir_decimate_fast_q15 = _mr("decimate", "decimate_fast_q15", "q15")
 arm_fir_decimate_fast_q31 = _mr("decimate", "decimate_fast_q31", "q31")
+del _k
+
+
+# cmsisdsp_filtering.c cmsis_arm_fir_sparse_init_* ("OhOOOh": S, numTaps, pCoeffs, pState,
+# pTapDelay, maxDelay; blockSize = len(pState) - len(pCoeffs) + 1, :6666-6690) and
+# cmsis_arm_fir_sparse_f32 ("OOO": S, pSrc, pScratchIn; returns len(pSrc) words, :6628-6662).
+# The module keeps its own state copy of at least maxDelay + blockSize words and refuses a
+# block that would not fit it (the C call would run past the caller's state).
+def _sparse_init(kind):
+    name = f"arm_fir_sparse_init_{kind}"
+
+    def init(inst, numTaps, pCoeffs, pState, pTapDelay, maxDelay):
+        c = _arr(pCoeffs, _DT[kind])
+        d = _arr(pTapDelay, _np.int32)
+        block = max(len(_np.asarray(pState)) - len(c) + 1, 0)
+        state = _np.zeros(max(len(_np.asarray(pState)), int(maxDelay) + block), dtype=_DT[kind])
+        inst._keep = [c, d, state]
+        getattr(_lib, name)(_C.byref(inst._s), int(numTaps), c.ctypes.data, state.ctypes.data, d.ctypes.data,
+                            int(maxDelay), block)
+        _check(name)
+    init.__name__ = name
+    return init
+
+
+def _sparse(kind):
+    name = f"arm_fir_sparse_{kind}"
+
+    def run(inst, pSrc, pScratchIn=None, pScratchOut=None):
+        x = _arr(pSrc, _DT[kind])
+        if inst._s.maxDelay + len(x) > len(inst._keep[2]):
+            raise ValueError(f"{name}: maxDelay + len(pSrc) exceeds the state given to the init call")
+        y = _np.zeros(len(x), dtype=_DT[kind])
+        if kind in ("q15", "q7"):
+            getattr(_lib, name)(_C.byref(inst._s), x.ctypes.data, y.ctypes.data, None, None, len(x))
+        else:
+            getattr(_lib, name)(_C.byref(inst._s), x.ctypes.data, y.ctypes.data, None, len(x))
+        _check(name)
+        return y
+    run.__name__ = name
+    return run
+
+
+for _k in ("f32", "q31", "q15", "q7"):
+    globals()[f"arm_fir_sparse_init_{_k}"] = _sparse_init(_k)
+    globals()[f"arm_fir_sparse_{_k}"] = _sparse(_k)
 del _k
 
 

@@ -65,6 +65,12 @@ class arm_fir_interpolate_instance(C.Structure):
     _fields_ = [("L", C.c_uint8), ("phaseLength", C.c_uint16), ("pCoeffs", C.c_void_p), ("pState", C.c_void_p)]
 
 
+# arm_fir_sparse_instance_{f32,q31,q15,q7} (filtering_functions.h:2033-2091), one layout
+class arm_fir_sparse_instance(C.Structure):
+    _fields_ = [("numTaps", C.c_uint16), ("stateIndex", C.c_uint16), ("pState", C.c_void_p), ("pCoeffs", C.c_void_p),
+                ("maxDelay", C.c_uint16), ("pTapDelay", C.c_void_p)]
+
+
 class arm_fir_instance_q15(C.Structure):
     # Include/dsp/filtering_functions.h:66-71
     _fields_ = [("numTaps", C.c_uint16), ("pState", c_i16p), ("pCoeffs", c_i16p)]
@@ -141,6 +147,12 @@ DROPIN = {
     **{f"arm_fir_{k}": (None, [P(arm_fir_interpolate_instance), C.c_void_p, C.c_void_p, C.c_uint32])
        for k in ("interpolate_f32", "interpolate_q15", "interpolate_q31")},
     "arm_fir_q7": (None, [P(arm_fir_instance_q7), C.c_void_p, C.c_void_p, C.c_uint32]),
+    **{f"arm_fir_sparse_init_{t}": (None, [P(arm_fir_sparse_instance), C.c_uint16, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_uint16, C.c_uint32]) for t in ("f32", "q31", "q15", "q7")},
+    **{f"arm_fir_sparse_{t}": (None, [P(arm_fir_sparse_instance), C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32])
+       for t in ("f32", "q31")},
+    **{f"arm_fir_sparse_{t}": (None, [P(arm_fir_sparse_instance), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_uint32]) for t in ("q15", "q7")},
     "arm_mat_init_f32": (None, [P(arm_matrix_instance_f32), C.c_uint16, C.c_uint16, C.c_void_p]),
     "arm_mat_init_q15": (None, [P(arm_matrix_instance_q15), C.c_uint16, C.c_uint16, C.c_void_p]),
     "arm_mat_init_q31": (None, [P(arm_matrix_instance_q31), C.c_uint16, C.c_uint16, C.c_void_p]),
@@ -218,6 +230,8 @@ BATCHED = {
     **{f"arm_fir_{k}_batch": (C.c_int, [P(arm_fir_interpolate_instance), C.c_void_p, C.c_void_p, C.c_uint32,
                                         C.c_uint32, C.c_void_p, C.c_void_p])
        for k in ("interpolate_f32", "interpolate_q15", "interpolate_q31")},
+    **{f"arm_fir_sparse_{t}_batch": (C.c_int, [P(arm_fir_sparse_instance), C.c_void_p, C.c_void_p, C.c_uint32,
+                                               C.c_uint32, C.c_void_p, C.c_void_p]) for t in ("f32", "q31", "q15", "q7")},
     "arm_mat_mult_f32_batch": (C.c_int, [P(arm_matrix_instance_f32), P(arm_matrix_instance_f32),
                                          P(arm_matrix_instance_f32), C.c_uint32, C.c_void_p]),
     "arm_mat_mult_q15_batch": (C.c_int, [P(arm_matrix_instance_q15), P(arm_matrix_instance_q15),

@@ -495,6 +495,101 @@ arm_status interpolate_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B
   return ARM_MATH_SUCCESS;
 }
 
+// ---- sparse FIR ---------------------------------------------------------------------------
+// Drop-in: the reference's circular state (L = maxDelay + blockSize words, host or device) gets
+// the block at stateIndex (arm_circularWrite_f32), then one kernel reads every tap straight from
+// it at the reference's read indices (arm_fir_sparse_f32.c); pScratchIn / pScratchOut are not
+// needed.  Host state + host input: the block is written into the caller's state on the host and
+// the state uploaded once (the kernel never modifies it).
+template <typename T, typename Inst>
+void sparse_init(Inst* S, uint16_t numTaps, const T* pCoeffs, T* pState, int32_t* pTapDelay, uint16_t maxDelay,
+                 uint32_t blockSize) {
+  if (!S) return;
+  S->numTaps = numTaps; S->pCoeffs = pCoeffs; S->pTapDelay = pTapDelay; S->maxDelay = maxDelay;
+  S->stateIndex = 0;                                                  // arm_fir_sparse_init_f32.c
+  if (pState) zero_words(pState, sizeof(T) * ((size_t)maxDelay + blockSize), "arm_fir_sparse_init");
+  S->pState = pState;
+}
+
+template <typename T, typename Inst>
+void sparse_sync(Inst* S, const T* pSrc, T* pDst, uint32_t B, int op, const char* what) {
+  if (!S || !S->pState || !S->pCoeffs || !S->pTapDelay || S->numTaps == 0 || B == 0) return;
+  const int taps = S->numTaps;
+  const uint32_t L = (uint32_t)S->maxDelay + B;
+  hipStream_t st = sync_stream();
+  bool ok = true, okd = true;
+  const T* dc = device_coeffs<T>(S->pCoeffs, taps, &ok);
+  const int32_t* dd = device_coeffs<int32_t>(S->pTapDelay, taps, &okd);
+  if (!ok || !okd) { set_error(hipErrorOutOfMemory, what); return; }
+  const bool dstate = is_device_ptr(S->pState), dsrc = is_device_ptr(pSrc), ddst = is_device_ptr(pDst);
+  // words moved: the circular length, or up to a stateIndex a larger earlier block left past it
+  const size_t es = sizeof(T), sb = es * B, lb = es * std::max<size_t>(L, (size_t)S->stateIndex + 1);
+  T* ds = dstate ? S->pState : (T*)scratch(lb + 16, 2);
+  // a device output overlapping the state would be read by later taps: write to scratch
+  const bool dalias = ddst && dstate && ranges_overlap(pDst, S->pState, lb > sb ? lb : sb);
+  T* dds = (ddst && !dalias) ? pDst : (T*)scratch(sb + 16, 4);
+  if (!ds || !dds) { set_error(hipErrorOutOfMemory, what); return; }
+  // arm_circularWrite_f32 position by position: sample i at w, then w + 1 wrapped once at L
+  // (a stateIndex left >= L by a larger earlier blockSize writes there first, as the reference
+  // does), as contiguous segments
+  auto circular_write = [&](auto&& copy) -> hipError_t {
+    int64_t w = S->stateIndex;
+    for (uint32_t i = 0; i < B;) {
+      const uint32_t n = w >= (int64_t)L ? 1u : (B - i < L - (uint32_t)w ? B - i : L - (uint32_t)w);
+      hipError_t e = copy((size_t)w, i, n);
+      if (e != hipSuccess) return e;
+      i += n;
+      w += n;
+      if (w >= (int64_t)L) w -= L;
+    }
+    S->stateIndex = (uint16_t)w;
+    return hipSuccess;
+  };
+  const uint16_t prev = S->stateIndex;
+  HostIO io(st);
+  hipError_t e = hipSuccess;
+  if (!dstate && !dsrc) {
+    e = circular_write([&](size_t w, uint32_t i, uint32_t n) {
+      memcpy(S->pState + w, pSrc + i, es * n);
+      return hipSuccess;
+    });
+    if (e == hipSuccess) e = io.in(ds, S->pState, lb);
+  } else {
+    if (!dstate) e = io.in(ds, S->pState, lb);
+    if (e == hipSuccess)
+      e = circular_write([&](size_t w, uint32_t i, uint32_t n) {
+        return dsrc ? hipMemcpyAsync(ds + w, pSrc + i, es * n, hipMemcpyDeviceToDevice, st) : io.in(ds + w, pSrc + i, es * n);
+      });
+  }
+  const uint16_t next = S->stateIndex;
+  S->stateIndex = prev;                                               // committed on success
+  const int r0 = (int32_t)((uint32_t)next - B);                       // arm_fir_sparse_f32.c readIndex
+  if (e == hipSuccess) e = fir_sparse_run(op, dc, dd, taps, S->maxDelay, ds, dds, B, 1, nullptr, (int)L, r0, st);
+  if (e == hipSuccess && dalias) e = hipMemcpyAsync(pDst, dds, sb, hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess && !ddst) e = io.out(pDst, dds, sb);
+  if (e == hipSuccess && !dstate && dsrc) e = io.out(S->pState, ds, lb);
+  if (e == hipSuccess) e = io.finish();
+  if (e != hipSuccess) { set_error(e, what); return; }
+  S->stateIndex = next;
+}
+
+// Batched: `batch` streams with linear histories d_hist[batch][maxDelay] (oldest first,
+// updated), delays in [0, maxDelay] (others read 0); stateIndex / pState are not used.
+template <typename T, typename Inst>
+arm_status sparse_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uint32_t batch, T* d_hist, void* stream,
+                        int op, const char* what) {
+  if (!S || !S->pCoeffs || !S->pTapDelay || S->numTaps == 0) return ARM_MATH_ARGUMENT_ERROR;
+  if (batch && B && (!d_src || !d_dst || (S->maxDelay > 0 && !d_hist))) return ARM_MATH_ARGUMENT_ERROR;
+  bool ok = true, okd = true;
+  const T* dc = device_coeffs<T>(S->pCoeffs, S->numTaps, &ok);
+  const int32_t* dd = device_coeffs<int32_t>(S->pTapDelay, S->numTaps, &okd);
+  if (!ok || !okd) { set_error(hipErrorOutOfMemory, what); return ARM_MATH_ARGUMENT_ERROR; }
+  hipError_t e = fir_sparse_run(op, dc, dd, S->numTaps, S->maxDelay, d_src, d_dst, B, batch, d_hist, 0, 0,
+                                (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(e, what); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
+}
+
 // ---- convolution / correlation family ------------------------------------------------
 // How each reference function maps onto one ConvJob (conv.hip):
 //   conv (exact):      x = pSrcA, h = pSrcB, all srcALen + srcBLen - 1 outputs forward;
@@ -1014,5 +1109,40 @@ MI355X_INTERP(arm_fir_interpolate_f32, arm_fir_interpolate_instance_f32, float32
 MI355X_INTERP(arm_fir_interpolate_q15, arm_fir_interpolate_instance_q15, q15_t, int16_t, kMrQ15)
 MI355X_INTERP(arm_fir_interpolate_q31, arm_fir_interpolate_instance_q31, q31_t, int32_t, kMrQ31)
 #undef MI355X_INTERP
+
+#define MI355X_SPARSE(T, CT, OP)                                                                        \
+  void arm_fir_sparse_init_##T(arm_fir_sparse_instance_##T* S, uint16_t numTaps, const CT* pCoeffs, CT* pState, \
+                               int32_t* pTapDelay, uint16_t maxDelay, uint32_t blockSize) {            \
+    sparse_init(S, numTaps, pCoeffs, pState, pTapDelay, maxDelay, blockSize);                           \
+  }                                                                                                     \
+  arm_status arm_fir_sparse_##T##_batch(const arm_fir_sparse_instance_##T* S, const CT* d_src, CT* d_dst, \
+                                        uint32_t blockSize, uint32_t batch, CT* d_hist, void* stream) { \
+    return sparse_batch(S, d_src, d_dst, blockSize, batch, d_hist, stream, OP, "arm_fir_sparse_" #T "_batch"); \
+  }
+MI355X_SPARSE(f32, float32_t, kSpF32)
+MI355X_SPARSE(q31, q31_t, kSpQ31)
+MI355X_SPARSE(q15, q15_t, kSpQ15)
+MI355X_SPARSE(q7, q7_t, kSpQ7)
+#undef MI355X_SPARSE
+void arm_fir_sparse_f32(arm_fir_sparse_instance_f32* S, const float32_t* pSrc, float32_t* pDst, float32_t* pScratchIn,
+                        uint32_t blockSize) {
+  (void)pScratchIn;
+  sparse_sync(S, pSrc, pDst, blockSize, kSpF32, "arm_fir_sparse_f32");
+}
+void arm_fir_sparse_q31(arm_fir_sparse_instance_q31* S, const q31_t* pSrc, q31_t* pDst, q31_t* pScratchIn,
+                        uint32_t blockSize) {
+  (void)pScratchIn;
+  sparse_sync(S, pSrc, pDst, blockSize, kSpQ31, "arm_fir_sparse_q31");
+}
+void arm_fir_sparse_q15(arm_fir_sparse_instance_q15* S, const q15_t* pSrc, q15_t* pDst, q15_t* pScratchIn,
+                        q31_t* pScratchOut, uint32_t blockSize) {
+  (void)pScratchIn; (void)pScratchOut;
+  sparse_sync(S, pSrc, pDst, blockSize, kSpQ15, "arm_fir_sparse_q15");
+}
+void arm_fir_sparse_q7(arm_fir_sparse_instance_q7* S, const q7_t* pSrc, q7_t* pDst, q7_t* pScratchIn,
+                       q31_t* pScratchOut, uint32_t blockSize) {
+  (void)pScratchIn; (void)pScratchOut;
+  sparse_sync(S, pSrc, pDst, blockSize, kSpQ7, "arm_fir_sparse_q7");
+}
 
 }  // extern "C"

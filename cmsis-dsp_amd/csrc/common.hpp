@@ -35,6 +35,7 @@ __device__ __forceinline__ int32_t multSub_R(int32_t a, int32_t x, int32_t y) {
 }
 // __SSAT(val, 16): none.h:78-94
 __device__ __forceinline__ int32_t ssat16(int32_t v) { return v > 32767 ? 32767 : (v < -32768 ? -32768 : v); }
+__device__ __forceinline__ int32_t ssat8(int32_t v) { return v > 127 ? 127 : (v < -128 ? -128 : v); }
 
 constexpr int kBlock = 256;   // 4 wave64 per workgroup
 

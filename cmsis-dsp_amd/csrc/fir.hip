@@ -1198,4 +1198,214 @@ hipError_t fir_interpolate_run(int op, const void* coeffs, int L, int phase_len,
   }
 }
 
+// ---- sparse FIR: arm_fir_sparse_{f32,q31,q15,q7} -------------------------------------------
+// y[n] = sum over k ascending of x[n - D_k] c_k (arm_fir_sparse_f32.c: the first tap stores
+// x c_0, every later tap adds x c_k to the output, mul then add; q31 (q31)((q63 x c) >> 32)
+// terms summed with wrap-around, output << 1 (arm_fir_sparse_q31.c); q15 / q7 q31 products
+// summed with wrap-around in the q31 scratch, __SSAT(acc >> 15, 16) / __SSAT(acc >> 7, 8)
+// (arm_fir_sparse_q15.c, _q7.c)).  Three sample sources:
+//   kSpLds:  batched streams, history [batch][maxDelay] (oldest first) + block; a workgroup
+//            stages x[n0 - maxDelay, n0 + kSpLOut) of its stream in LDS (delays outside
+//            [0, maxDelay] read 0; fir_sparse_lds_kernel);
+//   kSpGlob: the same addressing read straight from HBM/L2 (windows too large for LDS);
+//   kSpCirc: the drop-in call: the reference's circular state buffer of L = maxDelay +
+//            blockSize words after the block is written, tap k read from (r0 - D_k) (+ L if
+//            negative), advancing with wrap at L, exactly as arm_circularRead_f32 does.
+template <int OP> struct SpT;
+template <> struct SpT<kSpF32> {
+  using T = float; using Acc = float;
+  static __device__ __forceinline__ Acc first(T x, T c) { return x * c; }
+  static __device__ __forceinline__ Acc mac(Acc a, T x, T c) { const float p = x * c; return a + p; }
+  static __device__ __forceinline__ T out(Acc a) { return a; }
+};
+template <> struct SpT<kSpQ31> {
+  using T = int32_t; using Acc = uint32_t;
+  static __device__ __forceinline__ Acc first(T x, T c) { return (uint32_t)mulhi(x, c); }
+  static __device__ __forceinline__ Acc mac(Acc a, T x, T c) { return a + (uint32_t)mulhi(x, c); }
+  static __device__ __forceinline__ T out(Acc a) { return (T)(a << 1); }
+};
+template <> struct SpT<kSpQ15> {
+  using T = int16_t; using Acc = uint32_t;
+  static __device__ __forceinline__ Acc first(T x, T c) { return (uint32_t)((int32_t)x * (int32_t)c); }
+  static __device__ __forceinline__ Acc mac(Acc a, T x, T c) { return a + first(x, c); }
+  static __device__ __forceinline__ T out(Acc a) { return (T)ssat16((int32_t)a >> 15); }
+};
+template <> struct SpT<kSpQ7> {
+  using T = int8_t; using Acc = uint32_t;
+  static __device__ __forceinline__ Acc first(T x, T c) { return (uint32_t)((int32_t)x * (int32_t)c); }
+  static __device__ __forceinline__ Acc mac(Acc a, T x, T c) { return a + first(x, c); }
+  static __device__ __forceinline__ T out(Acc a) { return (T)ssat8((int32_t)a >> 7); }
+};
+
+enum SpSrc { kSpLds = 0, kSpGlob = 1, kSpCirc = 2 };
+constexpr int kSpR = 4;                        // outputs per lane (direct-read kernel)
+constexpr int kSpOut = kSpR * kBlock;          // outputs per workgroup (direct-read kernel)
+constexpr int kSpLR = 16;                      // outputs per lane (LDS kernel)
+constexpr int kSpLOut = kSpLR * kBlock;        // outputs per workgroup (LDS kernel)
+constexpr int kSpLdsBytes = 64 * 1024;         // largest staged window
+
+struct SpIn {
+  const void* src;      // kSpLds / kSpGlob: [batch][B];  kSpCirc: the circular state
+  const void* hist;     // [batch][maxD]
+  uint32_t B, nchunks;
+  int maxD;
+  int L, r0;            // kSpCirc
+};
+
+// LDS kernel: win[j] = x[n0 - maxD + j], j < maxD + kSpLOut (zero past the block), lane t's
+// outputs n0 + t + 256 r read win[maxD - D + t + 256 r]: one LDS base per tap and immediate
+// offsets, no per-sample bounds checks (a tap with D outside [0, maxD] reads zeros, decided
+// per tap); the taps' scalar loads are issued four at a time.
+template <int OP>
+__global__ __launch_bounds__(kBlock) void fir_sparse_lds_kernel(const typename SpT<OP>::T* __restrict__ coeffs,
+                                                                const int32_t* __restrict__ delays, int T, SpIn in,
+                                                                typename SpT<OP>::T* __restrict__ dst) {
+  using Op = SpT<OP>;
+  using E = typename Op::T;
+  extern __shared__ __align__(16) unsigned char sp_lds[];
+  E* win = reinterpret_cast<E*>(sp_lds);
+  const uint64_t f = blockIdx.x / in.nchunks;
+  const int n0 = (int)(blockIdx.x - f * in.nchunks) * kSpLOut;
+  const int cnt = min(kSpLOut, (int)in.B - n0);
+  const int maxD = in.maxD;
+  const E* src = reinterpret_cast<const E*>(in.src) + f * in.B;
+  const E* hist = reinterpret_cast<const E*>(in.hist) + f * (uint64_t)maxD;
+  for (int j = threadIdx.x; j < maxD + kSpLOut; j += kBlock) {
+    const int p = n0 - maxD + j;
+    win[j] = p < 0 ? hist[maxD + p] : (p < n0 + cnt ? src[p] : (E)0);
+  }
+  __syncthreads();
+  const E* wt = win + maxD + threadIdx.x;
+  typename Op::Acc acc[kSpLR];
+  auto tap = [&](E c, int D) {
+    if (D >= 0 && D <= maxD) {                             // wave-uniform
+      const E* w = wt - D;
+#pragma unroll
+      for (int r = 0; r < kSpLR; ++r) acc[r] = Op::mac(acc[r], w[r * kBlock], c);
+    } else {
+#pragma unroll
+      for (int r = 0; r < kSpLR; ++r) acc[r] = Op::mac(acc[r], (E)0, c);
+    }
+  };
+  {
+    const E c = coeffs[0];
+    const int D = delays[0];
+    const E* w = wt - ((D >= 0 && D <= maxD) ? D : 0);
+    const bool z = !(D >= 0 && D <= maxD);
+#pragma unroll
+    for (int r = 0; r < kSpLR; ++r) acc[r] = Op::first(z ? (E)0 : w[r * kBlock], c);
+  }
+  int k = 1;
+  for (; k + 4 <= T; k += 4) {
+    E c[4];
+    int D[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { c[u] = coeffs[k + u]; D[u] = delays[k + u]; }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) tap(c[u], D[u]);
+  }
+  for (; k < T; ++k) tap(coeffs[k], delays[k]);
+  E* y = dst + f * in.B + n0 + threadIdx.x;
+#pragma unroll
+  for (int r = 0; r < kSpLR; ++r)
+    if ((int)threadIdx.x + r * kBlock < cnt) y[r * kBlock] = Op::out(acc[r]);
+}
+
+template <int OP, int SRC>
+__global__ __launch_bounds__(kBlock) void fir_sparse_kernel(const typename SpT<OP>::T* __restrict__ coeffs,
+                                                            const int32_t* __restrict__ delays, int T, SpIn in,
+                                                            typename SpT<OP>::T* __restrict__ dst) {
+  using Op = SpT<OP>;
+  using E = typename Op::T;
+  const uint64_t f = blockIdx.x / in.nchunks;
+  const int n0 = (int)(blockIdx.x - f * in.nchunks) * kSpOut;
+  const int cnt = min(kSpOut, (int)in.B - n0);
+  const E* src = reinterpret_cast<const E*>(in.src) + (SRC == kSpCirc ? 0 : f * in.B);
+  const E* hist = reinterpret_cast<const E*>(in.hist) + f * (uint64_t)in.maxD;
+  auto fetch = [&](int n, int D, int idx) -> E {
+    if constexpr (SRC == kSpGlob) {
+      const int p = n - D;
+      return p >= 0 ? (p < (int)in.B ? src[p] : (E)0) : (p >= -in.maxD ? hist[in.maxD + p] : (E)0);
+    } else {
+      int q = idx + n;
+      if (q >= in.L) q -= in.L;
+      if ((unsigned)q >= (unsigned)in.L) q = ((q % in.L) + in.L) % in.L;
+      return src[q];
+    }
+  };
+  typename Op::Acc acc[kSpR];
+  for (int k = 0; k < T; ++k) {
+    const E c = coeffs[k];
+    const int D = delays[k];
+    int idx = 0;
+    if constexpr (SRC == kSpCirc) {
+      idx = in.r0 - D;
+      if (idx < 0) idx += in.L;
+    }
+#pragma unroll
+    for (int r = 0; r < kSpR; ++r) {
+      const int n = n0 + (int)threadIdx.x + r * kBlock;
+      const E x = n < n0 + cnt ? fetch(n, D, idx) : (E)0;
+      acc[r] = k == 0 ? Op::first(x, c) : Op::mac(acc[r], x, c);
+    }
+  }
+  E* y = dst + f * in.B;
+#pragma unroll
+  for (int r = 0; r < kSpR; ++r) {
+    const int n = n0 + (int)threadIdx.x + r * kBlock;
+    if (n < n0 + cnt) y[n] = Op::out(acc[r]);
+  }
+}
+
+template <int OP>
+static hipError_t sparse_launch(const void* coeffs, const int32_t* delays, int T, int maxD, const void* src,
+                                void* dst, uint32_t B, uint32_t batch, void* hist, int L, int r0, hipStream_t st) {
+  using E = typename SpT<OP>::T;
+  if (batch == 0 || B == 0) return hipSuccess;
+  if (T < 1 || maxD < 0) return hipErrorInvalidValue;
+  SpIn in{src, hist, B, (B + kSpOut - 1) / kSpOut, maxD, L, r0};
+  const uint64_t blocks = (uint64_t)in.nchunks * batch;
+  if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
+  if (L > 0) {                                 // drop-in: one stream, circular state
+    hipLaunchKernelGGL((fir_sparse_kernel<OP, kSpCirc>), dim3((uint32_t)blocks), dim3(kBlock), 0, st,
+                       (const E*)coeffs, delays, T, in, (E*)dst);
+    return hipGetLastError();
+  }
+  const size_t lds = sizeof(E) * ((size_t)maxD + kSpLOut);
+  const SpIn lin{src, hist, B, (B + kSpLOut - 1) / kSpLOut, maxD, 0, 0};
+  const uint64_t lblocks = (uint64_t)lin.nchunks * batch;
+  return mr_launch<E>((const E*)src, (E*)dst, (size_t)batch * B, B, batch, (E*)hist, maxD, B, st,
+                      [&](const E* s, const E* h) {
+                        if (lds <= (size_t)kSpLdsBytes) {
+                          SpIn l = lin;
+                          l.src = s;
+                          l.hist = h;
+                          hipLaunchKernelGGL(fir_sparse_lds_kernel<OP>, dim3((uint32_t)lblocks), dim3(kBlock), lds, st,
+                                             (const E*)coeffs, delays, T, l, (E*)dst);
+                        } else {
+                          in.src = s;
+                          in.hist = h;
+                          hipLaunchKernelGGL((fir_sparse_kernel<OP, kSpGlob>), dim3((uint32_t)blocks), dim3(kBlock),
+                                             0, st, (const E*)coeffs, delays, T, in, (E*)dst);
+                        }
+                        return hipSuccess;
+                      });
+}
+
+hipError_t fir_sparse_run(int op, const void* coeffs, const int32_t* delays, int num_taps, int max_delay,
+                          const void* src, void* dst, uint32_t block_size, uint32_t batch, void* hist, int circ_len,
+                          int circ_r0, hipStream_t st) {
+  switch (op) {
+    case kSpF32: return sparse_launch<kSpF32>(coeffs, delays, num_taps, max_delay, src, dst, block_size, batch, hist,
+                                              circ_len, circ_r0, st);
+    case kSpQ31: return sparse_launch<kSpQ31>(coeffs, delays, num_taps, max_delay, src, dst, block_size, batch, hist,
+                                              circ_len, circ_r0, st);
+    case kSpQ15: return sparse_launch<kSpQ15>(coeffs, delays, num_taps, max_delay, src, dst, block_size, batch, hist,
+                                              circ_len, circ_r0, st);
+    case kSpQ7: return sparse_launch<kSpQ7>(coeffs, delays, num_taps, max_delay, src, dst, block_size, batch, hist,
+                                            circ_len, circ_r0, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 }  // namespace mi355x

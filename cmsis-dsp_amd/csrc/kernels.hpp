@@ -75,6 +75,14 @@ hipError_t fir_decimate_run(int op, const void* coeffs, int num_taps, int M, con
                             uint32_t block_size, uint32_t batch, void* hist, hipStream_t st);
 hipError_t fir_interpolate_run(int op, const void* coeffs, int L, int phase_len, const void* src, void* dst,
                                uint32_t block_size, uint32_t batch, void* hist, hipStream_t st);
+// Sparse FIR (fir.hip): `batch` streams sharing taps c[k] at delays D[k] (device arrays).
+// circ_len == 0: block [batch][B] + history [batch][max_delay] (oldest first, updated);
+// circ_len = L > 0: one stream whose samples are the reference's circular state buffer `src`
+// of L words (block already written), tap k starting at circ_r0 - D[k] (wrapped), hist unused.
+enum SpOp { kSpF32 = 0, kSpQ31 = 1, kSpQ15 = 2, kSpQ7 = 3 };
+hipError_t fir_sparse_run(int op, const void* coeffs, const int32_t* delays, int num_taps, int max_delay,
+                          const void* src, void* dst, uint32_t block_size, uint32_t batch, void* hist, int circ_len,
+                          int circ_r0, hipStream_t st);
 
 // MFCC f32 around the batched RFFT (mfcc_f32.hip): frame normalisation + window, then the
 // spectrum -> Mel -> log -> DCT tail.  post needs mfcc_f32_post_lds(n, nb_mel) bytes of LDS.

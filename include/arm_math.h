@@ -179,6 +179,22 @@ typedef struct {
         float32_t *pState;
 } arm_fir_interpolate_instance_f32;
 
+/* Sparse FIR instances (Include/dsp/filtering_functions.h:2033-2091), same layout for each type. */
+#define MI355X_SPARSE_INST(T, ET)                                                               \
+  typedef struct {                                                                              \
+          uint16_t numTaps;    /* nonzero taps */                                               \
+          uint16_t stateIndex; /* circular write position in pState */                          \
+          ET      *pState;     /* maxDelay + blockSize words (circular) */                      \
+    const ET      *pCoeffs;    /* numTaps */                                                    \
+          uint16_t maxDelay;                                                                    \
+          int32_t *pTapDelay;  /* numTaps delays, each in [0, maxDelay] */                      \
+  } arm_fir_sparse_instance_##T;
+MI355X_SPARSE_INST(f32, float32_t)
+MI355X_SPARSE_INST(q31, q31_t)
+MI355X_SPARSE_INST(q15, q15_t)
+MI355X_SPARSE_INST(q7, q7_t)
+#undef MI355X_SPARSE_INST
+
 /* ---- matrix instances: Include/dsp/matrix_functions.h:118-123 (f32), :139-143 (q7),
  * :139-144 (q15), :149-154 (q31) */
 typedef struct {
@@ -434,6 +450,34 @@ void arm_fir_interpolate_q15(const arm_fir_interpolate_instance_q15 *S, const q1
                              uint32_t blockSize);
 void arm_fir_interpolate_q31(const arm_fir_interpolate_instance_q31 *S, const q31_t *pSrc, q31_t *pDst,
                              uint32_t blockSize);
+
+/* ===================================================================================
+ * Sparse FIR (widening).  Prototypes: Include/dsp/filtering_functions.h:2094-2231.  Reference
+ * bodies: Source/FilteringFunctions/arm_fir_sparse_{f32,q31,q15,q7}.c, inits
+ * arm_fir_sparse_init_*.c.  y[n] = sum over k ascending of x[n - pTapDelay[k]] pCoeffs[k]:
+ * f32 first tap x c, then mul-then-add; q31 (q31)((q63 x c) >> 32) terms summed with wrap,
+ * output << 1; q15 / q7 q31 product sums (wrap) then __SSAT(>> 15, 16) / __SSAT(>> 7, 8).
+ * The block is written into the circular pState at stateIndex and every tap read back from it
+ * at the reference's indices, so the state and stateIndex evolve exactly as the reference's.
+ * pScratchIn / pScratchOut are accepted and not used.  numTaps == 1 is one product per output
+ * (the reference's numTaps - 2 tap loop counter underflows there).
+ * =================================================================================== */
+void arm_fir_sparse_init_f32(arm_fir_sparse_instance_f32 *S, uint16_t numTaps, const float32_t *pCoeffs,
+                             float32_t *pState, int32_t *pTapDelay, uint16_t maxDelay, uint32_t blockSize);
+void arm_fir_sparse_init_q31(arm_fir_sparse_instance_q31 *S, uint16_t numTaps, const q31_t *pCoeffs, q31_t *pState,
+                             int32_t *pTapDelay, uint16_t maxDelay, uint32_t blockSize);
+void arm_fir_sparse_init_q15(arm_fir_sparse_instance_q15 *S, uint16_t numTaps, const q15_t *pCoeffs, q15_t *pState,
+                             int32_t *pTapDelay, uint16_t maxDelay, uint32_t blockSize);
+void arm_fir_sparse_init_q7(arm_fir_sparse_instance_q7 *S, uint16_t numTaps, const q7_t *pCoeffs, q7_t *pState,
+                            int32_t *pTapDelay, uint16_t maxDelay, uint32_t blockSize);
+void arm_fir_sparse_f32(arm_fir_sparse_instance_f32 *S, const float32_t *pSrc, float32_t *pDst,
+                        float32_t *pScratchIn, uint32_t blockSize);
+void arm_fir_sparse_q31(arm_fir_sparse_instance_q31 *S, const q31_t *pSrc, q31_t *pDst, q31_t *pScratchIn,
+                        uint32_t blockSize);
+void arm_fir_sparse_q15(arm_fir_sparse_instance_q15 *S, const q15_t *pSrc, q15_t *pDst, q15_t *pScratchIn,
+                        q31_t *pScratchOut, uint32_t blockSize);
+void arm_fir_sparse_q7(arm_fir_sparse_instance_q7 *S, const q7_t *pSrc, q7_t *pDst, q7_t *pScratchIn,
+                       q31_t *pScratchOut, uint32_t blockSize);
 
 /* ===================================================================================
  * Convolution.  Prototypes: Include/dsp/filtering_functions.h

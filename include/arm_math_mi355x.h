@@ -104,6 +104,20 @@ arm_status arm_fir_interpolate_q15_batch(const arm_fir_interpolate_instance_q15 
 arm_status arm_fir_interpolate_q31_batch(const arm_fir_interpolate_instance_q31 *S, const q31_t *d_src, q31_t *d_dst,
                                          uint32_t blockSize, uint32_t batch, q31_t *d_hist, void *stream);
 
+/* Sparse FIR over `batch` independent streams sharing S's taps and delays (host or device
+ * arrays): d_src / d_dst [batch][blockSize], d_hist [batch][maxDelay] = each stream's last
+ * maxDelay input samples, oldest first (zero-initialise, updated in place; the linear form of
+ * the reference's circular state, which the batched call does not use).  Delays outside
+ * [0, maxDelay] read zero.  Per-stream semantics: arm_fir_sparse_f32 / _q31 / _q15 / _q7. */
+arm_status arm_fir_sparse_f32_batch(const arm_fir_sparse_instance_f32 *S, const float32_t *d_src, float32_t *d_dst,
+                                    uint32_t blockSize, uint32_t batch, float32_t *d_hist, void *stream);
+arm_status arm_fir_sparse_q31_batch(const arm_fir_sparse_instance_q31 *S, const q31_t *d_src, q31_t *d_dst,
+                                    uint32_t blockSize, uint32_t batch, q31_t *d_hist, void *stream);
+arm_status arm_fir_sparse_q15_batch(const arm_fir_sparse_instance_q15 *S, const q15_t *d_src, q15_t *d_dst,
+                                    uint32_t blockSize, uint32_t batch, q15_t *d_hist, void *stream);
+arm_status arm_fir_sparse_q7_batch(const arm_fir_sparse_instance_q7 *S, const q7_t *d_src, q7_t *d_dst,
+                                   uint32_t blockSize, uint32_t batch, q7_t *d_hist, void *stream);
+
 /* Convolution of `batch` pairs: item i convolves d_a + i*strideA (srcALen samples) with
  * d_b + i*strideB (srcBLen samples; strideB = 0 shares one kernel) into
  * d_dst + i*(srcALen + srcBLen - 1).  Per-item semantics: arm_conv_f32 / _q15 / _q31. */

@@ -39,4 +39,22 @@ arm_status oracle_arm_mfcc_init_f32(arm_mfcc_instance_f32 *S, uint32_t fftLen, u
                                     const uint32_t *filterLengths, const float *filterCoefs,
                                     const float *windowCoefs);
 void oracle_arm_mfcc_f32(const arm_mfcc_instance_f32 *S, float *pSrc, float *pDst, float *pTmp);
+/* sparse FIR (oracle_multirate.c), the reference's signatures */
+#define ORACLE_SPARSE_PROTO(T, ET)                                                                          \
+  void oracle_arm_fir_sparse_init_##T(arm_fir_sparse_instance_##T *S, uint16_t numTaps, const ET *pCoeffs, \
+                                      ET *pState, int32_t *pTapDelay, uint16_t maxDelay, uint32_t blockSize);
+ORACLE_SPARSE_PROTO(f32, float)
+ORACLE_SPARSE_PROTO(q31, int32_t)
+ORACLE_SPARSE_PROTO(q15, int16_t)
+ORACLE_SPARSE_PROTO(q7, int8_t)
+void oracle_arm_fir_sparse_f32(arm_fir_sparse_instance_f32 *S, const float *pSrc, float *pDst, float *pScratchIn,
+                               uint32_t blockSize);
+void oracle_arm_fir_sparse_q31(arm_fir_sparse_instance_q31 *S, const int32_t *pSrc, int32_t *pDst, int32_t *pScratchIn,
+                               uint32_t blockSize);
+void oracle_arm_fir_sparse_q15(arm_fir_sparse_instance_q15 *S, const int16_t *pSrc, int16_t *pDst, int16_t *pScratchIn,
+                               int32_t *pScratchOut, uint32_t blockSize);
+void oracle_arm_fir_sparse_q7(arm_fir_sparse_instance_q7 *S, const int8_t *pSrc, int8_t *pDst, int8_t *pScratchIn,
+                              int32_t *pScratchOut, uint32_t blockSize);
+#undef ORACLE_SPARSE_PROTO
+
 #endif

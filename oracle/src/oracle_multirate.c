@@ -15,8 +15,16 @@
  *     to the front.
  *   arm_fir_decimate_init_*.c / arm_fir_interpolate_init_*.c: ARM_MATH_LENGTH_ERROR unless
  *     blockSize % M == 0 / numTaps % L == 0; the state is zeroed.
- * Pinned against oracle/_ref by tests/test_multirate.py. */
+ *   arm_fir_sparse_{f32,q31,q15,q7}.c: the block is written into the circular state (L =
+ *     maxDelay + blockSize words) at stateIndex, which advances by blockSize mod L
+ *     (arm_circularWrite_f32); tap k reads blockSize words from (stateIndex - blockSize -
+ *     D_k) (+ L if negative), wrapping at L (arm_circularRead_f32).  The first tap stores x c,
+ *     later taps add: f32 mul then add; q31 (q31)((q63 x c) >> 32) with wrap, output << 1; q15 /
+ *     q7 q31 products with wrap, __SSAT(>> 15, 16) / __SSAT(>> 7, 8).  arm_fir_sparse_init_*.c
+ *     zeroes maxDelay + blockSize words and stateIndex.
+ * Pinned against oracle/_ref by tests/test_multirate.py and tests/test_sparse.py. */
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "oracle.h"
@@ -115,3 +123,74 @@ INTERP(arm_fir_interpolate_q31, arm_fir_interpolate_instance_q31, int32_t, MR_Q3
 DINIT(f32, float)
 DINIT(q15, int16_t)
 DINIT(q31, int32_t)
+
+/* ---- sparse FIR ---- */
+enum { SP_F32, SP_Q31, SP_Q15, SP_Q7 };
+
+static int32_t sp_word(int op, const void *s, int32_t i) {
+  switch (op) {
+    case SP_Q31: return ((const int32_t *)s)[i];
+    case SP_Q15: return ((const int16_t *)s)[i];
+    default: return ((const int8_t *)s)[i];
+  }
+}
+
+static void sparse(int op, size_t es, uint16_t taps, uint16_t *stateIndex, uint16_t maxDelay, const void *h,
+                   const int32_t *delays, void *state, const void *src, void *dst, uint32_t B) {
+  const int32_t L = (int32_t)maxDelay + (int32_t)B;
+  int32_t w = *stateIndex;
+  for (uint32_t n = 0; n < B; ++n) {           /* circular write */
+    memcpy((char *)state + es * w, (const char *)src + es * n, es);
+    if (++w >= L) w -= L;
+  }
+  *stateIndex = (uint16_t)w;
+  float *yf = dst;
+  uint32_t *acc = NULL;
+  if (op != SP_F32) acc = calloc(B, sizeof(uint32_t));
+  for (uint16_t k = 0; k < taps; ++k) {
+    int32_t r = (int32_t)(*stateIndex - B) - delays[k];
+    if (r < 0) r += L;
+    for (uint32_t n = 0; n < B; ++n) {
+      if (op == SP_F32) {
+        const float p = ((const float *)state)[r] * ((const float *)h)[k];
+        yf[n] = k == 0 ? p : yf[n] + p;
+      } else {
+        const int32_t x = sp_word(op, state, r), c = sp_word(op, h, k);
+        const uint32_t t = op == SP_Q31 ? (uint32_t)(int32_t)(((int64_t)x * c) >> 32) : (uint32_t)(x * c);
+        acc[n] = k == 0 ? t : acc[n] + t;
+      }
+      if (++r >= L) r -= L;
+    }
+  }
+  for (uint32_t n = 0; op != SP_F32 && n < B; ++n) {
+    const int32_t a = (int32_t)acc[n];
+    if (op == SP_Q31) ((int32_t *)dst)[n] = (int32_t)((uint32_t)a << 1);
+    else if (op == SP_Q15) ((int16_t *)dst)[n] = sat16(a >> 15);
+    else ((int8_t *)dst)[n] = (int8_t)((a >> 7) > 127 ? 127 : (a >> 7) < -128 ? -128 : (a >> 7));
+  }
+  free(acc);
+}
+
+#define SPARSE_INIT(T, ET)                                                                                       \
+  void oracle_arm_fir_sparse_init_##T(arm_fir_sparse_instance_##T *S, uint16_t numTaps, const ET *pCoeffs,       \
+                                      ET *pState, int32_t *pTapDelay, uint16_t maxDelay, uint32_t blockSize) {   \
+    S->numTaps = numTaps; S->pCoeffs = pCoeffs; S->pTapDelay = pTapDelay; S->maxDelay = maxDelay;                \
+    S->stateIndex = 0;                                                                                           \
+    memset(pState, 0, sizeof(ET) * ((size_t)maxDelay + blockSize));                                              \
+    S->pState = pState;                                                                                          \
+  }
+SPARSE_INIT(f32, float)
+SPARSE_INIT(q31, int32_t)
+SPARSE_INIT(q15, int16_t)
+SPARSE_INIT(q7, int8_t)
+#define SPARSE_RUN(T, OP) \
+  sparse(OP, sizeof(*pSrc), S->numTaps, &S->stateIndex, S->maxDelay, S->pCoeffs, S->pTapDelay, S->pState, pSrc, pDst, blockSize)
+/* the reference's signatures; the scratch buffers are not needed */
+void oracle_arm_fir_sparse_f32(arm_fir_sparse_instance_f32 *S, const float *pSrc, float *pDst, float *pScratchIn,
+                               uint32_t blockSize) { SPARSE_RUN(f32, SP_F32); }
+void oracle_arm_fir_sparse_q31(arm_fir_sparse_instance_q31 *S, const int32_t *pSrc, int32_t *pDst, int32_t *pScratchIn,
+                               uint32_t blockSize) { SPARSE_RUN(q31, SP_Q31); }
+void oracle_arm_fir_sparse_q15(arm_fir_sparse_instance_q15 *S, const int16_t *pSrc, int16_t *pDst, int16_t *pScratchIn,
+                               int32_t *pScratchOut, uint32_t blockSize) { SPARSE_RUN(q15, SP_Q15); }
+void oracle_arm_fir_sparse_q7(arm_fir_sparse_instance_q7 *S, const int8_t *pSrc, int8_t *pDst, int8_t *pScratchIn,
+                              int32_t *pScratchOut, uint32_t blockSize) { SPARSE_RUN(q7, SP_Q7); }

@@ -145,6 +145,37 @@ class Host:
         self._keep = (c, state)
         return st, outs, state.copy()
 
+    def sparse(self, kind, coeffs, delays, max_delay, blocks, block_size=None, state_mem=None):
+        """Stream `blocks` through one arm_fir_sparse_<kind> instance: returns (outputs, final
+        circular state, final stateIndex).  state_mem(n, dtype) may supply the state buffer
+        (e.g. device memory) as (pointer, reader)."""
+        dt = DTYPE[kind]
+        c = np.ascontiguousarray(coeffs, dtype=dt)
+        d = np.ascontiguousarray(delays, dtype=np.int32)
+        bs = block_size or max(len(b) for b in blocks)
+        inst = _abi.arm_fir_sparse_instance()
+        if state_mem is None:
+            state = np.full(max_delay + bs, 7, dtype=dt)       # init must zero it
+            sptr, sread = state.ctypes.data, state.copy
+        else:
+            sptr, sread = state_mem(max_delay + bs, dt)
+        self.fn(f"arm_fir_sparse_init_{kind}")(C.byref(inst), len(c), c.ctypes.data, sptr, d.ctypes.data,
+                                                max_delay, bs)
+        f = self.fn(f"arm_fir_sparse_{kind}")
+        outs = []
+        for b in blocks:
+            b = np.ascontiguousarray(b, dtype=dt)
+            y = np.zeros(len(b), dtype=dt)
+            sin = np.zeros(len(b), dtype=dt)
+            if kind in ("q15", "q7"):
+                sout = np.zeros(len(b), dtype=np.int32)
+                f(C.byref(inst), b.ctypes.data, y.ctypes.data, sin.ctypes.data, sout.ctypes.data, len(b))
+            else:
+                f(C.byref(inst), b.ctypes.data, y.ctypes.data, sin.ctypes.data, len(b))
+            outs.append(y)
+        self._keep = (c, d)
+        return outs, sread(), inst.stateIndex
+
     def conv(self, kind, a, b):
         dt = DTYPE[kind]
         a = np.ascontiguousarray(a, dtype=dt)

@@ -35,6 +35,18 @@ int main(void) {
     F(arm_mfcc_instance_f32, windowCoefs) F(arm_mfcc_instance_f32, filterPos) F(arm_mfcc_instance_f32, filterLengths)
     F(arm_mfcc_instance_f32, fftLen) F(arm_mfcc_instance_f32, nbMelFilters) F(arm_mfcc_instance_f32, nbDctOutputs)
     F(arm_mfcc_instance_f32, rfft) E()
+  S(arm_fir_sparse_instance_f32) F(arm_fir_sparse_instance_f32, numTaps) F(arm_fir_sparse_instance_f32, stateIndex)
+    F(arm_fir_sparse_instance_f32, pState) F(arm_fir_sparse_instance_f32, pCoeffs)
+    F(arm_fir_sparse_instance_f32, maxDelay) F(arm_fir_sparse_instance_f32, pTapDelay) E()
+  S(arm_fir_sparse_instance_q7) F(arm_fir_sparse_instance_q7, numTaps) F(arm_fir_sparse_instance_q7, stateIndex)
+    F(arm_fir_sparse_instance_q7, pState) F(arm_fir_sparse_instance_q7, pCoeffs)
+    F(arm_fir_sparse_instance_q7, maxDelay) F(arm_fir_sparse_instance_q7, pTapDelay) E()
+  S(arm_fir_decimate_instance_q15) F(arm_fir_decimate_instance_q15, M) F(arm_fir_decimate_instance_q15, numTaps)
+    F(arm_fir_decimate_instance_q15, pCoeffs) F(arm_fir_decimate_instance_q15, pState) E()
+  S(arm_fir_interpolate_instance_f32) F(arm_fir_interpolate_instance_f32, L)
+    F(arm_fir_interpolate_instance_f32, phaseLength) F(arm_fir_interpolate_instance_f32, pCoeffs)
+    F(arm_fir_interpolate_instance_f32, pState) E()
+  S(arm_fir_instance_q7) F(arm_fir_instance_q7, numTaps) F(arm_fir_instance_q7, pState) F(arm_fir_instance_q7, pCoeffs) E()
   S(arm_rfft_instance_q31) F(arm_rfft_instance_q31, fftLenReal) F(arm_rfft_instance_q31, ifftFlagR)
     F(arm_rfft_instance_q31, bitReverseFlagR) F(arm_rfft_instance_q31, twidCoefRModifier)
     F(arm_rfft_instance_q31, pTwiddleAReal) F(arm_rfft_instance_q31, pTwiddleBReal) F(arm_rfft_instance_q31, pCfft) E()

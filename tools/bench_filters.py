@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Throughput of the filtering functions outside bench.py's workloads (round 2 additions):
-arm_fir_q7, arm_fir_decimate_*, arm_fir_interpolate_* through the batched device API on one
+arm_fir_q7, arm_fir_decimate_*, arm_fir_interpolate_*, arm_fir_sparse_* through the batched device API on one
 GPU, HIP-event timed on the launch stream after a clock-settle phase, each with a bit-exact
 check of 2 streams against the CPU checker (the reference build when present).
 Usage: python tools/bench_filters.py [name ...]  -> one JSON line per workload."""
@@ -21,6 +21,7 @@ from cmsisdsp_amd import _abi  # noqa: E402
 import refs  # noqa: E402
 
 BATCH, BLOCK, TAPS = 1 << 16, 4096, 128
+SP_TAPS, SP_DELAY = 32, 1024            # sparse: 32 nonzero taps at delays in [0, 1024]
 # name: (function, factor, dtype)
 CASES = {
     "fir_q7": ("q7", 1, "q7"),
@@ -30,6 +31,10 @@ CASES = {
     "fir_decimate_q31_m4": ("decimate_q31", 4, "q31"),
     "fir_interpolate_f32_l4": ("interpolate_f32", 4, "f32"),
     "fir_interpolate_q31_l4": ("interpolate_q31", 4, "q31"),
+    "fir_sparse_f32": ("sparse_f32", 1, "f32"),
+    "fir_sparse_q31": ("sparse_q31", 1, "q31"),
+    "fir_sparse_q15": ("sparse_q15", 1, "q15"),
+    "fir_sparse_q7": ("sparse_q7", 1, "q7"),
 }
 TDT = {"f32": torch.float32, "q15": torch.int16, "q31": torch.int32, "q7": torch.int8}
 
@@ -65,11 +70,14 @@ def run(name):
     fn, factor, kind = CASES[name]
     rng = np.random.default_rng(7)
     dt = refs.DTYPE[kind]
+    sparse = fn.startswith("sparse")
+    taps = SP_TAPS if sparse else TAPS
     if kind == "f32":
-        c = (rng.standard_normal(TAPS) / np.sqrt(TAPS)).astype(np.float32)
+        c = (rng.standard_normal(taps) / np.sqrt(taps)).astype(np.float32)
     else:
         info = np.iinfo(dt)
-        c = rng.integers(info.min, info.max, TAPS, endpoint=True).astype(dt)
+        c = rng.integers(info.min, info.max, taps, endpoint=True).astype(dt)
+    delays = np.sort(rng.choice(SP_DELAY + 1, taps, replace=False)).astype(np.int32)
     g = torch.Generator(device="cuda")
     g.manual_seed(11)
     if kind == "f32":
@@ -80,7 +88,12 @@ def run(name):
                             dtype=torch.int64).to(TDT[kind])
     dc = torch.from_numpy(c.copy()).cuda()
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    if fn == "q7":
+    if sparse:
+        dd = torch.from_numpy(delays.copy()).cuda()
+        S = _abi.arm_fir_sparse_instance(numTaps=taps, pCoeffs=dc.data_ptr(), maxDelay=SP_DELAY,
+                                         pTapDelay=dd.data_ptr())
+        H, nout, f = SP_DELAY, BLOCK, getattr(dsp.lib, f"arm_fir_{fn}_batch")
+    elif fn == "q7":
         S = _abi.arm_fir_instance_q7(numTaps=TAPS, pState=None, pCoeffs=dc.data_ptr())
         H, nout, f = TAPS - 1, BLOCK, dsp.lib.arm_fir_q7_batch
     elif fn.startswith("decimate"):
@@ -107,12 +120,18 @@ def run(name):
     ok = True
     for i in range(2):
         x = src[i].cpu().numpy()
-        want = host.fir("q7", c, [x])[0][0] if fn == "q7" else host.multirate(fn, factor, c, [x])[1][0]
+        if sparse:
+            want = host.sparse(kind, c, delays, SP_DELAY, [x])[0][0]
+        elif fn == "q7":
+            want = host.fir("q7", c, [x])[0][0]
+        else:
+            want = host.multirate(fn, factor, c, [x])[1][0]
         ok &= d2[i].cpu().numpy().tobytes() == want.tobytes()
-    macs = BATCH * (BLOCK * TAPS if fn == "q7" else (BLOCK // factor) * TAPS if fn.startswith("decimate")
+    macs = BATCH * (BLOCK * taps if fn == "q7" or sparse else (BLOCK // factor) * TAPS if fn.startswith("decimate")
                     else BLOCK * TAPS)
     esz = np.dtype(dt).itemsize
-    return {"workload": name, "function": f"arm_fir_{fn}", "numTaps": TAPS, "factor": factor, "blockSize": BLOCK,
+    extra = {"maxDelay": SP_DELAY} if sparse else {}
+    return {"workload": name, "function": f"arm_fir_{fn}", "numTaps": taps, **extra, "factor": factor, "blockSize": BLOCK,
             "batch": BATCH, "avg_kernel_ms": round(ms, 4),
             "input_gsamples_per_s": round(BATCH * BLOCK / (ms * 1e-3) * 1e-9, 2),
             "output_gsamples_per_s": round(BATCH * nout / (ms * 1e-3) * 1e-9, 2),
