@@ -60,6 +60,8 @@ for _t in ("f32", "q31", "q15"):
                                                          _abi.arm_fir_decimate_instance)
     globals()[f"arm_fir_interpolate_instance_{_t}"] = _make(f"arm_fir_interpolate_instance_{_t}",
                                                             _abi.arm_fir_interpolate_instance)
+for _t in ("f32", "q31", "q15"):
+    globals()[f"arm_fir_lattice_instance_{_t}"] = _make(f"arm_fir_lattice_instance_{_t}", _abi.arm_fir_lattice_instance)
 for _t in ("f32", "q31", "q15", "q7"):
     globals()[f"arm_fir_sparse_instance_{_t}"] = _make(f"arm_fir_sparse_instance_{_t}", _abi.arm_fir_sparse_instance)
 del _t
@@ -250,6 +252,40 @@ for _k in ("f32", "q31", "q15"):
     globals()[f"arm_fir_interpolate_{_k}"] = _mr("interpolate", f"interpolate_{_k}", _k)
 arm_fir_decimate_fast_q15 = _mr("decimate", "decimate_fast_q15", "q15")
 arm_fir_decimate_fast_q31 = _mr("decimate", "decimate_fast_q31", "q31")
+del _k
+
+
+# cmsisdsp_filtering.c cmsis_arm_fir_lattice_init_* ("OhOO": S, numStages, pCoeffs, pState) and
+# cmsis_arm_fir_lattice_* ("OO": S, pSrc; returns len(pSrc) words).
+def _lattice_init(kind):
+    name = f"arm_fir_lattice_init_{kind}"
+
+    def init(inst, numStages, pCoeffs, pState):
+        c = _arr(pCoeffs, _DT[kind])
+        state = _np.zeros(max(len(_np.asarray(pState)), int(numStages)), dtype=_DT[kind])
+        inst._keep = [c, state]
+        getattr(_lib, name)(_C.byref(inst._s), int(numStages), c.ctypes.data, state.ctypes.data)
+        _check(name)
+    init.__name__ = name
+    return init
+
+
+def _lattice(kind):
+    name = f"arm_fir_lattice_{kind}"
+
+    def run(inst, pSrc):
+        x = _arr(pSrc, _DT[kind])
+        y = _np.zeros(len(x), dtype=_DT[kind])
+        getattr(_lib, name)(_C.byref(inst._s), x.ctypes.data, y.ctypes.data, len(x))
+        _check(name)
+        return y
+    run.__name__ = name
+    return run
+
+
+for _k in ("f32", "q31", "q15"):
+    globals()[f"arm_fir_lattice_init_{_k}"] = _lattice_init(_k)
+    globals()[f"arm_fir_lattice_{_k}"] = _lattice(_k)
 del _k
 
 

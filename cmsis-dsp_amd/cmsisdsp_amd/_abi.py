@@ -65,6 +65,11 @@ class arm_fir_interpolate_instance(C.Structure):
     _fields_ = [("L", C.c_uint8), ("phaseLength", C.c_uint16), ("pCoeffs", C.c_void_p), ("pState", C.c_void_p)]
 
 
+# arm_fir_lattice_instance_{f32,q31,q15} (filtering_functions.h:1312-1340), one layout
+class arm_fir_lattice_instance(C.Structure):
+    _fields_ = [("numStages", C.c_uint16), ("pState", C.c_void_p), ("pCoeffs", C.c_void_p)]
+
+
 # arm_fir_sparse_instance_{f32,q31,q15,q7} (filtering_functions.h:2033-2091), one layout
 class arm_fir_sparse_instance(C.Structure):
     _fields_ = [("numTaps", C.c_uint16), ("stateIndex", C.c_uint16), ("pState", C.c_void_p), ("pCoeffs", C.c_void_p),
@@ -147,6 +152,10 @@ DROPIN = {
     **{f"arm_fir_{k}": (None, [P(arm_fir_interpolate_instance), C.c_void_p, C.c_void_p, C.c_uint32])
        for k in ("interpolate_f32", "interpolate_q15", "interpolate_q31")},
     "arm_fir_q7": (None, [P(arm_fir_instance_q7), C.c_void_p, C.c_void_p, C.c_uint32]),
+    **{f"arm_fir_lattice_init_{t}": (None, [P(arm_fir_lattice_instance), C.c_uint16, C.c_void_p, C.c_void_p])
+       for t in ("f32", "q31", "q15")},
+    **{f"arm_fir_lattice_{t}": (None, [P(arm_fir_lattice_instance), C.c_void_p, C.c_void_p, C.c_uint32])
+       for t in ("f32", "q31", "q15")},
     **{f"arm_fir_sparse_init_{t}": (None, [P(arm_fir_sparse_instance), C.c_uint16, C.c_void_p, C.c_void_p, C.c_void_p,
                                            C.c_uint16, C.c_uint32]) for t in ("f32", "q31", "q15", "q7")},
     **{f"arm_fir_sparse_{t}": (None, [P(arm_fir_sparse_instance), C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32])
@@ -230,6 +239,8 @@ BATCHED = {
     **{f"arm_fir_{k}_batch": (C.c_int, [P(arm_fir_interpolate_instance), C.c_void_p, C.c_void_p, C.c_uint32,
                                         C.c_uint32, C.c_void_p, C.c_void_p])
        for k in ("interpolate_f32", "interpolate_q15", "interpolate_q31")},
+    **{f"arm_fir_lattice_{t}_batch": (C.c_int, [P(arm_fir_lattice_instance), C.c_void_p, C.c_void_p, C.c_uint32,
+                                                C.c_uint32, C.c_void_p, C.c_void_p]) for t in ("f32", "q31", "q15")},
     **{f"arm_fir_sparse_{t}_batch": (C.c_int, [P(arm_fir_sparse_instance), C.c_void_p, C.c_void_p, C.c_uint32,
                                                C.c_uint32, C.c_void_p, C.c_void_p]) for t in ("f32", "q31", "q15", "q7")},
     "arm_mat_mult_f32_batch": (C.c_int, [P(arm_matrix_instance_f32), P(arm_matrix_instance_f32),

@@ -590,6 +590,54 @@ arm_status sparse_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uin
   return ARM_MATH_SUCCESS;
 }
 
+// ---- FIR lattice ----------------------------------------------------------------------------
+// Drop-in: state (numStages words, host or device) in, filter, state out (arm_fir_lattice_f32.c);
+// the kernel reads the old state from its own copy, so in-place device state is fine.
+template <typename T, typename Inst>
+void lattice_init(Inst* S, uint16_t numStages, const T* pCoeffs, T* pState) {
+  if (!S) return;
+  S->numStages = numStages; S->pCoeffs = pCoeffs; S->pState = pState;     // arm_fir_lattice_init_f32.c
+  if (pState && numStages) zero_words(pState, sizeof(T) * numStages, "arm_fir_lattice_init");
+}
+
+template <typename T, typename Inst>
+void lattice_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B, int op, const char* what) {
+  if (!S || !S->pState || !S->pCoeffs || S->numStages == 0 || B == 0) return;
+  const int M = S->numStages;
+  hipStream_t st = sync_stream();
+  bool ok = true;
+  const T* dc = device_coeffs<T>(S->pCoeffs, M, &ok);
+  if (!ok) { set_error(hipErrorOutOfMemory, what); return; }
+  const bool dstate = is_device_ptr(S->pState), dsrc = is_device_ptr(pSrc), ddst = is_device_ptr(pDst);
+  const size_t sb = sizeof(T) * (size_t)B, hb = sizeof(T) * (size_t)M;
+  T* dhist = dstate ? S->pState : (T*)scratch(hb + 16, 2);
+  const T* dsr = dsrc ? pSrc : (const T*)scratch(sb, 3);
+  T* dds = ddst ? pDst : (T*)scratch(sb + 16, 4);
+  if (!dhist || !dsr || !dds) { set_error(hipErrorOutOfMemory, what); return; }
+  HostIO io(st);
+  hipError_t e = hipSuccess;
+  if (!dstate) e = io.in(dhist, S->pState, hb);
+  if (e == hipSuccess && !dsrc) e = io.in((void*)dsr, pSrc, sb);
+  if (e == hipSuccess) e = fir_lattice_run(op, dc, M, dsr, dds, B, 1, dhist, st);
+  if (e == hipSuccess && !ddst) e = io.out(pDst, dds, sb);
+  if (e == hipSuccess && !dstate) e = io.out(S->pState, dhist, hb);
+  if (e == hipSuccess) e = io.finish();
+  if (e != hipSuccess) set_error(e, what);
+}
+
+template <typename T, typename Inst>
+arm_status lattice_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uint32_t batch, T* d_state,
+                         void* stream, int op, const char* what) {
+  if (!S || !S->pCoeffs || S->numStages == 0) return ARM_MATH_ARGUMENT_ERROR;
+  if (batch && B && (!d_src || !d_dst || !d_state)) return ARM_MATH_ARGUMENT_ERROR;
+  bool ok = true;
+  const T* dc = device_coeffs<T>(S->pCoeffs, S->numStages, &ok);
+  if (!ok) { set_error(hipErrorOutOfMemory, what); return ARM_MATH_ARGUMENT_ERROR; }
+  hipError_t e = fir_lattice_run(op, dc, S->numStages, d_src, d_dst, B, batch, d_state, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(e, what); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
+}
+
 // ---- convolution / correlation family ------------------------------------------------
 // How each reference function maps onto one ConvJob (conv.hip):
 //   conv (exact):      x = pSrcA, h = pSrcB, all srcALen + srcBLen - 1 outputs forward;
@@ -1124,6 +1172,22 @@ MI355X_SPARSE(q31, q31_t, kSpQ31)
 MI355X_SPARSE(q15, q15_t, kSpQ15)
 MI355X_SPARSE(q7, q7_t, kSpQ7)
 #undef MI355X_SPARSE
+#define MI355X_LATTICE(T, CT, OP)                                                                       \
+  void arm_fir_lattice_init_##T(arm_fir_lattice_instance_##T* S, uint16_t numStages, const CT* pCoeffs,  \
+                                CT* pState) {                                                           \
+    lattice_init(S, numStages, pCoeffs, pState);                                                        \
+  }                                                                                                     \
+  void arm_fir_lattice_##T(const arm_fir_lattice_instance_##T* S, const CT* pSrc, CT* pDst, uint32_t blockSize) { \
+    lattice_sync(S, pSrc, pDst, blockSize, OP, "arm_fir_lattice_" #T);                                  \
+  }                                                                                                     \
+  arm_status arm_fir_lattice_##T##_batch(const arm_fir_lattice_instance_##T* S, const CT* d_src, CT* d_dst, \
+                                         uint32_t blockSize, uint32_t batch, CT* d_state, void* stream) { \
+    return lattice_batch(S, d_src, d_dst, blockSize, batch, d_state, stream, OP, "arm_fir_lattice_" #T "_batch"); \
+  }
+MI355X_LATTICE(f32, float32_t, kLatF32)
+MI355X_LATTICE(q31, q31_t, kLatQ31)
+MI355X_LATTICE(q15, q15_t, kLatQ15)
+#undef MI355X_LATTICE
 void arm_fir_sparse_f32(arm_fir_sparse_instance_f32* S, const float32_t* pSrc, float32_t* pDst, float32_t* pScratchIn,
                         uint32_t blockSize) {
   (void)pScratchIn;

@@ -83,6 +83,11 @@ enum SpOp { kSpF32 = 0, kSpQ31 = 1, kSpQ15 = 2, kSpQ7 = 3 };
 hipError_t fir_sparse_run(int op, const void* coeffs, const int32_t* delays, int num_taps, int max_delay,
                           const void* src, void* dst, uint32_t block_size, uint32_t batch, void* hist, int circ_len,
                           int circ_r0, hipStream_t st);
+// FIR lattice (fir_lattice.hip): `batch` streams sharing numStages reflection coefficients;
+// state [batch][numStages] = g_m at each stream's previous sample (updated in place).
+enum LatOp { kLatF32 = 0, kLatQ31 = 1, kLatQ15 = 2 };
+hipError_t fir_lattice_run(int op, const void* coeffs, int num_stages, const void* src, void* dst,
+                           uint32_t block_size, uint32_t batch, void* state, hipStream_t st);
 
 // MFCC f32 around the batched RFFT (mfcc_f32.hip): frame normalisation + window, then the
 // spectrum -> Mel -> log -> DCT tail.  post needs mfcc_f32_post_lds(n, nb_mel) bytes of LDS.

@@ -195,6 +195,18 @@ MI355X_SPARSE_INST(q15, q15_t)
 MI355X_SPARSE_INST(q7, q7_t)
 #undef MI355X_SPARSE_INST
 
+/* FIR lattice instances (Include/dsp/filtering_functions.h:1312-1340), same layout per type. */
+#define MI355X_LATTICE_INST(T, ET)                                                              \
+  typedef struct {                                                                              \
+          uint16_t numStages;                                                                   \
+          ET      *pState;     /* numStages words: g_m at the previous sample */                \
+    const ET      *pCoeffs;    /* numStages reflection coefficients */                          \
+  } arm_fir_lattice_instance_##T;
+MI355X_LATTICE_INST(q15, q15_t)
+MI355X_LATTICE_INST(q31, q31_t)
+MI355X_LATTICE_INST(f32, float32_t)
+#undef MI355X_LATTICE_INST
+
 /* ---- matrix instances: Include/dsp/matrix_functions.h:118-123 (f32), :139-143 (q7),
  * :139-144 (q15), :149-154 (q31) */
 typedef struct {
@@ -478,6 +490,24 @@ void arm_fir_sparse_q15(arm_fir_sparse_instance_q15 *S, const q15_t *pSrc, q15_t
                         q31_t *pScratchOut, uint32_t blockSize);
 void arm_fir_sparse_q7(arm_fir_sparse_instance_q7 *S, const q7_t *pSrc, q7_t *pDst, q7_t *pScratchIn,
                        q31_t *pScratchOut, uint32_t blockSize);
+
+/* ===================================================================================
+ * FIR lattice (widening).  Prototypes: Include/dsp/filtering_functions.h:1350-1410.
+ * Reference bodies: Source/FilteringFunctions/arm_fir_lattice_{f32,q31,q15}.c, inits
+ * arm_fir_lattice_init_*.c (zero numStages state words).  f_m(n) = g_{m-1}(n-1) k_m +
+ * f_{m-1}(n), g_m(n) = f_{m-1}(n) k_m + g_{m-1}(n-1), y = f_M: f32 mul then add; q31
+ * ((q31)((q63 a k) >> 32) << 1) + b with wrap; q15 __SSAT(((a k) >> 15) + b, 16).
+ * =================================================================================== */
+void arm_fir_lattice_init_f32(arm_fir_lattice_instance_f32 *S, uint16_t numStages, const float32_t *pCoeffs,
+                              float32_t *pState);
+void arm_fir_lattice_init_q31(arm_fir_lattice_instance_q31 *S, uint16_t numStages, const q31_t *pCoeffs,
+                              q31_t *pState);
+void arm_fir_lattice_init_q15(arm_fir_lattice_instance_q15 *S, uint16_t numStages, const q15_t *pCoeffs,
+                              q15_t *pState);
+void arm_fir_lattice_f32(const arm_fir_lattice_instance_f32 *S, const float32_t *pSrc, float32_t *pDst,
+                         uint32_t blockSize);
+void arm_fir_lattice_q31(const arm_fir_lattice_instance_q31 *S, const q31_t *pSrc, q31_t *pDst, uint32_t blockSize);
+void arm_fir_lattice_q15(const arm_fir_lattice_instance_q15 *S, const q15_t *pSrc, q15_t *pDst, uint32_t blockSize);
 
 /* ===================================================================================
  * Convolution.  Prototypes: Include/dsp/filtering_functions.h

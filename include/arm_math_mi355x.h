@@ -118,6 +118,16 @@ arm_status arm_fir_sparse_q15_batch(const arm_fir_sparse_instance_q15 *S, const 
 arm_status arm_fir_sparse_q7_batch(const arm_fir_sparse_instance_q7 *S, const q7_t *d_src, q7_t *d_dst,
                                    uint32_t blockSize, uint32_t batch, q7_t *d_hist, void *stream);
 
+/* FIR lattice over `batch` independent streams sharing S's coefficients: d_src / d_dst
+ * [batch][blockSize], d_state [batch][numStages] (each stream's state in the reference's
+ * layout, zero-initialise; updated in place).  Per-stream semantics: arm_fir_lattice_*. */
+arm_status arm_fir_lattice_f32_batch(const arm_fir_lattice_instance_f32 *S, const float32_t *d_src, float32_t *d_dst,
+                                     uint32_t blockSize, uint32_t batch, float32_t *d_state, void *stream);
+arm_status arm_fir_lattice_q31_batch(const arm_fir_lattice_instance_q31 *S, const q31_t *d_src, q31_t *d_dst,
+                                     uint32_t blockSize, uint32_t batch, q31_t *d_state, void *stream);
+arm_status arm_fir_lattice_q15_batch(const arm_fir_lattice_instance_q15 *S, const q15_t *d_src, q15_t *d_dst,
+                                     uint32_t blockSize, uint32_t batch, q15_t *d_state, void *stream);
+
 /* Convolution of `batch` pairs: item i convolves d_a + i*strideA (srcALen samples) with
  * d_b + i*strideB (srcBLen samples; strideB = 0 shares one kernel) into
  * d_dst + i*(srcALen + srcBLen - 1).  Per-item semantics: arm_conv_f32 / _q15 / _q31. */

@@ -43,6 +43,8 @@ SRCS := \
   $(F)/arm_fir_sparse_f32.c $(F)/arm_fir_sparse_q31.c $(F)/arm_fir_sparse_q15.c $(F)/arm_fir_sparse_q7.c \
   $(F)/arm_fir_sparse_init_f32.c $(F)/arm_fir_sparse_init_q31.c $(F)/arm_fir_sparse_init_q15.c \
   $(F)/arm_fir_sparse_init_q7.c \
+  $(F)/arm_fir_lattice_f32.c $(F)/arm_fir_lattice_q31.c $(F)/arm_fir_lattice_q15.c \
+  $(F)/arm_fir_lattice_init_f32.c $(F)/arm_fir_lattice_init_q31.c $(F)/arm_fir_lattice_init_q15.c \
   $(F)/arm_fir_q7.c $(F)/arm_fir_init_q7.c $(F)/arm_conv_q7.c $(F)/arm_conv_partial_q7.c $(F)/arm_correlate_q7.c \
   $(M)/arm_mat_mult_f32.c $(M)/arm_mat_init_f32.c $(M)/arm_mat_vec_mult_f32.c \
   $(M)/arm_mat_mult_q15.c $(M)/arm_mat_mult_q31.c $(M)/arm_mat_mult_fast_q15.c $(M)/arm_mat_mult_fast_q31.c $(M)/arm_mat_init_q15.c $(M)/arm_mat_init_q31.c \

@@ -57,4 +57,18 @@ void oracle_arm_fir_sparse_q7(arm_fir_sparse_instance_q7 *S, const int8_t *pSrc,
                               int32_t *pScratchOut, uint32_t blockSize);
 #undef ORACLE_SPARSE_PROTO
 
+/* FIR lattice (oracle_multirate.c) */
+void oracle_arm_fir_lattice_init_f32(arm_fir_lattice_instance_f32 *S, uint16_t numStages, const float *pCoeffs,
+                                     float *pState);
+void oracle_arm_fir_lattice_init_q31(arm_fir_lattice_instance_q31 *S, uint16_t numStages, const int32_t *pCoeffs,
+                                     int32_t *pState);
+void oracle_arm_fir_lattice_init_q15(arm_fir_lattice_instance_q15 *S, uint16_t numStages, const int16_t *pCoeffs,
+                                     int16_t *pState);
+void oracle_arm_fir_lattice_f32(const arm_fir_lattice_instance_f32 *S, const float *pSrc, float *pDst,
+                                uint32_t blockSize);
+void oracle_arm_fir_lattice_q31(const arm_fir_lattice_instance_q31 *S, const int32_t *pSrc, int32_t *pDst,
+                                uint32_t blockSize);
+void oracle_arm_fir_lattice_q15(const arm_fir_lattice_instance_q15 *S, const int16_t *pSrc, int16_t *pDst,
+                                uint32_t blockSize);
+
 #endif

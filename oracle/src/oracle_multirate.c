@@ -22,7 +22,11 @@
  *     later taps add: f32 mul then add; q31 (q31)((q63 x c) >> 32) with wrap, output << 1; q15 /
  *     q7 q31 products with wrap, __SSAT(>> 15, 16) / __SSAT(>> 7, 8).  arm_fir_sparse_init_*.c
  *     zeroes maxDelay + blockSize words and stateIndex.
- * Pinned against oracle/_ref by tests/test_multirate.py and tests/test_sparse.py. */
+ *   arm_fir_lattice_{f32,q31,q15}.c: per sample f = g = x(n); stage m: f' = g_{m-1}(n-1) k + f,
+ *     g' = f k + g_{m-1}(n-1) (f32 mul then add; q31 ((q31)((q63 a k) >> 32) << 1) + b with
+ *     wrap; q15 __SSAT(((a k) >> 15) + b, 16)), state[m-1] <- g_{m-1}(n); y = f_M.
+ * Pinned against oracle/_ref by tests/test_multirate.py, tests/test_sparse.py and
+ * tests/test_lattice.py. */
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -194,3 +198,34 @@ void oracle_arm_fir_sparse_q15(arm_fir_sparse_instance_q15 *S, const int16_t *pS
                                int32_t *pScratchOut, uint32_t blockSize) { SPARSE_RUN(q15, SP_Q15); }
 void oracle_arm_fir_sparse_q7(arm_fir_sparse_instance_q7 *S, const int8_t *pSrc, int8_t *pDst, int8_t *pScratchIn,
                               int32_t *pScratchOut, uint32_t blockSize) { SPARSE_RUN(q7, SP_Q7); }
+
+/* ---- FIR lattice ---- */
+static float lat_f32(float a, float k, float b) { const float p = a * k; return p + b; }
+static int32_t lat_q31(int32_t a, int32_t k, int32_t b) {
+  return (int32_t)(((uint32_t)(int32_t)(((int64_t)a * k) >> 32) << 1) + (uint32_t)b);
+}
+static int32_t lat_q15(int32_t a, int32_t k, int32_t b) { return sat16(((a * k) >> 15) + (int64_t)b); }
+
+#define LATTICE(T, ET, VT, STEP)                                                                                \
+  void oracle_arm_fir_lattice_init_##T(arm_fir_lattice_instance_##T *S, uint16_t numStages, const ET *pCoeffs,  \
+                                       ET *pState) {                                                            \
+    S->numStages = numStages; S->pCoeffs = pCoeffs; S->pState = pState;                                         \
+    memset(pState, 0, sizeof(ET) * numStages);                                                                  \
+  }                                                                                                             \
+  void oracle_arm_fir_lattice_##T(const arm_fir_lattice_instance_##T *S, const ET *pSrc, ET *pDst,              \
+                                  uint32_t blockSize) {                                                         \
+    ET *g = S->pState;                                                                                          \
+    for (uint32_t n = 0; n < blockSize; ++n) {                                                                  \
+      VT f = pSrc[n], gc = f;                                                                                   \
+      for (uint16_t m = 0; m < S->numStages; ++m) {                                                             \
+        const VT k = S->pCoeffs[m], gp = g[m], fo = f;                                                          \
+        g[m] = (ET)gc;                                                                                          \
+        f = STEP(gp, k, fo);                                                                                    \
+        gc = STEP(fo, k, gp);                                                                                   \
+      }                                                                                                         \
+      pDst[n] = (ET)f;                                                                                          \
+    }                                                                                                           \
+  }
+LATTICE(f32, float, float, lat_f32)
+LATTICE(q31, int32_t, int32_t, lat_q31)
+LATTICE(q15, int16_t, int32_t, lat_q15)

@@ -145,6 +145,28 @@ class Host:
         self._keep = (c, state)
         return st, outs, state.copy()
 
+    def lattice(self, kind, coeffs, blocks, state_mem=None):
+        """Stream `blocks` through one arm_fir_lattice_<kind> instance: returns (outputs,
+        final state).  state_mem(n, dtype) may supply the state buffer as (pointer, reader)."""
+        dt = DTYPE[kind]
+        c = np.ascontiguousarray(coeffs, dtype=dt)
+        inst = _abi.arm_fir_lattice_instance()
+        if state_mem is None:
+            state = np.full(len(c), 5, dtype=dt)                  # init must zero it
+            sptr, sread = state.ctypes.data, state.copy
+        else:
+            sptr, sread = state_mem(len(c), dt)
+        self.fn(f"arm_fir_lattice_init_{kind}")(C.byref(inst), len(c), c.ctypes.data, sptr)
+        f = self.fn(f"arm_fir_lattice_{kind}")
+        outs = []
+        for b in blocks:
+            b = np.ascontiguousarray(b, dtype=dt)
+            y = np.zeros(len(b), dtype=dt)
+            f(C.byref(inst), b.ctypes.data, y.ctypes.data, len(b))
+            outs.append(y)
+        self._keep = (c,)
+        return outs, sread()
+
     def sparse(self, kind, coeffs, delays, max_delay, blocks, block_size=None, state_mem=None):
         """Stream `blocks` through one arm_fir_sparse_<kind> instance: returns (outputs, final
         circular state, final stateIndex).  state_mem(n, dtype) may supply the state buffer

@@ -47,6 +47,10 @@ int main(void) {
     F(arm_fir_interpolate_instance_f32, phaseLength) F(arm_fir_interpolate_instance_f32, pCoeffs)
     F(arm_fir_interpolate_instance_f32, pState) E()
   S(arm_fir_instance_q7) F(arm_fir_instance_q7, numTaps) F(arm_fir_instance_q7, pState) F(arm_fir_instance_q7, pCoeffs) E()
+  S(arm_fir_lattice_instance_q15) F(arm_fir_lattice_instance_q15, numStages) F(arm_fir_lattice_instance_q15, pState)
+    F(arm_fir_lattice_instance_q15, pCoeffs) E()
+  S(arm_fir_lattice_instance_f32) F(arm_fir_lattice_instance_f32, numStages) F(arm_fir_lattice_instance_f32, pState)
+    F(arm_fir_lattice_instance_f32, pCoeffs) E()
   S(arm_rfft_instance_q31) F(arm_rfft_instance_q31, fftLenReal) F(arm_rfft_instance_q31, ifftFlagR)
     F(arm_rfft_instance_q31, bitReverseFlagR) F(arm_rfft_instance_q31, twidCoefRModifier)
     F(arm_rfft_instance_q31, pTwiddleAReal) F(arm_rfft_instance_q31, pTwiddleBReal) F(arm_rfft_instance_q31, pCfft) E()

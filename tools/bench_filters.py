@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Throughput of the filtering functions outside bench.py's workloads (round 2 additions):
-arm_fir_q7, arm_fir_decimate_*, arm_fir_interpolate_*, arm_fir_sparse_* through the batched device API on one
+arm_fir_q7, arm_fir_decimate_*, arm_fir_interpolate_*, arm_fir_sparse_*, arm_fir_lattice_* through the batched device API on one
 GPU, HIP-event timed on the launch stream after a clock-settle phase, each with a bit-exact
 check of 2 streams against the CPU checker (the reference build when present).
 Usage: python tools/bench_filters.py [name ...]  -> one JSON line per workload."""
@@ -22,6 +22,7 @@ import refs  # noqa: E402
 
 BATCH, BLOCK, TAPS = 1 << 16, 4096, 128
 SP_TAPS, SP_DELAY = 32, 1024            # sparse: 32 nonzero taps at delays in [0, 1024]
+LAT_STAGES = 32                         # lattice: 32 stages
 # name: (function, factor, dtype)
 CASES = {
     "fir_q7": ("q7", 1, "q7"),
@@ -35,6 +36,9 @@ CASES = {
     "fir_sparse_q31": ("sparse_q31", 1, "q31"),
     "fir_sparse_q15": ("sparse_q15", 1, "q15"),
     "fir_sparse_q7": ("sparse_q7", 1, "q7"),
+    "fir_lattice_f32": ("lattice_f32", 1, "f32"),
+    "fir_lattice_q31": ("lattice_q31", 1, "q31"),
+    "fir_lattice_q15": ("lattice_q15", 1, "q15"),
 }
 TDT = {"f32": torch.float32, "q15": torch.int16, "q31": torch.int32, "q7": torch.int8}
 
@@ -71,8 +75,11 @@ def run(name):
     rng = np.random.default_rng(7)
     dt = refs.DTYPE[kind]
     sparse = fn.startswith("sparse")
-    taps = SP_TAPS if sparse else TAPS
-    if kind == "f32":
+    lattice = fn.startswith("lattice")
+    taps = SP_TAPS if sparse else LAT_STAGES if lattice else TAPS
+    if lattice and kind == "f32":
+        c = rng.uniform(-0.9, 0.9, taps).astype(np.float32)
+    elif kind == "f32":
         c = (rng.standard_normal(taps) / np.sqrt(taps)).astype(np.float32)
     else:
         info = np.iinfo(dt)
@@ -88,7 +95,10 @@ def run(name):
                             dtype=torch.int64).to(TDT[kind])
     dc = torch.from_numpy(c.copy()).cuda()
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    if sparse:
+    if lattice:
+        S = _abi.arm_fir_lattice_instance(numStages=taps, pState=None, pCoeffs=dc.data_ptr())
+        H, nout, f = taps, BLOCK, getattr(dsp.lib, f"arm_fir_{fn}_batch")
+    elif sparse:
         dd = torch.from_numpy(delays.copy()).cuda()
         S = _abi.arm_fir_sparse_instance(numTaps=taps, pCoeffs=dc.data_ptr(), maxDelay=SP_DELAY,
                                          pTapDelay=dd.data_ptr())
@@ -120,17 +130,19 @@ def run(name):
     ok = True
     for i in range(2):
         x = src[i].cpu().numpy()
-        if sparse:
+        if lattice:
+            want = host.lattice(kind, c, [x])[0][0]
+        elif sparse:
             want = host.sparse(kind, c, delays, SP_DELAY, [x])[0][0]
         elif fn == "q7":
             want = host.fir("q7", c, [x])[0][0]
         else:
             want = host.multirate(fn, factor, c, [x])[1][0]
         ok &= d2[i].cpu().numpy().tobytes() == want.tobytes()
-    macs = BATCH * (BLOCK * taps if fn == "q7" or sparse else (BLOCK // factor) * TAPS if fn.startswith("decimate")
+    macs = BATCH * (BLOCK * taps * (2 if lattice else 1) if fn == "q7" or sparse or lattice else (BLOCK // factor) * TAPS if fn.startswith("decimate")
                     else BLOCK * TAPS)
     esz = np.dtype(dt).itemsize
-    extra = {"maxDelay": SP_DELAY} if sparse else {}
+    extra = {"maxDelay": SP_DELAY} if sparse else {"numStages": taps} if lattice else {}
     return {"workload": name, "function": f"arm_fir_{fn}", "numTaps": taps, **extra, "factor": factor, "blockSize": BLOCK,
             "batch": BATCH, "avg_kernel_ms": round(ms, 4),
             "input_gsamples_per_s": round(BATCH * BLOCK / (ms * 1e-3) * 1e-9, 2),

@@ -11,7 +11,7 @@ FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -Wno-unused-
 OBJS=""
 for src in csrc/*.hip; do
   f=$(basename $src .hip)
-  EXTRA=""; { [ $f = fir ] || [ $f = conv ]; } && EXTRA="-fno-slp-vectorize"
+  EXTRA=""; { [ $f = fir ] || [ $f = conv ] || [ $f = fir_lattice ]; } && EXTRA="-fno-slp-vectorize"
   /opt/rocm/bin/hipcc $FLAGS $EXTRA -c $src -o $OUT/$f.o &
   OBJS="$OBJS $OUT/$f.o"
 done
