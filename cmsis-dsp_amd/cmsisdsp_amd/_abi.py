@@ -119,6 +119,10 @@ CONV_PARTIAL = ("conv_partial_f32", "conv_partial_q15", "conv_partial_q31", "con
 # product only (the oracle restates them as arm_conv_fast_* over the range; the reference's
 # own bodies are memory-unsafe for most ranges)
 CONV_PARTIAL_FAST = ("conv_partial_fast_q15", "conv_partial_fast_q31")
+# scratch-buffer forms: name -> number of trailing scratch pointers
+CONV_OPT_FULL = {"conv_opt_q15": 2, "conv_fast_opt_q15": 2, "conv_opt_q7": 2, "correlate_opt_q15": 1,
+                 "correlate_fast_opt_q15": 1, "correlate_opt_q7": 2}
+CONV_OPT_PARTIAL = ("conv_partial_opt_q15", "conv_partial_fast_opt_q15", "conv_partial_opt_q7")
 
 # name -> (restype, argtypes): the drop-in surface of include/arm_math.h
 DROPIN = {
@@ -152,6 +156,10 @@ DROPIN = {
     **{f"arm_fir_{k}": (None, [P(arm_fir_interpolate_instance), C.c_void_p, C.c_void_p, C.c_uint32])
        for k in ("interpolate_f32", "interpolate_q15", "interpolate_q31")},
     "arm_fir_q7": (None, [P(arm_fir_instance_q7), C.c_void_p, C.c_void_p, C.c_uint32]),
+    **{f"arm_{k}": (None, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p] + [C.c_void_p] * n)
+       for k, n in CONV_OPT_FULL.items()},
+    **{f"arm_{k}": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
+                              C.c_void_p, C.c_void_p]) for k in CONV_OPT_PARTIAL},
     **{f"arm_fir_lattice_init_{t}": (None, [P(arm_fir_lattice_instance), C.c_uint16, C.c_void_p, C.c_void_p])
        for t in ("f32", "q31", "q15")},
     **{f"arm_fir_lattice_{t}": (None, [P(arm_fir_lattice_instance), C.c_void_p, C.c_void_p, C.c_uint32])

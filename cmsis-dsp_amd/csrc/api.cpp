@@ -1104,6 +1104,65 @@ MI355X_CONV_PARTIAL(arm_conv_partial_fast_q15, q15_t, int16_t, kConvFastQ15)
 MI355X_CONV_PARTIAL(arm_conv_partial_fast_q31, q31_t, int32_t, kConvFastQ31)
 #undef MI355X_CONV_PARTIAL
 
+// The scratch-buffer ("_opt") forms (arm_conv_opt_q15.c, arm_conv_opt_q7.c,
+// arm_correlate_opt_q15.c, arm_correlate_opt_q7.c, arm_conv_partial_opt_q15.c, _q7.c): the
+// exact sums of the plain functions (tests/test_conv_opt.py pins that on the reference build),
+// so they run the same kernels; the fast q15 ones are a modular sum with a saturating output
+// (kConvFastOptQ15).  The scratch buffers are not needed.
+void arm_conv_opt_q15(const q15_t* pSrcA, uint32_t srcALen, const q15_t* pSrcB, uint32_t srcBLen, q15_t* pDst,
+                      q15_t* pScratch1, q15_t* pScratch2) {
+  (void)pScratch1; (void)pScratch2;
+  arm_conv_q15(pSrcA, srcALen, pSrcB, srcBLen, pDst);
+}
+void arm_conv_opt_q7(const q7_t* pSrcA, uint32_t srcALen, const q7_t* pSrcB, uint32_t srcBLen, q7_t* pDst,
+                     q15_t* pScratch1, q15_t* pScratch2) {
+  (void)pScratch1; (void)pScratch2;
+  arm_conv_q7(pSrcA, srcALen, pSrcB, srcBLen, pDst);
+}
+void arm_correlate_opt_q15(const q15_t* pSrcA, uint32_t srcALen, const q15_t* pSrcB, uint32_t srcBLen, q15_t* pDst,
+                           q15_t* pScratch) {
+  (void)pScratch;
+  arm_correlate_q15(pSrcA, srcALen, pSrcB, srcBLen, pDst);
+}
+void arm_correlate_opt_q7(const q7_t* pSrcA, uint32_t srcALen, const q7_t* pSrcB, uint32_t srcBLen, q7_t* pDst,
+                          q15_t* pScratch1, q15_t* pScratch2) {
+  (void)pScratch1; (void)pScratch2;
+  arm_correlate_q7(pSrcA, srcALen, pSrcB, srcBLen, pDst);
+}
+arm_status arm_conv_partial_opt_q15(const q15_t* pSrcA, uint32_t srcALen, const q15_t* pSrcB, uint32_t srcBLen,
+                                    q15_t* pDst, uint32_t firstIndex, uint32_t numPoints, q15_t* pScratch1,
+                                    q15_t* pScratch2) {
+  (void)pScratch1; (void)pScratch2;
+  return arm_conv_partial_q15(pSrcA, srcALen, pSrcB, srcBLen, pDst, firstIndex, numPoints);
+}
+arm_status arm_conv_partial_opt_q7(const q7_t* pSrcA, uint32_t srcALen, const q7_t* pSrcB, uint32_t srcBLen,
+                                   q7_t* pDst, uint32_t firstIndex, uint32_t numPoints, q15_t* pScratch1,
+                                   q15_t* pScratch2) {
+  (void)pScratch1; (void)pScratch2;
+  return arm_conv_partial_q7(pSrcA, srcALen, pSrcB, srcBLen, pDst, firstIndex, numPoints);
+}
+void arm_conv_fast_opt_q15(const q15_t* pSrcA, uint32_t srcALen, const q15_t* pSrcB, uint32_t srcBLen, q15_t* pDst,
+                           q15_t* pScratch1, q15_t* pScratch2) {
+  (void)pScratch1; (void)pScratch2;
+  conv_family_sync<int16_t>(kConvFastOptQ15, kVarConv, pSrcA, srcALen, pSrcB, srcBLen, pDst, 0, 0,
+                            "arm_conv_fast_opt_q15");
+}
+void arm_correlate_fast_opt_q15(const q15_t* pSrcA, uint32_t srcALen, const q15_t* pSrcB, uint32_t srcBLen,
+                                q15_t* pDst, q15_t* pScratch) {
+  (void)pScratch;
+  conv_family_sync<int16_t>(kConvFastOptQ15, kVarCorr, pSrcA, srcALen, pSrcB, srcBLen, pDst, 0, 0,
+                            "arm_correlate_fast_opt_q15");
+}
+arm_status arm_conv_partial_fast_opt_q15(const q15_t* pSrcA, uint32_t srcALen, const q15_t* pSrcB, uint32_t srcBLen,
+                                         q15_t* pDst, uint32_t firstIndex, uint32_t numPoints, q15_t* pScratch1,
+                                         q15_t* pScratch2) {
+  (void)pScratch1; (void)pScratch2;
+  if (!partial_range_ok(srcALen, srcBLen, firstIndex, numPoints)) return ARM_MATH_ARGUMENT_ERROR;
+  conv_family_sync<int16_t>(kConvFastOptQ15, kVarPartial, pSrcA, srcALen, pSrcB, srcBLen, pDst, firstIndex,
+                            numPoints, "arm_conv_partial_fast_opt_q15");
+  return ARM_MATH_SUCCESS;
+}
+
 // ---- multirate FIR ---------------------------------------------------------------------
 arm_status arm_fir_decimate_init_f32(arm_fir_decimate_instance_f32* S, uint16_t numTaps, uint8_t M,
                                      const float32_t* pCoeffs, float32_t* pState, uint32_t blockSize) {

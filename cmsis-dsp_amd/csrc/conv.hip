@@ -65,6 +65,14 @@ template <> struct ConvT<kConvFastQ15> {
   static __device__ __forceinline__ Acc mac(Acc a, T w, T c) { return a + (uint32_t)((int32_t)w * (int32_t)c); }
   static __device__ __forceinline__ T out(Acc a) { return (T)((int32_t)a >> 15); }
 };
+// arm_conv_fast_opt_q15.c / arm_correlate_fast_opt_q15.c / arm_conv_partial_fast_opt_q15.c:
+// __SMLAD over zero-padded scratch copies (no single-sample high-halfword term), a modular q31
+// sum, output __SSAT(acc >> 15, 16) -- saturating, unlike arm_conv_fast_q15's (q15) cast.
+template <> struct ConvT<kConvFastOptQ15> {
+  using T = int16_t; using Acc = uint32_t;
+  static __device__ __forceinline__ Acc mac(Acc a, T w, T c) { return a + (uint32_t)((int32_t)w * (int32_t)c); }
+  static __device__ __forceinline__ T out(Acc a) { return (T)ssat16((int32_t)a >> 15); }
+};
 template <> struct ConvT<kConvQ7> {
   using T = int8_t; using Acc = uint32_t;
   static __device__ __forceinline__ Acc mac(Acc a, T w, T c) { return a + (uint32_t)((int32_t)w * (int32_t)c); }
@@ -267,6 +275,7 @@ hipError_t conv_family_run(const ConvJob& j, hipStream_t st) {
     MI355X_CONV_CASE(kConvFastQ15)
     MI355X_CONV_CASE(kConvFastQ31)
     MI355X_CONV_CASE(kConvQ7)
+    MI355X_CONV_CASE(kConvFastOptQ15)
     default: return hipErrorInvalidValue;
   }
 #undef MI355X_CONV_CASE

@@ -115,7 +115,8 @@ hipError_t mat_mult_f32_launch(int m, int k, int n, const float* a, const float*
 //   (corr: correlation), for n in [first, first + num), stored at
 //   y[item * sy + yoff + ydir * n].  x / h item strides sx / sh (0 = shared).
 // kConvFastQ15 requires A >= B (the reference's x is the longer input).
-enum ConvOp { kConvF32 = 0, kConvQ15 = 1, kConvQ31 = 2, kConvFastQ15 = 3, kConvFastQ31 = 4, kConvQ7 = 5 };
+enum ConvOp { kConvF32 = 0, kConvQ15 = 1, kConvQ31 = 2, kConvFastQ15 = 3, kConvFastQ31 = 4, kConvQ7 = 5,
+              kConvFastOptQ15 = 6 };
 struct ConvJob {
   int op;
   bool corr;

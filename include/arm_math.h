@@ -571,6 +571,39 @@ arm_status arm_conv_partial_q7(const q7_t *pSrcA, uint32_t srcALen, const q7_t *
                                q7_t *pDst, uint32_t firstIndex, uint32_t numPoints);
 void arm_correlate_q7(const q7_t *pSrcA, uint32_t srcALen, const q7_t *pSrcB, uint32_t srcBLen, q7_t *pDst);
 
+/* Scratch-buffer ("_opt") forms.  Prototypes: Include/dsp/filtering_functions.h:469-476,
+ * :521-528, :573-580, :633-642, :700-709, :767-776, :1906-1912, :1956-1962, :2007-2014.
+ * Reference bodies: Source/FilteringFunctions/arm_conv_opt_q15.c, arm_conv_opt_q7.c,
+ * arm_conv_fast_opt_q15.c, arm_conv_partial_opt_q15.c, arm_conv_partial_opt_q7.c,
+ * arm_conv_partial_fast_opt_q15.c, arm_correlate_opt_q15.c, arm_correlate_opt_q7.c,
+ * arm_correlate_fast_opt_q15.c.  The exact forms return the plain functions' words; the fast
+ * q15 forms are a modular q31 sum with __SSAT(acc >> 15, 16) (arm_conv_fast_q15 casts
+ * instead).  The scratch buffers may be NULL: the GPU path does not use them.  (The exact q15
+ * forms accumulate exactly, as the Arm SMLALD instruction does; the reference's host C
+ * emulation of __SMLALD, Include/dsp/none.h:503-505, wraps a pair of two (-32768)^2 products
+ * in int32.) */
+void arm_conv_opt_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB, uint32_t srcBLen, q15_t *pDst,
+                      q15_t *pScratch1, q15_t *pScratch2);
+void arm_conv_fast_opt_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB, uint32_t srcBLen, q15_t *pDst,
+                           q15_t *pScratch1, q15_t *pScratch2);
+void arm_conv_opt_q7(const q7_t *pSrcA, uint32_t srcALen, const q7_t *pSrcB, uint32_t srcBLen, q7_t *pDst,
+                     q15_t *pScratch1, q15_t *pScratch2);
+arm_status arm_conv_partial_opt_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB, uint32_t srcBLen,
+                                    q15_t *pDst, uint32_t firstIndex, uint32_t numPoints, q15_t *pScratch1,
+                                    q15_t *pScratch2);
+arm_status arm_conv_partial_fast_opt_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB, uint32_t srcBLen,
+                                         q15_t *pDst, uint32_t firstIndex, uint32_t numPoints, q15_t *pScratch1,
+                                         q15_t *pScratch2);
+arm_status arm_conv_partial_opt_q7(const q7_t *pSrcA, uint32_t srcALen, const q7_t *pSrcB, uint32_t srcBLen,
+                                   q7_t *pDst, uint32_t firstIndex, uint32_t numPoints, q15_t *pScratch1,
+                                   q15_t *pScratch2);
+void arm_correlate_opt_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB, uint32_t srcBLen, q15_t *pDst,
+                           q15_t *pScratch);
+void arm_correlate_fast_opt_q15(const q15_t *pSrcA, uint32_t srcALen, const q15_t *pSrcB, uint32_t srcBLen,
+                                q15_t *pDst, q15_t *pScratch);
+void arm_correlate_opt_q7(const q7_t *pSrcA, uint32_t srcALen, const q7_t *pSrcB, uint32_t srcBLen, q7_t *pDst,
+                          q15_t *pScratch1, q15_t *pScratch2);
+
 /* ===================================================================================
  * Matrix multiply, f32.  Prototypes: Include/dsp/matrix_functions.h:341-344,630-634
  * Reference bodies: Source/MatrixFunctions/arm_mat_mult_f32.c:600-730,

@@ -18,6 +18,7 @@ B := $(REF)/Source/BasicMathFunctions
 X := $(REF)/Source/ComplexMathFunctions
 ST := $(REF)/Source/StatisticsFunctions
 FM := $(REF)/Source/FastMathFunctions
+SU := $(REF)/Source/SupportFunctions
 
 SRCS := \
   $(T)/arm_cfft_f32.c $(T)/arm_cfft_radix8_f32.c $(T)/arm_cfft_init_f32.c \
@@ -45,6 +46,10 @@ SRCS := \
   $(F)/arm_fir_sparse_init_q7.c \
   $(F)/arm_fir_lattice_f32.c $(F)/arm_fir_lattice_q31.c $(F)/arm_fir_lattice_q15.c \
   $(F)/arm_fir_lattice_init_f32.c $(F)/arm_fir_lattice_init_q31.c $(F)/arm_fir_lattice_init_q15.c \
+  $(F)/arm_conv_opt_q15.c $(F)/arm_conv_opt_q7.c $(F)/arm_conv_fast_opt_q15.c \
+  $(F)/arm_conv_partial_opt_q15.c $(F)/arm_conv_partial_opt_q7.c $(F)/arm_conv_partial_fast_opt_q15.c \
+  $(F)/arm_correlate_opt_q15.c $(F)/arm_correlate_opt_q7.c $(F)/arm_correlate_fast_opt_q15.c \
+  $(SU)/arm_copy_q15.c $(SU)/arm_fill_q15.c \
   $(F)/arm_fir_q7.c $(F)/arm_fir_init_q7.c $(F)/arm_conv_q7.c $(F)/arm_conv_partial_q7.c $(F)/arm_correlate_q7.c \
   $(M)/arm_mat_mult_f32.c $(M)/arm_mat_init_f32.c $(M)/arm_mat_vec_mult_f32.c \
   $(M)/arm_mat_mult_q15.c $(M)/arm_mat_mult_q31.c $(M)/arm_mat_mult_fast_q15.c $(M)/arm_mat_mult_fast_q31.c $(M)/arm_mat_init_q15.c $(M)/arm_mat_init_q31.c \

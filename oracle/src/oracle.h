@@ -71,4 +71,23 @@ void oracle_arm_fir_lattice_q31(const arm_fir_lattice_instance_q31 *S, const int
 void oracle_arm_fir_lattice_q15(const arm_fir_lattice_instance_q15 *S, const int16_t *pSrc, int16_t *pDst,
                                 uint32_t blockSize);
 
+/* scratch-buffer convolution forms (oracle_conv.c) */
+void oracle_arm_conv_opt_q15(const int16_t *a, uint32_t A, const int16_t *b, uint32_t B, int16_t *d, int16_t *s1,
+                             int16_t *s2);
+void oracle_arm_conv_fast_opt_q15(const int16_t *a, uint32_t A, const int16_t *b, uint32_t B, int16_t *d, int16_t *s1,
+                                  int16_t *s2);
+void oracle_arm_conv_opt_q7(const int8_t *a, uint32_t A, const int8_t *b, uint32_t B, int8_t *d, int16_t *s1,
+                            int16_t *s2);
+void oracle_arm_correlate_opt_q15(const int16_t *a, uint32_t A, const int16_t *b, uint32_t B, int16_t *d, int16_t *s);
+void oracle_arm_correlate_fast_opt_q15(const int16_t *a, uint32_t A, const int16_t *b, uint32_t B, int16_t *d,
+                                       int16_t *s);
+void oracle_arm_correlate_opt_q7(const int8_t *a, uint32_t A, const int8_t *b, uint32_t B, int8_t *d, int16_t *s1,
+                                 int16_t *s2);
+arm_status oracle_arm_conv_partial_opt_q15(const int16_t *a, uint32_t A, const int16_t *b, uint32_t B, int16_t *d,
+                                           uint32_t f, uint32_t n, int16_t *s1, int16_t *s2);
+arm_status oracle_arm_conv_partial_fast_opt_q15(const int16_t *a, uint32_t A, const int16_t *b, uint32_t B,
+                                                int16_t *d, uint32_t f, uint32_t n, int16_t *s1, int16_t *s2);
+arm_status oracle_arm_conv_partial_opt_q7(const int8_t *a, uint32_t A, const int8_t *b, uint32_t B, int8_t *d,
+                                          uint32_t f, uint32_t n, int16_t *s1, int16_t *s2);
+
 #endif

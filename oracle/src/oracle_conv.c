@@ -20,13 +20,19 @@
  *     sum of q7 x q7 products (int32 adds / __SMLAD pairs, wrapping), __SSAT(sum >> 7, 8).
  *   arm_conv_fast_q31.c / arm_correlate_fast_q31.c: sum = (q31)(((q63)sum << 32 + x*y) >> 32)
  *     per MAC (= sum + ((x*y) >> 32) mod 2^32), output sum << 1.
- * Pinned against oracle/_ref by tests/test_oracle.py::test_conv_family_oracle_equals_reference. */
+ *   the scratch-buffer forms (arm_conv_opt_q15.c, arm_conv_opt_q7.c, arm_correlate_opt_q15.c,
+ *   arm_correlate_opt_q7.c, arm_conv_partial_opt_q15.c / _q7.c): the exact sums above;
+ *   arm_conv_fast_opt_q15.c, arm_correlate_fast_opt_q15.c, arm_conv_partial_fast_opt_q15.c:
+ *   __SMLAD pairs over zero-padded scratch copies -- a modular q31 sum with no single-sample
+ *   term -- and __SSAT(sum >> 15, 16).
+ * Pinned against oracle/_ref by tests/test_oracle.py::test_conv_family_oracle_equals_reference
+ * and tests/test_conv_opt.py. */
 #include <stdint.h>
 #include <string.h>
 
 #include "oracle.h"
 
-enum { OP_F32, OP_Q15, OP_Q31, OP_FQ15, OP_FQ31, OP_Q7 };
+enum { OP_F32, OP_Q15, OP_Q31, OP_FQ15, OP_FQ31, OP_Q7, OP_FOQ15 };
 
 static int16_t sat16(int32_t v) { return (int16_t)(v > 32767 ? 32767 : v < -32768 ? -32768 : v); }
 
@@ -58,6 +64,11 @@ static void engine(int op, int corr, const void *xv, uint32_t A, const void *yv,
       for (uint32_t k = k0; k <= k1; ++k) s += (uint32_t)((int32_t)x[k] * G(int8_t));
       const int32_t v = (int32_t)s >> 7;
       ((int8_t *)out)[pos] = (int8_t)(v > 127 ? 127 : v < -128 ? -128 : v);
+    } else if (op == OP_FOQ15) {
+      const int16_t *x = xv;
+      uint32_t s = 0;
+      for (uint32_t k = k0; k <= k1; ++k) s += (uint32_t)((int32_t)x[k] * G(int16_t));
+      ((int16_t *)out)[pos] = sat16((int32_t)s >> 15);
     } else if (op == OP_FQ31) {
       const int32_t *x = xv;
       uint32_t s = 0;
@@ -119,3 +130,29 @@ void oracle_arm_conv_q7(const int8_t *a, uint32_t A, const int8_t *b, uint32_t B
 void oracle_arm_correlate_q7(const int8_t *a, uint32_t A, const int8_t *b, uint32_t B, int8_t *d) { correlate(OP_Q7, a, A, b, B, d); }
 arm_status oracle_arm_conv_partial_q7(const int8_t *a, uint32_t A, const int8_t *b, uint32_t B, int8_t *d,
                                       uint32_t f, uint32_t n) { return partial(OP_Q7, a, A, b, B, d, f, n); }
+
+/* scratch-buffer forms (the reference's signatures; the scratch buffers are not needed) */
+void oracle_arm_conv_opt_q15(const int16_t *a, uint32_t A, const int16_t *b, uint32_t B, int16_t *d, int16_t *s1,
+                             int16_t *s2) { conv_fast(OP_Q15, a, A, b, B, d); }
+void oracle_arm_conv_fast_opt_q15(const int16_t *a, uint32_t A, const int16_t *b, uint32_t B, int16_t *d, int16_t *s1,
+                                  int16_t *s2) { conv_fast(OP_FOQ15, a, A, b, B, d); }
+void oracle_arm_conv_opt_q7(const int8_t *a, uint32_t A, const int8_t *b, uint32_t B, int8_t *d, int16_t *s1,
+                            int16_t *s2) { conv_fast(OP_Q7, a, A, b, B, d); }
+void oracle_arm_correlate_opt_q15(const int16_t *a, uint32_t A, const int16_t *b, uint32_t B, int16_t *d,
+                                  int16_t *s) { correlate(OP_Q15, a, A, b, B, d); }
+void oracle_arm_correlate_fast_opt_q15(const int16_t *a, uint32_t A, const int16_t *b, uint32_t B, int16_t *d,
+                                       int16_t *s) { correlate(OP_FOQ15, a, A, b, B, d); }
+void oracle_arm_correlate_opt_q7(const int8_t *a, uint32_t A, const int8_t *b, uint32_t B, int8_t *d, int16_t *s1,
+                                 int16_t *s2) { correlate(OP_Q7, a, A, b, B, d); }
+arm_status oracle_arm_conv_partial_opt_q15(const int16_t *a, uint32_t A, const int16_t *b, uint32_t B, int16_t *d,
+                                           uint32_t f, uint32_t n, int16_t *s1, int16_t *s2) {
+  return partial(OP_Q15, a, A, b, B, d, f, n);
+}
+arm_status oracle_arm_conv_partial_fast_opt_q15(const int16_t *a, uint32_t A, const int16_t *b, uint32_t B,
+                                                int16_t *d, uint32_t f, uint32_t n, int16_t *s1, int16_t *s2) {
+  return partial(OP_FOQ15, a, A, b, B, d, f, n);
+}
+arm_status oracle_arm_conv_partial_opt_q7(const int8_t *a, uint32_t A, const int8_t *b, uint32_t B, int8_t *d,
+                                          uint32_t f, uint32_t n, int16_t *s1, int16_t *s2) {
+  return partial(OP_Q7, a, A, b, B, d, f, n);
+}
