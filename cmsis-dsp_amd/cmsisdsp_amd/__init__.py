@@ -21,7 +21,7 @@ from . import _abi
 from ._abi import (arm_cfft_instance_f32, arm_cfft_instance_q15, arm_cfft_instance_q31,  # noqa: F401
                    arm_fir_instance_f32, arm_fir_instance_q15, arm_fir_instance_q31, arm_fir_instance_q7,
                    arm_matrix_instance_f32,
-                   arm_rfft_fast_instance_f32, arm_mfcc_instance_f32, arm_matrix_instance_q15,
+                   arm_rfft_fast_instance_f32, arm_mfcc_instance_f32, arm_mfcc_instance_q31, arm_matrix_instance_q15,
                    arm_matrix_instance_q31, arm_rfft_instance_q31, arm_rfft_instance_q15, ARM_MATH_SUCCESS,
                    ARM_MATH_ARGUMENT_ERROR, ARM_MATH_SIZE_MISMATCH)
 
@@ -305,6 +305,51 @@ class MfccF32:
                                     C.c_void_p(work.data_ptr()), b, _stream_ptr(stream))
         if st != ARM_MATH_SUCCESS:
             raise RuntimeError(f"arm_mfcc_f32_batch -> {st}: {last_error()[1]}")
+        return out
+
+
+class MfccQ31:
+    """arm_mfcc_init_q31 + arm_mfcc_q31 (bit-exact) with the instance's tables kept alive.
+    dct: [nbDctOutputs, nbMelFilters] q31; pos/lengths: per Mel filter; coefs: concatenated
+    q31 filter weights; window: fftLen q31.  Tables: numpy (host) or torch device tensors."""
+
+    def __init__(self, fft_len, dct, pos, lengths, coefs, window):
+        def keep(a, dt):
+            if hasattr(a, "data_ptr"):
+                return a, a.data_ptr()
+            a = np.ascontiguousarray(a, dtype=dt)
+            return a, a.ctypes.data
+        self._t = [keep(dct, np.int32), keep(pos, np.uint32), keep(lengths, np.uint32), keep(coefs, np.int32),
+                   keep(window, np.int32)]
+        self.nb_mel = int(len(lengths))
+        self.nb_dct = int(dct.shape[0])
+        self.fft_len = int(fft_len)
+        self.S = arm_mfcc_instance_q31()
+        st = lib.arm_mfcc_init_q31(C.byref(self.S), self.fft_len, self.nb_mel, self.nb_dct,
+                                   *[p for _, p in self._t])
+        if st != ARM_MATH_SUCCESS:
+            raise ValueError(f"arm_mfcc_init_q31({fft_len}) -> {st}")
+
+    def __call__(self, x):
+        """One frame (numpy int32) -> nbDctOutputs q8.23 coefficients (the reference's call)."""
+        src = np.ascontiguousarray(x, dtype=np.int32).copy()
+        dst = np.zeros(self.nb_dct, dtype=np.int32)
+        tmp = np.zeros(2 * self.fft_len, dtype=np.int32)
+        st = lib.arm_mfcc_q31(C.byref(self.S), src.ctypes.data, dst.ctypes.data, tmp.ctypes.data)
+        if st != ARM_MATH_SUCCESS:
+            raise RuntimeError(f"arm_mfcc_q31 -> {st}: {last_error()[1]}")
+        return dst
+
+    def batch(self, frames, out=None, work=None, stream=None):
+        """frames: torch int32 device tensor [batch, fftLen] (overwritten) -> [batch, nbDct]."""
+        import torch
+        b = frames.shape[0]
+        out = torch.empty((b, self.nb_dct), dtype=torch.int32, device=frames.device) if out is None else out
+        work = torch.empty((b, 2 * self.fft_len), dtype=torch.int32, device=frames.device) if work is None else work
+        st = lib.arm_mfcc_q31_batch(C.byref(self.S), C.c_void_p(frames.data_ptr()), C.c_void_p(out.data_ptr()),
+                                    C.c_void_p(work.data_ptr()), b, _stream_ptr(stream))
+        if st != ARM_MATH_SUCCESS:
+            raise RuntimeError(f"arm_mfcc_q31_batch -> {st}: {last_error()[1]}")
         return out
 
 

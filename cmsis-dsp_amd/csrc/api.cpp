@@ -321,6 +321,77 @@ bool mfcc_run(const arm_mfcc_instance_f32* S, const MfccDev& d, float* x, float*
   return true;
 }
 
+// ---- MFCC q31 (arm_mfcc_q31.c:88-225): the same content-cached blob layout as the f32
+// instance, q31 words; the inner RFFT is the bit-exact batched q31 RFFT.  Mel filters must
+// stay within the fftLen/2 + 1 magnitudes (the reference would read its CFFT's leftovers).
+struct MfccQ31Dev {
+  const int32_t* dct = nullptr;
+  const int32_t* coefs = nullptr;
+  const int32_t* win = nullptr;
+  const uint32_t* pos = nullptr;
+  const uint32_t* len = nullptr;
+  const uint32_t* off = nullptr;
+  const int32_t* lut = nullptr;
+};
+
+bool mfcc_q31_prepare(const arm_mfcc_instance_q31* S, MfccQ31Dev& d) {
+  const uint32_t n = S->fftLen, nm = S->nbMelFilters, nd = S->nbDctOutputs;
+  if (!rfft_len_ok(n) || S->rfft.fftLenReal != n || S->rfft.ifftFlagR != 0) {
+    set_error(hipErrorInvalidValue, "mfcc q31 instance");
+    return false;
+  }
+  if (mfcc_q31_post_lds((int)n, (int)nm) > 65536) { set_error(hipErrorInvalidValue, "mfcc q31: too many Mel filters"); return false; }
+  std::vector<uint32_t> pos, len;
+  if (!host_copy(S->filterPos, nm, pos) || !host_copy(S->filterLengths, nm, len)) {
+    set_error(hipErrorInvalidValue, "mfcc q31 filter tables");
+    return false;
+  }
+  std::vector<uint32_t> off(nm);
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < nm; ++i) {
+    if ((uint64_t)pos[i] + len[i] > n / 2 + 1) { set_error(hipErrorInvalidValue, "mfcc q31 filter beyond fftLen/2"); return false; }
+    off[i] = (uint32_t)total;
+    total += len[i];
+  }
+  auto up16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  const size_t b_dct = up16(4 * (size_t)nm * nd), b_cf = up16(4 * total), b_win = up16(4 * (size_t)n);
+  const size_t b_u = up16(sizeof(uint32_t) * nm);
+  std::vector<uint8_t> blob(b_dct + b_cf + b_win + 3 * b_u + 16, 0);
+  std::vector<int32_t> tmp;
+  if (!host_copy(S->dctCoefs, (size_t)nm * nd, tmp)) { set_error(hipErrorInvalidValue, "mfcc q31 dct"); return false; }
+  memcpy(blob.data(), tmp.data(), 4 * tmp.size());
+  if (!host_copy(S->filterCoefs, (size_t)total, tmp)) { set_error(hipErrorInvalidValue, "mfcc q31 coefs"); return false; }
+  memcpy(blob.data() + b_dct, tmp.data(), 4 * tmp.size());
+  if (!host_copy(S->windowCoefs, (size_t)n, tmp)) { set_error(hipErrorInvalidValue, "mfcc q31 window"); return false; }
+  memcpy(blob.data() + b_dct + b_cf, tmp.data(), 4 * tmp.size());
+  uint8_t* u = blob.data() + b_dct + b_cf + b_win;
+  memcpy(u, pos.data(), sizeof(uint32_t) * nm);
+  memcpy(u + b_u, len.data(), sizeof(uint32_t) * nm);
+  memcpy(u + 2 * b_u, off.data(), sizeof(uint32_t) * nm);
+  const uint8_t* dev = (const uint8_t*)device_blob(blob.data(), blob.size());
+  d.lut = (const int32_t*)device_table(sqrt_initial_lut_q31, sizeof(int32_t) * 32);
+  if (!dev || !d.lut) return false;
+  d.dct = (const int32_t*)dev;
+  d.coefs = (const int32_t*)(dev + b_dct);
+  d.win = (const int32_t*)(dev + b_dct + b_cf);
+  d.pos = (const uint32_t*)(dev + b_dct + b_cf + b_win);
+  d.len = (const uint32_t*)(dev + b_dct + b_cf + b_win + b_u);
+  d.off = (const uint32_t*)(dev + b_dct + b_cf + b_win + 2 * b_u);
+  return true;
+}
+
+// x: [batch][n] frames (overwritten), y: [batch][2n] spectra, dst: [batch][nbDct]; the frame
+// maxima ride in dst[frame][0] between the launches (read before the row is written)
+bool mfcc_q31_run(const arm_mfcc_instance_q31* S, const MfccQ31Dev& d, int32_t* x, int32_t* y, int32_t* dst,
+                  uint32_t batch, hipStream_t st) {
+  const int n = (int)S->fftLen, nd = (int)S->nbDctOutputs, nm = (int)S->nbMelFilters;
+  MI_CHECK(mfcc_q31_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc q31 pre");
+  if (!rfft_fixed_run<int32_t>(&S->rfft, x, y, batch, st)) return false;
+  MI_CHECK(mfcc_q31_post_launch(n, y, dst, nd, nm, d.pos, d.len, d.off, d.coefs, nd, d.dct, d.lut, dst, batch, st),
+           "mfcc q31 post");
+  return true;
+}
+
 // FIR coefficients: device pointers in place, host sets through the content-keyed cache
 // (uploaded synchronously once per distinct set, so an asynchronous batch call never
 // shares a staging buffer with a later call on another stream)
@@ -992,6 +1063,42 @@ arm_status arm_mfcc_f32_batch(const arm_mfcc_instance_f32* S, float32_t* d_src, 
   MfccDev d;
   if (!mfcc_prepare(S, d)) return ARM_MATH_ARGUMENT_ERROR;
   return mfcc_run(S, d, d_src, d_tmp, d_dst, batch, (hipStream_t)stream) ? ARM_MATH_SUCCESS : ARM_MATH_ARGUMENT_ERROR;
+}
+
+// ---- MFCC q31 (drop-in + batched) ------------------------------------------------
+// Drop-in: the reference's pSrc / pTmp work contents are not reproduced (device scratch).
+arm_status arm_mfcc_q31(const arm_mfcc_instance_q31* S, q31_t* pSrc, q31_t* pDst, q31_t* pTmp) {
+  (void)pTmp;
+  if (!S || !pSrc || !pDst) return ARM_MATH_ARGUMENT_ERROR;
+  if (S->nbDctOutputs == 0) return ARM_MATH_SUCCESS;
+  MfccQ31Dev d;
+  if (!mfcc_q31_prepare(S, d)) return ARM_MATH_ARGUMENT_ERROR;
+  const uint32_t n = S->fftLen, nd = S->nbDctOutputs;
+  hipStream_t st = sync_stream();
+  int32_t* x = (int32_t*)scratch(sizeof(int32_t) * n, 0);
+  int32_t* y = (int32_t*)scratch(sizeof(int32_t) * 2 * n, 1);
+  const bool ddst = is_device_ptr(pDst);
+  int32_t* o = ddst ? pDst : (int32_t*)scratch(sizeof(int32_t) * nd, 2);
+  if (!x || !y || !o) { set_error(hipErrorOutOfMemory, "arm_mfcc_q31 scratch"); return ARM_MATH_ARGUMENT_ERROR; }
+  HostIO io(st);
+  hipError_t e = is_device_ptr(pSrc) ? hipMemcpyAsync(x, pSrc, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st)
+                                     : io.in(x, pSrc, sizeof(int32_t) * n);
+  if (e != hipSuccess) { set_error(e, "arm_mfcc_q31"); return ARM_MATH_ARGUMENT_ERROR; }
+  if (!mfcc_q31_run(S, d, x, y, o, 1, st)) { (void)hipStreamSynchronize(st); return ARM_MATH_ARGUMENT_ERROR; }
+  if (!ddst) e = io.out(pDst, o, sizeof(int32_t) * nd);
+  if (e == hipSuccess) e = io.finish();
+  if (e != hipSuccess) { set_error(e, "arm_mfcc_q31"); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
+}
+
+arm_status arm_mfcc_q31_batch(const arm_mfcc_instance_q31* S, q31_t* d_src, q31_t* d_dst, q31_t* d_tmp,
+                              uint32_t batch, void* stream) {
+  if (!S || (batch && (!d_src || !d_dst || !d_tmp))) return ARM_MATH_ARGUMENT_ERROR;
+  if (batch == 0 || S->nbDctOutputs == 0) return ARM_MATH_SUCCESS;
+  MfccQ31Dev d;
+  if (!mfcc_q31_prepare(S, d)) return ARM_MATH_ARGUMENT_ERROR;
+  return mfcc_q31_run(S, d, d_src, d_tmp, d_dst, batch, (hipStream_t)stream) ? ARM_MATH_SUCCESS
+                                                                               : ARM_MATH_ARGUMENT_ERROR;
 }
 
 // ---- matrix multiply q15 / q31 --------------------------------------------------

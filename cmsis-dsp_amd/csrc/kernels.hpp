@@ -100,6 +100,14 @@ hipError_t mfcc_f32_fused_launch(int n, const float* src, const float* win, cons
 // The frame maximum of frame f is written to / read from maxv[f * maxv_stride].
 hipError_t mfcc_f32_pre_launch(int n, const float* src, const float* win, float* x, float* maxv, uint32_t batch,
                                int maxv_stride, hipStream_t st);
+// MFCC q31 around the batched q31 RFFT (mfcc_q31.hip); post needs mfcc_q31_post_lds bytes.
+hipError_t mfcc_q31_pre_launch(int n, const int32_t* src, const int32_t* win, int32_t* x, int32_t* maxv,
+                               uint32_t batch, int maxv_stride, hipStream_t st);
+size_t mfcc_q31_post_lds(int n, int nb_mel);
+hipError_t mfcc_q31_post_launch(int n, const int32_t* y, const int32_t* maxv, int maxv_stride, int nb_mel,
+                                const uint32_t* pos, const uint32_t* len, const uint32_t* off, const int32_t* coefs,
+                                int nb_dct, const int32_t* dct, const int32_t* lut, int32_t* dst, uint32_t batch,
+                                hipStream_t st);
 size_t mfcc_f32_post_lds(int n, int nb_mel);
 hipError_t mfcc_f32_post_launch(int n, const float* y, const float* maxv, int maxv_stride, int nb_mel,
                                 const uint32_t* pos,

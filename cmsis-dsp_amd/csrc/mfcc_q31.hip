@@ -1,0 +1,211 @@
+// Batched MFCC q31 — MI355X kernels around the batched q31 real FFT, bit-exact.
+//
+// Replaces Source/TransformFunctions/arm_mfcc_q31.c:88-225 (RFFT-based default build, host
+// scalar path: ARM_MATH_LOOPUNROLL, no ARM_MATH_DSP) for `batch` frames, in three
+// stream-ordered launches:
+//   mfcc_q31_pre   m = max sat|x| (arm_absmax_q31), (quot, sh) = arm_divide_q31(0x7FFFFFFF, m),
+//                  x = arm_scale_q31(x, quot, sh) if m != 0, 0x7FFFFFFF, x = arm_mult_q31(x, w)
+//                  -> X (in place), m -> dst[frame][0]               [one wave per frame]
+//   rfft           arm_rfft_q31 forward on X -> Y                     [the bit-exact batched RFFT]
+//   mfcc_q31_post  |Y_k|, k <= fftLen/2 (arm_cmplx_mag_q31 + arm_sqrt_q31), Mel dot products
+//                  (arm_dot_prod_q31: Σ (a·b) >> 14, + MICRO_Q31, >> 28, __SSAT(int32, 31)),
+//                  arm_scale_q31(., m, 0), arm_vlog_q31, arm_offset_q31, arm_shift_q31(-3),
+//                  DCT rows (arm_mat_vec_mult_q31: (q31)(Σ a·b >> 31)) [one wave per frame, LDS]
+// Every stage is integer arithmetic; the sums are exact int64 (order-free), so each lane may
+// own whole Mel filters / DCT rows.  Shift counts are taken mod 32 as on the reference's host
+// (only m = 1 reaches a count of 32).
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace mi355x {
+
+constexpr int kMqWaves = 4;   // frames (waves) per 256-thread workgroup
+
+__device__ __forceinline__ int32_t mq_sat_abs(int32_t x) { return x > 0 ? x : (x == INT32_MIN ? INT32_MAX : -x); }
+__device__ __forceinline__ uint32_t mq_clz(uint32_t x) { return x ? (uint32_t)__builtin_clz(x) : 32u; }
+__device__ __forceinline__ int32_t mq_shl(int32_t x, int k) { return (int32_t)((uint32_t)x << (k & 31)); }
+__device__ __forceinline__ int32_t mq_ssat31(int32_t v) {
+  return v > 0x3FFFFFFF ? 0x3FFFFFFF : (v < -0x40000000 ? -0x40000000 : v);
+}
+__device__ __forceinline__ int32_t mq_hi(int32_t a, int32_t b) { return (int32_t)(((int64_t)a * b) >> 32); }
+
+// arm_scale_q31.c, one element: in = (x * frac) >> 32, then << kShift with saturation, or
+// >> -kShift (kShift = shift + 1 as int8_t)
+__device__ __forceinline__ int32_t mq_scale(int32_t x, int32_t frac, int k) {
+  const int32_t in = mq_hi(x, frac);
+  if (k >= 0) {
+    const int32_t out = mq_shl(in, k);
+    return in != (out >> (k & 31)) ? (0x7FFFFFFF ^ (in >> 31)) : out;
+  }
+  return in >> ((-k) & 31);
+}
+
+__device__ __forceinline__ int32_t wave_max_i(int32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// src and x may alias (in place): each lane rewrites only the words it read
+__global__ __launch_bounds__(256) void mfcc_q31_pre_kernel(const int32_t* src, const int32_t* __restrict__ win,
+                                                           int32_t* x, int32_t* maxv, int maxv_stride, int n,
+                                                           uint32_t batch) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t frame = blockIdx.x * kMqWaves + (threadIdx.x >> 6);
+  if (frame >= batch) return;
+  const int4* s = reinterpret_cast<const int4*>(src + (size_t)frame * n);
+  const int4* w = reinterpret_cast<const int4*>(win);
+  int4* o = reinterpret_cast<int4*>(x + (size_t)frame * n);
+  const int n4 = n >> 2;
+  // max of the saturated magnitudes (the reference's index is not used by the MFCC)
+  int32_t m = 0;
+  for (int i = lane; i < n4; i += 64) {
+    const int4 v = s[i];
+    m = max(m, max(max(mq_sat_abs(v.x), mq_sat_abs(v.y)), max(mq_sat_abs(v.z), mq_sat_abs(v.w))));
+  }
+  m = wave_max_i(m);
+  // arm_divide_q31(0x7FFFFFFF, m): both positive, temp = (num << 31) / den, normalised to 32 bits
+  const bool scale = m != 0 && m != 0x7FFFFFFF;
+  int32_t quot = 0;
+  int k = 1;
+  if (scale) {
+    int64_t t = (int64_t)(((uint64_t)0x7FFFFFFF << 31) / (uint64_t)m);
+    const int sn = 32 - (int)mq_clz((uint32_t)(t >> 31));
+    int sh = 0;
+    if (sn > 0) {
+      sh = sn;
+      t >>= sn;
+    }
+    quot = (int32_t)t;
+    k = (int)(int8_t)(sh + 1);     // kShift = (int8_t)(shift + 1)
+  }
+  for (int i = lane; i < n4; i += 64) {
+    int4 v = s[i];
+    if (scale) {
+      v.x = mq_scale(v.x, quot, k); v.y = mq_scale(v.y, quot, k);
+      v.z = mq_scale(v.z, quot, k); v.w = mq_scale(v.w, quot, k);
+    }
+    const int4 c = w[i];   // arm_mult_q31: __SSAT((a*b) >> 32, 31) << 1
+    o[i] = make_int4(mq_shl(mq_ssat31(mq_hi(v.x, c.x)), 1), mq_shl(mq_ssat31(mq_hi(v.y, c.y)), 1),
+                     mq_shl(mq_ssat31(mq_hi(v.z, c.z)), 1), mq_shl(mq_ssat31(mq_hi(v.w, c.w)), 1));
+  }
+  if (lane == 0) maxv[(size_t)frame * maxv_stride] = m;
+}
+
+// arm_sqrt_q31.c:55-125 (Newton on 1/sqrt from sqrt_initial_lut_q31, 3 iterations)
+__device__ __forceinline__ int32_t mq_sqrt(int32_t in, const int32_t* lut) {
+  if (in <= 0) return 0;
+  const int sb = (int)mq_clz((uint32_t)in) - 1;
+  const int e = sb & ~1;                             // signBits1 rounded down to even
+  const int32_t number = in << e;
+  int32_t v = lut[(number >> 26) - (0x20000000 >> 26)];
+#pragma unroll
+  for (int it = 0; it < 3; ++it) {
+    int32_t t = (int32_t)(((int64_t)v * v) >> 28);
+    t = (int32_t)(((int64_t)number * t) >> 31);
+    t = 0x30000000 - t;
+    v = (int32_t)(((int64_t)v * t) >> 29);
+  }
+  v = (int32_t)(((int64_t)number * v) >> 28);
+  return v >> (e >> 1);
+}
+
+// arm_vlog_q31.c:55-121 (arm_scalar_log_q31): q5.26 natural log of a q31 value
+__device__ __forceinline__ int32_t mq_log(uint32_t src) {
+  const int c = (int)mq_clz(src);
+  uint32_t x = c == 0 ? src >> 1 : src << (c - 1), y = 0, inc = (1u << 31) >> 6;
+#pragma unroll
+  for (int i = 0; i < 31; ++i) {
+    x = (uint32_t)(((uint64_t)x * x) >> 30);         // x < 2^31: the product fits 62 bits
+    if (x >= (1u << 31)) {
+      y += inc;
+      x >>= 1;
+    }
+    inc >>= 1;
+  }
+  const int32_t tmp = (int32_t)(y - ((uint32_t)c << 26));
+  return (int32_t)(((int64_t)tmp * (int64_t)0x58b90bfb) >> 31);
+}
+
+// maxv may alias dst (frame maxima carried in dst[frame][0]): read before any output store
+__global__ __launch_bounds__(256) void mfcc_q31_post_kernel(const int32_t* __restrict__ y, const int32_t* maxv,
+                                                            int maxv_stride, int n, int nb_mel,
+                                                            const uint32_t* __restrict__ pos,
+                                                            const uint32_t* __restrict__ len,
+                                                            const uint32_t* __restrict__ off,
+                                                            const int32_t* __restrict__ coefs, int nb_dct,
+                                                            const int32_t* __restrict__ dct,
+                                                            const int32_t* __restrict__ lut, int32_t* dst,
+                                                            uint32_t batch) {
+  extern __shared__ int32_t shq[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lim = (n >> 1) + 1;
+  int32_t* mag = shq + wave * (lim + nb_mel);
+  int32_t* mel = mag + lim;
+  const uint32_t frame = blockIdx.x * kMqWaves + wave;
+  const bool live = frame < batch;
+  const int32_t m = live ? maxv[(size_t)frame * maxv_stride] : 0;
+  const bool scale = m != 0 && m != 0x7FFFFFFF;
+  if (live) {
+    const int2* Y = reinterpret_cast<const int2*>(y + (size_t)frame * 2 * n);
+    for (int k = lane; k < lim; k += 64) {
+      const int2 c = Y[k];
+      const int32_t a0 = (int32_t)(((int64_t)c.x * c.x) >> 33), a1 = (int32_t)(((int64_t)c.y * c.y) >> 33);
+      mag[k] = mq_sqrt(a0 + a1, lut);
+    }
+  }
+  __syncthreads();
+  // log exponent (fftShift + 2 + SHIFT_MELFILTER_SATURATION_Q31) * LOG2TOLOG_Q31
+  const int32_t le = (int32_t)((uint32_t)(31 - (int)mq_clz((uint32_t)n) + 12) * 0x02C5C860u);
+  if (live) {
+    for (int i = lane; i < nb_mel; i += 64) {
+      const uint32_t p = pos[i], l = len[i];
+      const int32_t* c = coefs + off[i];
+      int64_t r = 0;
+      for (uint32_t j = 0; j < l; ++j) r += ((int64_t)mag[p + j] * c[j]) >> 14;
+      r += 0x08637BD0;                                 // MICRO_Q31
+      r >>= 28;                                        // SHIFT_MELFILTER_SATURATION_Q31 + 18
+      int32_t v = mq_ssat31((int32_t)r);               // __SSAT takes the low 32 bits
+      if (scale) v = mq_scale(v, m, 1);                // arm_scale_q31(., m, 0): kShift = 1
+      v = mq_log((uint32_t)v);
+      const int64_t s = (int64_t)v + le;               // arm_offset_q31 (saturating)
+      v = s > INT32_MAX ? INT32_MAX : (s < INT32_MIN ? INT32_MIN : (int32_t)s);
+      mel[i] = v >> 3;                                 // arm_shift_q31(., -3)
+    }
+  }
+  __syncthreads();
+  if (live) {
+    int32_t* o = dst + (size_t)frame * nb_dct;
+    for (int r = lane; r < nb_dct; r += 64) {
+      const int32_t* d = dct + (size_t)r * nb_mel;
+      int64_t sum = 0;
+      for (int i = 0; i < nb_mel; ++i) sum += (int64_t)d[i] * mel[i];
+      o[r] = (int32_t)(sum >> 31);
+    }
+  }
+}
+
+hipError_t mfcc_q31_pre_launch(int n, const int32_t* src, const int32_t* win, int32_t* x, int32_t* maxv,
+                               uint32_t batch, int maxv_stride, hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  if (n < 32 || (n & 3)) return hipErrorInvalidValue;
+  const uint32_t grid = (batch + kMqWaves - 1) / kMqWaves;
+  hipLaunchKernelGGL(mfcc_q31_pre_kernel, dim3(grid), dim3(64 * kMqWaves), 0, st, src, win, x, maxv, maxv_stride, n,
+                     batch);
+  return hipGetLastError();
+}
+
+size_t mfcc_q31_post_lds(int n, int nb_mel) { return sizeof(int32_t) * kMqWaves * (size_t)(n / 2 + 1 + nb_mel); }
+
+hipError_t mfcc_q31_post_launch(int n, const int32_t* y, const int32_t* maxv, int maxv_stride, int nb_mel,
+                                const uint32_t* pos, const uint32_t* len, const uint32_t* off, const int32_t* coefs,
+                                int nb_dct, const int32_t* dct, const int32_t* lut, int32_t* dst, uint32_t batch,
+                                hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  const uint32_t grid = (batch + kMqWaves - 1) / kMqWaves;
+  hipLaunchKernelGGL(mfcc_q31_post_kernel, dim3(grid), dim3(64 * kMqWaves), mfcc_q31_post_lds(n, nb_mel), st, y,
+                     maxv, maxv_stride, n, nb_mel, pos, len, off, coefs, nb_dct, dct, lut, dst, batch);
+  return hipGetLastError();
+}
+
+}  // namespace mi355x

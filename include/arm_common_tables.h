@@ -45,6 +45,9 @@ extern const int32_t realCoefBQ31[8192];
 extern const int16_t realCoefAQ15[8192];
 extern const int16_t realCoefBQ15[8192];
 
+/* initial 1/sqrt estimates of arm_sqrt_q31 (Include/arm_common_tables.h:297) */
+extern const int32_t sqrt_initial_lut_q31[32];
+
 /* bit-reversal table lengths: Include/arm_common_tables.h:181-235 */
 #define ARMBITREVINDEXTABLE_16_TABLE_LENGTH   ((uint16_t)20)
 #define ARMBITREVINDEXTABLE_32_TABLE_LENGTH   ((uint16_t)48)

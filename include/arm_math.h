@@ -110,6 +110,19 @@ typedef struct {
   arm_rfft_fast_instance_f32 rfft;
 } arm_mfcc_instance_f32;
 
+/* Include/dsp/transform_functions.h:1000-1020 (RFFT-based default build) */
+typedef struct {
+  const q31_t    *dctCoefs;
+  const q31_t    *filterCoefs;
+  const q31_t    *windowCoefs;
+  const uint32_t *filterPos;
+  const uint32_t *filterLengths;
+        uint32_t   fftLen;
+        uint32_t   nbMelFilters;
+        uint32_t   nbDctOutputs;
+  arm_rfft_instance_q31 rfft;
+} arm_mfcc_instance_q31;
+
 /* ---- FIR instances: Include/dsp/filtering_functions.h:56-61 (q7), 66-71, 76-81, 86-91 */
 typedef struct {
         uint16_t   numTaps;
@@ -381,6 +394,30 @@ arm_status arm_mfcc_init_f32(arm_mfcc_instance_f32 *S, uint32_t fftLen, uint32_t
                              const uint32_t *filterLengths, const float32_t *filterCoefs,
                              const float32_t *windowCoefs);
 void arm_mfcc_f32(const arm_mfcc_instance_f32 *S, float32_t *pSrc, float32_t *pDst, float32_t *pTmp);
+
+/* MFCC q31.  Reference bodies: Source/TransformFunctions/arm_mfcc_init_q31.c (generic and
+ * per-length init: RFFT q31 forward with bit reversal), arm_mfcc_q31.c:88-225 (RFFT-based
+ * default path; output q8.23).  pSrc and pTmp are work buffers of the reference; the GPU
+ * path uses device scratch and leaves them as they were.  Mel filters must lie within the
+ * fftLen/2 + 1 spectrum magnitudes (ARM_MATH_ARGUMENT_ERROR otherwise). */
+arm_status arm_mfcc_init_q31(arm_mfcc_instance_q31 *S, uint32_t fftLen, uint32_t nbMelFilters, uint32_t nbDctOutputs,
+                             const q31_t *dctCoefs, const uint32_t *filterPos, const uint32_t *filterLengths,
+                             const q31_t *filterCoefs, const q31_t *windowCoefs);
+#define ARM_MI355X_DECL_MFCC_Q31_INIT(N)                                                                    \
+  arm_status arm_mfcc_init_##N##_q31(arm_mfcc_instance_q31 *S, uint32_t nbMelFilters, uint32_t nbDctOutputs, \
+                                     const q31_t *dctCoefs, const uint32_t *filterPos,                       \
+                                     const uint32_t *filterLengths, const q31_t *filterCoefs,                \
+                                     const q31_t *windowCoefs);
+ARM_MI355X_DECL_MFCC_Q31_INIT(32)
+ARM_MI355X_DECL_MFCC_Q31_INIT(64)
+ARM_MI355X_DECL_MFCC_Q31_INIT(128)
+ARM_MI355X_DECL_MFCC_Q31_INIT(256)
+ARM_MI355X_DECL_MFCC_Q31_INIT(512)
+ARM_MI355X_DECL_MFCC_Q31_INIT(1024)
+ARM_MI355X_DECL_MFCC_Q31_INIT(2048)
+ARM_MI355X_DECL_MFCC_Q31_INIT(4096)
+#undef ARM_MI355X_DECL_MFCC_Q31_INIT
+arm_status arm_mfcc_q31(const arm_mfcc_instance_q31 *S, q31_t *pSrc, q31_t *pDst, q31_t *pTmp);
 
 /* ===================================================================================
  * FIR.  Prototypes: Include/dsp/filtering_functions.h:141-145,175-180,233-237,260-265

@@ -61,6 +61,10 @@ arm_status arm_rfft_q15_batch(const arm_rfft_instance_q15 *S, q15_t *d_src, q15_
  * call through the calling thread's staging buffers, in stream order). */
 arm_status arm_mfcc_f32_batch(const arm_mfcc_instance_f32 *S, float32_t *d_src, float32_t *d_dst,
                               float32_t *d_tmp, uint32_t batch, void *stream);
+/* MFCC q31 over `batch` contiguous frames (arm_mfcc_q31.c:88-225 per frame, bit-exact):
+ * d_src [batch][fftLen] (overwritten), d_tmp [batch][2*fftLen] work, d_dst [batch][nbDct]. */
+arm_status arm_mfcc_q31_batch(const arm_mfcc_instance_q31 *S, q31_t *d_src, q31_t *d_dst, q31_t *d_tmp,
+                              uint32_t batch, void *stream);
 
 /* FIR over `batch` independent filters sharing S->numTaps / S->pCoeffs (host or device
  * pointer; S->pState is not used).  d_src/d_dst: [batch][blockSize].  d_hist:

@@ -1,0 +1,124 @@
+"""MFCC q31 (the q31 caller of the q31 RFFT): arm_mfcc_q31 = normalise
+(absmax, divide, scale), window, RFFT q31, |X| (sqrt_q31), Mel, scale, log_q31, offset,
+shift, DCT (Source/TransformFunctions/arm_mfcc_q31.c:88-225).  Every stage is integer
+arithmetic, so the bar is bit-exact everywhere.
+
+CPU: the oracle restatement (oracle/src/oracle_mfcc_q31.c) is bit-identical to the reference
+build on the suite's inputs plus seeded and edge frames (tests/golden/mfcc_q31.npz, made by
+tools/make_golden.py mfcc_q31 from oracle/_ref) and meets the reference suite's own
+thresholds against its patterns (Testing/Source/Tests/MFCCQ31.cpp:7-15: SNR >= 66 dB,
+|err| <= 49000).  GPU: the drop-in and batched paths are bit-exact against the same fixture
+and against the reference build / oracle on generated configurations of every length.
+"""
+import numpy as np
+import pytest
+
+import mfcc_cfg
+from metrics import snr_db
+
+SUITE_N = (256, 512, 1024)
+GOLDEN = mfcc_cfg.GOLDEN.replace("mfcc_f32.npz", "mfcc_q31.npz")
+
+
+def golden():
+    return dict(np.load(GOLDEN))
+
+
+def suite_cfg(g, n):
+    return {"fftLen": n, "dct": g["dct"], "pos": g[f"pos_{n}"], "len": g[f"len_{n}"], "coefs": g[f"coefs_{n}"],
+            "window": g[f"window_{n}"]}
+
+
+def q31(a):
+    return np.clip(np.round(np.asarray(a, np.float64) * 2.0**31), -2**31, 2**31 - 1).astype(np.int32)
+
+
+def make_cfg_q31(n):
+    """mfcc_cfg.make_cfg's tables in q31 (Mel filters within the fftLen/2 + 1 magnitudes)."""
+    c = mfcc_cfg.make_cfg(n)
+    return {"fftLen": n, "dct": q31(c["dct"]), "pos": c["pos"], "len": c["len"], "coefs": q31(c["coefs"]),
+            "window": q31(c["window"])}
+
+
+def frames_for(n, rows, seed):
+    rng = np.random.default_rng(seed)
+    f = rng.integers(-2**30, 2**30, (rows, n)).astype(np.int32)
+    f[1] = 0
+    f[2] = rng.integers(-3, 4, n)
+    f[3, 5] = -2**31
+    f[4] = (np.sin(np.arange(n) * 0.21) * 2**29).astype(np.int32)
+    return f
+
+
+# ------------------------------------------------------------------ CPU (oracle)
+@pytest.mark.parametrize("n", SUITE_N)
+def test_oracle_bitexact_vs_reference_fixture(oracle, n):
+    g = golden()
+    got = oracle.mfcc_q31(suite_cfg(g, n), g[f"frames_{n}"])
+    assert got.tobytes() == g[f"out_{n}"].tobytes()
+
+
+@pytest.mark.parametrize("n", SUITE_N)
+@pytest.mark.parametrize("kind", ["Noise", "Sine"])
+def test_oracle_meets_reference_suite_thresholds(oracle, n, kind):
+    g = golden()
+    got = oracle.mfcc_q31(suite_cfg(g, n), g[f"input_{kind}_{n}"])[0]
+    ref = g[f"ref_{kind}_{n}"]
+    assert snr_db(ref.astype(np.float64), got.astype(np.float64)) >= 66
+    assert np.all(np.abs(got.astype(np.int64) - ref) <= 49000)
+
+
+def test_oracle_matches_reference_build_generated_configs(oracle, ref):
+    for n in (32, 64, 128, 2048, 4096):
+        cfg = make_cfg_q31(n)
+        x = frames_for(n, 6, n)
+        assert oracle.mfcc_q31(cfg, x).tobytes() == ref.mfcc_q31(cfg, x).tobytes(), n
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", SUITE_N)
+def test_gpu_dropin_and_batch_vs_reference_fixture(dsp, torch_gpu, n):
+    g = golden()
+    cfg = suite_cfg(g, n)
+    m = dsp.MfccQ31(n, cfg["dct"], cfg["pos"], cfg["len"], cfg["coefs"], cfg["window"])
+    want = g[f"out_{n}"]
+    got = np.stack([m(f) for f in g[f"frames_{n}"]])
+    assert got.tobytes() == want.tobytes(), np.argwhere(got != want)[:5]
+    b = m.batch(torch_gpu.from_numpy(g[f"frames_{n}"].copy()).cuda()).cpu().numpy()
+    assert b.tobytes() == want.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", (32, 64, 128, 256, 512, 1024, 2048, 4096))
+def test_gpu_batch_vs_reference_build(dsp, torch_gpu, ref, n):
+    cfg = make_cfg_q31(n)
+    frames = frames_for(n, 37, 11 * n)
+    want = ref.mfcc_q31(cfg, frames)
+    m = dsp.MfccQ31(n, cfg["dct"], cfg["pos"], cfg["len"], cfg["coefs"], cfg["window"])
+    got = m.batch(torch_gpu.from_numpy(frames.copy()).cuda()).cpu().numpy()
+    assert got.tobytes() == want.tobytes(), (n, np.argwhere(got != want)[:5])
+
+
+@pytest.mark.gpu
+def test_gpu_large_batch_vs_oracle_sample(dsp, torch_gpu, oracle):
+    """2^14 frames of 1024 in one call; every 509th frame replayed on the oracle."""
+    n = 1024
+    cfg = make_cfg_q31(n)
+    frames = np.random.default_rng(5).integers(-2**31, 2**31, (1 << 14, n), dtype=np.int64).astype(np.int32)
+    m = dsp.MfccQ31(n, cfg["dct"], cfg["pos"], cfg["len"], cfg["coefs"], cfg["window"])
+    got = m.batch(torch_gpu.from_numpy(frames.copy()).cuda()).cpu().numpy()
+    idx = np.arange(0, frames.shape[0], 509)
+    assert got[idx].tobytes() == oracle.mfcc_q31(cfg, frames[idx]).tobytes()
+
+
+def test_rejects_filters_beyond_half_spectrum(dsp):
+    n = 64
+    cfg = make_cfg_q31(n)
+    cfg["pos"] = cfg["pos"].copy()
+    cfg["pos"][-1] = n // 2          # pos + len > fftLen/2 + 1
+    m = dsp.MfccQ31(n, cfg["dct"], cfg["pos"], cfg["len"], cfg["coefs"], cfg["window"])
+    import cmsisdsp_amd
+    with pytest.raises(RuntimeError):
+        m(np.zeros(n, np.int32))
+    assert cmsisdsp_amd is dsp

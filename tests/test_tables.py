@@ -13,7 +13,7 @@ SIZES = [16, 32, 64, 128, 256, 512, 1024, 2048, 4096]
 
 def test_blobs_match_manifest():
     man = json.load(open(os.path.join(TAB, "MANIFEST.json")))
-    assert len(man["tables"]) == 57   # 53 CFFT/RFFT-fast tables + realCoef{A,B}{Q31,Q15}
+    assert len(man["tables"]) == 58   # 53 CFFT/RFFT-fast tables + realCoef{A,B}{Q31,Q15} + sqrt_initial_lut_q31
     for name, meta in man["tables"].items():
         raw = open(os.path.join(TAB, name + ".bin"), "rb").read()
         assert len(raw) == meta["bytes"] and hashlib.sha256(raw).hexdigest() == meta["sha256"], name
