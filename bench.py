@@ -54,6 +54,7 @@ WORKLOADS = {
     # three launches (pre in place, RFFT q31 -> 2N-word spectra, post): bytes moved per sample
     # 4 + 4 (pre) + 4 + 4 + 8 (RFFT: inner CFFT in place, 2N words out) + 4 (post reads N+2 words)
     "mfcc_q31": ("mfccq31", 1024, 1 << 18, 28),
+    "mfcc_q15": ("mfccq15", 1024, 1 << 18, 14),
     "rfft_f32": ("rfft", 1024, 1 << 20, 8),
     # real length 8192 (inner CFFT 4096 = the fixed-point specialist); bytes per sample:
     # N words in, N words written back (the inner CFFT overwrites pSrc), 2N words out
@@ -137,7 +138,7 @@ def cpu_share():
 _CPU_WL = {"cfft_f32_1024": "cfft_f32", "cfft_q31_4096": "cfft_q31", "cfft_q15_4096": "cfft_q15",
            "fir_f32": "fir_f32", "fir_q15": "fir_q15", "fir_q31": "fir_q31", "fir_fast_q15": "fir_fast_q15",
            "fir_fast_q31": "fir_fast_q31", "mat_mult_f32": "mat_mult_f32", "mfcc_f32": "mfcc_f32",
-           "mfcc_q31": "mfcc_q31",
+           "mfcc_q31": "mfcc_q31", "mfcc_q15": "mfcc_q15",
            "mat_mult_q15": "mat_mult_q15", "mat_mult_q31": "mat_mult_q31", "mat_mult_fast_q31": "mat_mult_fast_q31",
            "rfft_f32": "rfft_f32", "conv_f32": "conv_f32", "rfft_q31": "rfft_q31", "rfft_q15": "rfft_q15"}
 
@@ -475,26 +476,28 @@ def main_rank(args):
                                "bit_exact_fraction": float(np.mean(got.view(np.uint32) == want.view(np.uint32))),
                                "tolerance": "2e-5 + 1e-6*|ref| (device logf vs host libm logf; other stages exact)"}
 
-    def run_mfcc_q31(n, batch, steps, warmup):
-        """arm_mfcc_q31 (pre + RFFT q31 + post) on the suite's 1024 tables over full-range
+    def run_mfcc_fixed(t, n, batch, steps, warmup):
+        """arm_mfcc_q31 / _q15 (pre + RFFT + post) on the suite's 1024 tables over full-range
         frames (the pre pass rewrites them in place, as the reference does, so later steps
         process the previous step's windowed frames: the same work per step); 64 fresh frames
         checked bit-exact against the CPU checker."""
-        import test_mfcc_q31 as tq
+        import importlib
+        tq = importlib.import_module(f"test_mfcc_{t}")
         g = tq.golden()
         cfg = tq.suite_cfg(g, n)
-        m = dsp.MfccQ31(n, cfg["dct"], cfg["pos"], cfg["len"], cfg["coefs"], cfg["window"])
-        frames = synth("q31", batch * n).view(batch, n)
-        work = torch.empty((batch, 2 * n), dtype=torch.int32, device="cuda")
-        out = torch.empty((batch, m.nb_dct), dtype=torch.int32, device="cuda")
+        m = (dsp.MfccQ31 if t == "q31" else dsp.MfccQ15)(n, cfg["dct"], cfg["pos"], cfg["len"], cfg["coefs"],
+                                                         cfg["window"])
+        frames = synth(t, batch * n).view(batch, n)
+        work = torch.empty((batch, 2 * n), dtype=frames.dtype, device="cuda")
+        out = torch.empty((batch, m.nb_dct), dtype=frames.dtype, device="cuda")
 
         def launch(s):
             m.batch(frames, out, work)
 
         wall, kern_ms = time_launches(launch, steps, warmup)
         host, hk = cpu_checker()
-        fresh = synth("q31", 64 * n, salt=31).view(64, n)
-        want = host.mfcc_q31(cfg, fresh.cpu().numpy())
+        fresh = synth(t, 64 * n, salt=31).view(64, n)
+        want = getattr(host, f"mfcc_{t}")(cfg, fresh.cpu().numpy())
         got = m.batch(fresh.clone()).cpu().numpy()
         return wall, kern_ms, {"checker": hk, "frames_checked": 64, "bit_exact": bool(got.tobytes() == want.tobytes())}
 
@@ -555,8 +558,8 @@ def main_rank(args):
         algo_bytes = units * bps                           # N in, N written back, 2N spectrum out
     elif args.workload == "mfcc_f32":
         wall, kern_ms, parity = run_mfcc(n, batch, args.steps, args.warmup)
-    elif args.workload == "mfcc_q31":
-        wall, kern_ms, parity = run_mfcc_q31(n, batch, args.steps, args.warmup)
+    elif args.workload in ("mfcc_q31", "mfcc_q15"):
+        wall, kern_ms, parity = run_mfcc_fixed(args.workload[-3:], n, batch, args.steps, args.warmup)
         units = batch * n                                  # input samples
         algo_bytes = units * bps + batch * 13 * 4          # frames in + coefficients out
     else:
@@ -612,7 +615,8 @@ def main_rank(args):
                            "fir_q15": "q15 (int16 x int16 -> int64)", "mfcc": "f32",
                            "fir_q31": "q31 (int32 x int32 -> int64)", "fir_fast_q15": "q15 (int32 wrap accumulator)",
                            "fir_fast_q31": "q31 (rounded high-word accumulator)", "rfft": "f32", "conv": "f32",
-                           "rfftq31": "q31 (int32)", "rfftq15": "q15 (int16)", "mfccq31": "q31 (int32)"}[kind])
+                           "rfftq31": "q31 (int32)", "rfftq15": "q15 (int16)", "mfccq31": "q31 (int32)",
+                           "mfccq15": "q15 (int16)"}[kind])
         if args.workload.startswith("cfft"):
             cfg_tag = ("BASELINE configs[1]" if (kind == "f32" and n == 1024) else
                        "BASELINE configs[3]" if (kind != "f32" and n == 4096) else
@@ -637,8 +641,9 @@ def main_rank(args):
             line["config"] = {"workload": f"arm_rfft_{kind[4:]} N={n} forward (inner CFFT {n // 2}), "
                                           f"batch={batch}/GPU", "fftLenReal": n, "batch_per_gpu": batch,
                               "parallelism": f"dp{world_n} shards"}
-        elif kind == "mfccq31":
-            line["config"] = {"workload": f"arm_mfcc_q31 fftLen={n} 20 Mel / 13 DCT (reference MFCC Q31 suite "
+        elif kind in ("mfccq31", "mfccq15"):
+            line["config"] = {"workload": f"arm_mfcc_{kind[4:]} fftLen={n} 20 Mel / 13 DCT (reference MFCC "
+                                          f"{kind[4:].upper()} suite "
                                           f"tables) batch={batch} frames/GPU", "fftLen": n, "batch_per_gpu": batch,
                               "parallelism": f"dp{world_n} shards"}
         elif kind == "mfcc":

@@ -21,7 +21,8 @@ from . import _abi
 from ._abi import (arm_cfft_instance_f32, arm_cfft_instance_q15, arm_cfft_instance_q31,  # noqa: F401
                    arm_fir_instance_f32, arm_fir_instance_q15, arm_fir_instance_q31, arm_fir_instance_q7,
                    arm_matrix_instance_f32,
-                   arm_rfft_fast_instance_f32, arm_mfcc_instance_f32, arm_mfcc_instance_q31, arm_matrix_instance_q15,
+                   arm_rfft_fast_instance_f32, arm_mfcc_instance_f32, arm_mfcc_instance_q31, arm_mfcc_instance_q15,
+                   arm_matrix_instance_q15,
                    arm_matrix_instance_q31, arm_rfft_instance_q31, arm_rfft_instance_q15, ARM_MATH_SUCCESS,
                    ARM_MATH_ARGUMENT_ERROR, ARM_MATH_SIZE_MISMATCH)
 
@@ -308,49 +309,63 @@ class MfccF32:
         return out
 
 
-class MfccQ31:
-    """arm_mfcc_init_q31 + arm_mfcc_q31 (bit-exact) with the instance's tables kept alive.
-    dct: [nbDctOutputs, nbMelFilters] q31; pos/lengths: per Mel filter; coefs: concatenated
-    q31 filter weights; window: fftLen q31.  Tables: numpy (host) or torch device tensors."""
+class _MfccFixed:
+    """arm_mfcc_init_<t> + arm_mfcc_<t> (bit-exact) with the instance's tables kept alive.
+    dct: [nbDctOutputs, nbMelFilters]; pos/lengths: per Mel filter; coefs: concatenated filter
+    weights; window: fftLen.  Tables: numpy (host) or torch device tensors."""
+    T = None            # "q31" | "q15"
 
     def __init__(self, fft_len, dct, pos, lengths, coefs, window):
-        def keep(a, dt):
+        dt = np.int32 if self.T == "q31" else np.int16
+
+        def keep(a, d):
             if hasattr(a, "data_ptr"):
                 return a, a.data_ptr()
-            a = np.ascontiguousarray(a, dtype=dt)
+            a = np.ascontiguousarray(a, dtype=d)
             return a, a.ctypes.data
-        self._t = [keep(dct, np.int32), keep(pos, np.uint32), keep(lengths, np.uint32), keep(coefs, np.int32),
-                   keep(window, np.int32)]
+        self._dt = dt
+        self._t = [keep(dct, dt), keep(pos, np.uint32), keep(lengths, np.uint32), keep(coefs, dt), keep(window, dt)]
         self.nb_mel = int(len(lengths))
         self.nb_dct = int(dct.shape[0])
         self.fft_len = int(fft_len)
-        self.S = arm_mfcc_instance_q31()
-        st = lib.arm_mfcc_init_q31(C.byref(self.S), self.fft_len, self.nb_mel, self.nb_dct,
-                                   *[p for _, p in self._t])
+        self.S = (arm_mfcc_instance_q31 if self.T == "q31" else arm_mfcc_instance_q15)()
+        st = getattr(lib, f"arm_mfcc_init_{self.T}")(C.byref(self.S), self.fft_len, self.nb_mel, self.nb_dct,
+                                                     *[p for _, p in self._t])
         if st != ARM_MATH_SUCCESS:
-            raise ValueError(f"arm_mfcc_init_q31({fft_len}) -> {st}")
+            raise ValueError(f"arm_mfcc_init_{self.T}({fft_len}) -> {st}")
 
     def __call__(self, x):
-        """One frame (numpy int32) -> nbDctOutputs q8.23 coefficients (the reference's call)."""
-        src = np.ascontiguousarray(x, dtype=np.int32).copy()
-        dst = np.zeros(self.nb_dct, dtype=np.int32)
+        """One frame (numpy) -> nbDctOutputs coefficients (the reference's call shape)."""
+        src = np.ascontiguousarray(x, dtype=self._dt).copy()
+        dst = np.zeros(self.nb_dct, dtype=self._dt)
         tmp = np.zeros(2 * self.fft_len, dtype=np.int32)
-        st = lib.arm_mfcc_q31(C.byref(self.S), src.ctypes.data, dst.ctypes.data, tmp.ctypes.data)
+        st = getattr(lib, f"arm_mfcc_{self.T}")(C.byref(self.S), src.ctypes.data, dst.ctypes.data, tmp.ctypes.data)
         if st != ARM_MATH_SUCCESS:
-            raise RuntimeError(f"arm_mfcc_q31 -> {st}: {last_error()[1]}")
+            raise RuntimeError(f"arm_mfcc_{self.T} -> {st}: {last_error()[1]}")
         return dst
 
     def batch(self, frames, out=None, work=None, stream=None):
-        """frames: torch int32 device tensor [batch, fftLen] (overwritten) -> [batch, nbDct]."""
+        """frames: torch device tensor [batch, fftLen] (int32 / int16, overwritten) -> [batch, nbDct]."""
         import torch
         b = frames.shape[0]
-        out = torch.empty((b, self.nb_dct), dtype=torch.int32, device=frames.device) if out is None else out
-        work = torch.empty((b, 2 * self.fft_len), dtype=torch.int32, device=frames.device) if work is None else work
-        st = lib.arm_mfcc_q31_batch(C.byref(self.S), C.c_void_p(frames.data_ptr()), C.c_void_p(out.data_ptr()),
-                                    C.c_void_p(work.data_ptr()), b, _stream_ptr(stream))
+        out = torch.empty((b, self.nb_dct), dtype=frames.dtype, device=frames.device) if out is None else out
+        work = torch.empty((b, 2 * self.fft_len), dtype=frames.dtype, device=frames.device) if work is None else work
+        st = getattr(lib, f"arm_mfcc_{self.T}_batch")(C.byref(self.S), C.c_void_p(frames.data_ptr()),
+                                                      C.c_void_p(out.data_ptr()), C.c_void_p(work.data_ptr()), b,
+                                                      _stream_ptr(stream))
         if st != ARM_MATH_SUCCESS:
-            raise RuntimeError(f"arm_mfcc_q31_batch -> {st}: {last_error()[1]}")
+            raise RuntimeError(f"arm_mfcc_{self.T}_batch -> {st}: {last_error()[1]}")
         return out
+
+
+class MfccQ31(_MfccFixed):
+    """arm_mfcc_q31: q31 frames -> q8.23 coefficients."""
+    T = "q31"
+
+
+class MfccQ15(_MfccFixed):
+    """arm_mfcc_q15: q15 frames -> q8.7 coefficients."""
+    T = "q15"
 
 
 # ------------------------------------------------------------------ batched (torch, device)

@@ -107,6 +107,14 @@ class arm_mfcc_instance_q31(C.Structure):
                 ("rfft", arm_rfft_instance_q31)]
 
 
+class arm_mfcc_instance_q15(C.Structure):
+    # Include/dsp/transform_functions.h:1150-1168 (RFFT-based default build)
+    _fields_ = [("dctCoefs", c_i16p), ("filterCoefs", c_i16p), ("windowCoefs", c_i16p),
+                ("filterPos", C.POINTER(C.c_uint32)), ("filterLengths", C.POINTER(C.c_uint32)),
+                ("fftLen", C.c_uint32), ("nbMelFilters", C.c_uint32), ("nbDctOutputs", C.c_uint32),
+                ("rfft", arm_rfft_instance_q15)]
+
+
 class arm_matrix_instance_q15(C.Structure):
     # Include/dsp/matrix_functions.h:139-144
     _fields_ = [("numRows", C.c_uint16), ("numCols", C.c_uint16), ("pData", c_i16p)]
@@ -202,6 +210,9 @@ DROPIN = {
     "arm_mfcc_init_q31": (C.c_int, [P(arm_mfcc_instance_q31), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "arm_mfcc_q31": (C.c_int, [P(arm_mfcc_instance_q31), C.c_void_p, C.c_void_p, C.c_void_p]),
+    "arm_mfcc_init_q15": (C.c_int, [P(arm_mfcc_instance_q15), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "arm_mfcc_q15": (C.c_int, [P(arm_mfcc_instance_q15), C.c_void_p, C.c_void_p, C.c_void_p]),
     "arm_mat_mult_f32": (C.c_int, [P(arm_matrix_instance_f32), P(arm_matrix_instance_f32),
                                    P(arm_matrix_instance_f32)]),
 }
@@ -218,6 +229,9 @@ MFCC_LEN = {f"arm_mfcc_init_{n}_f32": (C.c_int, [P(arm_mfcc_instance_f32), C.c_u
                                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
             for n in RFFT_SIZES}
 MFCC_LEN.update({f"arm_mfcc_init_{n}_q31": (C.c_int, [P(arm_mfcc_instance_q31), C.c_uint32, C.c_uint32, C.c_void_p,
+                                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
+                 for n in RFFT_SIZES})
+MFCC_LEN.update({f"arm_mfcc_init_{n}_q15": (C.c_int, [P(arm_mfcc_instance_q15), C.c_uint32, C.c_uint32, C.c_void_p,
                                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
                  for n in RFFT_SIZES})
 
@@ -283,6 +297,8 @@ BATCHED = {
     "arm_mfcc_f32_batch": (C.c_int, [P(arm_mfcc_instance_f32), C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                      C.c_void_p]),
     "arm_mfcc_q31_batch": (C.c_int, [P(arm_mfcc_instance_q31), C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                     C.c_void_p]),
+    "arm_mfcc_q15_batch": (C.c_int, [P(arm_mfcc_instance_q15), C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                      C.c_void_p]),
     **{f"arm_cfft_{t}_batch_multi": (C.c_int, [P(inst), C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
                                                C.c_uint8, C.c_uint8])

@@ -321,20 +321,23 @@ bool mfcc_run(const arm_mfcc_instance_f32* S, const MfccDev& d, float* x, float*
   return true;
 }
 
-// ---- MFCC q31 (arm_mfcc_q31.c:88-225): the same content-cached blob layout as the f32
-// instance, q31 words; the inner RFFT is the bit-exact batched q31 RFFT.  Mel filters must
+// ---- MFCC q31 / q15 (arm_mfcc_q31.c:88-225, arm_mfcc_q15.c:96-228): the same content-cached
+// blob layout as the f32 instance in q31 / q15 words; the inner RFFT is the bit-exact batched
+// fixed-point RFFT.  Mel filters must
 // stay within the fftLen/2 + 1 magnitudes (the reference would read its CFFT's leftovers).
-struct MfccQ31Dev {
-  const int32_t* dct = nullptr;
-  const int32_t* coefs = nullptr;
-  const int32_t* win = nullptr;
+template <typename T>
+struct MfccFxDev {
+  const T* dct = nullptr;
+  const T* coefs = nullptr;
+  const T* win = nullptr;
   const uint32_t* pos = nullptr;
   const uint32_t* len = nullptr;
   const uint32_t* off = nullptr;
   const int32_t* lut = nullptr;
 };
 
-bool mfcc_q31_prepare(const arm_mfcc_instance_q31* S, MfccQ31Dev& d) {
+template <typename T, typename Inst>
+bool mfcc_fx_prepare(const Inst* S, MfccFxDev<T>& d) {
   const uint32_t n = S->fftLen, nm = S->nbMelFilters, nd = S->nbDctOutputs;
   if (!rfft_len_ok(n) || S->rfft.fftLenReal != n || S->rfft.ifftFlagR != 0) {
     set_error(hipErrorInvalidValue, "mfcc q31 instance");
@@ -354,16 +357,16 @@ bool mfcc_q31_prepare(const arm_mfcc_instance_q31* S, MfccQ31Dev& d) {
     total += len[i];
   }
   auto up16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
-  const size_t b_dct = up16(4 * (size_t)nm * nd), b_cf = up16(4 * total), b_win = up16(4 * (size_t)n);
+  const size_t b_dct = up16(sizeof(T) * nm * nd), b_cf = up16(sizeof(T) * total), b_win = up16(sizeof(T) * n);
   const size_t b_u = up16(sizeof(uint32_t) * nm);
   std::vector<uint8_t> blob(b_dct + b_cf + b_win + 3 * b_u + 16, 0);
-  std::vector<int32_t> tmp;
-  if (!host_copy(S->dctCoefs, (size_t)nm * nd, tmp)) { set_error(hipErrorInvalidValue, "mfcc q31 dct"); return false; }
-  memcpy(blob.data(), tmp.data(), 4 * tmp.size());
-  if (!host_copy(S->filterCoefs, (size_t)total, tmp)) { set_error(hipErrorInvalidValue, "mfcc q31 coefs"); return false; }
-  memcpy(blob.data() + b_dct, tmp.data(), 4 * tmp.size());
-  if (!host_copy(S->windowCoefs, (size_t)n, tmp)) { set_error(hipErrorInvalidValue, "mfcc q31 window"); return false; }
-  memcpy(blob.data() + b_dct + b_cf, tmp.data(), 4 * tmp.size());
+  std::vector<T> tmp;
+  if (!host_copy(S->dctCoefs, (size_t)nm * nd, tmp)) { set_error(hipErrorInvalidValue, "mfcc dct"); return false; }
+  memcpy(blob.data(), tmp.data(), sizeof(T) * tmp.size());
+  if (!host_copy(S->filterCoefs, (size_t)total, tmp)) { set_error(hipErrorInvalidValue, "mfcc coefs"); return false; }
+  memcpy(blob.data() + b_dct, tmp.data(), sizeof(T) * tmp.size());
+  if (!host_copy(S->windowCoefs, (size_t)n, tmp)) { set_error(hipErrorInvalidValue, "mfcc window"); return false; }
+  memcpy(blob.data() + b_dct + b_cf, tmp.data(), sizeof(T) * tmp.size());
   uint8_t* u = blob.data() + b_dct + b_cf + b_win;
   memcpy(u, pos.data(), sizeof(uint32_t) * nm);
   memcpy(u + b_u, len.data(), sizeof(uint32_t) * nm);
@@ -371,9 +374,9 @@ bool mfcc_q31_prepare(const arm_mfcc_instance_q31* S, MfccQ31Dev& d) {
   const uint8_t* dev = (const uint8_t*)device_blob(blob.data(), blob.size());
   d.lut = (const int32_t*)device_table(sqrt_initial_lut_q31, sizeof(int32_t) * 32);
   if (!dev || !d.lut) return false;
-  d.dct = (const int32_t*)dev;
-  d.coefs = (const int32_t*)(dev + b_dct);
-  d.win = (const int32_t*)(dev + b_dct + b_cf);
+  d.dct = (const T*)dev;
+  d.coefs = (const T*)(dev + b_dct);
+  d.win = (const T*)(dev + b_dct + b_cf);
   d.pos = (const uint32_t*)(dev + b_dct + b_cf + b_win);
   d.len = (const uint32_t*)(dev + b_dct + b_cf + b_win + b_u);
   d.off = (const uint32_t*)(dev + b_dct + b_cf + b_win + 2 * b_u);
@@ -382,13 +385,22 @@ bool mfcc_q31_prepare(const arm_mfcc_instance_q31* S, MfccQ31Dev& d) {
 
 // x: [batch][n] frames (overwritten), y: [batch][2n] spectra, dst: [batch][nbDct]; the frame
 // maxima ride in dst[frame][0] between the launches (read before the row is written)
-bool mfcc_q31_run(const arm_mfcc_instance_q31* S, const MfccQ31Dev& d, int32_t* x, int32_t* y, int32_t* dst,
-                  uint32_t batch, hipStream_t st) {
+template <typename T, typename Inst>
+bool mfcc_fx_run(const Inst* S, const MfccFxDev<T>& d, T* x, T* y, T* dst, uint32_t batch, hipStream_t st) {
   const int n = (int)S->fftLen, nd = (int)S->nbDctOutputs, nm = (int)S->nbMelFilters;
-  MI_CHECK(mfcc_q31_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc q31 pre");
-  if (!rfft_fixed_run<int32_t>(&S->rfft, x, y, batch, st)) return false;
-  MI_CHECK(mfcc_q31_post_launch(n, y, dst, nd, nm, d.pos, d.len, d.off, d.coefs, nd, d.dct, d.lut, dst, batch, st),
-           "mfcc q31 post");
+  if constexpr (sizeof(T) == 4) {
+    MI_CHECK(mfcc_q31_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc q31 pre");
+  } else {
+    MI_CHECK(mfcc_q15_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc q15 pre");
+  }
+  if (!rfft_fixed_run<T>(&S->rfft, x, y, batch, st)) return false;
+  if constexpr (sizeof(T) == 4) {
+    MI_CHECK(mfcc_q31_post_launch(n, y, dst, nd, nm, d.pos, d.len, d.off, d.coefs, nd, d.dct, d.lut, dst, batch, st),
+             "mfcc q31 post");
+  } else {
+    MI_CHECK(mfcc_q15_post_launch(n, y, dst, nd, nm, d.pos, d.len, d.off, d.coefs, nd, d.dct, d.lut, dst, batch, st),
+             "mfcc q15 post");
+  }
   return true;
 }
 
@@ -1065,40 +1077,59 @@ arm_status arm_mfcc_f32_batch(const arm_mfcc_instance_f32* S, float32_t* d_src, 
   return mfcc_run(S, d, d_src, d_tmp, d_dst, batch, (hipStream_t)stream) ? ARM_MATH_SUCCESS : ARM_MATH_ARGUMENT_ERROR;
 }
 
-// ---- MFCC q31 (drop-in + batched) ------------------------------------------------
+// ---- MFCC q31 / q15 (drop-in + batched) -----------------------------------------
 // Drop-in: the reference's pSrc / pTmp work contents are not reproduced (device scratch).
-arm_status arm_mfcc_q31(const arm_mfcc_instance_q31* S, q31_t* pSrc, q31_t* pDst, q31_t* pTmp) {
-  (void)pTmp;
+}  // extern "C"
+template <typename T, typename Inst>
+static arm_status mfcc_fx_dropin(const Inst* S, T* pSrc, T* pDst, const char* what) {
   if (!S || !pSrc || !pDst) return ARM_MATH_ARGUMENT_ERROR;
   if (S->nbDctOutputs == 0) return ARM_MATH_SUCCESS;
-  MfccQ31Dev d;
-  if (!mfcc_q31_prepare(S, d)) return ARM_MATH_ARGUMENT_ERROR;
+  MfccFxDev<T> d;
+  if (!mfcc_fx_prepare<T>(S, d)) return ARM_MATH_ARGUMENT_ERROR;
   const uint32_t n = S->fftLen, nd = S->nbDctOutputs;
   hipStream_t st = sync_stream();
-  int32_t* x = (int32_t*)scratch(sizeof(int32_t) * n, 0);
-  int32_t* y = (int32_t*)scratch(sizeof(int32_t) * 2 * n, 1);
+  T* x = (T*)scratch(sizeof(T) * n, 0);
+  T* y = (T*)scratch(sizeof(T) * 2 * n, 1);
   const bool ddst = is_device_ptr(pDst);
-  int32_t* o = ddst ? pDst : (int32_t*)scratch(sizeof(int32_t) * nd, 2);
-  if (!x || !y || !o) { set_error(hipErrorOutOfMemory, "arm_mfcc_q31 scratch"); return ARM_MATH_ARGUMENT_ERROR; }
+  T* o = ddst ? pDst : (T*)scratch(sizeof(T) * nd, 2);
+  if (!x || !y || !o) { set_error(hipErrorOutOfMemory, what); return ARM_MATH_ARGUMENT_ERROR; }
   HostIO io(st);
-  hipError_t e = is_device_ptr(pSrc) ? hipMemcpyAsync(x, pSrc, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st)
-                                     : io.in(x, pSrc, sizeof(int32_t) * n);
-  if (e != hipSuccess) { set_error(e, "arm_mfcc_q31"); return ARM_MATH_ARGUMENT_ERROR; }
-  if (!mfcc_q31_run(S, d, x, y, o, 1, st)) { (void)hipStreamSynchronize(st); return ARM_MATH_ARGUMENT_ERROR; }
-  if (!ddst) e = io.out(pDst, o, sizeof(int32_t) * nd);
+  hipError_t e = is_device_ptr(pSrc) ? hipMemcpyAsync(x, pSrc, sizeof(T) * n, hipMemcpyDeviceToDevice, st)
+                                     : io.in(x, pSrc, sizeof(T) * n);
+  if (e != hipSuccess) { set_error(e, what); return ARM_MATH_ARGUMENT_ERROR; }
+  if (!mfcc_fx_run<T>(S, d, x, y, o, 1, st)) { (void)hipStreamSynchronize(st); return ARM_MATH_ARGUMENT_ERROR; }
+  if (!ddst) e = io.out(pDst, o, sizeof(T) * nd);
   if (e == hipSuccess) e = io.finish();
-  if (e != hipSuccess) { set_error(e, "arm_mfcc_q31"); return ARM_MATH_ARGUMENT_ERROR; }
+  if (e != hipSuccess) { set_error(e, what); return ARM_MATH_ARGUMENT_ERROR; }
   return ARM_MATH_SUCCESS;
 }
 
-arm_status arm_mfcc_q31_batch(const arm_mfcc_instance_q31* S, q31_t* d_src, q31_t* d_dst, q31_t* d_tmp,
-                              uint32_t batch, void* stream) {
+template <typename T, typename Inst>
+static arm_status mfcc_fx_batch(const Inst* S, T* d_src, T* d_dst, T* d_tmp, uint32_t batch, void* stream) {
   if (!S || (batch && (!d_src || !d_dst || !d_tmp))) return ARM_MATH_ARGUMENT_ERROR;
   if (batch == 0 || S->nbDctOutputs == 0) return ARM_MATH_SUCCESS;
-  MfccQ31Dev d;
-  if (!mfcc_q31_prepare(S, d)) return ARM_MATH_ARGUMENT_ERROR;
-  return mfcc_q31_run(S, d, d_src, d_tmp, d_dst, batch, (hipStream_t)stream) ? ARM_MATH_SUCCESS
-                                                                               : ARM_MATH_ARGUMENT_ERROR;
+  MfccFxDev<T> d;
+  if (!mfcc_fx_prepare<T>(S, d)) return ARM_MATH_ARGUMENT_ERROR;
+  return mfcc_fx_run<T>(S, d, d_src, d_tmp, d_dst, batch, (hipStream_t)stream) ? ARM_MATH_SUCCESS
+                                                                                : ARM_MATH_ARGUMENT_ERROR;
+}
+extern "C" {
+
+arm_status arm_mfcc_q31(const arm_mfcc_instance_q31* S, q31_t* pSrc, q31_t* pDst, q31_t* pTmp) {
+  (void)pTmp;
+  return mfcc_fx_dropin<int32_t>(S, pSrc, pDst, "arm_mfcc_q31");
+}
+arm_status arm_mfcc_q31_batch(const arm_mfcc_instance_q31* S, q31_t* d_src, q31_t* d_dst, q31_t* d_tmp,
+                              uint32_t batch, void* stream) {
+  return mfcc_fx_batch<int32_t>(S, d_src, d_dst, d_tmp, batch, stream);
+}
+arm_status arm_mfcc_q15(const arm_mfcc_instance_q15* S, q15_t* pSrc, q15_t* pDst, q31_t* pTmp) {
+  (void)pTmp;
+  return mfcc_fx_dropin<int16_t>(S, pSrc, pDst, "arm_mfcc_q15");
+}
+arm_status arm_mfcc_q15_batch(const arm_mfcc_instance_q15* S, q15_t* d_src, q15_t* d_dst, q15_t* d_tmp,
+                              uint32_t batch, void* stream) {
+  return mfcc_fx_batch<int16_t>(S, d_src, d_dst, d_tmp, batch, stream);
 }
 
 // ---- matrix multiply q15 / q31 --------------------------------------------------

@@ -232,6 +232,47 @@ MI_MFCC_Q31_INIT(2048)
 MI_MFCC_Q31_INIT(4096)
 #undef MI_MFCC_Q31_INIT
 
+// ---- MFCC q15 init (arm_mfcc_init_q15.c): fields + arm_rfft_init_q15(&S->rfft, L, 0, 1)
+static void mfcc_q15_fields(arm_mfcc_instance_q15* S, uint32_t fftLen, uint32_t nbMelFilters, uint32_t nbDctOutputs,
+                            const q15_t* dctCoefs, const uint32_t* filterPos, const uint32_t* filterLengths,
+                            const q15_t* filterCoefs, const q15_t* windowCoefs) {
+  S->fftLen = fftLen;
+  S->nbMelFilters = nbMelFilters;
+  S->nbDctOutputs = nbDctOutputs;
+  S->dctCoefs = dctCoefs;
+  S->filterPos = filterPos;
+  S->filterLengths = filterLengths;
+  S->filterCoefs = filterCoefs;
+  S->windowCoefs = windowCoefs;
+}
+
+arm_status arm_mfcc_init_q15(arm_mfcc_instance_q15* S, uint32_t fftLen, uint32_t nbMelFilters, uint32_t nbDctOutputs,
+                             const q15_t* dctCoefs, const uint32_t* filterPos, const uint32_t* filterLengths,
+                             const q15_t* filterCoefs, const q15_t* windowCoefs) {
+  mfcc_q15_fields(S, fftLen, nbMelFilters, nbDctOutputs, dctCoefs, filterPos, filterLengths, filterCoefs,
+                  windowCoefs);
+  return arm_rfft_init_q15(&S->rfft, fftLen, 0, 1);
+}
+
+#define MI_MFCC_Q15_INIT(N)                                                                                    \
+  arm_status arm_mfcc_init_##N##_q15(arm_mfcc_instance_q15* S, uint32_t nbMelFilters, uint32_t nbDctOutputs,   \
+                                     const q15_t* dctCoefs, const uint32_t* filterPos,                         \
+                                     const uint32_t* filterLengths, const q15_t* filterCoefs,                  \
+                                     const q15_t* windowCoefs) {                                               \
+    mfcc_q15_fields(S, N, nbMelFilters, nbDctOutputs, dctCoefs, filterPos, filterLengths, filterCoefs,         \
+                    windowCoefs);                                                                              \
+    return arm_rfft_init_##N##_q15(&S->rfft, 0, 1);                                                            \
+  }
+MI_MFCC_Q15_INIT(32)
+MI_MFCC_Q15_INIT(64)
+MI_MFCC_Q15_INIT(128)
+MI_MFCC_Q15_INIT(256)
+MI_MFCC_Q15_INIT(512)
+MI_MFCC_Q15_INIT(1024)
+MI_MFCC_Q15_INIT(2048)
+MI_MFCC_Q15_INIT(4096)
+#undef MI_MFCC_Q15_INIT
+
 // (FIR init zeroes a state buffer that may be device memory: it lives in api.cpp.)
 
 // ---- matrix init (arm_mat_init_f32.c, arm_mat_init_q15.c, arm_mat_init_q31.c)

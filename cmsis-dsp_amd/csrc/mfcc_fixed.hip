@@ -1,4 +1,4 @@
-// Batched MFCC q31 — MI355X kernels around the batched q31 real FFT, bit-exact.
+// Batched MFCC q31 / q15 — MI355X kernels around the batched fixed-point real FFT, bit-exact.
 //
 // Replaces Source/TransformFunctions/arm_mfcc_q31.c:88-225 (RFFT-based default build, host
 // scalar path: ARM_MATH_LOOPUNROLL, no ARM_MATH_DSP) for `batch` frames, in three
@@ -183,6 +183,140 @@ __global__ __launch_bounds__(256) void mfcc_q31_post_kernel(const int32_t* __res
       o[r] = (int32_t)(sum >> 31);
     }
   }
+}
+
+// ---------------------------------------------------------------- q15
+// arm_mfcc_q15.c:96-228: the same three launches on q15 frames.  pre: m = max sat|x| (q15),
+// arm_divide_q15(0x7FFF, m) -> x = __SSAT((x * quot) >> (15 - shift), 16) (arm_scale_q15),
+// x = __SSAT((x * w) >> 15, 16) (arm_mult_q15).  post: |Y_k| = sqrt_q31(((u32)re² + (u32)im²)
+// >> 1) >> 16 (arm_cmplx_mag_q15), Mel = __SSAT((Σ mag·c + MICRO_Q15) >> 10, 31), scale_q31 by
+// m << 16, log_q31, offset, >> 19, truncated to q15; DCT rows as arm_mat_vec_mult_q15 with
+// its __SMLALD column pairs (int32-wrapped pair sums, none.h:497-506).
+__device__ __forceinline__ int32_t mq_sat_abs15(int32_t x) { return x > 0 ? x : (x == -32768 ? 32767 : -x); }
+__device__ __forceinline__ int32_t mq_ssat16(int32_t v) { return v > 32767 ? 32767 : (v < -32768 ? -32768 : v); }
+
+__global__ __launch_bounds__(256) void mfcc_q15_pre_kernel(const int16_t* src, const int16_t* __restrict__ win,
+                                                           int16_t* x, int16_t* maxv, int maxv_stride, int n,
+                                                           uint32_t batch) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t frame = blockIdx.x * kMqWaves + (threadIdx.x >> 6);
+  if (frame >= batch) return;
+  const short4* s = reinterpret_cast<const short4*>(src + (size_t)frame * n);
+  const short4* w = reinterpret_cast<const short4*>(win);
+  short4* o = reinterpret_cast<short4*>(x + (size_t)frame * n);
+  const int n4 = n >> 2;
+  int32_t m = 0;
+  for (int i = lane; i < n4; i += 64) {
+    const short4 v = s[i];
+    m = max(m, max(max(mq_sat_abs15(v.x), mq_sat_abs15(v.y)), max(mq_sat_abs15(v.z), mq_sat_abs15(v.w))));
+  }
+  m = wave_max_i(m);
+  const bool scale = m != 0 && m != 0x7FFF;
+  int32_t quot = 0, k = 15;
+  if (scale) {   // arm_divide_q15(0x7FFF, m): temp = (0x7FFF << 15) / m, normalised by 17 - clz(temp)
+    int32_t t = (int32_t)((0x7FFFu << 15) / (uint32_t)m);
+    const int sn = 17 - (int)mq_clz((uint32_t)t);
+    int sh = 0;
+    if (sn > 0) {
+      sh = sn;
+      t >>= sn;
+    }
+    quot = (int32_t)(int16_t)t;
+    k = (int)(int8_t)(15 - sh);
+  }
+  for (int i = lane; i < n4; i += 64) {
+    short4 v = s[i];
+    int32_t a[4] = {v.x, v.y, v.z, v.w};
+    const short4 c = w[i];
+    const int32_t cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (scale) a[j] = mq_ssat16((a[j] * quot) >> k);
+      a[j] = mq_ssat16((a[j] * cw[j]) >> 15);
+    }
+    o[i] = make_short4((short)a[0], (short)a[1], (short)a[2], (short)a[3]);
+  }
+  if (lane == 0) maxv[(size_t)frame * maxv_stride] = (int16_t)m;
+}
+
+__global__ __launch_bounds__(256) void mfcc_q15_post_kernel(const int16_t* __restrict__ y, const int16_t* maxv,
+                                                            int maxv_stride, int n, int nb_mel,
+                                                            const uint32_t* __restrict__ pos,
+                                                            const uint32_t* __restrict__ len,
+                                                            const uint32_t* __restrict__ off,
+                                                            const int16_t* __restrict__ coefs, int nb_dct,
+                                                            const int16_t* __restrict__ dct,
+                                                            const int32_t* __restrict__ lut, int16_t* dst,
+                                                            uint32_t batch) {
+  extern __shared__ int32_t shq[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lim = (n >> 1) + 1;
+  int32_t* mag = shq + wave * (lim + nb_mel);
+  int32_t* mel = mag + lim;
+  const uint32_t frame = blockIdx.x * kMqWaves + wave;
+  const bool live = frame < batch;
+  const int32_t m = live ? maxv[(size_t)frame * maxv_stride] : 0;
+  const bool scale = m != 0 && m != 0x7FFF;
+  if (live) {
+    const short2* Y = reinterpret_cast<const short2*>(y + (size_t)frame * 2 * n);
+    for (int k = lane; k < lim; k += 64) {
+      const short2 c = Y[k];
+      const uint32_t s2 = ((uint32_t)((int32_t)c.x * c.x) + (uint32_t)((int32_t)c.y * c.y)) >> 1;
+      mag[k] = mq_sqrt((int32_t)s2, lut) >> 16;
+    }
+  }
+  __syncthreads();
+  const int32_t le = (int32_t)((uint32_t)(31 - (int)mq_clz((uint32_t)n) + 12) * 0x02C5C860u);
+  if (live) {
+    for (int i = lane; i < nb_mel; i += 64) {
+      const uint32_t p = pos[i], l = len[i];
+      const int16_t* c = coefs + off[i];
+      int64_t r = 0;
+      for (uint32_t j = 0; j < l; ++j) r += (int64_t)(mag[p + j] * (int32_t)c[j]);
+      r += 0x219;                                      // MICRO_Q15
+      r >>= 10;                                        // SHIFT_MELFILTER_SATURATION_Q15
+      int32_t v = mq_ssat31((int32_t)r);
+      if (scale) v = mq_scale(v, (int32_t)((uint32_t)m << 16), 1);
+      const int64_t s = (int64_t)mq_log((uint32_t)v) + le;
+      v = s > INT32_MAX ? INT32_MAX : (s < INT32_MIN ? INT32_MIN : (int32_t)s);
+      mel[i] = (int32_t)(int16_t)(v >> 19);            // (q15_t) truncation
+    }
+  }
+  __syncthreads();
+  if (live) {
+    int16_t* o = dst + (size_t)frame * nb_dct;
+    const int grouped = nb_dct & ~3;
+    for (int r = lane; r < nb_dct; r += 64) {
+      const int16_t* d = dct + (size_t)r * nb_mel;
+      const int paired = r < grouped ? (nb_mel & ~1) : (nb_mel & ~3);
+      int64_t sum = 0;
+      for (int i = 0; i < paired; i += 2)
+        sum += (int32_t)((uint32_t)(d[i] * mel[i]) + (uint32_t)(d[i + 1] * mel[i + 1]));
+      for (int i = paired; i < nb_mel; ++i) sum += (int64_t)(d[i] * mel[i]);
+      o[r] = (int16_t)mq_ssat16((int32_t)(sum >> 15));
+    }
+  }
+}
+
+hipError_t mfcc_q15_pre_launch(int n, const int16_t* src, const int16_t* win, int16_t* x, int16_t* maxv,
+                               uint32_t batch, int maxv_stride, hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  if (n < 32 || (n & 3)) return hipErrorInvalidValue;
+  const uint32_t grid = (batch + kMqWaves - 1) / kMqWaves;
+  hipLaunchKernelGGL(mfcc_q15_pre_kernel, dim3(grid), dim3(64 * kMqWaves), 0, st, src, win, x, maxv, maxv_stride, n,
+                     batch);
+  return hipGetLastError();
+}
+
+hipError_t mfcc_q15_post_launch(int n, const int16_t* y, const int16_t* maxv, int maxv_stride, int nb_mel,
+                                const uint32_t* pos, const uint32_t* len, const uint32_t* off, const int16_t* coefs,
+                                int nb_dct, const int16_t* dct, const int32_t* lut, int16_t* dst, uint32_t batch,
+                                hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  const uint32_t grid = (batch + kMqWaves - 1) / kMqWaves;
+  hipLaunchKernelGGL(mfcc_q15_post_kernel, dim3(grid), dim3(64 * kMqWaves), mfcc_q31_post_lds(n, nb_mel), st, y,
+                     maxv, maxv_stride, n, nb_mel, pos, len, off, coefs, nb_dct, dct, lut, dst, batch);
+  return hipGetLastError();
 }
 
 hipError_t mfcc_q31_pre_launch(int n, const int32_t* src, const int32_t* win, int32_t* x, int32_t* maxv,

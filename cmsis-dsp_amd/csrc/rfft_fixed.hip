@@ -8,7 +8,7 @@
 //        (!ARM_MATH_DSP branches);
 //   the inverse's arm_shift_q31 / arm_shift_q15 by +1 is folded into the inverse CFFT's
 //   store (kSatShl1, cfft_fixed.hip).
-// L = N/2 complex bins of the inner CFFT.  One thread per (signal, k), k in [0, L):
+// L = N/2 complex bins of the inner CFFT.  One thread per k for 8 signals, k in [0, L):
 //   forward: reads bins k and L-k of the CFFT output, writes spectrum bin k and, for
 //            k >= 1, its mirror N-k (thread k = 0 writes bins 0 and L) -> 2N words out;
 //   inverse: reads bins k and L-k of the 2N-word spectrum row, writes bin k of the N-word
@@ -42,77 +42,100 @@ template <> struct Cx<int16_t> {
   }
 };
 
+// Work mapping: a workgroup takes kper = min(L, 256) consecutive k for R signals at a time
+// (256 / kper signals side by side); each thread loads its k's twiddles once — a strided
+// gather, realCoef index 2*mod*k — and reuses them for its R signals (the gather per element
+// bound the pass: 1.39 ms for 2^18 x 1024-point q31 splits at one signal per thread).
+constexpr int kRfftRows = 8;
+struct RfftMap {
+  uint64_t row0;    // first signal of this thread
+  uint32_t rstep;   // signals between this thread's consecutive rows
+  int k;
+};
+__device__ __forceinline__ RfftMap rfft_map(int L) {
+  const int kper = L < 256 ? L : 256;
+  const uint32_t nk = (uint32_t)(L / kper), side = 256u / (uint32_t)kper;
+  const uint32_t kc = blockIdx.x % nk, rg = blockIdx.x / nk;
+  RfftMap m;
+  m.k = (int)(kc * kper + threadIdx.x % kper);
+  m.rstep = side;
+  m.row0 = (uint64_t)rg * side * kRfftRows + threadIdx.x / kper;
+  return m;
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void rfft_fx_split_kernel(const T* __restrict__ src, T* __restrict__ dst,
-                                                            uint64_t total, int n, int log2l,
-                                                            const T* __restrict__ ta, const T* __restrict__ tb,
-                                                            uint32_t mod) {
-  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= total) return;
+                                                            uint64_t rows, int n, const T* __restrict__ ta,
+                                                            const T* __restrict__ tb, uint32_t mod) {
   const int L = n >> 1;
-  const uint64_t row = gid >> log2l;
-  const int k = (int)(gid & (uint64_t)(L - 1));
-  const T* x = src + row * (uint64_t)n;
-  T* y = dst + row * (uint64_t)(2 * n);
-  if (k == 0) {
-    const int2 v = Cx<T>::ld(x);
-    if constexpr (sizeof(T) == 4) {
-      Cx<T>::st(y + n, wsub(v.x, v.y) >> 1, 0);
-      Cx<T>::st(y, wadd(v.x, v.y) >> 1, 0);
-    } else {
-      Cx<T>::st(y + n, (v.x - v.y) >> 1, 0);
-      Cx<T>::st(y, (v.x + v.y) >> 1, 0);
-    }
-    return;
-  }
-  const int2 a = Cx<T>::ld(x + 2 * k), b = Cx<T>::ld(x + 2 * (L - k));
+  const RfftMap mp = rfft_map(L);
+  const int k = mp.k;
   const uint32_t c = 2u * mod * (uint32_t)k;
-  const int32_t a1 = ta[c], a2 = ta[c + 1], b1 = tb[c];
-  if constexpr (sizeof(T) == 4) {
-    // arm_rfft_q31.c:293-326
-    int32_t re = mult_R(a.x, a1), im = mult_R(a.x, a2);
-    re = multSub_R(re, a.y, a2); im = multAcc_R(im, a.y, a1);
-    re = multSub_R(re, b.y, a2); im = multSub_R(im, b.y, b1);
-    re = multAcc_R(re, b.x, b1); im = multSub_R(im, b.x, a2);
-    Cx<T>::st(y + 2 * k, re, im);
-    Cx<T>::st(y + 2 * n - 2 * k, re, wneg(im));
-  } else {
-    // arm_rfft_q15.c scalar branch: wrapping int sums, >> 16, stores truncate to q15_t
-    const int32_t b2 = tb[c + 1];
-    const int32_t re = (int32_t)(p16(a.x, a1) - p16(a.y, a2) + p16(b.x, b1) + p16(b.y, b2)) >> 16;
-    const int32_t im = (int32_t)(p16(b.x, b2) - p16(b.y, b1) + p16(a.y, a1) + p16(a.x, a2)) >> 16;
-    Cx<T>::st(y + 2 * k, re, im);
-    Cx<T>::st(y + 2 * n - 2 * k, re, -im);
+  const int32_t a1 = ta[c], a2 = ta[c + 1], b1 = tb[c], b2 = tb[c + 1];
+#pragma unroll 2
+  for (int r = 0; r < kRfftRows; ++r) {
+    const uint64_t row = mp.row0 + (uint64_t)r * mp.rstep;
+    if (row >= rows) break;
+    const T* x = src + row * (uint64_t)n;
+    T* y = dst + row * (uint64_t)(2 * n);
+    if (k == 0) {
+      const int2 v = Cx<T>::ld(x);
+      if constexpr (sizeof(T) == 4) {
+        Cx<T>::st(y + n, wsub(v.x, v.y) >> 1, 0);
+        Cx<T>::st(y, wadd(v.x, v.y) >> 1, 0);
+      } else {
+        Cx<T>::st(y + n, (v.x - v.y) >> 1, 0);
+        Cx<T>::st(y, (v.x + v.y) >> 1, 0);
+      }
+      continue;
+    }
+    const int2 a = Cx<T>::ld(x + 2 * k), b = Cx<T>::ld(x + 2 * (L - k));
+    if constexpr (sizeof(T) == 4) {
+      // arm_rfft_q31.c:293-326
+      int32_t re = mult_R(a.x, a1), im = mult_R(a.x, a2);
+      re = multSub_R(re, a.y, a2); im = multAcc_R(im, a.y, a1);
+      re = multSub_R(re, b.y, a2); im = multSub_R(im, b.y, b1);
+      re = multAcc_R(re, b.x, b1); im = multSub_R(im, b.x, a2);
+      Cx<T>::st(y + 2 * k, re, im);
+      Cx<T>::st(y + 2 * n - 2 * k, re, wneg(im));
+    } else {
+      // arm_rfft_q15.c scalar branch: wrapping int sums, >> 16, stores truncate to q15_t
+      const int32_t re = (int32_t)(p16(a.x, a1) - p16(a.y, a2) + p16(b.x, b1) + p16(b.y, b2)) >> 16;
+      const int32_t im = (int32_t)(p16(b.x, b2) - p16(b.y, b1) + p16(a.y, a1) + p16(a.x, a2)) >> 16;
+      Cx<T>::st(y + 2 * k, re, im);
+      Cx<T>::st(y + 2 * n - 2 * k, re, -im);
+    }
   }
 }
 
 template <typename T>
 __global__ __launch_bounds__(256) void rfft_fx_merge_kernel(const T* __restrict__ src, T* __restrict__ dst,
-                                                            uint64_t total, int n, int log2l,
-                                                            const T* __restrict__ ta, const T* __restrict__ tb,
-                                                            uint32_t mod) {
-  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= total) return;
+                                                            uint64_t rows, int n, const T* __restrict__ ta,
+                                                            const T* __restrict__ tb, uint32_t mod) {
   const int L = n >> 1;
-  const uint64_t row = gid >> log2l;
-  const int k = (int)(gid & (uint64_t)(L - 1));
-  const T* x = src + row * (uint64_t)(2 * n);
-  T* y = dst + row * (uint64_t)n;
-  const int2 a = Cx<T>::ld(x + 2 * k), b = Cx<T>::ld(x + 2 * (L - k));
+  const RfftMap mp = rfft_map(L);
+  const int k = mp.k;
   const uint32_t c = 2u * mod * (uint32_t)k;
-  const int32_t a1 = ta[c], a2 = ta[c + 1], b1 = tb[c];
-  if constexpr (sizeof(T) == 4) {
-    // arm_rfft_q31.c:430-466
-    int32_t re = mult_R(a.x, a1), im = mult_R(a.x, wneg(a2));
-    re = multAcc_R(re, a.y, a2); im = multAcc_R(im, a.y, a1);
-    re = multAcc_R(re, b.y, a2); im = multSub_R(im, b.y, b1);
-    re = multAcc_R(re, b.x, b1); im = multAcc_R(im, b.x, a2);
-    Cx<T>::st(y + 2 * k, re, im);
-  } else {
-    const int32_t b2 = tb[c + 1];
-    const int32_t re = (int32_t)(p16(b.x, b1) - p16(b.y, b2) + p16(a.x, a1) + p16(a.y, a2)) >> 16;
-    const int32_t im = (int32_t)(p16(a.y, a1) - p16(a.x, a2) - p16(b.x, b2) - p16(b.y, b1)) >> 16;
-    Cx<T>::st(y + 2 * k, re, im);
+  const int32_t a1 = ta[c], a2 = ta[c + 1], b1 = tb[c], b2 = tb[c + 1];
+#pragma unroll 2
+  for (int r = 0; r < kRfftRows; ++r) {
+    const uint64_t row = mp.row0 + (uint64_t)r * mp.rstep;
+    if (row >= rows) break;
+    const T* x = src + row * (uint64_t)(2 * n);
+    T* y = dst + row * (uint64_t)n;
+    const int2 a = Cx<T>::ld(x + 2 * k), b = Cx<T>::ld(x + 2 * (L - k));
+    if constexpr (sizeof(T) == 4) {
+      // arm_rfft_q31.c:430-466
+      int32_t re = mult_R(a.x, a1), im = mult_R(a.x, wneg(a2));
+      re = multAcc_R(re, a.y, a2); im = multAcc_R(im, a.y, a1);
+      re = multAcc_R(re, b.y, a2); im = multSub_R(im, b.y, b1);
+      re = multAcc_R(re, b.x, b1); im = multAcc_R(im, b.x, a2);
+      Cx<T>::st(y + 2 * k, re, im);
+    } else {
+      const int32_t re = (int32_t)(p16(b.x, b1) - p16(b.y, b2) + p16(a.x, a1) + p16(a.y, a2)) >> 16;
+      const int32_t im = (int32_t)(p16(a.y, a1) - p16(a.x, a2) - p16(b.x, b2) - p16(b.y, b1)) >> 16;
+      Cx<T>::st(y + 2 * k, re, im);
+    }
   }
 }
 
@@ -122,17 +145,16 @@ template <typename T>
 static hipError_t rfft_fx_pass(bool inverse, int n, const T* src, T* dst, uint32_t batch, const T* ta, const T* tb,
                                uint32_t mod, hipStream_t st) {
   if (batch == 0) return hipSuccess;
-  int log2l = 0;
-  while ((1 << log2l) < n / 2) ++log2l;
-  const uint64_t total = (uint64_t)batch << log2l;
-  const uint64_t blocks = (total + 255) / 256;
+  const int L = n / 2, kper = L < 256 ? L : 256;
+  const uint64_t side = 256 / kper, groups = (batch + side * kRfftRows - 1) / (side * kRfftRows);
+  const uint64_t blocks = groups * (uint64_t)(L / kper);
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
   if (inverse)
-    hipLaunchKernelGGL((rfft_fx_merge_kernel<T>), dim3((uint32_t)blocks), dim3(256), 0, st, src, dst, total, n, log2l,
-                       ta, tb, mod);
+    hipLaunchKernelGGL((rfft_fx_merge_kernel<T>), dim3((uint32_t)blocks), dim3(256), 0, st, src, dst, (uint64_t)batch,
+                       n, ta, tb, mod);
   else
-    hipLaunchKernelGGL((rfft_fx_split_kernel<T>), dim3((uint32_t)blocks), dim3(256), 0, st, src, dst, total, n, log2l,
-                       ta, tb, mod);
+    hipLaunchKernelGGL((rfft_fx_split_kernel<T>), dim3((uint32_t)blocks), dim3(256), 0, st, src, dst, (uint64_t)batch,
+                       n, ta, tb, mod);
   return hipGetLastError();
 }
 

@@ -123,6 +123,19 @@ typedef struct {
   arm_rfft_instance_q31 rfft;
 } arm_mfcc_instance_q31;
 
+/* Include/dsp/transform_functions.h:1150-1168 (RFFT-based default build) */
+typedef struct {
+  const q15_t    *dctCoefs;
+  const q15_t    *filterCoefs;
+  const q15_t    *windowCoefs;
+  const uint32_t *filterPos;
+  const uint32_t *filterLengths;
+        uint32_t   fftLen;
+        uint32_t   nbMelFilters;
+        uint32_t   nbDctOutputs;
+  arm_rfft_instance_q15 rfft;
+} arm_mfcc_instance_q15;
+
 /* ---- FIR instances: Include/dsp/filtering_functions.h:56-61 (q7), 66-71, 76-81, 86-91 */
 typedef struct {
         uint16_t   numTaps;
@@ -418,6 +431,28 @@ ARM_MI355X_DECL_MFCC_Q31_INIT(2048)
 ARM_MI355X_DECL_MFCC_Q31_INIT(4096)
 #undef ARM_MI355X_DECL_MFCC_Q31_INIT
 arm_status arm_mfcc_q31(const arm_mfcc_instance_q31 *S, q31_t *pSrc, q31_t *pDst, q31_t *pTmp);
+
+/* MFCC q15.  Reference bodies: Source/TransformFunctions/arm_mfcc_init_q15.c, arm_mfcc_q15.c:96-228
+ * (RFFT-based default path; q15 input, q8.7 output, q31 work buffer).  Same buffer contract as
+ * arm_mfcc_q31. */
+arm_status arm_mfcc_init_q15(arm_mfcc_instance_q15 *S, uint32_t fftLen, uint32_t nbMelFilters, uint32_t nbDctOutputs,
+                             const q15_t *dctCoefs, const uint32_t *filterPos, const uint32_t *filterLengths,
+                             const q15_t *filterCoefs, const q15_t *windowCoefs);
+#define ARM_MI355X_DECL_MFCC_Q15_INIT(N)                                                                    \
+  arm_status arm_mfcc_init_##N##_q15(arm_mfcc_instance_q15 *S, uint32_t nbMelFilters, uint32_t nbDctOutputs, \
+                                     const q15_t *dctCoefs, const uint32_t *filterPos,                       \
+                                     const uint32_t *filterLengths, const q15_t *filterCoefs,                \
+                                     const q15_t *windowCoefs);
+ARM_MI355X_DECL_MFCC_Q15_INIT(32)
+ARM_MI355X_DECL_MFCC_Q15_INIT(64)
+ARM_MI355X_DECL_MFCC_Q15_INIT(128)
+ARM_MI355X_DECL_MFCC_Q15_INIT(256)
+ARM_MI355X_DECL_MFCC_Q15_INIT(512)
+ARM_MI355X_DECL_MFCC_Q15_INIT(1024)
+ARM_MI355X_DECL_MFCC_Q15_INIT(2048)
+ARM_MI355X_DECL_MFCC_Q15_INIT(4096)
+#undef ARM_MI355X_DECL_MFCC_Q15_INIT
+arm_status arm_mfcc_q15(const arm_mfcc_instance_q15 *S, q15_t *pSrc, q15_t *pDst, q31_t *pTmp);
 
 /* ===================================================================================
  * FIR.  Prototypes: Include/dsp/filtering_functions.h:141-145,175-180,233-237,260-265

@@ -65,6 +65,10 @@ arm_status arm_mfcc_f32_batch(const arm_mfcc_instance_f32 *S, float32_t *d_src, 
  * d_src [batch][fftLen] (overwritten), d_tmp [batch][2*fftLen] work, d_dst [batch][nbDct]. */
 arm_status arm_mfcc_q31_batch(const arm_mfcc_instance_q31 *S, q31_t *d_src, q31_t *d_dst, q31_t *d_tmp,
                               uint32_t batch, void *stream);
+/* MFCC q15 over `batch` contiguous frames (arm_mfcc_q15.c:96-228 per frame, bit-exact):
+ * d_src [batch][fftLen] (overwritten), d_tmp [batch][2*fftLen] q15 work, d_dst [batch][nbDct]. */
+arm_status arm_mfcc_q15_batch(const arm_mfcc_instance_q15 *S, q15_t *d_src, q15_t *d_dst, q15_t *d_tmp,
+                              uint32_t batch, void *stream);
 
 /* FIR over `batch` independent filters sharing S->numTaps / S->pCoeffs (host or device
  * pointer; S->pState is not used).  d_src/d_dst: [batch][blockSize].  d_hist:

@@ -7,7 +7,7 @@
  * Usage: bench_xxx <workload> <n> <threads> <seconds>
  *   workload: cfft_f32 | cfft_q31 | cfft_q15 (n = fftLen), fir_f32 | fir_q15 (n = numTaps, block 4096),
  *             rfft_f32 | rfft_q31 | rfft_q15 (n = real length, forward),
- *             mat_mult_f32 (n = square dimension), mfcc_f32 / mfcc_q31 (n = fftLen; 20 triangular
+ *             mat_mult_f32 (n = square dimension), mfcc_f32 / mfcc_q31 / mfcc_q15 (n = fftLen; 20 triangular
  *             Mel filters, 13 DCT outputs, Hamming window -- the suite's shape)
  * Each thread owns its own buffers (the library is reentrant) and runs until the time
  * budget is spent; in-place transforms alternate forward / inverse to stay bounded.
@@ -202,6 +202,35 @@ static void *worker(void *arg) {
     do {
       memcpy(src, x, sizeof(int32_t) * n);
       F(arm_mfcc_q31)(&S, src, out, tmp);
+      samples += n;
+    } while (now() - t0 < j->seconds);
+    free(coefs); free(win); free(x); free(src); free(tmp);
+  } else if (!strcmp(j->wl, "mfcc_q15")) {           /* the same shape in q15 */
+    const int n = j->n, nm = 20, nd = 13;
+    uint32_t pos[20], len[20], total = 0;
+    int16_t *coefs = malloc(sizeof(int16_t) * n), dct[13 * 20];
+    int16_t *win = malloc(sizeof(int16_t) * n), *x = malloc(sizeof(int16_t) * n), *src = malloc(sizeof(int16_t) * n);
+    int32_t *tmp = calloc(2 * n, sizeof(int32_t));
+    int16_t out[13];
+    for (int i = 0; i < nm; ++i) {
+      pos[i] = 1 + (uint32_t)i * (n / 2 - 2) / (nm + 1);
+      len[i] = 2 * ((n / 2 - 2) / (nm + 1)) + 1;
+      if (pos[i] + len[i] > (uint32_t)n / 2) len[i] = n / 2 - pos[i];
+      for (uint32_t k = 0; k < len[i]; ++k)
+        coefs[total + k] = (int16_t)(32767.0 * (1.0 - fabs((double)k - len[i] / 2.0) / len[i]));
+      total += len[i];
+    }
+    for (int r = 0; r < nd; ++r)
+      for (int c = 0; c < nm; ++c) dct[r * nm + c] = (int16_t)(0.3 * 32767.0 * cos(3.14159265358979 / nm * (c + 0.5) * r));
+    for (int i = 0; i < n; ++i) {
+      win[i] = (int16_t)(32767.0 * (0.54 - 0.46 * cos(6.283185307179586 * i / n)));
+      x[i] = (int16_t)sm(&seed);
+    }
+    arm_mfcc_instance_q15 S;
+    F(arm_mfcc_init_q15)(&S, n, nm, nd, dct, pos, len, coefs, win);
+    do {
+      memcpy(src, x, sizeof(int16_t) * n);
+      F(arm_mfcc_q15)(&S, src, out, tmp);
       samples += n;
     } while (now() - t0 < j->seconds);
     free(coefs); free(win); free(x); free(src); free(tmp);

@@ -59,6 +59,9 @@ SRCS := \
   $(T)/arm_mfcc_q31.c $(T)/arm_mfcc_init_q31.c $(ST)/arm_absmax_q31.c $(FM)/arm_divide_q31.c \
   $(B)/arm_scale_q31.c $(B)/arm_mult_q31.c $(B)/arm_abs_q31.c $(X)/arm_cmplx_mag_q31.c $(FM)/arm_sqrt_q31.c \
   $(B)/arm_dot_prod_q31.c $(FM)/arm_vlog_q31.c $(B)/arm_offset_q31.c $(M)/arm_mat_vec_mult_q31.c \
+  $(T)/arm_mfcc_q15.c $(T)/arm_mfcc_init_q15.c $(ST)/arm_absmax_q15.c $(FM)/arm_divide_q15.c \
+  $(B)/arm_scale_q15.c $(B)/arm_mult_q15.c $(B)/arm_abs_q15.c $(X)/arm_cmplx_mag_q15.c $(B)/arm_dot_prod_q15.c \
+  $(M)/arm_mat_vec_mult_q15.c \
   $(C)/arm_common_tables.c $(C)/arm_const_structs.c
 
 OBJS := $(patsubst $(REF)/Source/%.c,$(OUT)/obj/%.o,$(SRCS))

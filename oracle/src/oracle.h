@@ -44,6 +44,11 @@ arm_status oracle_arm_mfcc_init_q31(arm_mfcc_instance_q31 *S, uint32_t fftLen, u
                                     const uint32_t *filterLengths, const int32_t *filterCoefs,
                                     const int32_t *windowCoefs);
 arm_status oracle_arm_mfcc_q31(const arm_mfcc_instance_q31 *S, int32_t *pSrc, int32_t *pDst, int32_t *pTmp);
+arm_status oracle_arm_mfcc_init_q15(arm_mfcc_instance_q15 *S, uint32_t fftLen, uint32_t nbMelFilters,
+                                    uint32_t nbDctOutputs, const int16_t *dctCoefs, const uint32_t *filterPos,
+                                    const uint32_t *filterLengths, const int16_t *filterCoefs,
+                                    const int16_t *windowCoefs);
+arm_status oracle_arm_mfcc_q15(const arm_mfcc_instance_q15 *S, int16_t *pSrc, int16_t *pDst, int32_t *pTmp);
 /* sparse FIR (oracle_multirate.c), the reference's signatures */
 #define ORACLE_SPARSE_PROTO(T, ET)                                                                          \
   void oracle_arm_fir_sparse_init_##T(arm_fir_sparse_instance_##T *S, uint16_t numTaps, const ET *pCoeffs, \

@@ -169,3 +169,100 @@ arm_status oracle_arm_mfcc_q31(const arm_mfcc_instance_q31 *S, int32_t *pSrc, in
   }
   return ARM_MATH_SUCCESS;
 }
+
+/*
+ * arm_mfcc_q15 (Source/TransformFunctions/arm_mfcc_q15.c:96-228), q15 frames, q31 work:
+ *   m      = max sat|x| (q15)                           arm_absmax_q15.c
+ *   if m != 0 and m != 0x7FFF:
+ *     (quot, sh) = divide_q15(0x7FFF, m)               arm_divide_q15.c (temp = (n << 15) / d,
+ *                                                       normalised by 17 - clz(temp))
+ *     x = ssat16((x·quot) >> (15 - sh))                arm_scale_q15.c
+ *   x      = ssat16((x·w) >> 15)                        arm_mult_q15.c
+ *   tmp    = rfft_q15(x)
+ *   mag_k  = sqrt_q31(((u32)re² + (u32)im²) >> 1) >> 16, k = 0 .. fftLen/2   arm_cmplx_mag_q15.c
+ *   mel_i  = ssat31((int32)((Σ mag·c + MICRO_Q15) >> 10))                    arm_dot_prod_q15.c
+ *   mel    = scale_q31(mel, m << 16, 0) if m != 0, 0x7FFF
+ *   mel    = (q15)(qadd(log_q31(mel), (fftShift + 12)·LOG2TOLOG) >> 19)     (a truncation)
+ *   out_r  = ssat16((int32)(Σ dct[r][i]·mel_i >> 15))   arm_mat_vec_mult_q15.c, whose __SMLALD
+ *            column pairs wrap in int32 (none.h:497-506): rows in groups of four pair columns
+ *            (0,1),(2,3).. up to numCols & ~1; the other rows pair within whole column quads;
+ *            the remaining columns add exactly.
+ */
+#define O_MICRO_Q15 0x00000219
+
+static int16_t o_sat_abs15(int16_t x) { return x > 0 ? x : (x == INT16_MIN ? INT16_MAX : (int16_t)-x); }
+static int16_t o_ssat16(int32_t v) { return (int16_t)(v > 32767 ? 32767 : (v < -32768 ? -32768 : v)); }
+
+arm_status oracle_arm_mfcc_init_q15(arm_mfcc_instance_q15 *S, uint32_t fftLen, uint32_t nbMelFilters,
+                                    uint32_t nbDctOutputs, const int16_t *dctCoefs, const uint32_t *filterPos,
+                                    const uint32_t *filterLengths, const int16_t *filterCoefs,
+                                    const int16_t *windowCoefs) {
+  S->fftLen = fftLen;
+  S->nbMelFilters = nbMelFilters;
+  S->nbDctOutputs = nbDctOutputs;
+  S->dctCoefs = dctCoefs;
+  S->filterPos = filterPos;
+  S->filterLengths = filterLengths;
+  S->filterCoefs = filterCoefs;
+  S->windowCoefs = windowCoefs;
+  return oracle_arm_rfft_init_q15(&S->rfft, fftLen, 0, 1);
+}
+
+arm_status oracle_arm_mfcc_q15(const arm_mfcc_instance_q15 *S, int16_t *pSrc, int16_t *pDst, int32_t *pTmp) {
+  const uint32_t n = S->fftLen, nm = S->nbMelFilters;
+  int16_t *pTmp2 = (int16_t *)pTmp;
+  int16_t m = o_sat_abs15(pSrc[0]);
+  for (uint32_t i = 1; i < n; ++i) {
+    const int16_t a = o_sat_abs15(pSrc[i]);
+    if (a > m) m = a;
+  }
+  const int scale = m != 0 && m != 0x7FFF;
+  if (scale) {
+    int32_t t = ((int32_t)0x7FFF << 15) / (int32_t)m;
+    int sh = 0;
+    const int sn = 17 - (int)o_clz((uint32_t)t);
+    if (sn > 0) {
+      sh = sn;
+      t >>= sn;
+    }
+    const int16_t quot = (int16_t)t;
+    const int k = (int)(int8_t)(15 - sh);
+    for (uint32_t i = 0; i < n; ++i) pSrc[i] = o_ssat16(((int32_t)pSrc[i] * quot) >> k);
+  }
+  for (uint32_t i = 0; i < n; ++i) pSrc[i] = o_ssat16(((int32_t)pSrc[i] * S->windowCoefs[i]) >> 15);
+  const uint32_t fftShift = 31 - o_clz(n);
+  oracle_arm_rfft_q15(&S->rfft, pSrc, pTmp2);
+  for (uint32_t k = 0; k < 1 + (n >> 1); ++k) {
+    const int32_t re = pTmp2[2 * k], im = pTmp2[2 * k + 1];
+    const uint32_t s2 = ((uint32_t)(re * re) + (uint32_t)(im * im)) >> 1;
+    pSrc[k] = (int16_t)(o_sqrt((int32_t)s2) >> 16);
+  }
+  uint32_t cp = 0;
+  for (uint32_t i = 0; i < nm; ++i) {
+    int64_t r = 0;
+    for (uint32_t j = 0; j < S->filterLengths[i]; ++j)
+      r += (int64_t)((int32_t)pSrc[S->filterPos[i] + j] * S->filterCoefs[cp + j]);
+    cp += S->filterLengths[i];
+    r += O_MICRO_Q15;
+    r >>= O_SHIFT_MELFILTER_SATURATION_Q31;
+    pTmp[i] = o_ssat((int32_t)r, 31);
+  }
+  if (scale) o_scale(pTmp, nm, (int32_t)((uint32_t)(int32_t)m << 16), 0);
+  const int32_t le = (int32_t)((fftShift + 2 + O_SHIFT_MELFILTER_SATURATION_Q31) * O_LOG2TOLOG_Q31);
+  for (uint32_t i = 0; i < nm; ++i) {
+    const int64_t s = (int64_t)o_log((uint32_t)pTmp[i]) + le;
+    const int32_t v = s > INT32_MAX ? INT32_MAX : (s < INT32_MIN ? INT32_MIN : (int32_t)s);
+    pSrc[i] = (int16_t)(v >> 19);
+  }
+  const uint32_t nd = S->nbDctOutputs, grouped = nd & ~3u;
+  for (uint32_t r = 0; r < nd; ++r) {
+    const int16_t *a = S->dctCoefs + (size_t)r * nm;
+    const uint32_t paired = r < grouped ? (nm & ~1u) : (nm & ~3u);
+    int64_t s = 0;
+    for (uint32_t i = 0; i < paired; i += 2)
+      s += (int32_t)((uint32_t)((int32_t)a[i] * pSrc[i]) + (uint32_t)((int32_t)a[i + 1] * pSrc[i + 1]));
+    for (uint32_t i = paired; i < nm; ++i) s += (int64_t)a[i] * pSrc[i];
+    pDst[r] = o_ssat16((int32_t)(s >> 15));
+  }
+  return ARM_MATH_SUCCESS;
+}

@@ -94,6 +94,25 @@ class Host:
             f(C.byref(S), src.ctypes.data, out[r].ctypes.data, tmp.ctypes.data)
         return out
 
+    def mfcc_q15(self, cfg, frames):
+        """arm_mfcc_q15 per frame (q15 tables and frames, q31 pTmp of 2*fftLen words)."""
+        n = int(cfg["fftLen"])
+        keep = [np.ascontiguousarray(cfg["dct"], dtype=np.int16), np.ascontiguousarray(cfg["pos"], dtype=np.uint32),
+                np.ascontiguousarray(cfg["len"], dtype=np.uint32), np.ascontiguousarray(cfg["coefs"], dtype=np.int16),
+                np.ascontiguousarray(cfg["window"], dtype=np.int16)]
+        nb_mel, nb_dct = keep[1].size, keep[0].shape[0]
+        S = _abi.arm_mfcc_instance_q15()
+        st = self.fn("arm_mfcc_init_q15")(C.byref(S), n, nb_mel, nb_dct, *[k.ctypes.data for k in keep])
+        assert st == 0, st
+        frames = np.atleast_2d(np.asarray(frames, dtype=np.int16))
+        out = np.zeros((frames.shape[0], nb_dct), dtype=np.int16)
+        f = self.fn("arm_mfcc_q15")
+        for r in range(frames.shape[0]):
+            src = frames[r].copy()
+            tmp = np.zeros(2 * n, dtype=np.int32)
+            f(C.byref(S), src.ctypes.data, out[r].ctypes.data, tmp.ctypes.data)
+        return out
+
     def mfcc_q31(self, cfg, frames):
         """cfg: dict with fftLen, dct [nbDct x nbMel] q31, pos, len, coefs q31, window q31;
         frames: [batch, fftLen] int32 -> [batch, nbDct] int32 (one arm_mfcc_q31 call per
