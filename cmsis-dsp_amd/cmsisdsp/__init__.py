@@ -55,6 +55,8 @@ arm_fir_instance_q31 = _make("arm_fir_instance_q31", _abi.arm_fir_instance_q31)
 arm_fir_instance_q15 = _make("arm_fir_instance_q15", _abi.arm_fir_instance_q15)
 arm_fir_instance_q7 = _make("arm_fir_instance_q7", _abi.arm_fir_instance_q7)
 arm_mfcc_instance_f32 = _make("arm_mfcc_instance_f32", _abi.arm_mfcc_instance_f32)
+arm_mfcc_instance_q31 = _make("arm_mfcc_instance_q31", _abi.arm_mfcc_instance_q31)
+arm_mfcc_instance_q15 = _make("arm_mfcc_instance_q15", _abi.arm_mfcc_instance_q15)
 for _t in ("f32", "q31", "q15"):
     globals()[f"arm_fir_decimate_instance_{_t}"] = _make(f"arm_fir_decimate_instance_{_t}",
                                                          _abi.arm_fir_decimate_instance)
@@ -416,6 +418,35 @@ def arm_mfcc_f32(inst, pSrc, pTmp, tmp2=None):
     _lib.arm_mfcc_f32(_C.byref(inst._s), src.ctypes.data, out.ctypes.data, tmp.ctypes.data)
     _check("arm_mfcc_f32")
     return out
+
+
+def _mfcc_fixed_init(t, dt):
+    def init(inst, fftLen, nbMelFilters, nbDctOutputs, dctCoefs, filterPos, filterLengths, filterCoefs, windowCoefs):
+        keep = [_arr(dctCoefs, dt).reshape(-1), _arr(filterPos, _np.uint32), _arr(filterLengths, _np.uint32),
+                _arr(filterCoefs, dt), _arr(windowCoefs, dt)]
+        inst._keep = keep
+        return getattr(_lib, f"arm_mfcc_init_{t}")(_C.byref(inst._s), int(fftLen), int(nbMelFilters),
+                                                   int(nbDctOutputs), *[k.ctypes.data for k in keep])
+    init.__name__ = f"arm_mfcc_init_{t}"
+    return init
+
+
+def _mfcc_fixed(t, dt):
+    # cmsisdsp_transform.c:2821-2870 (q15), the q31 analogue: returns (status, pDst)
+    def mfcc(inst, pSrc, pTmp, tmp2=None):
+        src = _arr(pSrc, dt).copy()
+        out = _np.zeros(inst._s.nbDctOutputs, dtype=dt)
+        tmp = _np.zeros(2 * inst._s.fftLen, dtype=_np.int32)
+        st = getattr(_lib, f"arm_mfcc_{t}")(_C.byref(inst._s), src.ctypes.data, out.ctypes.data, tmp.ctypes.data)
+        return st, out
+    mfcc.__name__ = f"arm_mfcc_{t}"
+    return mfcc
+
+
+arm_mfcc_init_q31 = _mfcc_fixed_init("q31", _np.int32)
+arm_mfcc_init_q15 = _mfcc_fixed_init("q15", _np.int16)
+arm_mfcc_q31 = _mfcc_fixed("q31", _np.int32)
+arm_mfcc_q15 = _mfcc_fixed("q15", _np.int16)
 
 
 def arm_mfcc_tmp_buffer_size(dt, fftLen, buf_id, arch=None, use_cfft=0):

@@ -333,6 +333,8 @@ struct MfccFxDev {
   const uint32_t* pos = nullptr;
   const uint32_t* len = nullptr;
   const uint32_t* off = nullptr;
+  const uint32_t* bf = nullptr;    // flat Mel coefficient g -> bin << 16 | filter
+  int total = 0;
   const int32_t* lut = nullptr;
 };
 
@@ -356,10 +358,11 @@ bool mfcc_fx_prepare(const Inst* S, MfccFxDev<T>& d) {
     off[i] = (uint32_t)total;
     total += len[i];
   }
+  if (nm > 0xFFFFu || total > 0x7FFFFFFFull) { set_error(hipErrorInvalidValue, "mfcc: too many Mel coefficients"); return false; }
   auto up16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   const size_t b_dct = up16(sizeof(T) * nm * nd), b_cf = up16(sizeof(T) * total), b_win = up16(sizeof(T) * n);
-  const size_t b_u = up16(sizeof(uint32_t) * nm);
-  std::vector<uint8_t> blob(b_dct + b_cf + b_win + 3 * b_u + 16, 0);
+  const size_t b_u = up16(sizeof(uint32_t) * nm), b_bf = up16(sizeof(uint32_t) * total);
+  std::vector<uint8_t> blob(b_dct + b_cf + b_win + 3 * b_u + b_bf + 16, 0);
   std::vector<T> tmp;
   if (!host_copy(S->dctCoefs, (size_t)nm * nd, tmp)) { set_error(hipErrorInvalidValue, "mfcc dct"); return false; }
   memcpy(blob.data(), tmp.data(), sizeof(T) * tmp.size());
@@ -371,6 +374,9 @@ bool mfcc_fx_prepare(const Inst* S, MfccFxDev<T>& d) {
   memcpy(u, pos.data(), sizeof(uint32_t) * nm);
   memcpy(u + b_u, len.data(), sizeof(uint32_t) * nm);
   memcpy(u + 2 * b_u, off.data(), sizeof(uint32_t) * nm);
+  uint32_t* bfh = reinterpret_cast<uint32_t*>(u + 3 * b_u);
+  for (uint32_t i = 0, g = 0; i < nm; ++i)
+    for (uint32_t j = 0; j < len[i]; ++j) bfh[g++] = ((pos[i] + j) << 16) | i;
   const uint8_t* dev = (const uint8_t*)device_blob(blob.data(), blob.size());
   d.lut = (const int32_t*)device_table(sqrt_initial_lut_q31, sizeof(int32_t) * 32);
   if (!dev || !d.lut) return false;
@@ -380,6 +386,8 @@ bool mfcc_fx_prepare(const Inst* S, MfccFxDev<T>& d) {
   d.pos = (const uint32_t*)(dev + b_dct + b_cf + b_win);
   d.len = (const uint32_t*)(dev + b_dct + b_cf + b_win + b_u);
   d.off = (const uint32_t*)(dev + b_dct + b_cf + b_win + 2 * b_u);
+  d.bf = (const uint32_t*)(dev + b_dct + b_cf + b_win + 3 * b_u);
+  d.total = (int)total;
   return true;
 }
 
@@ -395,10 +403,12 @@ bool mfcc_fx_run(const Inst* S, const MfccFxDev<T>& d, T* x, T* y, T* dst, uint3
   }
   if (!rfft_fixed_run<T>(&S->rfft, x, y, batch, st)) return false;
   if constexpr (sizeof(T) == 4) {
-    MI_CHECK(mfcc_q31_post_launch(n, y, dst, nd, nm, d.pos, d.len, d.off, d.coefs, nd, d.dct, d.lut, dst, batch, st),
+    MI_CHECK(mfcc_q31_post_launch(n, y, dst, nd, nm, d.pos, d.len, d.off, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst,
+                                  batch, st),
              "mfcc q31 post");
   } else {
-    MI_CHECK(mfcc_q15_post_launch(n, y, dst, nd, nm, d.pos, d.len, d.off, d.coefs, nd, d.dct, d.lut, dst, batch, st),
+    MI_CHECK(mfcc_q15_post_launch(n, y, dst, nd, nm, d.pos, d.len, d.off, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst,
+                                  batch, st),
              "mfcc q15 post");
   }
   return true;

@@ -93,12 +93,14 @@ __global__ __launch_bounds__(256) void mfcc_q31_pre_kernel(const int32_t* src, c
 }
 
 // arm_sqrt_q31.c:55-125 (Newton on 1/sqrt from sqrt_initial_lut_q31, 3 iterations)
-__device__ __forceinline__ int32_t mq_sqrt(int32_t in, const int32_t* lut) {
-  if (in <= 0) return 0;
+// lutv: lane l holds sqrt_initial_lut_q31[l & 31]; the entry is fetched with a lane shuffle
+// (every lane of the wave must be active: callers run uniform loops)
+__device__ __forceinline__ int32_t mq_sqrt(int32_t in, int32_t lutv) {
   const int sb = (int)mq_clz((uint32_t)in) - 1;
   const int e = sb & ~1;                             // signBits1 rounded down to even
   const int32_t number = in << e;
-  int32_t v = lut[(number >> 26) - (0x20000000 >> 26)];
+  int32_t v = __shfl(lutv, ((number >> 26) - (0x20000000 >> 26)) & 31, 64);
+  if (in <= 0) return 0;
 #pragma unroll
   for (int it = 0; it < 3; ++it) {
     int32_t t = (int32_t)(((int64_t)v * v) >> 28);
@@ -127,42 +129,79 @@ __device__ __forceinline__ int32_t mq_log(uint32_t src) {
   return (int32_t)(((int64_t)tmp * (int64_t)0x58b90bfb) >> 31);
 }
 
+
+// LDS per wave (int32 words): |X_k| (fftLen/2 + 1), Mel values (nb_mel), then int64 Mel sums.
+__host__ __device__ inline int mq_wave_words(int n, int nb_mel) { return ((n / 2 + 1 + nb_mel + 1) & ~1) + 2 * nb_mel; }
+
+// The Mel sums spread over the wave: the filters' coefficients as one flat list (bf[g] =
+// bin << 16 | filter), lane t summing the contiguous slice t of it and adding each filter's
+// partial sum to its int64 LDS total (ds_add_u64).  The sums are exact int64 of exact (or
+// per-term floor-shifted) products, so any order gives the reference's value.
+template <typename C, typename Term>
+__device__ __forceinline__ void mq_mel_sums(int lane, const int32_t* mag, const uint32_t* __restrict__ bf,
+                                            const C* __restrict__ coefs, int total, int64_t* acc, Term term) {
+  const int per = (total + 63) >> 6;
+  const int g0 = lane * per, g1 = min(total, g0 + per);
+  int cur = -1;
+  int64_t r = 0;
+  for (int g = g0; g < g1; ++g) {
+    const uint32_t e = bf[g];
+    const int f = (int)(e & 0xFFFFu);
+    if (f != cur) {
+      if (cur >= 0) atomicAdd(reinterpret_cast<unsigned long long*>(acc + cur), (unsigned long long)r);
+      cur = f;
+      r = 0;
+    }
+    r += term(mag[e >> 16], (int32_t)coefs[g]);
+  }
+  if (cur >= 0) atomicAdd(reinterpret_cast<unsigned long long*>(acc + cur), (unsigned long long)r);
+}
+
 // maxv may alias dst (frame maxima carried in dst[frame][0]): read before any output store
 __global__ __launch_bounds__(256) void mfcc_q31_post_kernel(const int32_t* __restrict__ y, const int32_t* maxv,
                                                             int maxv_stride, int n, int nb_mel,
                                                             const uint32_t* __restrict__ pos,
                                                             const uint32_t* __restrict__ len,
                                                             const uint32_t* __restrict__ off,
-                                                            const int32_t* __restrict__ coefs, int nb_dct,
+                                                            const int32_t* __restrict__ coefs,
+                                                            const uint32_t* __restrict__ bf, int total, int nb_dct,
                                                             const int32_t* __restrict__ dct,
                                                             const int32_t* __restrict__ lut, int32_t* dst,
                                                             uint32_t batch) {
   extern __shared__ int32_t shq[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lim = (n >> 1) + 1;
-  int32_t* mag = shq + wave * (lim + nb_mel);
+  int32_t* mag = shq + wave * mq_wave_words(n, nb_mel);
   int32_t* mel = mag + lim;
+  int64_t* acc = reinterpret_cast<int64_t*>(mag + ((lim + nb_mel + 1) & ~1));
+  for (int i = lane; i < nb_mel; i += 64) acc[i] = 0;
   const uint32_t frame = blockIdx.x * kMqWaves + wave;
   const bool live = frame < batch;
   const int32_t m = live ? maxv[(size_t)frame * maxv_stride] : 0;
   const bool scale = m != 0 && m != 0x7FFFFFFF;
   if (live) {
     const int2* Y = reinterpret_cast<const int2*>(y + (size_t)frame * 2 * n);
-    for (int k = lane; k < lim; k += 64) {
-      const int2 c = Y[k];
+    const int32_t lutv = lut[lane & 31];
+#pragma unroll 4
+    for (int k0 = 0; k0 < lim; k0 += 64) {             // uniform: the shuffle needs all lanes
+      const int k = k0 + lane;
+      const int2 c = Y[min(k, lim - 1)];
       const int32_t a0 = (int32_t)(((int64_t)c.x * c.x) >> 33), a1 = (int32_t)(((int64_t)c.y * c.y) >> 33);
-      mag[k] = mq_sqrt(a0 + a1, lut);
+      const int32_t v = mq_sqrt(a0 + a1, lutv);
+      if (k < lim) mag[k] = v;
     }
   }
   __syncthreads();
   // log exponent (fftShift + 2 + SHIFT_MELFILTER_SATURATION_Q31) * LOG2TOLOG_Q31
   const int32_t le = (int32_t)((uint32_t)(31 - (int)mq_clz((uint32_t)n) + 12) * 0x02C5C860u);
   if (live) {
+    mq_mel_sums(lane, mag, bf, coefs, total, acc,
+                [](int32_t a, int32_t c) { return ((int64_t)a * c) >> 14; });   // arm_dot_prod_q31
+  }
+  __syncthreads();
+  if (live) {
     for (int i = lane; i < nb_mel; i += 64) {
-      const uint32_t p = pos[i], l = len[i];
-      const int32_t* c = coefs + off[i];
-      int64_t r = 0;
-      for (uint32_t j = 0; j < l; ++j) r += ((int64_t)mag[p + j] * c[j]) >> 14;
+      int64_t r = acc[i];
       r += 0x08637BD0;                                 // MICRO_Q31
       r >>= 28;                                        // SHIFT_MELFILTER_SATURATION_Q31 + 18
       int32_t v = mq_ssat31((int32_t)r);               // __SSAT takes the low 32 bits
@@ -244,35 +283,44 @@ __global__ __launch_bounds__(256) void mfcc_q15_post_kernel(const int16_t* __res
                                                             const uint32_t* __restrict__ pos,
                                                             const uint32_t* __restrict__ len,
                                                             const uint32_t* __restrict__ off,
-                                                            const int16_t* __restrict__ coefs, int nb_dct,
+                                                            const int16_t* __restrict__ coefs,
+                                                            const uint32_t* __restrict__ bf, int total, int nb_dct,
                                                             const int16_t* __restrict__ dct,
                                                             const int32_t* __restrict__ lut, int16_t* dst,
                                                             uint32_t batch) {
   extern __shared__ int32_t shq[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lim = (n >> 1) + 1;
-  int32_t* mag = shq + wave * (lim + nb_mel);
+  int32_t* mag = shq + wave * mq_wave_words(n, nb_mel);
   int32_t* mel = mag + lim;
+  int64_t* acc = reinterpret_cast<int64_t*>(mag + ((lim + nb_mel + 1) & ~1));
+  for (int i = lane; i < nb_mel; i += 64) acc[i] = 0;
   const uint32_t frame = blockIdx.x * kMqWaves + wave;
   const bool live = frame < batch;
   const int32_t m = live ? maxv[(size_t)frame * maxv_stride] : 0;
   const bool scale = m != 0 && m != 0x7FFF;
   if (live) {
     const short2* Y = reinterpret_cast<const short2*>(y + (size_t)frame * 2 * n);
-    for (int k = lane; k < lim; k += 64) {
-      const short2 c = Y[k];
+    const int32_t lutv = lut[lane & 31];
+#pragma unroll 4
+    for (int k0 = 0; k0 < lim; k0 += 64) {             // uniform: the shuffle needs all lanes
+      const int k = k0 + lane;
+      const short2 c = Y[min(k, lim - 1)];
       const uint32_t s2 = ((uint32_t)((int32_t)c.x * c.x) + (uint32_t)((int32_t)c.y * c.y)) >> 1;
-      mag[k] = mq_sqrt((int32_t)s2, lut) >> 16;
+      const int32_t v = mq_sqrt((int32_t)s2, lutv) >> 16;
+      if (k < lim) mag[k] = v;
     }
   }
   __syncthreads();
   const int32_t le = (int32_t)((uint32_t)(31 - (int)mq_clz((uint32_t)n) + 12) * 0x02C5C860u);
   if (live) {
+    mq_mel_sums(lane, mag, bf, coefs, total, acc,
+                [](int32_t a, int32_t c) { return (int64_t)(a * c); });          // arm_dot_prod_q15
+  }
+  __syncthreads();
+  if (live) {
     for (int i = lane; i < nb_mel; i += 64) {
-      const uint32_t p = pos[i], l = len[i];
-      const int16_t* c = coefs + off[i];
-      int64_t r = 0;
-      for (uint32_t j = 0; j < l; ++j) r += (int64_t)(mag[p + j] * (int32_t)c[j]);
+      int64_t r = acc[i];
       r += 0x219;                                      // MICRO_Q15
       r >>= 10;                                        // SHIFT_MELFILTER_SATURATION_Q15
       int32_t v = mq_ssat31((int32_t)r);
@@ -310,12 +358,12 @@ hipError_t mfcc_q15_pre_launch(int n, const int16_t* src, const int16_t* win, in
 
 hipError_t mfcc_q15_post_launch(int n, const int16_t* y, const int16_t* maxv, int maxv_stride, int nb_mel,
                                 const uint32_t* pos, const uint32_t* len, const uint32_t* off, const int16_t* coefs,
-                                int nb_dct, const int16_t* dct, const int32_t* lut, int16_t* dst, uint32_t batch,
+                                const uint32_t* bf, int total, int nb_dct, const int16_t* dct, const int32_t* lut, int16_t* dst, uint32_t batch,
                                 hipStream_t st) {
   if (batch == 0) return hipSuccess;
   const uint32_t grid = (batch + kMqWaves - 1) / kMqWaves;
   hipLaunchKernelGGL(mfcc_q15_post_kernel, dim3(grid), dim3(64 * kMqWaves), mfcc_q31_post_lds(n, nb_mel), st, y,
-                     maxv, maxv_stride, n, nb_mel, pos, len, off, coefs, nb_dct, dct, lut, dst, batch);
+                     maxv, maxv_stride, n, nb_mel, pos, len, off, coefs, bf, total, nb_dct, dct, lut, dst, batch);
   return hipGetLastError();
 }
 
@@ -329,16 +377,16 @@ hipError_t mfcc_q31_pre_launch(int n, const int32_t* src, const int32_t* win, in
   return hipGetLastError();
 }
 
-size_t mfcc_q31_post_lds(int n, int nb_mel) { return sizeof(int32_t) * kMqWaves * (size_t)(n / 2 + 1 + nb_mel); }
+size_t mfcc_q31_post_lds(int n, int nb_mel) { return sizeof(int32_t) * kMqWaves * (size_t)mq_wave_words(n, nb_mel); }
 
 hipError_t mfcc_q31_post_launch(int n, const int32_t* y, const int32_t* maxv, int maxv_stride, int nb_mel,
                                 const uint32_t* pos, const uint32_t* len, const uint32_t* off, const int32_t* coefs,
-                                int nb_dct, const int32_t* dct, const int32_t* lut, int32_t* dst, uint32_t batch,
+                                const uint32_t* bf, int total, int nb_dct, const int32_t* dct, const int32_t* lut, int32_t* dst, uint32_t batch,
                                 hipStream_t st) {
   if (batch == 0) return hipSuccess;
   const uint32_t grid = (batch + kMqWaves - 1) / kMqWaves;
   hipLaunchKernelGGL(mfcc_q31_post_kernel, dim3(grid), dim3(64 * kMqWaves), mfcc_q31_post_lds(n, nb_mel), st, y,
-                     maxv, maxv_stride, n, nb_mel, pos, len, off, coefs, nb_dct, dct, lut, dst, batch);
+                     maxv, maxv_stride, n, nb_mel, pos, len, off, coefs, bf, total, nb_dct, dct, lut, dst, batch);
   return hipGetLastError();
 }
 

@@ -72,14 +72,24 @@ __global__ __launch_bounds__(256) void rfft_fx_split_kernel(const T* __restrict_
   const int k = mp.k;
   const uint32_t c = 2u * mod * (uint32_t)k;
   const int32_t a1 = ta[c], a2 = ta[c + 1], b1 = tb[c], b2 = tb[c + 1];
-#pragma unroll 2
+  // all rows' loads first (rows past the batch re-read the last row and store nothing), so
+  // each thread has 16 loads in flight instead of one row's latency at a time
+  int2 av[kRfftRows], bv[kRfftRows];
+#pragma unroll
+  for (int r = 0; r < kRfftRows; ++r) {
+    const uint64_t row = min(mp.row0 + (uint64_t)r * mp.rstep, rows - 1);
+    const T* x = src + row * (uint64_t)n;
+    av[r] = Cx<T>::ld(x + 2 * k);
+    bv[r] = Cx<T>::ld(x + (k == 0 ? 0 : 2 * (L - k)));   // bin L would lie past the row (k = 0 uses a only)
+  }
+#pragma unroll
   for (int r = 0; r < kRfftRows; ++r) {
     const uint64_t row = mp.row0 + (uint64_t)r * mp.rstep;
     if (row >= rows) break;
-    const T* x = src + row * (uint64_t)n;
     T* y = dst + row * (uint64_t)(2 * n);
+    const int2 a = av[r], b = bv[r];
     if (k == 0) {
-      const int2 v = Cx<T>::ld(x);
+      const int2 v = a;     // bin 0: x[0], x[1]
       if constexpr (sizeof(T) == 4) {
         Cx<T>::st(y + n, wsub(v.x, v.y) >> 1, 0);
         Cx<T>::st(y, wadd(v.x, v.y) >> 1, 0);
@@ -89,7 +99,6 @@ __global__ __launch_bounds__(256) void rfft_fx_split_kernel(const T* __restrict_
       }
       continue;
     }
-    const int2 a = Cx<T>::ld(x + 2 * k), b = Cx<T>::ld(x + 2 * (L - k));
     if constexpr (sizeof(T) == 4) {
       // arm_rfft_q31.c:293-326
       int32_t re = mult_R(a.x, a1), im = mult_R(a.x, a2);
@@ -117,13 +126,20 @@ __global__ __launch_bounds__(256) void rfft_fx_merge_kernel(const T* __restrict_
   const int k = mp.k;
   const uint32_t c = 2u * mod * (uint32_t)k;
   const int32_t a1 = ta[c], a2 = ta[c + 1], b1 = tb[c], b2 = tb[c + 1];
-#pragma unroll 2
+  int2 av[kRfftRows], bv[kRfftRows];
+#pragma unroll
+  for (int r = 0; r < kRfftRows; ++r) {
+    const uint64_t row = min(mp.row0 + (uint64_t)r * mp.rstep, rows - 1);
+    const T* x = src + row * (uint64_t)(2 * n);
+    av[r] = Cx<T>::ld(x + 2 * k);
+    bv[r] = Cx<T>::ld(x + 2 * (L - k));
+  }
+#pragma unroll
   for (int r = 0; r < kRfftRows; ++r) {
     const uint64_t row = mp.row0 + (uint64_t)r * mp.rstep;
     if (row >= rows) break;
-    const T* x = src + row * (uint64_t)(2 * n);
     T* y = dst + row * (uint64_t)n;
-    const int2 a = Cx<T>::ld(x + 2 * k), b = Cx<T>::ld(x + 2 * (L - k));
+    const int2 a = av[r], b = bv[r];
     if constexpr (sizeof(T) == 4) {
       // arm_rfft_q31.c:430-466
       int32_t re = mult_R(a.x, a1), im = mult_R(a.x, wneg(a2));

@@ -133,6 +133,24 @@ def test_mfcc_f32(cdsp, torch_gpu, ref):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("t", ["q31", "q15"])
+def test_mfcc_fixed(cdsp, torch_gpu, ref, t):
+    """testmfcc.py test_mfcc_q31 / _q15 call shape: (status, pDst) = arm_mfcc_<t>(inst, x, tmp);
+    bit-exact against the reference build on the suite's tables and inputs."""
+    import importlib
+    tm = importlib.import_module(f"test_mfcc_{t}")
+    g = tm.golden()
+    cfg = tm.suite_cfg(g, 512)
+    inst = getattr(cdsp, f"arm_mfcc_instance_{t}")()
+    st = getattr(cdsp, f"arm_mfcc_init_{t}")(inst, 512, 20, 13, cfg["dct"], cfg["pos"], cfg["len"], cfg["coefs"],
+                                             cfg["window"])
+    assert st == 0 and inst.fftLen() == 512 and inst.nbMelFilters() == 20 and inst.nbDctOutputs() == 13
+    x = g["input_Noise_512"]
+    err, res = getattr(cdsp, f"arm_mfcc_{t}")(inst, x, np.zeros(cdsp.arm_mfcc_tmp_buffer_size(0, 512, 1), np.int32))
+    assert err == 0 and res.tobytes() == getattr(ref, f"mfcc_{t}")(cfg, x)[0].tobytes()
+
+
+@pytest.mark.gpu
 def test_conv(cdsp, torch_gpu, ref):
     """testdsp.py-style conv: f32 against np.convolve (1e-6), fixed point bit-exact
     against the reference build."""

@@ -3,7 +3,7 @@
 # cmsisdsp wrapper replays), then one bench line per workload.  Output: gpurun_out/mfx/*.
 set -o pipefail
 mkdir -p gpurun_out/mfx
-timeout -k 10 300 python -u -m pytest tests/test_mfcc_q15.py tests/test_mfcc_q31.py tests/test_rfft_fixed.py \
+timeout -k 10 300 python -u -m pytest tests/test_mfcc_q15.py tests/test_mfcc_q31.py tests/test_rfft_fixed.py tests/test_pythonwrapper_compat.py \
   -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/mfx/tests.log 2>&1
 rc=$?; tail -3 gpurun_out/mfx/tests.log
 if [ $rc -ne 0 ]; then exit $rc; fi
