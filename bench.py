@@ -51,10 +51,10 @@ WORKLOADS = {
     "fir_fast_q31": ("fir_fast_q31", 128, 1 << 16, 8),
     "mat_mult_f32": ("mat", 1024, 256, None),
     "mfcc_f32": ("mfcc", 1024, 1 << 18, 4),
-    # three launches (pre in place, RFFT q31 -> 2N-word spectra, post): bytes moved per sample
-    # 4 + 4 (pre) + 4 + 4 + 8 (RFFT: inner CFFT in place, 2N words out) + 4 (post reads N+2 words)
-    "mfcc_q31": ("mfccq31", 1024, 1 << 18, 28),
-    "mfcc_q15": ("mfccq15", 1024, 1 << 18, 14),
+    # three launches (pre in place, inner CFFT in place, post with the RFFT split fused):
+    # bytes moved per sample 4 + 4 (pre) + 4 + 4 (CFFT) + 4 (post reads the N-word CFFT row)
+    "mfcc_q31": ("mfccq31", 1024, 1 << 18, 20),
+    "mfcc_q15": ("mfccq15", 1024, 1 << 18, 10),
     "rfft_f32": ("rfft", 1024, 1 << 20, 8),
     # real length 8192 (inner CFFT 4096 = the fixed-point specialist); bytes per sample:
     # N words in, N words written back (the inner CFFT overwrites pSrc), 2N words out

@@ -335,6 +335,7 @@ struct MfccFxDev {
   const uint32_t* off = nullptr;
   const uint32_t* bf = nullptr;    // flat Mel coefficient g -> bin << 16 | filter
   int total = 0;
+  const int4* tw = nullptr;        // split twiddles per bin k <= fftLen/2: {A[2mk], A[2mk+1], B[2mk], B[2mk+1]}
   const int32_t* lut = nullptr;
 };
 
@@ -362,7 +363,8 @@ bool mfcc_fx_prepare(const Inst* S, MfccFxDev<T>& d) {
   auto up16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   const size_t b_dct = up16(sizeof(T) * nm * nd), b_cf = up16(sizeof(T) * total), b_win = up16(sizeof(T) * n);
   const size_t b_u = up16(sizeof(uint32_t) * nm), b_bf = up16(sizeof(uint32_t) * total);
-  std::vector<uint8_t> blob(b_dct + b_cf + b_win + 3 * b_u + b_bf + 16, 0);
+  const size_t b_tw = up16(sizeof(int4) * (n / 2 + 1));
+  std::vector<uint8_t> blob(b_dct + b_cf + b_win + 3 * b_u + b_bf + b_tw + 16, 0);
   std::vector<T> tmp;
   if (!host_copy(S->dctCoefs, (size_t)nm * nd, tmp)) { set_error(hipErrorInvalidValue, "mfcc dct"); return false; }
   memcpy(blob.data(), tmp.data(), sizeof(T) * tmp.size());
@@ -377,6 +379,19 @@ bool mfcc_fx_prepare(const Inst* S, MfccFxDev<T>& d) {
   uint32_t* bfh = reinterpret_cast<uint32_t*>(u + 3 * b_u);
   for (uint32_t i = 0, g = 0; i < nm; ++i)
     for (uint32_t j = 0; j < len[i]; ++j) bfh[g++] = ((pos[i] + j) << 16) | i;
+  {   // the split's twiddle records (arm_rfft_q31.c:293-326 index 2 * modifier * k)
+    const uint32_t mod = S->rfft.twidCoefRModifier, words = mod * n;
+    std::vector<T> ta, tb;
+    if (!host_copy(S->rfft.pTwiddleAReal, words, ta) || !host_copy(S->rfft.pTwiddleBReal, words, tb)) {
+      set_error(hipErrorInvalidValue, "mfcc rfft tables");
+      return false;
+    }
+    int4* twh = reinterpret_cast<int4*>(u + 3 * b_u + b_bf);
+    for (uint32_t k = 1; k < n / 2; ++k) {
+      const uint32_t c = 2 * mod * k;
+      twh[k] = make_int4(ta[c], ta[c + 1], tb[c], tb[c + 1]);
+    }
+  }
   const uint8_t* dev = (const uint8_t*)device_blob(blob.data(), blob.size());
   d.lut = (const int32_t*)device_table(sqrt_initial_lut_q31, sizeof(int32_t) * 32);
   if (!dev || !d.lut) return false;
@@ -388,6 +403,7 @@ bool mfcc_fx_prepare(const Inst* S, MfccFxDev<T>& d) {
   d.off = (const uint32_t*)(dev + b_dct + b_cf + b_win + 2 * b_u);
   d.bf = (const uint32_t*)(dev + b_dct + b_cf + b_win + 3 * b_u);
   d.total = (int)total;
+  d.tw = (const int4*)(dev + b_dct + b_cf + b_win + 3 * b_u + b_bf);
   return true;
 }
 
@@ -401,13 +417,23 @@ bool mfcc_fx_run(const Inst* S, const MfccFxDev<T>& d, T* x, T* y, T* dst, uint3
   } else {
     MI_CHECK(mfcc_q15_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc q15 pre");
   }
-  if (!rfft_fixed_run<T>(&S->rfft, x, y, batch, st)) return false;
+  // the inner CFFT of the forward RFFT in place on x; the split is fused into post
+  // (arm_rfft_q31.c:148-183: cfft(L, fwd, bitrev) then arm_split_rfft)
+  const auto* in = S->rfft.pCfft;
+  const uint32_t L = (uint32_t)n / 2;
+  if (!in || in->fftLen != L || !cfft_len_ok(L)) { set_error(hipErrorInvalidValue, "mfcc rfft instance"); return false; }
+  CfftPrep pr;
+  if (!cfft_prepare(L, in->pTwiddle, in->pBitRevTable, in->bitRevLength, sizeof(T) == 4 ? 1 : 2, 0,
+                    S->rfft.bitReverseFlagR, pr))
+    return false;
+  MI_CHECK(cfft_launch(sizeof(T) == 4 ? 1 : 2, L, x, batch, pr, st), "mfcc cfft");
+  (void)y;
   if constexpr (sizeof(T) == 4) {
-    MI_CHECK(mfcc_q31_post_launch(n, y, dst, nd, nm, d.pos, d.len, d.off, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst,
+    MI_CHECK(mfcc_q31_post_launch(n, x, d.tw, dst, nd, nm, d.pos, d.len, d.off, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst,
                                   batch, st),
              "mfcc q31 post");
   } else {
-    MI_CHECK(mfcc_q15_post_launch(n, y, dst, nd, nm, d.pos, d.len, d.off, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst,
+    MI_CHECK(mfcc_q15_post_launch(n, x, d.tw, dst, nd, nm, d.pos, d.len, d.off, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst,
                                   batch, st),
              "mfcc q15 post");
   }

@@ -106,12 +106,12 @@ hipError_t mfcc_q31_pre_launch(int n, const int32_t* src, const int32_t* win, in
 size_t mfcc_q31_post_lds(int n, int nb_mel);
 hipError_t mfcc_q15_pre_launch(int n, const int16_t* src, const int16_t* win, int16_t* x, int16_t* maxv,
                                uint32_t batch, int maxv_stride, hipStream_t st);
-hipError_t mfcc_q15_post_launch(int n, const int16_t* y, const int16_t* maxv, int maxv_stride, int nb_mel,
+hipError_t mfcc_q15_post_launch(int n, const int16_t* y, const int4* tw, const int16_t* maxv, int maxv_stride, int nb_mel,
                                 const uint32_t* pos, const uint32_t* len, const uint32_t* off, const int16_t* coefs,
                                 const uint32_t* bf, int total, int nb_dct, const int16_t* dct, const int32_t* lut, int16_t* dst, uint32_t batch,
                                 hipStream_t st);
 
-hipError_t mfcc_q31_post_launch(int n, const int32_t* y, const int32_t* maxv, int maxv_stride, int nb_mel,
+hipError_t mfcc_q31_post_launch(int n, const int32_t* y, const int4* tw, const int32_t* maxv, int maxv_stride, int nb_mel,
                                 const uint32_t* pos, const uint32_t* len, const uint32_t* off, const int32_t* coefs,
                                 const uint32_t* bf, int total, int nb_dct, const int32_t* dct, const int32_t* lut, int32_t* dst, uint32_t batch,
                                 hipStream_t st);

@@ -157,8 +157,39 @@ __device__ __forceinline__ void mq_mel_sums(int lane, const int32_t* mag, const 
   if (cur >= 0) atomicAdd(reinterpret_cast<unsigned long long*>(acc + cur), (unsigned long long)r);
 }
 
+
+// Spectrum bin k (0 <= k <= L = fftLen/2) of the real FFT, formed from the inner CFFT output
+// x (L complex) as arm_split_rfft_q31 / _q15 do (arm_rfft_q31.c:256-341, arm_rfft_q15.c scalar
+// branch), with the k-th twiddle record tw[k] = {A[2mk], A[2mk+1], B[2mk], B[2mk+1]} (m = the
+// instance's twidCoefRModifier; built contiguous on the host, so the loads coalesce): the
+// post kernels take the magnitudes straight from the CFFT output, with no 2N-word spectrum.
+__device__ __forceinline__ int2 mq_split_q31(const int2* x, int k, int L, int4 t) {
+  if (k == 0 || k == L) {
+    const int2 v = x[0];
+    return make_int2((k == 0 ? wadd(v.x, v.y) : wsub(v.x, v.y)) >> 1, 0);
+  }
+  const int2 a = x[k], b = x[L - k];
+  int32_t re = mult_R(a.x, t.x), im = mult_R(a.x, t.y);
+  re = multSub_R(re, a.y, t.y); im = multAcc_R(im, a.y, t.x);
+  re = multSub_R(re, b.y, t.y); im = multSub_R(im, b.y, t.z);
+  re = multAcc_R(re, b.x, t.z); im = multSub_R(im, b.x, t.y);
+  return make_int2(re, im);
+}
+__device__ __forceinline__ int2 mq_split_q15(const short2* x, int k, int L, int4 t) {
+  if (k == 0 || k == L) {
+    const short2 v = x[0];
+    return make_int2((k == 0 ? v.x + v.y : v.x - v.y) >> 1, 0);
+  }
+  const short2 a = x[k], b = x[L - k];
+  auto p = [](int32_t u, int32_t v) { return (uint32_t)(u * v); };
+  const int32_t re = (int32_t)(p(a.x, t.x) - p(a.y, t.y) + p(b.x, t.z) + p(b.y, t.w)) >> 16;
+  const int32_t im = (int32_t)(p(b.x, t.w) - p(b.y, t.z) + p(a.y, t.x) + p(a.x, t.y)) >> 16;
+  return make_int2((int16_t)re, (int16_t)im);     // the split stores q15_t
+}
+
 // maxv may alias dst (frame maxima carried in dst[frame][0]): read before any output store
-__global__ __launch_bounds__(256) void mfcc_q31_post_kernel(const int32_t* __restrict__ y, const int32_t* maxv,
+__global__ __launch_bounds__(256) void mfcc_q31_post_kernel(const int32_t* __restrict__ y, const int4* __restrict__ tw,
+                                                            const int32_t* maxv,
                                                             int maxv_stride, int n, int nb_mel,
                                                             const uint32_t* __restrict__ pos,
                                                             const uint32_t* __restrict__ len,
@@ -180,12 +211,12 @@ __global__ __launch_bounds__(256) void mfcc_q31_post_kernel(const int32_t* __res
   const int32_t m = live ? maxv[(size_t)frame * maxv_stride] : 0;
   const bool scale = m != 0 && m != 0x7FFFFFFF;
   if (live) {
-    const int2* Y = reinterpret_cast<const int2*>(y + (size_t)frame * 2 * n);
+    const int2* X = reinterpret_cast<const int2*>(y + (size_t)frame * n);   // CFFT output, L complex
     const int32_t lutv = lut[lane & 31];
 #pragma unroll 4
     for (int k0 = 0; k0 < lim; k0 += 64) {             // uniform: the shuffle needs all lanes
-      const int k = k0 + lane;
-      const int2 c = Y[min(k, lim - 1)];
+      const int k = k0 + lane, kc = min(k, lim - 1);
+      const int2 c = mq_split_q31(X, kc, lim - 1, tw[kc]);
       const int32_t a0 = (int32_t)(((int64_t)c.x * c.x) >> 33), a1 = (int32_t)(((int64_t)c.y * c.y) >> 33);
       const int32_t v = mq_sqrt(a0 + a1, lutv);
       if (k < lim) mag[k] = v;
@@ -278,7 +309,8 @@ __global__ __launch_bounds__(256) void mfcc_q15_pre_kernel(const int16_t* src, c
   if (lane == 0) maxv[(size_t)frame * maxv_stride] = (int16_t)m;
 }
 
-__global__ __launch_bounds__(256) void mfcc_q15_post_kernel(const int16_t* __restrict__ y, const int16_t* maxv,
+__global__ __launch_bounds__(256) void mfcc_q15_post_kernel(const int16_t* __restrict__ y, const int4* __restrict__ tw,
+                                                            const int16_t* maxv,
                                                             int maxv_stride, int n, int nb_mel,
                                                             const uint32_t* __restrict__ pos,
                                                             const uint32_t* __restrict__ len,
@@ -300,12 +332,12 @@ __global__ __launch_bounds__(256) void mfcc_q15_post_kernel(const int16_t* __res
   const int32_t m = live ? maxv[(size_t)frame * maxv_stride] : 0;
   const bool scale = m != 0 && m != 0x7FFF;
   if (live) {
-    const short2* Y = reinterpret_cast<const short2*>(y + (size_t)frame * 2 * n);
+    const short2* X = reinterpret_cast<const short2*>(y + (size_t)frame * n);
     const int32_t lutv = lut[lane & 31];
 #pragma unroll 4
     for (int k0 = 0; k0 < lim; k0 += 64) {             // uniform: the shuffle needs all lanes
-      const int k = k0 + lane;
-      const short2 c = Y[min(k, lim - 1)];
+      const int k = k0 + lane, kc = min(k, lim - 1);
+      const int2 c = mq_split_q15(X, kc, lim - 1, tw[kc]);
       const uint32_t s2 = ((uint32_t)((int32_t)c.x * c.x) + (uint32_t)((int32_t)c.y * c.y)) >> 1;
       const int32_t v = mq_sqrt((int32_t)s2, lutv) >> 16;
       if (k < lim) mag[k] = v;
@@ -356,14 +388,14 @@ hipError_t mfcc_q15_pre_launch(int n, const int16_t* src, const int16_t* win, in
   return hipGetLastError();
 }
 
-hipError_t mfcc_q15_post_launch(int n, const int16_t* y, const int16_t* maxv, int maxv_stride, int nb_mel,
+hipError_t mfcc_q15_post_launch(int n, const int16_t* y, const int4* tw, const int16_t* maxv, int maxv_stride, int nb_mel,
                                 const uint32_t* pos, const uint32_t* len, const uint32_t* off, const int16_t* coefs,
                                 const uint32_t* bf, int total, int nb_dct, const int16_t* dct, const int32_t* lut, int16_t* dst, uint32_t batch,
                                 hipStream_t st) {
   if (batch == 0) return hipSuccess;
   const uint32_t grid = (batch + kMqWaves - 1) / kMqWaves;
   hipLaunchKernelGGL(mfcc_q15_post_kernel, dim3(grid), dim3(64 * kMqWaves), mfcc_q31_post_lds(n, nb_mel), st, y,
-                     maxv, maxv_stride, n, nb_mel, pos, len, off, coefs, bf, total, nb_dct, dct, lut, dst, batch);
+                     tw, maxv, maxv_stride, n, nb_mel, pos, len, off, coefs, bf, total, nb_dct, dct, lut, dst, batch);
   return hipGetLastError();
 }
 
@@ -379,14 +411,14 @@ hipError_t mfcc_q31_pre_launch(int n, const int32_t* src, const int32_t* win, in
 
 size_t mfcc_q31_post_lds(int n, int nb_mel) { return sizeof(int32_t) * kMqWaves * (size_t)mq_wave_words(n, nb_mel); }
 
-hipError_t mfcc_q31_post_launch(int n, const int32_t* y, const int32_t* maxv, int maxv_stride, int nb_mel,
+hipError_t mfcc_q31_post_launch(int n, const int32_t* y, const int4* tw, const int32_t* maxv, int maxv_stride, int nb_mel,
                                 const uint32_t* pos, const uint32_t* len, const uint32_t* off, const int32_t* coefs,
                                 const uint32_t* bf, int total, int nb_dct, const int32_t* dct, const int32_t* lut, int32_t* dst, uint32_t batch,
                                 hipStream_t st) {
   if (batch == 0) return hipSuccess;
   const uint32_t grid = (batch + kMqWaves - 1) / kMqWaves;
   hipLaunchKernelGGL(mfcc_q31_post_kernel, dim3(grid), dim3(64 * kMqWaves), mfcc_q31_post_lds(n, nb_mel), st, y,
-                     maxv, maxv_stride, n, nb_mel, pos, len, off, coefs, bf, total, nb_dct, dct, lut, dst, batch);
+                     tw, maxv, maxv_stride, n, nb_mel, pos, len, off, coefs, bf, total, nb_dct, dct, lut, dst, batch);
   return hipGetLastError();
 }
 
