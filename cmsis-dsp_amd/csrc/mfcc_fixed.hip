@@ -136,26 +136,7 @@ __host__ __device__ inline int mq_wave_words(int n, int nb_mel) { return ((n / 2
 // The Mel sums spread over the wave: the filters' coefficients as one flat list (bf[g] =
 // bin << 16 | filter), lane t summing the contiguous slice t of it and adding each filter's
 // partial sum to its int64 LDS total (ds_add_u64).  The sums are exact int64 of exact (or
-// per-term floor-shifted) products, so any order gives the reference's value.
-template <typename C, typename Term>
-__device__ __forceinline__ void mq_mel_sums(int lane, const int32_t* mag, const uint32_t* __restrict__ bf,
-                                            const C* __restrict__ coefs, int total, int64_t* acc, Term term) {
-  const int per = (total + 63) >> 6;
-  const int g0 = lane * per, g1 = min(total, g0 + per);
-  int cur = -1;
-  int64_t r = 0;
-  for (int g = g0; g < g1; ++g) {
-    const uint32_t e = bf[g];
-    const int f = (int)(e & 0xFFFFu);
-    if (f != cur) {
-      if (cur >= 0) atomicAdd(reinterpret_cast<unsigned long long*>(acc + cur), (unsigned long long)r);
-      cur = f;
-      r = 0;
-    }
-    r += term(mag[e >> 16], (int32_t)coefs[g]);
-  }
-  if (cur >= 0) atomicAdd(reinterpret_cast<unsigned long long*>(acc + cur), (unsigned long long)r);
-}
+// per-term floor-shifted) products, so any order gives the reference's value (mq_post_body).
 
 
 // Spectrum bin k (0 <= k <= L = fftLen/2) of the real FFT, formed from the inner CFFT output
@@ -187,72 +168,118 @@ __device__ __forceinline__ int2 mq_split_q15(const short2* x, int k, int L, int4
   return make_int2((int16_t)re, (int16_t)im);     // the split stores q15_t
 }
 
-// maxv may alias dst (frame maxima carried in dst[frame][0]): read before any output store
+// maxv may alias dst (frame maxima carried in dst[frame][0]): read before any output store.
+// A workgroup stages the frame-invariant tables (flat Mel list, coefficients, DCT rows) in LDS
+// once when they fit, then each wave runs kMqFpw frames; a wave's LDS region is its own, so the
+// stages are ordered by wave barriers only (waves run independently; PMC of the one-frame,
+// global-table version: 71 % of wave time waiting, VALU issue at 34 %).
+constexpr int kMqFpw = 4;   // frames per wave
+__device__ __forceinline__ void mq_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__host__ __device__ inline int mq_tab_words(int total, int nb_mel, int nb_dct) {
+  return (2 * total + nb_mel * nb_dct + 3) & ~3;
+}
+
+template <typename T, typename Split, typename Mag, typename Term, typename Fin, typename Dct>
+__device__ __forceinline__ void mq_post_body(const T* __restrict__ y, const int4* __restrict__ tw, const T* maxv,
+                                             int maxv_stride, int n, int nb_mel, const T* __restrict__ coefs,
+                                             const uint32_t* __restrict__ bf, int total, int nb_dct,
+                                             const T* __restrict__ dct, const int32_t* __restrict__ lut, T* dst,
+                                             uint32_t batch, int stage, Split split, Mag magf, Term term, Fin fin,
+                                             Dct dctf) {
+  extern __shared__ int32_t shq[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lim = (n >> 1) + 1;
+  int32_t* tab = shq;
+  if (stage) {
+    for (int i = threadIdx.x; i < total; i += blockDim.x) {
+      tab[i] = (int32_t)bf[i];
+      tab[total + i] = (int32_t)coefs[i];
+    }
+    for (int i = threadIdx.x; i < nb_mel * nb_dct; i += blockDim.x) tab[2 * total + i] = (int32_t)dct[i];
+  }
+  __syncthreads();
+  int32_t* mag = shq + (stage ? mq_tab_words(total, nb_mel, nb_dct) : 0) + wave * mq_wave_words(n, nb_mel);
+  int32_t* mel = mag + lim;
+  int64_t* acc = reinterpret_cast<int64_t*>(mag + ((lim + nb_mel + 1) & ~1));
+  const uint32_t* bfp = stage ? reinterpret_cast<const uint32_t*>(tab) : bf;
+  auto coef = [&](int g) { return stage ? tab[total + g] : (int32_t)coefs[g]; };
+  auto dctw = [&](int i) { return stage ? tab[2 * total + i] : (int32_t)dct[i]; };
+  const int32_t lutv = lut[lane & 31];
+  for (int it = 0; it < kMqFpw; ++it) {
+    const uint32_t frame = (blockIdx.x * kMqFpw + it) * kMqWaves + wave;
+    if (frame >= batch) break;                         // wave-uniform: no workgroup barrier below
+    const int32_t m = (int32_t)maxv[(size_t)frame * maxv_stride];
+    for (int i = lane; i < nb_mel; i += 64) acc[i] = 0;
+    const T* X = y + (size_t)frame * n;                // CFFT output, L complex
+#pragma unroll 4
+    for (int k0 = 0; k0 < lim; k0 += 64) {             // uniform: the shuffle needs all lanes
+      const int k = k0 + lane, kc = min(k, lim - 1);
+      const int32_t v = magf(split(X, kc, lim - 1, tw[kc]), lutv);
+      if (k < lim) mag[k] = v;
+    }
+    mq_wave_sync();
+    {   // the Mel sums over the flat list (see mq_mel_sums)
+      const int per = (total + 63) >> 6;
+      const int g0 = lane * per, g1 = min(total, g0 + per);
+      int cur = -1;
+      int64_t r = 0;
+      for (int g = g0; g < g1; ++g) {
+        const uint32_t e = bfp[g];
+        const int f = (int)(e & 0xFFFFu);
+        if (f != cur) {
+          if (cur >= 0) atomicAdd(reinterpret_cast<unsigned long long*>(acc + cur), (unsigned long long)r);
+          cur = f;
+          r = 0;
+        }
+        r += term(mag[e >> 16], coef(g));
+      }
+      if (cur >= 0) atomicAdd(reinterpret_cast<unsigned long long*>(acc + cur), (unsigned long long)r);
+    }
+    mq_wave_sync();
+    for (int i = lane; i < nb_mel; i += 64) mel[i] = fin(acc[i], m);
+    mq_wave_sync();
+    T* o = dst + (size_t)frame * nb_dct;
+    for (int r = lane; r < nb_dct; r += 64) o[r] = dctf(r, mel, dctw);
+    mq_wave_sync();                                    // mel / acc reused by the next frame
+  }
+}
+
 __global__ __launch_bounds__(256) void mfcc_q31_post_kernel(const int32_t* __restrict__ y, const int4* __restrict__ tw,
-                                                            const int32_t* maxv,
-                                                            int maxv_stride, int n, int nb_mel,
-                                                            const uint32_t* __restrict__ pos,
-                                                            const uint32_t* __restrict__ len,
-                                                            const uint32_t* __restrict__ off,
+                                                            const int32_t* maxv, int maxv_stride, int n, int nb_mel,
                                                             const int32_t* __restrict__ coefs,
                                                             const uint32_t* __restrict__ bf, int total, int nb_dct,
                                                             const int32_t* __restrict__ dct,
                                                             const int32_t* __restrict__ lut, int32_t* dst,
-                                                            uint32_t batch) {
-  extern __shared__ int32_t shq[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int lim = (n >> 1) + 1;
-  int32_t* mag = shq + wave * mq_wave_words(n, nb_mel);
-  int32_t* mel = mag + lim;
-  int64_t* acc = reinterpret_cast<int64_t*>(mag + ((lim + nb_mel + 1) & ~1));
-  for (int i = lane; i < nb_mel; i += 64) acc[i] = 0;
-  const uint32_t frame = blockIdx.x * kMqWaves + wave;
-  const bool live = frame < batch;
-  const int32_t m = live ? maxv[(size_t)frame * maxv_stride] : 0;
-  const bool scale = m != 0 && m != 0x7FFFFFFF;
-  if (live) {
-    const int2* X = reinterpret_cast<const int2*>(y + (size_t)frame * n);   // CFFT output, L complex
-    const int32_t lutv = lut[lane & 31];
-#pragma unroll 4
-    for (int k0 = 0; k0 < lim; k0 += 64) {             // uniform: the shuffle needs all lanes
-      const int k = k0 + lane, kc = min(k, lim - 1);
-      const int2 c = mq_split_q31(X, kc, lim - 1, tw[kc]);
-      const int32_t a0 = (int32_t)(((int64_t)c.x * c.x) >> 33), a1 = (int32_t)(((int64_t)c.y * c.y) >> 33);
-      const int32_t v = mq_sqrt(a0 + a1, lutv);
-      if (k < lim) mag[k] = v;
-    }
-  }
-  __syncthreads();
+                                                            uint32_t batch, int stage) {
   // log exponent (fftShift + 2 + SHIFT_MELFILTER_SATURATION_Q31) * LOG2TOLOG_Q31
   const int32_t le = (int32_t)((uint32_t)(31 - (int)mq_clz((uint32_t)n) + 12) * 0x02C5C860u);
-  if (live) {
-    mq_mel_sums(lane, mag, bf, coefs, total, acc,
-                [](int32_t a, int32_t c) { return ((int64_t)a * c) >> 14; });   // arm_dot_prod_q31
-  }
-  __syncthreads();
-  if (live) {
-    for (int i = lane; i < nb_mel; i += 64) {
-      int64_t r = acc[i];
-      r += 0x08637BD0;                                 // MICRO_Q31
-      r >>= 28;                                        // SHIFT_MELFILTER_SATURATION_Q31 + 18
-      int32_t v = mq_ssat31((int32_t)r);               // __SSAT takes the low 32 bits
-      if (scale) v = mq_scale(v, m, 1);                // arm_scale_q31(., m, 0): kShift = 1
-      v = mq_log((uint32_t)v);
-      const int64_t s = (int64_t)v + le;               // arm_offset_q31 (saturating)
-      v = s > INT32_MAX ? INT32_MAX : (s < INT32_MIN ? INT32_MIN : (int32_t)s);
-      mel[i] = v >> 3;                                 // arm_shift_q31(., -3)
-    }
-  }
-  __syncthreads();
-  if (live) {
-    int32_t* o = dst + (size_t)frame * nb_dct;
-    for (int r = lane; r < nb_dct; r += 64) {
-      const int32_t* d = dct + (size_t)r * nb_mel;
-      int64_t sum = 0;
-      for (int i = 0; i < nb_mel; ++i) sum += (int64_t)d[i] * mel[i];
-      o[r] = (int32_t)(sum >> 31);
-    }
-  }
+  mq_post_body<int32_t>(
+      y, tw, maxv, maxv_stride, n, nb_mel, coefs, bf, total, nb_dct, dct, lut, dst, batch, stage,
+      [](const int32_t* x, int k, int L, int4 t) { return mq_split_q31(reinterpret_cast<const int2*>(x), k, L, t); },
+      [](int2 c, int32_t lutv) {                       // arm_cmplx_mag_q31
+        const int32_t a0 = (int32_t)(((int64_t)c.x * c.x) >> 33), a1 = (int32_t)(((int64_t)c.y * c.y) >> 33);
+        return mq_sqrt(a0 + a1, lutv);
+      },
+      [](int32_t a, int32_t c) { return ((int64_t)a * c) >> 14; },    // arm_dot_prod_q31
+      [le](int64_t r, int32_t m) {
+        r += 0x08637BD0;                                 // MICRO_Q31
+        r >>= 28;                                        // SHIFT_MELFILTER_SATURATION_Q31 + 18
+        int32_t v = mq_ssat31((int32_t)r);               // __SSAT takes the low 32 bits
+        if (m != 0 && m != 0x7FFFFFFF) v = mq_scale(v, m, 1);   // arm_scale_q31(., m, 0)
+        v = mq_log((uint32_t)v);
+        const int64_t s = (int64_t)v + le;               // arm_offset_q31 (saturating)
+        v = s > INT32_MAX ? INT32_MAX : (s < INT32_MIN ? INT32_MIN : (int32_t)s);
+        return v >> 3;                                   // arm_shift_q31(., -3)
+      },
+      [nb_mel](int r, const int32_t* mel, auto dctw) {  // arm_mat_vec_mult_q31
+        int64_t sum = 0;
+        for (int i = 0; i < nb_mel; ++i) sum += (int64_t)dctw(r * nb_mel + i) * mel[i];
+        return (int32_t)(sum >> 31);
+      });
 }
 
 // ---------------------------------------------------------------- q15
@@ -310,72 +337,38 @@ __global__ __launch_bounds__(256) void mfcc_q15_pre_kernel(const int16_t* src, c
 }
 
 __global__ __launch_bounds__(256) void mfcc_q15_post_kernel(const int16_t* __restrict__ y, const int4* __restrict__ tw,
-                                                            const int16_t* maxv,
-                                                            int maxv_stride, int n, int nb_mel,
-                                                            const uint32_t* __restrict__ pos,
-                                                            const uint32_t* __restrict__ len,
-                                                            const uint32_t* __restrict__ off,
+                                                            const int16_t* maxv, int maxv_stride, int n, int nb_mel,
                                                             const int16_t* __restrict__ coefs,
                                                             const uint32_t* __restrict__ bf, int total, int nb_dct,
                                                             const int16_t* __restrict__ dct,
                                                             const int32_t* __restrict__ lut, int16_t* dst,
-                                                            uint32_t batch) {
-  extern __shared__ int32_t shq[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int lim = (n >> 1) + 1;
-  int32_t* mag = shq + wave * mq_wave_words(n, nb_mel);
-  int32_t* mel = mag + lim;
-  int64_t* acc = reinterpret_cast<int64_t*>(mag + ((lim + nb_mel + 1) & ~1));
-  for (int i = lane; i < nb_mel; i += 64) acc[i] = 0;
-  const uint32_t frame = blockIdx.x * kMqWaves + wave;
-  const bool live = frame < batch;
-  const int32_t m = live ? maxv[(size_t)frame * maxv_stride] : 0;
-  const bool scale = m != 0 && m != 0x7FFF;
-  if (live) {
-    const short2* X = reinterpret_cast<const short2*>(y + (size_t)frame * n);
-    const int32_t lutv = lut[lane & 31];
-#pragma unroll 4
-    for (int k0 = 0; k0 < lim; k0 += 64) {             // uniform: the shuffle needs all lanes
-      const int k = k0 + lane, kc = min(k, lim - 1);
-      const int2 c = mq_split_q15(X, kc, lim - 1, tw[kc]);
-      const uint32_t s2 = ((uint32_t)((int32_t)c.x * c.x) + (uint32_t)((int32_t)c.y * c.y)) >> 1;
-      const int32_t v = mq_sqrt((int32_t)s2, lutv) >> 16;
-      if (k < lim) mag[k] = v;
-    }
-  }
-  __syncthreads();
+                                                            uint32_t batch, int stage) {
   const int32_t le = (int32_t)((uint32_t)(31 - (int)mq_clz((uint32_t)n) + 12) * 0x02C5C860u);
-  if (live) {
-    mq_mel_sums(lane, mag, bf, coefs, total, acc,
-                [](int32_t a, int32_t c) { return (int64_t)(a * c); });          // arm_dot_prod_q15
-  }
-  __syncthreads();
-  if (live) {
-    for (int i = lane; i < nb_mel; i += 64) {
-      int64_t r = acc[i];
-      r += 0x219;                                      // MICRO_Q15
-      r >>= 10;                                        // SHIFT_MELFILTER_SATURATION_Q15
-      int32_t v = mq_ssat31((int32_t)r);
-      if (scale) v = mq_scale(v, (int32_t)((uint32_t)m << 16), 1);
-      const int64_t s = (int64_t)mq_log((uint32_t)v) + le;
-      v = s > INT32_MAX ? INT32_MAX : (s < INT32_MIN ? INT32_MIN : (int32_t)s);
-      mel[i] = (int32_t)(int16_t)(v >> 19);            // (q15_t) truncation
-    }
-  }
-  __syncthreads();
-  if (live) {
-    int16_t* o = dst + (size_t)frame * nb_dct;
-    const int grouped = nb_dct & ~3;
-    for (int r = lane; r < nb_dct; r += 64) {
-      const int16_t* d = dct + (size_t)r * nb_mel;
-      const int paired = r < grouped ? (nb_mel & ~1) : (nb_mel & ~3);
-      int64_t sum = 0;
-      for (int i = 0; i < paired; i += 2)
-        sum += (int32_t)((uint32_t)(d[i] * mel[i]) + (uint32_t)(d[i + 1] * mel[i + 1]));
-      for (int i = paired; i < nb_mel; ++i) sum += (int64_t)(d[i] * mel[i]);
-      o[r] = (int16_t)mq_ssat16((int32_t)(sum >> 15));
-    }
-  }
+  mq_post_body<int16_t>(
+      y, tw, maxv, maxv_stride, n, nb_mel, coefs, bf, total, nb_dct, dct, lut, dst, batch, stage,
+      [](const int16_t* x, int k, int L, int4 t) { return mq_split_q15(reinterpret_cast<const short2*>(x), k, L, t); },
+      [](int2 c, int32_t lutv) {                       // arm_cmplx_mag_q15
+        const uint32_t s2 = ((uint32_t)(c.x * c.x) + (uint32_t)(c.y * c.y)) >> 1;
+        return mq_sqrt((int32_t)s2, lutv) >> 16;
+      },
+      [](int32_t a, int32_t c) { return (int64_t)(a * c); },          // arm_dot_prod_q15
+      [le](int64_t r, int32_t m) {
+        r += 0x219;                                      // MICRO_Q15
+        r >>= 10;                                        // SHIFT_MELFILTER_SATURATION_Q15
+        int32_t v = mq_ssat31((int32_t)r);
+        if (m != 0 && m != 0x7FFF) v = mq_scale(v, (int32_t)((uint32_t)m << 16), 1);
+        const int64_t s = (int64_t)mq_log((uint32_t)v) + le;
+        v = s > INT32_MAX ? INT32_MAX : (s < INT32_MIN ? INT32_MIN : (int32_t)s);
+        return (int32_t)(int16_t)(v >> 19);              // (q15_t) truncation
+      },
+      [nb_mel, nb_dct](int r, const int32_t* mel, auto dctw) {   // arm_mat_vec_mult_q15
+        const int paired = r < (nb_dct & ~3) ? (nb_mel & ~1) : (nb_mel & ~3);
+        int64_t sum = 0;
+        for (int i = 0; i < paired; i += 2)
+          sum += (int32_t)((uint32_t)(dctw(r * nb_mel + i) * mel[i]) + (uint32_t)(dctw(r * nb_mel + i + 1) * mel[i + 1]));
+        for (int i = paired; i < nb_mel; ++i) sum += (int64_t)(dctw(r * nb_mel + i) * mel[i]);
+        return (int16_t)mq_ssat16((int32_t)(sum >> 15));
+      });
 }
 
 hipError_t mfcc_q15_pre_launch(int n, const int16_t* src, const int16_t* win, int16_t* x, int16_t* maxv,
@@ -394,8 +387,14 @@ hipError_t mfcc_q15_post_launch(int n, const int16_t* y, const int4* tw, const i
                                 hipStream_t st) {
   if (batch == 0) return hipSuccess;
   const uint32_t grid = (batch + kMqWaves - 1) / kMqWaves;
-  hipLaunchKernelGGL(mfcc_q15_post_kernel, dim3(grid), dim3(64 * kMqWaves), mfcc_q31_post_lds(n, nb_mel), st, y,
-                     tw, maxv, maxv_stride, n, nb_mel, pos, len, off, coefs, bf, total, nb_dct, dct, lut, dst, batch);
+  (void)pos; (void)len; (void)off;
+  const uint32_t grid2 = (batch + kMqFpw * kMqWaves - 1) / (kMqFpw * kMqWaves);
+  const size_t tab = sizeof(int32_t) * (size_t)mq_tab_words(total, nb_mel, nb_dct);
+  const int stage = mfcc_q31_post_lds(n, nb_mel) + tab <= 65536 ? 1 : 0;
+  (void)grid;
+  hipLaunchKernelGGL(mfcc_q15_post_kernel, dim3(grid2), dim3(64 * kMqWaves),
+                     mfcc_q31_post_lds(n, nb_mel) + (stage ? tab : 0), st, y, tw, maxv, maxv_stride, n, nb_mel, coefs,
+                     bf, total, nb_dct, dct, lut, dst, batch, stage);
   return hipGetLastError();
 }
 
@@ -417,8 +416,14 @@ hipError_t mfcc_q31_post_launch(int n, const int32_t* y, const int4* tw, const i
                                 hipStream_t st) {
   if (batch == 0) return hipSuccess;
   const uint32_t grid = (batch + kMqWaves - 1) / kMqWaves;
-  hipLaunchKernelGGL(mfcc_q31_post_kernel, dim3(grid), dim3(64 * kMqWaves), mfcc_q31_post_lds(n, nb_mel), st, y,
-                     tw, maxv, maxv_stride, n, nb_mel, pos, len, off, coefs, bf, total, nb_dct, dct, lut, dst, batch);
+  (void)pos; (void)len; (void)off;
+  const uint32_t grid2 = (batch + kMqFpw * kMqWaves - 1) / (kMqFpw * kMqWaves);
+  const size_t tab = sizeof(int32_t) * (size_t)mq_tab_words(total, nb_mel, nb_dct);
+  const int stage = mfcc_q31_post_lds(n, nb_mel) + tab <= 65536 ? 1 : 0;
+  (void)grid;
+  hipLaunchKernelGGL(mfcc_q31_post_kernel, dim3(grid2), dim3(64 * kMqWaves),
+                     mfcc_q31_post_lds(n, nb_mel) + (stage ? tab : 0), st, y, tw, maxv, maxv_stride, n, nb_mel, coefs,
+                     bf, total, nb_dct, dct, lut, dst, batch, stage);
   return hipGetLastError();
 }
 
