@@ -117,6 +117,70 @@ __global__ __launch_bounds__(256) void rfft_fx_split_kernel(const T* __restrict_
   }
 }
 
+// Paired forward split: bins k and L - k read the same two CFFT bins (x[k], x[L-k]), so one
+// thread forms both (j in [1, L/2): bins j and L - j; j = 0: bins 0, L and L/2) and every
+// CFFT word is read once instead of twice.  Same arithmetic per bin as rfft_fx_split_kernel.
+template <typename T>
+__device__ __forceinline__ int2 rfft_split_bin(int2 a, int2 b, int32_t a1, int32_t a2, int32_t b1, int32_t b2) {
+  if constexpr (sizeof(T) == 4) {
+    int32_t re = mult_R(a.x, a1), im = mult_R(a.x, a2);
+    re = multSub_R(re, a.y, a2); im = multAcc_R(im, a.y, a1);
+    re = multSub_R(re, b.y, a2); im = multSub_R(im, b.y, b1);
+    re = multAcc_R(re, b.x, b1); im = multSub_R(im, b.x, a2);
+    return make_int2(re, im);
+  } else {
+    const int32_t re = (int32_t)(p16(a.x, a1) - p16(a.y, a2) + p16(b.x, b1) + p16(b.y, b2)) >> 16;
+    const int32_t im = (int32_t)(p16(b.x, b2) - p16(b.y, b1) + p16(a.y, a1) + p16(a.x, a2)) >> 16;
+    return make_int2(re, im);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void rfft_st_pair(T* y, int k, int n, int2 v) {   // bin k and its mirror 2n - 2k
+  Cx<T>::st(y + 2 * k, v.x, v.y);
+  if constexpr (sizeof(T) == 4) Cx<T>::st(y + 2 * n - 2 * k, v.x, wneg(v.y));
+  else Cx<T>::st(y + 2 * n - 2 * k, v.x, -v.y);
+}
+template <typename T>
+__global__ __launch_bounds__(256) void rfft_fx_split2_kernel(const T* __restrict__ src, T* __restrict__ dst,
+                                                             uint64_t rows, int n, const T* __restrict__ ta,
+                                                             const T* __restrict__ tb, uint32_t mod) {
+  const int L = n >> 1, H = L >> 1;
+  const RfftMap mp = rfft_map(H);
+  const int j = mp.k;
+  const int k2 = j == 0 ? H : L - j;                   // the partner bin
+  const uint32_t c1 = 2u * mod * (uint32_t)j, c2 = 2u * mod * (uint32_t)k2;
+  const int32_t a1 = ta[c1], a2 = ta[c1 + 1], b1 = tb[c1], b2 = tb[c1 + 1];
+  const int32_t e1 = ta[c2], e2 = ta[c2 + 1], f1 = tb[c2], f2 = tb[c2 + 1];
+  int2 av[kRfftRows], bv[kRfftRows];
+#pragma unroll
+  for (int r = 0; r < kRfftRows; ++r) {
+    const uint64_t row = min(mp.row0 + (uint64_t)r * mp.rstep, rows - 1);
+    const T* x = src + row * (uint64_t)n;
+    av[r] = Cx<T>::ld(x + 2 * j);
+    bv[r] = Cx<T>::ld(x + 2 * k2);
+  }
+#pragma unroll
+  for (int r = 0; r < kRfftRows; ++r) {
+    const uint64_t row = mp.row0 + (uint64_t)r * mp.rstep;
+    if (row >= rows) break;
+    T* y = dst + row * (uint64_t)(2 * n);
+    const int2 a = av[r], b = bv[r];
+    if (j == 0) {
+      if constexpr (sizeof(T) == 4) {
+        Cx<T>::st(y + n, wsub(a.x, a.y) >> 1, 0);
+        Cx<T>::st(y, wadd(a.x, a.y) >> 1, 0);
+      } else {
+        Cx<T>::st(y + n, (a.x - a.y) >> 1, 0);
+        Cx<T>::st(y, (a.x + a.y) >> 1, 0);
+      }
+      rfft_st_pair<T>(y, H, n, rfft_split_bin<T>(b, b, e1, e2, f1, f2));   // bin L/2: x[L/2] both ways
+      continue;
+    }
+    rfft_st_pair<T>(y, j, n, rfft_split_bin<T>(a, b, a1, a2, b1, b2));
+    rfft_st_pair<T>(y, k2, n, rfft_split_bin<T>(b, a, e1, e2, f1, f2));
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void rfft_fx_merge_kernel(const T* __restrict__ src, T* __restrict__ dst,
                                                             uint64_t rows, int n, const T* __restrict__ ta,
@@ -168,7 +232,12 @@ static hipError_t rfft_fx_pass(bool inverse, int n, const T* src, T* dst, uint32
   if (inverse)
     hipLaunchKernelGGL((rfft_fx_merge_kernel<T>), dim3((uint32_t)blocks), dim3(256), 0, st, src, dst, (uint64_t)batch,
                        n, ta, tb, mod);
-  else
+  else if (L >= 4) {
+    const int H = L / 2, hper = H < 256 ? H : 256;
+    const uint64_t hside = 256 / hper, hgroups = (batch + hside * kRfftRows - 1) / (hside * kRfftRows);
+    hipLaunchKernelGGL((rfft_fx_split2_kernel<T>), dim3((uint32_t)(hgroups * (uint64_t)(H / hper))), dim3(256), 0, st,
+                       src, dst, (uint64_t)batch, n, ta, tb, mod);
+  } else
     hipLaunchKernelGGL((rfft_fx_split_kernel<T>), dim3((uint32_t)blocks), dim3(256), 0, st, src, dst, (uint64_t)batch,
                        n, ta, tb, mod);
   return hipGetLastError();
