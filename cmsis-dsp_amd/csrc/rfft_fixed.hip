@@ -219,6 +219,56 @@ __global__ __launch_bounds__(256) void rfft_fx_merge_kernel(const T* __restrict_
   }
 }
 
+// Paired inverse merge: bins k and L - k of the N-word CFFT input read the same two spectrum
+// bins (X[k], X[L-k]); j in [1, L/2) forms both, j = 0 forms bin 0 (X[0], X[L]) and bin L/2.
+template <typename T>
+__device__ __forceinline__ int2 rfft_merge_bin(int2 a, int2 b, int32_t a1, int32_t a2, int32_t b1, int32_t b2) {
+  if constexpr (sizeof(T) == 4) {
+    // arm_rfft_q31.c:430-466
+    int32_t re = mult_R(a.x, a1), im = mult_R(a.x, wneg(a2));
+    re = multAcc_R(re, a.y, a2); im = multAcc_R(im, a.y, a1);
+    re = multAcc_R(re, b.y, a2); im = multSub_R(im, b.y, b1);
+    re = multAcc_R(re, b.x, b1); im = multAcc_R(im, b.x, a2);
+    return make_int2(re, im);
+  } else {
+    const int32_t re = (int32_t)(p16(b.x, b1) - p16(b.y, b2) + p16(a.x, a1) + p16(a.y, a2)) >> 16;
+    const int32_t im = (int32_t)(p16(a.y, a1) - p16(a.x, a2) - p16(b.x, b2) - p16(b.y, b1)) >> 16;
+    return make_int2(re, im);
+  }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void rfft_fx_merge2_kernel(const T* __restrict__ src, T* __restrict__ dst,
+                                                             uint64_t rows, int n, const T* __restrict__ ta,
+                                                             const T* __restrict__ tb, uint32_t mod) {
+  const int L = n >> 1, H = L >> 1;
+  const RfftMap mp = rfft_map(H);
+  const int j = mp.k;
+  const int k2 = j == 0 ? H : L - j;
+  const uint32_t c1 = 2u * mod * (uint32_t)j, c2 = 2u * mod * (uint32_t)k2;
+  const int32_t a1 = ta[c1], a2 = ta[c1 + 1], b1 = tb[c1], b2 = tb[c1 + 1];
+  const int32_t e1 = ta[c2], e2 = ta[c2 + 1], f1 = tb[c2], f2 = tb[c2 + 1];
+  int2 av[kRfftRows], bv[kRfftRows], hv[kRfftRows];
+#pragma unroll
+  for (int r = 0; r < kRfftRows; ++r) {
+    const uint64_t row = min(mp.row0 + (uint64_t)r * mp.rstep, rows - 1);
+    const T* x = src + row * (uint64_t)(2 * n);
+    av[r] = Cx<T>::ld(x + 2 * j);
+    bv[r] = Cx<T>::ld(x + 2 * (L - j));                // j = 0: X[L], bin 0's partner
+    hv[r] = j == 0 ? Cx<T>::ld(x + 2 * H) : make_int2(0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < kRfftRows; ++r) {
+    const uint64_t row = mp.row0 + (uint64_t)r * mp.rstep;
+    if (row >= rows) break;
+    T* y = dst + row * (uint64_t)n;
+    const int2 a = av[r], b = bv[r];
+    const int2 v1 = rfft_merge_bin<T>(a, b, a1, a2, b1, b2);
+    Cx<T>::st(y + 2 * j, v1.x, v1.y);
+    const int2 v2 = j == 0 ? rfft_merge_bin<T>(hv[r], hv[r], e1, e2, f1, f2) : rfft_merge_bin<T>(b, a, e1, e2, f1, f2);
+    Cx<T>::st(y + 2 * k2, v2.x, v2.y);
+  }
+}
+
 }  // namespace
 
 template <typename T>
@@ -229,15 +279,18 @@ static hipError_t rfft_fx_pass(bool inverse, int n, const T* src, T* dst, uint32
   const uint64_t side = 256 / kper, groups = (batch + side * kRfftRows - 1) / (side * kRfftRows);
   const uint64_t blocks = groups * (uint64_t)(L / kper);
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  if (inverse)
-    hipLaunchKernelGGL((rfft_fx_merge_kernel<T>), dim3((uint32_t)blocks), dim3(256), 0, st, src, dst, (uint64_t)batch,
-                       n, ta, tb, mod);
-  else if (L >= 4) {
+  if (L >= 4) {   // paired kernels (every length the reference's init accepts)
     const int H = L / 2, hper = H < 256 ? H : 256;
     const uint64_t hside = 256 / hper, hgroups = (batch + hside * kRfftRows - 1) / (hside * kRfftRows);
-    hipLaunchKernelGGL((rfft_fx_split2_kernel<T>), dim3((uint32_t)(hgroups * (uint64_t)(H / hper))), dim3(256), 0, st,
-                       src, dst, (uint64_t)batch, n, ta, tb, mod);
-  } else
+    const dim3 g2((uint32_t)(hgroups * (uint64_t)(H / hper)));
+    if (inverse)
+      hipLaunchKernelGGL((rfft_fx_merge2_kernel<T>), g2, dim3(256), 0, st, src, dst, (uint64_t)batch, n, ta, tb, mod);
+    else
+      hipLaunchKernelGGL((rfft_fx_split2_kernel<T>), g2, dim3(256), 0, st, src, dst, (uint64_t)batch, n, ta, tb, mod);
+  } else if (inverse)
+    hipLaunchKernelGGL((rfft_fx_merge_kernel<T>), dim3((uint32_t)blocks), dim3(256), 0, st, src, dst, (uint64_t)batch,
+                       n, ta, tb, mod);
+  else
     hipLaunchKernelGGL((rfft_fx_split_kernel<T>), dim3((uint32_t)blocks), dim3(256), 0, st, src, dst, (uint64_t)batch,
                        n, ta, tb, mod);
   return hipGetLastError();
