@@ -1036,6 +1036,80 @@ __global__ __launch_bounds__(kBlock) void fir_interp_phases_kernel(const typenam
   }
 }
 
+// Four consecutive inputs per lane: the window rides in registers (one 16-B LDS read per lane
+// per 4 taps) and each scalar coefficient feeds 4 outputs, so a tap block of 4 costs 4·4·LG
+// MACs against one LDS read and LG·4 coefficient loads (the one-input-per-lane kernel above
+// waited on a scalar load every 4·LG MACs).  Per output the taps still run i = 0, 1, ... in
+// order.  Needs N % 4 == 0 (outputs per chunk) and a 16-B aligned window.
+template <int OP, int LG>
+__global__ __launch_bounds__(kBlock) void fir_interp_phases4_kernel(const typename MrT<OP>::T* __restrict__ hq, int L,
+                                                                    int q0, int P,
+                                                                    const typename MrT<OP>::T* __restrict__ src,
+                                                                    typename MrT<OP>::T* __restrict__ dst, uint32_t B,
+                                                                    const typename MrT<OP>::T* __restrict__ hist_in,
+                                                                    uint32_t nchunks, int N) {
+  using Op = MrT<OP>;
+  using E = typename Op::T;
+  __shared__ __attribute__((aligned(16))) E win[kMrWin + 8];
+  const uint32_t f = blockIdx.x / nchunks;
+  const int n0 = (int)(blockIdx.x - f * nchunks) * N;
+  const int cnt = min(N, (int)B - n0);
+  FirItem it;
+  it.f = f; it.n0 = n0; it.count = cnt; it.total = cnt + P - 1;
+  const int padded = (it.total + 8 + 3) & ~3;           // zero tail: the last block reads 4 past
+  for (int idx = threadIdx.x; idx < padded; idx += kBlock)
+    win[idx] = idx < it.total ? fir_sample(hist_in, src, it, B, P - 1, idx) : (E)0;
+  __syncthreads();
+  E* y = dst + ((uint64_t)f * B + n0) * (uint32_t)L + q0;
+  const E* h = hq + (size_t)q0 * P;
+  for (int nl = 4 * threadIdx.x; nl < cnt; nl += 4 * kBlock) {
+    const E* w = win + nl;
+    typename Op::Acc acc[4][LG];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < LG; ++q) acc[r][q] = 0;
+    E a[8];
+    {
+      const int j0 = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = w[j0 + u];
+    }
+    int i = 0;
+    for (; i + 4 <= P; i += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[4 + u] = w[i + 4 + u];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        E c[LG];
+#pragma unroll
+        for (int q = 0; q < LG; ++q) c[q] = h[q * P + i + u];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < LG; ++q) acc[r][q] = Op::mac(acc[r][q], a[u + r], c[q]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = a[4 + u];
+    }
+    for (; i < P; ++i) {                                // P % 4 tail taps
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const E x = w[i + r];
+#pragma unroll
+        for (int q = 0; q < LG; ++q) acc[r][q] = Op::mac(acc[r][q], x, h[q * P + i]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (nl + r >= cnt) break;
+      E* o = y + (uint64_t)(nl + r) * L;
+#pragma unroll
+      for (int q = 0; q < LG; ++q) o[q] = Op::out(acc[r][q]);
+    }
+  }
+}
+
 // h_q[i] = h[(L-1-q) + i L]: the interpolator's phases as contiguous coefficient rows
 template <typename E>
 __global__ void mr_phase_coeffs_kernel(const E* __restrict__ h, E* __restrict__ hq, int L, int P) {
@@ -1168,6 +1242,9 @@ static hipError_t interpolate_launch(const void* coeffs, int L, int P, const voi
                                  : lg == 3 ? fir_interp_phases_kernel<OP, 3> : lg == 4 ? fir_interp_phases_kernel<OP, 4>
                                  : lg == 5 ? fir_interp_phases_kernel<OP, 5> : lg == 6 ? fir_interp_phases_kernel<OP, 6>
                                  : lg == 7 ? fir_interp_phases_kernel<OP, 7> : fir_interp_phases_kernel<OP, 8>;
+                          if (N % 4 == 0 && lg <= 4)
+                            k = lg == 1 ? fir_interp_phases4_kernel<OP, 1> : lg == 2 ? fir_interp_phases4_kernel<OP, 2>
+                              : lg == 3 ? fir_interp_phases4_kernel<OP, 3> : fir_interp_phases4_kernel<OP, 4>;
                           hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(kBlock), 0, st, (const E*)hq, L, q0, P, s,
                                              (E*)dst, B, h, nchunks, N);
                         }
