@@ -1041,7 +1041,11 @@ __global__ __launch_bounds__(kBlock) void fir_interp_phases_kernel(const typenam
 // MACs against one LDS read and LG·4 coefficient loads (the one-input-per-lane kernel above
 // waited on a scalar load every 4·LG MACs).  Per output the taps still run i = 0, 1, ... in
 // order.  Needs N % 4 == 0 (outputs per chunk) and a 16-B aligned window.
-template <int OP, int LG>
+#ifndef MI355X_INTERP_R
+#define MI355X_INTERP_R 4       // consecutive inputs per lane (chunks of R x 256 outputs; R = 8 with
+                                // 1024-output chunks left half the lanes idle: 89 vs 106)
+#endif
+template <int OP, int LG, int R = MI355X_INTERP_R>
 __global__ __launch_bounds__(kBlock) void fir_interp_phases4_kernel(const typename MrT<OP>::T* __restrict__ hq, int L,
                                                                     int q0, int P,
                                                                     const typename MrT<OP>::T* __restrict__ src,
@@ -1056,52 +1060,49 @@ __global__ __launch_bounds__(kBlock) void fir_interp_phases4_kernel(const typena
   const int cnt = min(N, (int)B - n0);
   FirItem it;
   it.f = f; it.n0 = n0; it.count = cnt; it.total = cnt + P - 1;
-  const int padded = (it.total + 8 + 3) & ~3;           // zero tail: the last block reads 4 past
+  const int padded = (it.total + 8 + 3) & ~3;           // zero tail: the last block reads past
   for (int idx = threadIdx.x; idx < padded; idx += kBlock)
     win[idx] = idx < it.total ? fir_sample(hist_in, src, it, B, P - 1, idx) : (E)0;
   __syncthreads();
   E* y = dst + ((uint64_t)f * B + n0) * (uint32_t)L + q0;
   const E* h = hq + (size_t)q0 * P;
-  for (int nl = 4 * threadIdx.x; nl < cnt; nl += 4 * kBlock) {
+  for (int nl = R * threadIdx.x; nl < cnt; nl += R * kBlock) {
     const E* w = win + nl;
-    typename Op::Acc acc[4][LG];
+    typename Op::Acc acc[R][LG];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < R; ++r)
 #pragma unroll
       for (int q = 0; q < LG; ++q) acc[r][q] = 0;
-    E a[8];
-    {
-      const int j0 = 0;
+    E a[R + 4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) a[u] = w[j0 + u];
-    }
+    for (int u = 0; u < R; ++u) a[u] = w[u];
     int i = 0;
     for (; i + 4 <= P; i += 4) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) a[4 + u] = w[i + 4 + u];
+      for (int u = 0; u < 4; ++u) a[R + u] = w[i + R + u];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         E c[LG];
 #pragma unroll
         for (int q = 0; q < LG; ++q) c[q] = h[q * P + i + u];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < R; ++r)
 #pragma unroll
           for (int q = 0; q < LG; ++q) acc[r][q] = Op::mac(acc[r][q], a[u + r], c[q]);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) a[u] = a[4 + u];
+      for (int u = 0; u < R; ++u) a[u] = a[u + 4];
     }
     for (; i < P; ++i) {                                // P % 4 tail taps
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < R; ++r) {
         const E x = w[i + r];
 #pragma unroll
         for (int q = 0; q < LG; ++q) acc[r][q] = Op::mac(acc[r][q], x, h[q * P + i]);
       }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < R; ++r) {
       if (nl + r >= cnt) break;
       E* o = y + (uint64_t)(nl + r) * L;
 #pragma unroll
@@ -1224,7 +1225,7 @@ static hipError_t interpolate_launch(const void* coeffs, int L, int P, const voi
   if (batch == 0 || B == 0) return hipSuccess;
   if (L < 1 || P < 1 || P > kMrWin - kBlock) return hipErrorInvalidValue;
   int N = kMrWin - (P - 1);
-  N = N >= 4 * kBlock ? 4 * kBlock : (N >= kBlock ? (N / kBlock) * kBlock : N);
+  N = N >= MI355X_INTERP_R * kBlock ? MI355X_INTERP_R * kBlock : (N >= kBlock ? (N / kBlock) * kBlock : N);
   const uint32_t nchunks = (B + N - 1) / N;
   const uint64_t blocks = (uint64_t)nchunks * batch;
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
@@ -1242,7 +1243,7 @@ static hipError_t interpolate_launch(const void* coeffs, int L, int P, const voi
                                  : lg == 3 ? fir_interp_phases_kernel<OP, 3> : lg == 4 ? fir_interp_phases_kernel<OP, 4>
                                  : lg == 5 ? fir_interp_phases_kernel<OP, 5> : lg == 6 ? fir_interp_phases_kernel<OP, 6>
                                  : lg == 7 ? fir_interp_phases_kernel<OP, 7> : fir_interp_phases_kernel<OP, 8>;
-                          if (N % 4 == 0 && lg <= 4)
+                          if (N % MI355X_INTERP_R == 0 && lg <= 4)
                             k = lg == 1 ? fir_interp_phases4_kernel<OP, 1> : lg == 2 ? fir_interp_phases4_kernel<OP, 2>
                               : lg == 3 ? fir_interp_phases4_kernel<OP, 3> : fir_interp_phases4_kernel<OP, 4>;
                           hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(kBlock), 0, st, (const E*)hq, L, q0, P, s,
