@@ -1041,11 +1041,10 @@ __global__ __launch_bounds__(kBlock) void fir_interp_phases_kernel(const typenam
 // MACs against one LDS read and LG·4 coefficient loads (the one-input-per-lane kernel above
 // waited on a scalar load every 4·LG MACs).  Per output the taps still run i = 0, 1, ... in
 // order.  Needs N % 4 == 0 (outputs per chunk) and a 16-B aligned window.
-#ifndef MI355X_INTERP_R
-#define MI355X_INTERP_R 4       // consecutive inputs per lane (chunks of R x 256 outputs; R = 8 with
-                                // 1024-output chunks left half the lanes idle: 89 vs 106)
-#endif
-template <int OP, int LG, int R = MI355X_INTERP_R>
+// consecutive inputs per lane: f32 8 (2048-output chunks: 110 vs 106 G input samples/s at 4),
+// the int64-accumulator types 4 (chunks of R x 256 outputs keep every lane busy)
+template <int OP> constexpr int interp_r() { return OP == kMrF32 ? 8 : 4; }
+template <int OP, int LG, int R = interp_r<OP>()>
 __global__ __launch_bounds__(kBlock) void fir_interp_phases4_kernel(const typename MrT<OP>::T* __restrict__ hq, int L,
                                                                     int q0, int P,
                                                                     const typename MrT<OP>::T* __restrict__ src,
@@ -1225,7 +1224,8 @@ static hipError_t interpolate_launch(const void* coeffs, int L, int P, const voi
   if (batch == 0 || B == 0) return hipSuccess;
   if (L < 1 || P < 1 || P > kMrWin - kBlock) return hipErrorInvalidValue;
   int N = kMrWin - (P - 1);
-  N = N >= MI355X_INTERP_R * kBlock ? MI355X_INTERP_R * kBlock : (N >= kBlock ? (N / kBlock) * kBlock : N);
+  constexpr int kR = interp_r<OP>();
+  N = N >= kR * kBlock ? kR * kBlock : (N >= kBlock ? (N / kBlock) * kBlock : N);
   const uint32_t nchunks = (B + N - 1) / N;
   const uint64_t blocks = (uint64_t)nchunks * batch;
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
@@ -1243,7 +1243,7 @@ static hipError_t interpolate_launch(const void* coeffs, int L, int P, const voi
                                  : lg == 3 ? fir_interp_phases_kernel<OP, 3> : lg == 4 ? fir_interp_phases_kernel<OP, 4>
                                  : lg == 5 ? fir_interp_phases_kernel<OP, 5> : lg == 6 ? fir_interp_phases_kernel<OP, 6>
                                  : lg == 7 ? fir_interp_phases_kernel<OP, 7> : fir_interp_phases_kernel<OP, 8>;
-                          if (N % MI355X_INTERP_R == 0 && lg <= 4)
+                          if (N % kR == 0 && lg <= 4)
                             k = lg == 1 ? fir_interp_phases4_kernel<OP, 1> : lg == 2 ? fir_interp_phases4_kernel<OP, 2>
                               : lg == 3 ? fir_interp_phases4_kernel<OP, 3> : fir_interp_phases4_kernel<OP, 4>;
                           hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(kBlock), 0, st, (const E*)hq, L, q0, P, s,
