@@ -110,7 +110,13 @@ def launch_ranks(args, argv):
     log("bench: launching", args.gpus, "ranks:", " ".join(cmd))
     env = dict(os.environ)
     env.setdefault("OMP_NUM_THREADS", "4")
-    return subprocess.run(cmd, env=env).returncode
+    # stdout carries only the JSON line: library chatter the ranks print (e.g. gloo's
+    # connection messages) is passed on to stderr
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    for line in proc.stdout:
+        (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+        sys.stdout.flush()
+    return proc.wait()
 
 
 # ------------------------------------------------------------------ CPU baseline
