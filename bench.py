@@ -564,6 +564,8 @@ def main_rank(args):
         algo_bytes = units * bps                           # N in, N written back, 2N spectrum out
     elif args.workload == "mfcc_f32":
         wall, kern_ms, parity = run_mfcc(n, batch, args.steps, args.warmup)
+        units = batch * n                                  # input samples
+        algo_bytes = units * bps + batch * 13 * 4          # frames in + coefficients out
     elif args.workload in ("mfcc_q31", "mfcc_q15"):
         wall, kern_ms, parity = run_mfcc_fixed(args.workload[-3:], n, batch, args.steps, args.warmup)
         units = batch * n                                  # input samples

@@ -235,6 +235,7 @@ arm_status rfft_fixed_batch(const RInst* S, T* d_src, T* d_dst, uint32_t batch, 
 // ---- MFCC (arm_mfcc_f32.c:83-160): the instance's user tables packed into one
 // content-cached device blob: [dct | filter coefs | window | pos | len | coef offsets]
 struct MfccDev {
+  int total = 0;                   // Mel coefficients (sum of filterLengths)
   const float* dct = nullptr;
   const float* coefs = nullptr;
   const float* win = nullptr;
@@ -286,6 +287,7 @@ bool mfcc_prepare(const arm_mfcc_instance_f32* S, MfccDev& d) {
   memcpy(u + 2 * b_u, off.data(), sizeof(uint32_t) * nm);
   const uint8_t* dev = (const uint8_t*)device_blob(blob.data(), blob.size());
   if (!dev) return false;
+  d.total = (int)total;
   d.dct = (const float*)dev;
   d.coefs = (const float*)(dev + b_dct);
   d.win = (const float*)(dev + b_dct + b_cf);
@@ -310,7 +312,7 @@ bool mfcc_run(const arm_mfcc_instance_f32* S, const MfccDev& d, float* x, float*
     const void* twr = device_table(S->rfft.pTwiddleRFFT, sizeof(float) * n);
     if (!tw || !twr) return false;
     MI_CHECK(mfcc_f32_fused_launch(n, x, d.win, (const float*)tw, (const float*)twr, nm, d.pos, d.len, d.off,
-                                   d.coefs, nd, d.dct, dst, batch, st),
+                                   d.coefs, nd, d.dct, dst, batch, d.total, st),
              "mfcc fused");
     return true;
   }

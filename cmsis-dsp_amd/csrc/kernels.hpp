@@ -96,7 +96,7 @@ hipError_t fir_lattice_run(int op, const void* coeffs, int num_stages, const voi
 hipError_t mfcc_f32_fused_launch(int n, const float* src, const float* win, const float* tw, const float* twr,
                                  int nb_mel, const uint32_t* pos, const uint32_t* len, const uint32_t* off,
                                  const float* coefs, int nb_dct, const float* dct, float* dst, uint32_t batch,
-                                 hipStream_t st);
+                                 int total, hipStream_t st);
 // The frame maximum of frame f is written to / read from maxv[f * maxv_stride].
 hipError_t mfcc_f32_pre_launch(int n, const float* src, const float* win, float* x, float* maxv, uint32_t batch,
                                int maxv_stride, hipStream_t st);

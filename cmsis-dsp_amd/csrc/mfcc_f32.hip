@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kBlock) void mfcc_fused_kernel(const float* __restr
                                                             const uint32_t* __restrict__ off,
                                                             const float* __restrict__ coefs, int nb_dct,
                                                             const float* __restrict__ dct, float* __restrict__ dst,
-                                                            uint32_t batch) {
+                                                            uint32_t batch, int total, int stage) {
   using P = PlanF32<H>;
   constexpr int NF = 2 * H, LPT = P::LPT, TPB = P::TPB;
   __shared__ __attribute__((aligned(16))) float2 lds[TPB * H];
@@ -152,6 +152,15 @@ __global__ __launch_bounds__(kBlock) void mfcc_fused_kernel(const float* __restr
   __shared__ float wmax[kBlock / 64];
   const int tid = threadIdx.x;
   for (int i = tid; i < H; i += kBlock) { tws[i] = tw[i]; twrs[i] = twr[i]; }
+  // the Mel coefficients and DCT rows too, when they fit beside the frames (dynamic LDS):
+  // the sequential per-filter sums then wait on LDS instead of L2
+  extern __shared__ float mtab[];
+  if (stage) {
+    for (int i = tid; i < total; i += kBlock) mtab[i] = coefs[i];
+    for (int i = tid; i < nb_mel * nb_dct; i += kBlock) mtab[total + i] = dct[i];
+  }
+  const float* cbase = stage ? mtab : coefs;
+  const float* dbase = stage ? mtab + total : dct;
   const uint64_t f0 = (uint64_t)blockIdx.x * TPB;
   const int valid = (int)min<uint64_t>((uint64_t)TPB, batch - f0);
   {  // frames -> LDS (swizzled image), 16-B coalesced; frames past the batch end are zero-filled
@@ -238,7 +247,7 @@ __global__ __launch_bounds__(kBlock) void mfcc_fused_kernel(const float* __restr
 #endif
   for (int i = lane; i < nb_mel; i += LPT) {
     const uint32_t p = pos[i], l = len[i];
-    const float* c = coefs + off[i];
+    const float* c = cbase + off[i];
     float sum = 0.0f;
 #pragma unroll MI355X_MFCC_UNROLL
     for (uint32_t j = 0; j < l; ++j) {
@@ -252,7 +261,7 @@ __global__ __launch_bounds__(kBlock) void mfcc_fused_kernel(const float* __restr
   if (tr < valid) {
     float* o = dst + (f0 + tr) * (uint64_t)nb_dct;
     for (int r = lane; r < nb_dct; r += LPT) {
-      const float* d = dct + (size_t)r * nb_mel;
+      const float* d = dbase + (size_t)r * nb_mel;
       float sum = 0.0f;
 #pragma unroll MI355X_MFCC_UNROLL
       for (int i = 0; i < nb_mel; ++i) {
@@ -267,23 +276,31 @@ __global__ __launch_bounds__(kBlock) void mfcc_fused_kernel(const float* __restr
 template <int H>
 static hipError_t launch_fused(const float* src, const float* win, const float* tw, const float* twr, int nb_mel,
                                const uint32_t* pos, const uint32_t* len, const uint32_t* off, const float* coefs,
-                               int nb_dct, const float* dct, float* dst, uint32_t batch, hipStream_t st) {
+                               int nb_dct, const float* dct, float* dst, uint32_t batch, int total, hipStream_t st) {
   constexpr int TPB = PlanF32<H>::TPB;
   const uint32_t grid = (uint32_t)((batch + TPB - 1) / TPB);
-  hipLaunchKernelGGL(mfcc_fused_kernel<H>, dim3(grid), dim3(kBlock), 0, st, src, win, (const float2*)tw,
-                     (const float2*)twr, nb_mel, pos, len, off, coefs, nb_dct, dct, dst, batch);
+  static size_t static_lds = 0;
+  if (!static_lds) {
+    hipFuncAttributes a;
+    static_lds = hipFuncGetAttributes(&a, (const void*)mfcc_fused_kernel<H>) == hipSuccess ? a.sharedSizeBytes : 65536;
+  }
+  const size_t dyn = sizeof(float) * ((size_t)total + (size_t)nb_mel * nb_dct);
+  const int stage = total > 0 && static_lds + dyn <= 65536 ? 1 : 0;
+  hipLaunchKernelGGL(mfcc_fused_kernel<H>, dim3(grid), dim3(kBlock), stage ? dyn : 0, st, src, win, (const float2*)tw,
+                     (const float2*)twr, nb_mel, pos, len, off, coefs, nb_dct, dct, dst, batch, total, stage);
   return hipGetLastError();
 }
 
 hipError_t mfcc_f32_fused_launch(int n, const float* src, const float* win, const float* tw, const float* twr,
                                  int nb_mel, const uint32_t* pos, const uint32_t* len, const uint32_t* off,
                                  const float* coefs, int nb_dct, const float* dct, float* dst, uint32_t batch,
-                                 hipStream_t st) {
+                                 int total, hipStream_t st) {
   if (batch == 0) return hipSuccess;
   if (nb_mel > n / 2) return hipErrorInvalidValue;
   switch (n) {
 #define MI_FUSED(NF) \
-    case NF: return launch_fused<NF / 2>(src, win, tw, twr, nb_mel, pos, len, off, coefs, nb_dct, dct, dst, batch, st);
+    case NF: return launch_fused<NF / 2>(src, win, tw, twr, nb_mel, pos, len, off, coefs, nb_dct, dct, dst, batch, \
+                                         total, st);
     MI_FUSED(32) MI_FUSED(64) MI_FUSED(128) MI_FUSED(256) MI_FUSED(512) MI_FUSED(1024) MI_FUSED(2048) MI_FUSED(4096)
 #undef MI_FUSED
     default: return hipErrorInvalidValue;
