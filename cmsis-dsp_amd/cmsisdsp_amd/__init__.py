@@ -399,6 +399,11 @@ def cfft_batch_multi(S, shards, ifft, bitrev, kind=None):
         kind = {arm_cfft_instance_f32: "f32", arm_cfft_instance_q31: "q31",
                 arm_cfft_instance_q15: "q15"}[type(S)]
     k = len(shards)
+    # the C side runs each shard on the library's own stream of that device: order it after
+    # whatever torch work is still producing the shards
+    import torch
+    for d in sorted({t.device.index for t in shards}):
+        torch.cuda.synchronize(d)
     devs = (C.c_int * k)(*[t.device.index for t in shards])
     ptrs = (C.c_void_p * k)(*[t.data_ptr() for t in shards])
     cnts = (C.c_uint32 * k)(*[t.numel() // (2 * S.fftLen) for t in shards])
@@ -410,6 +415,15 @@ def cfft_batch_multi(S, shards, ifft, bitrev, kind=None):
 
 def device_count():
     return lib.arm_mi355x_device_count()
+
+
+def table_cache_bytes():
+    """Device bytes held by the content-keyed cache of host tables / coefficients."""
+    return lib.arm_mi355x_table_cache_bytes()
+
+
+def set_table_cache_limit(nbytes):
+    lib.arm_mi355x_set_table_cache_limit(C.c_size_t(nbytes))
 
 
 def rfft_fast_batch(S, p, out, ifft, stream=None):

@@ -903,7 +903,14 @@ void fir_init(Inst* S, uint16_t numTaps, const T* pCoeffs, T* pState, uint32_t b
 
 extern "C" {
 
-const char* arm_mi355x_version(void) { return "cmsisdsp-mi355x 0.1.0 gfx950"; }
+#ifndef MI355X_BUILD_DEFS
+#define MI355X_BUILD_DEFS ""
+#endif
+// "[...]" lists the non-default tuning macros of the build (Makefile DEFS, build_variant.sh)
+const char* arm_mi355x_version(void) {
+  return sizeof(MI355X_BUILD_DEFS) > 1 ? "cmsisdsp-mi355x 0.2.0 gfx950 [" MI355X_BUILD_DEFS "]"
+                                       : "cmsisdsp-mi355x 0.2.0 gfx950";
+}
 
 void arm_cfft_f32(const arm_cfft_instance_f32* S, float32_t* p1, uint8_t ifftFlag, uint8_t bitReverseFlag) {
   cfft_sync(S, p1, ifftFlag, bitReverseFlag, 0, sizeof(float));

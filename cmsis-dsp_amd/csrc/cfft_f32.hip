@@ -168,14 +168,10 @@ __global__ __launch_bounds__(64 * kN1024Wpb, MI355X_N1024_WAVES) void cfft_f32_n
 #pragma unroll
   for (int m = 0; m < 7; ++m) w1[m] = tw[16 * (m + 1) * j1];        // stage 1: j = l%8, modifier 16
 
-// MI355X_PF: software-pipelined loads (the next transform's 16 loads are issued right
-// after phase A, in flight during phases B/C).  MI355X_NT: non-temporal loads/stores (the
-// batch is streamed once).  Both on: +4% over neither under the persistent walk
-// (profiles/r01/variants_n1024.txt); with T = 4 consecutive transforms per wave the prefetch
-// measured 1% slower and is off, NT stays (-13% without it).
-#ifndef MI355X_PF
-#define MI355X_PF 0
-#endif
+// MI355X_NT: non-temporal loads/stores (the batch is streamed once; -13% without).  A
+// software-pipelined variant (the next transform's loads under phases B/C) was +4% under the
+// persistent walk (profiles/r01/variants_n1024.txt) and 1% slower with T = 4 consecutive
+// transforms per wave; it was removed in round 3.
 #ifndef MI355X_NT
 #define MI355X_NT 1
 #endif
@@ -185,24 +181,11 @@ __global__ __launch_bounds__(64 * kN1024Wpb, MI355X_N1024_WAVES) void cfft_f32_n
 #define LD(p) (*(p))
 #endif
   float2 a[8], b[8];
-#if MI355X_PF
-  float2 na[8], nb[8];
-  if (t_begin < t_end) {
-    const float2* X0 = data + (size_t)t_begin * 1024;
-#pragma unroll
-    for (int m = 0; m < 8; ++m) { na[m] = LD(&X0[l + 64 * m]); nb[m] = LD(&X0[512 + l + 64 * m]); }
-  }
-#endif
   for (uint32_t t = t_begin; t < t_end; t += t_step) {
     float2* X = data + (size_t)t * 1024;
     // ---------------- phase A
-#if MI355X_PF
-#pragma unroll
-    for (int m = 0; m < 8; ++m) { a[m] = na[m]; b[m] = nb[m]; }
-#else
 #pragma unroll
     for (int m = 0; m < 8; ++m) { a[m] = LD(&X[l + 64 * m]); b[m] = LD(&X[512 + l + 64 * m]); }
-#endif
     if (ifft) {
 #pragma unroll
       for (int m = 0; m < 8; ++m) { a[m].y = -a[m].y; b[m].y = -b[m].y; }
@@ -224,13 +207,6 @@ __global__ __launch_bounds__(64 * kN1024Wpb, MI355X_N1024_WAVES) void cfft_f32_n
     wave_sync();                    // previous transform's phase C reads are done
 #pragma unroll
     for (int m = 0; m < 8; ++m) { lds[s1024(l + 64 * m)] = a[m]; lds[s1024(512 + l + 64 * m)] = b[m]; }
-#if MI355X_PF
-    if (t + t_step < t_end) {          // next transform's loads fly under phases B and C
-      const float2* XN = data + (size_t)(t + t_step) * 1024;
-#pragma unroll
-      for (int m = 0; m < 8; ++m) { na[m] = LD(&XN[l + 64 * m]); nb[m] = LD(&XN[512 + l + 64 * m]); }
-    }
-#endif
     wave_sync();
     // ---------------- phase B: stage 1
     {

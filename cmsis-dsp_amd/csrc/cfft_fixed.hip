@@ -537,90 +537,10 @@ __global__ __launch_bounds__(256, MI355X_FXQ15_WAVES) void cfft_q15_4096_pk_kern
 #undef TW4Q
 
 // ============================================================================================
-// q31 N = 4096, one wave per transform (MI355X_FX_W4096 = 1): the access pattern of the one-wave
-// f32 kernels (N = 512 .. 2048 run at 74-76 % of HBM, the 256-thread-per-transform kernels at
-// 68-69 %).  Lane l holds x[l + 64m] (m < 64, 128 VGPRs); stages 0-2 (spans 4096, 1024, 256) are
-// butterflies between a lane's own registers; one LDS transpose (slot l + 65m -> lane l' reads
-// 65 l' + k: conflict free for ds_write_b64 and ds_read(2)_b64) gives lane l' the 64-element
-// block e = 64 l' + k, where stages 3-5 run in registers again with lane-uniform twiddles.  The
-// bit reversal is free: bin(64 l' + k) = 64 rev6(k) + rev6(l'), so every store instruction
-// writes one 512-byte row.  One workgroup of 4 waves per CU (LDS: 4 x 33 KiB exchange + the
-// 24 KiB twiddle table, read by all four waves), persistent over the batch.
-// Measured (profiles/r02/variants_fx4096w/): bit-exact, but 273 Gsamples/s against 345 for
-// cfft_fx4096_kernel -- at one wave per SIMD (LDS-bound) with no room for a register prefetch
-// (256 VGPRs + AGPR spills) each wave waits out its own loads; off.
-#ifndef MI355X_FX_W4096
-#define MI355X_FX_W4096 0
-#endif
-constexpr int kW4096Tw = 3072;             // the table's 3N/4 complex words
-constexpr int kW4096Row = 4096 + 64;       // exchange slots per wave (slot = e + e / 64)
-
-__device__ __forceinline__ void fx_wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-template <bool INV>
-__global__ __launch_bounds__(256, 1) void cfft_q31_4096w_kernel(int2* __restrict__ data, uint32_t batch,
-                                                              const int2* __restrict__ tw) {
-  __shared__ int2 twl[kW4096Tw];
-  __shared__ int2 xch[4][kW4096Row];
-  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < kW4096Tw; i += 256) twl[i] = tw[i];
-  __syncthreads();
-  int2* X = xch[wv];
-  int2 t1[4][3], t2[3];                    // lane-constant: stage 1 (index 4 (l + 64n)), stage 2 (16 l)
-#pragma unroll
-  for (int n = 0; n < 4; ++n)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) t1[n][k] = twl[(k + 1) * 4 * (l + 64 * n)];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) t2[k] = twl[(k + 1) * 16 * l];
-  const int rl = (int)(__brev((uint32_t)l) >> 26);
-  const uint32_t nw = gridDim.x * 4;
-  for (uint32_t tr = blockIdx.x * 4 + wv; tr < batch; tr += nw) {
-    const __amdgpu_buffer_rsrc_t r = fx_rsrc(data + (size_t)tr * 4096, 4096 * 8);
-    int2 v[64];
-#pragma unroll
-    for (int m = 0; m < 64; ++m) v[m] = FxIO<int2>::ld(r, l * 8, m * 512);
-#pragma unroll
-    for (int n = 0; n < 16; ++n) {         // stage 0 (span 4096): j = l + 64n
-      const int j = l + 64 * n;
-      bfly<int32_t, INV, 0>(v[n], v[n + 16], v[n + 32], v[n + 48], twl[j], twl[2 * j], twl[3 * j]);
-    }
-#pragma unroll
-    for (int d = 0; d < 4; ++d)            // stage 1 (span 1024): j = l + 64 (m mod 4)
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-        bfly<int32_t, INV, 1>(v[16 * d + n], v[16 * d + n + 4], v[16 * d + n + 8], v[16 * d + n + 12], t1[n][0],
-                              t1[n][1], t1[n][2]);
-#pragma unroll
-    for (int g = 0; g < 16; ++g)           // stage 2 (span 256): j = l
-      bfly<int32_t, INV, 1>(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3], t2[0], t2[1], t2[2]);
-    fx_wave_sync();                        // the previous transform's exchange reads are done
-#pragma unroll
-    for (int m = 0; m < 64; ++m) X[l + 65 * m] = v[m];
-    fx_wave_sync();
-#pragma unroll
-    for (int k = 0; k < 64; ++k) v[k] = X[65 * l + k];
-#pragma unroll
-    for (int k0 = 0; k0 < 16; ++k0)        // stage 3 (span 64): j = k0, index 64 j
-      bfly<int32_t, INV, 1>(v[k0], v[k0 + 16], v[k0 + 32], v[k0 + 48], twl[64 * k0], twl[128 * k0], twl[192 * k0]);
-#pragma unroll
-    for (int b = 0; b < 4; ++b)            // stage 4 (span 16): j = k1, index 256 j
-#pragma unroll
-      for (int k1 = 0; k1 < 4; ++k1)
-        bfly<int32_t, INV, 1>(v[16 * b + k1], v[16 * b + k1 + 4], v[16 * b + k1 + 8], v[16 * b + k1 + 12],
-                              twl[256 * k1], twl[512 * k1], twl[768 * k1]);
-#pragma unroll
-    for (int g = 0; g < 16; ++g)           // stage 5 (span 4, no twiddles)
-      bfly<int32_t, INV, 2>(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3], int2{}, int2{}, int2{});
-#pragma unroll
-    for (int k = 0; k < 64; ++k)           // bin 64 rev6(k) + rev6(l)
-      FxIO<int2>::st(r, rl * 8, (int)(__brev((uint32_t)k) >> 26) * 512, v[k]);
-  }
-}
+// A one-wave-per-transform q31 N = 4096 kernel (the one-wave f32 pattern; lane l holds x[l + 64m],
+// one LDS transpose) was bit-exact but ran 273 vs 345 Gsamples/s: a 32 KiB transform needs 33 KiB
+// of LDS per wave and 128 data VGPRs, leaving no room for the next transform's loads
+// (profiles/r02/variants_fx4096w/).  Removed in round 3.
 
 template <typename T, bool INV, bool BREV, bool SAT>
 static void launch_fx4096_t(void* data, uint32_t batch, const void* tw, hipStream_t st) {
@@ -629,10 +549,6 @@ static void launch_fx4096_t(void* data, uint32_t batch, const void* tw, hipStrea
     auto k = cfft_q15_4096_pk_kernel<INV, BREV, SAT>;
     const int grid = fx_grid<MI355X_FXQ15_T>((const void*)k, batch);
     hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (short2*)data, batch, (const short2*)tw);
-  } else if (sizeof(T) == 4 && MI355X_FX_W4096 && BREV && !SAT) {
-    auto k = cfft_q31_4096w_kernel<INV>;
-    const int grid = persistent_grid((const void*)k, 256, 0, (batch + 3) / 4);
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (int2*)data, batch, (const int2*)tw);
   } else {
     auto k = cfft_fx4096_kernel<T, INV, BREV, SAT>;
     const int grid = fx_grid<MI355X_FX_T>((const void*)k, batch);

@@ -7,12 +7,6 @@
 
 namespace mi355x {
 
-// MI355X_FX_NULL = 1 (experiments only): butterflies do nothing, so a kernel keeps only its
-// memory traffic and LDS exchanges -- the ceiling of its access pattern (results are wrong).
-#ifndef MI355X_FX_NULL
-#define MI355X_FX_NULL 0
-#endif
-
 // ------------------------------------------------------------------ q31 butterflies
 // stage kinds: 0 = first (>>4 in, <<1 out), 1 = middle (>>2 / >>1), 2 = last (no twiddle)
 template <bool INV, int KIND>
@@ -175,9 +169,6 @@ template <bool INV> __device__ __forceinline__ s16x2 cmul_pk(TwP w, s16x2 R) {
 
 template <bool INV, int KIND>
 __device__ __forceinline__ void bfly_pk(s16x2& a, s16x2& b, s16x2& c, s16x2& d, TwP w1, TwP w2, TwP w3) {
-#if MI355X_FX_NULL
-  a ^= w1.p; b ^= w2.q; c ^= w3.p; return;
-#endif
   constexpr short SH = KIND == 0 ? 2 : 0;
   const s16x2 A = a >> SH, B = b >> SH, Cc = c >> SH, D = d >> SH;
   s16x2 R = pk_sat_add(A, Cc), S = pk_sat_sub(A, Cc), T = pk_sat_add(B, D);
@@ -227,7 +218,6 @@ template <typename T> __device__ __forceinline__ int2 sat_shl1(int2 v) {
 
 template <typename T, bool INV, int KIND>
 __device__ __forceinline__ void bfly(int2& a, int2& b, int2& c, int2& d, int2 w1, int2 w2, int2 w3) {
-  if constexpr (MI355X_FX_NULL) { a.x ^= w1.x; b.y ^= w2.y; c.x ^= w3.x; return; }
   if constexpr (sizeof(T) == 4) bfly_q31<INV, KIND>(a, b, c, d, w1, w2, w3);
   else bfly_q15<INV, KIND>(a, b, c, d, w1, w2, w3);
 }
@@ -262,7 +252,7 @@ template <> struct FxIO<short2> {
 // persistent grid walking the batch with stride = grid; T > 0: workgroup b takes the T
 // consecutive transforms bT .. bT+T-1 (grid = batch / T; the prefetch runs inside the run).
 // Measured at 2^20 transforms (profiles/r02/variants_fx4096/): T = 8 ran at the ceiling of
-// the kernels' own access pattern (a build with the butterflies removed, MI355X_FX_NULL) on
+// the kernels' own access pattern (a probe build with the butterflies removed) on
 // every box, while the persistent walk ranged 316-354 Gsamples/s (q31) from box to box.
 #ifndef MI355X_FX_T
 #define MI355X_FX_T 8

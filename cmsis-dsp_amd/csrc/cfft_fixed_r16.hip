@@ -32,12 +32,9 @@ namespace mi355x {
 #ifndef MI355X_FXR_T
 #define MI355X_FXR_T 8
 #endif
-// MI355X_FXR_SMALL = 1: N = 32 / 64 / 128 on this kernel as well (bit-exact, but with 2-8
-// threads per transform each load instruction scatters over 32-8 transforms: q31 32/64/128
-// 42 / 201 / 254 Gsamples/s against 342 / 334 / 324 for the generic kernel; off).
-#ifndef MI355X_FXR_SMALL
-#define MI355X_FXR_SMALL 0
-#endif
+// N = 32 / 64 / 128 stay on the generic kernel: with 2-8 threads per transform each load
+// instruction would scatter over 32-8 transforms (measured on this kernel, bit-exact: q31
+// 42 / 201 / 254 Gsamples/s against 342 / 334 / 324 for the generic kernel).
 
 template <int N> struct R16 {
   static constexpr int LOG = Log2<N>::v;
@@ -345,11 +342,6 @@ static void launch_r16(void* data, uint32_t batch, const void* tw, uint32_t flag
 template <typename T>
 static bool dispatch_r16(int n, void* data, uint32_t batch, const void* tw, uint32_t flags, hipStream_t st) {
   switch (n) {
-#if MI355X_FXR_SMALL
-    case 32:   launch_r16<T, 32>(data, batch, tw, flags, st); return true;
-    case 64:   launch_r16<T, 64>(data, batch, tw, flags, st); return true;
-    case 128:  launch_r16<T, 128>(data, batch, tw, flags, st); return true;
-#endif
     case 256:  launch_r16<T, 256>(data, batch, tw, flags, st); return true;
     case 512:  launch_r16<T, 512>(data, batch, tw, flags, st); return true;
     case 1024: launch_r16<T, 1024>(data, batch, tw, flags, st); return true;

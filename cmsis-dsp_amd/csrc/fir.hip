@@ -33,6 +33,7 @@ constexpr int kFirMaxTaps = 1024;              // LDS budget: (2048 + 1023) * 4 
 struct FirItem {
   uint32_t f;
   int n0, count, total;   // first output, outputs in the chunk, window samples (count + T - 1)
+  int a = 0;              // tap offset of the window (long filters run in tap segments)
 };
 __device__ __forceinline__ FirItem fir_item(uint32_t item, uint32_t nchunks, uint32_t B, int T1,
                                             int chunk = kFirChunk) {
@@ -49,7 +50,7 @@ __device__ __forceinline__ FirItem fir_item(uint32_t item, uint32_t nchunks, uin
 template <typename T>
 __device__ __forceinline__ T fir_sample(const T* __restrict__ hist, const T* __restrict__ src, const FirItem& it,
                                         uint32_t B, int T1, int j) {
-  const int sidx = it.n0 + min(j, it.total - 1);
+  const int sidx = it.n0 + it.a + min(j, it.total - 1);
   const T* p = sidx < T1 ? hist + ((uint64_t)it.f * T1 + sidx) : src + ((uint64_t)it.f * B + (sidx - T1));
   const T v = *p;
   return j < it.total ? v : (T)0;
@@ -124,11 +125,13 @@ __device__ __forceinline__ int opaque(int x) {
 }
 // Rows k >= KPRE - 8 never reach the history (T1 < 256 (KPRE - 8)); the history words are
 // kept apart and OR-ed in when the window is written to LDS, so no wait is placed before the
-// MACs that the fetch is meant to overlap.
-template <int KPRE>
+// MACs that the fetch is meant to overlap.  A tap segment of a long filter (LONG, numTaps >
+// kFirSeg) starts a tap offset a into s, so any row can reach the history: all rows get one.
+template <int KPRE, bool LONG>
 struct F32Win {
+  static constexpr int kH = LONG ? KPRE : KPRE - 8;
   int x[KPRE];
-  int h[KPRE - 8];
+  int h[kH];
 };
 // Input addressing of fir_f32_kernel: filter f reads block samples from src + f * stride, of
 // which the first len are valid (beyond, and before 0, reads return 0), shifted by so (window
@@ -142,24 +145,25 @@ struct FirIn {
   uint32_t hist;
   uint64_t cstride;
 };
-template <int KPRE>
-__device__ __forceinline__ void fir_f32_fetch(F32Win<KPRE>& w, const FirItem& it, const float* __restrict__ src,
+// window of the tap segment starting at tap a: sample j = s[n0 + a + j]
+template <int KPRE, bool LONG>
+__device__ __forceinline__ void fir_f32_fetch(F32Win<KPRE, LONG>& w, const FirItem& it, const float* __restrict__ src,
                                               const float* __restrict__ hist_in, const FirIn& in, int T1, int tid) {
   const __amdgpu_buffer_rsrc_t r = buf_rsrc(src + it.f * in.stride, in.len * 4u);
   const __amdgpu_buffer_rsrc_t rh = in.hist ? buf_rsrc(hist_in + (uint64_t)it.f * T1, (uint32_t)T1 * 4u)
                                             : buf_rsrc(src, 0u);
-  const int v0 = (tid + it.n0 - T1 + in.so) * 4, h0 = (tid + it.n0) * 4;
+  const int v0 = (tid + it.n0 + it.a - T1 + in.so) * 4, h0 = (tid + it.n0 + it.a) * 4;
 #pragma unroll
   for (int k = 0; k < KPRE; ++k) w.x[k] = __builtin_amdgcn_raw_buffer_load_b32(r, opaque(v0 + 1024 * k), 0, 0);
 #pragma unroll
-  for (int k = 0; k < KPRE - 8; ++k)
-    w.h[k] = __builtin_amdgcn_raw_buffer_load_b32(rh, opaque(h0 + 1024 * k), 0, 0);   // n0 >= T1: out of range, 0
+  for (int k = 0; k < w.kH; ++k)
+    w.h[k] = __builtin_amdgcn_raw_buffer_load_b32(rh, opaque(h0 + 1024 * k), 0, 0);   // past the history: 0
 }
-template <int KPRE>
-__device__ __forceinline__ void fir_f32_put(float* wl, const F32Win<KPRE>& w) {
+template <int KPRE, bool LONG>
+__device__ __forceinline__ void fir_f32_put(float* wl, const F32Win<KPRE, LONG>& w) {
 #pragma unroll
   for (int k = 0; k < KPRE; ++k)
-    wl[wpos(k * kBlock)] = __builtin_bit_cast(float, k < KPRE - 8 ? (w.x[k] | w.h[k < KPRE - 8 ? k : 0]) : w.x[k]);
+    wl[wpos(k * kBlock)] = __builtin_bit_cast(float, k < w.kH ? (w.x[k] | w.h[k < w.kH ? k : 0]) : w.x[k]);
 }
 
 // Items per workgroup.  Workgroups of identical work started together finish together, so with
@@ -188,38 +192,60 @@ struct FirOut {
 #ifndef MI355X_FIR_F32_WAVES
 #define MI355X_FIR_F32_WAVES 8     // minimum waves per SIMD the register allocation must allow
 #endif
-template <int KPRE>
-__global__ __launch_bounds__(kBlock, MI355X_FIR_F32_WAVES) void fir_f32_kernel(const float* __restrict__ coeffs, int T,
-                                                         const float* __restrict__ src, float* __restrict__ dst,
-                                                         uint32_t B, const float* __restrict__ hist_in,
-                                                         uint32_t nchunks, uint32_t items, uint32_t ipw,
-                                                         FirIn in, FirOut fo) {
+// Long filters (numTaps > kFirSeg) run in tap segments of kFirSeg: a work unit is (item,
+// segment), the accumulators stay in registers from a unit with segment 0 to the one with the
+// last segment, so every output still sums its products k = 0, 1, .., numTaps - 1 in order.
+constexpr int kFirSeg = kFirMaxTaps;
+struct FirUnit {
+  FirItem it;
+  int Ts;              // taps in this segment
+  bool first, last;    // first / last segment of the item
+};
+template <bool LONG>
+__device__ __forceinline__ FirUnit fir_unit(uint32_t u, uint32_t nseg, uint32_t nchunks, uint32_t B, int T) {
+  FirUnit x;
+  const uint32_t item = LONG ? u / nseg : u;
+  const int seg = LONG ? (int)(u - item * nseg) : 0;
+  x.it = fir_item(item, nchunks, B, T - 1, kF32Chunk);
+  x.it.a = seg * kFirSeg;
+  x.Ts = LONG ? min(T - x.it.a, kFirSeg) : T;
+  x.first = seg == 0;
+  x.last = !LONG || seg == (int)nseg - 1;
+  return x;
+}
+template <int KPRE, bool LONG>
+__global__ __launch_bounds__(kBlock, LONG ? 6 : MI355X_FIR_F32_WAVES) void fir_f32_kernel(
+    const float* __restrict__ coeffs, int T, const float* __restrict__ src, float* __restrict__ dst, uint32_t B,
+    const float* __restrict__ hist_in, uint32_t nchunks, uint32_t items, uint32_t ipw, FirIn in, FirOut fo) {
   constexpr int kWin = KPRE * kBlock;
   __shared__ __attribute__((aligned(16))) float win[wpos(kWin) + 16];
   const int T1 = T - 1;
   const uint32_t i0 = blockIdx.x * ipw;
   if (i0 >= items) return;
-  const uint32_t i1 = min(items, i0 + ipw);
+  const uint32_t nseg = LONG ? (uint32_t)((T + kFirSeg - 1) / kFirSeg) : 1u;
+  const uint32_t u0 = i0 * nseg, u1 = min(items, i0 + ipw) * nseg;
   const int tid = threadIdx.x;
-  const int rounds = T >> 3;
   const int base = tid * kF32R;                     // local output index of this lane
   float* wl = win + wpos(tid);                      // wpos(tid + 256 k) = wpos(tid) + 320 k
-  F32Win<KPRE> pre;
-  FirItem cur = fir_item(i0, nchunks, B, T1, kF32Chunk);
-  fir_f32_fetch<KPRE>(pre, cur, src, hist_in, in, T1, tid);
-  fir_f32_put<KPRE>(wl, pre);
-  // Per item: barrier (window ready) -> next window's loads -> MACs -> barrier (window free)
+  F32Win<KPRE, LONG> pre;
+  FirUnit cur = fir_unit<LONG>(u0, nseg, nchunks, B, T);
+  fir_f32_fetch<KPRE, LONG>(pre, cur.it, src, hist_in, in, T1, tid);
+  fir_f32_put<KPRE, LONG>(wl, pre);
+  float acc[8];
+  // Per unit: barrier (window ready) -> next window's loads -> MACs -> barrier (window free)
   // -> next window to LDS -> output stores.  The window write waits only for loads that had a
-  // whole item of MACs to land; the stores are issued after it, so no wait ever covers them.
-  for (uint32_t item = i0;;) {
+  // whole unit of MACs to land; the stores are issued after it, so no wait ever covers them.
+  for (uint32_t u = u0;;) {
     __syncthreads();
-    const bool more = item + 1 < i1;
-    const FirItem nxt = more ? fir_item(item + 1, nchunks, B, T1, kF32Chunk) : cur;
-    if (more) fir_f32_fetch<KPRE>(pre, nxt, src, hist_in, in, T1, tid);
-    float acc[8];
-    if (base < cur.count) {
+    const bool more = u + 1 < u1;
+    const FirUnit nxt = more ? fir_unit<LONG>(u + 1, nseg, nchunks, B, T) : cur;
+    if (more) fir_f32_fetch<KPRE, LONG>(pre, nxt.it, src, hist_in, in, T1, tid);
+    if (base < cur.it.count) {
+      if (cur.first) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) acc[r] = 0.0f;
+        for (int r = 0; r < 8; ++r) acc[r] = 0.0f;
+      }
+      const int Ts = cur.Ts, rounds = Ts >> 3;
       F32Grp X0, X1, X2, X3;
       float c0[8], c1[8];
       // Four group buffers rotate by name over a block of four rounds; the window pointer
@@ -227,7 +253,7 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_F32_WAVES) void fir_f32_kernel(c
       // wave-uniform: scalar loads (s_load_dwordx8 per round) into SGPRs, the v_mul operand
       // (no VGPRs, no LDS reads).
       const float* wp = win + 10 * tid;
-      const float* const ci = coeffs + cur.f * in.cstride;
+      const float* const ci = coeffs + cur.it.f * in.cstride + cur.it.a;
       const float* cp = ci;
       ld_grp(X0, wp, 0);
       ld_grp(X1, wp, 1);
@@ -267,7 +293,7 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_F32_WAVES) void fir_f32_kernel(c
         }
       }
       // numTaps % 8 tail taps, straight from LDS
-      for (int k = 8 * rounds; k < T; ++k) {
+      for (int k = 8 * rounds; k < Ts; ++k) {
         const float c = ci[k];
 #pragma unroll
         for (int r = 0; r < 8; ++r) acc[r] = acc[r] + win[wpos(base + k + r)] * c;
@@ -275,33 +301,34 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_F32_WAVES) void fir_f32_kernel(c
     }
     if (more) {
       __syncthreads();                              // every wave is done reading this window
-      fir_f32_put<KPRE>(wl, pre);
+      fir_f32_put<KPRE, LONG>(wl, pre);
     }
-    if (base < cur.count) {
+    if (cur.last && base < cur.it.count) {
+      const FirItem& it = cur.it;
       const bool run = fo.M == 1 && fo.L == 1 && fo.dir == 1;
       if (run) {                                    // contiguous outputs
-        float* o = dst + cur.f * fo.per_filter + fo.off + cur.n0 + base;
-        if (((fo.per_filter | (uint64_t)fo.off) & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + 8 <= cur.count) {
+        float* o = dst + it.f * fo.per_filter + fo.off + it.n0 + base;
+        if (((fo.per_filter | (uint64_t)fo.off) & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + 8 <= it.count) {
           reinterpret_cast<float4*>(o)[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
           reinterpret_cast<float4*>(o)[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
         } else {
 #pragma unroll
           for (int r = 0; r < 8; ++r)
-            if (base + r < cur.count) o[r] = acc[r];
+            if (base + r < it.count) o[r] = acc[r];
         }
       } else {                                      // decimator / reversed runs
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-          const uint32_t n = (uint32_t)(cur.n0 + base + r);
-          if (base + r < cur.count && n % fo.M == 0)
-            dst[(int64_t)(cur.f * fo.per_filter) + fo.off + (int64_t)fo.dir * ((int64_t)(n / fo.M) * fo.L + fo.q)] =
+          const uint32_t n = (uint32_t)(it.n0 + base + r);
+          if (base + r < it.count && n % fo.M == 0)
+            dst[(int64_t)(it.f * fo.per_filter) + fo.off + (int64_t)fo.dir * ((int64_t)(n / fo.M) * fo.L + fo.q)] =
                 acc[r];
         }
       }
     }
     if (!more) break;
     cur = nxt;
-    ++item;
+    ++u;
   }
 }
 
@@ -484,7 +511,10 @@ __device__ __forceinline__ void fir_q15_fast(const uint32_t* lds, const uint32_t
 // __SMLADX and plain int32 adds (none.h) -- every partial sum wraps mod 2^32, so the result
 // is the mod-2^32 sum of the products in ANY order: one accumulating v_dot2 per tap pair on
 // the raw sample-pair words (planes 0/1 = even/odd pairs), y = __SSAT(acc >> 15, 16).
-template <bool FAST>
+// numTaps > kFirMaxTaps: the window and the tap pairs are staged per segment of kFirMaxTaps
+// taps (an even count, so pairs never straddle segments) and the segment sums are added in
+// int64 (the reference's accumulator is one q63 sum of the pair sums: order-free).
+template <bool FAST, bool LONG>
 __global__ __launch_bounds__(kBlock, MI355X_FIR_Q15_WAVES) void fir_q15_kernel(const int16_t* __restrict__ coeffs, int T,
                                                          const int16_t* __restrict__ src, int16_t* __restrict__ dst,
                                                          uint32_t B, const int16_t* __restrict__ hist_in,
@@ -494,71 +524,90 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_Q15_WAVES) void fir_q15_kernel(c
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cw = reinterpret_cast<uint32_t*>(cw4);
   const int T1 = T - 1;
-  const int pairs = T >> 1;
-  const FirItem it = fir_item(blockIdx.x, nchunks, B, T1);
-  // staging: every load of this thread is issued before the first LDS write
-  const int words = min((it.total + 1) / 2 + 12, kQ15W);
-  constexpr int kPer = (kQ15W + kBlock - 1) / kBlock;
-  uint32_t x[kPer][3];
+  const FirItem it0 = fir_item(blockIdx.x, nchunks, B, T1);
+  const int base = threadIdx.x * kFirR;
+  const bool active = base < it0.count;
+  int64_t tot[kFirR];
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int j = threadIdx.x + k * kBlock;
+  for (int r = 0; r < kFirR; ++r) tot[r] = 0;
+  for (int a = 0; a < (LONG ? T : 1); a += kFirMaxTaps) {   // !LONG: one pass, T <= kFirMaxTaps
+    const int Ts = LONG ? min(T - a, kFirMaxTaps) : T;
+    FirItem it = it0;
+    it.a = a;
+    it.total = it.count + Ts - 1;
+    if (LONG && a) __syncthreads();                          // the previous segment is done with LDS
+    // staging: every load of this thread is issued before the first LDS write
+    const int words = min((it.total + 1) / 2 + 12, kQ15W);
+    constexpr int kPer = (kQ15W + kBlock - 1) / kBlock;
+    uint32_t x[kPer][3];
 #pragma unroll
-    for (int h = 0; h < 3; ++h) {
-      const int i = 2 * j + h;
-      x[k][h] = (uint16_t)fir_sample(hist_in, src, it, B, T1, i);
-    }
-  }
+    for (int k = 0; k < kPer; ++k) {
+      const int j = threadIdx.x + k * kBlock;
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int j = threadIdx.x + k * kBlock;
-    if (j < words) {
-      const uint32_t e = x[k][0] | (x[k][1] << 16), o = x[k][1] | (x[k][2] << 16);
-      if constexpr (FAST) {
-        lds[j] = e;
-        lds[kQ15W + j] = o;
-      } else {
-        lds[j] = hi8(e);
-        lds[kQ15W + j] = lo8(e);
-        lds[2 * kQ15W + j] = hi8(o);
-        lds[3 * kQ15W + j] = lo8(o);
+      for (int h = 0; h < 3; ++h) {
+        const int i = 2 * j + h;
+        x[k][h] = (uint16_t)fir_sample(hist_in, src, it, B, T1, i);
       }
     }
-  }
-  int wrap = 0;
-  for (int m = threadIdx.x; m < pairs; m += kBlock) {
-    const uint32_t c = (uint32_t)(uint16_t)coeffs[2 * m] | ((uint32_t)(uint16_t)coeffs[2 * m + 1] << 16);
-    cw[m] = c;
-    wrap |= c == 0x80008000u;
-  }
-  const bool split = !__syncthreads_or(wrap);
-
-  const int base = threadIdx.x * kFirR;
-  if (base >= it.count) return;
-  int64_t acc[kFirR];
-  if constexpr (FAST) {
-    int32_t a32[kFirR];
-    fir_q15_fast(lds, cw, pairs, base >> 1, a32);
 #pragma unroll
-    for (int r = 0; r < kFirR; ++r) acc[r] = a32[r];  // (acc >> 15) of the int32 sum below
-  } else if (split && pairs <= kQ15Chunk) {
-    fir_q15_split<false>(lds, cw, pairs, base >> 1, acc);
-  } else if (split) {
-    fir_q15_split<true>(lds, cw, pairs, base >> 1, acc);
-  } else {
-    const int unrolled_end = (int)(B - (B & 3u));  // outputs before this use the pair-wrap path
-    fir_q15_wide(lds, cw, pairs, base >> 1, unrolled_end - (it.n0 + base), acc);
+    for (int k = 0; k < kPer; ++k) {
+      const int j = threadIdx.x + k * kBlock;
+      if (j < words) {
+        const uint32_t e = x[k][0] | (x[k][1] << 16), o = x[k][1] | (x[k][2] << 16);
+        if constexpr (FAST) {
+          lds[j] = e;
+          lds[kQ15W + j] = o;
+        } else {
+          lds[j] = hi8(e);
+          lds[kQ15W + j] = lo8(e);
+          lds[2 * kQ15W + j] = hi8(o);
+          lds[3 * kQ15W + j] = lo8(o);
+        }
+      }
+    }
+    const int pairs = Ts >> 1;
+    const int16_t* cs = coeffs + a;
+    int wrap = 0;
+    for (int m = threadIdx.x; m < pairs; m += kBlock) {
+      const uint32_t c = (uint32_t)(uint16_t)cs[2 * m] | ((uint32_t)(uint16_t)cs[2 * m + 1] << 16);
+      cw[m] = c;
+      wrap |= c == 0x80008000u;
+    }
+    const bool split = !__syncthreads_or(wrap);
+    if (active) {
+      int64_t acc[kFirR];
+      if constexpr (FAST) {
+        int32_t a32[kFirR];
+        fir_q15_fast(lds, cw, pairs, base >> 1, a32);
+#pragma unroll
+        for (int r = 0; r < kFirR; ++r) acc[r] = a32[r];
+      } else if (split && pairs <= kQ15Chunk) {
+        fir_q15_split<false>(lds, cw, pairs, base >> 1, acc);
+      } else if (split) {
+        fir_q15_split<true>(lds, cw, pairs, base >> 1, acc);
+      } else {
+        const int unrolled_end = (int)(B - (B & 3u));  // outputs before this use the pair-wrap path
+        fir_q15_wide(lds, cw, pairs, base >> 1, unrolled_end - (it.n0 + base), acc);
+      }
+#pragma unroll
+      for (int r = 0; r < kFirR; ++r) tot[r] += acc[r];
+    }
   }
+  if (!active) return;
   int16_t y[kFirR];
 #pragma unroll
-  for (int r = 0; r < kFirR; ++r) y[r] = (int16_t)ssat16((int32_t)(acc[r] >> 15));   // arm_fir_q15.c:674
-  int16_t* o = dst + (uint64_t)it.f * B + it.n0 + base;
-  if ((B & 7u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + kFirR <= it.count) {
+  for (int r = 0; r < kFirR; ++r) {
+    // FAST: the q31_t accumulator wraps mod 2^32 (acc >> 15 of the int32 sum)
+    const int64_t acc = FAST ? (int64_t)(int32_t)(uint32_t)(uint64_t)tot[r] : tot[r];
+    y[r] = (int16_t)ssat16((int32_t)(acc >> 15));   // arm_fir_q15.c:674
+  }
+  int16_t* o = dst + (uint64_t)it0.f * B + it0.n0 + base;
+  if ((B & 7u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + kFirR <= it0.count) {
     *reinterpret_cast<uint4*>(o) = *reinterpret_cast<const uint4*>(y);
   } else {
 #pragma unroll
     for (int r = 0; r < kFirR; ++r)
-      if (base + r < it.count) o[r] = y[r];
+      if (base + r < it0.count) o[r] = y[r];
   }
 }
 
@@ -569,67 +618,80 @@ __global__ __launch_bounds__(kBlock, MI355X_FIR_Q15_WAVES) void fir_q15_kernel(c
 // = acc + ((x*c + 2^31) >> 32) mod 2^32 (acc << 32 has a zero low word), y = (q31)(acc << 1).
 // Both accumulators only ever wrap (gcc x86-64 semantics of the reference build): the
 // results are mod-2^64 / mod-2^32 sums, the same in any order.  Structure as fir_f32.
-template <bool FAST>
+template <bool FAST, bool LONG>
 __global__ __launch_bounds__(kBlock) void fir_q31_kernel(const int32_t* __restrict__ coeffs, int T,
                                                          const int32_t* __restrict__ src, int32_t* __restrict__ dst,
                                                          uint32_t B, const int32_t* __restrict__ hist_in,
                                                          uint32_t nchunks) {
   __shared__ int32_t win[(kFirChunk + kFirMaxTaps) * 9 / 8 + 32];
   const int T1 = T - 1;
-  const FirItem it = fir_item(blockIdx.x, nchunks, B, T1);
-  int32_t pre[kFirPre];
-#pragma unroll
-  for (int k = 0; k < kFirPre; ++k) pre[k] = fir_sample(hist_in, src, it, B, T1, (int)threadIdx.x + k * kBlock);
-#pragma unroll
-  for (int k = 0; k < kFirPre; ++k) {
-    const int j = threadIdx.x + k * kBlock;
-    if (j < it.total) win[padx(j)] = pre[k];
-  }
-  __syncthreads();
+  const FirItem it0 = fir_item(blockIdx.x, nchunks, B, T1);
   const int base = threadIdx.x * kFirR;
-  if (base >= it.count) return;
+  const bool active = base < it0.count;
   using Acc = typename std::conditional<FAST, uint32_t, uint64_t>::type;
   Acc acc[kFirR];
-  int32_t w[kFirR];
+#pragma unroll
+  for (int r = 0; r < kFirR; ++r) acc[r] = 0;
   auto mac = [](Acc a, int32_t x, int32_t c) -> Acc {
     const int64_t p = (int64_t)x * c;
     if constexpr (FAST) return a + (uint32_t)((p + 0x80000000LL) >> 32);
     else return a + (uint64_t)p;
   };
+  // numTaps > kFirMaxTaps: one window per tap segment, the modular sums carried in registers
+  for (int a = 0; a < (LONG ? T : 1); a += kFirMaxTaps) {   // !LONG: one pass, T <= kFirMaxTaps
+    const int Ts = LONG ? min(T - a, kFirMaxTaps) : T;
+    FirItem it = it0;
+    it.a = a;
+    it.total = it.count + Ts - 1;
+    if (LONG && a) __syncthreads();
+    int32_t pre[kFirPre];
 #pragma unroll
-  for (int r = 0; r < kFirR; ++r) { acc[r] = 0; w[r] = win[padx(base + r)]; }
-  int k = 0;
-  for (; k + kFirR <= T; k += kFirR) {
+    for (int k = 0; k < kFirPre; ++k) pre[k] = fir_sample(hist_in, src, it, B, T1, (int)threadIdx.x + k * kBlock);
 #pragma unroll
-    for (int u = 0; u < kFirR; ++u) {
-      const int32_t c = coeffs[k + u];
+    for (int k = 0; k < kFirPre; ++k) {
+      const int j = threadIdx.x + k * kBlock;
+      if (j < it.total) win[padx(j)] = pre[k];
+    }
+    __syncthreads();
+    if (!active) continue;
+    const int32_t* cs = coeffs + a;
+    int32_t w[kFirR];
 #pragma unroll
-      for (int r = 0; r < kFirR; ++r) acc[r] = mac(acc[r], w[(r + u) % kFirR], c);
-      w[u] = win[padx(base + k + u + kFirR)];
+    for (int r = 0; r < kFirR; ++r) w[r] = win[padx(base + r)];
+    int k = 0;
+    for (; k + kFirR <= Ts; k += kFirR) {
+#pragma unroll
+      for (int u = 0; u < kFirR; ++u) {
+        const int32_t c = cs[k + u];
+#pragma unroll
+        for (int r = 0; r < kFirR; ++r) acc[r] = mac(acc[r], w[(r + u) % kFirR], c);
+        w[u] = win[padx(base + k + u + kFirR)];
+      }
+    }
+    for (; k < Ts; ++k) {
+      const int32_t c = cs[k];
+#pragma unroll
+      for (int r = 0; r < kFirR; ++r) acc[r] = mac(acc[r], w[r], c);
+#pragma unroll
+      for (int r = 0; r < kFirR - 1; ++r) w[r] = w[r + 1];
+      w[kFirR - 1] = win[padx(base + kFirR + k)];
     }
   }
-  for (; k < T; ++k) {
-    const int32_t c = coeffs[k];
-#pragma unroll
-    for (int r = 0; r < kFirR; ++r) acc[r] = mac(acc[r], w[r], c);
-#pragma unroll
-    for (int r = 0; r < kFirR - 1; ++r) w[r] = w[r + 1];
-    w[kFirR - 1] = win[padx(base + kFirR + k)];
-  }
+  if (!active) return;
   int32_t y[kFirR];
 #pragma unroll
   for (int r = 0; r < kFirR; ++r) {
     if constexpr (FAST) y[r] = (int32_t)(acc[r] << 1);
     else y[r] = (int32_t)((int64_t)acc[r] >> 31);
   }
-  int32_t* o = dst + (uint64_t)it.f * B + it.n0 + base;
-  if ((B & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + kFirR <= it.count) {
+  int32_t* o = dst + (uint64_t)it0.f * B + it0.n0 + base;
+  if ((B & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + kFirR <= it0.count) {
     reinterpret_cast<int4*>(o)[0] = make_int4(y[0], y[1], y[2], y[3]);
     reinterpret_cast<int4*>(o)[1] = make_int4(y[4], y[5], y[6], y[7]);
   } else {
 #pragma unroll
     for (int r = 0; r < kFirR; ++r)
-      if (base + r < it.count) o[r] = y[r];
+      if (base + r < it0.count) o[r] = y[r];
   }
 }
 
@@ -666,6 +728,7 @@ __device__ __forceinline__ void q7_block(Q7Ring& r, const uint32_t* lds, int w_a
   }
 }
 
+template <bool LONG>
 __global__ __launch_bounds__(kBlock) void fir_q7_kernel(const int8_t* __restrict__ coeffs, int T,
                                                         const int8_t* __restrict__ src, int8_t* __restrict__ dst,
                                                         uint32_t B, const int8_t* __restrict__ hist_in,
@@ -676,74 +739,85 @@ __global__ __launch_bounds__(kBlock) void fir_q7_kernel(const int8_t* __restrict
   uint32_t* lds = reinterpret_cast<uint32_t*>(planes2);
   uint32_t* cq = reinterpret_cast<uint32_t*>(cq2);
   const int T1 = T - 1;
-  const int quads = (T + 3) >> 2;
-  const FirItem it = fir_item(blockIdx.x, nchunks, B, T1);
-  const int nw = kFirChunk / 4 + quads + 1;        // plane words any lane reads (<= kQ7W)
-  for (int i = threadIdx.x; i <= nw; i += kBlock) {
-    uint32_t w = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) w |= (uint32_t)(uint8_t)fir_sample(hist_in, src, it, B, T1, 4 * i + b) << (8 * b);
-    wq[i] = w;
-  }
-  for (int m = threadIdx.x; m < 2 * ((quads + 1) >> 1); m += kBlock) {
-    uint32_t w = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int k = 4 * m + b;
-      w |= k < T ? (uint32_t)(uint8_t)coeffs[k] << (8 * b) : 0u;
-    }
-    cq[m] = w;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < nw; i += kBlock) {
-    const uint32_t a = wq[i], b = wq[i + 1];
-    lds[i] = a;
-    lds[kQ7W + i] = __builtin_amdgcn_alignbyte(b, a, 1);
-    lds[2 * kQ7W + i] = __builtin_amdgcn_alignbyte(b, a, 2);
-    lds[3 * kQ7W + i] = __builtin_amdgcn_alignbyte(b, a, 3);
-  }
-  __syncthreads();
+  const FirItem it0 = fir_item(blockIdx.x, nchunks, B, T1);
   const int base = threadIdx.x * kFirR;
-  if (base >= it.count) return;
+  const bool active = base < it0.count;
   const int wb = base >> 2;
   int32_t A[kFirR];
 #pragma unroll
   for (int r = 0; r < kFirR; ++r) A[r] = 0;
-  Q7Ring ring;
-  q7_fetch<0>(ring, lds, wb);
-  q7_fetch<1>(ring, lds, wb + 2);
-  int m = 0;
-  for (; m + 6 <= quads; m += 6) {
-    q7_block<0>(ring, lds, wb + m + 4, cq2[m / 2], A);
-    q7_block<1>(ring, lds, wb + m + 6, cq2[m / 2 + 1], A);
-    q7_block<2>(ring, lds, wb + m + 8, cq2[m / 2 + 2], A);
-  }
-  if (m + 2 <= quads) {
-    q7_block<0>(ring, lds, wb + m + 4, cq2[m / 2], A);
-    m += 2;
+  // numTaps > kFirMaxTaps: one window per tap segment, the modular int32 sums carried on
+  for (int a = 0; a < (LONG ? T : 1); a += kFirMaxTaps) {   // !LONG: one pass, T <= kFirMaxTaps
+    const int Ts = LONG ? min(T - a, kFirMaxTaps) : T;
+    FirItem it = it0;
+    it.a = a;
+    it.total = it.count + Ts - 1;
+    const int quads = (Ts + 3) >> 2;
+    const int nw = kFirChunk / 4 + quads + 1;      // plane words any lane reads (<= kQ7W)
+    if (LONG && a) __syncthreads();
+    for (int i = threadIdx.x; i <= nw; i += kBlock) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) w |= (uint32_t)(uint8_t)fir_sample(hist_in, src, it, B, T1, 4 * i + b) << (8 * b);
+      wq[i] = w;
+    }
+    const int8_t* cs = coeffs + a;
+    for (int m = threadIdx.x; m < 2 * ((quads + 1) >> 1); m += kBlock) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int k = 4 * m + b;
+        w |= k < Ts ? (uint32_t)(uint8_t)cs[k] << (8 * b) : 0u;
+      }
+      cq[m] = w;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nw; i += kBlock) {
+      const uint32_t a0 = wq[i], b0 = wq[i + 1];
+      lds[i] = a0;
+      lds[kQ7W + i] = __builtin_amdgcn_alignbyte(b0, a0, 1);
+      lds[2 * kQ7W + i] = __builtin_amdgcn_alignbyte(b0, a0, 2);
+      lds[3 * kQ7W + i] = __builtin_amdgcn_alignbyte(b0, a0, 3);
+    }
+    __syncthreads();
+    if (!active) continue;
+    Q7Ring ring;
+    q7_fetch<0>(ring, lds, wb);
+    q7_fetch<1>(ring, lds, wb + 2);
+    int m = 0;
+    for (; m + 6 <= quads; m += 6) {
+      q7_block<0>(ring, lds, wb + m + 4, cq2[m / 2], A);
+      q7_block<1>(ring, lds, wb + m + 6, cq2[m / 2 + 1], A);
+      q7_block<2>(ring, lds, wb + m + 8, cq2[m / 2 + 2], A);
+    }
     if (m + 2 <= quads) {
-      q7_block<1>(ring, lds, wb + m + 4, cq2[m / 2], A);
+      q7_block<0>(ring, lds, wb + m + 4, cq2[m / 2], A);
       m += 2;
+      if (m + 2 <= quads) {
+        q7_block<1>(ring, lds, wb + m + 4, cq2[m / 2], A);
+        m += 2;
+      }
+    }
+    if (m < quads) {                                  // odd quad count: the last one from LDS
+      const uint32_t c = cq[m];
+#pragma unroll
+      for (int r = 0; r < kFirR; ++r) A[r] = dot4(lds[(r & 3) * kQ7W + wb + (r >> 2) + m], c, A[r]);
     }
   }
-  if (m < quads) {                                  // odd quad count: the last one from LDS
-    const uint32_t c = cq[m];
-#pragma unroll
-    for (int r = 0; r < kFirR; ++r) A[r] = dot4(lds[(r & 3) * kQ7W + wb + (r >> 2) + m], c, A[r]);
-  }
+  if (!active) return;
   int8_t y[kFirR];
 #pragma unroll
   for (int r = 0; r < kFirR; ++r) {
     const int32_t v = A[r] >> 7;
     y[r] = (int8_t)(v > 127 ? 127 : v < -128 ? -128 : v);                   // arm_fir_q7.c:530
   }
-  int8_t* o = dst + (uint64_t)it.f * B + it.n0 + base;
-  if ((B & 7u) == 0 && ((uintptr_t)dst & 7u) == 0 && base + kFirR <= it.count) {
+  int8_t* o = dst + (uint64_t)it0.f * B + it0.n0 + base;
+  if ((B & 7u) == 0 && ((uintptr_t)dst & 7u) == 0 && base + kFirR <= it0.count) {
     *reinterpret_cast<uint2*>(o) = *reinterpret_cast<const uint2*>(y);
   } else {
 #pragma unroll
     for (int r = 0; r < kFirR; ++r)
-      if (base + r < it.count) o[r] = y[r];
+      if (base + r < it0.count) o[r] = y[r];
   }
 }
 
@@ -766,10 +840,13 @@ static void fir_f32_pass(const float* coeffs, int T, const float* src, float* ds
                          const float* hist_in, FirIn in, FirOut fo, hipStream_t st) {
   const uint32_t nchunks = (B + kF32Chunk - 1) / kF32Chunk;
   const uint32_t items = nchunks * batch;
-  const int kpre = fir_f32_kpre(T);
-  auto k = kpre <= 9 ? fir_f32_kernel<9> : kpre == 10 ? fir_f32_kernel<10> : kpre == 11 ? fir_f32_kernel<11>
-         : kpre == 12 ? fir_f32_kernel<12> : fir_f32_kernel<13>;
+  const int kpre = fir_f32_kpre(T < kFirSeg ? T : kFirSeg);
+  auto k = T > kFirSeg ? fir_f32_kernel<fir_f32_kpre(kFirSeg), true>
+         : kpre <= 9 ? fir_f32_kernel<9, false> : kpre == 10 ? fir_f32_kernel<10, false>
+         : kpre == 11 ? fir_f32_kernel<11, false> : kpre == 12 ? fir_f32_kernel<12, false>
+         : fir_f32_kernel<13, false>;
   uint32_t ipw = MI355X_FIR_IPW;
+  if (T > kFirSeg) ipw = 1;                         // a long item is already many units
   if (!ipw) {
     const uint32_t resident = (uint32_t)persistent_grid((const void*)k, kBlock, 0, items);
     ipw = (items + resident - 1) / resident;
@@ -796,7 +873,7 @@ template <typename T>
 static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T* dst, uint32_t B, uint32_t batch,
                              T* hist, hipStream_t st) {
   if (batch == 0 || B == 0) return hipSuccess;
-  if (T_ < 1 || T_ > kFirMaxTaps) return hipErrorInvalidValue;
+  if (T_ < 1) return hipErrorInvalidValue;        // numTaps > kFirMaxTaps: tap segments
   const int T1 = T_ - 1;
   const int chunk = kind == kFirF32 ? kF32Chunk : kFirChunk;
   const uint32_t nchunks = (B + chunk - 1) / chunk;
@@ -837,18 +914,20 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
     }
     case kFirQ15:
     case kFirFastQ15: {
-      auto k = kind == kFirQ15 ? fir_q15_kernel<false> : fir_q15_kernel<true>;
+      auto k = kind == kFirQ15 ? (T_ > kFirMaxTaps ? fir_q15_kernel<false, true> : fir_q15_kernel<false, false>)
+                               : (T_ > kFirMaxTaps ? fir_q15_kernel<true, true> : fir_q15_kernel<true, false>);
       hipLaunchKernelGGL(k, dim3(items), dim3(kBlock), 0, st, (const int16_t*)coeffs, T_, (const int16_t*)src,
                          (int16_t*)dst, B, (const int16_t*)hist_in, nchunks);
       break;
     }
     case kFirQ7: {
-      hipLaunchKernelGGL(fir_q7_kernel, dim3(items), dim3(kBlock), 0, st, (const int8_t*)coeffs, T_,
+      hipLaunchKernelGGL(T_ > kFirMaxTaps ? fir_q7_kernel<true> : fir_q7_kernel<false>, dim3(items), dim3(kBlock), 0, st, (const int8_t*)coeffs, T_,
                          (const int8_t*)src, (int8_t*)dst, B, (const int8_t*)hist_in, nchunks);
       break;
     }
     default: {
-      auto k = kind == kFirQ31 ? fir_q31_kernel<false> : fir_q31_kernel<true>;
+      auto k = kind == kFirQ31 ? (T_ > kFirMaxTaps ? fir_q31_kernel<false, true> : fir_q31_kernel<false, false>)
+                               : (T_ > kFirMaxTaps ? fir_q31_kernel<true, true> : fir_q31_kernel<true, false>);
       hipLaunchKernelGGL(k, dim3(items), dim3(kBlock), 0, st, (const int32_t*)coeffs, T_, (const int32_t*)src,
                          (int32_t*)dst, B, (const int32_t*)hist_in, nchunks);
     }
@@ -1110,6 +1189,30 @@ __global__ __launch_bounds__(kBlock) void fir_interp_phases4_kernel(const typena
   }
 }
 
+// Windows that do not fit the LDS image (decimator M (ceil(T / M) + 2) > kMrWin, interpolator
+// phaseLength > kMrWin - 256): one thread per output reading its window straight from HBM/L2,
+// taps ascending from a zero accumulator (the reference's order, arm_fir_decimate_f32.c /
+// arm_fir_interpolate_f32.c generic paths).  Decimator: output j of filter f = sum_t s[M j + t]
+// h[t]; interpolator (M = 1, phase stride L): output n L + q = sum_i s[n + i] h[(L-1-q) + i L].
+template <int OP>
+__global__ __launch_bounds__(kBlock) void fir_mr_direct_kernel(const typename MrT<OP>::T* __restrict__ h, int taps,
+                                                               int M, int L, const typename MrT<OP>::T* __restrict__ src,
+                                                               typename MrT<OP>::T* __restrict__ dst, uint32_t B,
+                                                               const typename MrT<OP>::T* __restrict__ hist_in, int H,
+                                                               uint32_t outs, uint32_t batch) {
+  using Op = MrT<OP>;
+  const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (g >= (uint64_t)batch * outs) return;
+  const uint32_t f = (uint32_t)(g / outs), o = (uint32_t)(g - (uint64_t)f * outs);
+  const uint32_t n = o / (uint32_t)L, q = o - n * (uint32_t)L;   // decimator: L = 1, q = 0
+  FirItem it;
+  it.f = f; it.n0 = (int)(M * n); it.count = 1; it.total = taps;
+  typename Op::Acc acc = 0;
+  const typename MrT<OP>::T* hq = h + (L - 1 - (int)q);
+  for (int i = 0; i < taps; ++i) acc = Op::mac(acc, fir_sample(hist_in, src, it, B, H, i), hq[(size_t)i * L]);
+  dst[g] = Op::out(acc);
+}
+
 // h_q[i] = h[(L-1-q) + i L]: the interpolator's phases as contiguous coefficient rows
 template <typename E>
 __global__ void mr_phase_coeffs_kernel(const E* __restrict__ h, E* __restrict__ hq, int L, int P) {
@@ -1178,7 +1281,19 @@ static hipError_t decimate_launch(const void* coeffs, int T, int M, const void* 
   const int outs = (int)(B / (uint32_t)M);
   const int per_phase = (T + M - 1) / M;
   int J = kMrWin / M - per_phase - 1;               // M * (J + per_phase + 1) <= kMrWin
-  if (J < 1) return hipErrorInvalidValue;
+  if (J < 1) {                                      // window past the LDS image: direct kernel
+    const uint64_t n = (uint64_t)batch * outs;
+    if (n == 0) return mr_launch<E>((const E*)src, (E*)dst, 0, B, batch, (E*)hist, T - 1, (uint32_t)(outs * M), st,
+                                    [&](const E*, const E*) { return hipSuccess; });
+    if ((n + kBlock - 1) / kBlock > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    return mr_launch<E>((const E*)src, (E*)dst, (size_t)n, B, batch, (E*)hist, T - 1, (uint32_t)(outs * M), st,
+                        [&](const E* s, const E* h) {
+                          hipLaunchKernelGGL(fir_mr_direct_kernel<OP>, dim3((uint32_t)((n + kBlock - 1) / kBlock)),
+                                             dim3(kBlock), 0, st, (const E*)coeffs, T, M, 1, s, (E*)dst, B, h, T - 1,
+                                             (uint32_t)outs, batch);
+                          return hipSuccess;
+                        });
+  }
   J = J >= 2 * kBlock ? 4 * kBlock < J ? 4 * kBlock : (J / kBlock) * kBlock : J;
   const int Wp = J + per_phase + 1;
   const uint32_t nchunks = outs > 0 ? (uint32_t)((outs + J - 1) / J) : 0;
@@ -1222,7 +1337,19 @@ static hipError_t interpolate_launch(const void* coeffs, int L, int P, const voi
                                      uint32_t batch, void* hist, hipStream_t st) {
   using E = typename MrT<OP>::T;
   if (batch == 0 || B == 0) return hipSuccess;
-  if (L < 1 || P < 1 || P > kMrWin - kBlock) return hipErrorInvalidValue;
+  if (L < 1 || P < 1) return hipErrorInvalidValue;
+  if (P > kMrWin - kBlock) {                        // window past the LDS image: direct kernel
+    const uint64_t n = (uint64_t)batch * B * (uint32_t)L;
+    if ((n + kBlock - 1) / kBlock > 0x7FFFFFFFull || (uint64_t)B * (uint32_t)L > 0xFFFFFFFFull)
+      return hipErrorInvalidValue;
+    return mr_launch<E>((const E*)src, (E*)dst, (size_t)n, B, batch, (E*)hist, P - 1, B, st,
+                        [&](const E* s, const E* h) {
+                          hipLaunchKernelGGL(fir_mr_direct_kernel<OP>, dim3((uint32_t)((n + kBlock - 1) / kBlock)),
+                                             dim3(kBlock), 0, st, (const E*)coeffs, P, 1, L, s, (E*)dst, B, h, P - 1,
+                                             (uint32_t)(B * (uint32_t)L), batch);
+                          return hipSuccess;
+                        });
+  }
   int N = kMrWin - (P - 1);
   constexpr int kR = interp_r<OP>();
   N = N >= kR * kBlock ? kR * kBlock : (N >= kBlock ? (N / kBlock) * kBlock : N);

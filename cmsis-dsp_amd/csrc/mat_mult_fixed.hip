@@ -26,12 +26,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef short s2x __attribute__((ext_vector_type(2)));
 
-constexpr int kMT = 64, kNT = 64, kKT = 64;     // workgroup tile: 4 waves of 32x32, K step 64
-constexpr int kRowB = kKT + 16;                  // LDS row pitch in bytes (k-contiguous rows)
 constexpr int kMatI8MaxK = 32704;
-#ifndef MI355X_MATI8_V1
-#define MI355X_MATI8_V1 0
-#endif
 
 template <typename T> struct Slices;
 template <> struct Slices<int16_t> { static constexpr int P = 2; static constexpr int64_t C0 = 128; };
@@ -45,125 +40,6 @@ __device__ __forceinline__ uint32_t plane4(uint32_t v0, uint32_t v1, uint32_t v2
   const uint32_t lo = __builtin_amdgcn_perm(v1, v0, sel), hi = __builtin_amdgcn_perm(v3, v2, sel);
   const uint32_t w = lo | (hi << 16);
   return p == P - 1 ? w : w ^ 0x80808080u;
-}
-
-// 16 consecutive elements of a row (zero past `valid`), as one raw dword per element.
-template <typename T>
-__device__ __forceinline__ void load_row16(const T* __restrict__ p, int valid, bool vec, uint32_t (&v)[16]) {
-  if (vec && valid >= 16) {
-    if constexpr (sizeof(T) == 2) {
-      const uint4 a = reinterpret_cast<const uint4*>(p)[0], b = reinterpret_cast<const uint4*>(p)[1];
-      const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-      for (int i = 0; i < 8; ++i) { v[2 * i] = (uint32_t)(int32_t)(int16_t)(d[i] & 0xffffu); v[2 * i + 1] = (uint32_t)((int32_t)d[i] >> 16); }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint4 a = reinterpret_cast<const uint4*>(p)[i];
-        v[4 * i] = a.x; v[4 * i + 1] = a.y; v[4 * i + 2] = a.z; v[4 * i + 3] = a.w;
-      }
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = j < valid ? (uint32_t)(int32_t)p[j] : 0u;
-  }
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void mat_mult_i8_kernel(const T* __restrict__ A, const T* __restrict__ B,
-                                                          T* __restrict__ C, int M, int K, int N) {
-  constexpr int P = Slices<T>::P, S = 2 * P - 1;
-  constexpr int64_t C0 = Slices<T>::C0;
-  __shared__ __attribute__((aligned(16))) int8_t As[P][kMT][kRowB];
-  __shared__ __attribute__((aligned(16))) int8_t Bs[P][kNT][kRowB];   // transposed: [col][k]
-  __shared__ int64_t rsum[4][kMT], csum[4][kNT];
-
-  const int tilesN = (N + kNT - 1) / kNT;
-  const int tm = blockIdx.x / tilesN, tn = blockIdx.x % tilesN;
-  const size_t bz = blockIdx.z;
-  A += bz * (size_t)M * K;
-  B += bz * (size_t)K * N;
-  C += bz * (size_t)M * N;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int row0 = tm * kMT, col0 = tn * kNT;
-
-  // staging roles: A row (tid>>2), k sub-range 16*(tid&3); B column (tid&63), k sub-range 16*(tid>>6)
-  const int ar = tid >> 2, ak = 16 * (tid & 3);
-  const int bc = tid & 63, bk = 16 * (tid >> 6);
-  const int gr = row0 + ar, gc = col0 + bc;
-  const bool vec = ((K * (int)sizeof(T)) % 16) == 0 && (((uintptr_t)A) & 15) == 0;
-  int64_t my_rsum = 0, my_csum = 0;
-
-  i32x16 acc[S];
-#pragma unroll
-  for (int s = 0; s < S; ++s) acc[s] = i32x16{};
-  const int wm = wid >> 1, wn = wid & 1;
-  const int r = lane & 31, h = lane >> 5;
-
-  const int nk = (K + kKT - 1) / kKT;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int k0 = kt * kKT;
-    uint32_t av[16], bv[16];
-    load_row16<T>(A + (size_t)gr * K + k0 + ak, gr < M ? K - (k0 + ak) : 0, vec, av);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int kb = k0 + bk + j;
-      bv[j] = (gc < N && kb < K) ? (uint32_t)(int32_t)B[(size_t)kb * N + gc] : 0u;
-    }
-    __syncthreads();                     // the previous step's fragments are consumed
-    int64_t ra = 0, cb = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) { ra += (int32_t)av[j]; cb += (int32_t)bv[j]; }
-    my_rsum += ra;
-    my_csum += cb;
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      uint4 pa, pb;
-      pa.x = plane4<P>(av[0], av[1], av[2], av[3], p);     pb.x = plane4<P>(bv[0], bv[1], bv[2], bv[3], p);
-      pa.y = plane4<P>(av[4], av[5], av[6], av[7], p);     pb.y = plane4<P>(bv[4], bv[5], bv[6], bv[7], p);
-      pa.z = plane4<P>(av[8], av[9], av[10], av[11], p);   pb.z = plane4<P>(bv[8], bv[9], bv[10], bv[11], p);
-      pa.w = plane4<P>(av[12], av[13], av[14], av[15], p); pb.w = plane4<P>(bv[12], bv[13], bv[14], bv[15], p);
-      *reinterpret_cast<uint4*>(&As[p][ar][ak]) = pa;
-      *reinterpret_cast<uint4*>(&Bs[p][bc][bk]) = pb;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < kKT / 32; ++kk) {
-      i32x4 fa[P], fb[P];
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        fa[p] = *reinterpret_cast<const i32x4*>(&As[p][wm * 32 + r][32 * kk + 16 * h]);
-        fb[p] = *reinterpret_cast<const i32x4*>(&Bs[p][wn * 32 + r][32 * kk + 16 * h]);
-      }
-#pragma unroll
-      for (int p = 0; p < P; ++p)
-#pragma unroll
-        for (int q = 0; q < P; ++q) acc[p + q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[p], fb[q], acc[p + q], 0, 0, 0);
-    }
-  }
-
-  // exact row / column sums of the original values
-  rsum[tid & 3][ar] = my_rsum;
-  csum[tid >> 6][bc] = my_csum;
-  __syncthreads();
-  const int64_t kpad = (int64_t)nk * kKT;   // padded k terms are zeros: the identity holds over kpad
-  const int cc = wn * 32 + r;
-  const int64_t cs = csum[0][cc] + csum[1][cc] + csum[2][cc] + csum[3][cc];
-  const int gcol = col0 + cc;
-#pragma unroll
-  for (int reg = 0; reg < 16; ++reg) {
-    const int rr = wm * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-    const int grow = row0 + rr;
-    const int64_t rs = rsum[0][rr] + rsum[1][rr] + rsum[2][rr] + rsum[3][rr];
-    uint64_t v = (uint64_t)(C0 * (rs + cs)) - (uint64_t)kpad * (uint64_t)(C0 * C0);
-#pragma unroll
-    for (int s = 0; s < S; ++s) v += (uint64_t)(int64_t)acc[s][reg] << (8 * s);
-    if (grow < M && gcol < N) {
-      const int64_t sum = (int64_t)v;
-      if constexpr (sizeof(T) == 2) C[(size_t)grow * N + gcol] = (T)ssat16((int32_t)(sum >> 15));
-      else C[(size_t)grow * N + gcol] = (T)(int32_t)(sum >> 31);
-    }
-  }
 }
 
 // ---- v2 kernel: 128 x 128 (q15) / 128 x 64 (q31) workgroup tiles of 8 waves (4 x 2), wave
@@ -474,11 +350,7 @@ static hipError_t launch_fixed(int m, int k, int n, const T* a, const T* b, T* c
                                int fast = 0) {
   if (batch == 0 || m == 0 || n == 0) return hipSuccess;
   if (k == 0) return hipMemsetAsync(c, 0, sizeof(T) * (size_t)m * n * batch, st);
-  if (k <= kMatI8MaxK && !(MI355X_MATI8_V1 && fast)) {
-#if MI355X_MATI8_V1
-    const int tiles = ((m + kMT - 1) / kMT) * ((n + kNT - 1) / kNT);
-    hipLaunchKernelGGL(mat_mult_i8_kernel<T>, dim3(tiles, 1, batch), dim3(256), 0, st, a, b, c, m, k, n);
-#else
+  if (k <= kMatI8MaxK) {
     using G = I8Cfg<T>;
     const int tiles = ((m + G::BM - 1) / G::BM) * ((n + G::BN - 1) / G::BN);
     const bool full = m % G::BM == 0 && n % G::BN == 0 && k % G::KT == 0 &&
@@ -490,7 +362,6 @@ static hipError_t launch_fixed(int m, int k, int n, const T* a, const T* b, T* c
     else
       hipLaunchKernelGGL((mat_mult_i8v2_kernel<T, false>), dim3(tiles * batch), dim3(kNT2), 0, st, a, b, c, m, k, n,
                          fast);
-#endif
   } else {
     hipLaunchKernelGGL(mat_mult_fixed_valu_kernel<T>, dim3((n + 255) / 256, m, batch), dim3(256), 0, st, a, b, c,
                        m, k, n, fast);

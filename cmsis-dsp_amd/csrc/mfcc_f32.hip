@@ -35,9 +35,6 @@ constexpr int kMfccWaves = 4;   // frames (waves) per 256-thread workgroup
 #ifndef MI355X_MFCC_UNROLL
 #define MI355X_MFCC_UNROLL 8        // Mel / DCT dot products: loads issued 8 taps ahead
 #endif
-#ifndef MI355X_MFCC_SKIP_TAIL
-#define MI355X_MFCC_SKIP_TAIL 0     // diagnostic only: stop after the spectrum (no Mel/log/DCT)
-#endif
 
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
@@ -241,10 +238,6 @@ __global__ __launch_bounds__(kBlock) void mfcc_fused_kernel(const float* __restr
 #pragma unroll
   for (int i = 0; i < KPL; ++i) mag[lane + i * LPT] = mg[i];
   __syncthreads();
-#if MI355X_MFCC_SKIP_TAIL
-  if (tr < valid && lane == 0) dst[(f0 + tr) * (uint64_t)nb_dct] = mag[1] + mag[H - 1];
-  return;
-#endif
   for (int i = lane; i < nb_mel; i += LPT) {
     const uint32_t p = pos[i], l = len[i];
     const float* c = cbase + off[i];

@@ -22,8 +22,37 @@ std::mutex g_table_mu;
 std::map<std::tuple<int, const void*, size_t>, void*> g_tables;
 std::map<std::tuple<int, const void*, uint16_t, int, int>, std::pair<void*, bool>> g_perms;
 
-struct Blob { std::vector<uint8_t> host; void* dev = nullptr; };
+// Content-keyed blob cache, bounded: an LRU by bytes per process (default 256 MiB, set with
+// arm_mi355x_set_table_cache_limit).  Evicting synchronizes the device before hipFree, since
+// an asynchronous batched call may still be reading the blob on any stream.
+struct Blob { std::vector<uint8_t> host; void* dev = nullptr; int d = 0; uint64_t tick = 0; };
 std::map<std::tuple<int, uint64_t, size_t>, std::vector<Blob>> g_blobs;
+size_t g_blob_bytes = 0;
+size_t g_blob_limit = size_t(256) << 20;
+uint64_t g_blob_tick = 0;
+
+// evict least-recently-used blobs until `incoming` more bytes fit (caller holds g_table_mu)
+void blob_evict(size_t incoming) {
+  while (g_blob_bytes + incoming > g_blob_limit && g_blob_bytes > 0) {
+    auto victim_bucket = g_blobs.end();
+    size_t victim = 0;
+    uint64_t oldest = UINT64_MAX;
+    for (auto it = g_blobs.begin(); it != g_blobs.end(); ++it)
+      for (size_t i = 0; i < it->second.size(); ++i)
+        if (it->second[i].tick < oldest) { oldest = it->second[i].tick; victim_bucket = it; victim = i; }
+    if (victim_bucket == g_blobs.end()) break;
+    Blob& b = victim_bucket->second[victim];
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != b.d) (void)hipSetDevice(b.d);
+    (void)hipDeviceSynchronize();           // no kernel may still read it
+    (void)hipFree(b.dev);
+    if (prev != b.d) (void)hipSetDevice(prev);
+    g_blob_bytes -= b.host.size();
+    victim_bucket->second.erase(victim_bucket->second.begin() + (long)victim);
+    if (victim_bucket->second.empty()) g_blobs.erase(victim_bucket);
+  }
+}
 
 uint64_t fnv1a(const uint8_t* p, size_t n) {
   uint64_t h = 1469598103934665603ull;
@@ -108,11 +137,17 @@ const void* device_blob(const void* host, size_t bytes) {
   const int dev = cur_dev();
   const auto key = std::make_tuple(dev, fnv1a(h, bytes), bytes);
   std::lock_guard<std::mutex> lk(g_table_mu);
-  std::vector<Blob>& bucket = g_blobs[key];
-  for (const Blob& b : bucket)
-    if (memcmp(b.host.data(), h, bytes) == 0) return b.dev;
+  {
+    auto it = g_blobs.find(key);
+    if (it != g_blobs.end())
+      for (Blob& b : it->second)
+        if (memcmp(b.host.data(), h, bytes) == 0) { b.tick = ++g_blob_tick; return b.dev; }
+  }
+  blob_evict(bytes);
   Blob b;
   b.host.assign(h, h + bytes);
+  b.d = dev;
+  b.tick = ++g_blob_tick;
   hipError_t e = hipMalloc(&b.dev, bytes);
   if (e != hipSuccess) { set_error(e, "device_blob: hipMalloc"); return nullptr; }
   e = hipMemcpy(b.dev, h, bytes, hipMemcpyHostToDevice);
@@ -121,8 +156,20 @@ const void* device_blob(const void* host, size_t bytes) {
     (void)hipFree(b.dev);
     return nullptr;
   }
+  std::vector<Blob>& bucket = g_blobs[key];
   bucket.push_back(std::move(b));
+  g_blob_bytes += bytes;
   return bucket.back().dev;
+}
+
+size_t blob_cache_bytes() {
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  return g_blob_bytes;
+}
+void set_blob_cache_limit(size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  g_blob_limit = bytes;
+  blob_evict(0);
 }
 
 const uint16_t* device_perm(int n, const uint16_t* table, uint16_t len, int kind, bool* canonical, bool* ok) {
@@ -217,7 +264,14 @@ hipError_t HostIO::out(void* host, const void* dev, size_t bytes) {
   return e;
 }
 
+// A call that returns early after queueing a copy must not leave a DMA reading a pinned slot
+// that the next call overwrites (or frees, when it needs a larger one): drain the stream.
+HostIO::~HostIO() {
+  if (slot_ > 0 && !finished_) (void)hipStreamSynchronize(st_);
+}
+
 hipError_t HostIO::finish() {
+  finished_ = true;
   hipError_t e = hipStreamSynchronize(st_);
   if (e != hipSuccess) return e;
   for (int i = 0; i < nouts_; ++i) memcpy(outs_[i].host, outs_[i].pin, outs_[i].bytes);
@@ -240,5 +294,7 @@ hipStream_t sync_stream() {
 extern "C" {
 int arm_mi355x_last_error(void) { return mi355x::g_err; }
 const char* arm_mi355x_last_error_string(void) { return mi355x::g_err_msg.c_str(); }
+size_t arm_mi355x_table_cache_bytes(void) { return mi355x::blob_cache_bytes(); }
+void arm_mi355x_set_table_cache_limit(size_t bytes) { mi355x::set_blob_cache_limit(bytes); }
 void arm_mi355x_clear_error(void) { mi355x::clear_error(); }
 }

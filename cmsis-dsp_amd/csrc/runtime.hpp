@@ -30,8 +30,13 @@ const void* device_table(const void* host, size_t bytes);
 
 // Device copy of a host byte blob, cached by CONTENT (hash + full compare): uploaded once
 // per distinct contents and device, immune to a caller reusing a buffer for new values.
-// Used for user-supplied coefficient tables (MFCC).  Returns nullptr on failure.
+// Used for user-supplied tables and coefficients (FIR taps, MFCC filterbanks, ...).  The
+// cache is an LRU bounded in bytes (blob_cache_bytes / set_blob_cache_limit): a caller that
+// changes coefficients on every call cycles through it instead of growing it.  Returns
+// nullptr on failure.
 const void* device_blob(const void* host, size_t bytes);
+size_t blob_cache_bytes();
+void set_blob_cache_limit(size_t bytes);
 
 // Device permutation implementing a bit-reversal swap table of a non-canonical instance.
 // *canonical is set when the table induces the reference's own permutation (then the
@@ -48,10 +53,14 @@ void* pinned(size_t bytes, int slot);
 // Host <-> device staging of one synchronous drop-in call: host words are copied into a
 // pinned bounce buffer and DMA'd from there (in), device results are DMA'd into a pinned
 // buffer and copied to the caller's memory after the stream has drained (finish).  One
-// pinned slot per transfer; every call ends with finish(), so slots are free again.
+// pinned slot per transfer; a call ends with finish(), or the destructor drains the stream
+// (error returns), so the slots are free again for the next call.
 class HostIO {
  public:
   explicit HostIO(hipStream_t st) : st_(st) {}
+  ~HostIO();
+  HostIO(const HostIO&) = delete;
+  HostIO& operator=(const HostIO&) = delete;
   hipError_t in(void* dev, const void* host, size_t bytes);
   hipError_t out(void* host, const void* dev, size_t bytes);
   hipError_t finish();
@@ -62,6 +71,7 @@ class HostIO {
   int slot_ = 0;
   Pending outs_[4];
   int nouts_ = 0;
+  bool finished_ = false;
 };
 
 // The internal stream used by the synchronous drop-in API on the current device.

@@ -12,8 +12,11 @@
  *     tolerance (arm_mat_mult_f32_batch, MFMA accumulation — DESIGN.md §mat_mult);
  *   - return ARM_MATH_SUCCESS, ARM_MATH_ARGUMENT_ERROR (unsupported length, NULL pointer,
  *     launch failure; details in arm_mi355x_last_error_string()).
- * Instance structs are the reference's own (arm_math.h); tables they point to are
- * uploaded once per device and cached by address, so they must stay immutable.
+ * Instance structs are the reference's own (arm_math.h).  Tables and coefficients they point
+ * to: a device pointer is used in place; the library's own CommonTables are uploaded once per
+ * device and cached by address; any other host table is cached by CONTENT (hash + compare) in
+ * an LRU bounded in bytes (arm_mi355x_set_table_cache_limit), so changing coefficients
+ * between calls is always seen and never grows device memory without bound.
  * Multi-GPU: either one process (or host thread) per device, each calling these on its
  * own shard with that device current (the library's caches, scratch and internal streams
  * are per device and per thread), or one call of the *_batch_multi entry points below,
@@ -235,7 +238,14 @@ int arm_mi355x_last_error(void);
 const char *arm_mi355x_last_error_string(void);
 void arm_mi355x_clear_error(void);
 
-/* Library identification: "cmsisdsp-mi355x <version> gfx950". */
+/* Device bytes held by the content-keyed cache of host tables / coefficients (all devices),
+ * and its limit (default 256 MiB; lowering it evicts least-recently-used entries now, after
+ * synchronizing the device they live on). */
+size_t arm_mi355x_table_cache_bytes(void);
+void arm_mi355x_set_table_cache_limit(size_t bytes);
+
+/* Library identification: "cmsisdsp-mi355x <version> gfx950", followed by " [macros]" when
+ * the library was built with any non-default tuning macro (bench lines print it). */
 const char *arm_mi355x_version(void);
 
 #ifdef __cplusplus

@@ -246,3 +246,47 @@ def test_dropin_pinned_staging_repeated_sizes(dsp, torch_gpu, ref):
     st, c = dsp.arm_mat_mult_f32(a, b)
     assert st == 0
     np.testing.assert_allclose(c, a.astype(np.float64) @ b.astype(np.float64), rtol=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------------------------ table cache bound
+def test_coefficient_cache_stays_bounded(dsp, torch_gpu, ref):
+    """Fresh coefficients on every call (a time-varying filter) go through the content-keyed
+    cache; with a 1 MiB limit the cache cycles instead of growing, results stay bit-exact, and
+    the device memory the process holds stays flat."""
+    torch = torch_gpu
+    rng = np.random.default_rng(3)
+    taps, block = 1024, 64                       # 4 KiB of taps per call
+    dsp.set_table_cache_limit(1 << 20)
+    try:
+        x = rng.uniform(-1, 1, block).astype(np.float32)
+        torch.cuda.synchronize()
+        free0 = torch.cuda.mem_get_info()[0]
+        for i in range(600):                     # 2.4 MiB of distinct coefficient sets
+            c = rng.standard_normal(taps).astype(np.float32)
+            f = dsp.FirF32(c, block)
+            got = f(x)
+            if i % 97 == 0:
+                want, _ = ref.fir("f32", c, [x])
+                assert got.tobytes() == want[0].tobytes()
+            assert dsp.table_cache_bytes() <= 1 << 20
+        torch.cuda.synchronize()
+        assert free0 - torch.cuda.mem_get_info()[0] < 64 << 20
+    finally:
+        dsp.set_table_cache_limit(256 << 20)
+
+
+def test_cfft_batch_multi_orders_after_torch_work(dsp, torch_gpu, ref):
+    """Shards written by torch kernels still in flight (no explicit synchronize): the wrapper
+    orders the library's streams after them."""
+    torch = torch_gpu
+    n, rows = 1024, 64
+    x = np.stack([refs.rand_input("f32", 2 * n, seed=500 + r) for r in range(rows)])
+    src = torch.from_numpy(x).cuda()
+    S = dsp.const_instance("arm_cfft_sR_f32_len1024")
+    for _ in range(3):
+        shard = torch.zeros_like(src)
+        for _ in range(20):                      # queue enough torch work to still be running
+            shard.mul_(0.5)
+        shard.copy_(src)
+        dsp.cfft_batch_multi(S, [shard], 0, 1)
+        assert shard.cpu().numpy().tobytes() == ref.cfft_many("f32", n, x, 0, 1).tobytes()

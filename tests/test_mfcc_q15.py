@@ -45,6 +45,10 @@ def frames_for(n, rows, seed):
     f[2] = rng.integers(-3, 4, n)
     f[3, 5] = -2**15
     f[4] = (np.sin(np.arange(n) * 0.21) * 2**13).astype(np.int16)
+    # max |x| == 1: the only frame for which arm_scale's shift count reaches the word size
+    # (the reference's undefined shift, taken mod 32 on the x86 host)
+    f[5] = rng.integers(-1, 2, n)
+    f[5, 3] = -1
     return f
 
 
