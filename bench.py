@@ -51,10 +51,10 @@ WORKLOADS = {
     "fir_fast_q31": ("fir_fast_q31", 128, 1 << 16, 8),
     "mat_mult_f32": ("mat", 1024, 256, None),
     "mfcc_f32": ("mfcc", 1024, 1 << 18, 4),
-    # three launches (pre in place, inner CFFT in place, post with the RFFT split fused):
-    # bytes moved per sample 4 + 4 (pre) + 4 + 4 (CFFT) + 4 (post reads the N-word CFFT row)
-    "mfcc_q31": ("mfccq31", 1024, 1 << 18, 20),
-    "mfcc_q15": ("mfccq15", 1024, 1 << 18, 10),
+    # algorithmic bytes per sample: the frame read once and written back once (the reference
+    # normalises and windows pSrc in place, arm_mfcc_q31.c:133-138), + 13 coefficients per frame
+    "mfcc_q31": ("mfccq31", 1024, 1 << 18, 8),
+    "mfcc_q15": ("mfccq15", 1024, 1 << 18, 4),
     "rfft_f32": ("rfft", 1024, 1 << 20, 8),
     # real length 8192 (inner CFFT 4096 = the fixed-point specialist); bytes per sample:
     # N words in, N words written back (the inner CFFT overwrites pSrc), 2N words out
@@ -65,6 +65,10 @@ WORKLOADS = {
     "mat_mult_q31": ("matq31", 1024, 64, None),
     "mat_mult_fast_q31": ("matfast_q31", 1024, 64, None),
 }
+
+
+# bytes the implementation moves per sample (for comparison with the algorithmic bytes)
+MFCC_FIXED_MOVED = {"mfcc_q31": 20, "mfcc_q15": 10}
 
 
 def log(*a):
@@ -87,6 +91,11 @@ def parse_args(argv=None):
     ap.add_argument("--no-config3", "--no-companion", dest="no_config3", action="store_true",
                     help="skip the configs[3] q31 + q15 N=4096 strong-scaling measurement")
     ap.add_argument("--dist-backend", default=None, help="nccl (default on GPUs, RCCL) or gloo (rehearsal)")
+    ap.add_argument("--scatter", action="store_true",
+                    help="configs[3]: also time rank 0 scattering the global q31 / q15 batch to the ranks "
+                         "(point-to-point over RCCL/xGMI), reported beside the compute (SURVEY 8e)")
+    ap.add_argument("--cpu-secs", type=float, default=None,
+                    help="seconds per CPU-baseline leg (default 1 s all-core, 3 s one core)")
     ap.add_argument("--dry-run", action="store_true",
                     help="plumbing only (CPU, gloo): launch, shard spans, reductions and the line, no device work")
     return ap.parse_args(argv)
@@ -159,11 +168,11 @@ def cpu_baseline(workload, n, all_secs=1.0, one_secs=3.0):
     if not os.path.exists(exe):
         return None
     wl = _CPU_WL[workload]
-    nn = 256 if workload.startswith("mat_mult") else n   # 1024^3 takes seconds per matrix on one core
+    nn = n                      # mat_mult: the config's 1024^3 (one matrix takes ~4 s on one core)
     threads, machine = cpu_share()
 
     def run(t, secs):
-        out = subprocess.run([exe, wl, str(nn), str(t), str(secs)], capture_output=True, text=True, timeout=120)
+        out = subprocess.run([exe, wl, str(nn), str(t), str(secs)], capture_output=True, text=True, timeout=300)
         return json.loads(out.stdout)
 
     one, allc = run(1, one_secs), run(threads, all_secs)
@@ -171,9 +180,13 @@ def cpu_baseline(workload, n, all_secs=1.0, one_secs=3.0):
     pick = (lambda r: r["gflops"] * 1e-3) if mat else (lambda r: r["gsamples_per_s"])
     unit = ("TFLOP/s" if workload.endswith("f32") else "TOPS") if mat else "Gsamples/s"
     what = f"arm_{workload} {nn}^3" if mat else f"{wl} n={nn}"
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = None
     return {"value": round(pick(allc), 6), "unit": unit, "cores": threads, "kind": kind,
             "single_core_value": round(pick(one), 6), "threads": threads, "cpu_model": cpu_model(),
-            "machine_logical_cpus": machine,
+            "machine_logical_cpus": machine, "affinity_cpus": affinity,
             "sample": f"{what}: 1 thread x {one_secs:.0f} s, then {threads} threads x {all_secs:.0f} s "
                       f"({int(allc['samples'])} samples), each thread its own buffers "
                       f"(reference scalar C, gcc -O2, no FMA)"}
@@ -476,11 +489,8 @@ def main_rank(args):
         fresh = synth("f32", 64 * n, salt=29).view(64, n)
         want = host.mfcc(cfg, fresh.cpu().numpy())
         got = m.batch(fresh.clone()).cpu().numpy()
-        err = np.abs(got.astype(np.float64) - want)
-        return wall, kern_ms, {"checker": hk, "frames_checked": 64, "max_abs_err": float(err.max()),
-                               "within_tolerance": bool(np.all(err <= 2e-5 + 1e-6 * np.abs(want))),
-                               "bit_exact_fraction": float(np.mean(got.view(np.uint32) == want.view(np.uint32))),
-                               "tolerance": "2e-5 + 1e-6*|ref| (device logf vs host libm logf; other stages exact)"}
+        return wall, kern_ms, {"checker": hk, "frames_checked": 64, "bit_exact": got.tobytes() == want.tobytes(),
+                               "logf": "host glibc logf restated on the device (host_logf.hpp)"}
 
     def run_mfcc_fixed(t, n, batch, steps, warmup):
         """arm_mfcc_q31 / _q15 (pre + RFFT + post) on the suite's 1024 tables over full-range
@@ -523,6 +533,37 @@ def main_rank(args):
         st, want = host.mat_mult_fixed(kind, a[0].cpu().numpy(), b[0].cpu().numpy())
         ok = st == 0 and c[0].cpu().numpy().tobytes() == want.tobytes()
         return wall, kern_ms, {"checker": hk, "bit_exact": bool(ok), "matrices_checked": 1}
+
+    def run_scatter(kind, n):
+        """SURVEY 8e's separately timed scatter: rank 0 generates the whole configs[3] global
+        batch on its GPU and sends every rank its contiguous slice point to point (RCCL over
+        xGMI with nccl; CPU tensors with gloo), bracketed by barrier + synchronize; every rank
+        then checks its received slice against its own rank-local generation of the same rows."""
+        G = args.global_batch
+        spans = [parallel.shard(G, r, world_n) for r in range(world_n)]
+        esz = 4 if kind == "q31" else 2
+        dev = world.backend != "gloo"
+        full = synth_global(kind, n, 0, G) if rank == 0 else None
+        if rank == 0 and not dev:
+            full = full.cpu()
+        dt = torch.int32 if kind == "q31" else torch.int16
+        out = torch.empty((spans[rank][1], 2 * n), dtype=dt, device="cuda" if dev else "cpu")
+        parallel.barrier(world)
+        t0 = time.perf_counter()
+        parallel.scatter_rows(world, full, spans, out)
+        parallel.barrier(world)
+        secs = parallel.reduce_max(world, time.perf_counter() - t0)
+        ok = bool(torch.equal(out.to("cuda"), synth_global(kind, n, *spans[rank])))
+        oks = parallel.gather_objects(world, ok)
+        del full, out
+        torch.cuda.empty_cache()
+        moved = (G - spans[0][1]) * 2 * n * esz              # bytes that left rank 0
+        return {"bytes_moved": moved, "ms": round(secs * 1e3, 3),
+                "GB_per_s": round(moved / secs * 1e-9, 2) if moved else None,
+                "path": "rank 0 -> ranks, point-to-point " + ("RCCL over xGMI (device tensors)" if dev else
+                                                             "gloo (host tensors, rehearsal)"),
+                "slices_verified": bool(all(oks)), "ranks": world_n,
+                "note": "timed separately; never part of value (rank-local generation is the headline)"}
 
     # ---------------------------------------------------------------- dispatch
     world_n = world.size
@@ -584,7 +625,7 @@ def main_rank(args):
             "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True, "scaling": scaling,
             "vs_baseline": None, "data": "synthetic (device generator seeded per rank / per global block; no scatter)",
             "ranks": world_n, "devices_used": devices, "dist_backend": world.backend,
-            "settle_launches": settle["launches"]}
+            "settle_launches": settle["launches"], "library": dsp.version()}
     if args.workload == "mat_mult_fast_q31":
         ops = 2.0 * n * n * n * batch
         line.update(value=round(total_units * 2.0 * n ** 3 / wall * 1e-12, 4), unit="TOPS (2*M*N*K int MAC)",
@@ -673,6 +714,8 @@ def main_rank(args):
             valu = units * n * 2 / (kern_ms * 1e-3) * 1e-12
             line["roofline"]["valu_tflops_nofma"] = {"achieved": round(valu, 2), "peak": FP32_NOFMA_TFLOPS,
                                                      "frac": round(valu / FP32_NOFMA_TFLOPS, 4)}
+        if args.workload in ("mfcc_q31", "mfcc_q15"):
+            line["roofline"]["bytes_moved_per_sample"] = MFCC_FIXED_MOVED[args.workload]
         if args.workload == "rfft_f32":
             # the forward transform also leaves the inner CFFT output in p (reference semantics)
             line["roofline"]["bytes_moved_per_sample"] = 12
@@ -710,17 +753,28 @@ def main_rank(args):
                                                   "algorithmic_bytes_per_launch": biggest * 4096 * qbps,
                                                   "avg_kernel_ms": round(k2, 4)},
                       "parity": p2}
+        if args.scatter:
+            for qk in ("q31", "q15"):
+                c3[qk]["scatter"] = run_scatter(qk, 4096)
         line["config3"] = c3
 
-    if world_n == 1 and rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
+        secs = (args.cpu_secs, args.cpu_secs) if args.cpu_secs else (1.0, 3.0)
         try:
-            line["cpu_baseline"] = cpu_baseline(args.workload, n)
+            line["cpu_baseline"] = cpu_baseline(args.workload, n, *secs)
             if "config3" in line:
                 for qk in ("q31", "q15"):
-                    line["config3"][qk]["cpu_baseline"] = cpu_baseline(f"cfft_{qk}_4096", 4096, 1.0, 2.0)
+                    line["config3"][qk]["cpu_baseline"] = cpu_baseline(f"cfft_{qk}_4096", 4096, secs[0],
+                                                                       min(secs[1], 2.0))
+            if line["cpu_baseline"] is not None:
+                line["cpu_baseline"]["scope"] = (
+                    "rank 0's host CPU share (the box allots 16 CPUs per GPU): the CPU path one GPU of this line "
+                    f"replaces; {world_n} GPU(s) replace up to {world_n}x this" if world_n > 1 else
+                    "the host CPU share of the one GPU (16 CPUs per GPU)")
         except Exception as e:  # a missing/failed baseline must not hide the GPU number
             log("cpu_baseline failed:", e)
             line["cpu_baseline"] = None
+    parallel.barrier(world)                       # the other ranks wait for rank 0's CPU legs
     if rank == 0:
         print(json.dumps(line), flush=True)
     parallel.shutdown(world)
@@ -730,15 +784,34 @@ def main_rank(args):
 def dry_run(args, world, parallel):
     """CPU plumbing rehearsal (gloo): shard spans of configs[3], the MAX / gather reductions
     and the line shape; no library call, no device."""
+    import torch
     span = parallel.shard(args.global_batch, world.rank, world.size)
     recs = parallel.gather_objects(world, {"rank": world.rank, "span": list(span), "pid": os.getpid()})
     wall = parallel.reduce_max(world, 0.001 * (1 + world.rank))
+    line = None
     if world.rank == 0:
         spans = [r["span"] for r in sorted(recs, key=lambda r: r["rank"])]
-        print(json.dumps({"metric": METRIC, "n_gpus": world.size, "ranks": world.size, "dry_run": True,
-                          "dist_backend": world.backend, "spans": spans, "pids": [r["pid"] for r in recs],
-                          "max_wall_s": wall, "scaling": args.scaling, "global_batch": args.global_batch}),
-              flush=True)
+        line = {"metric": METRIC, "n_gpus": world.size, "ranks": world.size, "dry_run": True,
+                "dist_backend": world.backend, "spans": spans, "pids": [r["pid"] for r in recs],
+                "max_wall_s": wall, "scaling": args.scaling, "global_batch": args.global_batch}
+    if args.scatter:
+        # the scatter leg's plumbing on a small host batch: row i holds words 8 i .. 8 i + 7
+        G = min(args.global_batch, 4096)
+        sp = [parallel.shard(G, r, world.size) for r in range(world.size)]
+        full = torch.arange(G * 8, dtype=torch.int32).view(G, 8) if world.rank == 0 else None
+        out = torch.empty((sp[world.rank][1], 8), dtype=torch.int32)
+        parallel.scatter_rows(world, full, sp, out)
+        s0, c0 = sp[world.rank]
+        ok = bool(torch.equal(out, torch.arange(s0 * 8, (s0 + c0) * 8, dtype=torch.int32).view(c0, 8)))
+        oks = parallel.gather_objects(world, ok)
+        if line is not None:
+            line["scatter"] = {"rows": G, "slices_verified": bool(all(oks)), "ranks": world.size}
+    if world.rank == 0 and not args.no_cpu_baseline:
+        secs = args.cpu_secs or 0.2
+        line["cpu_baseline"] = cpu_baseline("cfft_f32_1024", 1024, secs, secs)
+    parallel.barrier(world, sync_device=False)
+    if line is not None:
+        print(json.dumps(line), flush=True)
     parallel.shutdown(world)
     return 0
 

@@ -6,7 +6,10 @@ Every rank owns a contiguous slice of the global batch and generates (or receive
 own data, so the hot path never communicates.  Collectives are used only around it:
   * a barrier + MAX reduction of the timed interval (bench contract),
   * an all-gather of per-rank parity digests ("checksum of checksums") so rank 0 can
-    assert that every shard matched the reference bit for bit.
+    assert that every shard matched the reference bit for bit,
+  * the separately timed scatter leg of SURVEY §8e (scatter_rows: rank 0 holds a global
+    batch and sends each rank its contiguous slice point to point, RCCL over xGMI), which
+    is reported beside the compute, never inside it.
 Backends: "nccl" (= RCCL over xGMI on ROCm) on GPUs, "gloo" for CPU rehearsals and tests.
 Nothing here touches the HIP kernels; tests/test_dist.py runs it with gloo, world size 2.
 """
@@ -135,6 +138,31 @@ def gather_objects(world, obj):
     out = [None] * world.size
     dist.all_gather_object(out, obj)
     return out
+
+
+def scatter_rows(world, full, spans, out):
+    """Rank 0 holds `full` (the global batch, rows = items) and every rank r receives rows
+    [spans[r][0], spans[r][0] + spans[r][1]) into `out`; rank 0 copies its own slice.  The
+    sends are posted together (batch_isend_irecv: with nccl one RCCL group of point-to-point
+    transfers over xGMI, rank 0 -> each peer on its own link); gloo moves CPU tensors."""
+    s0, c0 = spans[world.rank]
+    if not world.distributed:
+        out.copy_(full[s0:s0 + c0])
+        return
+    import torch.distributed as dist
+    ops = []
+    if world.rank == 0:
+        for r in range(1, world.size):
+            s, c = spans[r]
+            if c:
+                ops.append(dist.P2POp(dist.isend, full[s:s + c], r))
+    elif c0:
+        ops.append(dist.P2POp(dist.irecv, out, 0))
+    reqs = dist.batch_isend_irecv(ops) if ops else []
+    if world.rank == 0 and c0:
+        out.copy_(full[s0:s0 + c0])
+    for q in reqs:
+        q.wait()
 
 
 def checksum_of_checksums(records):

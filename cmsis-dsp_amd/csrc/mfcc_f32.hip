@@ -19,10 +19,11 @@
 //              :124-125), *max (arm_scale_f32), Mel dot products (arm_dot_prod_f32),
 //              logf(. + 1e-6f) (arm_offset_f32, arm_vlog_f32), DCT rows (arm_mat_vec_mult_f32)
 //                                                       [one wave per frame, spectrum in LDS]
-// Every sum is k-ordered mul-then-add as in the reference (contract off): the stages are
-// bit-identical to the reference up to logf, whose device implementation may differ from
-// the host libm's by an ulp.
+// Every sum is k-ordered mul-then-add as in the reference (contract off), and the log is the
+// host libm's logf restated for the device (host_logf.hpp, proven equal on all 2^32 inputs):
+// every stage is bit-identical to the reference build.
 #include "common.hpp"
+#include "host_logf.hpp"
 #include "kernels.hpp"
 #include "cfft_f32_core.hpp"
 
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(256) void mfcc_post_kernel(const float* __restrict_
         const float prod = (k < (uint32_t)half ? mag[k] : 0.0f) * c[j];
         sum = sum + prod;
       }
-      mel[i] = logf(sum + 1.0e-6f);
+      mel[i] = host_logf(sum + 1.0e-6f);
     }
   }
   __syncthreads();
@@ -248,7 +249,7 @@ __global__ __launch_bounds__(kBlock) void mfcc_fused_kernel(const float* __restr
       const float prod = (k < (uint32_t)H ? mag[k] : 0.0f) * c[j];
       sum = sum + prod;
     }
-    mel[i] = logf(sum + 1.0e-6f);
+    mel[i] = host_logf(sum + 1.0e-6f);
   }
   __syncthreads();
   if (tr < valid) {

@@ -35,6 +35,19 @@ def test_gpus2_launches_two_ranks_strong_spans():
     assert line["max_wall_s"] == 0.002          # MAX over ranks (rank r reports 0.001 * (r + 1))
 
 
+def test_gpus2_scatter_leg_and_cpu_baseline():
+    """N > 1 lines carry rank 0's cpu_baseline, and --scatter moves each rank its contiguous
+    slice of the global batch from rank 0 (point-to-point; gloo on CPU here)."""
+    r = _run(["--gpus", "2", "--dry-run", "--scaling", "strong", "--global-batch", "1000", "--scatter",
+              "--cpu-secs", "0.2"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _line(r.stdout)
+    assert line["scatter"] == {"rows": 1000, "slices_verified": True, "ranks": 2}
+    cb = line["cpu_baseline"]
+    if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "bench_ref")):
+        assert cb["kind"] == "reference" and cb["value"] > 0 and cb["cores"] >= 1 and cb["affinity_cpus"] >= 1
+
+
 def test_gpus3_ragged_global_batch():
     r = _run(["--gpus", "3", "--dry-run", "--scaling", "strong", "--global-batch", "10"])
     assert r.returncode == 0, r.stderr[-2000:]

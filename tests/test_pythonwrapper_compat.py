@@ -130,6 +130,7 @@ def test_mfcc_f32(cdsp, torch_gpu, ref):
     x = g["input_Noise_512"]
     res = cdsp.arm_mfcc_f32(inst, x, np.zeros(cdsp.arm_mfcc_tmp_buffer_size(0, 512, 1), np.float32))
     np.testing.assert_allclose(res, ref.mfcc(cfg, x)[0], 3e-6, 3e-6)     # testmfcc.py tolerance
+    assert np.asarray(res, np.float32).tobytes() == ref.mfcc(cfg, x)[0].tobytes()   # and bit-exact
 
 
 @pytest.mark.gpu
