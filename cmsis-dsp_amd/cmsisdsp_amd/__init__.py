@@ -434,13 +434,15 @@ def rfft_fast_batch(S, p, out, ifft, stream=None):
         raise RuntimeError(f"arm_rfft_fast_f32_batch -> {st}: {last_error()[1]}")
 
 
-_FIR_BATCH = {"f32": "arm_fir_f32_batch", "q15": "arm_fir_q15_batch", "q31": "arm_fir_q31_batch",
+_FIR_BATCH = {"f32": "arm_fir_f32_batch", "f32_fma": "arm_fir_f32_batch_fma", "q15": "arm_fir_q15_batch",
+              "q31": "arm_fir_q31_batch",
               "fast_q15": "arm_fir_fast_q15_batch", "fast_q31": "arm_fir_fast_q31_batch", "q7": "arm_fir_q7_batch"}
 
 
 def fir_batch(S, src, dst, hist, stream=None, q15=False, kind=None):
     """src/dst: [batch, blockSize] device tensors; hist: [batch, numTaps-1] device state.
-    kind: f32 | q15 | q31 | fast_q15 | fast_q31 | q7 (default from the instance type / q15 flag)."""
+    kind: f32 | f32_fma (opt-in tolerance path) | q15 | q31 | fast_q15 | fast_q31 | q7 (default from
+    the instance type / q15 flag)."""
     if kind is None:
         kind = "q15" if q15 else {arm_fir_instance_f32: "f32", arm_fir_instance_q15: "q15",
                                   arm_fir_instance_q31: "q31", arm_fir_instance_q7: "q7"}[type(S)]

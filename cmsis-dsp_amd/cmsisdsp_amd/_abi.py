@@ -259,6 +259,8 @@ BATCHED = {
     "arm_rfft_q15_batch": (C.c_int, [P(arm_rfft_instance_q15), C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
     "arm_fir_f32_batch": (C.c_int, [P(arm_fir_instance_f32), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                     C.c_void_p, C.c_void_p]),
+    "arm_fir_f32_batch_fma": (C.c_int, [P(arm_fir_instance_f32), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                        C.c_void_p, C.c_void_p]),
     "arm_fir_q15_batch": (C.c_int, [P(arm_fir_instance_q15), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                     C.c_void_p, C.c_void_p]),
     "arm_fir_fast_q15_batch": (C.c_int, [P(arm_fir_instance_q15), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,

@@ -73,6 +73,15 @@ void cfft_sync(const Inst* S, void* p1, uint8_t ifftFlag, uint8_t bitReverseFlag
     if (e != hipSuccess) set_error(e, "arm_cfft");
     return;
   }
+  if (bytes <= kZeroCopyMax) {               // one launch on the coherent pinned copy, no DMA
+    HostIO io(st);
+    void* z = io.zinout(p1, bytes);
+    if (!z) { set_error(hipErrorOutOfMemory, "arm_cfft staging"); return; }
+    hipError_t e = cfft_launch(kind, n, z, 1, pr, st);
+    if (e == hipSuccess) e = io.finish();
+    if (e != hipSuccess) set_error(e, "arm_cfft");
+    return;
+  }
   void* d = scratch(bytes, 0);
   if (!d) { set_error(hipErrorOutOfMemory, "arm_cfft scratch"); return; }
   HostIO io(st);
@@ -411,16 +420,14 @@ bool mfcc_fx_prepare(const Inst* S, MfccFxDev<T>& d) {
 
 // x: [batch][n] frames (overwritten), y: [batch][2n] spectra, dst: [batch][nbDct]; the frame
 // maxima ride in dst[frame][0] between the launches (read before the row is written)
+#ifndef MI355X_MFCC_FX_FUSED
+#define MI355X_MFCC_FX_FUSED 1    // 0: always the three-launch path (A/B builds)
+#endif
 template <typename T, typename Inst>
 bool mfcc_fx_run(const Inst* S, const MfccFxDev<T>& d, T* x, T* y, T* dst, uint32_t batch, hipStream_t st) {
   const int n = (int)S->fftLen, nd = (int)S->nbDctOutputs, nm = (int)S->nbMelFilters;
-  if constexpr (sizeof(T) == 4) {
-    MI_CHECK(mfcc_q31_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc q31 pre");
-  } else {
-    MI_CHECK(mfcc_q15_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc q15 pre");
-  }
-  // the inner CFFT of the forward RFFT in place on x; the split is fused into post
-  // (arm_rfft_q31.c:148-183: cfft(L, fwd, bitrev) then arm_split_rfft)
+  // the forward RFFT's inner CFFT (arm_rfft_q31.c:148-183: cfft(L, fwd, bitReverseFlagR), then
+  // arm_split_rfft): its tables and bit-reversal mode
   const auto* in = S->rfft.pCfft;
   const uint32_t L = (uint32_t)n / 2;
   if (!in || in->fftLen != L || !cfft_len_ok(L)) { set_error(hipErrorInvalidValue, "mfcc rfft instance"); return false; }
@@ -428,6 +435,18 @@ bool mfcc_fx_run(const Inst* S, const MfccFxDev<T>& d, T* x, T* y, T* dst, uint3
   if (!cfft_prepare(L, in->pTwiddle, in->pBitRevTable, in->bitRevLength, sizeof(T) == 4 ? 1 : 2, 0,
                     S->rfft.bitReverseFlagR, pr))
     return false;
+  if (MI355X_MFCC_FX_FUSED && !pr.perm) {   // the reference's own bit reversal: one fused launch
+    const hipError_t e = mfcc_fx_fused_launch<T>(n, x, d.win, pr.tw, S->rfft.bitReverseFlagR ? 1 : 0, d.tw, nm,
+                                                 d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst, batch, st);
+    if (e == hipSuccess) return true;
+    if (e != hipErrorInvalidValue) { set_error(e, "mfcc fused"); return false; }
+    (void)hipGetLastError();                // unsupported shape: the three-launch path below
+  }
+  if constexpr (sizeof(T) == 4) {
+    MI_CHECK(mfcc_q31_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc q31 pre");
+  } else {
+    MI_CHECK(mfcc_q15_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc q15 pre");
+  }
   MI_CHECK(cfft_launch(sizeof(T) == 4 ? 1 : 2, L, x, batch, pr, st), "mfcc cfft");
   (void)y;
   if constexpr (sizeof(T) == 4) {
@@ -469,6 +488,21 @@ void fir_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B, int kind) {
   if (!ok) { set_error(hipErrorOutOfMemory, "arm_fir coeffs"); return; }
   const bool dstate = is_device_ptr(S->pState), dsrc = is_device_ptr(pSrc), ddst = is_device_ptr(pDst);
   const size_t sb = sizeof(T) * (size_t)B, hb = sizeof(T) * (size_t)T1;
+  if (!dstate && !dsrc && !ddst && hb + sb <= kZeroCopyMax) {
+    // all host, small: the caller's state buffer itself, [history ; block], staged as one
+    // coherent pinned copy the kernels use in place (the filter reads it, the history kernel
+    // rewrites its head), so after finish() it holds [new history ; block input] exactly as the
+    // reference leaves pState; outputs likewise -- two launches, no DMA
+    HostIO io(st);
+    T* zs = (T*)io.zinout(S->pState, hb + sb);
+    T* zd = (T*)io.zout(pDst, sb);
+    if (!zs || !zd) { set_error(hipErrorOutOfMemory, "arm_fir staging"); return; }
+    memmove(zs + T1, pSrc, sb);                   // pSrc may alias pDst: read before anything
+    hipError_t e = fir_run(kind, dc, taps, zs + T1, zd, B, 1, zs, st);
+    if (e == hipSuccess) e = io.finish();
+    if (e != hipSuccess) set_error(e, "arm_fir");
+    return;
+  }
   // in place on the device (pSrc overlapping pDst): filter from a copy of the input, which
   // also feeds the new history and the state tail (the reference copies each input into
   // pState before writing pDst, arm_fir_f32.c:947-975)
@@ -1035,6 +1069,10 @@ void arm_fir_fast_q31(const arm_fir_instance_q31* S, const q31_t* pSrc, q31_t* p
 arm_status arm_fir_f32_batch(const arm_fir_instance_f32* S, const float32_t* d_src, float32_t* d_dst,
                              uint32_t blockSize, uint32_t batch, float32_t* d_hist, void* stream) {
   return fir_batch<float>(S, d_src, d_dst, blockSize, batch, d_hist, stream, kFirF32);
+}
+arm_status arm_fir_f32_batch_fma(const arm_fir_instance_f32* S, const float32_t* d_src, float32_t* d_dst,
+                                 uint32_t blockSize, uint32_t batch, float32_t* d_hist, void* stream) {
+  return fir_batch<float>(S, d_src, d_dst, blockSize, batch, d_hist, stream, kFirF32Fma);
 }
 arm_status arm_fir_q15_batch(const arm_fir_instance_q15* S, const q15_t* d_src, q15_t* d_dst, uint32_t blockSize,
                              uint32_t batch, q15_t* d_hist, void* stream) {

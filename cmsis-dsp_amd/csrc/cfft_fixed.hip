@@ -18,62 +18,6 @@
 
 namespace mi355x {
 
-template <int N> struct PlanFx {
-  static constexpr bool BY2 = (Log2<N>::v & 1) != 0;       // 32,128,512,2048
-  static constexpr int M = BY2 ? N / 2 : N;                 // radix-4 length
-  static constexpr int STAGES = Log2<M>::v / 2;
-  static constexpr int LPT = N / 16;
-  static constexpr int TPB = kBlock / LPT;
-};
-
-
-template <typename T, int N, bool INV>
-__device__ __forceinline__ void radix4_stages(typename Fx<T>::C* x, const typename Fx<T>::C* __restrict__ tw,
-                                              int lane) {
-  using P = PlanFx<N>;
-  using F = Fx<T>;
-  constexpr int M = P::M;
-  constexpr int mod0 = P::BY2 ? 2 : 1;
-#pragma unroll
-  for (int s = 0; s < P::STAGES; ++s) {
-    const int n1 = M >> (2 * s), n2 = n1 >> 2;
-    const int mod = mod0 << (2 * s);
-#pragma unroll
-    for (int r = 0; r < (N / 4) / P::LPT; ++r) {
-      const int bi = lane + r * P::LPT;
-      const int c = bi / (M / 4), rr = bi % (M / 4);
-      const int j = rr % n2, q = rr / n2;
-      typename F::C* p = x + c * M + q * n1 + j;
-      if constexpr (sizeof(T) == 2 && MI355X_FX_Q15_PACKED) {
-        uint32_t* pu = reinterpret_cast<uint32_t*>(p);
-        s16x2 A = pk(pu[0]), B = pk(pu[n2]), C = pk(pu[2 * n2]), D = pk(pu[3 * n2]);
-        if (s == P::STAGES - 1) {
-          const TwP z{};
-          bfly_pk<INV, 2>(A, B, C, D, z, z, z);
-        } else {
-          const int ia = j * mod;
-          const TwP w1 = twp<INV>(tw[ia]), w2 = twp<INV>(tw[2 * ia]), w3 = twp<INV>(tw[3 * ia]);
-          if (s == 0) bfly_pk<INV, 0>(A, B, C, D, w1, w2, w3);
-          else        bfly_pk<INV, 1>(A, B, C, D, w1, w2, w3);
-        }
-        pu[0] = upk(A); pu[n2] = upk(B); pu[2 * n2] = upk(C); pu[3 * n2] = upk(D);
-        continue;
-      }
-      int2 A = F::ld(p), B = F::ld(p + n2), C = F::ld(p + 2 * n2), D = F::ld(p + 3 * n2);
-      if (s == P::STAGES - 1) {
-        bfly<T, INV, 2>(A, B, C, D, int2{}, int2{}, int2{});
-      } else {
-        const int ia = j * mod;
-        const int2 w1 = F::ld(tw + ia), w2 = F::ld(tw + 2 * ia), w3 = F::ld(tw + 3 * ia);
-        if (s == 0) bfly<T, INV, 0>(A, B, C, D, w1, w2, w3);
-        else        bfly<T, INV, 1>(A, B, C, D, w1, w2, w3);
-      }
-      F::st(p, A); F::st(p + n2, B); F::st(p + 2 * n2, C); F::st(p + 3 * n2, D);
-    }
-    __syncthreads();
-  }
-}
-
 template <typename T, int N, bool INV>
 __global__ __launch_bounds__(kBlock) void cfft_fx_kernel(typename Fx<T>::C* __restrict__ data, uint32_t batch,
                                                          const typename Fx<T>::C* __restrict__ tw,
@@ -108,36 +52,7 @@ __global__ __launch_bounds__(kBlock) void cfft_fx_kernel(typename Fx<T>::C* __re
   const int tr = tid / P::LPT, lane = tid % P::LPT;
   C* x = lds + tr * SP;
 
-  if constexpr (P::BY2) {
-    // radix-2 pre-pass: arm_cfft_q31.c:774-794 / :835-855, arm_cfft_q15.c:782-800 / :881-899
-    constexpr int H = N / 2;
-#pragma unroll
-    for (int it = 0; it < H / P::LPT; ++it) {
-      const int i = lane + it * P::LPT;
-      const int2 w = F::ld(tw + i);
-      int2 a = F::ld(x + i), b = F::ld(x + i + H);
-      if constexpr (sizeof(T) == 4) {
-        const int32_t xt = wsub(a.x >> 2, b.x >> 2);
-        const int32_t yt = wsub(a.y >> 2, b.y >> 2);
-        F::st(x + i, make_int2(wadd(a.x >> 2, b.x >> 2), wadd(b.y >> 2, a.y >> 2)));
-        int32_t p0 = mult_R(xt, w.x), p1 = mult_R(yt, w.x);
-        if (!INV) { p0 = multAcc_R(p0, yt, w.y); p1 = multSub_R(p1, xt, w.y); }
-        else      { p0 = multSub_R(p0, yt, w.y); p1 = multAcc_R(p1, xt, w.y); }
-        F::st(x + i + H, make_int2(wshl(p0, 1), wshl(p1, 1)));
-      } else {
-        const int32_t xt = t16((a.x >> 1) - (b.x >> 1));
-        const int32_t yt = t16((a.y >> 1) - (b.y >> 1));
-        F::st(x + i, make_int2(((a.x >> 1) + (b.x >> 1)) >> 1, ((b.y >> 1) + (a.y >> 1)) >> 1));
-        const int32_t xc = t16((xt * w.x) >> 16), ys = t16((yt * w.y) >> 16);
-        const int32_t yc = t16((yt * w.x) >> 16), xs = t16((xt * w.y) >> 16);
-        if (!INV) F::st(x + i + H, make_int2(t16(xc + ys), t16(yc - xs)));
-        else      F::st(x + i + H, make_int2(t16(xc - ys), t16(yc + xs)));
-      }
-    }
-    __syncthreads();
-  }
-
-  radix4_stages<T, N, INV>(x, tw, lane);
+  cfft_fx_lds_body<T, N, INV>(x, tw, lane);
 
   {  // store: binary bit reversal as an LDS gather; radix4by2 post-pass "<<1" folded here
     constexpr int LOG = Log2<N>::v;

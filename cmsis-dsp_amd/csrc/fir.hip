@@ -57,9 +57,14 @@ __device__ __forceinline__ T fir_sample(const T* __restrict__ hist, const T* __r
 }
 
 // ---------------------------------------------------------------- f32
-constexpr int kF32R = 8;                                // outputs per lane (fir_f32_kernel)
-constexpr int kF32Chunk = kBlock * kF32R;              // outputs per workgroup
-constexpr int kFirPre = (kF32Chunk + kFirMaxTaps - 1 + kBlock - 1) / kBlock;   // window samples per thread
+#ifndef MI355X_FIR_F32_R
+#define MI355X_FIR_F32_R 16
+#endif
+constexpr int kF32R = MI355X_FIR_F32_R;                 // outputs per lane (fir_f32_kernel)
+static_assert(kF32R == 8 || kF32R == 16, "fir_f32_kernel: 8 or 16 outputs per lane");
+constexpr int kF32G = kF32R / 8 + 1;                     // 8-sample groups one round reads
+constexpr int kF32Chunk = kBlock * kF32R;              // outputs per workgroup item
+constexpr int kFirPre = (kFirChunk + kFirMaxTaps - 1 + kBlock - 1) / kBlock;   // q31 window samples per thread
 
 // LDS index with one pad word every 8: lanes read at a stride of R = 8 words from any
 // offset, and i + i/8 keeps every ds_read_b32 32-lane group on 32 distinct banks (one
@@ -67,25 +72,36 @@ constexpr int kFirPre = (kF32Chunk + kFirMaxTaps - 1 + kBlock - 1) / kBlock;   /
 __device__ __forceinline__ int padx(int i) { return i + (i >> 3); }
 
 // ---- fir_f32_kernel: a register-window formulation with no ring rotation.
-// A round is 8 consecutive taps k..k+7; output r of a lane needs window samples
-// base + r + k .. base + r + k + 7, i.e. the two 8-sample groups base + k and base + k + 8
-// (base = 8 * lane).  Four 8-register group buffers rotate by name over an unrolled block of
-// four rounds: round q computes from buffers (q, q+1) while group q + 2 is read from LDS,
-// one round (128 VALU) ahead of its use, so every operand index is a compile-time constant
-// and no register moves.  LDS window layout: 8-sample groups at a pitch of 10 words
-// (wpos), so each ds_read2_b64 of a group (lanes 8 words apart in sample terms) lands each
-// 16-lane access on 32 distinct banks.  Coefficients are wave-uniform scalar loads into
-// SGPRs (the v_mul operand: no VGPRs, no LDS reads); the loop is 2 VALU per tap and output
-// plus 3 instructions per 512 (PMC: SQ_INSTS_VALU = 1.019 x the MAC minimum at 128 taps).
-__host__ __device__ constexpr int wpos(int j) { return j + 2 * (j >> 3); }
+// A round is 8 consecutive taps k..k+7; output r of a lane (base = R * lane) needs window
+// samples base + r + k .. base + r + k + 7, i.e. the R/8 + 1 8-sample groups from base + k.
+// Four 8-register group buffers rotate by name over an unrolled block of four rounds: round q
+// computes from buffers q .. q + R/8 while group q + R/8 + 1 is read from LDS, one round
+// (8R VALU) ahead of its use, so every operand index is a compile-time constant and no register
+// moves.  Coefficients are wave-uniform scalar loads into SGPRs (the v_mul operand: no VGPRs,
+// no LDS reads); the loop is 2 VALU per tap and output (1 with FMA) plus a few per round.
+// R = 16 (round 3) halves the LDS reads and the per-item overhead (barriers, staging) per MAC
+// against R = 8 (PMC at R = 8: SQ_INSTS_VALU = 1.019 x the MAC minimum but VALU busy 82 %).
+//
+// LDS window layout: 8-sample group g at word gword(g) = 10 g (+ 2 when bit 4 of g is set, R =
+// 16), so each 16-lane access of a group's ds_read2_b64 (lanes R/8 groups apart) lands on 32
+// distinct banks; staging writes go through fir_stage_lane, a thread -> sample permutation under
+// which every 32-lane ds_write_b32 group covers 32 distinct banks (round 2's identity mapping
+// was two-way conflicted: 9.4 M conflict cycles per launch, profiles/r02/fir_f32/pmc.json).
+// Both checked by tools/fir_lds_model.py.
+__host__ __device__ constexpr int gword(int g) { return 10 * g + (kF32R == 16 ? 2 * ((g >> 4) & 1) : 0); }
+__host__ __device__ constexpr int wpos(int j) { return gword(j >> 3) + (j & 7); }
+__device__ __forceinline__ int fir_stage_lane(int tid) {
+  const int h = tid >> 5, q = tid & 31, a = q >> 3, e = q & 7;
+  return 8 * (16 * (h >> 2) + 4 * a + (h & 3)) + e;     // groups c, c+4, c+8, c+12 per half-wave
+}
 
 #ifndef MI355X_FIR_SCHED_BARRIER
 #define MI355X_FIR_SCHED_BARRIER 1
 #endif
 struct F32Grp { float v[8]; };
-// group i after p (p + 10 i words): two ds_read2_b64 with immediate offsets
-__device__ __forceinline__ void ld_grp(F32Grp& g, const float* p, int i) {
-  const float2* q = reinterpret_cast<const float2*>(p + 10 * i);
+// group g of the window: two ds_read2_b64
+__device__ __forceinline__ void ld_grp(F32Grp& g, const float* win, int grp) {
+  const float2* q = reinterpret_cast<const float2*>(win + gword(grp));
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     const float2 x = q[h];
@@ -97,12 +113,24 @@ __device__ __forceinline__ void ld_coef(float (&c)[8], const float* cl, int k) {
   const float4 a = *reinterpret_cast<const float4*>(cl + k), b = *reinterpret_cast<const float4*>(cl + k + 4);
   c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w; c[4] = b.x; c[5] = b.y; c[6] = b.z; c[7] = b.w;
 }
-// one round: acc[r] += s[base + r + k + u] * c[k + u], u ascending (the reference's order)
-__device__ __forceinline__ void f32_round(float (&acc)[8], const F32Grp& A, const F32Grp& B, const float (&c)[8]) {
+// one round: acc[r] += s[base + r + k + u] * c[k + u], u ascending (the reference's order);
+// FMA: the opt-in tolerance path (arm_fir_f32_batch_fma), one v_fma_f32 per MAC in the same order
+template <bool FMA>
+__device__ __forceinline__ float f32_mac(float acc, float x, float c) {
+  if constexpr (FMA) return __builtin_fmaf(x, c, acc);
+  else return acc + x * c;
+}
+// groups A, B (, C for R = 16) hold window samples base + k + [0, 8), [8, 16), [16, 24)
+template <bool FMA>
+__device__ __forceinline__ void f32_round(float (&acc)[kF32R], const F32Grp& A, const F32Grp& B, const F32Grp& C,
+                                          const float (&c)[8]) {
 #pragma unroll
   for (int u = 0; u < 8; ++u)
 #pragma unroll
-    for (int r = 0; r < 8; ++r) acc[r] = acc[r] + (r + u < 8 ? A.v[r + u] : B.v[r + u - 8]) * c[u];
+    for (int r = 0; r < kF32R; ++r) {
+      const int j = r + u;
+      acc[r] = f32_mac<FMA>(acc[r], j < 8 ? A.v[j] : j < 16 ? B.v[j - 8] : C.v[j - 16], c[u]);
+    }
 #if MI355X_FIR_SCHED_BARRIER
   __builtin_amdgcn_sched_barrier(0);   // keep each round's products next to their adds
 #endif
@@ -123,13 +151,13 @@ __device__ __forceinline__ int opaque(int x) {
   asm volatile("" : "+v"(x));
   return x;
 }
-// Rows k >= KPRE - 8 never reach the history (T1 < 256 (KPRE - 8)); the history words are
+// Rows k >= KPRE - R never reach the history (T1 < 256 (KPRE - R)); the history words are
 // kept apart and OR-ed in when the window is written to LDS, so no wait is placed before the
 // MACs that the fetch is meant to overlap.  A tap segment of a long filter (LONG, numTaps >
 // kFirSeg) starts a tap offset a into s, so any row can reach the history: all rows get one.
 template <int KPRE, bool LONG>
 struct F32Win {
-  static constexpr int kH = LONG ? KPRE : KPRE - 8;
+  static constexpr int kH = LONG ? KPRE : KPRE - kF32R;
   int x[KPRE];
   int h[kH];
 };
@@ -148,11 +176,12 @@ struct FirIn {
 // window of the tap segment starting at tap a: sample j = s[n0 + a + j]
 template <int KPRE, bool LONG>
 __device__ __forceinline__ void fir_f32_fetch(F32Win<KPRE, LONG>& w, const FirItem& it, const float* __restrict__ src,
-                                              const float* __restrict__ hist_in, const FirIn& in, int T1, int tid) {
+                                              const float* __restrict__ hist_in, const FirIn& in, int T1, int jl) {
+  // jl = fir_stage_lane(thread): the row sample this thread stages
   const __amdgpu_buffer_rsrc_t r = buf_rsrc(src + it.f * in.stride, in.len * 4u);
   const __amdgpu_buffer_rsrc_t rh = in.hist ? buf_rsrc(hist_in + (uint64_t)it.f * T1, (uint32_t)T1 * 4u)
                                             : buf_rsrc(src, 0u);
-  const int v0 = (tid + it.n0 + it.a - T1 + in.so) * 4, h0 = (tid + it.n0 + it.a) * 4;
+  const int v0 = (jl + it.n0 + it.a - T1 + in.so) * 4, h0 = (jl + it.n0 + it.a) * 4;
 #pragma unroll
   for (int k = 0; k < KPRE; ++k) w.x[k] = __builtin_amdgcn_raw_buffer_load_b32(r, opaque(v0 + 1024 * k), 0, 0);
 #pragma unroll
@@ -190,7 +219,7 @@ struct FirOut {
 };
 
 #ifndef MI355X_FIR_F32_WAVES
-#define MI355X_FIR_F32_WAVES 8     // minimum waves per SIMD the register allocation must allow
+#define MI355X_FIR_F32_WAVES (kF32R == 16 ? 5 : 8)   // minimum waves per SIMD the allocation must allow
 #endif
 // Long filters (numTaps > kFirSeg) run in tap segments of kFirSeg: a work unit is (item,
 // segment), the accumulators stay in registers from a unit with segment 0 to the one with the
@@ -213,25 +242,27 @@ __device__ __forceinline__ FirUnit fir_unit(uint32_t u, uint32_t nseg, uint32_t 
   x.last = !LONG || seg == (int)nseg - 1;
   return x;
 }
-template <int KPRE, bool LONG>
-__global__ __launch_bounds__(kBlock, LONG ? 6 : MI355X_FIR_F32_WAVES) void fir_f32_kernel(
+template <int KPRE, bool LONG, bool FMA>
+__global__ __launch_bounds__(kBlock, LONG ? 4 : MI355X_FIR_F32_WAVES) void fir_f32_kernel(
     const float* __restrict__ coeffs, int T, const float* __restrict__ src, float* __restrict__ dst, uint32_t B,
     const float* __restrict__ hist_in, uint32_t nchunks, uint32_t items, uint32_t ipw, FirIn in, FirOut fo) {
+  constexpr int R = kF32R;
   constexpr int kWin = KPRE * kBlock;
-  __shared__ __attribute__((aligned(16))) float win[wpos(kWin) + 16];
+  __shared__ __attribute__((aligned(16))) float win[wpos(kWin) + 32];
   const int T1 = T - 1;
   const uint32_t i0 = blockIdx.x * ipw;
   if (i0 >= items) return;
   const uint32_t nseg = LONG ? (uint32_t)((T + kFirSeg - 1) / kFirSeg) : 1u;
   const uint32_t u0 = i0 * nseg, u1 = min(items, i0 + ipw) * nseg;
   const int tid = threadIdx.x;
-  const int base = tid * kF32R;                     // local output index of this lane
-  float* wl = win + wpos(tid);                      // wpos(tid + 256 k) = wpos(tid) + 320 k
+  const int base = tid * R;                         // local output index of this lane
+  const int jl = fir_stage_lane(tid);               // the row sample this thread stages
+  float* wl = win + wpos(jl);                       // wpos(jl + 256 k) = wpos(jl) + 320 k
   F32Win<KPRE, LONG> pre;
   FirUnit cur = fir_unit<LONG>(u0, nseg, nchunks, B, T);
-  fir_f32_fetch<KPRE, LONG>(pre, cur.it, src, hist_in, in, T1, tid);
+  fir_f32_fetch<KPRE, LONG>(pre, cur.it, src, hist_in, in, T1, jl);
   fir_f32_put<KPRE, LONG>(wl, pre);
-  float acc[8];
+  float acc[R];
   // Per unit: barrier (window ready) -> next window's loads -> MACs -> barrier (window free)
   // -> next window to LDS -> output stores.  The window write waits only for loads that had a
   // whole unit of MACs to land; the stores are issued after it, so no wait ever covers them.
@@ -239,56 +270,70 @@ __global__ __launch_bounds__(kBlock, LONG ? 6 : MI355X_FIR_F32_WAVES) void fir_f
     __syncthreads();
     const bool more = u + 1 < u1;
     const FirUnit nxt = more ? fir_unit<LONG>(u + 1, nseg, nchunks, B, T) : cur;
-    if (more) fir_f32_fetch<KPRE, LONG>(pre, nxt.it, src, hist_in, in, T1, tid);
+    if (more) fir_f32_fetch<KPRE, LONG>(pre, nxt.it, src, hist_in, in, T1, jl);
     if (base < cur.it.count) {
       if (cur.first) {
 #pragma unroll
-        for (int r = 0; r < 8; ++r) acc[r] = 0.0f;
+        for (int r = 0; r < R; ++r) acc[r] = 0.0f;
       }
       const int Ts = cur.Ts, rounds = Ts >> 3;
       F32Grp X0, X1, X2, X3;
       float c0[8], c1[8];
-      // Four group buffers rotate by name over a block of four rounds; the window pointer
-      // advances once per block, so every LDS read is base + immediate.  Coefficients are
-      // wave-uniform: scalar loads (s_load_dwordx8 per round) into SGPRs, the v_mul operand
-      // (no VGPRs, no LDS reads).
-      const float* wp = win + 10 * tid;
+      // Four group buffers rotate by name over a block of four rounds; round q uses buffers
+      // q .. q + R/8 and reads group q + R/8 + 1.  Coefficients are wave-uniform: scalar loads
+      // (s_load_dwordx8 per round) into SGPRs, the v_mul operand (no VGPRs, no LDS reads).
+      int g = base >> 3;                            // the lane's first group
       const float* const ci = coeffs + cur.it.f * in.cstride + cur.it.a;
       const float* cp = ci;
-      ld_grp(X0, wp, 0);
-      ld_grp(X1, wp, 1);
+      ld_grp(X0, win, g);
+      ld_grp(X1, win, g + 1);
+      if constexpr (R == 16) ld_grp(X2, win, g + 2);
       int nb = rounds >> 2;
       if (nb > 0) {
         do {
-          ld_coef(c0, cp, 0);
-          ld_grp(X2, wp, 2);
-          f32_round(acc, X0, X1, c0);
-          ld_coef(c1, cp, 8);
-          ld_grp(X3, wp, 3);
-          f32_round(acc, X1, X2, c1);
-          ld_coef(c0, cp, 16);
-          ld_grp(X0, wp, 4);
-          f32_round(acc, X2, X3, c0);
-          ld_coef(c1, cp, 24);
-          ld_grp(X1, wp, 5);
-          f32_round(acc, X3, X0, c1);
-          wp += 40;
+          if constexpr (R == 8) {
+            ld_coef(c0, cp, 0);  ld_grp(X2, win, g + 2); f32_round<FMA>(acc, X0, X1, X1, c0);
+            ld_coef(c1, cp, 8);  ld_grp(X3, win, g + 3); f32_round<FMA>(acc, X1, X2, X2, c1);
+            ld_coef(c0, cp, 16); ld_grp(X0, win, g + 4); f32_round<FMA>(acc, X2, X3, X3, c0);
+            ld_coef(c1, cp, 24); ld_grp(X1, win, g + 5); f32_round<FMA>(acc, X3, X0, X0, c1);
+          } else {
+            ld_coef(c0, cp, 0);  ld_grp(X3, win, g + 3); f32_round<FMA>(acc, X0, X1, X2, c0);
+            ld_coef(c1, cp, 8);  ld_grp(X0, win, g + 4); f32_round<FMA>(acc, X1, X2, X3, c1);
+            ld_coef(c0, cp, 16); ld_grp(X1, win, g + 5); f32_round<FMA>(acc, X2, X3, X0, c0);
+            ld_coef(c1, cp, 24); ld_grp(X2, win, g + 6); f32_round<FMA>(acc, X3, X0, X1, c1);
+          }
+          g += 4;
           cp += 32;
         } while (--nb);
       }
       // 0..3 remaining whole rounds, same buffer order
       const int rem = rounds & 3;
       if (rem > 0) {
-        ld_coef(c0, cp, 0);
-        ld_grp(X2, wp, 2);
-        f32_round(acc, X0, X1, c0);
-        if (rem > 1) {
-          ld_coef(c1, cp, 8);
-          ld_grp(X3, wp, 3);
-          f32_round(acc, X1, X2, c1);
-          if (rem > 2) {
-            ld_coef(c0, cp, 16);
-            f32_round(acc, X2, X3, c0);
+        if constexpr (R == 8) {
+          ld_coef(c0, cp, 0);
+          ld_grp(X2, win, g + 2);
+          f32_round<FMA>(acc, X0, X1, X1, c0);
+          if (rem > 1) {
+            ld_coef(c1, cp, 8);
+            ld_grp(X3, win, g + 3);
+            f32_round<FMA>(acc, X1, X2, X2, c1);
+            if (rem > 2) {
+              ld_coef(c0, cp, 16);
+              f32_round<FMA>(acc, X2, X3, X3, c0);
+            }
+          }
+        } else {
+          ld_coef(c0, cp, 0);
+          ld_grp(X3, win, g + 3);
+          f32_round<FMA>(acc, X0, X1, X2, c0);
+          if (rem > 1) {
+            ld_coef(c1, cp, 8);
+            ld_grp(X0, win, g + 4);
+            f32_round<FMA>(acc, X1, X2, X3, c1);
+            if (rem > 2) {
+              ld_coef(c0, cp, 16);
+              f32_round<FMA>(acc, X2, X3, X0, c0);
+            }
           }
         }
       }
@@ -296,7 +341,7 @@ __global__ __launch_bounds__(kBlock, LONG ? 6 : MI355X_FIR_F32_WAVES) void fir_f
       for (int k = 8 * rounds; k < Ts; ++k) {
         const float c = ci[k];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) acc[r] = acc[r] + win[wpos(base + k + r)] * c;
+        for (int r = 0; r < R; ++r) acc[r] = f32_mac<FMA>(acc[r], win[wpos(base + k + r)], c);
       }
     }
     if (more) {
@@ -308,17 +353,18 @@ __global__ __launch_bounds__(kBlock, LONG ? 6 : MI355X_FIR_F32_WAVES) void fir_f
       const bool run = fo.M == 1 && fo.L == 1 && fo.dir == 1;
       if (run) {                                    // contiguous outputs
         float* o = dst + it.f * fo.per_filter + fo.off + it.n0 + base;
-        if (((fo.per_filter | (uint64_t)fo.off) & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + 8 <= it.count) {
-          reinterpret_cast<float4*>(o)[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-          reinterpret_cast<float4*>(o)[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+        if (((fo.per_filter | (uint64_t)fo.off) & 3u) == 0 && ((uintptr_t)dst & 15u) == 0 && base + R <= it.count) {
+#pragma unroll
+          for (int q = 0; q < R / 4; ++q)
+            reinterpret_cast<float4*>(o)[q] = make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
         } else {
 #pragma unroll
-          for (int r = 0; r < 8; ++r)
+          for (int r = 0; r < R; ++r)
             if (base + r < it.count) o[r] = acc[r];
         }
       } else {                                      // decimator / reversed runs
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
+        for (int r = 0; r < R; ++r) {
           const uint32_t n = (uint32_t)(it.n0 + base + r);
           if (base + r < it.count && n % fo.M == 0)
             dst[(int64_t)(it.f * fo.per_filter) + fo.off + (int64_t)fo.dir * ((int64_t)(n / fo.M) * fo.L + fo.q)] =
@@ -837,14 +883,20 @@ __global__ void fir_hist_kernel(const T* __restrict__ src, T* __restrict__ hist,
 
 // One f32 FIR pass over `batch` filters (T <= kFirMaxTaps), outputs on the lattice `fo`.
 static void fir_f32_pass(const float* coeffs, int T, const float* src, float* dst, uint32_t B, uint32_t batch,
-                         const float* hist_in, FirIn in, FirOut fo, hipStream_t st) {
+                         const float* hist_in, FirIn in, FirOut fo, hipStream_t st, bool fma = false) {
   const uint32_t nchunks = (B + kF32Chunk - 1) / kF32Chunk;
   const uint32_t items = nchunks * batch;
   const int kpre = fir_f32_kpre(T < kFirSeg ? T : kFirSeg);
-  auto k = T > kFirSeg ? fir_f32_kernel<fir_f32_kpre(kFirSeg), true>
-         : kpre <= 9 ? fir_f32_kernel<9, false> : kpre == 10 ? fir_f32_kernel<10, false>
-         : kpre == 11 ? fir_f32_kernel<11, false> : kpre == 12 ? fir_f32_kernel<12, false>
-         : fir_f32_kernel<13, false>;
+  constexpr int K0 = fir_f32_kpre(1), KL = fir_f32_kpre(kFirSeg);     // 9..13 (R = 8), 17..21 (R = 16)
+  static_assert(KL - K0 == 4, "five window sizes");
+  auto pick = [&](auto fma_tag) {
+    constexpr bool F = decltype(fma_tag)::value;
+    return T > kFirSeg ? fir_f32_kernel<KL, true, F>
+         : kpre <= K0 ? fir_f32_kernel<K0, false, F> : kpre == K0 + 1 ? fir_f32_kernel<K0 + 1, false, F>
+         : kpre == K0 + 2 ? fir_f32_kernel<K0 + 2, false, F> : kpre == K0 + 3 ? fir_f32_kernel<K0 + 3, false, F>
+         : fir_f32_kernel<KL, false, F>;
+  };
+  auto k = fma ? pick(std::true_type{}) : pick(std::false_type{});
   uint32_t ipw = MI355X_FIR_IPW;
   if (T > kFirSeg) ipw = 1;                         // a long item is already many units
   if (!ipw) {
@@ -875,7 +927,7 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
   if (batch == 0 || B == 0) return hipSuccess;
   if (T_ < 1) return hipErrorInvalidValue;        // numTaps > kFirMaxTaps: tap segments
   const int T1 = T_ - 1;
-  const int chunk = kind == kFirF32 ? kF32Chunk : kFirChunk;
+  const int chunk = kind == kFirF32 || kind == kFirF32Fma ? kF32Chunk : kFirChunk;
   const uint32_t nchunks = (B + chunk - 1) / chunk;
   const uint64_t items64 = (uint64_t)nchunks * batch;
   if (items64 > 0xFFFFFFFFull) return hipErrorInvalidValue;
@@ -887,7 +939,7 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
   if (T1 > 0 && (int64_t)B < T1) {
     hipError_t e = hipMallocAsync((void**)&tmp, sizeof(T) * (size_t)batch * T1, st);
     if (e != hipSuccess) return e;
-    e = hipMemcpyAsync(tmp, hist, sizeof(T) * (size_t)batch * T1, hipMemcpyDeviceToDevice, st);
+    e = hipMemcpyAsync(tmp, hist, sizeof(T) * (size_t)batch * T1, hipMemcpyDefault, st);
     if (e != hipSuccess) return e;
     hist_in = tmp;
   }
@@ -901,15 +953,16 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
     if (s0 < d0 + bytes && d0 < s0 + bytes) {
       hipError_t e = hipMallocAsync((void**)&src_copy, bytes, st);
       if (e != hipSuccess) return e;
-      e = hipMemcpyAsync(src_copy, src, bytes, hipMemcpyDeviceToDevice, st);
+      e = hipMemcpyAsync(src_copy, src, bytes, hipMemcpyDefault, st);
       if (e != hipSuccess) return e;
       src = src_copy;
     }
   }
   switch (kind) {
-    case kFirF32: {
+    case kFirF32:
+    case kFirF32Fma: {
       fir_f32_pass((const float*)coeffs, T_, (const float*)src, (float*)dst, B, batch, (const float*)hist_in,
-                   FirIn{B, B, 0, 1u, 0}, FirOut{1u, 1u, 0u, 1, 0, (uint64_t)B}, st);
+                   FirIn{B, B, 0, 1u, 0}, FirOut{1u, 1u, 0u, 1, 0, (uint64_t)B}, st, kind == kFirF32Fma);
       break;
     }
     case kFirQ15:
@@ -950,6 +1003,7 @@ hipError_t fir_run(int kind, const void* coeffs, int num_taps, const void* src, 
                    uint32_t batch, void* hist, hipStream_t st) {
   switch (kind) {
     case kFirF32:
+    case kFirF32Fma:
       return fir_launch<float>(kind, (const float*)coeffs, num_taps, (const float*)src, (float*)dst, block_size,
                                batch, (float*)hist, st);
     case kFirQ15:
@@ -1233,7 +1287,7 @@ static hipError_t mr_launch(const E* src, E* dst, size_t out_words, uint32_t B, 
   if (H > 0 && (int64_t)start < H) {
     hipError_t e = hipMallocAsync((void**)&tmp, sizeof(E) * (size_t)batch * H, st);
     if (e != hipSuccess) return e;
-    e = hipMemcpyAsync(tmp, hist, sizeof(E) * (size_t)batch * H, hipMemcpyDeviceToDevice, st);
+    e = hipMemcpyAsync(tmp, hist, sizeof(E) * (size_t)batch * H, hipMemcpyDefault, st);
     if (e != hipSuccess) return e;
     hist_in = tmp;
   }
@@ -1244,7 +1298,7 @@ static hipError_t mr_launch(const E* src, E* dst, size_t out_words, uint32_t B, 
     if (s0 < d0 + ob && d0 < s0 + ib) {
       hipError_t e = hipMallocAsync((void**)&src_copy, ib, st);
       if (e != hipSuccess) return e;
-      e = hipMemcpyAsync(src_copy, src, ib, hipMemcpyDeviceToDevice, st);
+      e = hipMemcpyAsync(src_copy, src, ib, hipMemcpyDefault, st);
       if (e != hipSuccess) return e;
       src = src_copy;
     }

@@ -62,7 +62,8 @@ hipError_t rfft_q15_pass_launch(bool inverse, int n, const int16_t* src, int16_t
 // FIR: `batch` independent filters sharing one coefficient set, any of the five reference
 // variants (kind).  hist: [batch][numTaps-1] streaming state (read, then overwritten with
 // the new tail).  Element type: f32 float, q15/fast_q15 int16, q31/fast_q31 int32, q7 int8.
-enum FirKind { kFirF32 = 0, kFirQ15 = 1, kFirQ31 = 2, kFirFastQ15 = 3, kFirFastQ31 = 4, kFirQ7 = 5 };
+enum FirKind { kFirF32 = 0, kFirQ15 = 1, kFirQ31 = 2, kFirFastQ15 = 3, kFirFastQ31 = 4, kFirQ7 = 5,
+               kFirF32Fma = 6 };   // kFirF32Fma: the opt-in fused-multiply-add f32 path (tolerance)
 hipError_t fir_run(int kind, const void* coeffs, int num_taps, const void* src, void* dst, uint32_t block_size,
                    uint32_t batch, void* hist, hipStream_t st);
 
@@ -104,6 +105,12 @@ hipError_t mfcc_f32_pre_launch(int n, const float* src, const float* win, float*
 hipError_t mfcc_q31_pre_launch(int n, const int32_t* src, const int32_t* win, int32_t* x, int32_t* maxv,
                                uint32_t batch, int maxv_stride, hipStream_t st);
 size_t mfcc_q31_post_lds(int n, int nb_mel);
+// MFCC q31 / q15 in one launch (frames in LDS: pre, the inner CFFT, post); hipErrorInvalidValue
+// when the length or the LDS footprint is not supported (callers take the three-launch path).
+template <typename T>
+hipError_t mfcc_fx_fused_launch(int n, const T* src, const T* win, const void* ctw, int brev, const int4* stw,
+                                int nb_mel, const T* coefs, const uint32_t* bf, int total, int nb_dct, const T* dct,
+                                const int32_t* lut, T* dst, uint32_t batch, hipStream_t st);
 hipError_t mfcc_q15_pre_launch(int n, const int16_t* src, const int16_t* win, int16_t* x, int16_t* maxv,
                                uint32_t batch, int maxv_stride, hipStream_t st);
 hipError_t mfcc_q15_post_launch(int n, const int16_t* y, const int4* tw, const int16_t* maxv, int maxv_stride, int nb_mel,

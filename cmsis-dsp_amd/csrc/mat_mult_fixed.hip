@@ -52,12 +52,28 @@ template <typename T> struct I8Cfg;
 #ifndef MI355X_I8_SCHED
 #define MI355X_I8_SCHED 6
 #endif
-#ifndef MI355X_I8_KT15
-#define MI355X_I8_KT15 64
-#endif
-template <> struct I8Cfg<int16_t> { static constexpr int BM = 128, BN = 128, WBM = 1, WBN = 2, KT = MI355X_I8_KT15; };
+template <> struct I8Cfg<int16_t> { static constexpr int BM = 128, BN = 128, WBM = 1, WBN = 2, KT = 64; };
 template <> struct I8Cfg<int32_t> { static constexpr int BM = 128, BN = 64, WBM = 1, WBN = 1, KT = 64; };
 constexpr int kNT2 = 512, kWavesM = 4, kWavesN = 2;
+
+// LDS plane layout: rows of 64 k-bytes (4 chunks of 16 B) with no padding; chunk c of row
+// `row` sits at chunk c ^ ((row >> 2) & 3), and B's column `col` at row col ^ ((col >> CWL) & 1)
+// (CWL = log2 of the columns one staging thread owns).  Conflict free for every access
+// (MI355X_MICROARCH.md §LDS):
+//  * fragment reads (ds_read_b128, 16-lane groups {0-3,12-15,20-27}, ..., banks mod 64): the 16
+//    rows of a group hold (row mod 4, swizzled chunk) pairs that are all distinct, i.e. 16
+//    distinct 4-bank sets (B's row permutation only swaps rows within such groups);
+//  * A staging (ds_write_b128, 8 contiguous lanes, banks mod 32): two consecutive rows x 4
+//    chunks -- the rows' parities differ, so the 16-dword halves do;
+//  * B staging (ds_write_b32, 32-lane groups, banks mod 32): lanes 0-15 and 16-31 write 16
+//    k-dwords of columns CW apart, whose rows the column permutation gives opposite parities.
+// (Round 2's 80-byte pitch left both staging writes two-way conflicted: 12.5 M / 54.8 M conflict
+// cycles per launch for q15 / q31, profiles/r02/mat_mult_q15|q31/pmc.json.)
+__device__ __forceinline__ int i8_chunk(int row, int c) { return (c ^ (row >> 2)) & 3; }
+template <int CW> __device__ __forceinline__ int i8_brow(int col) {
+  constexpr int L = CW == 8 ? 3 : CW == 4 ? 2 : CW == 2 ? 1 : 0;
+  return col ^ ((col >> L) & 1);
+}
 
 // plane p of the two q15 values in each of d0, d1: [d0.lo, d0.hi, d1.lo, d1.hi] byte p
 template <int P>
@@ -81,7 +97,8 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
   using G = I8Cfg<T>;
   constexpr int P = Slices<T>::P, S = 2 * P - 1;
   constexpr int64_t C0 = Slices<T>::C0;
-  constexpr int BM = G::BM, BN = G::BN, WBM = G::WBM, WBN = G::WBN, kKT2 = G::KT, kPitch2 = kKT2 + 16;
+  constexpr int BM = G::BM, BN = G::BN, WBM = G::WBM, WBN = G::WBN, kKT2 = G::KT, kPitch2 = kKT2;
+  static_assert(kKT2 == 64, "the LDS swizzle assumes 4 chunks of 16 k-bytes per row");
   static_assert(BM == kWavesM * 32 * WBM && BN == kWavesN * 32 * WBN, "wave grid covers the tile");
   constexpr int EPD = 4 / sizeof(T);             // elements per dword
   constexpr int AK = BM * kKT2 / kNT2;           // A elements per staging thread (16)
@@ -215,13 +232,15 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
       }
 #pragma unroll
       for (int q = 0; q < AK / 16; ++q)
-        *reinterpret_cast<uint4*>(&As[p][ar][ak0 + 16 * q]) = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+        *reinterpret_cast<uint4*>(&As[p][ar][16 * i8_chunk(ar, ak0 / 16 + q)]) =
+            make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 #pragma unroll
       for (int c = 0; c < CW; ++c) {
         const int d = c / EPD, o = (c % EPD) * (int)sizeof(T) + p;
         uint32_t g = gather4(bd[0][d], bd[1][d], bd[2][d], bd[3][d], o);
         if (p != P - 1) g ^= 0x80808080u;
-        *reinterpret_cast<uint32_t*>(&Bs[p][bg * CW + c][4 * bq]) = g;
+        const int row = i8_brow<CW>(bg * CW + c);
+        *reinterpret_cast<uint32_t*>(&Bs[p][row][16 * i8_chunk(row, bq >> 2) + 4 * (bq & 3)]) = g;
       }
     }
   };
@@ -235,11 +254,15 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
 #pragma unroll
       for (int p = 0; p < P; ++p) {
 #pragma unroll
-        for (int i = 0; i < WBM; ++i)
-          fa[kk][p][i] = *reinterpret_cast<const i32x4*>(&As[p][wm * 32 * WBM + i * 32 + r][32 * kk + 16 * h]);
+        for (int i = 0; i < WBM; ++i) {
+          const int row = wm * 32 * WBM + i * 32 + r;
+          fa[kk][p][i] = *reinterpret_cast<const i32x4*>(&As[p][row][16 * i8_chunk(row, 2 * kk + h)]);
+        }
 #pragma unroll
-        for (int j = 0; j < WBN; ++j)
-          fb[kk][p][j] = *reinterpret_cast<const i32x4*>(&Bs[p][wn * 32 * WBN + j * 32 + r][32 * kk + 16 * h]);
+        for (int j = 0; j < WBN; ++j) {
+          const int row = i8_brow<CW>(wn * 32 * WBN + j * 32 + r);
+          fb[kk][p][j] = *reinterpret_cast<const i32x4*>(&Bs[p][row][16 * i8_chunk(row, 2 * kk + h)]);
+        }
       }
   };
   auto mma = [&]() {

@@ -16,6 +16,9 @@
 // (only m = 1 reaches a count of 32).
 #include "common.hpp"
 #include "kernels.hpp"
+#include "cfft_fixed_core.hpp"
+
+#include <type_traits>
 
 namespace mi355x {
 
@@ -130,8 +133,13 @@ __device__ __forceinline__ int32_t mq_log(uint32_t src) {
 }
 
 
-// LDS per wave (int32 words): |X_k| (fftLen/2 + 1), Mel values (nb_mel), then int64 Mel sums.
-__host__ __device__ inline int mq_wave_words(int n, int nb_mel) { return ((n / 2 + 1 + nb_mel + 1) & ~1) + 2 * nb_mel; }
+// LDS per wave (int32 words): |X_k| (fftLen/2 + 1, at mq_mpad(k)), Mel values (nb_mel), then
+// int64 Mel sums.  mq_mpad(k) = k + k / 16: the magnitudes are written in the CFFT's storage
+// order (bit-reversed bins in the fused kernels, 16 apart per 32-lane group) and read by the Mel
+// sums at lane strides of a slice length; the pad keeps both on distinct banks.
+__host__ __device__ inline int mq_mpad(int k) { return k + (k >> 4); }
+__host__ __device__ inline int mq_mag_words(int n) { return mq_mpad(n / 2) + 1; }
+__host__ __device__ inline int mq_wave_words(int n, int nb_mel) { return ((mq_mag_words(n) + nb_mel + 1) & ~1) + 2 * nb_mel; }
 
 // The Mel sums spread over the wave: the filters' coefficients as one flat list (bf[g] =
 // bin << 16 | filter), lane t summing the contiguous slice t of it and adding each filter's
@@ -144,24 +152,27 @@ __host__ __device__ inline int mq_wave_words(int n, int nb_mel) { return ((n / 2
 // branch), with the k-th twiddle record tw[k] = {A[2mk], A[2mk+1], B[2mk], B[2mk+1]} (m = the
 // instance's twidCoefRModifier; built contiguous on the host, so the loads coalesce): the
 // post kernels take the magnitudes straight from the CFFT output, with no 2N-word spectrum.
-__device__ __forceinline__ int2 mq_split_q31(const int2* x, int k, int L, int4 t) {
+// get(i) returns CFFT bin i (global memory in the three-launch path, LDS in the fused kernels).
+template <typename Get>
+__device__ __forceinline__ int2 mq_split_q31(Get get, int k, int L, int4 t) {
   if (k == 0 || k == L) {
-    const int2 v = x[0];
+    const int2 v = get(0);
     return make_int2((k == 0 ? wadd(v.x, v.y) : wsub(v.x, v.y)) >> 1, 0);
   }
-  const int2 a = x[k], b = x[L - k];
+  const int2 a = get(k), b = get(L - k);
   int32_t re = mult_R(a.x, t.x), im = mult_R(a.x, t.y);
   re = multSub_R(re, a.y, t.y); im = multAcc_R(im, a.y, t.x);
   re = multSub_R(re, b.y, t.y); im = multSub_R(im, b.y, t.z);
   re = multAcc_R(re, b.x, t.z); im = multSub_R(im, b.x, t.y);
   return make_int2(re, im);
 }
-__device__ __forceinline__ int2 mq_split_q15(const short2* x, int k, int L, int4 t) {
+template <typename Get>   // get(i): bin i as int2 of sign-extended q15 words
+__device__ __forceinline__ int2 mq_split_q15(Get get, int k, int L, int4 t) {
   if (k == 0 || k == L) {
-    const short2 v = x[0];
+    const int2 v = get(0);
     return make_int2((k == 0 ? v.x + v.y : v.x - v.y) >> 1, 0);
   }
-  const short2 a = x[k], b = x[L - k];
+  const int2 a = get(k), b = get(L - k);
   auto p = [](int32_t u, int32_t v) { return (uint32_t)(u * v); };
   const int32_t re = (int32_t)(p(a.x, t.x) - p(a.y, t.y) + p(b.x, t.z) + p(b.y, t.w)) >> 16;
   const int32_t im = (int32_t)(p(b.x, t.w) - p(b.y, t.z) + p(a.y, t.x) + p(a.x, t.y)) >> 16;
@@ -182,18 +193,21 @@ __device__ __forceinline__ void mq_wave_sync() {
 __host__ __device__ inline int mq_tab_words(int total, int nb_mel, int nb_dct) {
   return (2 * total + nb_mel * nb_dct + 3) & ~3;
 }
+// int32 words of the fused kernel's frame image: TPB = 4096 / L frames of SP complex, 16-B rounded
+template <typename T, int L> __host__ __device__ constexpr int mq_fused_frame_words() {
+  return (int)(((4096 / L) * (L + (L / 16 <= 4 ? 1 : 0)) * 2 * sizeof(T) / 4 + 3) & ~3);
+}
 
-template <typename T, typename Split, typename Mag, typename Term, typename Fin, typename Dct>
-__device__ __forceinline__ void mq_post_body(const T* __restrict__ y, const int4* __restrict__ tw, const T* maxv,
-                                             int maxv_stride, int n, int nb_mel, const T* __restrict__ coefs,
-                                             const uint32_t* __restrict__ bf, int total, int nb_dct,
-                                             const T* __restrict__ dct, const int32_t* __restrict__ lut, T* dst,
-                                             uint32_t batch, int stage, Split split, Mag magf, Term term, Fin fin,
-                                             Dct dctf) {
-  extern __shared__ int32_t shq[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int lim = (n >> 1) + 1;
-  int32_t* tab = shq;
+// The frame-invariant tables a workgroup reads: staged in LDS (shq) when `stage`, else global.
+struct MqTabs {
+  const uint32_t* bf;       // flat Mel list: bin << 16 | filter
+  const int32_t* cf;        // staged coefficients (stage) ...
+  const int32_t* dc;        // ... and DCT rows
+  bool stage;
+};
+template <typename T>
+__device__ __forceinline__ MqTabs mq_stage_tables(int32_t* tab, const T* __restrict__ coefs, const uint32_t* __restrict__ bf,
+                                                  int total, int nb_mel, int nb_dct, const T* __restrict__ dct, int stage) {
   if (stage) {
     for (int i = threadIdx.x; i < total; i += blockDim.x) {
       tab[i] = (int32_t)bf[i];
@@ -202,51 +216,140 @@ __device__ __forceinline__ void mq_post_body(const T* __restrict__ y, const int4
     for (int i = threadIdx.x; i < nb_mel * nb_dct; i += blockDim.x) tab[2 * total + i] = (int32_t)dct[i];
   }
   __syncthreads();
+  return MqTabs{stage ? reinterpret_cast<const uint32_t*>(tab) : bf, tab + total, tab + 2 * total, stage != 0};
+}
+
+// One frame on one wave, from the CFFT output get(i) (i < L = n/2) and the frame maximum m:
+// |X_k| for k <= L (split + magnitude) into mag, the Mel sums (int64 LDS totals, acc), the
+// per-filter finish (fin) into mel, the DCT rows into o.  mag / mel / acc are the wave's own.
+// kmap(p) = the bin lanes take at step p (p < fftLen/2): the CFFT's storage order, so the reads
+// get(k), get(L - k) of a step are conflict free (bin L, from get(0) only, comes last).
+template <typename T, typename Ops, typename Get, typename KMap>
+__device__ __forceinline__ void mq_post_frame(const Ops& op, Get get, KMap kmap, const int4* __restrict__ tw, int n,
+                                              int32_t m, T* o,
+                                              int nb_mel, int nb_dct, int total, const MqTabs& tb,
+                                              const T* __restrict__ coefs, const T* __restrict__ dct, int32_t lutv,
+                                              int32_t* mag, int32_t* mel, int64_t* acc) {
+  const int lane = threadIdx.x & 63;
+  const int lim = (n >> 1) + 1;
+  auto coef = [&](int g) { return tb.stage ? tb.cf[g] : (int32_t)coefs[g]; };
+  auto dctw = [&](int i) { return tb.stage ? tb.dc[i] : (int32_t)dct[i]; };
+  for (int i = lane; i < nb_mel; i += 64) acc[i] = 0;
+  const int L = lim - 1;
+#pragma unroll 4
+  for (int p0 = 0; p0 < L; p0 += 64) {                 // uniform: the shuffle needs all lanes
+    const int p = p0 + lane, k = kmap(min(p, L - 1));
+    const int32_t v = op.mag(op.split(get, k, L, tw[k]), lutv);
+    if (p < L) mag[mq_mpad(k)] = v;
+  }
+  {
+    const int32_t v = op.mag(op.split(get, L, L, tw[L]), lutv);   // bin L (every lane: the shuffle)
+    if (lane == 0) mag[mq_mpad(L)] = v;
+  }
+  mq_wave_sync();
+  {   // the Mel sums over the flat list (see mq_mel_sums)
+    const int per = (total + 63) >> 6;
+    const int g0 = lane * per, g1 = min(total, g0 + per);
+    int cur = -1;
+    int64_t r = 0;
+    for (int g = g0; g < g1; ++g) {
+      const uint32_t e = tb.bf[g];
+      const int f = (int)(e & 0xFFFFu);
+      if (f != cur) {
+        if (cur >= 0) atomicAdd(reinterpret_cast<unsigned long long*>(acc + cur), (unsigned long long)r);
+        cur = f;
+        r = 0;
+      }
+      r += op.term(mag[mq_mpad((int)(e >> 16))], coef(g));
+    }
+    if (cur >= 0) atomicAdd(reinterpret_cast<unsigned long long*>(acc + cur), (unsigned long long)r);
+  }
+  mq_wave_sync();
+  for (int i = lane; i < nb_mel; i += 64) mel[i] = op.fin(acc[i], m);
+  mq_wave_sync();
+  for (int r = lane; r < nb_dct; r += 64) o[r] = op.dct(r, mel, dctw);
+  mq_wave_sync();                                      // mel / acc reused by the next frame
+}
+
+// The three-launch path's post kernel: frames' CFFT outputs in global memory (y), maxima in maxv.
+template <typename T, typename Ops>
+__device__ __forceinline__ void mq_post_body(const Ops& op, const T* __restrict__ y, const int4* __restrict__ tw,
+                                             const T* maxv, int maxv_stride, int n, int nb_mel,
+                                             const T* __restrict__ coefs, const uint32_t* __restrict__ bf, int total,
+                                             int nb_dct, const T* __restrict__ dct, const int32_t* __restrict__ lut,
+                                             T* dst, uint32_t batch, int stage) {
+  extern __shared__ int32_t shq[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lim = (n >> 1) + 1;
+  const MqTabs tb = mq_stage_tables<T>(shq, coefs, bf, total, nb_mel, nb_dct, dct, stage);
   int32_t* mag = shq + (stage ? mq_tab_words(total, nb_mel, nb_dct) : 0) + wave * mq_wave_words(n, nb_mel);
-  int32_t* mel = mag + lim;
-  int64_t* acc = reinterpret_cast<int64_t*>(mag + ((lim + nb_mel + 1) & ~1));
-  const uint32_t* bfp = stage ? reinterpret_cast<const uint32_t*>(tab) : bf;
-  auto coef = [&](int g) { return stage ? tab[total + g] : (int32_t)coefs[g]; };
-  auto dctw = [&](int i) { return stage ? tab[2 * total + i] : (int32_t)dct[i]; };
+  int32_t* mel = mag + mq_mag_words(n);
+  int64_t* acc = reinterpret_cast<int64_t*>(mag + ((mq_mag_words(n) + nb_mel + 1) & ~1));
   const int32_t lutv = lut[lane & 31];
+  (void)lim;
   for (int it = 0; it < kMqFpw; ++it) {
     const uint32_t frame = (blockIdx.x * kMqFpw + it) * kMqWaves + wave;
     if (frame >= batch) break;                         // wave-uniform: no workgroup barrier below
     const int32_t m = (int32_t)maxv[(size_t)frame * maxv_stride];
-    for (int i = lane; i < nb_mel; i += 64) acc[i] = 0;
     const T* X = y + (size_t)frame * n;                // CFFT output, L complex
-#pragma unroll 4
-    for (int k0 = 0; k0 < lim; k0 += 64) {             // uniform: the shuffle needs all lanes
-      const int k = k0 + lane, kc = min(k, lim - 1);
-      const int32_t v = magf(split(X, kc, lim - 1, tw[kc]), lutv);
-      if (k < lim) mag[k] = v;
-    }
-    mq_wave_sync();
-    {   // the Mel sums over the flat list (see mq_mel_sums)
-      const int per = (total + 63) >> 6;
-      const int g0 = lane * per, g1 = min(total, g0 + per);
-      int cur = -1;
-      int64_t r = 0;
-      for (int g = g0; g < g1; ++g) {
-        const uint32_t e = bfp[g];
-        const int f = (int)(e & 0xFFFFu);
-        if (f != cur) {
-          if (cur >= 0) atomicAdd(reinterpret_cast<unsigned long long*>(acc + cur), (unsigned long long)r);
-          cur = f;
-          r = 0;
-        }
-        r += term(mag[e >> 16], coef(g));
-      }
-      if (cur >= 0) atomicAdd(reinterpret_cast<unsigned long long*>(acc + cur), (unsigned long long)r);
-    }
-    mq_wave_sync();
-    for (int i = lane; i < nb_mel; i += 64) mel[i] = fin(acc[i], m);
-    mq_wave_sync();
-    T* o = dst + (size_t)frame * nb_dct;
-    for (int r = lane; r < nb_dct; r += 64) o[r] = dctf(r, mel, dctw);
-    mq_wave_sync();                                    // mel / acc reused by the next frame
+    auto get = [X](int i) {
+      if constexpr (sizeof(T) == 4) return reinterpret_cast<const int2*>(X)[i];
+      else { const short2 v = reinterpret_cast<const short2*>(X)[i]; return make_int2(v.x, v.y); }
+    };
+    mq_post_frame<T>(op, get, [](int p) { return p; }, tw, n, m, dst + (size_t)frame * nb_dct, nb_mel, nb_dct, total,
+                     tb, coefs, dct, lutv, mag, mel, acc);
   }
 }
+
+// The q31 chain of arm_mfcc_q31.c:119-223 as per-element operations (shared by the post kernel
+// and the fused kernel): pre = arm_absmax_q31 / arm_divide_q31 / arm_scale_q31 / arm_mult_q31,
+// post = arm_split_rfft_q31 + arm_cmplx_mag_q31, arm_dot_prod_q31, the Mel finish, the DCT rows.
+struct MqOpsQ31 {
+  int32_t le;      // log exponent (fftShift + 2 + SHIFT_MELFILTER_SATURATION_Q31) * LOG2TOLOG_Q31
+  int nb_mel;
+  __device__ MqOpsQ31(int n, int nm, int /*nd*/)
+      : le((int32_t)((uint32_t)(31 - (int)mq_clz((uint32_t)n) + 12) * 0x02C5C860u)), nb_mel(nm) {}
+  static constexpr int32_t kFull = 0x7FFFFFFF;
+  __device__ static int32_t sat_abs(int32_t x) { return mq_sat_abs(x); }
+  // arm_divide_q31(0x7FFFFFFF, m): both positive, temp = (num << 31) / den, normalised to 32 bits;
+  // k = (int8_t)(shift + 1), the arm_scale_q31 exponent
+  __device__ static void divide(int32_t m, int32_t& quot, int& k) {
+    int64_t t = (int64_t)(((uint64_t)0x7FFFFFFF << 31) / (uint64_t)m);
+    const int sn = 32 - (int)mq_clz((uint32_t)(t >> 31));
+    int sh = 0;
+    if (sn > 0) {
+      sh = sn;
+      t >>= sn;
+    }
+    quot = (int32_t)t;
+    k = (int)(int8_t)(sh + 1);
+  }
+  __device__ static int32_t pre(int32_t x, int32_t w, bool scale, int32_t quot, int k) {
+    if (scale) x = mq_scale(x, quot, k);
+    return mq_shl(mq_ssat31(mq_hi(x, w)), 1);          // arm_mult_q31: __SSAT((a*b) >> 32, 31) << 1
+  }
+  template <typename Get> __device__ int2 split(Get get, int k, int L, int4 t) const { return mq_split_q31(get, k, L, t); }
+  __device__ int32_t mag(int2 c, int32_t lutv) const {   // arm_cmplx_mag_q31
+    const int32_t a0 = (int32_t)(((int64_t)c.x * c.x) >> 33), a1 = (int32_t)(((int64_t)c.y * c.y) >> 33);
+    return mq_sqrt(a0 + a1, lutv);
+  }
+  __device__ int64_t term(int32_t a, int32_t c) const { return ((int64_t)a * c) >> 14; }   // arm_dot_prod_q31
+  __device__ int32_t fin(int64_t r, int32_t m) const {
+    r += 0x08637BD0;                                 // MICRO_Q31
+    r >>= 28;                                        // SHIFT_MELFILTER_SATURATION_Q31 + 18
+    int32_t v = mq_ssat31((int32_t)r);               // __SSAT takes the low 32 bits
+    if (m != 0 && m != 0x7FFFFFFF) v = mq_scale(v, m, 1);   // arm_scale_q31(., m, 0)
+    v = mq_log((uint32_t)v);
+    const int64_t s = (int64_t)v + le;               // arm_offset_q31 (saturating)
+    v = s > INT32_MAX ? INT32_MAX : (s < INT32_MIN ? INT32_MIN : (int32_t)s);
+    return v >> 3;                                   // arm_shift_q31(., -3)
+  }
+  template <typename W> __device__ int32_t dct(int r, const int32_t* mel, W dctw) const {   // arm_mat_vec_mult_q31
+    int64_t sum = 0;
+    for (int i = 0; i < nb_mel; ++i) sum += (int64_t)dctw(r * nb_mel + i) * mel[i];
+    return (int32_t)(sum >> 31);
+  }
+};
 
 __global__ __launch_bounds__(256) void mfcc_q31_post_kernel(const int32_t* __restrict__ y, const int4* __restrict__ tw,
                                                             const int32_t* maxv, int maxv_stride, int n, int nb_mel,
@@ -255,31 +358,8 @@ __global__ __launch_bounds__(256) void mfcc_q31_post_kernel(const int32_t* __res
                                                             const int32_t* __restrict__ dct,
                                                             const int32_t* __restrict__ lut, int32_t* dst,
                                                             uint32_t batch, int stage) {
-  // log exponent (fftShift + 2 + SHIFT_MELFILTER_SATURATION_Q31) * LOG2TOLOG_Q31
-  const int32_t le = (int32_t)((uint32_t)(31 - (int)mq_clz((uint32_t)n) + 12) * 0x02C5C860u);
-  mq_post_body<int32_t>(
-      y, tw, maxv, maxv_stride, n, nb_mel, coefs, bf, total, nb_dct, dct, lut, dst, batch, stage,
-      [](const int32_t* x, int k, int L, int4 t) { return mq_split_q31(reinterpret_cast<const int2*>(x), k, L, t); },
-      [](int2 c, int32_t lutv) {                       // arm_cmplx_mag_q31
-        const int32_t a0 = (int32_t)(((int64_t)c.x * c.x) >> 33), a1 = (int32_t)(((int64_t)c.y * c.y) >> 33);
-        return mq_sqrt(a0 + a1, lutv);
-      },
-      [](int32_t a, int32_t c) { return ((int64_t)a * c) >> 14; },    // arm_dot_prod_q31
-      [le](int64_t r, int32_t m) {
-        r += 0x08637BD0;                                 // MICRO_Q31
-        r >>= 28;                                        // SHIFT_MELFILTER_SATURATION_Q31 + 18
-        int32_t v = mq_ssat31((int32_t)r);               // __SSAT takes the low 32 bits
-        if (m != 0 && m != 0x7FFFFFFF) v = mq_scale(v, m, 1);   // arm_scale_q31(., m, 0)
-        v = mq_log((uint32_t)v);
-        const int64_t s = (int64_t)v + le;               // arm_offset_q31 (saturating)
-        v = s > INT32_MAX ? INT32_MAX : (s < INT32_MIN ? INT32_MIN : (int32_t)s);
-        return v >> 3;                                   // arm_shift_q31(., -3)
-      },
-      [nb_mel](int r, const int32_t* mel, auto dctw) {  // arm_mat_vec_mult_q31
-        int64_t sum = 0;
-        for (int i = 0; i < nb_mel; ++i) sum += (int64_t)dctw(r * nb_mel + i) * mel[i];
-        return (int32_t)(sum >> 31);
-      });
+  mq_post_body<int32_t>(MqOpsQ31(n, nb_mel, nb_dct), y, tw, maxv, maxv_stride, n, nb_mel, coefs, bf, total, nb_dct, dct, lut,
+                        dst, batch, stage);
 }
 
 // ---------------------------------------------------------------- q15
@@ -336,6 +416,54 @@ __global__ __launch_bounds__(256) void mfcc_q15_pre_kernel(const int16_t* src, c
   if (lane == 0) maxv[(size_t)frame * maxv_stride] = (int16_t)m;
 }
 
+struct MqOpsQ15 {
+  int32_t le;
+  int nb_mel, nb_dct;
+  __device__ MqOpsQ15(int n, int nm, int nd)
+      : le((int32_t)((uint32_t)(31 - (int)mq_clz((uint32_t)n) + 12) * 0x02C5C860u)), nb_mel(nm), nb_dct(nd) {}
+  static constexpr int32_t kFull = 0x7FFF;
+  __device__ static int32_t sat_abs(int32_t x) { return mq_sat_abs15(x); }
+  // arm_divide_q15(0x7FFF, m): temp = (0x7FFF << 15) / m, normalised by 17 - clz(temp); k = 15 - shift
+  __device__ static void divide(int32_t m, int32_t& quot, int& k) {
+    int32_t t = (int32_t)((0x7FFFu << 15) / (uint32_t)m);
+    const int sn = 17 - (int)mq_clz((uint32_t)t);
+    int sh = 0;
+    if (sn > 0) {
+      sh = sn;
+      t >>= sn;
+    }
+    quot = (int32_t)(int16_t)t;
+    k = (int)(int8_t)(15 - sh);
+  }
+  __device__ static int32_t pre(int32_t x, int32_t w, bool scale, int32_t quot, int k) {
+    if (scale) x = mq_ssat16((x * quot) >> k);       // arm_scale_q15
+    return mq_ssat16((x * w) >> 15);                  // arm_mult_q15
+  }
+  template <typename Get> __device__ int2 split(Get get, int k, int L, int4 t) const { return mq_split_q15(get, k, L, t); }
+  __device__ int32_t mag(int2 c, int32_t lutv) const {   // arm_cmplx_mag_q15
+    const uint32_t s2 = ((uint32_t)(c.x * c.x) + (uint32_t)(c.y * c.y)) >> 1;
+    return mq_sqrt((int32_t)s2, lutv) >> 16;
+  }
+  __device__ int64_t term(int32_t a, int32_t c) const { return (int64_t)(a * c); }   // arm_dot_prod_q15
+  __device__ int32_t fin(int64_t r, int32_t m) const {
+    r += 0x219;                                      // MICRO_Q15
+    r >>= 10;                                        // SHIFT_MELFILTER_SATURATION_Q15
+    int32_t v = mq_ssat31((int32_t)r);
+    if (m != 0 && m != 0x7FFF) v = mq_scale(v, (int32_t)((uint32_t)m << 16), 1);
+    const int64_t s = (int64_t)mq_log((uint32_t)v) + le;
+    v = s > INT32_MAX ? INT32_MAX : (s < INT32_MIN ? INT32_MIN : (int32_t)s);
+    return (int32_t)(int16_t)(v >> 19);              // (q15_t) truncation
+  }
+  template <typename W> __device__ int16_t dct(int r, const int32_t* mel, W dctw) const {   // arm_mat_vec_mult_q15
+    const int paired = r < (nb_dct & ~3) ? (nb_mel & ~1) : (nb_mel & ~3);
+    int64_t sum = 0;
+    for (int i = 0; i < paired; i += 2)
+      sum += (int32_t)((uint32_t)(dctw(r * nb_mel + i) * mel[i]) + (uint32_t)(dctw(r * nb_mel + i + 1) * mel[i + 1]));
+    for (int i = paired; i < nb_mel; ++i) sum += (int64_t)(dctw(r * nb_mel + i) * mel[i]);
+    return (int16_t)mq_ssat16((int32_t)(sum >> 15));
+  }
+};
+
 __global__ __launch_bounds__(256) void mfcc_q15_post_kernel(const int16_t* __restrict__ y, const int4* __restrict__ tw,
                                                             const int16_t* maxv, int maxv_stride, int n, int nb_mel,
                                                             const int16_t* __restrict__ coefs,
@@ -343,33 +471,133 @@ __global__ __launch_bounds__(256) void mfcc_q15_post_kernel(const int16_t* __res
                                                             const int16_t* __restrict__ dct,
                                                             const int32_t* __restrict__ lut, int16_t* dst,
                                                             uint32_t batch, int stage) {
-  const int32_t le = (int32_t)((uint32_t)(31 - (int)mq_clz((uint32_t)n) + 12) * 0x02C5C860u);
-  mq_post_body<int16_t>(
-      y, tw, maxv, maxv_stride, n, nb_mel, coefs, bf, total, nb_dct, dct, lut, dst, batch, stage,
-      [](const int16_t* x, int k, int L, int4 t) { return mq_split_q15(reinterpret_cast<const short2*>(x), k, L, t); },
-      [](int2 c, int32_t lutv) {                       // arm_cmplx_mag_q15
-        const uint32_t s2 = ((uint32_t)(c.x * c.x) + (uint32_t)(c.y * c.y)) >> 1;
-        return mq_sqrt((int32_t)s2, lutv) >> 16;
-      },
-      [](int32_t a, int32_t c) { return (int64_t)(a * c); },          // arm_dot_prod_q15
-      [le](int64_t r, int32_t m) {
-        r += 0x219;                                      // MICRO_Q15
-        r >>= 10;                                        // SHIFT_MELFILTER_SATURATION_Q15
-        int32_t v = mq_ssat31((int32_t)r);
-        if (m != 0 && m != 0x7FFF) v = mq_scale(v, (int32_t)((uint32_t)m << 16), 1);
-        const int64_t s = (int64_t)mq_log((uint32_t)v) + le;
-        v = s > INT32_MAX ? INT32_MAX : (s < INT32_MIN ? INT32_MIN : (int32_t)s);
-        return (int32_t)(int16_t)(v >> 19);              // (q15_t) truncation
-      },
-      [nb_mel, nb_dct](int r, const int32_t* mel, auto dctw) {   // arm_mat_vec_mult_q15
-        const int paired = r < (nb_dct & ~3) ? (nb_mel & ~1) : (nb_mel & ~3);
-        int64_t sum = 0;
-        for (int i = 0; i < paired; i += 2)
-          sum += (int32_t)((uint32_t)(dctw(r * nb_mel + i) * mel[i]) + (uint32_t)(dctw(r * nb_mel + i + 1) * mel[i + 1]));
-        for (int i = paired; i < nb_mel; ++i) sum += (int64_t)(dctw(r * nb_mel + i) * mel[i]);
-        return (int16_t)mq_ssat16((int32_t)(sum >> 15));
-      });
+  mq_post_body<int16_t>(MqOpsQ15(n, nb_mel, nb_dct), y, tw, maxv, maxv_stride, n, nb_mel, coefs, bf, total, nb_dct,
+                        dct, lut, dst, batch, stage);
 }
+
+// ---------------------------------------------------------------- fused: one launch
+// mfcc_fx_fused_kernel<T, L> (L = fftLen / 2, the RFFT's inner CFFT length): a workgroup holds
+// TPB = 4096 / L frames in LDS (the generic fixed-point CFFT's geometry, L / 16 lanes per frame),
+// reads each frame from HBM once and writes only its DCT outputs:
+//   pre   the frame's lanes find max sat|x| (LDS atomic max), divide, scale, window in LDS
+//         (MqOps::pre, arm_mfcc_q31.c:119-138 / arm_mfcc_q15.c:128-146);
+//   cfft  the RFFT's inner CFFT in place in LDS (cfft_fx_lds_body: radix4by2 + radix-4 stages,
+//         the same code as the batched kernels), bins read through the bit reversal;
+//   post  wave w takes frames w, w + 4, ...: the split + magnitudes, Mel, log, DCT of
+//         mq_post_frame with the CFFT bins read from LDS instead of HBM.
+// Traffic per frame: fftLen words in + nbDctOutputs words out (the batched API's d_src is
+// work space; the three-launch path moved 20 / 10 B per sample).
+template <typename T, int L>
+__global__ __launch_bounds__(kBlock) void mfcc_fx_fused_kernel(const T* __restrict__ src, const T* __restrict__ win,
+                                                               const typename Fx<T>::C* __restrict__ ctw, int brev,
+                                                               const int4* __restrict__ stw, int nb_mel,
+                                                               const T* __restrict__ coefs,
+                                                               const uint32_t* __restrict__ bf, int total, int nb_dct,
+                                                               const T* __restrict__ dct,
+                                                               const int32_t* __restrict__ lut, T* __restrict__ dst,
+                                                               uint32_t batch, int stage) {
+  using P = PlanFx<L>;
+  using F = Fx<T>;
+  using C = typename F::C;
+  using Ops = typename std::conditional<sizeof(T) == 4, MqOpsQ31, MqOpsQ15>::type;
+  constexpr int n = 2 * L, LOG = Log2<L>::v;
+  constexpr int SP = L + (P::LPT <= 4 ? 1 : 0);
+  extern __shared__ int32_t shq[];
+  C* frames = reinterpret_cast<C*>(shq);
+  int32_t* mx = shq + mq_fused_frame_words<T, L>();   // TPB frame maxima
+  int32_t* rest = mx + ((P::TPB + 3) & ~3);
+  const int tid = threadIdx.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * P::TPB;
+  const int valid = (int)min<uint64_t>((uint64_t)P::TPB, batch - t0);
+  if (tid < P::TPB) mx[tid] = 0;
+  {  // coalesced 16-B loads of the valid frames (the rest zero), scattered to the padded image
+    constexpr int PER16 = 16 / (int)sizeof(C);
+    const int4* s4 = reinterpret_cast<const int4*>(src + t0 * n);
+    constexpr int n16 = P::TPB * L / PER16;
+#pragma unroll 4
+    for (int i = tid; i < n16; i += kBlock) {
+      const int e = i * PER16, t = e / L, k = e % L;
+      const int4 v = t < valid ? s4[i] : make_int4(0, 0, 0, 0);
+      const C* c = reinterpret_cast<const C*>(&v);
+#pragma unroll
+      for (int u = 0; u < PER16; ++u) frames[t * SP + k + u] = c[u];
+    }
+  }
+  __syncthreads();
+  const int tr = tid / P::LPT, lane = tid % P::LPT;
+  C* x = frames + tr * SP;
+  T* xr = reinterpret_cast<T*>(x);                     // the frame's n real words
+  int32_t m = 0;
+  for (int i = lane; i < n; i += P::LPT) m = max(m, Ops::sat_abs((int32_t)xr[i]));
+  atomicMax(mx + tr, m);
+  __syncthreads();
+  m = mx[tr];
+  const bool scale = m != 0 && m != Ops::kFull;
+  int32_t quot = 0;
+  int k = 0;
+  if (scale) Ops::divide(m, quot, k);
+  for (int i = lane; i < n; i += P::LPT) xr[i] = (T)Ops::pre((int32_t)xr[i], (int32_t)win[i], scale, quot, k);
+  __syncthreads();
+  cfft_fx_lds_body<T, L, false>(x, ctw, lane);        // arm_rfft_q31.c: cfft(L, forward) in place
+
+  const MqTabs tb = mq_stage_tables<T>(rest, coefs, bf, total, nb_mel, nb_dct, dct, stage);
+  const int wave = tid >> 6;
+  int32_t* mag = rest + (stage ? mq_tab_words(total, nb_mel, nb_dct) : 0) + wave * mq_wave_words(n, nb_mel);
+  int32_t* mel = mag + mq_mag_words(n);
+  int64_t* acc = reinterpret_cast<int64_t*>(mag + ((mq_mag_words(n) + nb_mel + 1) & ~1));
+  const int32_t lutv = lut[tid & 31];
+  const Ops op(n, nb_mel, nb_dct);
+  for (int f = wave; f < valid; f += kBlock / 64) {
+    const C* xf = frames + f * SP;
+    auto get = [xf, brev](int i) { return fx_by2_out<T, L>(F::ld(xf + (brev ? bitrev<LOG>(i) : i))); };
+    auto kmap = [brev](int p) { return brev ? bitrev<LOG>(p) : p; };   // bins in storage order
+    mq_post_frame<T>(op, get, kmap, stw, n, mx[f], dst + (t0 + f) * (uint64_t)nb_dct, nb_mel, nb_dct, total, tb,
+                     coefs, dct, lutv, mag, mel, acc);
+  }
+}
+
+template <typename T, int L>
+static hipError_t mfcc_fx_fused_l(const T* src, const T* win, const void* ctw, int brev, const int4* stw, int nb_mel,
+                                  const T* coefs, const uint32_t* bf, int total, int nb_dct, const T* dct,
+                                  const int32_t* lut, T* dst, uint32_t batch, hipStream_t st) {
+  using P = PlanFx<L>;
+  const size_t base = sizeof(int32_t) * ((size_t)mq_fused_frame_words<T, L>() + ((P::TPB + 3) & ~3) +
+                                         (size_t)(kBlock / 64) * mq_wave_words(2 * L, nb_mel));
+  const size_t tab = sizeof(int32_t) * (size_t)mq_tab_words(total, nb_mel, nb_dct);
+  const int stage = base + tab <= 98304 ? 1 : 0;
+  const size_t lds = base + (stage ? tab : 0);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  auto k = mfcc_fx_fused_kernel<T, L>;
+  if (lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  const uint32_t grid = (uint32_t)((batch + P::TPB - 1) / P::TPB);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), lds, st, src, win, (const typename Fx<T>::C*)ctw, brev, stw, nb_mel,
+                     coefs, bf, total, nb_dct, dct, lut, dst, batch, stage);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t mfcc_fx_fused_launch(int n, const T* src, const T* win, const void* ctw, int brev, const int4* stw,
+                                int nb_mel, const T* coefs, const uint32_t* bf, int total, int nb_dct, const T* dct,
+                                const int32_t* lut, T* dst, uint32_t batch, hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+#define MQ_FUSED_CASE(LL) \
+  case 2 * LL: return mfcc_fx_fused_l<T, LL>(src, win, ctw, brev, stw, nb_mel, coefs, bf, total, nb_dct, dct, lut, dst, batch, st);
+  switch (n) {
+    MQ_FUSED_CASE(16) MQ_FUSED_CASE(32) MQ_FUSED_CASE(64) MQ_FUSED_CASE(128) MQ_FUSED_CASE(256)
+    MQ_FUSED_CASE(512) MQ_FUSED_CASE(1024) MQ_FUSED_CASE(2048)
+    default: return hipErrorInvalidValue;
+  }
+#undef MQ_FUSED_CASE
+}
+template hipError_t mfcc_fx_fused_launch<int32_t>(int, const int32_t*, const int32_t*, const void*, int, const int4*,
+                                                  int, const int32_t*, const uint32_t*, int, int, const int32_t*,
+                                                  const int32_t*, int32_t*, uint32_t, hipStream_t);
+template hipError_t mfcc_fx_fused_launch<int16_t>(int, const int16_t*, const int16_t*, const void*, int, const int4*,
+                                                  int, const int16_t*, const uint32_t*, int, int, const int16_t*,
+                                                  const int32_t*, int16_t*, uint32_t, hipStream_t);
 
 hipError_t mfcc_q15_pre_launch(int n, const int16_t* src, const int16_t* win, int16_t* x, int16_t* maxv,
                                uint32_t batch, int maxv_stride, hipStream_t st) {

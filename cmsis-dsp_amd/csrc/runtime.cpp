@@ -64,6 +64,7 @@ struct Scratch { void* p = nullptr; size_t n = 0; };
 thread_local std::map<std::pair<int, int>, Scratch> g_scratch;
 struct Pinned { void* p = nullptr; size_t n = 0; };   // kept until process exit, like Scratch
 thread_local std::map<int, Pinned> g_pinned;
+thread_local std::map<int, Pinned> g_zpinned;      // coherent, device-accessed in place
 thread_local std::map<int, hipStream_t> g_streams;
 
 int cur_dev() { int d = 0; (void)hipGetDevice(&d); return d; }
@@ -246,6 +247,38 @@ void* pinned(size_t bytes, int slot) {
   return s.p;
 }
 
+static void* zpinned(size_t bytes, int slot) {
+  Pinned& s = g_zpinned[slot];
+  if (s.n < bytes) {
+    if (s.p) (void)hipHostFree(s.p);
+    s.p = nullptr;
+    s.n = 0;
+    if (hipHostMalloc(&s.p, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;
+    s.n = bytes;
+  }
+  return s.p;
+}
+
+void* HostIO::zin(const void* host, size_t bytes) {
+  void* z = zpinned(bytes ? bytes : 4, zslot_++);
+  if (z && bytes) memcpy(z, host, bytes);
+  return z;
+}
+
+void* HostIO::zout(void* host, size_t bytes) {
+  if (nouts_ == 6) return nullptr;
+  void* z = zpinned(bytes ? bytes : 4, zslot_++);
+  if (z && bytes) outs_[nouts_++] = {host, z, bytes};
+  return z;
+}
+
+void* HostIO::zinout(void* host, size_t bytes) {
+  if (nouts_ == 6) return nullptr;
+  void* z = zin(host, bytes);
+  if (z && bytes) outs_[nouts_++] = {host, z, bytes};
+  return z;
+}
+
 hipError_t HostIO::in(void* dev, const void* host, size_t bytes) {
   if (!bytes) return hipSuccess;
   void* pin = pinned(bytes, slot_++);
@@ -256,7 +289,7 @@ hipError_t HostIO::in(void* dev, const void* host, size_t bytes) {
 
 hipError_t HostIO::out(void* host, const void* dev, size_t bytes) {
   if (!bytes) return hipSuccess;
-  if (nouts_ == 4) return hipErrorInvalidValue;
+  if (nouts_ == 6) return hipErrorInvalidValue;
   void* pin = pinned(bytes, slot_++);
   if (!pin) return hipErrorOutOfMemory;
   hipError_t e = hipMemcpyAsync(pin, dev, bytes, hipMemcpyDeviceToHost, st_);
@@ -267,7 +300,7 @@ hipError_t HostIO::out(void* host, const void* dev, size_t bytes) {
 // A call that returns early after queueing a copy must not leave a DMA reading a pinned slot
 // that the next call overwrites (or frees, when it needs a larger one): drain the stream.
 HostIO::~HostIO() {
-  if (slot_ > 0 && !finished_) (void)hipStreamSynchronize(st_);
+  if ((slot_ > 0 || zslot_ > 0) && !finished_) (void)hipStreamSynchronize(st_);
 }
 
 hipError_t HostIO::finish() {

@@ -55,6 +55,13 @@ void* pinned(size_t bytes, int slot);
 // buffer and copied to the caller's memory after the stream has drained (finish).  One
 // pinned slot per transfer; a call ends with finish(), or the destructor drains the stream
 // (error returns), so the slots are free again for the next call.
+//
+// Small calls (kZeroCopyMax bytes per buffer) skip the DMA engines: zin / zout / zinout return
+// a COHERENT pinned buffer (hipHostMallocCoherent: the GPU reads and writes it directly over the
+// host link, uncached, so no stale line survives between calls) holding the caller's words, the
+// kernel runs on it in place, and finish() copies the results back -- one launch and one
+// synchronize per call instead of two copies around the launch (tools/latency/).
+constexpr size_t kZeroCopyMax = size_t(1) << 20;
 class HostIO {
  public:
   explicit HostIO(hipStream_t st) : st_(st) {}
@@ -63,13 +70,16 @@ class HostIO {
   HostIO& operator=(const HostIO&) = delete;
   hipError_t in(void* dev, const void* host, size_t bytes);
   hipError_t out(void* host, const void* dev, size_t bytes);
+  void* zin(const void* host, size_t bytes);                 // nullptr: allocation failed
+  void* zout(void* host, size_t bytes);
+  void* zinout(void* host, size_t bytes);
   hipError_t finish();
 
  private:
   struct Pending { void* host; const void* pin; size_t bytes; };
   hipStream_t st_;
-  int slot_ = 0;
-  Pending outs_[4];
+  int slot_ = 0, zslot_ = 0;
+  Pending outs_[6];
   int nouts_ = 0;
   bool finished_ = false;
 };

@@ -80,6 +80,14 @@ arm_status arm_mfcc_q15_batch(const arm_mfcc_instance_q15 *S, q15_t *d_src, q15_
  * (arm_fir_f32.c:1242-1278).  Zero it to start a stream (arm_fir_init_f32). */
 arm_status arm_fir_f32_batch(const arm_fir_instance_f32 *S, const float32_t *d_src, float32_t *d_dst,
                              uint32_t blockSize, uint32_t batch, float32_t *d_hist, void *stream);
+/* Opt-in TOLERANCE path of arm_fir_f32_batch (same arguments and state contract): every
+ * output still sums its taps in the reference's order, but each MAC is one fused multiply-add
+ * (v_fma_f32: the product is not rounded before the add), so results differ from the reference
+ * in the last bits: |y - y_exact| <= numTaps * 2^-24 * sum_k |x b| (checked against float64 in
+ * tests/test_fir_fma.py, with the reference suite's thresholds, FIRF32.cpp).  About twice the
+ * bit-exact kernel's throughput (one VALU instruction per MAC instead of two). */
+arm_status arm_fir_f32_batch_fma(const arm_fir_instance_f32 *S, const float32_t *d_src, float32_t *d_dst,
+                                 uint32_t blockSize, uint32_t batch, float32_t *d_hist, void *stream);
 arm_status arm_fir_q15_batch(const arm_fir_instance_q15 *S, const q15_t *d_src, q15_t *d_dst,
                              uint32_t blockSize, uint32_t batch, q15_t *d_hist, void *stream);
 arm_status arm_fir_fast_q15_batch(const arm_fir_instance_q15 *S, const q15_t *d_src, q15_t *d_dst,

@@ -47,7 +47,7 @@ def test_rfft_dropin(dsp, torch_gpu, ref, n):
 def _fir_batched(dsp, torch, kind, coeffs, blocks_per_filter):
     """blocks_per_filter: [batch][calls] arrays; runs the batched API call by call."""
     import ctypes as C
-    base = kind.split("_")[-1]
+    base = "f32" if kind == "f32_fma" else kind.split("_")[-1]
     dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32, "q7": np.int8}[base]
     batch, calls = len(blocks_per_filter), len(blocks_per_filter[0])
     c = np.ascontiguousarray(coeffs, dtype=dt)

@@ -290,3 +290,32 @@ def test_cfft_batch_multi_orders_after_torch_work(dsp, torch_gpu, ref):
         shard.copy_(src)
         dsp.cfft_batch_multi(S, [shard], 0, 1)
         assert shard.cpu().numpy().tobytes() == ref.cfft_many("f32", n, x, 0, 1).tobytes()
+
+
+# ------------------------------------------------------------------ zero-copy drop-in staging
+def test_dropin_zero_copy_fresh_every_call(dsp, torch_gpu, ref):
+    """Small host-pointer calls run the kernel on a coherent pinned copy (no DMA): 40
+    consecutive arm_cfft_q31 / arm_cfft_f32 calls on fresh data reuse the same staging slot and
+    must never see a previous call's words."""
+    rng = np.random.default_rng(9)
+    for kind, n in (("f32", 1024), ("q31", 4096), ("q15", 256)):
+        S = dsp.const_instance(f"arm_cfft_sR_{kind}_len{n}")
+        fn = {"f32": dsp.arm_cfft_f32, "q31": dsp.arm_cfft_q31, "q15": dsp.arm_cfft_q15}[kind]
+        for i in range(40):
+            x = refs.rand_input(kind, 2 * n, seed=int(rng.integers(1 << 30)))
+            got = fn(S, x.copy(), i & 1, 1)
+            assert np.asarray(got).tobytes() == ref.cfft(kind, n, x, i & 1, 1).tobytes(), (kind, i)
+
+
+@pytest.mark.parametrize("taps,block", [(29, 32), (64, 10), (300, 7), (2, 1)])
+def test_dropin_fir_zero_copy_short_blocks(dsp, torch_gpu, ref, taps, block):
+    """Blocks shorter than the history (the new history reaches into the old one) and many
+    calls in a row through the zero-copy path: outputs and the caller's state buffer."""
+    rng = np.random.default_rng(taps * 31 + block)
+    c = (rng.standard_normal(taps) / np.sqrt(taps)).astype(np.float32)
+    blocks = [rng.uniform(-1, 1, block).astype(np.float32) for _ in range(25)]
+    f = dsp.FirF32(c, block)
+    want, state = ref.fir("f32", c, blocks)
+    for b, w in zip(blocks, want):
+        assert f(b).tobytes() == w.tobytes()
+    assert f.state.tobytes() == state.tobytes()

@@ -35,6 +35,10 @@ __global__ __launch_bounds__(256) void probe(int* out, int seed) {
   if constexpr (K == 13) CHAIN8(asm volatile("v_pk_ashrrev_i16 %0, 1, %0" : "+v"(a[i])))
   if constexpr (K == 14) CHAIN8(asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(c), "v"(d)))
   if constexpr (K == 15) CHAIN8(asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[i]) : "v"(c)))
+  // FIR-shaped FMAs: accumulator + window VGPR + coefficient (SGPR or VGPR)
+  if constexpr (K == 16) CHAIN8(asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(f[i]) : "s"((float)c), "v"(f[(i + 1) & 7])))
+  if constexpr (K == 17) CHAIN8(asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(f[i]) : "v"((float)d), "v"(f[(i + 1) & 7])))
+  if constexpr (K == 18) CHAIN8(asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(f[i]) : "s"((float)c), "v"((float)d)))
   int s = 0;
   for (int i = 0; i < 8; ++i) s += a[i] + (int)f[i];
   out[blockIdx.x * 256 + threadIdx.x] = s;
@@ -76,5 +80,8 @@ int main() {
   run<13>(out, "v_pk_ashrrev_i16");
   run<14>(out, "v_perm_b32");
   run<15>(out, "v_mul_lo_u32");
+  run<16>(out, "v_fmac_f32 s,v(acc'),acc");
+  run<17>(out, "v_fmac_f32 v,v(acc'),acc");
+  run<18>(out, "v_fmac_f32 s,v(const),acc");
   return 0;
 }

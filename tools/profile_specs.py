@@ -19,14 +19,15 @@ SPECS = {
     "rfft_q31": ("--workload rfft_q31 --steps 10 --warmup 3", "fx4096", ""),
     "rfft_q15": ("--workload rfft_q15 --steps 10 --warmup 3", "q15_4096_pk", ""),
     "fir_f32": ("--workload fir_f32 --steps 10 --warmup 3", "fir_f32_kernel", ""),
+    "fir_f32_fma": ("--workload fir_f32_fma --steps 10 --warmup 3", "fir_f32_kernel", ""),
     "fir_q15": ("--workload fir_q15 --steps 10 --warmup 3", "fir_q15_kernel", ""),
     "fir_q31": ("--workload fir_q31 --steps 10 --warmup 3", "fir_q31_kernel", ""),
     "fir_fast_q15": ("--workload fir_fast_q15 --steps 10 --warmup 3", "fir_q15_kernel", ""),
     "fir_fast_q31": ("--workload fir_fast_q31 --steps 10 --warmup 3", "fir_q31_kernel", ""),
     "conv_f32": ("--workload conv_f32 --steps 10 --warmup 3", "fir_f32_kernel", ""),
     "mfcc_f32": ("--workload mfcc_f32 --steps 10 --warmup 3", "mfcc_fused", ""),
-    "mfcc_q31": ("--workload mfcc_q31 --steps 10 --warmup 3", "mfcc_q31_post", ""),
-    "mfcc_q15": ("--workload mfcc_q15 --steps 10 --warmup 3", "mfcc_q15_post", ""),
+    "mfcc_q31": ("--workload mfcc_q31 --steps 10 --warmup 3", "mfcc_fx_fused", ""),
+    "mfcc_q15": ("--workload mfcc_q15 --steps 10 --warmup 3", "mfcc_fx_fused", ""),
     "mat_mult_f32": ("--workload mat_mult_f32 --steps 6 --warmup 2", "mat_mult_f32_full", ""),
     "mat_mult_q15": ("--workload mat_mult_q15 --steps 6 --warmup 2", "mat_mult_i8v2", ""),
     "mat_mult_q31": ("--workload mat_mult_q31 --steps 6 --warmup 2", "mat_mult_i8v2", ""),
