@@ -420,8 +420,13 @@ bool mfcc_fx_prepare(const Inst* S, MfccFxDev<T>& d) {
 
 // x: [batch][n] frames (overwritten), y: [batch][2n] spectra, dst: [batch][nbDct]; the frame
 // maxima ride in dst[frame][0] between the launches (read before the row is written)
-#ifndef MI355X_MFCC_FX_FUSED
-#define MI355X_MFCC_FX_FUSED 1    // 0: always the three-launch path (A/B builds)
+// MFCC q31 / q15 schedule: 1 = two launches (the MFCC front end fused into the radix-16 CFFT's
+// load phase, fftLen 512..4096 with the reference's own CFFT bit reversal, then post), 0 = three
+// launches (pre, CFFT, post: other lengths and custom bit-reversal tables).  A one-launch kernel
+// (frames resident in LDS through pre, CFFT and post) was measured slower than both and removed
+// (DESIGN.md §4 mfcc_q31 / mfcc_q15).
+#ifndef MI355X_MFCC_FX_MODE
+#define MI355X_MFCC_FX_MODE 1
 #endif
 template <typename T, typename Inst>
 bool mfcc_fx_run(const Inst* S, const MfccFxDev<T>& d, T* x, T* y, T* dst, uint32_t batch, hipStream_t st) {
@@ -435,19 +440,24 @@ bool mfcc_fx_run(const Inst* S, const MfccFxDev<T>& d, T* x, T* y, T* dst, uint3
   if (!cfft_prepare(L, in->pTwiddle, in->pBitRevTable, in->bitRevLength, sizeof(T) == 4 ? 1 : 2, 0,
                     S->rfft.bitReverseFlagR, pr))
     return false;
-  if (MI355X_MFCC_FX_FUSED && !pr.perm) {   // the reference's own bit reversal: one fused launch
-    const hipError_t e = mfcc_fx_fused_launch<T>(n, x, d.win, pr.tw, S->rfft.bitReverseFlagR ? 1 : 0, d.tw, nm,
-                                                 d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst, batch, st);
-    if (e == hipSuccess) return true;
-    if (e != hipErrorInvalidValue) { set_error(e, "mfcc fused"); return false; }
-    (void)hipGetLastError();                // unsupported shape: the three-launch path below
+  bool front = false;                       // pre + CFFT done by one launch
+  if (MI355X_MFCC_FX_MODE >= 1 && !pr.perm) {
+    if constexpr (sizeof(T) == 4)
+      front = cfft_q31_r16_mfcc_launch((int)L, x, batch, (const int32_t*)pr.tw, d.win, dst, nd,
+                                       S->rfft.bitReverseFlagR != 0, st);
+    else
+      front = cfft_q15_r16_mfcc_launch((int)L, x, batch, (const int16_t*)pr.tw, d.win, dst, nd,
+                                       S->rfft.bitReverseFlagR != 0, st);
+    if (front) MI_CHECK(hipGetLastError(), "mfcc front");
   }
-  if constexpr (sizeof(T) == 4) {
-    MI_CHECK(mfcc_q31_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc q31 pre");
-  } else {
-    MI_CHECK(mfcc_q15_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc q15 pre");
+  if (!front) {
+    if constexpr (sizeof(T) == 4) {
+      MI_CHECK(mfcc_q31_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc q31 pre");
+    } else {
+      MI_CHECK(mfcc_q15_pre_launch(n, x, d.win, x, dst, batch, nd, st), "mfcc q15 pre");
+    }
+    MI_CHECK(cfft_launch(sizeof(T) == 4 ? 1 : 2, L, x, batch, pr, st), "mfcc cfft");
   }
-  MI_CHECK(cfft_launch(sizeof(T) == 4 ? 1 : 2, L, x, batch, pr, st), "mfcc cfft");
   (void)y;
   if constexpr (sizeof(T) == 4) {
     MI_CHECK(mfcc_q31_post_launch(n, x, d.tw, dst, nd, nm, d.pos, d.len, d.off, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst,

@@ -26,6 +26,7 @@
 #include "common.hpp"
 #include "kernels.hpp"
 #include "cfft_fixed_core.hpp"
+#include "mfcc_fixed_ops.hpp"
 
 namespace mi355x {
 
@@ -86,6 +87,8 @@ template <bool INV> struct R16Ops<int32_t, INV> {
   static __device__ __forceinline__ V ld(__amdgpu_buffer_rsrc_t r, int vo, int so) { return FxIO<int2>::ld(r, vo, so); }
   static __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, int vo, int so, V v) { FxIO<int2>::st(r, vo, so, v); }
   static __device__ __forceinline__ V by2_post(V v) { return make_int2(wshl(v.x, 1), wshl(v.y, 1)); }
+  static __device__ __forceinline__ int2 unpack(V v) { return v; }
+  static __device__ __forceinline__ V pack(int32_t x, int32_t y) { return make_int2(x, y); }
   static __device__ __forceinline__ V sat(V v) { return sat_shl1<int32_t>(v); }
   // radix4by2 pre-pass pair (arm_cfft_q31.c:774-794 forward, :835-855 inverse)
   static __device__ __forceinline__ void by2_pre(V& a, V& b, C w) {
@@ -115,6 +118,8 @@ template <bool INV> struct R16Ops<int16_t, INV> {
     __builtin_amdgcn_raw_buffer_store_b32((int)upk(v), r, vo, so, MI355X_FX_NT);
   }
   static __device__ __forceinline__ V by2_post(V v) { return v << (short)1; }        // t16(x << 1)
+  static __device__ __forceinline__ int2 unpack(V v) { return make_int2(v.x, v.y); }
+  static __device__ __forceinline__ V pack(int32_t x, int32_t y) { return s16x2{(short)x, (short)y}; }
   static __device__ __forceinline__ V sat(V v) { return pk_sat_add(v, v); }          // __SSAT(x << 1, 16)
   // radix4by2 pre-pass pair, scalar branch (arm_cfft_q15.c:782-800 forward, :881-899 inverse)
   static __device__ __forceinline__ void by2_pre(V& A, V& B, C w) {
@@ -128,10 +133,17 @@ template <bool INV> struct R16Ops<int16_t, INV> {
   }
 };
 
-template <typename T, int N, bool INV, bool BREV, bool SAT>
+// PRE: the MFCC q31 / q15 front end on the RFFT's inner CFFT (arm_mfcc_q31.c:119-138, the N
+// complex words of a transform being the frame's 2N real samples): the transform's P threads find
+// max sat|x| (lane shuffles; an LDS pair for P = 128), scale and window their 32 words in
+// registers (MqPre) before the first pass, and lane 0 leaves m in maxv[frame * mstride] for the
+// post kernel -- the separate pre pass (one read and one write of every frame) disappears.
+template <typename T, int N, bool INV, bool BREV, bool SAT, bool PRE = false>
 __global__ __launch_bounds__(kBlock) void cfft_fx_r16_kernel(typename R16Ops<T, INV>::C* __restrict__ data,
                                                              uint32_t batch,
-                                                             const typename R16Ops<T, INV>::C* __restrict__ tw) {
+                                                             const typename R16Ops<T, INV>::C* __restrict__ tw,
+                                                             const typename R16Ops<T, INV>::C* __restrict__ win = nullptr,
+                                                             T* __restrict__ maxv = nullptr, int mstride = 0) {
   using R = R16<N>;
   using O = R16Ops<T, INV>;
   using V = typename O::V;
@@ -207,10 +219,39 @@ __global__ __launch_bounds__(kBlock) void cfft_fx_r16_kernel(typename R16Ops<T, 
     for (int u = 0; u < 16; ++u) nq[u] = O::ld(r, vin, P * u * kC);   // e = tp + P u
   };
   V v[16];
+  __shared__ int32_t red[PRE && P > 64 ? 2 * R::TPW : 1];
   // first pass from nq, then the next group's loads (they fly under the later passes)
   auto pass0 = [&](uint32_t g) {
 #pragma unroll
     for (int u = 0; u < 16; ++u) v[u] = nq[u];
+    if constexpr (PRE) {
+      using Pre = MqPre<T>;
+      int32_t m = 0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int2 z = O::unpack(v[u]);
+        m = max(m, max(Pre::sat_abs(z.x), Pre::sat_abs(z.y)));
+      }
+#pragma unroll
+      for (int o = (P < 64 ? P : 64) >> 1; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+      if constexpr (P > 64) {                         // the transform spans two waves
+        if ((tp & 63) == 0) red[2 * w + (tp >> 6)] = m;
+        __syncthreads();
+        m = max(red[2 * w], red[2 * w + 1]);
+      }
+      const bool scale = m != 0 && m != Pre::kFull;
+      int32_t quot = 0;
+      int k = 0;
+      if (scale) Pre::divide(m, quot, k);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const C wv = win[tp + P * u];                 // window words 2e, 2e + 1 of element e
+        const int2 z = O::unpack(v[u]);
+        v[u] = O::pack(Pre::pre(z.x, (int32_t)wv.x, scale, quot, k), Pre::pre(z.y, (int32_t)wv.y, scale, quot, k));
+      }
+      const uint32_t f = g * R::TPW + (uint32_t)w;
+      if (tp == 0 && f < batch) maxv[(size_t)f * mstride] = (T)m;
+    }
     if constexpr (R::BY2) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) O::by2_pre(v[u], v[u + 8], twpre[u]);
@@ -336,6 +377,38 @@ static void launch_r16(void* data, uint32_t batch, const void* tw, uint32_t flag
     if (brev) sat ? launch_r16_t<T, N, false, true, true>(data, batch, tw, st) : launch_r16_t<T, N, false, true, false>(data, batch, tw, st);
     else      sat ? launch_r16_t<T, N, false, false, true>(data, batch, tw, st) : launch_r16_t<T, N, false, false, false>(data, batch, tw, st);
   }
+}
+
+template <typename T, int N>
+static void launch_r16_mfcc(void* data, uint32_t batch, const void* tw, const void* win, T* maxv, int mstride,
+                            bool brev, hipStream_t st) {
+  using C = typename R16Ops<T, false>::C;
+  const uint32_t ngroups = (batch + R16<N>::TPW - 1) / R16<N>::TPW;
+  const uint32_t grid = (ngroups + MI355X_FXR_T - 1) / MI355X_FXR_T;
+  auto k = brev ? cfft_fx_r16_kernel<T, N, false, true, false, true> : cfft_fx_r16_kernel<T, N, false, false, false, true>;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, st, (C*)data, batch, (const C*)tw, (const C*)win, maxv, mstride);
+}
+
+// MFCC front end + the RFFT's inner forward CFFT of length n in place (n = fftLen / 2 in
+// 256..2048, the reference's own bit-reversal table); false: not handled here.
+template <typename T>
+static bool dispatch_r16_mfcc(int n, T* data, uint32_t batch, const T* tw, const T* win, T* maxv, int mstride,
+                              bool brev, hipStream_t st) {
+  switch (n) {
+    case 256:  launch_r16_mfcc<T, 256>(data, batch, tw, win, maxv, mstride, brev, st); return true;
+    case 512:  launch_r16_mfcc<T, 512>(data, batch, tw, win, maxv, mstride, brev, st); return true;
+    case 1024: launch_r16_mfcc<T, 1024>(data, batch, tw, win, maxv, mstride, brev, st); return true;
+    case 2048: launch_r16_mfcc<T, 2048>(data, batch, tw, win, maxv, mstride, brev, st); return true;
+    default:   return false;
+  }
+}
+bool cfft_q31_r16_mfcc_launch(int n, int32_t* data, uint32_t batch, const int32_t* tw, const int32_t* win,
+                              int32_t* maxv, int mstride, bool brev, hipStream_t st) {
+  return dispatch_r16_mfcc<int32_t>(n, data, batch, tw, win, maxv, mstride, brev, st);
+}
+bool cfft_q15_r16_mfcc_launch(int n, int16_t* data, uint32_t batch, const int16_t* tw, const int16_t* win,
+                              int16_t* maxv, int mstride, bool brev, hipStream_t st) {
+  return dispatch_r16_mfcc<int16_t>(n, data, batch, tw, win, maxv, mstride, brev, st);
 }
 
 // Returns true if N is handled here (the reference's own bit-reversal table only).

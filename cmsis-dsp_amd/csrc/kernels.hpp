@@ -35,6 +35,12 @@ hipError_t cfft_f32_launch(int n, float* data, uint32_t batch, const float* tw, 
 // false if N is not one of those lengths.
 bool cfft_q31_r16_launch(int n, int32_t* data, uint32_t batch, const int32_t* tw, uint32_t flags, hipStream_t st);
 bool cfft_q15_r16_launch(int n, int16_t* data, uint32_t batch, const int16_t* tw, uint32_t flags, hipStream_t st);
+// The same kernels with the MFCC front end fused into their load phase (PRE): forward, frame
+// maxima to maxv[frame * mstride]; false when n is not 256..2048.
+bool cfft_q31_r16_mfcc_launch(int n, int32_t* data, uint32_t batch, const int32_t* tw, const int32_t* win,
+                              int32_t* maxv, int mstride, bool brev, hipStream_t st);
+bool cfft_q15_r16_mfcc_launch(int n, int16_t* data, uint32_t batch, const int16_t* tw, const int16_t* win,
+                              int16_t* maxv, int mstride, bool brev, hipStream_t st);
 hipError_t cfft_q31_launch(int n, int32_t* data, uint32_t batch, const int32_t* tw, const uint16_t* perm,
                            uint32_t flags, hipStream_t st);
 hipError_t cfft_q15_launch(int n, int16_t* data, uint32_t batch, const int16_t* tw, const uint16_t* perm,
@@ -105,12 +111,6 @@ hipError_t mfcc_f32_pre_launch(int n, const float* src, const float* win, float*
 hipError_t mfcc_q31_pre_launch(int n, const int32_t* src, const int32_t* win, int32_t* x, int32_t* maxv,
                                uint32_t batch, int maxv_stride, hipStream_t st);
 size_t mfcc_q31_post_lds(int n, int nb_mel);
-// MFCC q31 / q15 in one launch (frames in LDS: pre, the inner CFFT, post); hipErrorInvalidValue
-// when the length or the LDS footprint is not supported (callers take the three-launch path).
-template <typename T>
-hipError_t mfcc_fx_fused_launch(int n, const T* src, const T* win, const void* ctw, int brev, const int4* stw,
-                                int nb_mel, const T* coefs, const uint32_t* bf, int total, int nb_dct, const T* dct,
-                                const int32_t* lut, T* dst, uint32_t batch, hipStream_t st);
 hipError_t mfcc_q15_pre_launch(int n, const int16_t* src, const int16_t* win, int16_t* x, int16_t* maxv,
                                uint32_t batch, int maxv_stride, hipStream_t st);
 hipError_t mfcc_q15_post_launch(int n, const int16_t* y, const int4* tw, const int16_t* maxv, int maxv_stride, int nb_mel,

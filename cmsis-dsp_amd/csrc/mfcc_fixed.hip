@@ -17,31 +17,11 @@
 #include "common.hpp"
 #include "kernels.hpp"
 #include "cfft_fixed_core.hpp"
-
-#include <type_traits>
+#include "mfcc_fixed_ops.hpp"
 
 namespace mi355x {
 
 constexpr int kMqWaves = 4;   // frames (waves) per 256-thread workgroup
-
-__device__ __forceinline__ int32_t mq_sat_abs(int32_t x) { return x > 0 ? x : (x == INT32_MIN ? INT32_MAX : -x); }
-__device__ __forceinline__ uint32_t mq_clz(uint32_t x) { return x ? (uint32_t)__builtin_clz(x) : 32u; }
-__device__ __forceinline__ int32_t mq_shl(int32_t x, int k) { return (int32_t)((uint32_t)x << (k & 31)); }
-__device__ __forceinline__ int32_t mq_ssat31(int32_t v) {
-  return v > 0x3FFFFFFF ? 0x3FFFFFFF : (v < -0x40000000 ? -0x40000000 : v);
-}
-__device__ __forceinline__ int32_t mq_hi(int32_t a, int32_t b) { return (int32_t)(((int64_t)a * b) >> 32); }
-
-// arm_scale_q31.c, one element: in = (x * frac) >> 32, then << kShift with saturation, or
-// >> -kShift (kShift = shift + 1 as int8_t)
-__device__ __forceinline__ int32_t mq_scale(int32_t x, int32_t frac, int k) {
-  const int32_t in = mq_hi(x, frac);
-  if (k >= 0) {
-    const int32_t out = mq_shl(in, k);
-    return in != (out >> (k & 31)) ? (0x7FFFFFFF ^ (in >> 31)) : out;
-  }
-  return in >> ((-k) & 31);
-}
 
 __device__ __forceinline__ int32_t wave_max_i(int32_t v) {
 #pragma unroll
@@ -134,9 +114,8 @@ __device__ __forceinline__ int32_t mq_log(uint32_t src) {
 
 
 // LDS per wave (int32 words): |X_k| (fftLen/2 + 1, at mq_mpad(k)), Mel values (nb_mel), then
-// int64 Mel sums.  mq_mpad(k) = k + k / 16: the magnitudes are written in the CFFT's storage
-// order (bit-reversed bins in the fused kernels, 16 apart per 32-lane group) and read by the Mel
-// sums at lane strides of a slice length; the pad keeps both on distinct banks.
+// int64 Mel sums.  mq_mpad(k) = k + k / 16: the Mel sums read the magnitudes at lane strides of
+// a slice length (often a multiple of 16 words), which the pad spreads over distinct banks.
 __host__ __device__ inline int mq_mpad(int k) { return k + (k >> 4); }
 __host__ __device__ inline int mq_mag_words(int n) { return mq_mpad(n / 2) + 1; }
 __host__ __device__ inline int mq_wave_words(int n, int nb_mel) { return ((mq_mag_words(n) + nb_mel + 1) & ~1) + 2 * nb_mel; }
@@ -152,7 +131,7 @@ __host__ __device__ inline int mq_wave_words(int n, int nb_mel) { return ((mq_ma
 // branch), with the k-th twiddle record tw[k] = {A[2mk], A[2mk+1], B[2mk], B[2mk+1]} (m = the
 // instance's twidCoefRModifier; built contiguous on the host, so the loads coalesce): the
 // post kernels take the magnitudes straight from the CFFT output, with no 2N-word spectrum.
-// get(i) returns CFFT bin i (global memory in the three-launch path, LDS in the fused kernels).
+// get(i) returns CFFT bin i of the frame (the CFFT output in global memory).
 template <typename Get>
 __device__ __forceinline__ int2 mq_split_q31(Get get, int k, int L, int4 t) {
   if (k == 0 || k == L) {
@@ -193,10 +172,6 @@ __device__ __forceinline__ void mq_wave_sync() {
 __host__ __device__ inline int mq_tab_words(int total, int nb_mel, int nb_dct) {
   return (2 * total + nb_mel * nb_dct + 3) & ~3;
 }
-// int32 words of the fused kernel's frame image: TPB = 4096 / L frames of SP complex, 16-B rounded
-template <typename T, int L> __host__ __device__ constexpr int mq_fused_frame_words() {
-  return (int)(((4096 / L) * (L + (L / 16 <= 4 ? 1 : 0)) * 2 * sizeof(T) / 4 + 3) & ~3);
-}
 
 // The frame-invariant tables a workgroup reads: staged in LDS (shq) when `stage`, else global.
 struct MqTabs {
@@ -222,10 +197,9 @@ __device__ __forceinline__ MqTabs mq_stage_tables(int32_t* tab, const T* __restr
 // One frame on one wave, from the CFFT output get(i) (i < L = n/2) and the frame maximum m:
 // |X_k| for k <= L (split + magnitude) into mag, the Mel sums (int64 LDS totals, acc), the
 // per-filter finish (fin) into mel, the DCT rows into o.  mag / mel / acc are the wave's own.
-// kmap(p) = the bin lanes take at step p (p < fftLen/2): the CFFT's storage order, so the reads
-// get(k), get(L - k) of a step are conflict free (bin L, from get(0) only, comes last).
-template <typename T, typename Ops, typename Get, typename KMap>
-__device__ __forceinline__ void mq_post_frame(const Ops& op, Get get, KMap kmap, const int4* __restrict__ tw, int n,
+// Bins 0 .. L - 1 take one lane each per step; bin L (from get(0) only) comes last.
+template <typename T, typename Ops, typename Get>
+__device__ __forceinline__ void mq_post_frame(const Ops& op, Get get, const int4* __restrict__ tw, int n,
                                               int32_t m, T* o,
                                               int nb_mel, int nb_dct, int total, const MqTabs& tb,
                                               const T* __restrict__ coefs, const T* __restrict__ dct, int32_t lutv,
@@ -238,7 +212,7 @@ __device__ __forceinline__ void mq_post_frame(const Ops& op, Get get, KMap kmap,
   const int L = lim - 1;
 #pragma unroll 4
   for (int p0 = 0; p0 < L; p0 += 64) {                 // uniform: the shuffle needs all lanes
-    const int p = p0 + lane, k = kmap(min(p, L - 1));
+    const int p = p0 + lane, k = min(p, L - 1);
     const int32_t v = op.mag(op.split(get, k, L, tw[k]), lutv);
     if (p < L) mag[mq_mpad(k)] = v;
   }
@@ -296,38 +270,20 @@ __device__ __forceinline__ void mq_post_body(const Ops& op, const T* __restrict_
       if constexpr (sizeof(T) == 4) return reinterpret_cast<const int2*>(X)[i];
       else { const short2 v = reinterpret_cast<const short2*>(X)[i]; return make_int2(v.x, v.y); }
     };
-    mq_post_frame<T>(op, get, [](int p) { return p; }, tw, n, m, dst + (size_t)frame * nb_dct, nb_mel, nb_dct, total,
+    mq_post_frame<T>(op, get, tw, n, m, dst + (size_t)frame * nb_dct, nb_mel, nb_dct, total,
                      tb, coefs, dct, lutv, mag, mel, acc);
   }
 }
 
-// The q31 chain of arm_mfcc_q31.c:119-223 as per-element operations (shared by the post kernel
-// and the fused kernel): pre = arm_absmax_q31 / arm_divide_q31 / arm_scale_q31 / arm_mult_q31,
-// post = arm_split_rfft_q31 + arm_cmplx_mag_q31, arm_dot_prod_q31, the Mel finish, the DCT rows.
-struct MqOpsQ31 {
+// The q31 chain of arm_mfcc_q31.c:119-223 as per-element operations: pre (MqPre, shared with the
+// radix-16 CFFT's MFCC prologue) = arm_absmax_q31 / arm_divide_q31 / arm_scale_q31 /
+// arm_mult_q31; post = arm_split_rfft_q31 + arm_cmplx_mag_q31, arm_dot_prod_q31, the Mel
+// finish, the DCT rows.
+struct MqOpsQ31 : MqPre<int32_t> {
   int32_t le;      // log exponent (fftShift + 2 + SHIFT_MELFILTER_SATURATION_Q31) * LOG2TOLOG_Q31
   int nb_mel;
   __device__ MqOpsQ31(int n, int nm, int /*nd*/)
       : le((int32_t)((uint32_t)(31 - (int)mq_clz((uint32_t)n) + 12) * 0x02C5C860u)), nb_mel(nm) {}
-  static constexpr int32_t kFull = 0x7FFFFFFF;
-  __device__ static int32_t sat_abs(int32_t x) { return mq_sat_abs(x); }
-  // arm_divide_q31(0x7FFFFFFF, m): both positive, temp = (num << 31) / den, normalised to 32 bits;
-  // k = (int8_t)(shift + 1), the arm_scale_q31 exponent
-  __device__ static void divide(int32_t m, int32_t& quot, int& k) {
-    int64_t t = (int64_t)(((uint64_t)0x7FFFFFFF << 31) / (uint64_t)m);
-    const int sn = 32 - (int)mq_clz((uint32_t)(t >> 31));
-    int sh = 0;
-    if (sn > 0) {
-      sh = sn;
-      t >>= sn;
-    }
-    quot = (int32_t)t;
-    k = (int)(int8_t)(sh + 1);
-  }
-  __device__ static int32_t pre(int32_t x, int32_t w, bool scale, int32_t quot, int k) {
-    if (scale) x = mq_scale(x, quot, k);
-    return mq_shl(mq_ssat31(mq_hi(x, w)), 1);          // arm_mult_q31: __SSAT((a*b) >> 32, 31) << 1
-  }
   template <typename Get> __device__ int2 split(Get get, int k, int L, int4 t) const { return mq_split_q31(get, k, L, t); }
   __device__ int32_t mag(int2 c, int32_t lutv) const {   // arm_cmplx_mag_q31
     const int32_t a0 = (int32_t)(((int64_t)c.x * c.x) >> 33), a1 = (int32_t)(((int64_t)c.y * c.y) >> 33);
@@ -369,8 +325,6 @@ __global__ __launch_bounds__(256) void mfcc_q31_post_kernel(const int32_t* __res
 // >> 1) >> 16 (arm_cmplx_mag_q15), Mel = __SSAT((Σ mag·c + MICRO_Q15) >> 10, 31), scale_q31 by
 // m << 16, log_q31, offset, >> 19, truncated to q15; DCT rows as arm_mat_vec_mult_q15 with
 // its __SMLALD column pairs (int32-wrapped pair sums, none.h:497-506).
-__device__ __forceinline__ int32_t mq_sat_abs15(int32_t x) { return x > 0 ? x : (x == -32768 ? 32767 : -x); }
-__device__ __forceinline__ int32_t mq_ssat16(int32_t v) { return v > 32767 ? 32767 : (v < -32768 ? -32768 : v); }
 
 __global__ __launch_bounds__(256) void mfcc_q15_pre_kernel(const int16_t* src, const int16_t* __restrict__ win,
                                                            int16_t* x, int16_t* maxv, int maxv_stride, int n,
@@ -416,29 +370,11 @@ __global__ __launch_bounds__(256) void mfcc_q15_pre_kernel(const int16_t* src, c
   if (lane == 0) maxv[(size_t)frame * maxv_stride] = (int16_t)m;
 }
 
-struct MqOpsQ15 {
+struct MqOpsQ15 : MqPre<int16_t> {
   int32_t le;
   int nb_mel, nb_dct;
   __device__ MqOpsQ15(int n, int nm, int nd)
       : le((int32_t)((uint32_t)(31 - (int)mq_clz((uint32_t)n) + 12) * 0x02C5C860u)), nb_mel(nm), nb_dct(nd) {}
-  static constexpr int32_t kFull = 0x7FFF;
-  __device__ static int32_t sat_abs(int32_t x) { return mq_sat_abs15(x); }
-  // arm_divide_q15(0x7FFF, m): temp = (0x7FFF << 15) / m, normalised by 17 - clz(temp); k = 15 - shift
-  __device__ static void divide(int32_t m, int32_t& quot, int& k) {
-    int32_t t = (int32_t)((0x7FFFu << 15) / (uint32_t)m);
-    const int sn = 17 - (int)mq_clz((uint32_t)t);
-    int sh = 0;
-    if (sn > 0) {
-      sh = sn;
-      t >>= sn;
-    }
-    quot = (int32_t)(int16_t)t;
-    k = (int)(int8_t)(15 - sh);
-  }
-  __device__ static int32_t pre(int32_t x, int32_t w, bool scale, int32_t quot, int k) {
-    if (scale) x = mq_ssat16((x * quot) >> k);       // arm_scale_q15
-    return mq_ssat16((x * w) >> 15);                  // arm_mult_q15
-  }
   template <typename Get> __device__ int2 split(Get get, int k, int L, int4 t) const { return mq_split_q15(get, k, L, t); }
   __device__ int32_t mag(int2 c, int32_t lutv) const {   // arm_cmplx_mag_q15
     const uint32_t s2 = ((uint32_t)(c.x * c.x) + (uint32_t)(c.y * c.y)) >> 1;
@@ -474,130 +410,6 @@ __global__ __launch_bounds__(256) void mfcc_q15_post_kernel(const int16_t* __res
   mq_post_body<int16_t>(MqOpsQ15(n, nb_mel, nb_dct), y, tw, maxv, maxv_stride, n, nb_mel, coefs, bf, total, nb_dct,
                         dct, lut, dst, batch, stage);
 }
-
-// ---------------------------------------------------------------- fused: one launch
-// mfcc_fx_fused_kernel<T, L> (L = fftLen / 2, the RFFT's inner CFFT length): a workgroup holds
-// TPB = 4096 / L frames in LDS (the generic fixed-point CFFT's geometry, L / 16 lanes per frame),
-// reads each frame from HBM once and writes only its DCT outputs:
-//   pre   the frame's lanes find max sat|x| (LDS atomic max), divide, scale, window in LDS
-//         (MqOps::pre, arm_mfcc_q31.c:119-138 / arm_mfcc_q15.c:128-146);
-//   cfft  the RFFT's inner CFFT in place in LDS (cfft_fx_lds_body: radix4by2 + radix-4 stages,
-//         the same code as the batched kernels), bins read through the bit reversal;
-//   post  wave w takes frames w, w + 4, ...: the split + magnitudes, Mel, log, DCT of
-//         mq_post_frame with the CFFT bins read from LDS instead of HBM.
-// Traffic per frame: fftLen words in + nbDctOutputs words out (the batched API's d_src is
-// work space; the three-launch path moved 20 / 10 B per sample).
-template <typename T, int L>
-__global__ __launch_bounds__(kBlock) void mfcc_fx_fused_kernel(const T* __restrict__ src, const T* __restrict__ win,
-                                                               const typename Fx<T>::C* __restrict__ ctw, int brev,
-                                                               const int4* __restrict__ stw, int nb_mel,
-                                                               const T* __restrict__ coefs,
-                                                               const uint32_t* __restrict__ bf, int total, int nb_dct,
-                                                               const T* __restrict__ dct,
-                                                               const int32_t* __restrict__ lut, T* __restrict__ dst,
-                                                               uint32_t batch, int stage) {
-  using P = PlanFx<L>;
-  using F = Fx<T>;
-  using C = typename F::C;
-  using Ops = typename std::conditional<sizeof(T) == 4, MqOpsQ31, MqOpsQ15>::type;
-  constexpr int n = 2 * L, LOG = Log2<L>::v;
-  constexpr int SP = L + (P::LPT <= 4 ? 1 : 0);
-  extern __shared__ int32_t shq[];
-  C* frames = reinterpret_cast<C*>(shq);
-  int32_t* mx = shq + mq_fused_frame_words<T, L>();   // TPB frame maxima
-  int32_t* rest = mx + ((P::TPB + 3) & ~3);
-  const int tid = threadIdx.x;
-  const uint64_t t0 = (uint64_t)blockIdx.x * P::TPB;
-  const int valid = (int)min<uint64_t>((uint64_t)P::TPB, batch - t0);
-  if (tid < P::TPB) mx[tid] = 0;
-  {  // coalesced 16-B loads of the valid frames (the rest zero), scattered to the padded image
-    constexpr int PER16 = 16 / (int)sizeof(C);
-    const int4* s4 = reinterpret_cast<const int4*>(src + t0 * n);
-    constexpr int n16 = P::TPB * L / PER16;
-#pragma unroll 4
-    for (int i = tid; i < n16; i += kBlock) {
-      const int e = i * PER16, t = e / L, k = e % L;
-      const int4 v = t < valid ? s4[i] : make_int4(0, 0, 0, 0);
-      const C* c = reinterpret_cast<const C*>(&v);
-#pragma unroll
-      for (int u = 0; u < PER16; ++u) frames[t * SP + k + u] = c[u];
-    }
-  }
-  __syncthreads();
-  const int tr = tid / P::LPT, lane = tid % P::LPT;
-  C* x = frames + tr * SP;
-  T* xr = reinterpret_cast<T*>(x);                     // the frame's n real words
-  int32_t m = 0;
-  for (int i = lane; i < n; i += P::LPT) m = max(m, Ops::sat_abs((int32_t)xr[i]));
-  atomicMax(mx + tr, m);
-  __syncthreads();
-  m = mx[tr];
-  const bool scale = m != 0 && m != Ops::kFull;
-  int32_t quot = 0;
-  int k = 0;
-  if (scale) Ops::divide(m, quot, k);
-  for (int i = lane; i < n; i += P::LPT) xr[i] = (T)Ops::pre((int32_t)xr[i], (int32_t)win[i], scale, quot, k);
-  __syncthreads();
-  cfft_fx_lds_body<T, L, false>(x, ctw, lane);        // arm_rfft_q31.c: cfft(L, forward) in place
-
-  const MqTabs tb = mq_stage_tables<T>(rest, coefs, bf, total, nb_mel, nb_dct, dct, stage);
-  const int wave = tid >> 6;
-  int32_t* mag = rest + (stage ? mq_tab_words(total, nb_mel, nb_dct) : 0) + wave * mq_wave_words(n, nb_mel);
-  int32_t* mel = mag + mq_mag_words(n);
-  int64_t* acc = reinterpret_cast<int64_t*>(mag + ((mq_mag_words(n) + nb_mel + 1) & ~1));
-  const int32_t lutv = lut[tid & 31];
-  const Ops op(n, nb_mel, nb_dct);
-  for (int f = wave; f < valid; f += kBlock / 64) {
-    const C* xf = frames + f * SP;
-    auto get = [xf, brev](int i) { return fx_by2_out<T, L>(F::ld(xf + (brev ? bitrev<LOG>(i) : i))); };
-    auto kmap = [brev](int p) { return brev ? bitrev<LOG>(p) : p; };   // bins in storage order
-    mq_post_frame<T>(op, get, kmap, stw, n, mx[f], dst + (t0 + f) * (uint64_t)nb_dct, nb_mel, nb_dct, total, tb,
-                     coefs, dct, lutv, mag, mel, acc);
-  }
-}
-
-template <typename T, int L>
-static hipError_t mfcc_fx_fused_l(const T* src, const T* win, const void* ctw, int brev, const int4* stw, int nb_mel,
-                                  const T* coefs, const uint32_t* bf, int total, int nb_dct, const T* dct,
-                                  const int32_t* lut, T* dst, uint32_t batch, hipStream_t st) {
-  using P = PlanFx<L>;
-  const size_t base = sizeof(int32_t) * ((size_t)mq_fused_frame_words<T, L>() + ((P::TPB + 3) & ~3) +
-                                         (size_t)(kBlock / 64) * mq_wave_words(2 * L, nb_mel));
-  const size_t tab = sizeof(int32_t) * (size_t)mq_tab_words(total, nb_mel, nb_dct);
-  const int stage = base + tab <= 98304 ? 1 : 0;
-  const size_t lds = base + (stage ? tab : 0);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  auto k = mfcc_fx_fused_kernel<T, L>;
-  if (lds > 65536) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
-  const uint32_t grid = (uint32_t)((batch + P::TPB - 1) / P::TPB);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), lds, st, src, win, (const typename Fx<T>::C*)ctw, brev, stw, nb_mel,
-                     coefs, bf, total, nb_dct, dct, lut, dst, batch, stage);
-  return hipGetLastError();
-}
-
-template <typename T>
-hipError_t mfcc_fx_fused_launch(int n, const T* src, const T* win, const void* ctw, int brev, const int4* stw,
-                                int nb_mel, const T* coefs, const uint32_t* bf, int total, int nb_dct, const T* dct,
-                                const int32_t* lut, T* dst, uint32_t batch, hipStream_t st) {
-  if (batch == 0) return hipSuccess;
-#define MQ_FUSED_CASE(LL) \
-  case 2 * LL: return mfcc_fx_fused_l<T, LL>(src, win, ctw, brev, stw, nb_mel, coefs, bf, total, nb_dct, dct, lut, dst, batch, st);
-  switch (n) {
-    MQ_FUSED_CASE(16) MQ_FUSED_CASE(32) MQ_FUSED_CASE(64) MQ_FUSED_CASE(128) MQ_FUSED_CASE(256)
-    MQ_FUSED_CASE(512) MQ_FUSED_CASE(1024) MQ_FUSED_CASE(2048)
-    default: return hipErrorInvalidValue;
-  }
-#undef MQ_FUSED_CASE
-}
-template hipError_t mfcc_fx_fused_launch<int32_t>(int, const int32_t*, const int32_t*, const void*, int, const int4*,
-                                                  int, const int32_t*, const uint32_t*, int, int, const int32_t*,
-                                                  const int32_t*, int32_t*, uint32_t, hipStream_t);
-template hipError_t mfcc_fx_fused_launch<int16_t>(int, const int16_t*, const int16_t*, const void*, int, const int4*,
-                                                  int, const int16_t*, const uint32_t*, int, int, const int16_t*,
-                                                  const int32_t*, int16_t*, uint32_t, hipStream_t);
 
 hipError_t mfcc_q15_pre_launch(int n, const int16_t* src, const int16_t* win, int16_t* x, int16_t* maxv,
                                uint32_t batch, int maxv_stride, hipStream_t st) {

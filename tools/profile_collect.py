@@ -70,6 +70,17 @@ def trace_summary(d, steps=None):
 
 
 def pmc_summary(d, ksub):
+    """Per-dispatch counter averages of the kernel(s) matching ksub; "a|b" sums the kernels of a
+    multi-launch step (e.g. the MFCC front-end CFFT + post), each averaged over its timed grid."""
+    if "|" in ksub:
+        parts = [pmc_summary(d, k) for k in ksub.split("|")]
+        if any(x is None for x in parts):
+            return None
+        tot = defaultdict(float)
+        for c, _ in parts:
+            for name, v in c.items():
+                tot[name] += v
+        return dict(tot), max(g for _, g in parts)
     per = defaultdict(lambda: defaultdict(float))     # (pass, dispatch) -> counter -> value
     grids = {}
     for f in glob.glob(os.path.join(d, "pmc_*", "**", "*counter_collection.csv"), recursive=True):
@@ -105,7 +116,7 @@ def main():
         os.makedirs(dest, exist_ok=True)
         line = bench_line(os.path.join(d, "bench_trace.json"))
         tr = trace_summary(d, line.get("steps") if line else None)
-        dom = [k for k in tr if ksub in k]
+        dom = [k for k in tr if ksub.split("|")[0] in k]
         rec = {"name": name, "bench_args": SPECS[name][0], "dominant_kernel_substring": ksub, "kernels": tr,
                "bench_config": line.get("config") if line else None}
         if dom:
@@ -129,7 +140,7 @@ def main():
         pm = pmc_summary(d, ksub)
         if pm:
             c, gmax = pm
-            ms = rec.get("trace_timed_avg_ms")
+            ms = rec.get("trace_pipeline_avg_ms") if "|" in ksub else rec.get("trace_timed_avg_ms")
             p = {"kernel_substring": ksub, "grid": gmax, "counters_per_dispatch": c}
             if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
                 p["read_bytes"] = c["FETCH_SIZE"] * 1024 * 2

@@ -26,8 +26,9 @@ SPECS = {
     "fir_fast_q31": ("--workload fir_fast_q31 --steps 10 --warmup 3", "fir_q31_kernel", ""),
     "conv_f32": ("--workload conv_f32 --steps 10 --warmup 3", "fir_f32_kernel", ""),
     "mfcc_f32": ("--workload mfcc_f32 --steps 10 --warmup 3", "mfcc_fused", ""),
-    "mfcc_q31": ("--workload mfcc_q31 --steps 10 --warmup 3", "mfcc_fx_fused", ""),
-    "mfcc_q15": ("--workload mfcc_q15 --steps 10 --warmup 3", "mfcc_fx_fused", ""),
+    # two launches per step: the MFCC front end fused into the radix-16 CFFT, then post (summed)
+    "mfcc_q31": ("--workload mfcc_q31 --steps 10 --warmup 3", "mfcc_q31_post|cfft_fx_r16_kernel", ""),
+    "mfcc_q15": ("--workload mfcc_q15 --steps 10 --warmup 3", "mfcc_q15_post|cfft_fx_r16_kernel", ""),
     "mat_mult_f32": ("--workload mat_mult_f32 --steps 6 --warmup 2", "mat_mult_f32_full", ""),
     "mat_mult_q15": ("--workload mat_mult_q15 --steps 6 --warmup 2", "mat_mult_i8v2", ""),
     "mat_mult_q31": ("--workload mat_mult_q31 --steps 6 --warmup 2", "mat_mult_i8v2", ""),
