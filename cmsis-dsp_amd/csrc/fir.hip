@@ -125,15 +125,55 @@ template <bool FMA>
 __device__ __forceinline__ void f32_round(float (&acc)[kF32R], const F32Grp& A, const F32Grp& B, const F32Grp& C,
                                           const float (&c)[8]) {
 #pragma unroll
-  for (int u = 0; u < 8; ++u)
+  for (int u = 0; u < 8; ++u) {
+    const float cu = c[u];
 #pragma unroll
     for (int r = 0; r < kF32R; ++r) {
       const int j = r + u;
-      acc[r] = f32_mac<FMA>(acc[r], j < 8 ? A.v[j] : j < 16 ? B.v[j - 8] : C.v[j - 16], c[u]);
+      acc[r] = f32_mac<FMA>(acc[r], j < 8 ? A.v[j] : j < 16 ? B.v[j - 8] : C.v[j - 16], cu);
     }
+  }
 #if MI355X_FIR_SCHED_BARRIER
   __builtin_amdgcn_sched_barrier(0);   // keep each round's products next to their adds
 #endif
+}
+
+// R = 16 rounds with coefficients read from LDS one round ahead (the FMA path: v_fmac_f32
+// takes its coefficient from a VGPR at full rate).  win: the window image, g: the lane's first
+// group, cp: the unit's taps in LDS (read-ahead of up to 40 words past the last round).
+template <bool FMA>
+__device__ __forceinline__ void f32_rounds_ldsc(float (&acc)[kF32R], const float* win, int g, const float* cp,
+                                                int rounds) {
+  static_assert(kF32R == 16, "LDS-coefficient rounds: 16 outputs per lane");
+  F32Grp X0, X1, X2, X3;
+  float c0[8], c1[8];
+  ld_grp(X0, win, g);
+  ld_grp(X1, win, g + 1);
+  ld_grp(X2, win, g + 2);
+  ld_coef(c0, cp, 0);
+  int nb = rounds >> 2;
+  if (nb > 0) {
+    do {
+      ld_coef(c1, cp, 8);  ld_grp(X3, win, g + 3); f32_round<FMA>(acc, X0, X1, X2, c0);
+      ld_coef(c0, cp, 16); ld_grp(X0, win, g + 4); f32_round<FMA>(acc, X1, X2, X3, c1);
+      ld_coef(c1, cp, 24); ld_grp(X1, win, g + 5); f32_round<FMA>(acc, X2, X3, X0, c0);
+      ld_coef(c0, cp, 32); ld_grp(X2, win, g + 6); f32_round<FMA>(acc, X3, X0, X1, c1);
+      g += 4;
+      cp += 32;
+    } while (--nb);
+  }
+  const int rem = rounds & 3;
+  if (rem > 0) {
+    ld_coef(c1, cp, 8);
+    ld_grp(X3, win, g + 3);
+    f32_round<FMA>(acc, X0, X1, X2, c0);
+    if (rem > 1) {
+      ld_coef(c0, cp, 16);
+      ld_grp(X0, win, g + 4);
+      f32_round<FMA>(acc, X1, X2, X3, c1);
+      if (rem > 2) f32_round<FMA>(acc, X2, X3, X0, c0);
+    }
+  }
 }
 
 // Window rows staged per thread: KPRE * 256 >= chunk + T + 8 (the last block reads one group
@@ -188,11 +228,36 @@ __device__ __forceinline__ void fir_f32_fetch(F32Win<KPRE, LONG>& w, const FirIt
   for (int k = 0; k < w.kH; ++k)
     w.h[k] = __builtin_amdgcn_raw_buffer_load_b32(rh, opaque(h0 + 1024 * k), 0, 0);   // past the history: 0
 }
+// Rows are 320 words apart (a multiple of 64), so the compiler would pair them into
+// ds_write2st64_b32, which is banked like ds_write_b64 (16-lane groups, both dwords of a lane
+// on one bank: 2-way conflicted).  Volatile stores stay single ds_write_b32 (32-lane groups,
+// conflict free under fir_stage_lane).
 template <int KPRE, bool LONG>
 __device__ __forceinline__ void fir_f32_put(float* wl, const F32Win<KPRE, LONG>& w) {
+  auto* v = (__attribute__((address_space(3))) volatile float*)wl;
 #pragma unroll
   for (int k = 0; k < KPRE; ++k)
-    wl[wpos(k * kBlock)] = __builtin_bit_cast(float, k < w.kH ? (w.x[k] | w.h[k < w.kH ? k : 0]) : w.x[k]);
+    v[wpos(k * kBlock)] = __builtin_bit_cast(float, k < w.kH ? (w.x[k] | w.h[k < w.kH ? k : 0]) : w.x[k]);
+}
+
+// FMA path: the unit's taps are staged to LDS with its window and read as broadcast VGPRs,
+// because v_fmac_f32 with an SGPR operand issues at half rate on gfx950 (a VGPR coefficient:
+// full rate; tools/probes/fmac_bank.hip, profiles/r03/probe_fmac_bank.txt), while the
+// bit-exact path's v_mul_f32 takes its SGPR coefficient at full rate.  Thread t holds taps
+// t + 256 q of the next unit (zero past Ts: range-checked loads).
+constexpr int kFirSeg = kFirMaxTaps;
+struct F32Coef {
+  int c[kFirSeg / kBlock];
+};
+__device__ __forceinline__ void fir_f32_cfetch(F32Coef& w, const float* __restrict__ coeffs, const FirItem& it,
+                                               const FirIn& in, int Ts, int tid) {
+  const __amdgpu_buffer_rsrc_t r = buf_rsrc(coeffs + it.f * in.cstride + it.a, (uint32_t)Ts * 4u);
+#pragma unroll
+  for (int q = 0; q < kFirSeg / kBlock; ++q) w.c[q] = __builtin_amdgcn_raw_buffer_load_b32(r, opaque((tid + kBlock * q) * 4), 0, 0);
+}
+__device__ __forceinline__ void fir_f32_cput(float* cl, const F32Coef& w, int tid) {
+#pragma unroll
+  for (int q = 0; q < kFirSeg / kBlock; ++q) cl[tid + kBlock * q] = __builtin_bit_cast(float, w.c[q]);
 }
 
 // Items per workgroup.  Workgroups of identical work started together finish together, so with
@@ -221,10 +286,12 @@ struct FirOut {
 #ifndef MI355X_FIR_F32_WAVES
 #define MI355X_FIR_F32_WAVES (kF32R == 16 ? 5 : 8)   // minimum waves per SIMD the allocation must allow
 #endif
+#ifndef MI355X_FIR_F32_FMA_WAVES
+#define MI355X_FIR_F32_FMA_WAVES 4                   // FMA: + 8 coefficient and 4 tap-staging VGPRs
+#endif
 // Long filters (numTaps > kFirSeg) run in tap segments of kFirSeg: a work unit is (item,
 // segment), the accumulators stay in registers from a unit with segment 0 to the one with the
 // last segment, so every output still sums its products k = 0, 1, .., numTaps - 1 in order.
-constexpr int kFirSeg = kFirMaxTaps;
 struct FirUnit {
   FirItem it;
   int Ts;              // taps in this segment
@@ -243,12 +310,13 @@ __device__ __forceinline__ FirUnit fir_unit(uint32_t u, uint32_t nseg, uint32_t 
   return x;
 }
 template <int KPRE, bool LONG, bool FMA>
-__global__ __launch_bounds__(kBlock, LONG ? 4 : MI355X_FIR_F32_WAVES) void fir_f32_kernel(
+__global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32_FMA_WAVES : MI355X_FIR_F32_WAVES) void fir_f32_kernel(
     const float* __restrict__ coeffs, int T, const float* __restrict__ src, float* __restrict__ dst, uint32_t B,
     const float* __restrict__ hist_in, uint32_t nchunks, uint32_t items, uint32_t ipw, FirIn in, FirOut fo) {
   constexpr int R = kF32R;
   constexpr int kWin = KPRE * kBlock;
   __shared__ __attribute__((aligned(16))) float win[wpos(kWin) + 32];
+  __shared__ __attribute__((aligned(16))) float cl[FMA ? kFirSeg + 64 : 4];   // FMA: the unit's taps (+ read-ahead)
   const int T1 = T - 1;
   const uint32_t i0 = blockIdx.x * ipw;
   if (i0 >= items) return;
@@ -259,9 +327,14 @@ __global__ __launch_bounds__(kBlock, LONG ? 4 : MI355X_FIR_F32_WAVES) void fir_f
   const int jl = fir_stage_lane(tid);               // the row sample this thread stages
   float* wl = win + wpos(jl);                       // wpos(jl + 256 k) = wpos(jl) + 320 k
   F32Win<KPRE, LONG> pre;
+  F32Coef pc;
   FirUnit cur = fir_unit<LONG>(u0, nseg, nchunks, B, T);
   fir_f32_fetch<KPRE, LONG>(pre, cur.it, src, hist_in, in, T1, jl);
   fir_f32_put<KPRE, LONG>(wl, pre);
+  if constexpr (FMA) {
+    fir_f32_cfetch(pc, coeffs, cur.it, in, cur.Ts, tid);
+    fir_f32_cput(cl, pc, tid);
+  }
   float acc[R];
   // Per unit: barrier (window ready) -> next window's loads -> MACs -> barrier (window free)
   // -> next window to LDS -> output stores.  The window write waits only for loads that had a
@@ -271,6 +344,7 @@ __global__ __launch_bounds__(kBlock, LONG ? 4 : MI355X_FIR_F32_WAVES) void fir_f
     const bool more = u + 1 < u1;
     const FirUnit nxt = more ? fir_unit<LONG>(u + 1, nseg, nchunks, B, T) : cur;
     if (more) fir_f32_fetch<KPRE, LONG>(pre, nxt.it, src, hist_in, in, T1, jl);
+    if (FMA && more) fir_f32_cfetch(pc, coeffs, nxt.it, in, nxt.Ts, tid);
     if (base < cur.it.count) {
       if (cur.first) {
 #pragma unroll
@@ -284,11 +358,14 @@ __global__ __launch_bounds__(kBlock, LONG ? 4 : MI355X_FIR_F32_WAVES) void fir_f
       // (s_load_dwordx8 per round) into SGPRs, the v_mul operand (no VGPRs, no LDS reads).
       int g = base >> 3;                            // the lane's first group
       const float* const ci = coeffs + cur.it.f * in.cstride + cur.it.a;
-      const float* cp = ci;
+      const float* cp = FMA ? cl : ci;
       ld_grp(X0, win, g);
       ld_grp(X1, win, g + 1);
       if constexpr (R == 16) ld_grp(X2, win, g + 2);
       int nb = rounds >> 2;
+      if constexpr (FMA && R == 16) {
+        f32_rounds_ldsc<FMA>(acc, win, g, cp, rounds);
+      } else {
       if (nb > 0) {
         do {
           if constexpr (R == 8) {
@@ -337,6 +414,7 @@ __global__ __launch_bounds__(kBlock, LONG ? 4 : MI355X_FIR_F32_WAVES) void fir_f
           }
         }
       }
+      }
       // numTaps % 8 tail taps, straight from LDS
       for (int k = 8 * rounds; k < Ts; ++k) {
         const float c = ci[k];
@@ -347,6 +425,7 @@ __global__ __launch_bounds__(kBlock, LONG ? 4 : MI355X_FIR_F32_WAVES) void fir_f
     if (more) {
       __syncthreads();                              // every wave is done reading this window
       fir_f32_put<KPRE, LONG>(wl, pre);
+      if constexpr (FMA) fir_f32_cput(cl, pc, tid);
     }
     if (cur.last && base < cur.it.count) {
       const FirItem& it = cur.it;

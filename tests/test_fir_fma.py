@@ -48,7 +48,8 @@ def test_fma_reference_suite_thresholds(dsp, torch_gpu, pat):  # noqa: F811
     assert metrics.rel_error(got, want, metrics.FIR_TOL["f32"]["rel"])
 
 
-@pytest.mark.parametrize("taps,block", [(128, 4096), (29, 32), (1, 64), (255, 1000), (1024, 3000), (2047, 2500)])
+@pytest.mark.parametrize("taps,block", [(128, 4096), (29, 32), (1, 64), (255, 1000), (256, 1500), (257, 777), (64, 5000),
+                                        (7, 1023), (1024, 3000), (2047, 2500)])
 def test_fma_elementwise_bound_vs_float64(dsp, torch_gpu, taps, block):
     rng = np.random.default_rng(taps + block)
     batch = 3
