@@ -50,6 +50,58 @@ __global__ __launch_bounds__(TH) void tile_kernel(int* __restrict__ x, long nxf,
   }
 }
 
+
+// One wave per transform (the one-wave f32 kernels' pattern): wave w of a WPB-wave workgroup
+// owns T consecutive S-byte transforms; per transform it loads (VBL-byte words), round-trips
+// them through its own LDS region (no barrier: a wave's LDS operations run in order) or, with
+// BAR, through the region with a workgroup barrier after the write and after the read (the
+// multi-wave kernels' coupling), and stores in place (VBS-byte words).
+template <int S, int T, int VBL, int VBS, int WPB, int BAR>
+__global__ __launch_bounds__(64 * WPB) void wave_kernel(int* __restrict__ x, int s) {
+  using VL = typename Vec<VBL>::T;
+  using VS = typename Vec<VBS>::T;
+  constexpr int PL = S / (64 * VBL), PS = S / (64 * VBS);
+  extern __shared__ v4i lds_raw[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  char* lw = reinterpret_cast<char*>(lds_raw) + w * (S + 256);
+  const long t0 = ((long)blockIdx.x * WPB + w) * T;
+  for (int t = 0; t < T; ++t) {
+    const VL* p = reinterpret_cast<const VL*>(reinterpret_cast<char*>(x) + (t0 + t) * S) + lane;
+    VL r[PL];
+#pragma unroll
+    for (int m = 0; m < PL; ++m) r[m] = __builtin_nontemporal_load(p + 64 * m);
+#pragma unroll
+    for (int m = 0; m < PL; ++m) reinterpret_cast<VL*>(lw)[lane + 64 * m] = r[m] + s;
+    if (BAR) __syncthreads();
+    VS o[PS];
+#pragma unroll
+    for (int m = 0; m < PS; ++m) o[m] = reinterpret_cast<VS*>(lw)[(63 - lane) + 64 * m];
+    if (BAR) __syncthreads();
+    VS* q = reinterpret_cast<VS*>(reinterpret_cast<char*>(x) + (t0 + t) * S) + lane;
+#pragma unroll
+    for (int m = 0; m < PS; ++m) __builtin_nontemporal_store(o[m], q + 64 * m);
+  }
+}
+template <int S, int T, int VBL, int VBS, int WPB, int BAR>
+void timew(int* x, long bytes, hipEvent_t e0, hipEvent_t e1) {
+  const long nxf = bytes / S;
+  const dim3 g(nxf / (T * WPB)), b(64 * WPB);
+  const size_t lds = (size_t)WPB * (S + 256);
+  auto k = wave_kernel<S, T, VBL, VBS, WPB, BAR>;
+  hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(k, g, b, lds, 0, x, 1);
+  hipEventRecord(e0);
+  for (int i = 0; i < 10; ++i) hipLaunchKernelGGL(k, g, b, lds, 0, x, 1);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  ms /= 10;
+  printf("wave S=%5d T=%d VBL=%2d VBS=%2d WPB=%d BAR=%d lds=%6zu  %.3f ms  %.3f TB/s\n", S, T, VBL, VBS, WPB, BAR, lds, ms,
+         2.0 * bytes / (ms * 1e-3) * 1e-12);
+  fflush(stdout);
+}
+
 template <int TH, int S, int VB, int T, bool PF, bool Q = false>
 void timeit(int* x, long bytes, int extra_lds, hipEvent_t e0, hipEvent_t e1) {
   const long nxf = bytes / S;
@@ -78,24 +130,23 @@ int main() {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  // per-wave contiguous parts (Q) vs interleaved, q31 / f32-4096 (32 KiB) and q15 (16 KiB)
-  timeit<256, 32768, 8, 8, true>(x, bytes, 0, e0, e1);
-  timeit<256, 32768, 8, 8, true, true>(x, bytes, 0, e0, e1);
-  timeit<256, 32768, 16, 8, true, true>(x, bytes, 0, e0, e1);
-  timeit<256, 32768, 16, 4, true, true>(x, bytes, 0, e0, e1);
-  timeit<256, 32768, 16, 2, true, true>(x, bytes, 0, e0, e1);
-  timeit<256, 32768, 16, 16, true, true>(x, bytes, 0, e0, e1);
-  timeit<256, 32768, 16, 8, false, true>(x, bytes, 0, e0, e1);
-  timeit<256, 32768, 16, 8, true, true>(x, bytes, 22 * 1024, e0, e1);
-  timeit<512, 32768, 16, 8, true, true>(x, bytes, 0, e0, e1);
-  timeit<256, 16384, 8, 8, true>(x, bytes, 0, e0, e1);
-  timeit<256, 16384, 16, 8, true, true>(x, bytes, 0, e0, e1);
-  timeit<256, 16384, 16, 16, true, true>(x, bytes, 0, e0, e1);
-  timeit<256, 16384, 16, 4, true, true>(x, bytes, 0, e0, e1);
-  timeit<128, 16384, 16, 8, true, true>(x, bytes, 0, e0, e1);
-  timeit<64, 16384, 16, 2, true, true>(x, bytes, 0, e0, e1);
-  timeit<64, 16384, 16, 2, false, true>(x, bytes, 0, e0, e1);
-  timeit<64, 8192, 16, 4, false, true>(x, bytes, 0, e0, e1);
+  // one wave per transform: the f32 N=1024 kernel's pattern (8 KiB, T = 4, 8 waves, 8-B loads,
+  // 16-B stores), then one property at a time toward the 256-thread fixed-point kernels
+  timew<8192, 4, 8, 16, 8, 0>(x, bytes, e0, e1);
+  timew<8192, 4, 8, 16, 8, 1>(x, bytes, e0, e1);
+  timew<8192, 4, 16, 16, 8, 0>(x, bytes, e0, e1);
+  timew<8192, 2, 8, 16, 8, 0>(x, bytes, e0, e1);
+  timew<8192, 8, 8, 16, 8, 0>(x, bytes, e0, e1);
+  timew<16384, 2, 8, 16, 4, 0>(x, bytes, e0, e1);
+  timew<16384, 2, 16, 16, 4, 0>(x, bytes, e0, e1);
+  timew<16384, 2, 16, 16, 4, 1>(x, bytes, e0, e1);
+  timew<16384, 4, 16, 16, 4, 0>(x, bytes, e0, e1);
+  timew<16384, 1, 16, 16, 4, 0>(x, bytes, e0, e1);
+  timew<16384, 2, 16, 16, 2, 0>(x, bytes, e0, e1);
+  timew<16384, 2, 16, 16, 8, 0>(x, bytes, e0, e1);
+  timew<32768, 2, 16, 16, 2, 0>(x, bytes, e0, e1);
+  timew<32768, 1, 16, 16, 4, 0>(x, bytes, e0, e1);
+  timew<32768, 2, 16, 16, 4, 0>(x, bytes, e0, e1);
   hipFree(x);
   return 0;
 }
