@@ -57,13 +57,11 @@ __device__ __forceinline__ T fir_sample(const T* __restrict__ hist, const T* __r
 }
 
 // ---------------------------------------------------------------- f32
-#ifndef MI355X_FIR_F32_R
-#define MI355X_FIR_F32_R 16
-#endif
-constexpr int kF32R = MI355X_FIR_F32_R;                 // outputs per lane (fir_f32_kernel)
-static_assert(kF32R == 8 || kF32R == 16, "fir_f32_kernel: 8 or 16 outputs per lane");
-constexpr int kF32G = kF32R / 8 + 1;                     // 8-sample groups one round reads
-constexpr int kF32Chunk = kBlock * kF32R;              // outputs per workgroup item
+// fir_f32_kernel runs R = 16 outputs per lane (4096-output items) or R = 8 (2048): fir_f32_pass
+// takes 8 when the 4096-output items would pad the outputs per filter by > 12 % more (e.g. the
+// 4096 + 128 - 1 outputs of a convolution: 8192 against 6144 output slots).
+template <int R> constexpr int kF32Chunk = kBlock * R;     // outputs per workgroup item
+constexpr int kF32ChunkMin = kF32Chunk<8>;
 constexpr int kFirPre = (kFirChunk + kFirMaxTaps - 1 + kBlock - 1) / kBlock;   // q31 window samples per thread
 
 // LDS index with one pad word every 8: lanes read at a stride of R = 8 words from any
@@ -88,8 +86,8 @@ __device__ __forceinline__ int padx(int i) { return i + (i >> 3); }
 // which every 32-lane ds_write_b32 group covers 32 distinct banks (round 2's identity mapping
 // was two-way conflicted: 9.4 M conflict cycles per launch, profiles/r02/fir_f32/pmc.json).
 // Both checked by tools/fir_lds_model.py.
-__host__ __device__ constexpr int gword(int g) { return 10 * g + (kF32R == 16 ? 2 * ((g >> 4) & 1) : 0); }
-__host__ __device__ constexpr int wpos(int j) { return gword(j >> 3) + (j & 7); }
+template <int R> __host__ __device__ constexpr int gword(int g) { return 10 * g + (R == 16 ? 2 * ((g >> 4) & 1) : 0); }
+template <int R> __host__ __device__ constexpr int wpos(int j) { return gword<R>(j >> 3) + (j & 7); }
 __device__ __forceinline__ int fir_stage_lane(int tid) {
   const int h = tid >> 5, q = tid & 31, a = q >> 3, e = q & 7;
   return 8 * (16 * (h >> 2) + 4 * a + (h & 3)) + e;     // groups c, c+4, c+8, c+12 per half-wave
@@ -100,8 +98,9 @@ __device__ __forceinline__ int fir_stage_lane(int tid) {
 #endif
 struct F32Grp { float v[8]; };
 // group g of the window: two ds_read2_b64
+template <int R>
 __device__ __forceinline__ void ld_grp(F32Grp& g, const float* win, int grp) {
-  const float2* q = reinterpret_cast<const float2*>(win + gword(grp));
+  const float2* q = reinterpret_cast<const float2*>(win + gword<R>(grp));
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     const float2 x = q[h];
@@ -121,14 +120,14 @@ __device__ __forceinline__ float f32_mac(float acc, float x, float c) {
   else return acc + x * c;
 }
 // groups A, B (, C for R = 16) hold window samples base + k + [0, 8), [8, 16), [16, 24)
-template <bool FMA>
-__device__ __forceinline__ void f32_round(float (&acc)[kF32R], const F32Grp& A, const F32Grp& B, const F32Grp& C,
+template <int R, bool FMA>
+__device__ __forceinline__ void f32_round(float (&acc)[R], const F32Grp& A, const F32Grp& B, const F32Grp& C,
                                           const float (&c)[8]) {
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const float cu = c[u];
 #pragma unroll
-    for (int r = 0; r < kF32R; ++r) {
+    for (int r = 0; r < R; ++r) {
       const int j = r + u;
       acc[r] = f32_mac<FMA>(acc[r], j < 8 ? A.v[j] : j < 16 ? B.v[j - 8] : C.v[j - 16], cu);
     }
@@ -142,22 +141,22 @@ __device__ __forceinline__ void f32_round(float (&acc)[kF32R], const F32Grp& A, 
 // takes its coefficient from a VGPR at full rate).  win: the window image, g: the lane's first
 // group, cp: the unit's taps in LDS (read-ahead of up to 40 words past the last round).
 template <bool FMA>
-__device__ __forceinline__ void f32_rounds_ldsc(float (&acc)[kF32R], const float* win, int g, const float* cp,
+__device__ __forceinline__ void f32_rounds_ldsc(float (&acc)[16], const float* win, int g, const float* cp,
                                                 int rounds) {
-  static_assert(kF32R == 16, "LDS-coefficient rounds: 16 outputs per lane");
+  constexpr int R = 16;
   F32Grp X0, X1, X2, X3;
   float c0[8], c1[8];
-  ld_grp(X0, win, g);
-  ld_grp(X1, win, g + 1);
-  ld_grp(X2, win, g + 2);
+  ld_grp<R>(X0, win, g);
+  ld_grp<R>(X1, win, g + 1);
+  ld_grp<R>(X2, win, g + 2);
   ld_coef(c0, cp, 0);
   int nb = rounds >> 2;
   if (nb > 0) {
     do {
-      ld_coef(c1, cp, 8);  ld_grp(X3, win, g + 3); f32_round<FMA>(acc, X0, X1, X2, c0);
-      ld_coef(c0, cp, 16); ld_grp(X0, win, g + 4); f32_round<FMA>(acc, X1, X2, X3, c1);
-      ld_coef(c1, cp, 24); ld_grp(X1, win, g + 5); f32_round<FMA>(acc, X2, X3, X0, c0);
-      ld_coef(c0, cp, 32); ld_grp(X2, win, g + 6); f32_round<FMA>(acc, X3, X0, X1, c1);
+      ld_coef(c1, cp, 8);  ld_grp<R>(X3, win, g + 3); f32_round<R, FMA>(acc, X0, X1, X2, c0);
+      ld_coef(c0, cp, 16); ld_grp<R>(X0, win, g + 4); f32_round<R, FMA>(acc, X1, X2, X3, c1);
+      ld_coef(c1, cp, 24); ld_grp<R>(X1, win, g + 5); f32_round<R, FMA>(acc, X2, X3, X0, c0);
+      ld_coef(c0, cp, 32); ld_grp<R>(X2, win, g + 6); f32_round<R, FMA>(acc, X3, X0, X1, c1);
       g += 4;
       cp += 32;
     } while (--nb);
@@ -165,20 +164,20 @@ __device__ __forceinline__ void f32_rounds_ldsc(float (&acc)[kF32R], const float
   const int rem = rounds & 3;
   if (rem > 0) {
     ld_coef(c1, cp, 8);
-    ld_grp(X3, win, g + 3);
-    f32_round<FMA>(acc, X0, X1, X2, c0);
+    ld_grp<R>(X3, win, g + 3);
+    f32_round<R, FMA>(acc, X0, X1, X2, c0);
     if (rem > 1) {
       ld_coef(c0, cp, 16);
-      ld_grp(X0, win, g + 4);
-      f32_round<FMA>(acc, X1, X2, X3, c1);
-      if (rem > 2) f32_round<FMA>(acc, X2, X3, X0, c0);
+      ld_grp<R>(X0, win, g + 4);
+      f32_round<R, FMA>(acc, X1, X2, X3, c1);
+      if (rem > 2) f32_round<R, FMA>(acc, X2, X3, X0, c0);
     }
   }
 }
 
 // Window rows staged per thread: KPRE * 256 >= chunk + T + 8 (the last block reads one group
 // past its taps), so the LDS image, the staging loads and the zero tail scale with numTaps.
-__host__ __device__ constexpr int fir_f32_kpre(int T) { return (kF32Chunk + T + 8 + kBlock - 1) / kBlock; }
+template <int R> __host__ __device__ constexpr int fir_f32_kpre(int T) { return (kF32Chunk<R> + T + 8 + kBlock - 1) / kBlock; }
 
 // Window staging of one item into registers, through buffer resources: window sample j is
 // block sample s = n0 - T1 + j, read from [0, n0 + count) of the filter's block (a negative
@@ -195,9 +194,9 @@ __device__ __forceinline__ int opaque(int x) {
 // kept apart and OR-ed in when the window is written to LDS, so no wait is placed before the
 // MACs that the fetch is meant to overlap.  A tap segment of a long filter (LONG, numTaps >
 // kFirSeg) starts a tap offset a into s, so any row can reach the history: all rows get one.
-template <int KPRE, bool LONG>
+template <int R, int KPRE, bool LONG>
 struct F32Win {
-  static constexpr int kH = LONG ? KPRE : KPRE - kF32R;
+  static constexpr int kH = LONG ? KPRE : KPRE - R;
   int x[KPRE];
   int h[kH];
 };
@@ -214,8 +213,8 @@ struct FirIn {
   uint64_t cstride;
 };
 // window of the tap segment starting at tap a: sample j = s[n0 + a + j]
-template <int KPRE, bool LONG>
-__device__ __forceinline__ void fir_f32_fetch(F32Win<KPRE, LONG>& w, const FirItem& it, const float* __restrict__ src,
+template <int R, int KPRE, bool LONG>
+__device__ __forceinline__ void fir_f32_fetch(F32Win<R, KPRE, LONG>& w, const FirItem& it, const float* __restrict__ src,
                                               const float* __restrict__ hist_in, const FirIn& in, int T1, int jl) {
   // jl = fir_stage_lane(thread): the row sample this thread stages
   const __amdgpu_buffer_rsrc_t r = buf_rsrc(src + it.f * in.stride, in.len * 4u);
@@ -232,12 +231,12 @@ __device__ __forceinline__ void fir_f32_fetch(F32Win<KPRE, LONG>& w, const FirIt
 // ds_write2st64_b32, which is banked like ds_write_b64 (16-lane groups, both dwords of a lane
 // on one bank: 2-way conflicted).  Volatile stores stay single ds_write_b32 (32-lane groups,
 // conflict free under fir_stage_lane).
-template <int KPRE, bool LONG>
-__device__ __forceinline__ void fir_f32_put(float* wl, const F32Win<KPRE, LONG>& w) {
+template <int R, int KPRE, bool LONG>
+__device__ __forceinline__ void fir_f32_put(float* wl, const F32Win<R, KPRE, LONG>& w) {
   auto* v = (__attribute__((address_space(3))) volatile float*)wl;
 #pragma unroll
   for (int k = 0; k < KPRE; ++k)
-    v[wpos(k * kBlock)] = __builtin_bit_cast(float, k < w.kH ? (w.x[k] | w.h[k < w.kH ? k : 0]) : w.x[k]);
+    v[wpos<R>(k * kBlock)] = __builtin_bit_cast(float, k < w.kH ? (w.x[k] | w.h[k < w.kH ? k : 0]) : w.x[k]);
 }
 
 // FMA path: the unit's taps are staged to LDS with its window and read as broadcast VGPRs,
@@ -284,7 +283,7 @@ struct FirOut {
 };
 
 #ifndef MI355X_FIR_F32_WAVES
-#define MI355X_FIR_F32_WAVES (kF32R == 16 ? 5 : 8)   // minimum waves per SIMD the allocation must allow
+#define MI355X_FIR_F32_WAVES(R) ((R) == 16 ? 5 : 8)   // minimum waves per SIMD the allocation must allow
 #endif
 #ifndef MI355X_FIR_F32_FMA_WAVES
 #define MI355X_FIR_F32_FMA_WAVES 4                   // FMA: + 8 coefficient and 4 tap-staging VGPRs
@@ -297,25 +296,25 @@ struct FirUnit {
   int Ts;              // taps in this segment
   bool first, last;    // first / last segment of the item
 };
-template <bool LONG>
+template <int R, bool LONG>
 __device__ __forceinline__ FirUnit fir_unit(uint32_t u, uint32_t nseg, uint32_t nchunks, uint32_t B, int T) {
   FirUnit x;
   const uint32_t item = LONG ? u / nseg : u;
   const int seg = LONG ? (int)(u - item * nseg) : 0;
-  x.it = fir_item(item, nchunks, B, T - 1, kF32Chunk);
+  x.it = fir_item(item, nchunks, B, T - 1, kF32Chunk<R>);
   x.it.a = seg * kFirSeg;
   x.Ts = LONG ? min(T - x.it.a, kFirSeg) : T;
   x.first = seg == 0;
   x.last = !LONG || seg == (int)nseg - 1;
   return x;
 }
-template <int KPRE, bool LONG, bool FMA>
-__global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32_FMA_WAVES : MI355X_FIR_F32_WAVES) void fir_f32_kernel(
+template <int R, int KPRE, bool LONG, bool FMA>
+__global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32_FMA_WAVES : MI355X_FIR_F32_WAVES(R)) void fir_f32_kernel(
     const float* __restrict__ coeffs, int T, const float* __restrict__ src, float* __restrict__ dst, uint32_t B,
     const float* __restrict__ hist_in, uint32_t nchunks, uint32_t items, uint32_t ipw, FirIn in, FirOut fo) {
-  constexpr int R = kF32R;
+  static_assert(R == 16 || (R == 8 && !FMA), "R = 16, or R = 8 for the bit-exact path");
   constexpr int kWin = KPRE * kBlock;
-  __shared__ __attribute__((aligned(16))) float win[wpos(kWin) + 32];
+  __shared__ __attribute__((aligned(16))) float win[wpos<R>(kWin) + 32];
   __shared__ __attribute__((aligned(16))) float cl[FMA ? kFirSeg + 64 : 4];   // FMA: the unit's taps (+ read-ahead)
   const int T1 = T - 1;
   const uint32_t i0 = blockIdx.x * ipw;
@@ -325,12 +324,12 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
   const int tid = threadIdx.x;
   const int base = tid * R;                         // local output index of this lane
   const int jl = fir_stage_lane(tid);               // the row sample this thread stages
-  float* wl = win + wpos(jl);                       // wpos(jl + 256 k) = wpos(jl) + 320 k
-  F32Win<KPRE, LONG> pre;
+  float* wl = win + wpos<R>(jl);                       // wpos(jl + 256 k) = wpos(jl) + 320 k
+  F32Win<R, KPRE, LONG> pre;
   F32Coef pc;
-  FirUnit cur = fir_unit<LONG>(u0, nseg, nchunks, B, T);
-  fir_f32_fetch<KPRE, LONG>(pre, cur.it, src, hist_in, in, T1, jl);
-  fir_f32_put<KPRE, LONG>(wl, pre);
+  FirUnit cur = fir_unit<R, LONG>(u0, nseg, nchunks, B, T);
+  fir_f32_fetch<R, KPRE, LONG>(pre, cur.it, src, hist_in, in, T1, jl);
+  fir_f32_put<R, KPRE, LONG>(wl, pre);
   if constexpr (FMA) {
     fir_f32_cfetch(pc, coeffs, cur.it, in, cur.Ts, tid);
     fir_f32_cput(cl, pc, tid);
@@ -342,8 +341,8 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
   for (uint32_t u = u0;;) {
     __syncthreads();
     const bool more = u + 1 < u1;
-    const FirUnit nxt = more ? fir_unit<LONG>(u + 1, nseg, nchunks, B, T) : cur;
-    if (more) fir_f32_fetch<KPRE, LONG>(pre, nxt.it, src, hist_in, in, T1, jl);
+    const FirUnit nxt = more ? fir_unit<R, LONG>(u + 1, nseg, nchunks, B, T) : cur;
+    if (more) fir_f32_fetch<R, KPRE, LONG>(pre, nxt.it, src, hist_in, in, T1, jl);
     if (FMA && more) fir_f32_cfetch(pc, coeffs, nxt.it, in, nxt.Ts, tid);
     if (base < cur.it.count) {
       if (cur.first) {
@@ -359,9 +358,9 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
       int g = base >> 3;                            // the lane's first group
       const float* const ci = coeffs + cur.it.f * in.cstride + cur.it.a;
       const float* cp = FMA ? cl : ci;
-      ld_grp(X0, win, g);
-      ld_grp(X1, win, g + 1);
-      if constexpr (R == 16) ld_grp(X2, win, g + 2);
+      ld_grp<R>(X0, win, g);
+      ld_grp<R>(X1, win, g + 1);
+      if constexpr (R == 16) ld_grp<R>(X2, win, g + 2);
       int nb = rounds >> 2;
       if constexpr (FMA && R == 16) {
         f32_rounds_ldsc<FMA>(acc, win, g, cp, rounds);
@@ -369,15 +368,15 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
       if (nb > 0) {
         do {
           if constexpr (R == 8) {
-            ld_coef(c0, cp, 0);  ld_grp(X2, win, g + 2); f32_round<FMA>(acc, X0, X1, X1, c0);
-            ld_coef(c1, cp, 8);  ld_grp(X3, win, g + 3); f32_round<FMA>(acc, X1, X2, X2, c1);
-            ld_coef(c0, cp, 16); ld_grp(X0, win, g + 4); f32_round<FMA>(acc, X2, X3, X3, c0);
-            ld_coef(c1, cp, 24); ld_grp(X1, win, g + 5); f32_round<FMA>(acc, X3, X0, X0, c1);
+            ld_coef(c0, cp, 0);  ld_grp<R>(X2, win, g + 2); f32_round<R, FMA>(acc, X0, X1, X1, c0);
+            ld_coef(c1, cp, 8);  ld_grp<R>(X3, win, g + 3); f32_round<R, FMA>(acc, X1, X2, X2, c1);
+            ld_coef(c0, cp, 16); ld_grp<R>(X0, win, g + 4); f32_round<R, FMA>(acc, X2, X3, X3, c0);
+            ld_coef(c1, cp, 24); ld_grp<R>(X1, win, g + 5); f32_round<R, FMA>(acc, X3, X0, X0, c1);
           } else {
-            ld_coef(c0, cp, 0);  ld_grp(X3, win, g + 3); f32_round<FMA>(acc, X0, X1, X2, c0);
-            ld_coef(c1, cp, 8);  ld_grp(X0, win, g + 4); f32_round<FMA>(acc, X1, X2, X3, c1);
-            ld_coef(c0, cp, 16); ld_grp(X1, win, g + 5); f32_round<FMA>(acc, X2, X3, X0, c0);
-            ld_coef(c1, cp, 24); ld_grp(X2, win, g + 6); f32_round<FMA>(acc, X3, X0, X1, c1);
+            ld_coef(c0, cp, 0);  ld_grp<R>(X3, win, g + 3); f32_round<R, FMA>(acc, X0, X1, X2, c0);
+            ld_coef(c1, cp, 8);  ld_grp<R>(X0, win, g + 4); f32_round<R, FMA>(acc, X1, X2, X3, c1);
+            ld_coef(c0, cp, 16); ld_grp<R>(X1, win, g + 5); f32_round<R, FMA>(acc, X2, X3, X0, c0);
+            ld_coef(c1, cp, 24); ld_grp<R>(X2, win, g + 6); f32_round<R, FMA>(acc, X3, X0, X1, c1);
           }
           g += 4;
           cp += 32;
@@ -388,28 +387,28 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
       if (rem > 0) {
         if constexpr (R == 8) {
           ld_coef(c0, cp, 0);
-          ld_grp(X2, win, g + 2);
-          f32_round<FMA>(acc, X0, X1, X1, c0);
+          ld_grp<R>(X2, win, g + 2);
+          f32_round<R, FMA>(acc, X0, X1, X1, c0);
           if (rem > 1) {
             ld_coef(c1, cp, 8);
-            ld_grp(X3, win, g + 3);
-            f32_round<FMA>(acc, X1, X2, X2, c1);
+            ld_grp<R>(X3, win, g + 3);
+            f32_round<R, FMA>(acc, X1, X2, X2, c1);
             if (rem > 2) {
               ld_coef(c0, cp, 16);
-              f32_round<FMA>(acc, X2, X3, X3, c0);
+              f32_round<R, FMA>(acc, X2, X3, X3, c0);
             }
           }
         } else {
           ld_coef(c0, cp, 0);
-          ld_grp(X3, win, g + 3);
-          f32_round<FMA>(acc, X0, X1, X2, c0);
+          ld_grp<R>(X3, win, g + 3);
+          f32_round<R, FMA>(acc, X0, X1, X2, c0);
           if (rem > 1) {
             ld_coef(c1, cp, 8);
-            ld_grp(X0, win, g + 4);
-            f32_round<FMA>(acc, X1, X2, X3, c1);
+            ld_grp<R>(X0, win, g + 4);
+            f32_round<R, FMA>(acc, X1, X2, X3, c1);
             if (rem > 2) {
               ld_coef(c0, cp, 16);
-              f32_round<FMA>(acc, X2, X3, X0, c0);
+              f32_round<R, FMA>(acc, X2, X3, X0, c0);
             }
           }
         }
@@ -419,12 +418,12 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
       for (int k = 8 * rounds; k < Ts; ++k) {
         const float c = ci[k];
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = f32_mac<FMA>(acc[r], win[wpos(base + k + r)], c);
+        for (int r = 0; r < R; ++r) acc[r] = f32_mac<FMA>(acc[r], win[wpos<R>(base + k + r)], c);
       }
     }
     if (more) {
       __syncthreads();                              // every wave is done reading this window
-      fir_f32_put<KPRE, LONG>(wl, pre);
+      fir_f32_put<R, KPRE, LONG>(wl, pre);
       if constexpr (FMA) fir_f32_cput(cl, pc, tid);
     }
     if (cur.last && base < cur.it.count) {
@@ -960,22 +959,19 @@ __global__ void fir_hist_kernel(const T* __restrict__ src, T* __restrict__ hist,
   hist[g] = sidx < T1 ? hist_in[f * T1 + sidx] : src[f * B + (sidx - T1)];
 }
 
-// One f32 FIR pass over `batch` filters (T <= kFirMaxTaps), outputs on the lattice `fo`.
-static void fir_f32_pass(const float* coeffs, int T, const float* src, float* dst, uint32_t B, uint32_t batch,
-                         const float* hist_in, FirIn in, FirOut fo, hipStream_t st, bool fma = false) {
-  const uint32_t nchunks = (B + kF32Chunk - 1) / kF32Chunk;
+// One f32 FIR pass over `batch` filters, outputs on the lattice `fo`.
+template <int R, bool F>
+static void fir_f32_launch(const float* coeffs, int T, const float* src, float* dst, uint32_t B, uint32_t batch,
+                           const float* hist_in, FirIn in, FirOut fo, hipStream_t st) {
+  const uint32_t nchunks = (B + kF32Chunk<R> - 1) / kF32Chunk<R>;
   const uint32_t items = nchunks * batch;
-  const int kpre = fir_f32_kpre(T < kFirSeg ? T : kFirSeg);
-  constexpr int K0 = fir_f32_kpre(1), KL = fir_f32_kpre(kFirSeg);     // 9..13 (R = 8), 17..21 (R = 16)
+  const int kpre = fir_f32_kpre<R>(T < kFirSeg ? T : kFirSeg);
+  constexpr int K0 = fir_f32_kpre<R>(1), KL = fir_f32_kpre<R>(kFirSeg);     // 9..13 (R = 8), 17..21 (R = 16)
   static_assert(KL - K0 == 4, "five window sizes");
-  auto pick = [&](auto fma_tag) {
-    constexpr bool F = decltype(fma_tag)::value;
-    return T > kFirSeg ? fir_f32_kernel<KL, true, F>
-         : kpre <= K0 ? fir_f32_kernel<K0, false, F> : kpre == K0 + 1 ? fir_f32_kernel<K0 + 1, false, F>
-         : kpre == K0 + 2 ? fir_f32_kernel<K0 + 2, false, F> : kpre == K0 + 3 ? fir_f32_kernel<K0 + 3, false, F>
-         : fir_f32_kernel<KL, false, F>;
-  };
-  auto k = fma ? pick(std::true_type{}) : pick(std::false_type{});
+  auto k = T > kFirSeg ? fir_f32_kernel<R, KL, true, F>
+         : kpre <= K0 ? fir_f32_kernel<R, K0, false, F> : kpre == K0 + 1 ? fir_f32_kernel<R, K0 + 1, false, F>
+         : kpre == K0 + 2 ? fir_f32_kernel<R, K0 + 2, false, F> : kpre == K0 + 3 ? fir_f32_kernel<R, K0 + 3, false, F>
+         : fir_f32_kernel<R, KL, false, F>;
   uint32_t ipw = MI355X_FIR_IPW;
   if (T > kFirSeg) ipw = 1;                         // a long item is already many units
   if (!ipw) {
@@ -985,6 +981,15 @@ static void fir_f32_pass(const float* coeffs, int T, const float* src, float* ds
   hipLaunchKernelGGL(k, dim3((items + ipw - 1) / ipw), dim3(kBlock), 0, st, coeffs, T, src, dst, B, hist_in, nchunks,
                      items, ipw, in, fo);
 }
+static void fir_f32_pass(const float* coeffs, int T, const float* src, float* dst, uint32_t B, uint32_t batch,
+                         const float* hist_in, FirIn in, FirOut fo, hipStream_t st, bool fma = false) {
+  if (fma) return fir_f32_launch<16, true>(coeffs, T, src, dst, B, batch, hist_in, in, fo, st);
+  // output slots per filter at 4096- and 2048-output items: R = 8 when R = 16 pads > 12 % more
+  const uint64_t s16 = (uint64_t)((B + kF32Chunk<16> - 1) / kF32Chunk<16>) * kF32Chunk<16>;
+  const uint64_t s8 = (uint64_t)((B + kF32Chunk<8> - 1) / kF32Chunk<8>) * kF32Chunk<8>;
+  if (s16 * 100 > s8 * 112) return fir_f32_launch<8, false>(coeffs, T, src, dst, B, batch, hist_in, in, fo, st);
+  fir_f32_launch<16, false>(coeffs, T, src, dst, B, batch, hist_in, in, fo, st);
+}
 
 // The f32 convolution family's windowed outputs as one FIR pass (conv.hip): taps c (row
 // stride cstride), x rows of A samples (stride sx), outputs n = first .. first + num - 1 of
@@ -993,7 +998,7 @@ hipError_t fir_f32_conv_pass(const float* c, uint64_t cstride, int T, const floa
                              uint32_t first, float* y, uint64_t sy, int64_t off, int dir, uint32_t num, uint32_t batch,
                              hipStream_t st) {
   if (num == 0 || batch == 0) return hipSuccess;
-  if (T < 1 || T > kFirMaxTaps || (uint64_t)((num + kF32Chunk - 1) / kF32Chunk) * batch > 0xFFFFFFFFull)
+  if (T < 1 || T > kFirMaxTaps || (uint64_t)((num + kF32ChunkMin - 1) / kF32ChunkMin) * batch > 0xFFFFFFFFull)
     return hipErrorInvalidValue;
   fir_f32_pass(c, T, x, y, num, batch, nullptr, FirIn{sx, A, (int)first, 0u, cstride},
                FirOut{1u, 1u, 0u, dir, off, sy}, st);
@@ -1006,7 +1011,7 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
   if (batch == 0 || B == 0) return hipSuccess;
   if (T_ < 1) return hipErrorInvalidValue;        // numTaps > kFirMaxTaps: tap segments
   const int T1 = T_ - 1;
-  const int chunk = kind == kFirF32 || kind == kFirF32Fma ? kF32Chunk : kFirChunk;
+  const int chunk = kind == kFirF32 || kind == kFirF32Fma ? kF32ChunkMin : kFirChunk;
   const uint32_t nchunks = (B + chunk - 1) / chunk;
   const uint64_t items64 = (uint64_t)nchunks * batch;
   if (items64 > 0xFFFFFFFFull) return hipErrorInvalidValue;
@@ -1436,7 +1441,7 @@ static hipError_t decimate_launch(const void* coeffs, int T, int M, const void* 
   // input position, storing the outputs with n % M == 0 (M x the MACs at the FIR kernel's
   // issue efficiency beats the one-output-per-lane kernel up to M = 4: tools/bench_filters.py)
   const bool via_fir = OP == kMrF32 && M <= 4 && B % (uint32_t)M == 0 && T <= kFirMaxTaps &&
-                       (uint64_t)((B + kF32Chunk - 1) / kF32Chunk) * batch <= 0xFFFFFFFFull;
+                       (uint64_t)((B + kF32ChunkMin - 1) / kF32ChunkMin) * batch <= 0xFFFFFFFFull;
   return mr_launch<E>((const E*)src, (E*)dst, (size_t)batch * outs, B, batch, (E*)hist, T - 1, (uint32_t)(outs * M),
                       st, [&](const E* s, const E* h) {
                         if (blocks == 0) return hipSuccess;

@@ -2,6 +2,7 @@
 #include "runtime.hpp"
 
 #include <dlfcn.h>
+#include <link.h>
 #include <string.h>
 
 #include <map>
@@ -101,19 +102,47 @@ bool is_device_ptr(const void* p) {
   return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
-bool is_library_addr(const void* p) {
-  static const void* self = [] {
-    Dl_info i{};
-    return dladdr((const void*)&is_library_addr, &i) ? i.dli_fbase : (void*)nullptr;
+// The address range of this library's loaded segments, found once (dl_iterate_phdr), so the
+// per-call test is two compares instead of a dladdr symbol lookup.
+namespace {
+struct AddrRange { uintptr_t lo = 0, hi = 0; };
+int find_self(dl_phdr_info* info, size_t, void* data) {
+  auto* r = static_cast<AddrRange*>(data);
+  const uintptr_t fn = (uintptr_t)&find_self;
+  uintptr_t lo = UINTPTR_MAX, hi = 0;
+  bool mine = false;
+  for (int i = 0; i < info->dlpi_phnum; ++i) {
+    const ElfW(Phdr)& ph = info->dlpi_phdr[i];
+    if (ph.p_type != PT_LOAD) continue;
+    const uintptr_t a = info->dlpi_addr + ph.p_vaddr, b = a + ph.p_memsz;
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+    mine |= fn >= a && fn < b;
+  }
+  if (!mine) return 0;
+  r->lo = lo;
+  r->hi = hi;
+  return 1;
+}
+const AddrRange& self_range() {
+  static const AddrRange r = [] {
+    AddrRange x;
+    dl_iterate_phdr(find_self, &x);
+    return x;
   }();
-  Dl_info i{};
-  return p && self && dladdr(p, &i) && i.dli_fbase == self;
+  return r;
+}
+}  // namespace
+
+bool is_library_addr(const void* p) {
+  const AddrRange& r = self_range();
+  return p && (uintptr_t)p >= r.lo && (uintptr_t)p < r.hi;
 }
 
 const void* device_table(const void* host, size_t bytes) {
   if (!host || !bytes) { set_error(hipErrorInvalidValue, "device_table: null table"); return nullptr; }
-  if (is_device_ptr(host)) return host;
-  if (!is_library_addr(host)) return device_blob(host, bytes);
+  // the library's own CommonTables first: no pointer-attribute query on the drop-in's hot path
+  if (!is_library_addr(host)) return is_device_ptr(host) ? host : device_blob(host, bytes);
   const int dev = cur_dev();
   std::lock_guard<std::mutex> lk(g_table_mu);
   auto key = std::make_tuple(dev, host, bytes);
