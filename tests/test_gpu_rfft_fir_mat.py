@@ -275,7 +275,10 @@ def test_mat_mult_1024_vs_reference_slice(dsp, torch_gpu, ref):
                                         (33, 100, 31, "mixed"), (3, 33000, 2, None),
                                         # whole 128 x 128 / 128 x 64 tiles, K % 64 == 0: the unguarded kernel
                                         (128, 128, 128, None), (256, 192, 256, "min"), (128, 320, 128, "mixed"),
-                                        (256, 64, 128, "max")])
+                                        (256, 64, 128, "max"),
+                                        # the int32 class accumulators at their exact limit (K = 32704,
+                                        # every plane byte -128), and K just past a 64-deep step
+                                        (2, 32704, 3, "min"), (130, 65, 129, "min")])
 def test_mat_mult_fixed_bitexact(dsp, torch_gpu, ref, kind, m, k, n, fill):
     """Byte-sliced i8-MFMA kernel (K <= 32704) and the VALU kernel beyond, vs the reference
     build bit for bit, including all-extreme operands (q63 wrap for q31, saturation for q15);
