@@ -28,7 +28,7 @@ class World:
 
     @property
     def distributed(self):
-        return self.size > 1
+        return self.backend != "none"
 
 
 def init(backend=None, device=True):
@@ -44,7 +44,10 @@ def init(backend=None, device=True):
     ndev = torch.cuda.device_count() if device else 0
     if device:
         torch.cuda.set_device(local % max(1, ndev))
-    if size == 1:
+    # CMSISDSP_DIST_SINGLE=1: build the process group even for one rank, so the RCCL path
+    # (init, barrier, MAX all-reduce, digest all-gather, scatter) runs on a one-GPU box, where
+    # RCCL cannot hold two ranks on one device (tests/test_gpu_dist_nccl.py).
+    if size == 1 and os.environ.get("CMSISDSP_DIST_SINGLE") != "1":
         return World(rank, size, local, "none")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend is None:
