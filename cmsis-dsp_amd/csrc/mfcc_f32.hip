@@ -234,12 +234,23 @@ __global__ __launch_bounds__(kBlock) void mfcc_fused_kernel(const float* __restr
     mg[i] = v;
   }
   __syncthreads();                                    // every spectrum read is done
-  float* mag = xf;                                    // H magnitudes, then nb_mel log-Mel values
-  float* mel = xf + H;
+  // Magnitudes then log-Mel values in the frame's own LDS rows.  The Mel stage runs one thread
+  // per (filter, frame) pair, frame fastest (thread t: frame t % TPB, filter t / TPB), so a wave
+  // holds a few CONSECUTIVE filters -- similar lengths (the suite's run 12 .. 115 taps) -- and its
+  // loop runs to their longest instead of to the longest of all filters (one lane per filter:
+  // ~26 % of the lanes' iterations did work).  Each sum keeps its sequential order.  A per-frame
+  // skew of the magnitude rows puts the same bin of up to 8 frames on different banks.
+  const bool skewed = nb_mel <= H - 8;
+  const int skew = skewed ? (tr & 7) : 0, melo = skewed ? H + 8 : H;
+  {
+    float* mag = xf + skew;
 #pragma unroll
-  for (int i = 0; i < KPL; ++i) mag[lane + i * LPT] = mg[i];
+    for (int i = 0; i < KPL; ++i) mag[lane + i * LPT] = mg[i];
+  }
   __syncthreads();
-  for (int i = lane; i < nb_mel; i += LPT) {
+  for (int q = tid; q < TPB * nb_mel; q += kBlock) {
+    const int f = q % TPB, i = q / TPB;
+    const float* mag = reinterpret_cast<const float*>(lds + f * H) + (skewed ? (f & 7) : 0);
     const uint32_t p = pos[i], l = len[i];
     const float* c = cbase + off[i];
     float sum = 0.0f;
@@ -249,9 +260,10 @@ __global__ __launch_bounds__(kBlock) void mfcc_fused_kernel(const float* __restr
       const float prod = (k < (uint32_t)H ? mag[k] : 0.0f) * c[j];
       sum = sum + prod;
     }
-    mel[i] = host_logf(sum + 1.0e-6f);
+    reinterpret_cast<float*>(lds + f * H)[melo + i] = host_logf(sum + 1.0e-6f);
   }
   __syncthreads();
+  const float* mel = xf + melo;
   if (tr < valid) {
     float* o = dst + (f0 + tr) * (uint64_t)nb_dct;
     for (int r = lane; r < nb_dct; r += LPT) {
