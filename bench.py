@@ -98,6 +98,29 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+# ------------------------------------------------------------------ stdout = the JSON line only
+_LINE_FD = None
+
+
+def reserve_stdout():
+    """Point fd 1 at stderr before torch, RCCL or the library load (RCCL prints its version
+    banner on fd 1 at init, which a driver running torch.distributed.run directly would read
+    beside the line) and keep a duplicate of the original fd 1 for the JSON line alone."""
+    global _LINE_FD
+    sys.stdout.flush()
+    _LINE_FD = os.dup(1)
+    os.dup2(2, 1)
+
+
+def emit_line(line):
+    data = json.dumps(line) + "\n"
+    if _LINE_FD is None:
+        print(data, end="", flush=True)
+    else:
+        sys.stdout.flush()
+        os.write(_LINE_FD, data.encode())
+
+
 # ------------------------------------------------------------------ N-rank launcher
 def _free_port():
     s = socket.socket()
@@ -790,7 +813,7 @@ def main_rank(args):
             line["cpu_baseline"] = None
     parallel.barrier(world)                       # the other ranks wait for rank 0's CPU legs
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        emit_line(line)
     parallel.shutdown(world)
     return 0
 
@@ -825,7 +848,7 @@ def dry_run(args, world, parallel):
         line["cpu_baseline"] = cpu_baseline("cfft_f32_1024", 1024, secs, secs)
     parallel.barrier(world, sync_device=False)
     if line is not None:
-        print(json.dumps(line), flush=True)
+        emit_line(line)
     parallel.shutdown(world)
     return 0
 
@@ -856,6 +879,7 @@ def main(argv=None):
     args = parse_args(argv)
     if args.gpus and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args, argv)
+    reserve_stdout()
     return main_rank(args)
 
 

@@ -60,3 +60,25 @@ def test_world_size_mismatch_fails_loudly():
     r = _run(["--gpus", "2", "--dry-run"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
     assert "WORLD_SIZE=1" in (r.stderr + r.stdout)
+
+
+def test_driver_style_torchrun_stdout_is_one_json_line():
+    """The driver runs `python -m torch.distributed.run ... bench.py --gpus N` itself (no
+    launcher in between): whatever the ranks' libraries print (gloo / RCCL banners) must reach
+    stderr, and stdout must hold exactly rank 0's JSON line."""
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--dry-run", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=240, env=e, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["ranks"] == 2

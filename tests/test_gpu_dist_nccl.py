@@ -31,8 +31,8 @@ def test_bench_one_rank_rccl_group(torch_gpu):
                         "--batch", "65536", "--global-batch", "65536", "--scatter", "--no-cpu-baseline"],
                        capture_output=True, text=True, timeout=110, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]   # RCCL's banner goes to stderr
     line = json.loads(lines[0])
     assert line["dist_backend"] == "nccl" and line["n_gpus"] == 1 and line["devices_used"] == 1
     assert line["parity"]["bit_exact"] and line["parity"]["ranks_checked"] == 1
