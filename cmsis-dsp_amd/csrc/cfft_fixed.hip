@@ -113,7 +113,15 @@ template <typename C> __device__ __forceinline__ int sfx(int e) {
   if constexpr (sizeof(C) == 8) return e + (e >> 8);
   else return s4096(e);
 }
-template <typename C> constexpr int kFxSlots = sizeof(C) == 8 ? 4096 + 16 : 4351;
+// LDS complex slots of the q31 N = 4096 kernel: 4112 are used; the image is sized to 6912 (54 KiB)
+// so that two workgroups share a CU (three fit by registers): configs[3] q31 344-348 -> 350-352
+// Gsamples/s, bit-exact (profiles/r03/experiments/fx4096_residency.json; one workgroup per CU
+// 274, and the q15 kernel is fastest at its register-bound three).  The in-place streaming probe
+// of this access pattern ranks the same way (profiles/r03/probe_hbm_wgtile.txt, lds = 55296).
+#ifndef MI355X_FX_Q31_SLOTS
+#define MI355X_FX_Q31_SLOTS 6912
+#endif
+template <typename C> constexpr int kFxSlots = sizeof(C) == 8 ? MI355X_FX_Q31_SLOTS : 4351;
 
 #ifndef MI355X_FX_WAVES
 #define MI355X_FX_WAVES 1     // minimum waves per SIMD the register allocation must allow
@@ -311,6 +319,9 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 // MI355X_FXQ15_TW34_LDS = 1: the stage-3/4 twiddle pairs (functions of t % 16 only) live in
 // LDS tables (1.5 KiB + 384 B) instead of 30 VGPRs; MI355X_FXQ15_WAVES = the minimum waves per
 // SIMD the register allocation must allow.
+#ifndef MI355X_FXQ15_SLOTS
+#define MI355X_FXQ15_SLOTS 4351   // LDS words of the q15 kernel (more: fewer workgroups per CU)
+#endif
 #ifndef MI355X_FXQ15_TW34_LDS
 #define MI355X_FXQ15_TW34_LDS 0
 #endif
@@ -320,7 +331,7 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 template <bool INV, bool BREV, bool SAT>
 __global__ __launch_bounds__(256, MI355X_FXQ15_WAVES) void cfft_q15_4096_pk_kernel(short2* __restrict__ data, uint32_t batch,
                                                                     const short2* __restrict__ tw) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[4351];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[MI355X_FXQ15_SLOTS];
   const int t = threadIdx.x;
   const int q2 = t >> 4, j2 = t & 15;
   const int q3 = (int)(__brev((uint32_t)t) >> 24);        // rev8(t)
