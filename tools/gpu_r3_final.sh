@@ -16,5 +16,5 @@ cat $O/bench_default.json
 CMSISDSP_DIST_SINGLE=1 RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 LOCAL_WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29611 \
   timeout -k 10 300 python -u bench.py --gpus 1 --scatter > $O/bench_rccl1.json 2> $O/bench_rccl1.err
 cat $O/bench_rccl1.json
-bash tools/profile_round.sh r03 mfcc_f32:hbm > $O/profile.log 2>&1
+bash tools/profile_round.sh r03 cfft_q31_4096_strong1M:hbm > $O/profile.log 2>&1
 tail -3 $O/profile.log
