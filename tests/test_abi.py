@@ -98,3 +98,12 @@ def test_init_functions_match_reference(dsp, ref, kind):
         assert st == st_r
         if st == 0:
             assert (S.fftLen, S.bitRevLength) == (Sr.fftLen, Sr.bitRevLength)
+
+
+def test_shipped_library_is_the_default_build(dsp):
+    """The in-tree library that tests, smoke() and bench.py load is built with no tuning macro
+    (arm_mi355x_version() lists any in brackets, and every bench line prints it as `library`),
+    so the measured kernels are the documented defaults."""
+    v = dsp.version()
+    assert v.startswith("cmsisdsp-mi355x ") and "gfx950" in v
+    assert "[" not in v, v
