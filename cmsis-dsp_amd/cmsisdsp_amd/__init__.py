@@ -454,6 +454,51 @@ def fir_batch(S, src, dst, hist, stream=None, q15=False, kind=None):
         raise RuntimeError(f"{fn.__name__} -> {st}: {last_error()[1]}")
 
 
+def fir_batch_multi(S, shards, kind=None):
+    """FIR over filter shards on several devices through one arm_fir_*_batch_multi call
+    (synchronous): shards = [(src, dst, hist), ...], torch tensors [batch_s, blockSize] /
+    [batch_s, numTaps-1] on each shard's device."""
+    import torch
+    if kind is None:
+        kind = {arm_fir_instance_f32: "f32", arm_fir_instance_q15: "q15",
+                arm_fir_instance_q31: "q31", arm_fir_instance_q7: "q7"}[type(S)]
+    k = len(shards)
+    for d in sorted({t[0].device.index for t in shards}):
+        torch.cuda.synchronize(d)
+    block = shards[0][0].shape[1] if k else 0
+    devs = (C.c_int * k)(*[t[0].device.index for t in shards])
+    src = (C.c_void_p * k)(*[t[0].data_ptr() for t in shards])
+    dst = (C.c_void_p * k)(*[t[1].data_ptr() for t in shards])
+    hist = (C.c_void_p * k)(*[t[2].data_ptr() if t[2] is not None and t[2].numel() else 0 for t in shards])
+    cnts = (C.c_uint32 * k)(*[t[0].shape[0] for t in shards])
+    fn = getattr(lib, f"arm_fir_{kind}_batch_multi")
+    st = fn(C.byref(S), k, devs, src, dst, hist, block, cnts)
+    if st != ARM_MATH_SUCCESS:
+        raise RuntimeError(f"{fn.__name__} -> {st}: {last_error()[1]}")
+
+
+def mat_mult_batch_multi(shards):
+    """c[i] = a[i] @ b[i] per shard through one arm_mat_mult_*_batch_multi call (synchronous):
+    shards = [(a, b, c), ...] with [batch_s, M, K] x [batch_s, K, N] -> [batch_s, M, N] tensors
+    on each shard's device (f32 / int16 / int32)."""
+    import torch
+    a0, b0, _ = shards[0]
+    m, k_, n = a0.shape[1], a0.shape[2], b0.shape[2]
+    kind, inst = {torch.float32: ("f32", arm_matrix_instance_f32), torch.int16: ("q15", arm_matrix_instance_q15),
+                  torch.int32: ("q31", arm_matrix_instance_q31)}[a0.dtype]
+    for d in sorted({t[0].device.index for t in shards}):
+        torch.cuda.synchronize(d)
+    k = len(shards)
+    A, B, Cm = inst(m, k_, None), inst(k_, n, None), inst(m, n, None)
+    devs = (C.c_int * k)(*[t[0].device.index for t in shards])
+    pa, pb, pc = ((C.c_void_p * k)(*[t[i].data_ptr() for t in shards]) for i in range(3))
+    cnts = (C.c_uint32 * k)(*[t[0].shape[0] for t in shards])
+    fn = getattr(lib, f"arm_mat_mult_{kind}_batch_multi")
+    st = fn(C.byref(A), C.byref(B), C.byref(Cm), k, devs, pa, pb, pc, cnts)
+    if st != ARM_MATH_SUCCESS:
+        raise RuntimeError(f"{fn.__name__} -> {st}: {last_error()[1]}")
+
+
 def arm_conv(kind, a, b):
     """arm_conv_f32 / _q15 / _q31 / _q7 (drop-in, numpy): len(a) + len(b) - 1 samples."""
     dt = {"f32": np.float32, "q15": np.int16, "q31": np.int32, "q7": np.int8}[kind]

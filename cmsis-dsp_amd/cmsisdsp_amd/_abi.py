@@ -306,6 +306,14 @@ BATCHED = {
                                                C.c_uint8, C.c_uint8])
        for t, inst in (("f32", arm_cfft_instance_f32), ("q31", arm_cfft_instance_q31),
                        ("q15", arm_cfft_instance_q15))},
+    **{f"arm_fir_{t}_batch_multi": (C.c_int, [P(inst), C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                              C.c_uint32, C.c_void_p])
+       for t, inst in (("f32", arm_fir_instance_f32), ("q15", arm_fir_instance_q15), ("fast_q15", arm_fir_instance_q15),
+                       ("q31", arm_fir_instance_q31), ("fast_q31", arm_fir_instance_q31), ("q7", arm_fir_instance_q7))},
+    **{f"arm_mat_mult_{t}_batch_multi": (C.c_int, [P(inst), P(inst), P(inst), C.c_uint32, C.c_void_p, C.c_void_p,
+                                                   C.c_void_p, C.c_void_p, C.c_void_p])
+       for t, inst in (("f32", arm_matrix_instance_f32), ("q15", arm_matrix_instance_q15),
+                       ("q31", arm_matrix_instance_q31))},
     "arm_mi355x_device_count": (C.c_int, []),
     "arm_mi355x_last_error": (C.c_int, []),
     "arm_mi355x_last_error_string": (C.c_char_p, []),

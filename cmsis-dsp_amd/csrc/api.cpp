@@ -63,9 +63,10 @@ template <typename Inst>
 void cfft_sync(const Inst* S, void* p1, uint8_t ifftFlag, uint8_t bitReverseFlag, int kind, size_t word) {
   if (!S || !p1 || !cfft_len_ok(S->fftLen)) return;       // reference: silent no-op
   const uint32_t n = S->fftLen;
+  hipStream_t st = sync_stream();
+  BlobScope hold(st);
   CfftPrep pr;
   if (!cfft_prepare(n, S->pTwiddle, S->pBitRevTable, S->bitRevLength, kind, ifftFlag, bitReverseFlag, pr)) return;
-  hipStream_t st = sync_stream();
   const size_t bytes = 2 * word * n;
   if (is_device_ptr(p1)) {
     hipError_t e = cfft_launch(kind, n, p1, 1, pr, st);
@@ -96,6 +97,7 @@ template <typename Inst>
 arm_status cfft_batch(const Inst* S, void* d_p1, uint32_t batch, uint8_t ifftFlag, uint8_t bitReverseFlag,
                       void* stream, int kind) {
   if (!S || (!d_p1 && batch) || !cfft_len_ok(S->fftLen)) return ARM_MATH_ARGUMENT_ERROR;
+  BlobScope hold((hipStream_t)stream);
   CfftPrep pr;
   if (!cfft_prepare(S->fftLen, S->pTwiddle, S->pBitRevTable, S->bitRevLength, kind, ifftFlag, bitReverseFlag, pr))
     return ARM_MATH_ARGUMENT_ERROR;
@@ -104,15 +106,15 @@ arm_status cfft_batch(const Inst* S, void* d_p1, uint32_t batch, uint8_t ifftFla
   return ARM_MATH_SUCCESS;
 }
 
-// multi-GPU: validate every shard, launch each on its device's internal stream, then wait
-template <typename Inst>
-arm_status cfft_batch_multi(const Inst* S, uint32_t nshards, const int* devices, void* const* d_p1,
-                            const uint32_t* batch, uint8_t ifftFlag, uint8_t bitReverseFlag, int kind) {
-  if (!S || !cfft_len_ok(S->fftLen) || (nshards && (!devices || !d_p1 || !batch))) return ARM_MATH_ARGUMENT_ERROR;
+// multi-GPU: validate every shard, launch each on its device's internal stream (one BlobScope per
+// shard, so the tables a shard uses stay held until its launches are enqueued), then wait for
+// every device that received work.  launch(s, st) enqueues shard s on st (its device current).
+template <typename Launch>
+arm_status run_multi(uint32_t nshards, const int* devices, const uint32_t* batch, const char* what, Launch&& launch) {
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) { (void)hipGetLastError(); ndev = 0; }
   for (uint32_t s = 0; s < nshards; ++s)
-    if (devices[s] < 0 || devices[s] >= ndev || (batch[s] && !d_p1[s])) return ARM_MATH_ARGUMENT_ERROR;
+    if (devices[s] < 0 || devices[s] >= ndev) return ARM_MATH_ARGUMENT_ERROR;
   int prev = 0;
   (void)hipGetDevice(&prev);
   std::vector<int> used;
@@ -120,24 +122,36 @@ arm_status cfft_batch_multi(const Inst* S, uint32_t nshards, const int* devices,
   for (uint32_t s = 0; s < nshards && status == ARM_MATH_SUCCESS; ++s) {
     if (!batch[s]) continue;
     hipError_t e = hipSetDevice(devices[s]);
-    CfftPrep pr;
-    if (e != hipSuccess) { set_error(e, "arm_cfft_batch_multi: hipSetDevice"); status = ARM_MATH_ARGUMENT_ERROR; break; }
-    if (!cfft_prepare(S->fftLen, S->pTwiddle, S->pBitRevTable, S->bitRevLength, kind, ifftFlag, bitReverseFlag, pr)) {
-      status = ARM_MATH_ARGUMENT_ERROR;
-      break;
-    }
-    hipStream_t st = sync_stream();
-    e = st ? cfft_launch(kind, S->fftLen, d_p1[s], batch[s], pr, st) : hipErrorOutOfMemory;
-    if (e != hipSuccess) { set_error(e, "arm_cfft_batch_multi"); status = ARM_MATH_ARGUMENT_ERROR; }
+    if (e != hipSuccess) { set_error(e, what); status = ARM_MATH_ARGUMENT_ERROR; break; }
     if (std::find(used.begin(), used.end(), devices[s]) == used.end()) used.push_back(devices[s]);
+    hipStream_t st = sync_stream();
+    if (!st) { set_error(hipErrorOutOfMemory, what); status = ARM_MATH_ARGUMENT_ERROR; break; }
+    BlobScope hold(st);
+    if (!launch(s, st)) status = ARM_MATH_ARGUMENT_ERROR;
   }
   for (int d : used) {   // drain every device that received work, also after a failure
     hipError_t e = hipSetDevice(d);
     if (e == hipSuccess) e = hipStreamSynchronize(sync_stream());
-    if (e != hipSuccess) { set_error(e, "arm_cfft_batch_multi: sync"); status = ARM_MATH_ARGUMENT_ERROR; }
+    if (e != hipSuccess) { set_error(e, what); status = ARM_MATH_ARGUMENT_ERROR; }
   }
   (void)hipSetDevice(prev);
   return status;
+}
+
+template <typename Inst>
+arm_status cfft_batch_multi(const Inst* S, uint32_t nshards, const int* devices, void* const* d_p1,
+                            const uint32_t* batch, uint8_t ifftFlag, uint8_t bitReverseFlag, int kind) {
+  if (!S || !cfft_len_ok(S->fftLen) || (nshards && (!devices || !d_p1 || !batch))) return ARM_MATH_ARGUMENT_ERROR;
+  for (uint32_t s = 0; s < nshards; ++s)
+    if (batch[s] && !d_p1[s]) return ARM_MATH_ARGUMENT_ERROR;
+  return run_multi(nshards, devices, batch, "arm_cfft_batch_multi", [&](uint32_t s, hipStream_t st) {
+    CfftPrep pr;
+    if (!cfft_prepare(S->fftLen, S->pTwiddle, S->pBitRevTable, S->bitRevLength, kind, ifftFlag, bitReverseFlag, pr))
+      return false;
+    hipError_t e = cfft_launch(kind, S->fftLen, d_p1[s], batch[s], pr, st);
+    if (e != hipSuccess) { set_error(e, "arm_cfft_batch_multi"); return false; }
+    return true;
+  });
 }
 
 bool rfft_len_ok(uint32_t n) { return n >= 32 && n <= 4096 && (n & (n - 1)) == 0; }
@@ -147,6 +161,7 @@ bool rfft_run(const arm_rfft_fast_instance_f32* S, float* d_p, float* d_out, uin
               hipStream_t st) {
   const uint32_t n = S->fftLenRFFT, h = S->Sint.fftLen;
   if (h != n / 2 || !cfft_len_ok(h)) { set_error(hipErrorInvalidValue, "rfft instance"); return false; }
+  BlobScope hold(st);
   const void* twr = device_table(S->pTwiddleRFFT, sizeof(float) * n);
   if (!twr) return false;
   CfftPrep pr;
@@ -180,6 +195,7 @@ bool rfft_fixed_run(const RInst* S, T* d_src, T* d_dst, uint32_t batch, hipStrea
   const uint32_t n = S->fftLenReal, L = n / 2;
   const auto* in = S->pCfft;
   if (!in || in->fftLen != L || !cfft_len_ok(L) || n > 8192) { set_error(hipErrorInvalidValue, "rfft instance"); return false; }
+  BlobScope hold(st);
   // the split reads realCoef[2*mod*k + 1] for k < L: mod * N words cover it
   const size_t words = std::max<size_t>(2, (size_t)S->twidCoefRModifier * n);
   const T* ta = (const T*)device_table(S->pTwiddleAReal, sizeof(T) * words);
@@ -314,6 +330,7 @@ bool mfcc_run(const arm_mfcc_instance_f32* S, const MfccDev& d, float* x, float*
               hipStream_t st) {
   const int n = (int)S->fftLen, nd = (int)S->nbDctOutputs, nm = (int)S->nbMelFilters;
   const arm_cfft_instance_f32& in = S->rfft.Sint;
+  BlobScope hold(st);
   bool canon = true, ok = true;
   if (in.pBitRevTable) (void)device_perm((int)in.fftLen, in.pBitRevTable, in.bitRevLength, 0, &canon, &ok);
   if (ok && canon && nm <= n / 2 && in.fftLen == (uint32_t)n / 2) {
@@ -436,6 +453,7 @@ bool mfcc_fx_run(const Inst* S, const MfccFxDev<T>& d, T* x, T* y, T* dst, uint3
   const auto* in = S->rfft.pCfft;
   const uint32_t L = (uint32_t)n / 2;
   if (!in || in->fftLen != L || !cfft_len_ok(L)) { set_error(hipErrorInvalidValue, "mfcc rfft instance"); return false; }
+  BlobScope hold(st);
   CfftPrep pr;
   if (!cfft_prepare(L, in->pTwiddle, in->pBitRevTable, in->bitRevLength, sizeof(T) == 4 ? 1 : 2, 0,
                     S->rfft.bitReverseFlagR, pr))
@@ -493,6 +511,7 @@ void fir_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B, int kind) {
   if (!S || !S->pState || !S->pCoeffs || S->numTaps == 0 || B == 0) return;
   const int taps = S->numTaps, T1 = taps - 1;
   hipStream_t st = sync_stream();
+  BlobScope hold(st);
   bool ok = true;
   const T* dc = device_coeffs<T>(S->pCoeffs, taps, &ok);
   if (!ok) { set_error(hipErrorOutOfMemory, "arm_fir coeffs"); return; }
@@ -545,12 +564,32 @@ arm_status fir_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uint32
   if (!S || !S->pCoeffs || S->numTaps == 0 || (batch && B && (!d_src || !d_dst))) return ARM_MATH_ARGUMENT_ERROR;
   if (S->numTaps > 1 && batch && !d_hist) return ARM_MATH_ARGUMENT_ERROR;
   hipStream_t st = (hipStream_t)stream;
+  BlobScope hold(st);
   bool ok = true;
   const T* dc = device_coeffs<T>(S->pCoeffs, S->numTaps, &ok);
   if (!ok) { set_error(hipErrorOutOfMemory, "arm_fir_batch coeffs"); return ARM_MATH_ARGUMENT_ERROR; }
   hipError_t e = fir_run(kind, dc, S->numTaps, d_src, d_dst, B, batch, d_hist, st);
   if (e != hipSuccess) { set_error(e, "arm_fir_batch"); return ARM_MATH_ARGUMENT_ERROR; }
   return ARM_MATH_SUCCESS;
+}
+
+// multi-GPU FIR (the batch is sliced by filter, each shard's history rows stay on
+// its device): shard s = batch[s] filters at d_src[s] / d_dst[s] / d_hist[s] on devices[s].
+template <typename T, typename Inst>
+arm_status fir_batch_multi(const Inst* S, uint32_t nshards, const int* devices, const T* const* d_src, T* const* d_dst,
+                           T* const* d_hist, uint32_t B, const uint32_t* batch, int kind) {
+  if (!S || !S->pCoeffs || S->numTaps == 0 || (nshards && (!devices || !batch || !d_src || !d_dst || !d_hist)))
+    return ARM_MATH_ARGUMENT_ERROR;
+  for (uint32_t s = 0; s < nshards; ++s)
+    if (batch[s] && ((B && (!d_src[s] || !d_dst[s])) || (S->numTaps > 1 && !d_hist[s]))) return ARM_MATH_ARGUMENT_ERROR;
+  return run_multi(nshards, devices, batch, "arm_fir_batch_multi", [&](uint32_t s, hipStream_t st) {
+    bool ok = true;
+    const T* dc = device_coeffs<T>(S->pCoeffs, S->numTaps, &ok);   // uploaded once per device
+    if (!ok) return false;
+    hipError_t e = fir_run(kind, dc, S->numTaps, d_src[s], d_dst[s], B, batch[s], d_hist[s], st);
+    if (e != hipSuccess) { set_error(e, "arm_fir_batch_multi"); return false; }
+    return true;
+  });
 }
 
 // zero a host or device buffer (the init functions' memset)
@@ -573,6 +612,7 @@ void mr_sync(T* pState, const T* pCoeffs, int ncoef, int H, const T* pSrc, T* pD
              const char* what, Run&& run) {
   if (!pState || !pCoeffs || ncoef <= 0 || B == 0) return;
   hipStream_t st = sync_stream();
+  BlobScope hold(st);
   bool ok = true;
   const T* dc = device_coeffs<T>(pCoeffs, ncoef, &ok);
   if (!ok) { set_error(hipErrorOutOfMemory, what); return; }
@@ -639,6 +679,7 @@ arm_status decimate_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, u
                           void* stream, int op, const char* what) {
   if (!S || !S->pCoeffs || S->numTaps == 0 || S->M == 0) return ARM_MATH_ARGUMENT_ERROR;
   if (batch && B && (!d_src || (B >= S->M && !d_dst) || (S->numTaps > 1 && !d_hist))) return ARM_MATH_ARGUMENT_ERROR;
+  BlobScope hold((hipStream_t)stream);
   bool ok = true;
   const T* dc = device_coeffs<T>(S->pCoeffs, S->numTaps, &ok);
   if (!ok) { set_error(hipErrorOutOfMemory, what); return ARM_MATH_ARGUMENT_ERROR; }
@@ -651,6 +692,7 @@ arm_status interpolate_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B
                              void* stream, int op, const char* what) {
   if (!S || !S->pCoeffs || S->phaseLength == 0 || S->L == 0) return ARM_MATH_ARGUMENT_ERROR;
   if (batch && B && (!d_src || !d_dst || (S->phaseLength > 1 && !d_hist))) return ARM_MATH_ARGUMENT_ERROR;
+  BlobScope hold((hipStream_t)stream);
   bool ok = true;
   const T* dc = device_coeffs<T>(S->pCoeffs, (int)S->L * S->phaseLength, &ok);
   if (!ok) { set_error(hipErrorOutOfMemory, what); return ARM_MATH_ARGUMENT_ERROR; }
@@ -682,6 +724,7 @@ void sparse_sync(Inst* S, const T* pSrc, T* pDst, uint32_t B, int op, const char
   const int taps = S->numTaps;
   const uint32_t L = (uint32_t)S->maxDelay + B;
   hipStream_t st = sync_stream();
+  BlobScope hold(st);
   bool ok = true, okd = true;
   const T* dc = device_coeffs<T>(S->pCoeffs, taps, &ok);
   const int32_t* dd = device_coeffs<int32_t>(S->pTapDelay, taps, &okd);
@@ -745,6 +788,7 @@ arm_status sparse_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, uin
                         int op, const char* what) {
   if (!S || !S->pCoeffs || !S->pTapDelay || S->numTaps == 0) return ARM_MATH_ARGUMENT_ERROR;
   if (batch && B && (!d_src || !d_dst || (S->maxDelay > 0 && !d_hist))) return ARM_MATH_ARGUMENT_ERROR;
+  BlobScope hold((hipStream_t)stream);
   bool ok = true, okd = true;
   const T* dc = device_coeffs<T>(S->pCoeffs, S->numTaps, &ok);
   const int32_t* dd = device_coeffs<int32_t>(S->pTapDelay, S->numTaps, &okd);
@@ -770,6 +814,7 @@ void lattice_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B, int op, con
   if (!S || !S->pState || !S->pCoeffs || S->numStages == 0 || B == 0) return;
   const int M = S->numStages;
   hipStream_t st = sync_stream();
+  BlobScope hold(st);
   bool ok = true;
   const T* dc = device_coeffs<T>(S->pCoeffs, M, &ok);
   if (!ok) { set_error(hipErrorOutOfMemory, what); return; }
@@ -795,6 +840,7 @@ arm_status lattice_batch(const Inst* S, const T* d_src, T* d_dst, uint32_t B, ui
                          void* stream, int op, const char* what) {
   if (!S || !S->pCoeffs || S->numStages == 0) return ARM_MATH_ARGUMENT_ERROR;
   if (batch && B && (!d_src || !d_dst || !d_state)) return ARM_MATH_ARGUMENT_ERROR;
+  BlobScope hold((hipStream_t)stream);
   bool ok = true;
   const T* dc = device_coeffs<T>(S->pCoeffs, S->numStages, &ok);
   if (!ok) { set_error(hipErrorOutOfMemory, what); return ARM_MATH_ARGUMENT_ERROR; }
@@ -895,6 +941,23 @@ bool partial_range_ok(uint32_t alen, uint32_t blen, uint32_t first, uint32_t num
 template <typename M>
 bool mat_shapes_ok(const M* a, const M* b, const M* c) {
   return a->numCols == b->numRows && a->numRows == c->numRows && b->numCols == c->numCols;
+}
+
+// multi-GPU matrix multiply: shard s = batch[s] matrices (shapes of the instances) at d_a[s],
+// d_b[s], d_c[s] on devices[s].  launch(m, k, n, a, b, c, batch, st) is the per-type launcher.
+template <typename T, typename M, typename Launch>
+arm_status mat_batch_multi(const M* pSrcA, const M* pSrcB, M* pDst, uint32_t nshards, const int* devices,
+                           const T* const* d_a, const T* const* d_b, T* const* d_c, const uint32_t* batch,
+                           const char* what, Launch&& launch) {
+  if (!pSrcA || !pSrcB || !pDst || (nshards && (!devices || !batch || !d_a || !d_b || !d_c))) return ARM_MATH_ARGUMENT_ERROR;
+  if (!mat_shapes_ok(pSrcA, pSrcB, pDst)) return ARM_MATH_SIZE_MISMATCH;
+  for (uint32_t s = 0; s < nshards; ++s)
+    if (batch[s] && (!d_a[s] || !d_b[s] || !d_c[s])) return ARM_MATH_ARGUMENT_ERROR;
+  return run_multi(nshards, devices, batch, what, [&](uint32_t s, hipStream_t st) {
+    hipError_t e = launch(pSrcA->numRows, pSrcA->numCols, pSrcB->numCols, d_a[s], d_b[s], d_c[s], batch[s], st);
+    if (e != hipSuccess) { set_error(e, what); return false; }
+    return true;
+  });
 }
 
 // drop-in fixed-point matrix multiply (host or device operands), synchronous
@@ -1105,6 +1168,42 @@ arm_status arm_fir_q7_batch(const arm_fir_instance_q7* S, const q7_t* d_src, q7_
   return fir_batch<int8_t>(S, d_src, d_dst, blockSize, batch, d_hist, stream, kFirQ7);
 }
 
+#define MI355X_FIR_MULTI(NAME, INST, T, CT, KIND)                                                          \
+  arm_status NAME##_batch_multi(const INST* S, uint32_t nshards, const int* devices, const T* const* d_src, \
+                                T* const* d_dst, T* const* d_hist, uint32_t blockSize, const uint32_t* batch) { \
+    return fir_batch_multi<CT>(S, nshards, devices, (const CT* const*)d_src, (CT* const*)d_dst,          \
+                               (CT* const*)d_hist, blockSize, batch, KIND);                              \
+  }
+MI355X_FIR_MULTI(arm_fir_f32, arm_fir_instance_f32, float32_t, float, kFirF32)
+MI355X_FIR_MULTI(arm_fir_q15, arm_fir_instance_q15, q15_t, int16_t, kFirQ15)
+MI355X_FIR_MULTI(arm_fir_fast_q15, arm_fir_instance_q15, q15_t, int16_t, kFirFastQ15)
+MI355X_FIR_MULTI(arm_fir_q31, arm_fir_instance_q31, q31_t, int32_t, kFirQ31)
+MI355X_FIR_MULTI(arm_fir_fast_q31, arm_fir_instance_q31, q31_t, int32_t, kFirFastQ31)
+MI355X_FIR_MULTI(arm_fir_q7, arm_fir_instance_q7, q7_t, int8_t, kFirQ7)
+#undef MI355X_FIR_MULTI
+
+arm_status arm_mat_mult_f32_batch_multi(const arm_matrix_instance_f32* pSrcA, const arm_matrix_instance_f32* pSrcB,
+                                        arm_matrix_instance_f32* pDst, uint32_t nshards, const int* devices,
+                                        const float32_t* const* d_a, const float32_t* const* d_b,
+                                        float32_t* const* d_c, const uint32_t* batch) {
+  return mat_batch_multi<float>(pSrcA, pSrcB, pDst, nshards, devices, d_a, d_b, d_c, batch,
+                                "arm_mat_mult_f32_batch_multi", mat_mult_f32_launch);
+}
+arm_status arm_mat_mult_q15_batch_multi(const arm_matrix_instance_q15* pSrcA, const arm_matrix_instance_q15* pSrcB,
+                                        arm_matrix_instance_q15* pDst, uint32_t nshards, const int* devices,
+                                        const q15_t* const* d_a, const q15_t* const* d_b, q15_t* const* d_c,
+                                        const uint32_t* batch) {
+  return mat_batch_multi<int16_t>(pSrcA, pSrcB, pDst, nshards, devices, d_a, d_b, d_c, batch,
+                                  "arm_mat_mult_q15_batch_multi", mat_mult_q15_launch);
+}
+arm_status arm_mat_mult_q31_batch_multi(const arm_matrix_instance_q31* pSrcA, const arm_matrix_instance_q31* pSrcB,
+                                        arm_matrix_instance_q31* pDst, uint32_t nshards, const int* devices,
+                                        const q31_t* const* d_a, const q31_t* const* d_b, q31_t* const* d_c,
+                                        const uint32_t* batch) {
+  return mat_batch_multi<int32_t>(pSrcA, pSrcB, pDst, nshards, devices, d_a, d_b, d_c, batch,
+                                  "arm_mat_mult_q31_batch_multi", mat_mult_q31_launch);
+}
+
 arm_status arm_mat_mult_f32(const arm_matrix_instance_f32* pSrcA, const arm_matrix_instance_f32* pSrcB,
                             arm_matrix_instance_f32* pDst) {
   if (!pSrcA || !pSrcB || !pDst) return ARM_MATH_ARGUMENT_ERROR;
@@ -1142,10 +1241,11 @@ arm_status arm_mat_mult_f32_batch(const arm_matrix_instance_f32* pSrcA, const ar
 void arm_mfcc_f32(const arm_mfcc_instance_f32* S, float32_t* pSrc, float32_t* pDst, float32_t* pTmp) {
   (void)pTmp;   // work space lives on the device; the reference's pTmp contents are not reproduced
   if (!S || !pSrc || !pDst || S->nbDctOutputs == 0) return;
+  hipStream_t st = sync_stream();
+  BlobScope hold(st);
   MfccDev d;
   if (!mfcc_prepare(S, d)) return;
   const uint32_t n = S->fftLen, nd = S->nbDctOutputs;
-  hipStream_t st = sync_stream();
   float* x = (float*)scratch(sizeof(float) * n, 0);
   float* y = (float*)scratch(sizeof(float) * n, 1);
   const bool ddst = is_device_ptr(pDst);
@@ -1165,6 +1265,7 @@ arm_status arm_mfcc_f32_batch(const arm_mfcc_instance_f32* S, float32_t* d_src, 
                               uint32_t batch, void* stream) {
   if (!S || (batch && (!d_src || !d_dst || !d_tmp))) return ARM_MATH_ARGUMENT_ERROR;
   if (batch == 0 || S->nbDctOutputs == 0) return ARM_MATH_SUCCESS;
+  BlobScope hold((hipStream_t)stream);
   MfccDev d;
   if (!mfcc_prepare(S, d)) return ARM_MATH_ARGUMENT_ERROR;
   return mfcc_run(S, d, d_src, d_tmp, d_dst, batch, (hipStream_t)stream) ? ARM_MATH_SUCCESS : ARM_MATH_ARGUMENT_ERROR;
@@ -1177,10 +1278,11 @@ template <typename T, typename Inst>
 static arm_status mfcc_fx_dropin(const Inst* S, T* pSrc, T* pDst, const char* what) {
   if (!S || !pSrc || !pDst) return ARM_MATH_ARGUMENT_ERROR;
   if (S->nbDctOutputs == 0) return ARM_MATH_SUCCESS;
+  hipStream_t st = sync_stream();
+  BlobScope hold(st);
   MfccFxDev<T> d;
   if (!mfcc_fx_prepare<T>(S, d)) return ARM_MATH_ARGUMENT_ERROR;
   const uint32_t n = S->fftLen, nd = S->nbDctOutputs;
-  hipStream_t st = sync_stream();
   T* x = (T*)scratch(sizeof(T) * n, 0);
   T* y = (T*)scratch(sizeof(T) * 2 * n, 1);
   const bool ddst = is_device_ptr(pDst);
@@ -1201,6 +1303,7 @@ template <typename T, typename Inst>
 static arm_status mfcc_fx_batch(const Inst* S, T* d_src, T* d_dst, T* d_tmp, uint32_t batch, void* stream) {
   if (!S || (batch && (!d_src || !d_dst || !d_tmp))) return ARM_MATH_ARGUMENT_ERROR;
   if (batch == 0 || S->nbDctOutputs == 0) return ARM_MATH_SUCCESS;
+  BlobScope hold((hipStream_t)stream);
   MfccFxDev<T> d;
   if (!mfcc_fx_prepare<T>(S, d)) return ARM_MATH_ARGUMENT_ERROR;
   return mfcc_fx_run<T>(S, d, d_src, d_tmp, d_dst, batch, (hipStream_t)stream) ? ARM_MATH_SUCCESS

@@ -513,15 +513,11 @@ static hipError_t launch_fx(void* data, uint32_t batch, const void* tw, const ui
   return hipGetLastError();
 }
 
-// MI355X_FX_R16 = 0 routes N = 256..2048 to the generic LDS-stage kernels (A/B builds).
-#ifndef MI355X_FX_R16
-#define MI355X_FX_R16 1
-#endif
 template <typename T>
 static hipError_t dispatch_fx(int n, void* data, uint32_t batch, const void* tw, const uint16_t* perm,
                               uint32_t flags, hipStream_t st) {
   if (batch == 0) return hipSuccess;
-  if (MI355X_FX_R16 && !perm) {   // the reference's own table: radix-16-pass kernels
+  if (!perm) {   // the reference's own table: radix-16-pass kernels (the MFCC front end uses them too)
     const bool done = sizeof(T) == 4
         ? cfft_q31_r16_launch(n, (int32_t*)data, batch, (const int32_t*)tw, flags, st)
         : cfft_q15_r16_launch(n, (int16_t*)data, batch, (const int16_t*)tw, flags, st);

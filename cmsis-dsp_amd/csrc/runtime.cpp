@@ -5,7 +5,9 @@
 #include <link.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <tuple>
@@ -21,38 +23,141 @@ thread_local std::string g_err_msg;
 
 std::mutex g_table_mu;
 std::map<std::tuple<int, const void*, size_t>, void*> g_tables;
-std::map<std::tuple<int, const void*, uint16_t, int, int>, std::pair<void*, bool>> g_perms;
+// library-address bit-reversal tables: their verdict and, when not canonical, the permutation
+// (re-resolved through the blob cache on every call: no raw blob pointer is kept here)
+struct PermEntry { bool canon = true; std::vector<uint16_t> perm; };
+std::map<std::tuple<int, const void*, uint16_t, int, int>, PermEntry> g_perms;
 
-// Content-keyed blob cache, bounded: an LRU by bytes per process (default 256 MiB, set with
-// arm_mi355x_set_table_cache_limit).  Evicting synchronizes the device before hipFree, since
-// an asynchronous batched call may still be reading the blob on any stream.
-struct Blob { std::vector<uint8_t> host; void* dev = nullptr; int d = 0; uint64_t tick = 0; };
-std::map<std::tuple<int, uint64_t, size_t>, std::vector<Blob>> g_blobs;
-size_t g_blob_bytes = 0;
-size_t g_blob_limit = size_t(256) << 20;
-uint64_t g_blob_tick = 0;
+// ---- content-keyed blob cache --------------------------------------------------------------
+// An LRU bounded in bytes PER DEVICE (default 256 MiB, arm_mi355x_set_table_cache_limit).
+// Lifetime rules (round 4):
+//  * a blob handed out inside a BlobScope is HELD (holds > 0) until the scope ends, so no other
+//    thread's insertion -- and no later lookup of the same call -- can evict it before the
+//    launches that read it are enqueued;
+//  * the scope then records one event on its stream after that work; the blob keeps the events
+//    of its uses that may still be pending;
+//  * eviction never synchronizes the device and never runs under g_table_mu: the victim leaves
+//    the map under the lock, and afterwards its memory is released with hipFreeAsync on a
+//    per-device reclaim stream made to wait on the victim's use events (stream order, so later
+//    work on other streams is not stalled).
+// Blobs are allocated with hipMallocAsync (stream-ordered pool) on a per-device upload stream.
+// All state lives in heap objects that are never destroyed: no static-destruction ordering.
+struct EvPool {
+  std::mutex mu;
+  std::map<int, std::vector<hipEvent_t>> free;
+};
+EvPool& ev_pool() { static EvPool* p = new EvPool; return *p; }
 
-// evict least-recently-used blobs until `incoming` more bytes fit (caller holds g_table_mu)
-void blob_evict(size_t incoming) {
-  while (g_blob_bytes + incoming > g_blob_limit && g_blob_bytes > 0) {
-    auto victim_bucket = g_blobs.end();
-    size_t victim = 0;
-    uint64_t oldest = UINT64_MAX;
-    for (auto it = g_blobs.begin(); it != g_blobs.end(); ++it)
-      for (size_t i = 0; i < it->second.size(); ++i)
-        if (it->second[i].tick < oldest) { oldest = it->second[i].tick; victim_bucket = it; victim = i; }
-    if (victim_bucket == g_blobs.end()) break;
-    Blob& b = victim_bucket->second[victim];
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    if (prev != b.d) (void)hipSetDevice(b.d);
-    (void)hipDeviceSynchronize();           // no kernel may still read it
-    (void)hipFree(b.dev);
-    if (prev != b.d) (void)hipSetDevice(prev);
-    g_blob_bytes -= b.host.size();
-    victim_bucket->second.erase(victim_bucket->second.begin() + (long)victim);
-    if (victim_bucket->second.empty()) g_blobs.erase(victim_bucket);
+struct Ev {                       // one recorded use event, shared by the blobs of one scope
+  hipEvent_t e = nullptr;
+  int d = 0;
+  ~Ev() {
+    if (!e) return;
+    EvPool& p = ev_pool();
+    std::lock_guard<std::mutex> lk(p.mu);
+    p.free[d].push_back(e);
   }
+};
+using EvRef = std::shared_ptr<Ev>;
+
+struct Blob {
+  std::vector<uint8_t> host;
+  void* dev = nullptr;
+  int d = 0;
+  uint64_t tick = 0;
+  int holds = 0;                  // live BlobScopes holding it
+  bool unscoped = false;          // handed out with no scope: released after a device sync
+  std::vector<EvRef> uses;        // events after the enqueued work that reads it
+};
+using BlobRef = std::shared_ptr<Blob>;
+
+struct BlobCache {
+  std::map<std::tuple<int, uint64_t, size_t>, std::vector<BlobRef>> map;
+  std::map<int, size_t> bytes;    // per device
+  size_t limit = size_t(256) << 20;
+  uint64_t tick = 0;
+};
+BlobCache& cache() { static BlobCache* c = new BlobCache; return *c; }   // under g_table_mu
+
+thread_local std::vector<BlobRef> t_held;   // blobs held by this thread's live scopes
+thread_local int t_scopes = 0;
+
+// per-device internal streams of the cache (created once, never destroyed)
+std::mutex g_cache_stream_mu;
+hipStream_t cache_stream(int d, int which) {
+  static std::map<std::pair<int, int>, hipStream_t>* m = new std::map<std::pair<int, int>, hipStream_t>;
+  std::lock_guard<std::mutex> lk(g_cache_stream_mu);
+  auto it = m->find({d, which});
+  if (it != m->end()) return it->second;
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  (*m)[{d, which}] = s;
+  return s;
+}
+enum { kUploadStream = 0, kReclaimStream = 1 };
+
+// drop events whose work has completed (caller holds g_table_mu)
+void prune_uses(Blob& b) {
+  b.uses.erase(std::remove_if(b.uses.begin(), b.uses.end(),
+                              [](const EvRef& r) { return hipEventQuery(r->e) == hipSuccess; }),
+               b.uses.end());
+}
+
+// take least-recently-used, unheld blobs of device d out of the map until `incoming` more bytes
+// fit (caller holds g_table_mu); returns them for release_blobs() outside the lock
+std::vector<BlobRef> evict_locked(int d, size_t incoming) {
+  BlobCache& c = cache();
+  std::vector<BlobRef> out;
+  size_t& used = c.bytes[d];
+  while (used + incoming > c.limit && used > 0) {
+    auto vb = c.map.end();
+    size_t vi = 0;
+    uint64_t oldest = UINT64_MAX;
+    for (auto it = c.map.begin(); it != c.map.end(); ++it) {
+      if (std::get<0>(it->first) != d) continue;
+      for (size_t i = 0; i < it->second.size(); ++i) {
+        const Blob& b = *it->second[i];
+        if (b.holds == 0 && b.tick < oldest) { oldest = b.tick; vb = it; vi = i; }
+      }
+    }
+    if (vb == c.map.end()) break;             // everything left is held by a live call
+    BlobRef v = vb->second[vi];
+    used -= v->host.size();
+    vb->second.erase(vb->second.begin() + (long)vi);
+    if (vb->second.empty()) c.map.erase(vb);
+    out.push_back(std::move(v));
+  }
+  return out;
+}
+
+// release evicted blobs (no lock held): stream-ordered after every recorded use
+void release_blobs(std::vector<BlobRef>& victims) {
+  if (victims.empty()) return;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  for (BlobRef& v : victims) {
+    if (v->d != prev) (void)hipSetDevice(v->d);
+    hipStream_t rs = cache_stream(v->d, kReclaimStream);
+    if (v->unscoped || !rs) (void)hipDeviceSynchronize();   // a use the cache could not track
+    else
+      for (const EvRef& r : v->uses) (void)hipStreamWaitEvent(rs, r->e, 0);
+    (void)hipFreeAsync(v->dev, rs);
+    v->uses.clear();
+    if (v->d != prev) (void)hipSetDevice(prev);
+  }
+  victims.clear();
+}
+
+// hand out blob b (caller holds g_table_mu): held by the innermost scope, if any
+const void* hand_out(const BlobRef& b) {
+  b->tick = ++cache().tick;
+  if (t_scopes > 0) {
+    ++b->holds;
+    t_held.push_back(b);
+  } else {
+    b->unscoped = true;
+  }
+  return b->dev;
 }
 
 uint64_t fnv1a(const uint8_t* p, size_t n) {
@@ -166,40 +271,96 @@ const void* device_blob(const void* host, size_t bytes) {
   const uint8_t* h = (const uint8_t*)host;
   const int dev = cur_dev();
   const auto key = std::make_tuple(dev, fnv1a(h, bytes), bytes);
-  std::lock_guard<std::mutex> lk(g_table_mu);
+  std::vector<BlobRef> victims;
   {
-    auto it = g_blobs.find(key);
-    if (it != g_blobs.end())
-      for (Blob& b : it->second)
-        if (memcmp(b.host.data(), h, bytes) == 0) { b.tick = ++g_blob_tick; return b.dev; }
+    std::lock_guard<std::mutex> lk(g_table_mu);
+    auto it = cache().map.find(key);
+    if (it != cache().map.end())
+      for (const BlobRef& b : it->second)
+        if (memcmp(b->host.data(), h, bytes) == 0) return hand_out(b);
+    victims = evict_locked(dev, bytes);
   }
-  blob_evict(bytes);
-  Blob b;
-  b.host.assign(h, h + bytes);
-  b.d = dev;
-  b.tick = ++g_blob_tick;
-  hipError_t e = hipMalloc(&b.dev, bytes);
-  if (e != hipSuccess) { set_error(e, "device_blob: hipMalloc"); return nullptr; }
-  e = hipMemcpy(b.dev, h, bytes, hipMemcpyHostToDevice);
+  release_blobs(victims);
+  auto b = std::make_shared<Blob>();
+  b->host.assign(h, h + bytes);
+  b->d = dev;
+  hipStream_t us = cache_stream(dev, kUploadStream);
+  if (!us) { set_error(hipErrorOutOfMemory, "device_blob: stream"); return nullptr; }
+  hipError_t e = hipMallocAsync(&b->dev, bytes, us);
+  if (e != hipSuccess) { set_error(e, "device_blob: hipMallocAsync"); return nullptr; }
+  e = hipMemcpyAsync(b->dev, b->host.data(), bytes, hipMemcpyHostToDevice, us);
+  if (e == hipSuccess) e = hipStreamSynchronize(us);
   if (e != hipSuccess) {
-    set_error(e, "device_blob: hipMemcpy");
-    (void)hipFree(b.dev);
+    set_error(e, "device_blob: upload");
+    (void)hipFreeAsync(b->dev, us);
     return nullptr;
   }
-  std::vector<Blob>& bucket = g_blobs[key];
-  bucket.push_back(std::move(b));
-  g_blob_bytes += bytes;
-  return bucket.back().dev;
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  cache().map[key].push_back(b);
+  cache().bytes[dev] += bytes;
+  return hand_out(b);
 }
 
 size_t blob_cache_bytes() {
   std::lock_guard<std::mutex> lk(g_table_mu);
-  return g_blob_bytes;
+  size_t s = 0;
+  for (const auto& kv : cache().bytes) s += kv.second;
+  return s;
 }
 void set_blob_cache_limit(size_t bytes) {
-  std::lock_guard<std::mutex> lk(g_table_mu);
-  g_blob_limit = bytes;
-  blob_evict(0);
+  std::vector<BlobRef> victims;
+  {
+    std::lock_guard<std::mutex> lk(g_table_mu);
+    cache().limit = bytes;
+    std::vector<int> devs;
+    for (const auto& kv : cache().bytes) devs.push_back(kv.first);
+    for (int d : devs) {
+      std::vector<BlobRef> v = evict_locked(d, 0);
+      victims.insert(victims.end(), v.begin(), v.end());
+    }
+  }
+  release_blobs(victims);
+}
+
+BlobScope::BlobScope(hipStream_t st) : st_(st), base_(t_held.size()), dev_(cur_dev()) { ++t_scopes; }
+
+BlobScope::~BlobScope() {
+  --t_scopes;
+  if (t_held.size() <= base_) return;
+  // one event after everything this scope enqueued on st_, attached to every blob it held
+  EvRef ev;
+  {
+    hipEvent_t e = nullptr;
+    {
+      EvPool& p = ev_pool();
+      std::lock_guard<std::mutex> lk(p.mu);
+      auto& f = p.free[dev_];
+      if (!f.empty()) { e = f.back(); f.pop_back(); }
+    }
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != dev_) (void)hipSetDevice(dev_);
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    if (e && hipEventRecord(e, st_) == hipSuccess) {
+      ev = std::make_shared<Ev>();
+      ev->e = e;
+      ev->d = dev_;
+    } else if (e) {
+      (void)hipEventDestroy(e);
+    }
+    if (prev != dev_) (void)hipSetDevice(prev);
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_table_mu);
+    for (size_t i = base_; i < t_held.size(); ++i) {
+      Blob& b = *t_held[i];
+      prune_uses(b);
+      if (ev) b.uses.push_back(ev);
+      else b.unscoped = true;                // untracked use: release after a device sync
+      --b.holds;
+    }
+  }
+  t_held.resize(base_);
 }
 
 const uint16_t* device_perm(int n, const uint16_t* table, uint16_t len, int kind, bool* canonical, bool* ok) {
@@ -207,47 +368,51 @@ const uint16_t* device_perm(int n, const uint16_t* table, uint16_t len, int kind
   *canonical = true;
   if (!table) { return nullptr; }
   const int dev = cur_dev();
-  // the library's own tables are immutable: cache their verdict by address; any other
-  // table is re-derived from its current words on every call (O(len)) and a non-canonical
-  // permutation is uploaded through the content-keyed blob cache
+  // the library's own tables are immutable: cache their verdict (and permutation) by address;
+  // any other table is re-derived from its current words on every call (O(len)).  A
+  // non-canonical permutation is always resolved through the content-keyed blob cache.
   const bool lib = is_library_addr(table);
   auto key = std::make_tuple(dev, (const void*)table, len, kind, n);
+  std::vector<uint16_t> a;
+  bool canon = true, cached = false;
   if (lib) {
     std::lock_guard<std::mutex> lk(g_table_mu);
     auto it = g_perms.find(key);
     if (it != g_perms.end()) {
-      *canonical = it->second.second;
-      return (const uint16_t*)it->second.first;
+      canon = it->second.canon;
+      if (!canon) a = it->second.perm;
+      cached = true;
     }
   }
-  // apply the reference's sequential swaps (arm_bitreversal2.c:84-108) to an identity
-  // array of complex indices: a[pos] = pre-reversal index that ends up at pos.
-  const uint16_t* host = table;
-  std::vector<uint16_t> tmp;
-  if (is_device_ptr(table)) {
-    tmp.resize(len);
-    if (hipMemcpy(tmp.data(), table, len * sizeof(uint16_t), hipMemcpyDeviceToHost) != hipSuccess) { *ok = false; return nullptr; }
-    host = tmp.data();
-  }
-  std::vector<uint16_t> a(n);
-  for (int i = 0; i < n; ++i) a[i] = (uint16_t)i;
-  for (int i = 0; i + 1 < len; i += 2) {
-    const int x = host[i] >> 3, y = host[i + 1] >> 3;
-    if (x >= n || y >= n) { *ok = false; return nullptr; }
-    std::swap(a[x], a[y]);
-  }
-  bool canon = true;
-  for (int k = 0; k < n && canon; ++k) canon = a[k] == (kind == 0 ? f32_src(n, k) : fixed_src(n, k));
-  const void* d = nullptr;
-  if (!canon) {
-    d = device_blob(a.data(), n * sizeof(uint16_t));
-    if (!d) { *ok = false; return nullptr; }
-  }
-  if (lib) {
-    std::lock_guard<std::mutex> lk(g_table_mu);
-    g_perms[key] = {(void*)d, canon};
+  if (!cached) {
+    // apply the reference's sequential swaps (arm_bitreversal2.c:84-108) to an identity
+    // array of complex indices: a[pos] = pre-reversal index that ends up at pos.
+    const uint16_t* host = table;
+    std::vector<uint16_t> tmp;
+    if (is_device_ptr(table)) {
+      tmp.resize(len);
+      if (hipMemcpy(tmp.data(), table, len * sizeof(uint16_t), hipMemcpyDeviceToHost) != hipSuccess) { *ok = false; return nullptr; }
+      host = tmp.data();
+    }
+    a.resize(n);
+    for (int i = 0; i < n; ++i) a[i] = (uint16_t)i;
+    for (int i = 0; i + 1 < len; i += 2) {
+      const int x = host[i] >> 3, y = host[i + 1] >> 3;
+      if (x >= n || y >= n) { *ok = false; return nullptr; }
+      std::swap(a[x], a[y]);
+    }
+    for (int k = 0; k < n && canon; ++k) canon = a[k] == (kind == 0 ? f32_src(n, k) : fixed_src(n, k));
+    if (lib) {
+      std::lock_guard<std::mutex> lk(g_table_mu);
+      PermEntry& pe = g_perms[key];
+      pe.canon = canon;
+      if (!canon) pe.perm = a;
+    }
   }
   *canonical = canon;
+  if (canon) return nullptr;
+  const void* d = device_blob(a.data(), n * sizeof(uint16_t));
+  if (!d) { *ok = false; return nullptr; }
   return (const uint16_t*)d;
 }
 

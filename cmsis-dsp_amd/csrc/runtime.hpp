@@ -31,12 +31,31 @@ const void* device_table(const void* host, size_t bytes);
 // Device copy of a host byte blob, cached by CONTENT (hash + full compare): uploaded once
 // per distinct contents and device, immune to a caller reusing a buffer for new values.
 // Used for user-supplied tables and coefficients (FIR taps, MFCC filterbanks, ...).  The
-// cache is an LRU bounded in bytes (blob_cache_bytes / set_blob_cache_limit): a caller that
-// changes coefficients on every call cycles through it instead of growing it.  Returns
-// nullptr on failure.
+// cache is an LRU bounded in bytes per device (blob_cache_bytes / set_blob_cache_limit): a
+// caller that changes coefficients on every call cycles through it instead of growing it.
+// The returned pointer stays valid while the calling thread's innermost BlobScope lives and
+// until the work enqueued before that scope ended has completed.  Returns nullptr on failure.
 const void* device_blob(const void* host, size_t bytes);
 size_t blob_cache_bytes();
-void set_blob_cache_limit(size_t bytes);
+void set_blob_cache_limit(size_t bytes);   // per device
+
+// Pins every blob device_blob / device_table / device_perm hand out on this thread while the
+// scope lives (eviction skips held blobs), then records one event on `st` -- after the work the
+// call enqueued -- that the blobs' eventual release waits on (stream-ordered hipFreeAsync, no
+// device synchronize).  Declare one in every entry point that fetches tables, before the first
+// fetch, with the stream its launches go to; scopes nest (the innermost holds).
+class BlobScope {
+ public:
+  explicit BlobScope(hipStream_t st);
+  ~BlobScope();
+  BlobScope(const BlobScope&) = delete;
+  BlobScope& operator=(const BlobScope&) = delete;
+
+ private:
+  hipStream_t st_;
+  size_t base_;
+  int dev_;
+};
 
 // Device permutation implementing a bit-reversal swap table of a non-canonical instance.
 // *canonical is set when the table induces the reference's own permutation (then the

@@ -237,6 +237,49 @@ arm_status arm_cfft_q15_batch_multi(const arm_cfft_instance_q15 *S, uint32_t nsh
                                     q15_t *const *d_p1, const uint32_t *batch, uint8_t ifftFlag,
                                     uint8_t bitReverseFlag);
 
+/* Multi-GPU FIR (the batch is sliced by filter, so each filter's history stays on
+ * its device; per filter: arm_fir_f32.c:911-1280, arm_fir_q15.c:458-726, ...).  Shard s of
+ * `nshards` is batch[s] filters of blockSize samples on HIP device devices[s]: DEVICE pointers
+ * d_src[s] / d_dst[s] [batch[s]][blockSize] and d_hist[s] [batch[s]][numTaps-1] with the
+ * arm_fir_*_batch state contract.  S->pCoeffs: a host pointer (uploaded once per device), or a
+ * device pointer every shard's device can read.  Launch/validate/wait semantics as
+ * arm_cfft_f32_batch_multi. */
+arm_status arm_fir_f32_batch_multi(const arm_fir_instance_f32 *S, uint32_t nshards, const int *devices,
+                                   const float32_t *const *d_src, float32_t *const *d_dst, float32_t *const *d_hist,
+                                   uint32_t blockSize, const uint32_t *batch);
+arm_status arm_fir_q15_batch_multi(const arm_fir_instance_q15 *S, uint32_t nshards, const int *devices,
+                                   const q15_t *const *d_src, q15_t *const *d_dst, q15_t *const *d_hist,
+                                   uint32_t blockSize, const uint32_t *batch);
+arm_status arm_fir_fast_q15_batch_multi(const arm_fir_instance_q15 *S, uint32_t nshards, const int *devices,
+                                        const q15_t *const *d_src, q15_t *const *d_dst, q15_t *const *d_hist,
+                                        uint32_t blockSize, const uint32_t *batch);
+arm_status arm_fir_q31_batch_multi(const arm_fir_instance_q31 *S, uint32_t nshards, const int *devices,
+                                   const q31_t *const *d_src, q31_t *const *d_dst, q31_t *const *d_hist,
+                                   uint32_t blockSize, const uint32_t *batch);
+arm_status arm_fir_fast_q31_batch_multi(const arm_fir_instance_q31 *S, uint32_t nshards, const int *devices,
+                                        const q31_t *const *d_src, q31_t *const *d_dst, q31_t *const *d_hist,
+                                        uint32_t blockSize, const uint32_t *batch);
+arm_status arm_fir_q7_batch_multi(const arm_fir_instance_q7 *S, uint32_t nshards, const int *devices,
+                                  const q7_t *const *d_src, q7_t *const *d_dst, q7_t *const *d_hist,
+                                  uint32_t blockSize, const uint32_t *batch);
+
+/* Multi-GPU matrix multiply (per matrix: arm_mat_mult_f32.c:600-730 / _q15 / _q31): shard s is
+ * batch[s] contiguous matrices with the instances' shapes (their pData are not used) at DEVICE
+ * pointers d_a[s], d_b[s], d_c[s] on devices[s].  ARM_MATH_SIZE_MISMATCH on incompatible
+ * shapes; otherwise as arm_cfft_f32_batch_multi. */
+arm_status arm_mat_mult_f32_batch_multi(const arm_matrix_instance_f32 *pSrcA, const arm_matrix_instance_f32 *pSrcB,
+                                        arm_matrix_instance_f32 *pDst, uint32_t nshards, const int *devices,
+                                        const float32_t *const *d_a, const float32_t *const *d_b,
+                                        float32_t *const *d_c, const uint32_t *batch);
+arm_status arm_mat_mult_q15_batch_multi(const arm_matrix_instance_q15 *pSrcA, const arm_matrix_instance_q15 *pSrcB,
+                                        arm_matrix_instance_q15 *pDst, uint32_t nshards, const int *devices,
+                                        const q15_t *const *d_a, const q15_t *const *d_b, q15_t *const *d_c,
+                                        const uint32_t *batch);
+arm_status arm_mat_mult_q31_batch_multi(const arm_matrix_instance_q31 *pSrcA, const arm_matrix_instance_q31 *pSrcB,
+                                        arm_matrix_instance_q31 *pDst, uint32_t nshards, const int *devices,
+                                        const q31_t *const *d_a, const q31_t *const *d_b, q31_t *const *d_c,
+                                        const uint32_t *batch);
+
 /* Number of HIP devices visible to the process (0 when none). */
 int arm_mi355x_device_count(void);
 
@@ -247,8 +290,10 @@ const char *arm_mi355x_last_error_string(void);
 void arm_mi355x_clear_error(void);
 
 /* Device bytes held by the content-keyed cache of host tables / coefficients (all devices),
- * and its limit (default 256 MiB; lowering it evicts least-recently-used entries now, after
- * synchronizing the device they live on). */
+ * and its limit PER DEVICE (default 256 MiB).  Lowering it evicts least-recently-used entries
+ * now.  An entry in use by a call that is still being enqueued is never evicted, and an
+ * evicted entry's memory is released in stream order after the work that read it (an event
+ * recorded after each call's launches; no device synchronize, no lock held while waiting). */
 size_t arm_mi355x_table_cache_bytes(void);
 void arm_mi355x_set_table_cache_limit(size_t bytes);
 

@@ -23,6 +23,8 @@ void oracle_arm_fir_q31(const arm_fir_instance_q31 *S, const int32_t *pSrc, int3
 void oracle_arm_fir_fast_q31(const arm_fir_instance_q31 *S, const int32_t *pSrc, int32_t *pDst, uint32_t blockSize);
 arm_status oracle_arm_mat_mult_f32(const arm_matrix_instance_f32 *A, const arm_matrix_instance_f32 *B,
                                    arm_matrix_instance_f32 *C);
+arm_status oracle_mat_mult_f32_fmaf(const arm_matrix_instance_f32 *A, const arm_matrix_instance_f32 *B,
+                                    arm_matrix_instance_f32 *Cm);
 arm_status oracle_arm_mat_mult_q15(const arm_matrix_instance_q15 *A, const arm_matrix_instance_q15 *B,
                                    arm_matrix_instance_q15 *C, int16_t *pState);
 arm_status oracle_arm_mat_mult_q31(const arm_matrix_instance_q31 *A, const arm_matrix_instance_q31 *B,

@@ -12,8 +12,14 @@
  *   state        s = [history (numTaps-1) ; block]; afterwards the state holds
  *                [last numTaps-1 samples of s ; block] (:1242-1278).
  *   arm_mat_mult_f32  arm_mat_mult_f32.c:600-730: per element, k-ordered mul-then-add.
+ *   oracle_mat_mult_f32_fmaf: NOT a reference function -- the MI355X product's own stated
+ *                semantics for arm_mat_mult_f32 (v_mfma_f32_32x32x2_f32 accumulates as a
+ *                k-ordered fmaf chain from +0.0f, one rounding per term), used to pin the GPU
+ *                kernel bit for bit (tests/test_gpu_rfft_fir_mat.py); same k order as the
+ *                reference, one rounding fewer per term.
  * Pinned by tests/test_oracle.py against oracle/_ref bit for bit.
  */
+#include <math.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -129,6 +135,21 @@ arm_status oracle_arm_mat_mult_f32(const arm_matrix_instance_f32 *A, const arm_m
         const float prod = A->pData[i * K + k] * B->pData[k * N + j];
         acc = acc + prod;
       }
+      Cm->pData[i * N + j] = acc;
+    }
+  return ARM_MATH_SUCCESS;
+}
+
+/* C[i][j] = fmaf(A[i][K-1], B[K-1][j], ... fmaf(A[i][0], B[0][j], +0.0f)): k ascending, exact
+ * products, one rounding per term (libm fmaf is correctly rounded; no contraction elsewhere). */
+arm_status oracle_mat_mult_f32_fmaf(const arm_matrix_instance_f32 *A, const arm_matrix_instance_f32 *B,
+                                    arm_matrix_instance_f32 *Cm) {
+  const uint32_t M = A->numRows, K = A->numCols, N = B->numCols;
+  if (K != B->numRows || M != Cm->numRows || N != Cm->numCols) return ARM_MATH_SIZE_MISMATCH;
+  for (uint32_t i = 0; i < M; ++i)
+    for (uint32_t j = 0; j < N; ++j) {
+      float acc = 0.0f;
+      for (uint32_t k = 0; k < K; ++k) acc = fmaf(A->pData[i * K + k], B->pData[k * N + j], acc);
       Cm->pData[i * N + j] = acc;
     }
   return ARM_MATH_SUCCESS;

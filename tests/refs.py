@@ -280,6 +280,23 @@ class Host:
             st = self.fn(f"arm_mat_mult_{kind}")(C.byref(A), C.byref(B), C.byref(Cm))
         return st, c
 
+    def mat_mult_fmaf(self, a, b):
+        """oracle_mat_mult_f32_fmaf (restatement only): the product's stated k-ordered fmaf-chain
+        semantics for arm_mat_mult_f32 -> (status, C)."""
+        a = np.ascontiguousarray(a, dtype=np.float32)
+        b = np.ascontiguousarray(b, dtype=np.float32)
+        c = np.zeros((a.shape[0], b.shape[1]), dtype=np.float32)
+        A, B, Cm = (_abi.arm_matrix_instance_f32() for _ in range(3))
+        init = self.fn("arm_mat_init_f32")
+        init(C.byref(A), a.shape[0], a.shape[1], a.ctypes.data)
+        init(C.byref(B), b.shape[0], b.shape[1], b.ctypes.data)
+        init(C.byref(Cm), c.shape[0], c.shape[1], c.ctypes.data)
+        f = self.lib.oracle_mat_mult_f32_fmaf
+        f.restype = C.c_int
+        f.argtypes = [C.c_void_p] * 3
+        st = f(C.byref(A), C.byref(B), C.byref(Cm))
+        return st, c
+
     def mat_mult(self, a, b):
         a = np.ascontiguousarray(a, dtype=np.float32)
         b = np.ascontiguousarray(b, dtype=np.float32)

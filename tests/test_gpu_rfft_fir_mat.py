@@ -221,6 +221,72 @@ def _bf16(x):
     return torch.from_numpy(x).bfloat16().double().numpy()
 
 
+def _tf32(x):
+    """Round f32 to a 10-bit mantissa (TF32 / xf32 operands), nearest-even."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0xFFF + ((u >> 13) & 1)) & ~np.uint64(0x1FFF)
+    return u.astype(np.uint32).view(np.float32)
+
+
+def _rms_ok(got, exact, mag, k):
+    """Statistical f32 check: rms(|C - C64| / (|A||B|)) <= sqrt(K) 2^-24.  f32 summation (the
+    reference's mul-then-add and an fmaf chain alike) sits at 0.01-0.1 of it; TF32-rounded
+    operands at 5-400x (numpy simulation at K = 16 ... 1024), bf16 far above."""
+    r = np.abs(got - exact) / np.maximum(mag, 1e-300)
+    return float(np.sqrt(np.mean(r ** 2)) / (np.sqrt(k) * 2.0 ** -24))
+
+
+def _mat_inputs(rng, shape_a, shape_b, dist):
+    if dist == "uniform":
+        return rng.uniform(-1, 1, shape_a).astype(np.float32), rng.uniform(-1, 1, shape_b).astype(np.float32)
+    if dist == "subnormal":     # |a b| in [2^-134, 2^-132): every product subnormal, none zero
+        f = lambda sh: (rng.uniform(0.5, 1.0, sh) * rng.choice([-1.0, 1.0], sh) * 2.0 ** -66).astype(np.float32)
+        return f(shape_a), f(shape_b)
+    if dist == "mixed":         # exponents over 2^-20 .. 2^20, exact zeros and negative zeros
+        def f(sh):
+            v = rng.uniform(0.5, 1.0, sh) * rng.choice([-1.0, 1.0], sh) * 2.0 ** rng.integers(-20, 21, sh)
+            z = rng.uniform(0, 1, sh)
+            v[z < 0.1] = 0.0
+            v[(z >= 0.1) & (z < 0.2)] = -0.0
+            return v.astype(np.float32)
+        return f(shape_a), f(shape_b)
+    raise ValueError(dist)
+
+
+@pytest.mark.parametrize("m,k,n,batch,dist", [
+    (1, 1, 1, 1, "uniform"), (17, 33, 9, 1, "uniform"), (300, 130, 200, 2, "uniform"),
+    (64, 37, 96, 1, "uniform"), (128, 1000, 128, 1, "uniform"),          # K not a multiple of 16
+    (256, 256, 256, 2, "uniform"), (128, 16, 384, 2, "uniform"),         # whole tiles: the fast kernel
+    (384, 48, 128, 1, "subnormal"), (300, 130, 200, 1, "subnormal"),
+    (256, 64, 128, 1, "mixed"), (65, 77, 33, 1, "mixed")])
+def test_mat_mult_f32_fmaf_chain_bitexact(dsp, torch_gpu, oracle, m, k, n, batch, dist):
+    """The kernel's stated semantics pinned bit for bit: C = the k-ordered fmaf chain from +0.0f
+    (oracle_mat_mult_f32_fmaf; v_mfma_f32_32x32x2_f32, mat_mult_f32.hip:1-12), on both kernels,
+    with subnormal products and signed zeros.  Negative control: the same chain on TF32-rounded
+    operands differs from the kernel's words."""
+    torch = torch_gpu
+    rng = np.random.default_rng(m * 7 + k * 3 + n + len(dist))
+    a, b = _mat_inputs(rng, (batch, m, k), (batch, k, n), dist)
+    dc = torch.empty((batch, m, n), dtype=torch.float32, device="cuda")
+    dsp.mat_mult_batch(torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda(), dc)
+    got = dc.cpu().numpy()
+    for i in range(batch):
+        st, want = oracle.mat_mult_fmaf(a[i], b[i])
+        assert st == 0
+        assert got[i].tobytes() == want.tobytes(), f"item {i}: {np.sum(got[i].view(np.uint32) != want.view(np.uint32))} words differ"
+    if k >= 16 and dist != "subnormal":
+        _, tf = oracle.mat_mult_fmaf(_tf32(a[0]), _tf32(b[0]))
+        assert np.mean(tf.view(np.uint32) != got[0].view(np.uint32)) > 0.5
+
+
+def test_mat_mult_f32_dropin_fmaf_bitexact(dsp, torch_gpu, oracle):
+    """The host-pointer drop-in arm_mat_mult_f32 returns the same fmaf-chain words."""
+    rng = np.random.default_rng(99)
+    a, b = _mat_inputs(rng, (17, 33), (33, 9), "uniform")
+    st, got = dsp.arm_mat_mult_f32(a, b)
+    assert st == 0 and got.tobytes() == oracle.mat_mult_fmaf(a, b)[1].tobytes()
+
+
 @pytest.mark.parametrize("m,k,n,batch", [(256, 256, 256, 3), (300, 130, 200, 2), (1024, 1024, 1024, 1),
                                           (128, 16, 384, 2), (384, 48, 128, 1), (128, 1000, 128, 1)])
 def test_mat_mult_batch_elementwise(dsp, torch_gpu, ref, m, k, n, batch):
@@ -238,14 +304,18 @@ def test_mat_mult_batch_elementwise(dsp, torch_gpu, ref, m, k, n, batch):
     exact = np.einsum("bmk,bkn->bmn", a.astype(np.float64), b.astype(np.float64))
     bound = _elementwise_bound(a, b)
     assert np.all(np.abs(got - exact) <= bound)
+    mag = bound / (k * 2.0 ** -24)
+    assert _rms_ok(got, exact, mag, k) <= 1.0
     bf = np.einsum("bmk,bkn->bmn", _bf16(a), _bf16(b))     # negative control
     assert np.mean(np.abs(bf - exact) > bound) > 0.1
+    tf = np.einsum("bmk,bkn->bmn", _tf32(a).astype(np.float64), _tf32(b).astype(np.float64))
+    assert _rms_ok(tf, exact, mag, k) > 2.0                 # TF32-class operands are rejected
     if m * k * n <= 256 ** 3:   # the reference itself on one item (seconds on the host)
         st, want = ref.mat_mult(a[0], b[0])
         assert np.all(np.abs(got[0] - want) <= 2 * bound[0])
 
 
-def test_mat_mult_1024_vs_reference_slice(dsp, torch_gpu, ref):
+def test_mat_mult_1024_vs_reference_slice(dsp, torch_gpu, ref, oracle):
     """BASELINE configs[4] shape (1024^3): a 16-row slice of A times all of B through the
     reference's own arm_mat_mult_f32 (full K), held per element to 2 K 2^-24 (|A||B|)ij;
     the whole product per element to K 2^-24 (|A||B|)ij vs float64; and the bf16 negative
@@ -264,8 +334,14 @@ def test_mat_mult_1024_vs_reference_slice(dsp, torch_gpu, ref):
     st, want = ref.mat_mult(a[:16], b)
     assert st == 0
     assert np.all(np.abs(got[:16] - want) <= 2 * bound[:16])
+    mag = bound / (1024 * 2.0 ** -24)
+    assert _rms_ok(got, exact, mag, 1024) <= 1.0
     bf = (torch.from_numpy(_bf16(a)) @ torch.from_numpy(_bf16(b))).numpy()
     assert np.mean(np.abs(bf - exact) > bound) > 0.1
+    tf = (torch.from_numpy(_tf32(a)).double() @ torch.from_numpy(_tf32(b)).double()).numpy()
+    assert _rms_ok(tf, exact, mag, 1024) > 2.0
+    st, fm = oracle.mat_mult_fmaf(a[:16], b)              # the stated semantics, bit for bit
+    assert st == 0 and dc[0, :16].cpu().numpy().tobytes() == fm.tobytes()
 
 
 # ------------------------------------------------------------------ mat mult q15 / q31

@@ -319,3 +319,146 @@ def test_dropin_fir_zero_copy_short_blocks(dsp, torch_gpu, ref, taps, block):
     for b, w in zip(blocks, want):
         assert f(b).tobytes() == w.tobytes()
     assert f.state.tobytes() == state.tobytes()
+
+
+# ------------------------------------------------------------------ multi-GPU FIR / mat_mult
+@pytest.mark.parametrize("kind", ["f32", "q15", "fast_q15", "q31", "fast_q31", "q7"])
+def test_fir_batch_multi_bitexact(dsp, torch_gpu, ref, kind):
+    """arm_fir_*_batch_multi: filters sharded with their history rows over every visible device
+    (two ragged shards per device), two calls with state carry, host coefficients (uploaded per
+    device): every filter equals the reference's stream."""
+    torch = torch_gpu
+    base = kind.split("_")[-1]
+    ndev = dsp.device_count()
+    taps, block = (64 if base == "q15" else 37), 777
+    c = refs.rand_input(base, taps, seed=5)
+    counts = [3 + 2 * s for s in range(2 * ndev)]
+    devs = [s % ndev for s in range(2 * ndev)]
+    blocks = [[[refs.rand_input(base, block, seed=1000 * s + 10 * f + k) for k in range(2)] for f in range(cnt)]
+              for s, cnt in enumerate(counts)]
+    S = {"f32": dsp.arm_fir_instance_f32, "q15": dsp.arm_fir_instance_q15, "q31": dsp.arm_fir_instance_q31,
+         "q7": dsp.arm_fir_instance_q7}[base]()
+    S.numTaps = taps
+    S.pCoeffs = C.cast(c.ctypes.data, S._fields_[2][1])
+    dt = {"f32": torch.float32, "q15": torch.int16, "q31": torch.int32, "q7": torch.int8}[base]
+    hists = [torch.zeros((cnt, taps - 1), dtype=dt, device=f"cuda:{d}") for cnt, d in zip(counts, devs)]
+    for k in range(2):
+        shards = []
+        for s, (cnt, d) in enumerate(zip(counts, devs)):
+            src = torch.from_numpy(np.stack([blocks[s][f][k] for f in range(cnt)])).to(f"cuda:{d}")
+            shards.append((src, torch.empty_like(src), hists[s]))
+        dsp.fir_batch_multi(S, shards, kind=kind)
+        for s, (src, dst, _) in enumerate(shards):
+            got = dst.cpu().numpy()
+            for f in range(counts[s]):
+                want, _ = ref.fir(kind, c, blocks[s][f][:k + 1])
+                assert got[f].tobytes() == want[k].tobytes(), (s, f, k)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "q15", "q31"])
+def test_mat_mult_batch_multi_bitexact(dsp, torch_gpu, ref, oracle, dtype):
+    """arm_mat_mult_*_batch_multi over every visible device: f32 equals the fmaf-chain
+    restatement bit for bit, q15 / q31 the reference."""
+    torch = torch_gpu
+    ndev = dsp.device_count()
+    m, k, n = 65, 70, 33
+    counts = [2 + s for s in range(2 * ndev)]
+    devs = [s % ndev for s in range(2 * ndev)]
+    rng = np.random.default_rng(7)
+    shards, host = [], []
+    for cnt, d in zip(counts, devs):
+        if dtype == "f32":
+            a = rng.uniform(-1, 1, (cnt, m, k)).astype(np.float32)
+            b = rng.uniform(-1, 1, (cnt, k, n)).astype(np.float32)
+        else:
+            bits, npdt = (15, np.int16) if dtype == "q15" else (31, np.int32)
+            a = rng.integers(-(1 << bits), 1 << bits, (cnt, m, k)).astype(npdt)
+            b = rng.integers(-(1 << bits), 1 << bits, (cnt, k, n)).astype(npdt)
+        ta, tb = torch.from_numpy(a).to(f"cuda:{d}"), torch.from_numpy(b).to(f"cuda:{d}")
+        tc = torch.empty((cnt, m, n), dtype=ta.dtype, device=f"cuda:{d}")
+        shards.append((ta, tb, tc))
+        host.append((a, b))
+    dsp.mat_mult_batch_multi(shards)
+    for (a, b), (_, _, tc) in zip(host, shards):
+        got = tc.cpu().numpy()
+        for i in range(a.shape[0]):
+            want = oracle.mat_mult_fmaf(a[i], b[i])[1] if dtype == "f32" else ref.mat_mult_fixed(dtype, a[i], b[i])[1]
+            assert got[i].tobytes() == want.tobytes(), i
+
+
+# ------------------------------------------------------------------ cache eviction under load
+def test_table_cache_eviction_two_threads(dsp, torch_gpu, ref):
+    """two host threads with a 64 KiB table-cache limit.  Each calls the
+    drop-in arm_cfft_f32 with a custom bit-reversal table AND user twiddles that change every
+    call (two content-cached blobs per call, which must not evict each other), and queues
+    arm_fir_f32_batch with fresh host coefficients per call on its own stream without waiting
+    (evicted coefficient sets may still be read by queued kernels: they must be released only
+    after them).  Every result is bit-exact."""
+    torch = torch_gpu
+    n, taps, block, batch, iters = 64, 256, 512, 2, 120
+    base_tw = np.ctypeslib.as_array(C.cast(dsp.const_instance("arm_cfft_sR_f32_len64").pTwiddle,
+                                           C.POINTER(C.c_float)), (2 * n,)).copy()
+    tab = np.array([8 * 3, 8 * 7, 8 * 4, 8 * 60, 8 * 1, 8 * 5], dtype=np.uint16)
+    errors = []
+    results = [dict() for _ in range(2)]
+    dsp.set_table_cache_limit(64 << 10)
+    try:
+        def worker(t):
+            try:
+                torch.cuda.set_device(0)
+                rng = np.random.default_rng(100 + t)
+                st = torch.cuda.Stream()
+                xs = rng.uniform(-1, 1, (batch, block)).astype(np.float32)
+                fir_in = torch.from_numpy(xs).cuda()
+                outs, cs, fft = [], [], []
+                keep = []
+                with torch.cuda.stream(st):
+                    for i in range(iters):
+                        tw = (base_tw * rng.uniform(0.5, 1.5, 2 * n)).astype(np.float32)   # new contents
+                        x = rng.uniform(-1, 1, 2 * n).astype(np.float32)
+                        S = dsp.arm_cfft_instance_f32()
+                        dsp.arm_cfft_init_f32(S, n)
+                        S.pTwiddle = tw.ctypes.data_as(C.POINTER(C.c_float))
+                        S.pBitRevTable = tab.ctypes.data_as(C.POINTER(C.c_uint16))
+                        S.bitRevLength = len(tab)
+                        fft.append((tw, x, dsp.arm_cfft_f32(S, x, i & 1, 1)))
+                        c = rng.standard_normal(taps).astype(np.float32)
+                        fir = dsp.arm_fir_instance_f32()
+                        fir.numTaps = taps
+                        fir.pCoeffs = c.ctypes.data_as(C.POINTER(C.c_float))
+                        dst = torch.empty_like(fir_in)
+                        hist = torch.zeros((batch, taps - 1), device="cuda")
+                        dsp.fir_batch(fir, fir_in, dst, hist, stream=st)   # no wait
+                        outs.append(dst)
+                        cs.append(c)
+                        keep.append(hist)
+                    st.synchronize()
+                results[t] = {"fft": fft, "fir": [(c, o.cpu().numpy()) for c, o in zip(cs, outs)], "x": xs}
+            except Exception as e:   # noqa: BLE001 - reported below
+                errors.append(repr(e))
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=300)
+        assert not errors, errors
+        assert dsp.table_cache_bytes() <= 64 << 10
+    finally:
+        dsp.set_table_cache_limit(256 << 20)
+    for t in range(2):
+        for i, (tw, x, got) in enumerate(results[t]["fft"]):
+            Sr = ref.cfft_instance("f32", n)
+            Sr.pTwiddle = tw.ctypes.data_as(C.POINTER(C.c_float))
+            Sr.pBitRevTable = tab.ctypes.data_as(C.POINTER(C.c_uint16))
+            Sr.bitRevLength = len(tab)
+            buf = x.copy()
+            ref.fn("arm_cfft_f32")(C.byref(Sr), buf.ctypes.data, i & 1, 1)
+            assert np.asarray(got).tobytes() == buf.tobytes(), (t, i)
+        xs = results[t]["x"]
+        for i, (c, got) in enumerate(results[t]["fir"]):
+            if i % 7 and i != len(results[t]["fir"]) - 1:
+                continue                              # every 7th set and the last against the reference
+            for f in range(batch):
+                want, _ = ref.fir("f32", c, [xs[f]])
+                assert got[f].tobytes() == want[0].tobytes(), (t, i, f)

@@ -101,6 +101,44 @@ def test_mat_mult_oracle_equals_reference(oracle, ref, m, k, n):
     assert sa == sb == 0 and ca.tobytes() == cb.tobytes()
 
 
+def _fma_f32_exact(a, b, c):
+    """round-to-nearest-even f32 of the exact a*b + c (Fractions; no double rounding)."""
+    from fractions import Fraction
+    s = Fraction(float(a)) * Fraction(float(b)) + Fraction(float(c))
+    f = np.float32(float(s))
+    cands = [np.nextafter(f, np.float32(-np.inf)), f, np.nextafter(f, np.float32(np.inf))]
+    best = min(cands, key=lambda v: (abs(Fraction(float(v)) - s), int(np.float32(v).view(np.uint32)) & 1))
+    if s == 0:       # IEEE 754 RN: -0 only when a*b and c are both -0
+        ab = float(a) * float(b)
+        both_neg = ab == 0 and float(c) == 0 and np.signbit(ab) and np.signbit(c)
+        return np.float32(-0.0) if both_neg else np.float32(0.0)
+    return np.float32(best)
+
+
+@pytest.mark.parametrize("m,k,n,scale", [(3, 5, 4, 1.0), (4, 17, 3, 1.0), (3, 9, 3, 2.0 ** -66), (2, 33, 2, 1e3)])
+def test_mat_mult_fmaf_oracle_is_an_exact_fma_chain(oracle, ref, m, k, n, scale):
+    """oracle_mat_mult_f32_fmaf (the GPU kernel's stated semantics, v_mfma_f32_32x32x2_f32)
+    equals a k-ordered chain of correctly rounded fused multiply-adds computed with exact
+    rationals -- including subnormal products (scale 2^-66: |a b| < 2^-126) -- and stays within
+    the f32 summation bound of the reference's own mul-then-add arm_mat_mult_f32."""
+    rng = np.random.default_rng(m * 100 + k)
+    a = (rng.uniform(-1, 1, (m, k)) * scale).astype(np.float32)
+    b = (rng.uniform(-1, 1, (k, n)) * scale).astype(np.float32)
+    st, got = oracle.mat_mult_fmaf(a, b)
+    assert st == 0
+    want = np.zeros((m, n), dtype=np.float32)
+    for i in range(m):
+        for j in range(n):
+            acc = np.float32(0.0)
+            for kk in range(k):
+                acc = _fma_f32_exact(a[i, kk], b[kk, j], acc)
+            want[i, j] = acc
+    assert got.tobytes() == want.tobytes()
+    _, r = ref.mat_mult(a, b)
+    mag = np.abs(a).astype(np.float64) @ np.abs(b).astype(np.float64)
+    assert np.all(np.abs(got.astype(np.float64) - r) <= 2 * k * 2.0 ** -24 * mag + 2.0 ** -149 * k)
+
+
 @pytest.mark.parametrize("kind", ["q15", "q31"])
 @pytest.mark.parametrize("m,k,n,fill", [(1, 1, 1, None), (7, 13, 5, None), (33, 70, 17, None), (8, 64, 9, "min"),
                                         (8, 64, 9, "max")])
