@@ -542,8 +542,17 @@ def main_rank(args):
         fresh = synth("f32", 64 * n, salt=29).view(64, n)
         want = host.mfcc(cfg, fresh.cpu().numpy())
         got = m.batch(fresh.clone()).cpu().numpy()
+        err = float(np.nanmax(np.abs(got.astype(np.float64) - want)))
+        try:
+            libm_ok, libm_bad, glibc = mfcc_cfg.host_libm_status()
+        except OSError:
+            libm_ok, libm_bad, glibc = None, None, None
         return wall, kern_ms, {"checker": hk, "frames_checked": 64, "bit_exact": got.tobytes() == want.tobytes(),
-                               "logf": "host glibc logf restated on the device (host_logf.hpp)"}
+                               "max_abs_err": err,
+                               "within_suite_tolerance": bool(np.all(np.abs(got - want) <= 1e-5 + 1.2e-3 * np.abs(want))),
+                               "logf": "host glibc logf restated on the device (host_logf.hpp)",
+                               "host_libm": glibc, "host_logf_equals_restated": libm_ok,
+                               "host_logf_sampled_mismatches": libm_bad}
 
     def run_mfcc_fixed(t, n, batch, steps, warmup):
         """arm_mfcc_q31 / _q15 (pre + RFFT + post) on the suite's 1024 tables over full-range

@@ -43,3 +43,47 @@ def make_cfg(n, nb_mel=20, nb_dct=13, fs=16000.0, fmin=64.0):
     return {"fftLen": n, "dct": dct.astype(np.float32), "pos": np.array(pos, np.uint32),
             "len": np.array(lens, np.uint32), "coefs": np.concatenate(coefs).astype(np.float32),
             "window": win.astype(np.float32)}
+
+
+_LIBM = {}
+
+
+def host_libm_status(stride=4099):
+    """(matches, mismatches, glibc): does the host libm logf -- the one libm call of the
+    reference's MFCC f32 (arm_vlog_f32.c:110) -- equal the device restatement of glibc 2.35's
+    __logf_fma (csrc/host_logf.hpp) on a strided sample of all 2^32 inputs (~1M values)?  When
+    it does not, bit-exactness against the reference build is not assessable on this host
+    (oracle/src/logf_probe.cpp; tools/logf_check.cpp is the exhaustive form)."""
+    if "s" not in _LIBM:
+        import ctypes as C
+        so = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_build",
+                          "liblogfprobe.so")
+        lib = C.CDLL(so)
+        lib.logf_probe_mismatches.restype = C.c_uint64
+        lib.logf_probe_mismatches.argtypes = [C.c_uint32, C.c_uint32]
+        bad = int(lib.logf_probe_mismatches(stride, 17))
+        try:
+            glibc = os.confstr("CS_GNU_LIBC_VERSION")
+        except (ValueError, OSError):
+            glibc = None
+        _LIBM["s"] = (bad == 0, bad, glibc)
+    return _LIBM["s"]
+
+
+def assert_parity(got, want, suite_tolerance=True):
+    """MFCC f32 parity against the reference build's words: bit-exact when the host libm logf
+    is the restated one; otherwise the reference suite's tolerance (MFCCF32.cpp:7-13:
+    |err| <= 1e-5 + 1.2e-3 |ref|) is asserted and the test is SKIPPED as "libm differs" --
+    a different libm, not a parity failure."""
+    import pytest
+    g = np.ascontiguousarray(got, np.float32)
+    w = np.ascontiguousarray(want, np.float32)
+    same = g.view(np.uint32) == w.view(np.uint32)
+    ok, bad, glibc = host_libm_status()
+    if ok:
+        assert same.all(), (np.argwhere(~same)[:5], float(np.nanmax(np.abs(g - w))))
+        return
+    if suite_tolerance:
+        assert np.all(np.abs(g - w) <= 1e-5 + 1.2e-3 * np.abs(w)), float(np.nanmax(np.abs(g - w)))
+    pytest.skip(f"host libm differs ({glibc}: logf != restated glibc 2.35 __logf_fma on {bad} sampled inputs); "
+                "suite tolerance checked, bit-exactness not assessable on this host")

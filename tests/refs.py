@@ -17,7 +17,8 @@ from cmsisdsp_amd import _abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libcmsisdsp_ref.so")
-ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+# CMSISDSP_ORACLE_SO overrides the restatement (tools/oracle_san.sh: the ASan/UBSan build)
+ORACLE_SO = os.environ.get("CMSISDSP_ORACLE_SO") or os.path.join(ROOT, "oracle", "_build", "liboracle.so")
 
 _INST = {"f32": _abi.arm_cfft_instance_f32, "q31": _abi.arm_cfft_instance_q31, "q15": _abi.arm_cfft_instance_q15}
 DTYPE = {"f32": np.float32, "q31": np.int32, "q15": np.int16, "q7": np.int8}

@@ -1,4 +1,4 @@
-"""Fit the headline kernel's time per launch against batch (tools/gpu_r3_d.sh output):
+"""Fit the headline kernel's time per launch against batch (a batch sweep of bench.py --batch lines):
 t(batch) = t0 + batch / R by least squares over the launch_b<k>.json bench lines.
 Usage: python tools/launch_fit.py gpurun_out/r3d [out.json]"""
 import glob
