@@ -8,6 +8,7 @@
 // Usage: dropin_latency <product.so> <reference.so> [calls]   -> one JSON line on stdout.
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
