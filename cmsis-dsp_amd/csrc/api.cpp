@@ -70,7 +70,7 @@ void cfft_sync(const Inst* S, void* p1, uint8_t ifftFlag, uint8_t bitReverseFlag
   const size_t bytes = 2 * word * n;
   if (is_device_ptr(p1)) {
     hipError_t e = cfft_launch(kind, n, p1, 1, pr, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = wait_stream(st);
     if (e != hipSuccess) set_error(e, "arm_cfft");
     return;
   }
@@ -437,13 +437,14 @@ bool mfcc_fx_prepare(const Inst* S, MfccFxDev<T>& d) {
 
 // x: [batch][n] frames (overwritten), y: [batch][2n] spectra, dst: [batch][nbDct]; the frame
 // maxima ride in dst[frame][0] between the launches (read before the row is written)
-// MFCC q31 / q15 schedule: 1 = two launches (the MFCC front end fused into the radix-16 CFFT's
-// load phase, fftLen 512..4096 with the reference's own CFFT bit reversal, then post), 0 = three
-// launches (pre, CFFT, post: other lengths and custom bit-reversal tables).  A one-launch kernel
-// (frames resident in LDS through pre, CFFT and post) was measured slower than both and removed
-// (DESIGN.md §4 mfcc_q31 / mfcc_q15).
+// MFCC q31 / q15 schedule (fftLen 512..4096 with the reference's own CFFT bit reversal):
+// 2 = one launch (round 4: front end, radix-16 CFFT and back end in one kernel, the spectra
+// never leave LDS), 1 = two launches (front end fused into the CFFT's load phase, then the post
+// kernel), 0 = three launches (pre, CFFT, post: also every other length and custom bit-reversal
+// tables).  The round-3 one-launch kernel (generic LDS-stage CFFT, frames resident in LDS) was
+// slower than the two-launch schedule and was removed (DESIGN.md §4 mfcc_q31 / mfcc_q15).
 #ifndef MI355X_MFCC_FX_MODE
-#define MI355X_MFCC_FX_MODE 1
+#define MI355X_MFCC_FX_MODE 2
 #endif
 template <typename T, typename Inst>
 bool mfcc_fx_run(const Inst* S, const MfccFxDev<T>& d, T* x, T* y, T* dst, uint32_t batch, hipStream_t st) {
@@ -458,6 +459,19 @@ bool mfcc_fx_run(const Inst* S, const MfccFxDev<T>& d, T* x, T* y, T* dst, uint3
   if (!cfft_prepare(L, in->pTwiddle, in->pBitRevTable, in->bitRevLength, sizeof(T) == 4 ? 1 : 2, 0,
                     S->rfft.bitReverseFlagR, pr))
     return false;
+  if (MI355X_MFCC_FX_MODE >= 2 && !pr.perm) {    // the whole MFCC in one launch
+    hipError_t e;
+    if constexpr (sizeof(T) == 4)
+      e = mfcc_q31_fused_launch((int)L, x, batch, (const int32_t*)pr.tw, d.win, S->rfft.bitReverseFlagR != 0, d.tw,
+                                nm, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst, st);
+    else
+      e = mfcc_q15_fused_launch((int)L, x, batch, (const int16_t*)pr.tw, d.win, S->rfft.bitReverseFlagR != 0, d.tw,
+                                nm, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst, st);
+    if (e != hipErrorNotSupported) {
+      MI_CHECK(e, "mfcc fused");
+      return true;
+    }
+  }
   bool front = false;                       // pre + CFFT done by one launch
   if (MI355X_MFCC_FX_MODE >= 1 && !pr.perm) {
     if constexpr (sizeof(T) == 4)

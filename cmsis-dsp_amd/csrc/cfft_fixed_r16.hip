@@ -23,10 +23,13 @@
 //     dropped, so a partial last group needs no bounds code), nontemporal; workgroup b takes
 //     the MI355X_FXR_T consecutive groups, the next group's words prefetched into registers
 //     under passes 2+, the loop entered after the first pass (see cfft_fx4096_kernel).
+#include <type_traits>
+
 #include "common.hpp"
 #include "kernels.hpp"
 #include "cfft_fixed_core.hpp"
 #include "mfcc_fixed_ops.hpp"
+#include "mfcc_fixed_post.hpp"
 
 namespace mi355x {
 
@@ -138,12 +141,28 @@ template <bool INV> struct R16Ops<int16_t, INV> {
 // max sat|x| (lane shuffles; an LDS pair for P = 128), scale and window their 32 words in
 // registers (MqPre) before the first pass, and lane 0 leaves m in maxv[frame * mstride] for the
 // post kernel -- the separate pre pass (one read and one write of every frame) disappears.
-template <typename T, int N, bool INV, bool BREV, bool SAT, bool PRE = false>
+// POST (round 4): the whole MFCC in this kernel.  The last pass leaves the
+// group's spectra in the LDS image (the CFFT's storage order, unpadded) instead of HBM, and the
+// four waves then run the MFCC back end on them (mfcc_fixed_post.hpp: split + magnitudes, Mel
+// sums, the grouped finish and DCT rows) while the next group's frames are already in flight;
+// only the DCT outputs are written.  Traffic per frame: the frame once + nbDct words.
+template <typename T> struct MqPostArgs {
+  const int4* tw = nullptr;        // split twiddle records per bin (MfccFxDev::tw)
+  const T* coefs = nullptr;
+  const uint32_t* bf = nullptr;    // flat Mel list
+  const T* dct = nullptr;
+  const int32_t* lut = nullptr;    // sqrt_initial_lut_q31
+  T* dst = nullptr;                // [batch][nb_dct]
+  int nb_mel = 0, total = 0, nb_dct = 0, stage = 0;
+};
+template <typename T, int N, bool INV, bool BREV, bool SAT, bool PRE = false, bool POST = false>
 __global__ __launch_bounds__(kBlock) void cfft_fx_r16_kernel(typename R16Ops<T, INV>::C* __restrict__ data,
                                                              uint32_t batch,
                                                              const typename R16Ops<T, INV>::C* __restrict__ tw,
                                                              const typename R16Ops<T, INV>::C* __restrict__ win = nullptr,
-                                                             T* __restrict__ maxv = nullptr, int mstride = 0) {
+                                                             T* __restrict__ maxv = nullptr, int mstride = 0,
+                                                             MqPostArgs<T> pa = {}) {
+  static_assert(!POST || (PRE && !INV && !SAT), "the fused MFCC runs the forward front end");
   using R = R16<N>;
   using O = R16Ops<T, INV>;
   using V = typename O::V;
@@ -206,6 +225,20 @@ __global__ __launch_bounds__(kBlock) void cfft_fx_r16_kernel(typename R16Ops<T, 
   const uint32_t g0 = blockIdx.x * MI355X_FXR_T;
   const uint32_t gend = min(ngroups, g0 + MI355X_FXR_T);
   if (g0 >= gend) return;
+  // POST: the back end's tables (LDS when they fit) and each wave's work area
+  using PostOps = typename std::conditional<sizeof(T) == 4, MqOpsQ31, MqOpsQ15>::type;
+  constexpr int kFrameLen = 2 * N;                    // the MFCC frame: fftLen real samples
+  extern __shared__ int32_t shq[];
+  MqTabs tb{};
+  int32_t *mag = nullptr, *mel = nullptr, *mv = nullptr;
+  int64_t* acc = nullptr;
+  if constexpr (POST) {
+    tb = mq_stage_tables<T>(shq, pa.coefs, pa.bf, pa.total, pa.nb_mel, pa.nb_dct, pa.dct, pa.stage);
+    mag = shq + (pa.stage ? mq_tab_words(pa.total, pa.nb_mel, pa.nb_dct) : 0) + (t >> 6) * mq_wave_words(kFrameLen, pa.nb_mel);
+    mel = mag + mq_mel_off(kFrameLen, pa.nb_mel);
+    mv = mag + mq_m_off(kFrameLen, pa.nb_mel);
+    acc = reinterpret_cast<int64_t*>(mag + mq_acc_off(kFrameLen, pa.nb_mel));
+  }
   auto group_rsrc = [&](uint32_t g) {
     const uint32_t first = g * R::TPW;
     const uint32_t valid = min((uint32_t)R::TPW, batch - first);
@@ -220,6 +253,7 @@ __global__ __launch_bounds__(kBlock) void cfft_fx_r16_kernel(typename R16Ops<T, 
   };
   V v[16];
   __shared__ int32_t red[PRE && P > 64 ? 2 * R::TPW : 1];
+  __shared__ int32_t mvals[POST ? R::TPW : 1];        // POST: the group's frame maxima
   // first pass from nq, then the next group's loads (they fly under the later passes)
   auto pass0 = [&](uint32_t g) {
 #pragma unroll
@@ -250,7 +284,11 @@ __global__ __launch_bounds__(kBlock) void cfft_fx_r16_kernel(typename R16Ops<T, 
         v[u] = O::pack(Pre::pre(z.x, (int32_t)wv.x, scale, quot, k), Pre::pre(z.y, (int32_t)wv.y, scale, quot, k));
       }
       const uint32_t f = g * R::TPW + (uint32_t)w;
-      if (tp == 0 && f < batch) maxv[(size_t)f * mstride] = (T)m;
+      if constexpr (POST) {
+        if (tp == 0) mvals[w] = m;
+      } else {
+        if (tp == 0 && f < batch) maxv[(size_t)f * mstride] = (T)m;
+      }
     }
     if constexpr (R::BY2) {
 #pragma unroll
@@ -346,12 +384,43 @@ __global__ __launch_bounds__(kBlock) void cfft_fx_r16_kernel(typename R16Ops<T, 
         O::template bf<2>(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3], z, z, z);
       }
     }
+    if constexpr (POST) {
+      __syncthreads();                                // every thread is done reading the image
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        if constexpr (R::BY2) v[u] = O::by2_post(v[u]);
+        lds[BREV ? tp + bin[u] : epos[u]] = O::to_w(v[u]);   // storage order, unpadded
+      }
+      __syncthreads();
+      // the back end: wave wv takes the group's transforms wv, wv + 4, ... in chunks of G
+      const PostOps op(kFrameLen, pa.nb_mel, pa.nb_dct);
+      const int wv = t >> 6, lane = t & 63;
+      const int32_t lutv = pa.lut[lane & 31];
+      const int G = mq_group(pa.nb_mel);
+      auto dctw = [&](int i) { return tb.stage ? tb.dc[i] : (int32_t)pa.dct[i]; };
+      const uint32_t fbase = g * R::TPW;
+      for (int s0 = wv; s0 < R::TPW; s0 += 4 * G) {
+        int gn = 0;
+        for (int s = s0; s < R::TPW && s < s0 + 4 * G && fbase + s < batch; s += 4, ++gn) {
+          const W* img = lds_all + s * PD::stride;
+          auto get = [img](int i) { return O::unpack(O::from_w(img[i])); };
+          if (lane == 0) mv[gn] = mvals[s];
+          mq_mel_frame<T>(op, get, pa.tw, kFrameLen, pa.nb_mel, pa.total, tb, pa.coefs, lutv, mag,
+                          acc + gn * pa.nb_mel);
+        }
+        if (gn == 0) break;
+        mq_finish_group(op, gn, pa.nb_mel, pa.nb_dct, acc, mv, mel, dctw, [&](int j, int r, int32_t val) {
+          pa.dst[(size_t)(fbase + s0 + 4 * j) * pa.nb_dct + r] = (T)val;
+        });
+      }
+    } else {
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       if constexpr (R::BY2) v[u] = O::by2_post(v[u]);   // radix4by2 post-pass <<1
       if constexpr (SAT) v[u] = O::sat(v[u]);
       if constexpr (BREV) O::st(rx, vin, bin[u] * kC, v[u]);
       else O::st(rx, (w * N + epos[u]) * kC, 0, v[u]);
+    }
     }
     if (++g >= gend) return;
     pass0(g);
@@ -364,7 +433,7 @@ static void launch_r16_t(void* data, uint32_t batch, const void* tw, hipStream_t
   const uint32_t ngroups = (batch + R16<N>::TPW - 1) / R16<N>::TPW;
   const uint32_t grid = (ngroups + MI355X_FXR_T - 1) / MI355X_FXR_T;
   hipLaunchKernelGGL((cfft_fx_r16_kernel<T, N, INV, BREV, SAT>), dim3(grid), dim3(kBlock), 0, st, (C*)data, batch,
-                     (const C*)tw);
+                     (const C*)tw, (const C*)nullptr, (T*)nullptr, 0, MqPostArgs<T>{});
 }
 
 template <typename T, int N>
@@ -386,7 +455,65 @@ static void launch_r16_mfcc(void* data, uint32_t batch, const void* tw, const vo
   const uint32_t ngroups = (batch + R16<N>::TPW - 1) / R16<N>::TPW;
   const uint32_t grid = (ngroups + MI355X_FXR_T - 1) / MI355X_FXR_T;
   auto k = brev ? cfft_fx_r16_kernel<T, N, false, true, false, true> : cfft_fx_r16_kernel<T, N, false, false, false, true>;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, st, (C*)data, batch, (const C*)tw, (const C*)win, maxv, mstride);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, st, (C*)data, batch, (const C*)tw, (const C*)win, maxv, mstride,
+                     MqPostArgs<T>{});
+}
+
+template <typename T, int N>
+static hipError_t launch_r16_mfcc_fused(const void* data, uint32_t batch, const void* tw, const void* win, bool brev,
+                                        const MqPostArgs<T>& pa0, hipStream_t st) {
+  using C = typename R16Ops<T, false>::C;
+  MqPostArgs<T> pa = pa0;
+  const size_t tab = sizeof(int32_t) * (size_t)mq_tab_words(pa.total, pa.nb_mel, pa.nb_dct);
+  const size_t waves = sizeof(int32_t) * 4 * (size_t)mq_wave_words(2 * N, pa.nb_mel);
+  pa.stage = waves + tab <= 32768 ? 1 : 0;
+  const size_t lds = waves + (pa.stage ? tab : 0);
+  auto k = brev ? cfft_fx_r16_kernel<T, N, false, true, false, true, true>
+                : cfft_fx_r16_kernel<T, N, false, false, false, true, true>;
+  if (lds > 65536) {
+    if (lds > 100 * 1024) return hipErrorInvalidValue;
+    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  const uint32_t ngroups = (batch + R16<N>::TPW - 1) / R16<N>::TPW;
+  const uint32_t grid = (ngroups + MI355X_FXR_T - 1) / MI355X_FXR_T;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), lds, st, (C*)data, batch, (const C*)tw, (const C*)win, (T*)nullptr,
+                     0, pa);
+  return hipGetLastError();
+}
+
+// The whole MFCC q31 / q15 of fftLen 2n frames in one launch (n = 256..2048, the reference's own
+// bit-reversal table); hipErrorNotSupported: not handled here (the caller takes the two-launch
+// schedule).
+template <typename T>
+static hipError_t dispatch_r16_mfcc_fused(int n, const T* frames, uint32_t batch, const T* tw, const T* win, bool brev,
+                                          const MqPostArgs<T>& pa, hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  switch (n) {
+    case 256:  return launch_r16_mfcc_fused<T, 256>(frames, batch, tw, win, brev, pa, st);
+    case 512:  return launch_r16_mfcc_fused<T, 512>(frames, batch, tw, win, brev, pa, st);
+    case 1024: return launch_r16_mfcc_fused<T, 1024>(frames, batch, tw, win, brev, pa, st);
+    case 2048: return launch_r16_mfcc_fused<T, 2048>(frames, batch, tw, win, brev, pa, st);
+    default:   return hipErrorNotSupported;
+  }
+}
+hipError_t mfcc_q31_fused_launch(int n, const int32_t* frames, uint32_t batch, const int32_t* tw, const int32_t* win,
+                                 bool brev, const int4* stw, int nb_mel, const int32_t* coefs, const uint32_t* bf,
+                                 int total, int nb_dct, const int32_t* dct, const int32_t* lut, int32_t* dst,
+                                 hipStream_t st) {
+  MqPostArgs<int32_t> pa;
+  pa.tw = stw; pa.coefs = coefs; pa.bf = bf; pa.dct = dct; pa.lut = lut; pa.dst = dst;
+  pa.nb_mel = nb_mel; pa.total = total; pa.nb_dct = nb_dct;
+  return dispatch_r16_mfcc_fused<int32_t>(n, frames, batch, tw, win, brev, pa, st);
+}
+hipError_t mfcc_q15_fused_launch(int n, const int16_t* frames, uint32_t batch, const int16_t* tw, const int16_t* win,
+                                 bool brev, const int4* stw, int nb_mel, const int16_t* coefs, const uint32_t* bf,
+                                 int total, int nb_dct, const int16_t* dct, const int32_t* lut, int16_t* dst,
+                                 hipStream_t st) {
+  MqPostArgs<int16_t> pa;
+  pa.tw = stw; pa.coefs = coefs; pa.bf = bf; pa.dct = dct; pa.lut = lut; pa.dst = dst;
+  pa.nb_mel = nb_mel; pa.total = total; pa.nb_dct = nb_dct;
+  return dispatch_r16_mfcc_fused<int16_t>(n, frames, batch, tw, win, brev, pa, st);
 }
 
 // MFCC front end + the RFFT's inner forward CFFT of length n in place (n = fftLen / 2 in

@@ -308,13 +308,22 @@ __device__ __forceinline__ FirUnit fir_unit(uint32_t u, uint32_t nseg, uint32_t 
   x.last = !LONG || seg == (int)nseg - 1;
   return x;
 }
-template <int R, int KPRE, bool LONG, bool FMA>
+// DB (round 4): two LDS window images.  The next unit's window is written to
+// the other image right after the one barrier of a unit, while the current image is read by the
+// MACs, so a unit costs one __syncthreads instead of two and no wave waits for the others'
+// MACs before the staging writes (not for LONG / FMA units).
+#ifndef MI355X_FIR_DB
+#define MI355X_FIR_DB 0
+#endif
+template <int R, int KPRE, bool LONG, bool FMA, bool DB = false>
 __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32_FMA_WAVES : MI355X_FIR_F32_WAVES(R)) void fir_f32_kernel(
     const float* __restrict__ coeffs, int T, const float* __restrict__ src, float* __restrict__ dst, uint32_t B,
     const float* __restrict__ hist_in, uint32_t nchunks, uint32_t items, uint32_t ipw, FirIn in, FirOut fo) {
   static_assert(R == 16 || (R == 8 && !FMA), "R = 16, or R = 8 for the bit-exact path");
+  static_assert(!DB || (!LONG && !FMA), "double-buffered windows: short bit-exact filters");
   constexpr int kWin = KPRE * kBlock;
-  __shared__ __attribute__((aligned(16))) float win[wpos<R>(kWin) + 32];
+  constexpr int kImg = wpos<R>(kWin) + 32;          // words per window image
+  __shared__ __attribute__((aligned(16))) float win[(DB ? 2 : 1) * kImg];
   __shared__ __attribute__((aligned(16))) float cl[FMA ? kFirSeg + 64 : 4];   // FMA: the unit's taps (+ read-ahead)
   const int T1 = T - 1;
   const uint32_t i0 = blockIdx.x * ipw;
@@ -324,26 +333,12 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
   const int tid = threadIdx.x;
   const int base = tid * R;                         // local output index of this lane
   const int jl = fir_stage_lane(tid);               // the row sample this thread stages
-  float* wl = win + wpos<R>(jl);                       // wpos(jl + 256 k) = wpos(jl) + 320 k
   F32Win<R, KPRE, LONG> pre;
   F32Coef pc;
-  FirUnit cur = fir_unit<R, LONG>(u0, nseg, nchunks, B, T);
-  fir_f32_fetch<R, KPRE, LONG>(pre, cur.it, src, hist_in, in, T1, jl);
-  fir_f32_put<R, KPRE, LONG>(wl, pre);
-  if constexpr (FMA) {
-    fir_f32_cfetch(pc, coeffs, cur.it, in, cur.Ts, tid);
-    fir_f32_cput(cl, pc, tid);
-  }
   float acc[R];
-  // Per unit: barrier (window ready) -> next window's loads -> MACs -> barrier (window free)
-  // -> next window to LDS -> output stores.  The window write waits only for loads that had a
-  // whole unit of MACs to land; the stores are issued after it, so no wait ever covers them.
-  for (uint32_t u = u0;;) {
-    __syncthreads();
-    const bool more = u + 1 < u1;
-    const FirUnit nxt = more ? fir_unit<R, LONG>(u + 1, nseg, nchunks, B, T) : cur;
-    if (more) fir_f32_fetch<R, KPRE, LONG>(pre, nxt.it, src, hist_in, in, T1, jl);
-    if (FMA && more) fir_f32_cfetch(pc, coeffs, nxt.it, in, nxt.Ts, tid);
+
+  // the MACs of unit `cur` from window image wimg
+  auto macs = [&](const FirUnit& cur, const float* wimg) {
     if (base < cur.it.count) {
       if (cur.first) {
 #pragma unroll
@@ -358,25 +353,25 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
       int g = base >> 3;                            // the lane's first group
       const float* const ci = coeffs + cur.it.f * in.cstride + cur.it.a;
       const float* cp = FMA ? cl : ci;
-      ld_grp<R>(X0, win, g);
-      ld_grp<R>(X1, win, g + 1);
-      if constexpr (R == 16) ld_grp<R>(X2, win, g + 2);
+      ld_grp<R>(X0, wimg, g);
+      ld_grp<R>(X1, wimg, g + 1);
+      if constexpr (R == 16) ld_grp<R>(X2, wimg, g + 2);
       int nb = rounds >> 2;
       if constexpr (FMA && R == 16) {
-        f32_rounds_ldsc<FMA>(acc, win, g, cp, rounds);
+        f32_rounds_ldsc<FMA>(acc, wimg, g, cp, rounds);
       } else {
       if (nb > 0) {
         do {
           if constexpr (R == 8) {
-            ld_coef(c0, cp, 0);  ld_grp<R>(X2, win, g + 2); f32_round<R, FMA>(acc, X0, X1, X1, c0);
-            ld_coef(c1, cp, 8);  ld_grp<R>(X3, win, g + 3); f32_round<R, FMA>(acc, X1, X2, X2, c1);
-            ld_coef(c0, cp, 16); ld_grp<R>(X0, win, g + 4); f32_round<R, FMA>(acc, X2, X3, X3, c0);
-            ld_coef(c1, cp, 24); ld_grp<R>(X1, win, g + 5); f32_round<R, FMA>(acc, X3, X0, X0, c1);
+            ld_coef(c0, cp, 0);  ld_grp<R>(X2, wimg, g + 2); f32_round<R, FMA>(acc, X0, X1, X1, c0);
+            ld_coef(c1, cp, 8);  ld_grp<R>(X3, wimg, g + 3); f32_round<R, FMA>(acc, X1, X2, X2, c1);
+            ld_coef(c0, cp, 16); ld_grp<R>(X0, wimg, g + 4); f32_round<R, FMA>(acc, X2, X3, X3, c0);
+            ld_coef(c1, cp, 24); ld_grp<R>(X1, wimg, g + 5); f32_round<R, FMA>(acc, X3, X0, X0, c1);
           } else {
-            ld_coef(c0, cp, 0);  ld_grp<R>(X3, win, g + 3); f32_round<R, FMA>(acc, X0, X1, X2, c0);
-            ld_coef(c1, cp, 8);  ld_grp<R>(X0, win, g + 4); f32_round<R, FMA>(acc, X1, X2, X3, c1);
-            ld_coef(c0, cp, 16); ld_grp<R>(X1, win, g + 5); f32_round<R, FMA>(acc, X2, X3, X0, c0);
-            ld_coef(c1, cp, 24); ld_grp<R>(X2, win, g + 6); f32_round<R, FMA>(acc, X3, X0, X1, c1);
+            ld_coef(c0, cp, 0);  ld_grp<R>(X3, wimg, g + 3); f32_round<R, FMA>(acc, X0, X1, X2, c0);
+            ld_coef(c1, cp, 8);  ld_grp<R>(X0, wimg, g + 4); f32_round<R, FMA>(acc, X1, X2, X3, c1);
+            ld_coef(c0, cp, 16); ld_grp<R>(X1, wimg, g + 5); f32_round<R, FMA>(acc, X2, X3, X0, c0);
+            ld_coef(c1, cp, 24); ld_grp<R>(X2, wimg, g + 6); f32_round<R, FMA>(acc, X3, X0, X1, c1);
           }
           g += 4;
           cp += 32;
@@ -387,11 +382,11 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
       if (rem > 0) {
         if constexpr (R == 8) {
           ld_coef(c0, cp, 0);
-          ld_grp<R>(X2, win, g + 2);
+          ld_grp<R>(X2, wimg, g + 2);
           f32_round<R, FMA>(acc, X0, X1, X1, c0);
           if (rem > 1) {
             ld_coef(c1, cp, 8);
-            ld_grp<R>(X3, win, g + 3);
+            ld_grp<R>(X3, wimg, g + 3);
             f32_round<R, FMA>(acc, X1, X2, X2, c1);
             if (rem > 2) {
               ld_coef(c0, cp, 16);
@@ -400,11 +395,11 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
           }
         } else {
           ld_coef(c0, cp, 0);
-          ld_grp<R>(X3, win, g + 3);
+          ld_grp<R>(X3, wimg, g + 3);
           f32_round<R, FMA>(acc, X0, X1, X2, c0);
           if (rem > 1) {
             ld_coef(c1, cp, 8);
-            ld_grp<R>(X0, win, g + 4);
+            ld_grp<R>(X0, wimg, g + 4);
             f32_round<R, FMA>(acc, X1, X2, X3, c1);
             if (rem > 2) {
               ld_coef(c0, cp, 16);
@@ -418,14 +413,12 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
       for (int k = 8 * rounds; k < Ts; ++k) {
         const float c = ci[k];
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = f32_mac<FMA>(acc[r], win[wpos<R>(base + k + r)], c);
+        for (int r = 0; r < R; ++r) acc[r] = f32_mac<FMA>(acc[r], wimg[wpos<R>(base + k + r)], c);
       }
     }
-    if (more) {
-      __syncthreads();                              // every wave is done reading this window
-      fir_f32_put<R, KPRE, LONG>(wl, pre);
-      if constexpr (FMA) fir_f32_cput(cl, pc, tid);
-    }
+  };
+  // the outputs of unit `cur` (its last tap segment)
+  auto store = [&](const FirUnit& cur) {
     if (cur.last && base < cur.it.count) {
       const FirItem& it = cur.it;
       const bool run = fo.M == 1 && fo.L == 1 && fo.dir == 1;
@@ -450,6 +443,55 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
         }
       }
     }
+  };
+
+  FirUnit cur = fir_unit<R, LONG>(u0, nseg, nchunks, B, T);
+  fir_f32_fetch<R, KPRE, LONG>(pre, cur.it, src, hist_in, in, T1, jl);
+  fir_f32_put<R, KPRE, LONG>(win + wpos<R>(jl), pre);
+  if constexpr (FMA) {
+    fir_f32_cfetch(pc, coeffs, cur.it, in, cur.Ts, tid);
+    fir_f32_cput(cl, pc, tid);
+  }
+  if constexpr (DB) {
+    // Per unit: barrier (image b holds this unit's window; every wave has left image b ^ 1)
+    // -> the next unit's window (loaded one unit ago) to image b ^ 1 -> the unit after next's
+    // loads -> MACs on image b -> stores.
+    bool more = u0 + 1 < u1;
+    if (more) fir_f32_fetch<R, KPRE, LONG>(pre, fir_unit<R, LONG>(u0 + 1, nseg, nchunks, B, T).it, src, hist_in, in, T1, jl);
+    int b = 0;
+    for (uint32_t u = u0;;) {
+      __syncthreads();
+      if (more) {
+        fir_f32_put<R, KPRE, LONG>(win + (b ^ 1) * kImg + wpos<R>(jl), pre);
+        if (u + 2 < u1)
+          fir_f32_fetch<R, KPRE, LONG>(pre, fir_unit<R, LONG>(u + 2, nseg, nchunks, B, T).it, src, hist_in, in, T1, jl);
+      }
+      macs(cur, win + b * kImg);
+      store(cur);
+      if (!more) break;
+      ++u;
+      cur = fir_unit<R, LONG>(u, nseg, nchunks, B, T);
+      more = u + 1 < u1;
+      b ^= 1;
+    }
+    return;
+  }
+  // Per unit: barrier (window ready) -> next window's loads -> MACs -> barrier (window free)
+  // -> next window to LDS -> output stores.  The window write waits only for loads that had a
+  // whole unit of MACs to land; the stores are issued after it, so no wait ever covers them.
+  for (uint32_t u = u0;;) {
+    __syncthreads();
+    const bool more = u + 1 < u1;
+    const FirUnit nxt = more ? fir_unit<R, LONG>(u + 1, nseg, nchunks, B, T) : cur;
+    if (more) fir_f32_fetch<R, KPRE, LONG>(pre, nxt.it, src, hist_in, in, T1, jl);
+    if (FMA && more) fir_f32_cfetch(pc, coeffs, nxt.it, in, nxt.Ts, tid);
+    macs(cur, win);
+    if (more) {
+      __syncthreads();                              // every wave is done reading this window
+      fir_f32_put<R, KPRE, LONG>(win + wpos<R>(jl), pre);
+      if constexpr (FMA) fir_f32_cput(cl, pc, tid);
+    }
+    store(cur);
     if (!more) break;
     cur = nxt;
     ++u;
@@ -959,6 +1001,29 @@ __global__ void fir_hist_kernel(const T* __restrict__ src, T* __restrict__ hist,
   hist[g] = sidx < T1 ? hist_in[f * T1 + sidx] : src[f * B + (sidx - T1)];
 }
 
+// Latency path for the drop-in arm_fir_f32 (one short block per call, e.g. the 29-tap x
+// 32-sample arm_fir_example_f32.c:141-239): one workgroup per filter stages s = [history ;
+// block] in LDS, every output sums its taps k = 0 .. T-1 in order (mul then add, the
+// reference's rounding), and the new history s[B .. B+T-1) is written from the LDS image -- one
+// launch instead of filter pass + history kernel, and in place / B < T-1 need no copies (every
+// read of src and hist_in precedes the barrier, every write follows it).
+constexpr int kFirSmallMax = 8192;           // T - 1 + B words of LDS
+__global__ __launch_bounds__(kBlock) void fir_f32_small_kernel(const float* __restrict__ coeffs, int T,
+                                                               const float* src, float* dst, uint32_t B,
+                                                               float* hist, const float* hist_in) {
+  __shared__ float s[kFirSmallMax];
+  const int T1 = T - 1, tid = threadIdx.x;
+  const uint64_t f = blockIdx.x;
+  for (int j = tid; j < T1 + (int)B; j += kBlock) s[j] = j < T1 ? hist_in[f * T1 + j] : src[f * B + (j - T1)];
+  __syncthreads();
+  for (int n = tid; n < (int)B; n += kBlock) {
+    float acc = 0.0f;
+    for (int k = 0; k < T; ++k) acc = acc + s[n + k] * coeffs[k];
+    dst[f * B + n] = acc;
+  }
+  for (int j = tid; j < T1; j += kBlock) hist[f * T1 + j] = s[B + j];
+}
+
 // One f32 FIR pass over `batch` filters, outputs on the lattice `fo`.
 template <int R, bool F>
 static void fir_f32_launch(const float* coeffs, int T, const float* src, float* dst, uint32_t B, uint32_t batch,
@@ -968,10 +1033,11 @@ static void fir_f32_launch(const float* coeffs, int T, const float* src, float* 
   const int kpre = fir_f32_kpre<R>(T < kFirSeg ? T : kFirSeg);
   constexpr int K0 = fir_f32_kpre<R>(1), KL = fir_f32_kpre<R>(kFirSeg);     // 9..13 (R = 8), 17..21 (R = 16)
   static_assert(KL - K0 == 4, "five window sizes");
+  constexpr bool DB = MI355X_FIR_DB && !F;
   auto k = T > kFirSeg ? fir_f32_kernel<R, KL, true, F>
-         : kpre <= K0 ? fir_f32_kernel<R, K0, false, F> : kpre == K0 + 1 ? fir_f32_kernel<R, K0 + 1, false, F>
-         : kpre == K0 + 2 ? fir_f32_kernel<R, K0 + 2, false, F> : kpre == K0 + 3 ? fir_f32_kernel<R, K0 + 3, false, F>
-         : fir_f32_kernel<R, KL, false, F>;
+         : kpre <= K0 ? fir_f32_kernel<R, K0, false, F, DB> : kpre == K0 + 1 ? fir_f32_kernel<R, K0 + 1, false, F, DB>
+         : kpre == K0 + 2 ? fir_f32_kernel<R, K0 + 2, false, F, DB> : kpre == K0 + 3 ? fir_f32_kernel<R, K0 + 3, false, F, DB>
+         : fir_f32_kernel<R, KL, false, F, DB>;
   uint32_t ipw = MI355X_FIR_IPW;
   if (T > kFirSeg) ipw = 1;                         // a long item is already many units
   if (!ipw) {
@@ -1011,6 +1077,13 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
   if (batch == 0 || B == 0) return hipSuccess;
   if (T_ < 1) return hipErrorInvalidValue;        // numTaps > kFirMaxTaps: tap segments
   const int T1 = T_ - 1;
+  if constexpr (sizeof(T) == 4) {
+    if (kind == kFirF32 && batch <= 8 && (int64_t)T1 + B <= kFirSmallMax && (uint64_t)B * T_ <= (1u << 16)) {
+      hipLaunchKernelGGL(fir_f32_small_kernel, dim3(batch), dim3(kBlock), 0, st, (const float*)coeffs, T_,
+                         (const float*)src, (float*)dst, B, (float*)hist, (const float*)hist);
+      return hipGetLastError();
+    }
+  }
   const int chunk = kind == kFirF32 || kind == kFirF32Fma ? kF32ChunkMin : kFirChunk;
   const uint32_t nchunks = (B + chunk - 1) / chunk;
   const uint64_t items64 = (uint64_t)nchunks * batch;

@@ -37,6 +37,16 @@ bool cfft_q31_r16_launch(int n, int32_t* data, uint32_t batch, const int32_t* tw
 bool cfft_q15_r16_launch(int n, int16_t* data, uint32_t batch, const int16_t* tw, uint32_t flags, hipStream_t st);
 // The same kernels with the MFCC front end fused into their load phase (PRE): forward, frame
 // maxima to maxv[frame * mstride]; false when n is not 256..2048.
+// The whole MFCC q31 / q15 in one launch (front end + CFFT + back end, cfft_fixed_r16.hip);
+// n = fftLen / 2.  hipErrorNotSupported: not handled (take the two-launch schedule).
+hipError_t mfcc_q31_fused_launch(int n, const int32_t* frames, uint32_t batch, const int32_t* tw, const int32_t* win,
+                                 bool brev, const int4* stw, int nb_mel, const int32_t* coefs, const uint32_t* bf,
+                                 int total, int nb_dct, const int32_t* dct, const int32_t* lut, int32_t* dst,
+                                 hipStream_t st);
+hipError_t mfcc_q15_fused_launch(int n, const int16_t* frames, uint32_t batch, const int16_t* tw, const int16_t* win,
+                                 bool brev, const int4* stw, int nb_mel, const int16_t* coefs, const uint32_t* bf,
+                                 int total, int nb_dct, const int16_t* dct, const int32_t* lut, int16_t* dst,
+                                 hipStream_t st);
 bool cfft_q31_r16_mfcc_launch(int n, int32_t* data, uint32_t batch, const int32_t* tw, const int32_t* win,
                               int32_t* maxv, int mstride, bool brev, hipStream_t st);
 bool cfft_q15_r16_mfcc_launch(int n, int16_t* data, uint32_t batch, const int16_t* tw, const int16_t* win,

@@ -2,6 +2,7 @@
 #include "runtime.hpp"
 
 #include <dlfcn.h>
+#include <stdlib.h>
 #include <link.h>
 #include <string.h>
 
@@ -14,6 +15,10 @@
 #include <vector>
 
 #include "../../include/arm_math_mi355x.h"
+
+#ifndef MI355X_SYNC_DEFAULT
+#define MI355X_SYNC_DEFAULT 0
+#endif
 
 namespace mi355x {
 
@@ -497,9 +502,58 @@ HostIO::~HostIO() {
   if ((slot_ > 0 || zslot_ > 0) && !finished_) (void)hipStreamSynchronize(st_);
 }
 
+// Completion of a synchronous drop-in call.  kSyncSpin: a stream write of a
+// per-thread sequence number into a coherent, device-mapped host word after the call's work, and
+// the host spins on that word (bounded; then hipStreamSynchronize, which also reports errors)
+// instead of the runtime's blocking wait.  CMSISDSP_MI355X_SYNC=sync|spin overrides the default.
+namespace {
+struct DoneWord { volatile uint32_t* h = nullptr; uint32_t* d = nullptr; uint32_t seq = 0; };
+thread_local std::map<int, DoneWord> t_done;
+int sync_mode() {
+  static const int m = [] {
+    const char* e = getenv("CMSISDSP_MI355X_SYNC");
+    if (e && !strcmp(e, "sync")) return 0;
+    if (e && !strcmp(e, "spin")) return 1;
+    return MI355X_SYNC_DEFAULT;
+  }();
+  return m;
+}
+}  // namespace
+
+hipError_t wait_stream(hipStream_t st) {
+  if (sync_mode() == 1) {
+    const int dev = cur_dev();
+    DoneWord& w = t_done[dev];
+    if (!w.h) {
+      void* p = nullptr;
+      if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess) {
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, p, 0) == hipSuccess) {
+          w.h = (volatile uint32_t*)p;
+          w.d = (uint32_t*)d;
+          *w.h = 0;
+        } else {
+          (void)hipHostFree(p);
+        }
+      }
+    }
+    if (w.h) {
+      const uint32_t v = ++w.seq;
+      if (hipStreamWriteValue32(st, w.d, v, 0) == hipSuccess) {
+        // spin up to ~2^22 polls (milliseconds); a slow or failed call falls through to the sync
+        for (uint32_t i = 0; i < (1u << 22); ++i)
+          if (__atomic_load_n(w.h, __ATOMIC_ACQUIRE) == v) return hipSuccess;
+      } else {
+        (void)hipGetLastError();
+      }
+    }
+  }
+  return hipStreamSynchronize(st);
+}
+
 hipError_t HostIO::finish() {
   finished_ = true;
-  hipError_t e = hipStreamSynchronize(st_);
+  hipError_t e = wait_stream(st_);
   if (e != hipSuccess) return e;
   for (int i = 0; i < nouts_; ++i) memcpy(outs_[i].host, outs_[i].pin, outs_[i].bytes);
   nouts_ = 0;

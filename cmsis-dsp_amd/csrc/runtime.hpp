@@ -103,6 +103,10 @@ class HostIO {
   bool finished_ = false;
 };
 
+// Wait for everything enqueued on st (the synchronous drop-in calls' completion): a spin on a
+// host word written by the stream, or hipStreamSynchronize (runtime.cpp, CMSISDSP_MI355X_SYNC).
+hipError_t wait_stream(hipStream_t st);
+
 // The internal stream used by the synchronous drop-in API on the current device.
 hipStream_t sync_stream();
 

@@ -6,6 +6,8 @@
 //   graph+sync/spin   : the same kernels launched as a captured one-node hipGraph
 //   copy8k+spin       : kernel reads 8 KiB from coherent pinned memory and writes 8 KiB back
 //                       (the cfft N=1024 drop-in's data movement), host spins on a flag
+//   writevalue+spin   : kernel, then hipStreamWriteValue32 of a sequence number into the mapped
+//                       host flag (no change to the kernel), host spins on it
 // Each under hipDeviceScheduleAuto (default) and hipDeviceScheduleSpin.  Prints one JSON line.
 // Usage: launch_floor [calls] [spin]
 #include <hip/hip_runtime.h>
@@ -102,6 +104,21 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(copy_flag_kernel, dim3(1), dim3(512), 0, st, zin, zout, flag, seq);
     (void)hipStreamSynchronize(st);
   }, calls);
+  // empty kernel, then a stream write of the sequence number into the mapped host flag
+  unsigned* dflag = nullptr;
+  CK(hipHostGetDevicePointer((void**)&dflag, flag, 0));
+  const double wv_spin = per_call_us([&](int) {
+    ++seq;
+    hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, st);
+    (void)hipStreamWriteValue32(st, dflag, seq, 0);
+    wait_flag(seq);
+  }, calls);
+  const double copy_wv_spin = per_call_us([&](int) {
+    ++seq;
+    hipLaunchKernelGGL(copy_flag_kernel, dim3(1), dim3(512), 0, st, zin, zout, flag, seq + 1000000000u);
+    (void)hipStreamWriteValue32(st, dflag, seq, 0);
+    wait_flag(seq);
+  }, calls);
   // one-node graph of the empty kernel
   hipGraph_t g;
   hipGraphExec_t ge;
@@ -115,7 +132,9 @@ int main(int argc, char** argv) {
   }, calls);
   (void)hipStreamSynchronize(st);
   std::printf("{\"spin_schedule\": %s, \"calls\": %d, \"empty_sync_us\": %.2f, \"empty_event_us\": %.2f, "
-              "\"flag_spin_us\": %.2f, \"copy8k_spin_us\": %.2f, \"copy8k_sync_us\": %.2f, \"graph_sync_us\": %.2f}\n",
-              spin ? "true" : "false", calls, empty_sync, empty_event, flag_spin, copy_spin, copy_sync, graph_sync);
+              "\"flag_spin_us\": %.2f, \"copy8k_spin_us\": %.2f, \"copy8k_sync_us\": %.2f, \"graph_sync_us\": %.2f, "
+              "\"writevalue_spin_us\": %.2f, \"copy8k_writevalue_spin_us\": %.2f}\n",
+              spin ? "true" : "false", calls, empty_sync, empty_event, flag_spin, copy_spin, copy_sync, graph_sync, wv_spin,
+              copy_wv_spin);
   return 0;
 }
