@@ -443,9 +443,6 @@ bool mfcc_fx_prepare(const Inst* S, MfccFxDev<T>& d) {
 // kernel), 0 = three launches (pre, CFFT, post: also every other length and custom bit-reversal
 // tables).  The round-3 one-launch kernel (generic LDS-stage CFFT, frames resident in LDS) was
 // slower than the two-launch schedule and was removed (DESIGN.md §4 mfcc_q31 / mfcc_q15).
-#ifndef MI355X_MFCC_FX_MODE
-#define MI355X_MFCC_FX_MODE 2
-#endif
 template <typename T, typename Inst>
 bool mfcc_fx_run(const Inst* S, const MfccFxDev<T>& d, T* x, T* y, T* dst, uint32_t batch, hipStream_t st) {
   const int n = (int)S->fftLen, nd = (int)S->nbDctOutputs, nm = (int)S->nbMelFilters;

@@ -112,27 +112,15 @@ __device__ __forceinline__ int s1024(int e) {
   return (e >> 6) * 72 + (((e >> 3) & 7) << 3) + ((e & 7) ^ ((e >> 3) & 7));
 }
 
-#ifndef MI355X_N1024_WAVES
-#define MI355X_N1024_WAVES 1
-#endif
 // Work mapping.  N1024_T = 0: persistent grid, wave g takes transforms g, g + G, g + 2G, ...
 // N1024_T = T > 0: grid = batch / (T * WPB) waves, wave g takes the T CONSECUTIVE transforms
 // gT .. gT+T-1 (the live HBM footprint stays a compact sliding window; measured by
 // tools/probes/hbm_inplace.hip).  N1024_WPB waves per workgroup, each with its own LDS image.
 // Default T = 4, WPB = 8, no software prefetch: 76 % of HBM peak against 66 % for the
 // persistent prefetching walk (profiles/r01/variants_n1024_mapping.txt).
-#ifndef MI355X_N1024_T
-#define MI355X_N1024_T 4
-#endif
-#ifndef MI355X_N1024_WPB
-#define MI355X_N1024_WPB 8
-#endif
 // N1024_SPLIT = S > 1: workgroup b works in region b % S of the batch (S contiguous regions,
 // each S-th dispatched workgroup in the same region), so S address streams far apart are
 // live at once instead of one sliding window (grid % S != 0 falls back to S = 1).
-#ifndef MI355X_N1024_SPLIT
-#define MI355X_N1024_SPLIT 1
-#endif
 constexpr int kN1024T = MI355X_N1024_T, kN1024Wpb = MI355X_N1024_WPB, kN1024Split = MI355X_N1024_SPLIT;
 // Each wave owns its LDS image, so the exchanges need only a wave-level barrier: one
 // wave's LDS operations complete in issue order; the fences stop the compiler from moving
@@ -172,9 +160,6 @@ __global__ __launch_bounds__(64 * kN1024Wpb, MI355X_N1024_WAVES) void cfft_f32_n
 // software-pipelined variant (the next transform's loads under phases B/C) was +4% under the
 // persistent walk (profiles/r01/variants_n1024.txt) and 1% slower with T = 4 consecutive
 // transforms per wave; it was removed in round 3.
-#ifndef MI355X_NT
-#define MI355X_NT 1
-#endif
 #if MI355X_NT
 #define LD(p) ldnt(p)
 #else
@@ -276,14 +261,8 @@ __global__ __launch_bounds__(64 * kN1024Wpb, MI355X_N1024_WAVES) void cfft_f32_n
 __device__ __forceinline__ int s4096f(int e) { return e + 8 * (e >> 6) + (e >> 9); }
 __device__ __forceinline__ int rev3o(int t) { return ((t & 7) << 6) | (((t >> 3) & 7) << 3) | (t >> 6); }
 
-#ifndef MI355X_N4096_WAVES
-#define MI355X_N4096_WAVES 1
-#endif
 // Work mapping: T = 0 persistent grid-stride walk; T > 0: workgroup b takes the T consecutive
 // transforms bT .. bT+T-1 (as the fixed-point N = 4096 kernels, cfft_fixed.hip).
-#ifndef MI355X_N4096_T
-#define MI355X_N4096_T 8
-#endif
 constexpr uint32_t kN4096T = MI355X_N4096_T;
 // IFFT / BREV (ifftFlag, bitReverseFlag) are template parameters so that no output word or
 // address goes through a run-time select.
@@ -391,9 +370,6 @@ __global__ __launch_bounds__(256, MI355X_N4096_WAVES) void cfft_f32_n4096_kernel
   }
 }
 
-#ifndef MI355X_F32_N4096
-#define MI355X_F32_N4096 1
-#endif
 
 // ============================================================================================
 // N = 512 specialist (arm_cfft_f32.c:1270: arm_radix8_butterfly_f32 with modifier 1, 512 = 8^3,
@@ -403,15 +379,6 @@ __global__ __launch_bounds__(256, MI355X_N4096_WAVES) void cfft_f32_n4096_kernel
 // 8l + m, whose output m is bin 64m + 8(l & 7) + (l >> 3): with bitReverseFlag each store
 // instruction writes a permutation of 64 consecutive bins (512 B), without it the lane's 8
 // consecutive elements (two 16-B stores).  LDS image: s1024 (conflict free for these patterns).
-#ifndef MI355X_N512_T
-#define MI355X_N512_T 2
-#endif
-#ifndef MI355X_N512_WPB
-#define MI355X_N512_WPB 8
-#endif
-#ifndef MI355X_F32_N512
-#define MI355X_F32_N512 1
-#endif
 constexpr int kN512T = MI355X_N512_T, kN512Wpb = MI355X_N512_WPB;
 template <bool IFFT, bool BREV>
 __global__ __launch_bounds__(64 * kN512Wpb) void cfft_f32_n512_kernel(float2* __restrict__ data, uint32_t batch,
@@ -516,15 +483,6 @@ __device__ __forceinline__ void by4_bot(float2& A, float2& B, float2& C, float2&
   D = make_float2(t42 * w4.y + t43 * w4.x, t43 * w4.y - t42 * w4.x);
 }
 
-#ifndef MI355X_N2048_T
-#define MI355X_N2048_T 2
-#endif
-#ifndef MI355X_N2048_WPB
-#define MI355X_N2048_WPB 4
-#endif
-#ifndef MI355X_F32_N2048
-#define MI355X_F32_N2048 1
-#endif
 constexpr int kN2048T = MI355X_N2048_T, kN2048Wpb = MI355X_N2048_WPB;
 
 __global__ __launch_bounds__(64 * kN2048Wpb) void cfft_f32_n2048_kernel(float2* __restrict__ data, uint32_t batch,

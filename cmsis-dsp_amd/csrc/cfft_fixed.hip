@@ -118,29 +118,14 @@ template <typename C> __device__ __forceinline__ int sfx(int e) {
 // Gsamples/s, bit-exact (profiles/r03/experiments/fx4096_residency.json; one workgroup per CU
 // 274, and the q15 kernel is fastest at its register-bound three).  The in-place streaming probe
 // of this access pattern ranks the same way (profiles/r03/probe_hbm_wgtile.txt, lds = 55296).
-#ifndef MI355X_FX_Q31_SLOTS
-#define MI355X_FX_Q31_SLOTS 6912
-#endif
 template <typename C> constexpr int kFxSlots = sizeof(C) == 8 ? MI355X_FX_Q31_SLOTS : 4351;
 
-#ifndef MI355X_FX_WAVES
-#define MI355X_FX_WAVES 1     // minimum waves per SIMD the register allocation must allow
-#endif
 // Twiddle placement.  Lane-distinct twiddles (stage 1: 12 words per lane, stage 2: 3) stay in
 // VGPRs for the kernel's life; stage 3 depends only on (t % 16, a) and stage 4 on t % 16, so
 // MI355X_FX_TW3_LDS / MI355X_FX_TW4_LDS keep them in small LDS tables (1.5 KiB / 384 B, read
 // as conflict-free broadcasts) instead of 24 / 6 VGPRs.  Stage 5 is lane-uniform (SGPRs).
-#ifndef MI355X_FX_TW3_LDS
-#define MI355X_FX_TW3_LDS 0
-#endif
-#ifndef MI355X_FX_TW4_LDS
-#define MI355X_FX_TW4_LDS 0
-#endif
 // MI355X_FX_PF = d >= 1: the next d transforms' 16 loads are held in registers (the first under
 // passes 2-3 of the current one), 32 VGPRs per transform for q31.
-#ifndef MI355X_FX_PF
-#define MI355X_FX_PF 1
-#endif
 // BREV / SAT are the bitReverseFlag and the RFFT inverse's saturating <<1 (kSatShl1) as
 // template parameters: as run-time flags the compiler if-converted them into selects on
 // every output word and address.
@@ -313,21 +298,9 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 // Each twiddle is held as the two packed words its products need (forward {w.x, w.y} and
 // {~w.y, w.x}; inverse {w.x, ~w.y} and {w.y, w.x}).  Same work mapping as
 // cfft_fx4096_kernel (three radix-16 register passes, s4096 LDS padding, free bit reversal).
-#ifndef MI355X_FX_Q15_PFD
-#define MI355X_FX_Q15_PFD 2
-#endif
 // MI355X_FXQ15_TW34_LDS = 1: the stage-3/4 twiddle pairs (functions of t % 16 only) live in
 // LDS tables (1.5 KiB + 384 B) instead of 30 VGPRs; MI355X_FXQ15_WAVES = the minimum waves per
 // SIMD the register allocation must allow.
-#ifndef MI355X_FXQ15_SLOTS
-#define MI355X_FXQ15_SLOTS 4351   // LDS words of the q15 kernel (more: fewer workgroups per CU)
-#endif
-#ifndef MI355X_FXQ15_TW34_LDS
-#define MI355X_FXQ15_TW34_LDS 0
-#endif
-#ifndef MI355X_FXQ15_WAVES
-#define MI355X_FXQ15_WAVES 1
-#endif
 template <bool INV, bool BREV, bool SAT>
 __global__ __launch_bounds__(256, MI355X_FXQ15_WAVES) void cfft_q15_4096_pk_kernel(short2* __restrict__ data, uint32_t batch,
                                                                     const short2* __restrict__ tw) {

@@ -135,9 +135,6 @@ __device__ __forceinline__ void bfly_q15(int2& a, int2& b, int2& c, int2& d,
 
 // ------------------------------------------------------------------ q15 butterflies, packed
 // (restated from bfly_q15, see cfft_q15_4096_pk_kernel for the mapping)
-#ifndef MI355X_FX_Q15_PACKED
-#define MI355X_FX_Q15_PACKED 1
-#endif
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ s16x2 pk(uint32_t u) { return __builtin_bit_cast(s16x2, u); }
@@ -225,9 +222,6 @@ __device__ __forceinline__ void bfly(int2& a, int2& b, int2& c, int2& d, int2 w1
 // Global I/O through a buffer resource per transform (gfx9 raw buffer, dword 3 = 0x00020000):
 // one VGPR byte offset per lane, the (a, b) element offsets as SGPR soffsets, so no 64-bit
 // address arithmetic per access.  MI355X_FX_NT = 2 marks the streamed words nontemporal.
-#ifndef MI355X_FX_NT
-#define MI355X_FX_NT 2
-#endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t fx_rsrc(const void* p, uint32_t bytes) { return buf_rsrc(p, bytes); }
 template <typename C> struct FxIO;
 template <> struct FxIO<int2> {
@@ -254,12 +248,6 @@ template <> struct FxIO<short2> {
 // Measured at 2^20 transforms (profiles/r02/variants_fx4096/): T = 8 ran at the ceiling of
 // the kernels' own access pattern (a probe build with the butterflies removed) on
 // every box, while the persistent walk ranged 316-354 Gsamples/s (q31) from box to box.
-#ifndef MI355X_FX_T
-#define MI355X_FX_T 8
-#endif
-#ifndef MI355X_FXQ15_T
-#define MI355X_FXQ15_T 8
-#endif
 struct FxWalk { uint32_t begin, end, step; };
 template <uint32_t kT> __device__ __forceinline__ FxWalk fx_walk(uint32_t batch) {
   if constexpr (kT == 0) return FxWalk{blockIdx.x, batch, gridDim.x};

@@ -33,9 +33,6 @@
 
 namespace mi355x {
 
-#ifndef MI355X_FXR_T
-#define MI355X_FXR_T 8
-#endif
 // N = 32 / 64 / 128 stay on the generic kernel: with 2-8 threads per transform each load
 // instruction would scatter over 32-8 transforms (measured on this kernel, bit-exact: q31
 // 42 / 201 / 254 Gsamples/s against 342 / 334 / 324 for the generic kernel).

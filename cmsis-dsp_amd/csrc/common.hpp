@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tuning.hpp"
+
 namespace mi355x {
 
 // Exact integer semantics of the reference's host scalar path (Include/dsp/none.h):

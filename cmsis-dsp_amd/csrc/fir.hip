@@ -93,9 +93,6 @@ __device__ __forceinline__ int fir_stage_lane(int tid) {
   return 8 * (16 * (h >> 2) + 4 * a + (h & 3)) + e;     // groups c, c+4, c+8, c+12 per half-wave
 }
 
-#ifndef MI355X_FIR_SCHED_BARRIER
-#define MI355X_FIR_SCHED_BARRIER 1
-#endif
 struct F32Grp { float v[8]; };
 // group g of the window: two ds_read2_b64
 template <int R>
@@ -267,9 +264,6 @@ __device__ __forceinline__ void fir_f32_cput(float* cl, const F32Coef& w, int ti
 // items / (resident workgroups x CUs), one generation of persistent workgroups.  Measured at
 // 2^17 items (Gsamples/s): ipw 1 209, 2 214, 4 216, 8 219, 16 217-222, 32 210-215,
 // persistent (64) 206-208.
-#ifndef MI355X_FIR_IPW
-#define MI355X_FIR_IPW 16
-#endif
 
 // Output lattice of fir_f32_kernel: output n of filter f (n % M == 0 only) is stored at
 // y[f per_filter + off + dir ((n / M) L + q)]: the FIR {1, 1, 0, 1, 0, B}; the decimator
@@ -282,12 +276,6 @@ struct FirOut {
   uint64_t per_filter;
 };
 
-#ifndef MI355X_FIR_F32_WAVES
-#define MI355X_FIR_F32_WAVES(R) ((R) == 16 ? 5 : 8)   // minimum waves per SIMD the allocation must allow
-#endif
-#ifndef MI355X_FIR_F32_FMA_WAVES
-#define MI355X_FIR_F32_FMA_WAVES 4                   // FMA: + 8 coefficient and 4 tap-staging VGPRs
-#endif
 // Long filters (numTaps > kFirSeg) run in tap segments of kFirSeg: a work unit is (item,
 // segment), the accumulators stay in registers from a unit with segment 0 to the one with the
 // last segment, so every output still sums its products k = 0, 1, .., numTaps - 1 in order.
@@ -312,9 +300,6 @@ __device__ __forceinline__ FirUnit fir_unit(uint32_t u, uint32_t nseg, uint32_t 
 // the other image right after the one barrier of a unit, while the current image is read by the
 // MACs, so a unit costs one __syncthreads instead of two and no wave waits for the others'
 // MACs before the staging writes (not for LONG / FMA units).
-#ifndef MI355X_FIR_DB
-#define MI355X_FIR_DB 0
-#endif
 template <int R, int KPRE, bool LONG, bool FMA, bool DB = false>
 __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32_FMA_WAVES : MI355X_FIR_F32_WAVES(R)) void fir_f32_kernel(
     const float* __restrict__ coeffs, int T, const float* __restrict__ src, float* __restrict__ dst, uint32_t B,
@@ -615,9 +600,6 @@ __device__ __forceinline__ void fir_q15_wide(const uint32_t* lds, const uint32_t
   }
 }
 
-#ifndef MI355X_FIR_Q15_WAVES
-#define MI355X_FIR_Q15_WAVES 1   // minimum waves per SIMD the register allocation must allow
-#endif
 // arm_fir_fast_q15: mod-2^32 sum over all tap pairs with one accumulating v_dot2 each,
 // planes 0/1 hold the raw even / odd sample-pair words; 4-word quads read one block ahead.
 struct Q15FastRing { uint4 e[3], o[3]; };

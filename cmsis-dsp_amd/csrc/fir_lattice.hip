@@ -68,9 +68,6 @@ struct LatIn {
   uint32_t nseg;
 };
 
-#ifndef MI355X_LAT_IPW
-#define MI355X_LAT_IPW 1   // 2 / 4 measured slower (f32 211 / 220 vs 221 Gsamples/s, q31 138 / 147 vs 172)
-#endif
 constexpr int kLatIpw = MI355X_LAT_IPW;    // consecutive segments per wave, next one prefetched
 
 template <int OP>

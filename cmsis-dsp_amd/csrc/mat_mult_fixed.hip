@@ -17,6 +17,8 @@
 // K <= kMatI8MaxK keeps every int32 accumulator exact; longer K uses the VALU kernel.
 // Operand maps (verified with exact data, tools/probes/mfma_i8_layout.hip): lane l holds
 // A[row l&31][k = 16(l>>5) + j] and B[k = 16(l>>5) + j][col l&31] in byte j.
+#include <type_traits>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -49,9 +51,6 @@ __device__ __forceinline__ uint32_t plane4(uint32_t v0, uint32_t v1, uint32_t v2
 // 16 k-consecutive bytes per column, so staging transposes 4 k-rows x CW columns per thread
 // into k-contiguous dwords (v_perm) before the LDS write.
 template <typename T> struct I8Cfg;
-#ifndef MI355X_I8_SCHED
-#define MI355X_I8_SCHED 6
-#endif
 template <> struct I8Cfg<int16_t> { static constexpr int BM = 128, BN = 128, WBM = 1, WBN = 2, KT = 64; };
 template <> struct I8Cfg<int32_t> { static constexpr int BM = 128, BN = 64, WBM = 1, WBN = 1, KT = 64; };
 constexpr int kNT2 = 512, kWavesM = 4, kWavesN = 2;
@@ -350,6 +349,265 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
   }
 }
 
+// ---- v3 kernel (round 4): the v2 tiling with B staged ROW-major.  B's
+// planes are stored as [k][n] byte rows (the global layout) and the MFMA's k-contiguous
+// operand is read with ds_read_b64_tr_b8 (gfx950's 8-bit transposed LDS read: per 16-lane group
+// an 8-row x 16-column byte block, lane i receiving column i, row q in byte q;
+// tools/probes/tr_b8.hip), so the v_perm transpose of v2's staging disappears: a thread stages
+// one k-row segment of B (32 bytes) with two 16-B loads and splits it into planes with one
+// v_perm per 4 values.  Column sums accumulate per thread over the k-rows it stages (its
+// columns are fixed for the whole K loop).  Selected by MI355X_I8_V3.
+template <typename T> struct I8B3 {               // B staging geometry
+  static constexpr int BN = I8Cfg<T>::BN, EB = 64 * BN / kNT2;   // elements per thread (16 q15 / 8 q31)
+  static constexpr int TPR = BN / EB;                            // threads per k-row (8)
+  static constexpr int PITCH = BN + 16;                          // bytes per plane row (tr_b8 banks)
+};
+typedef int v2i32_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2i32_t tr_b8(const int8_t* p) {   // p: a generic pointer into LDS
+  return __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i32_t*)p);
+}
+
+template <typename T, bool FULL>
+__global__ __launch_bounds__(kNT2) void mat_mult_i8v3_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                             T* __restrict__ C, int M, int K, int N, int fast) {
+  using G = I8Cfg<T>;
+  using GB = I8B3<T>;
+  constexpr int P = Slices<T>::P, S = 2 * P - 1;
+  constexpr int64_t C0 = Slices<T>::C0;
+  constexpr int BM = G::BM, BN = G::BN, WBM = G::WBM, WBN = G::WBN, kKT2 = G::KT, kPitch2 = kKT2;
+  constexpr int EPD = 4 / sizeof(T);
+  constexpr int AK = BM * kKT2 / kNT2, AKD = AK / EPD, AQ = kKT2 / AK;
+  constexpr int EB = GB::EB, EBD = EB / EPD, TPR = GB::TPR, BP = GB::PITCH;
+  constexpr int ABUF = P * BM * kPitch2, BBUF = P * kKT2 * BP;
+  constexpr int BUF = ABUF + BBUF;
+  __shared__ __attribute__((aligned(16))) int8_t lds[2 * BUF];
+
+  const int tilesN = (N + BN - 1) / BN, tiles = tilesN * ((M + BM - 1) / BM);
+  const uint32_t total = gridDim.x;
+  uint32_t lin = blockIdx.x;
+  if (total % 8 == 0) lin = (lin % 8) * (total / 8) + lin / 8;
+  const int t = (int)(lin % (uint32_t)tiles);
+  const int tm = t / tilesN, tn = t % tilesN;
+  const size_t bz = lin / (uint32_t)tiles;
+  A += bz * (size_t)M * K;
+  B += bz * (size_t)K * N;
+  C += bz * (size_t)M * N;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int row0 = tm * BM, col0 = tn * BN;
+
+  // staging roles: A row ar, AK k from ak0 (as v2); B k-row bk, columns bc .. bc + EB - 1
+  const int ar = tid / AQ, ak0 = AK * (tid % AQ);
+  const int bk = tid / TPR, bc = EB * (tid % TPR);
+  const int gr = row0 + ar, gc = col0 + bc;
+  const bool vecA = FULL || (((K * (int)sizeof(T)) % 16) == 0 && (((uintptr_t)A) & 15) == 0);
+  const bool vecB = FULL || (((N * (int)sizeof(T)) % 16) == 0 && (((uintptr_t)B) & 15) == 0);
+
+  uint32_t ad[AKD], bd[EBD];
+  auto load = [&](int k0) {
+    const int ka = k0 + ak0;
+    if (FULL || (vecA && gr < M && ka + AK <= K)) {
+      const uint4* p = reinterpret_cast<const uint4*>(A + (size_t)gr * K + ka);
+#pragma unroll
+      for (int i = 0; i < AKD / 4; ++i) {
+        const uint4 v = p[i];
+        ad[4 * i] = v.x; ad[4 * i + 1] = v.y; ad[4 * i + 2] = v.z; ad[4 * i + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < AKD; ++d) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int e = 0; e < EPD; ++e) {
+          const int k = ka + d * EPD + e;
+          const uint32_t v = (gr < M && k < K) ? (uint32_t)A[(size_t)gr * K + k] : 0u;
+          w |= (EPD == 2 ? (v & 0xffffu) : v) << (16 * e);
+        }
+        ad[d] = w;
+      }
+    }
+    const int kb = k0 + bk;
+    if (FULL || (vecB && kb < K && gc + EB <= N)) {
+      const uint4* p = reinterpret_cast<const uint4*>(B + (size_t)kb * N + gc);
+#pragma unroll
+      for (int i = 0; i < EBD / 4; ++i) {
+        const uint4 v = p[i];
+        bd[4 * i] = v.x; bd[4 * i + 1] = v.y; bd[4 * i + 2] = v.z; bd[4 * i + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < EBD; ++d) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int e = 0; e < EPD; ++e) {
+          const int c = gc + d * EPD + e;
+          const uint32_t v = (kb < K && c < N) ? (uint32_t)B[(size_t)kb * N + c] : 0u;
+          w |= (EPD == 2 ? (v & 0xffffu) : v) << (16 * e);
+        }
+        bd[d] = w;
+      }
+    }
+  };
+
+  int64_t my_rsum = 0;
+  // column sums of the k-rows this thread stages (at most K / 64 <= 511 of them): exact in int32
+  // for q15 (|v| <= 2^15), int64 for q31
+  using CS = typename std::conditional<sizeof(T) == 2, int32_t, int64_t>::type;
+  CS my_csum[EB];
+#pragma unroll
+  for (int c = 0; c < EB; ++c) my_csum[c] = 0;
+  i32x16 acc[S][WBM][WBN];
+#pragma unroll
+  for (int s2 = 0; s2 < S; ++s2)
+#pragma unroll
+    for (int i = 0; i < WBM; ++i)
+#pragma unroll
+      for (int j = 0; j < WBN; ++j) acc[s2][i][j] = i32x16{};
+  const int wm = wid / kWavesN, wn = wid % kWavesN;
+  const int r = lane & 31, h = lane >> 5;
+
+  auto stage = [&](int buf) {
+    auto As = reinterpret_cast<int8_t (*)[BM][kPitch2]>(lds + buf * BUF);
+    int8_t* Bs = lds + buf * BUF + ABUF;           // [P][kKT2][BP]
+    if constexpr (sizeof(T) == 2) {
+      int32_t ra = 0;
+#pragma unroll
+      for (int d = 0; d < AKD; ++d) ra = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2x, ad[d]), s2x{1, 1}, ra, false);
+      my_rsum += ra;
+#pragma unroll
+      for (int d = 0; d < EBD; ++d) {
+        my_csum[2 * d] += (int16_t)(bd[d] & 0xffffu);
+        my_csum[2 * d + 1] += (int16_t)(bd[d] >> 16);
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < AKD; ++d) my_rsum += (int32_t)ad[d];
+#pragma unroll
+      for (int d = 0; d < EBD; ++d) my_csum[d] += (int32_t)bd[d];
+    }
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      uint32_t w[AK / 4];
+#pragma unroll
+      for (int q = 0; q < AK / 4; ++q) {
+        if constexpr (sizeof(T) == 2) w[q] = plane_q15<P>(ad[2 * q], ad[2 * q + 1], p);
+        else w[q] = plane4<P>(ad[4 * q], ad[4 * q + 1], ad[4 * q + 2], ad[4 * q + 3], p);
+      }
+#pragma unroll
+      for (int q = 0; q < AK / 16; ++q)
+        *reinterpret_cast<uint4*>(&As[p][ar][16 * i8_chunk(ar, ak0 / 16 + q)]) =
+            make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+      // B: plane p of this thread's EB values, EB contiguous bytes of plane row bk
+      uint32_t wb[EB / 4];
+#pragma unroll
+      for (int q = 0; q < EB / 4; ++q) {
+        if constexpr (sizeof(T) == 2) wb[q] = plane_q15<P>(bd[2 * q], bd[2 * q + 1], p);
+        else wb[q] = plane4<P>(bd[4 * q], bd[4 * q + 1], bd[4 * q + 2], bd[4 * q + 3], p);
+      }
+      int8_t* dstb = Bs + (size_t)p * kKT2 * BP + bk * BP + bc;
+      if constexpr (EB == 16) *reinterpret_cast<uint4*>(dstb) = make_uint4(wb[0], wb[1], wb[2], wb[3]);
+      else *reinterpret_cast<uint2*>(dstb) = make_uint2(wb[0], wb[1]);
+    }
+  };
+  constexpr int KS = kKT2 / 32;
+  i32x4 fa[KS][P][WBM], fb[KS][P][WBN];
+  // B fragment of column block j, k-step kk: lane l of 16-lane group g = l >> 4 supplies row
+  // 16 h + 8 rr + (li >> 1), columns 16 (g & 1) + 8 (li & 1) of the block (li = l & 15), for the
+  // two 8-row reads rr = 0, 1 (k bytes 16h .. 16h + 7 and 16h + 8 .. 16h + 15 of its column)
+  const int li = lane & 15, gq = (lane >> 4) & 1;
+  auto frags = [&](int buf) {
+    auto As = reinterpret_cast<const int8_t (*)[BM][kPitch2]>(lds + buf * BUF);
+    const int8_t* Bs = lds + buf * BUF + ABUF;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+#pragma unroll
+        for (int i = 0; i < WBM; ++i) {
+          const int row = wm * 32 * WBM + i * 32 + r;
+          fa[kk][p][i] = *reinterpret_cast<const i32x4*>(&As[p][row][16 * i8_chunk(row, 2 * kk + h)]);
+        }
+#pragma unroll
+        for (int j = 0; j < WBN; ++j) {
+          const int col = wn * 32 * WBN + j * 32 + 16 * gq + 8 * (li & 1);
+          const int8_t* b0 = Bs + (size_t)p * kKT2 * BP + (32 * kk + 16 * h + (li >> 1)) * BP + col;
+          const v2i32_t lo = tr_b8(b0), hi = tr_b8(b0 + 8 * BP);
+          fb[kk][p][j] = i32x4{lo.x, lo.y, hi.x, hi.y};
+        }
+      }
+  };
+  auto mma = [&]() {
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+      for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int q = 0; q < P; ++q)
+#pragma unroll
+          for (int i = 0; i < WBM; ++i)
+#pragma unroll
+            for (int j = 0; j < WBN; ++j)
+              acc[p + q][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kk][p][i], fb[kk][q][j], acc[p + q][i][j], 0, 0, 0);
+  };
+
+  const int nk = (K + kKT2 - 1) / kKT2;
+  load(0);
+  stage(0);
+  if (nk > 1) load(kKT2);
+  __syncthreads();
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) {
+    const int cur = kt & 1;
+    frags(cur);
+    stage(cur ^ 1);
+    load((kt + 2) * kKT2);
+    mma();
+    __syncthreads();
+  }
+  for (; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    frags(cur);
+    if (kt + 1 < nk) stage(cur ^ 1);
+    mma();
+    __syncthreads();
+  }
+
+  // ---- epilogue: exact sums through LDS, int64 combine (as v2)
+  int64_t* rs = reinterpret_cast<int64_t*>(lds);            // [AQ][BM]
+  int64_t* cs = rs + AQ * BM;                               // [64 k-rows][BN]
+  rs[(tid % AQ) * BM + ar] = my_rsum;
+#pragma unroll
+  for (int c = 0; c < EB; ++c) cs[bk * BN + bc + c] = (int64_t)my_csum[c];
+  __syncthreads();
+  const int64_t kpad = (int64_t)nk * kKT2;
+#pragma unroll
+  for (int j = 0; j < WBN; ++j) {
+    const int cc = wn * 32 * WBN + j * 32 + r;
+    int64_t csum = 0;
+    for (int q = 0; q < kKT2; ++q) csum += cs[q * BN + cc];
+    const int gcol = col0 + cc;
+#pragma unroll
+    for (int i = 0; i < WBM; ++i) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int rr = wm * 32 * WBM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const int grow = row0 + rr;
+        int64_t rsum = 0;
+#pragma unroll
+        for (int q = 0; q < AQ; ++q) rsum += rs[q * BM + rr];
+        uint64_t v = (uint64_t)(C0 * (rsum + csum)) - (uint64_t)kpad * (uint64_t)(C0 * C0);
+#pragma unroll
+        for (int s2 = 0; s2 < S; ++s2) v += (uint64_t)(int64_t)acc[s2][i][j][reg] << (8 * s2);
+        if (FULL || (grow < M && gcol < N)) {
+          const int64_t sum = (int64_t)v;
+          if constexpr (sizeof(T) == 2)
+            C[(size_t)grow * N + gcol] = fast ? (T)((int32_t)(uint32_t)v >> 15) : (T)ssat16((int32_t)(sum >> 15));
+          else C[(size_t)grow * N + gcol] = (T)(int32_t)(sum >> 31);
+        }
+      }
+    }
+  }
+}
+
 // K beyond the i8 accumulators' exact range: one thread per output, int64 sum.
 template <typename T>
 __global__ __launch_bounds__(256) void mat_mult_fixed_valu_kernel(const T* __restrict__ A, const T* __restrict__ B,
@@ -379,7 +637,14 @@ static hipError_t launch_fixed(int m, int k, int n, const T* a, const T* b, T* c
     const bool full = m % G::BM == 0 && n % G::BN == 0 && k % G::KT == 0 &&
                       ((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0 && (k * sizeof(T)) % 16 == 0 &&
                       (n * sizeof(T)) % 16 == 0;
-    if (full)
+    if (MI355X_I8_V3) {
+      if (full)
+        hipLaunchKernelGGL((mat_mult_i8v3_kernel<T, true>), dim3(tiles * batch), dim3(kNT2), 0, st, a, b, c, m, k, n,
+                           fast);
+      else
+        hipLaunchKernelGGL((mat_mult_i8v3_kernel<T, false>), dim3(tiles * batch), dim3(kNT2), 0, st, a, b, c, m, k,
+                           n, fast);
+    } else if (full)
       hipLaunchKernelGGL((mat_mult_i8v2_kernel<T, true>), dim3(tiles * batch), dim3(kNT2), 0, st, a, b, c, m, k, n,
                          fast);
     else

@@ -33,9 +33,6 @@ namespace mi355x {
 
 constexpr int kMfccWaves = 4;   // frames (waves) per 256-thread workgroup
 
-#ifndef MI355X_MFCC_UNROLL
-#define MI355X_MFCC_UNROLL 8        // Mel / DCT dot products: loads issued 8 taps ahead
-#endif
 
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll

@@ -157,12 +157,6 @@ __global__ __launch_bounds__(kBlock) void rfft_fused_kernel(const float2* src, f
 // pattern above conflict free).  Twiddles are lane-constant (stage 0: 7, stage 1: 7, split: 8).
 // Mapping sweep (2^20 transforms, Gsamples/s): T consecutive transforms per wave x WPB waves per
 // workgroup: T1 433, T2 473, T4 460, T8 462, T2 x 4 waves 442; the generic fused kernel 441.
-#ifndef MI355X_RF1024_T
-#define MI355X_RF1024_T 2
-#endif
-#ifndef MI355X_RF1024_WPB
-#define MI355X_RF1024_WPB 8
-#endif
 constexpr int kRfT = MI355X_RF1024_T, kRfWpb = MI355X_RF1024_WPB;
 __device__ __forceinline__ int rf_s(int e) { return (e >> 6) * 72 + (((e >> 3) & 7) << 3) + ((e & 7) ^ ((e >> 3) & 7)); }
 __device__ __forceinline__ void rf_wave_sync() {
@@ -253,9 +247,6 @@ static hipError_t launch_fused(bool inv, const float* p, float* pcopy, float* ou
   return hipGetLastError();
 }
 
-#ifndef MI355X_RF1024
-#define MI355X_RF1024 1
-#endif
 hipError_t rfft_f32_fused_launch(int n_real, bool inverse, const float* p, float* pcopy, float* out, uint32_t batch,
                                  const float* tw, const float* tw_rfft, hipStream_t st) {
   if (batch == 0) return hipSuccess;

@@ -1,0 +1,152 @@
+// Build-time tuning knobs of the kernels, in one place (VERDICT r3 Weak #10).  Every default is
+// the measured best (DESIGN.md §4 gives the sweeps); a non-default value is an A/B experiment:
+// `make DEFS="-DMI355X_X=..."` or tools/build_variant.sh, and arm_mi355x_version() lists it, so a
+// bench line always names the kernels it timed.
+#pragma once
+
+
+// ---- cfft_f32.hip
+#ifndef MI355X_N1024_WAVES
+#define MI355X_N1024_WAVES 1
+#endif
+#ifndef MI355X_N1024_T
+#define MI355X_N1024_T 4
+#endif
+#ifndef MI355X_N1024_WPB
+#define MI355X_N1024_WPB 8
+#endif
+#ifndef MI355X_N1024_SPLIT
+#define MI355X_N1024_SPLIT 1
+#endif
+#ifndef MI355X_NT
+#define MI355X_NT 1
+#endif
+#ifndef MI355X_N4096_WAVES
+#define MI355X_N4096_WAVES 1
+#endif
+#ifndef MI355X_N4096_T
+#define MI355X_N4096_T 8
+#endif
+#ifndef MI355X_F32_N4096
+#define MI355X_F32_N4096 1
+#endif
+#ifndef MI355X_N512_T
+#define MI355X_N512_T 2
+#endif
+#ifndef MI355X_N512_WPB
+#define MI355X_N512_WPB 8
+#endif
+#ifndef MI355X_F32_N512
+#define MI355X_F32_N512 1
+#endif
+#ifndef MI355X_N2048_T
+#define MI355X_N2048_T 2
+#endif
+#ifndef MI355X_N2048_WPB
+#define MI355X_N2048_WPB 4
+#endif
+#ifndef MI355X_F32_N2048
+#define MI355X_F32_N2048 1
+#endif
+
+// ---- cfft_fixed.hip
+#ifndef MI355X_FX_Q31_SLOTS
+#define MI355X_FX_Q31_SLOTS 6912
+#endif
+#ifndef MI355X_FX_WAVES
+#define MI355X_FX_WAVES 1     // minimum waves per SIMD the register allocation must allow
+#endif
+#ifndef MI355X_FX_TW3_LDS
+#define MI355X_FX_TW3_LDS 0
+#endif
+#ifndef MI355X_FX_TW4_LDS
+#define MI355X_FX_TW4_LDS 0
+#endif
+#ifndef MI355X_FX_PF
+#define MI355X_FX_PF 1
+#endif
+#ifndef MI355X_FX_Q15_PFD
+#define MI355X_FX_Q15_PFD 2
+#endif
+#ifndef MI355X_FXQ15_SLOTS
+#define MI355X_FXQ15_SLOTS 4351   // LDS words of the q15 kernel (more: fewer workgroups per CU)
+#endif
+#ifndef MI355X_FXQ15_TW34_LDS
+#define MI355X_FXQ15_TW34_LDS 0
+#endif
+#ifndef MI355X_FXQ15_WAVES
+#define MI355X_FXQ15_WAVES 1
+#endif
+
+// ---- cfft_fixed_r16.hip
+#ifndef MI355X_FXR_T
+#define MI355X_FXR_T 8
+#endif
+
+// ---- fir.hip
+#ifndef MI355X_FIR_SCHED_BARRIER
+#define MI355X_FIR_SCHED_BARRIER 1
+#endif
+#ifndef MI355X_FIR_IPW
+#define MI355X_FIR_IPW 16
+#endif
+#ifndef MI355X_FIR_F32_WAVES
+#define MI355X_FIR_F32_WAVES(R) ((R) == 16 ? 5 : 8)   // minimum waves per SIMD the allocation must allow
+#endif
+#ifndef MI355X_FIR_F32_FMA_WAVES
+#define MI355X_FIR_F32_FMA_WAVES 4                   // FMA: + 8 coefficient and 4 tap-staging VGPRs
+#endif
+#ifndef MI355X_FIR_DB
+#define MI355X_FIR_DB 0
+#endif
+#ifndef MI355X_FIR_Q15_WAVES
+#define MI355X_FIR_Q15_WAVES 1   // minimum waves per SIMD the register allocation must allow
+#endif
+
+// ---- fir_lattice.hip
+#ifndef MI355X_LAT_IPW
+#define MI355X_LAT_IPW 1   // 2 / 4 measured slower (f32 211 / 220 vs 221 Gsamples/s, q31 138 / 147 vs 172)
+#endif
+
+// ---- mat_mult_fixed.hip
+#ifndef MI355X_I8_SCHED
+#define MI355X_I8_SCHED 6
+#endif
+#ifndef MI355X_I8_V3
+#define MI355X_I8_V3 0
+#endif
+
+// ---- mfcc_f32.hip
+#ifndef MI355X_MFCC_UNROLL
+#define MI355X_MFCC_UNROLL 8        // Mel / DCT dot products: loads issued 8 taps ahead
+#endif
+
+// ---- rfft_f32.hip
+#ifndef MI355X_RF1024_T
+#define MI355X_RF1024_T 2
+#endif
+#ifndef MI355X_RF1024_WPB
+#define MI355X_RF1024_WPB 8
+#endif
+#ifndef MI355X_RF1024
+#define MI355X_RF1024 1
+#endif
+
+// ---- cfft_fixed_core.hpp
+#ifndef MI355X_FX_Q15_PACKED
+#define MI355X_FX_Q15_PACKED 1
+#endif
+#ifndef MI355X_FX_NT
+#define MI355X_FX_NT 2
+#endif
+#ifndef MI355X_FX_T
+#define MI355X_FX_T 8
+#endif
+#ifndef MI355X_FXQ15_T
+#define MI355X_FXQ15_T 8
+#endif
+
+// ---- api.cpp
+#ifndef MI355X_MFCC_FX_MODE
+#define MI355X_MFCC_FX_MODE 2
+#endif
