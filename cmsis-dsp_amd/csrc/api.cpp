@@ -437,12 +437,13 @@ bool mfcc_fx_prepare(const Inst* S, MfccFxDev<T>& d) {
 
 // x: [batch][n] frames (overwritten), y: [batch][2n] spectra, dst: [batch][nbDct]; the frame
 // maxima ride in dst[frame][0] between the launches (read before the row is written)
-// MFCC q31 / q15 schedule (fftLen 512..4096 with the reference's own CFFT bit reversal):
-// 2 = one launch (round 4: front end, radix-16 CFFT and back end in one kernel, the spectra
-// never leave LDS), 1 = two launches (front end fused into the CFFT's load phase, then the post
-// kernel), 0 = three launches (pre, CFFT, post: also every other length and custom bit-reversal
-// tables).  The round-3 one-launch kernel (generic LDS-stage CFFT, frames resident in LDS) was
-// slower than the two-launch schedule and was removed (DESIGN.md §4 mfcc_q31 / mfcc_q15).
+// MFCC q31 / q15 schedule (MI355X_MFCC_FX_MODE, tuning.hpp; fftLen 512..4096 with the reference's
+// own CFFT bit reversal): 1 = two launches (default: front end fused into the radix-16 CFFT's load
+// phase, then the post kernel), 2 = one launch (round 4: front end, radix-16 CFFT and back end in
+// one kernel, the spectra never leave LDS: traffic = the frames once, but 1.30 / 1.09 ms against
+// 1.02 / 0.83 ms per 2^18 frames -- the CFFT and back-end phases of a workgroup serialise at two
+// workgroups per CU), 0 = three launches (pre, CFFT, post: also every other length
+// and custom bit-reversal tables).
 template <typename T, typename Inst>
 bool mfcc_fx_run(const Inst* S, const MfccFxDev<T>& d, T* x, T* y, T* dst, uint32_t batch, hipStream_t st) {
   const int n = (int)S->fftLen, nd = (int)S->nbDctOutputs, nm = (int)S->nbMelFilters;

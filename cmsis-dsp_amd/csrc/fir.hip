@@ -296,19 +296,17 @@ __device__ __forceinline__ FirUnit fir_unit(uint32_t u, uint32_t nseg, uint32_t 
   x.last = !LONG || seg == (int)nseg - 1;
   return x;
 }
-// DB (round 4): two LDS window images.  The next unit's window is written to
-// the other image right after the one barrier of a unit, while the current image is read by the
-// MACs, so a unit costs one __syncthreads instead of two and no wave waits for the others'
-// MACs before the staging writes (not for LONG / FMA units).
-template <int R, int KPRE, bool LONG, bool FMA, bool DB = false>
+// (Round 4 measured a double-buffered-window variant -- two LDS images, one barrier per item,
+// VERDICT r3 item 7 -- at 212.7 vs 215-216 Gsamples/s for this kernel on the same box, bit-exact:
+// at three workgroups per CU instead of five the staging it overlaps is worth less than the
+// occupancy it costs; not kept.  profiles/r04/README.md.)
+template <int R, int KPRE, bool LONG, bool FMA>
 __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32_FMA_WAVES : MI355X_FIR_F32_WAVES(R)) void fir_f32_kernel(
     const float* __restrict__ coeffs, int T, const float* __restrict__ src, float* __restrict__ dst, uint32_t B,
     const float* __restrict__ hist_in, uint32_t nchunks, uint32_t items, uint32_t ipw, FirIn in, FirOut fo) {
   static_assert(R == 16 || (R == 8 && !FMA), "R = 16, or R = 8 for the bit-exact path");
-  static_assert(!DB || (!LONG && !FMA), "double-buffered windows: short bit-exact filters");
   constexpr int kWin = KPRE * kBlock;
-  constexpr int kImg = wpos<R>(kWin) + 32;          // words per window image
-  __shared__ __attribute__((aligned(16))) float win[(DB ? 2 : 1) * kImg];
+  __shared__ __attribute__((aligned(16))) float win[wpos<R>(kWin) + 32];
   __shared__ __attribute__((aligned(16))) float cl[FMA ? kFirSeg + 64 : 4];   // FMA: the unit's taps (+ read-ahead)
   const int T1 = T - 1;
   const uint32_t i0 = blockIdx.x * ipw;
@@ -318,12 +316,26 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
   const int tid = threadIdx.x;
   const int base = tid * R;                         // local output index of this lane
   const int jl = fir_stage_lane(tid);               // the row sample this thread stages
+  float* wl = win + wpos<R>(jl);                       // wpos(jl + 256 k) = wpos(jl) + 320 k
   F32Win<R, KPRE, LONG> pre;
   F32Coef pc;
+  FirUnit cur = fir_unit<R, LONG>(u0, nseg, nchunks, B, T);
+  fir_f32_fetch<R, KPRE, LONG>(pre, cur.it, src, hist_in, in, T1, jl);
+  fir_f32_put<R, KPRE, LONG>(wl, pre);
+  if constexpr (FMA) {
+    fir_f32_cfetch(pc, coeffs, cur.it, in, cur.Ts, tid);
+    fir_f32_cput(cl, pc, tid);
+  }
   float acc[R];
-
-  // the MACs of unit `cur` from window image wimg
-  auto macs = [&](const FirUnit& cur, const float* wimg) {
+  // Per unit: barrier (window ready) -> next window's loads -> MACs -> barrier (window free)
+  // -> next window to LDS -> output stores.  The window write waits only for loads that had a
+  // whole unit of MACs to land; the stores are issued after it, so no wait ever covers them.
+  for (uint32_t u = u0;;) {
+    __syncthreads();
+    const bool more = u + 1 < u1;
+    const FirUnit nxt = more ? fir_unit<R, LONG>(u + 1, nseg, nchunks, B, T) : cur;
+    if (more) fir_f32_fetch<R, KPRE, LONG>(pre, nxt.it, src, hist_in, in, T1, jl);
+    if (FMA && more) fir_f32_cfetch(pc, coeffs, nxt.it, in, nxt.Ts, tid);
     if (base < cur.it.count) {
       if (cur.first) {
 #pragma unroll
@@ -338,25 +350,25 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
       int g = base >> 3;                            // the lane's first group
       const float* const ci = coeffs + cur.it.f * in.cstride + cur.it.a;
       const float* cp = FMA ? cl : ci;
-      ld_grp<R>(X0, wimg, g);
-      ld_grp<R>(X1, wimg, g + 1);
-      if constexpr (R == 16) ld_grp<R>(X2, wimg, g + 2);
+      ld_grp<R>(X0, win, g);
+      ld_grp<R>(X1, win, g + 1);
+      if constexpr (R == 16) ld_grp<R>(X2, win, g + 2);
       int nb = rounds >> 2;
       if constexpr (FMA && R == 16) {
-        f32_rounds_ldsc<FMA>(acc, wimg, g, cp, rounds);
+        f32_rounds_ldsc<FMA>(acc, win, g, cp, rounds);
       } else {
       if (nb > 0) {
         do {
           if constexpr (R == 8) {
-            ld_coef(c0, cp, 0);  ld_grp<R>(X2, wimg, g + 2); f32_round<R, FMA>(acc, X0, X1, X1, c0);
-            ld_coef(c1, cp, 8);  ld_grp<R>(X3, wimg, g + 3); f32_round<R, FMA>(acc, X1, X2, X2, c1);
-            ld_coef(c0, cp, 16); ld_grp<R>(X0, wimg, g + 4); f32_round<R, FMA>(acc, X2, X3, X3, c0);
-            ld_coef(c1, cp, 24); ld_grp<R>(X1, wimg, g + 5); f32_round<R, FMA>(acc, X3, X0, X0, c1);
+            ld_coef(c0, cp, 0);  ld_grp<R>(X2, win, g + 2); f32_round<R, FMA>(acc, X0, X1, X1, c0);
+            ld_coef(c1, cp, 8);  ld_grp<R>(X3, win, g + 3); f32_round<R, FMA>(acc, X1, X2, X2, c1);
+            ld_coef(c0, cp, 16); ld_grp<R>(X0, win, g + 4); f32_round<R, FMA>(acc, X2, X3, X3, c0);
+            ld_coef(c1, cp, 24); ld_grp<R>(X1, win, g + 5); f32_round<R, FMA>(acc, X3, X0, X0, c1);
           } else {
-            ld_coef(c0, cp, 0);  ld_grp<R>(X3, wimg, g + 3); f32_round<R, FMA>(acc, X0, X1, X2, c0);
-            ld_coef(c1, cp, 8);  ld_grp<R>(X0, wimg, g + 4); f32_round<R, FMA>(acc, X1, X2, X3, c1);
-            ld_coef(c0, cp, 16); ld_grp<R>(X1, wimg, g + 5); f32_round<R, FMA>(acc, X2, X3, X0, c0);
-            ld_coef(c1, cp, 24); ld_grp<R>(X2, wimg, g + 6); f32_round<R, FMA>(acc, X3, X0, X1, c1);
+            ld_coef(c0, cp, 0);  ld_grp<R>(X3, win, g + 3); f32_round<R, FMA>(acc, X0, X1, X2, c0);
+            ld_coef(c1, cp, 8);  ld_grp<R>(X0, win, g + 4); f32_round<R, FMA>(acc, X1, X2, X3, c1);
+            ld_coef(c0, cp, 16); ld_grp<R>(X1, win, g + 5); f32_round<R, FMA>(acc, X2, X3, X0, c0);
+            ld_coef(c1, cp, 24); ld_grp<R>(X2, win, g + 6); f32_round<R, FMA>(acc, X3, X0, X1, c1);
           }
           g += 4;
           cp += 32;
@@ -367,11 +379,11 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
       if (rem > 0) {
         if constexpr (R == 8) {
           ld_coef(c0, cp, 0);
-          ld_grp<R>(X2, wimg, g + 2);
+          ld_grp<R>(X2, win, g + 2);
           f32_round<R, FMA>(acc, X0, X1, X1, c0);
           if (rem > 1) {
             ld_coef(c1, cp, 8);
-            ld_grp<R>(X3, wimg, g + 3);
+            ld_grp<R>(X3, win, g + 3);
             f32_round<R, FMA>(acc, X1, X2, X2, c1);
             if (rem > 2) {
               ld_coef(c0, cp, 16);
@@ -380,11 +392,11 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
           }
         } else {
           ld_coef(c0, cp, 0);
-          ld_grp<R>(X3, wimg, g + 3);
+          ld_grp<R>(X3, win, g + 3);
           f32_round<R, FMA>(acc, X0, X1, X2, c0);
           if (rem > 1) {
             ld_coef(c1, cp, 8);
-            ld_grp<R>(X0, wimg, g + 4);
+            ld_grp<R>(X0, win, g + 4);
             f32_round<R, FMA>(acc, X1, X2, X3, c1);
             if (rem > 2) {
               ld_coef(c0, cp, 16);
@@ -398,12 +410,14 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
       for (int k = 8 * rounds; k < Ts; ++k) {
         const float c = ci[k];
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = f32_mac<FMA>(acc[r], wimg[wpos<R>(base + k + r)], c);
+        for (int r = 0; r < R; ++r) acc[r] = f32_mac<FMA>(acc[r], win[wpos<R>(base + k + r)], c);
       }
     }
-  };
-  // the outputs of unit `cur` (its last tap segment)
-  auto store = [&](const FirUnit& cur) {
+    if (more) {
+      __syncthreads();                              // every wave is done reading this window
+      fir_f32_put<R, KPRE, LONG>(wl, pre);
+      if constexpr (FMA) fir_f32_cput(cl, pc, tid);
+    }
     if (cur.last && base < cur.it.count) {
       const FirItem& it = cur.it;
       const bool run = fo.M == 1 && fo.L == 1 && fo.dir == 1;
@@ -428,55 +442,6 @@ __global__ __launch_bounds__(kBlock, LONG ? (FMA ? 3 : 4) : FMA ? MI355X_FIR_F32
         }
       }
     }
-  };
-
-  FirUnit cur = fir_unit<R, LONG>(u0, nseg, nchunks, B, T);
-  fir_f32_fetch<R, KPRE, LONG>(pre, cur.it, src, hist_in, in, T1, jl);
-  fir_f32_put<R, KPRE, LONG>(win + wpos<R>(jl), pre);
-  if constexpr (FMA) {
-    fir_f32_cfetch(pc, coeffs, cur.it, in, cur.Ts, tid);
-    fir_f32_cput(cl, pc, tid);
-  }
-  if constexpr (DB) {
-    // Per unit: barrier (image b holds this unit's window; every wave has left image b ^ 1)
-    // -> the next unit's window (loaded one unit ago) to image b ^ 1 -> the unit after next's
-    // loads -> MACs on image b -> stores.
-    bool more = u0 + 1 < u1;
-    if (more) fir_f32_fetch<R, KPRE, LONG>(pre, fir_unit<R, LONG>(u0 + 1, nseg, nchunks, B, T).it, src, hist_in, in, T1, jl);
-    int b = 0;
-    for (uint32_t u = u0;;) {
-      __syncthreads();
-      if (more) {
-        fir_f32_put<R, KPRE, LONG>(win + (b ^ 1) * kImg + wpos<R>(jl), pre);
-        if (u + 2 < u1)
-          fir_f32_fetch<R, KPRE, LONG>(pre, fir_unit<R, LONG>(u + 2, nseg, nchunks, B, T).it, src, hist_in, in, T1, jl);
-      }
-      macs(cur, win + b * kImg);
-      store(cur);
-      if (!more) break;
-      ++u;
-      cur = fir_unit<R, LONG>(u, nseg, nchunks, B, T);
-      more = u + 1 < u1;
-      b ^= 1;
-    }
-    return;
-  }
-  // Per unit: barrier (window ready) -> next window's loads -> MACs -> barrier (window free)
-  // -> next window to LDS -> output stores.  The window write waits only for loads that had a
-  // whole unit of MACs to land; the stores are issued after it, so no wait ever covers them.
-  for (uint32_t u = u0;;) {
-    __syncthreads();
-    const bool more = u + 1 < u1;
-    const FirUnit nxt = more ? fir_unit<R, LONG>(u + 1, nseg, nchunks, B, T) : cur;
-    if (more) fir_f32_fetch<R, KPRE, LONG>(pre, nxt.it, src, hist_in, in, T1, jl);
-    if (FMA && more) fir_f32_cfetch(pc, coeffs, nxt.it, in, nxt.Ts, tid);
-    macs(cur, win);
-    if (more) {
-      __syncthreads();                              // every wave is done reading this window
-      fir_f32_put<R, KPRE, LONG>(win + wpos<R>(jl), pre);
-      if constexpr (FMA) fir_f32_cput(cl, pc, tid);
-    }
-    store(cur);
     if (!more) break;
     cur = nxt;
     ++u;
@@ -1015,13 +980,16 @@ static void fir_f32_launch(const float* coeffs, int T, const float* src, float* 
   const int kpre = fir_f32_kpre<R>(T < kFirSeg ? T : kFirSeg);
   constexpr int K0 = fir_f32_kpre<R>(1), KL = fir_f32_kpre<R>(kFirSeg);     // 9..13 (R = 8), 17..21 (R = 16)
   static_assert(KL - K0 == 4, "five window sizes");
-  constexpr bool DB = MI355X_FIR_DB && !F;
   auto k = T > kFirSeg ? fir_f32_kernel<R, KL, true, F>
-         : kpre <= K0 ? fir_f32_kernel<R, K0, false, F, DB> : kpre == K0 + 1 ? fir_f32_kernel<R, K0 + 1, false, F, DB>
-         : kpre == K0 + 2 ? fir_f32_kernel<R, K0 + 2, false, F, DB> : kpre == K0 + 3 ? fir_f32_kernel<R, K0 + 3, false, F, DB>
-         : fir_f32_kernel<R, KL, false, F, DB>;
+         : kpre <= K0 ? fir_f32_kernel<R, K0, false, F> : kpre == K0 + 1 ? fir_f32_kernel<R, K0 + 1, false, F>
+         : kpre == K0 + 2 ? fir_f32_kernel<R, K0 + 2, false, F> : kpre == K0 + 3 ? fir_f32_kernel<R, K0 + 3, false, F>
+         : fir_f32_kernel<R, KL, false, F>;
   uint32_t ipw = MI355X_FIR_IPW;
   if (T > kFirSeg) ipw = 1;                         // a long item is already many units
+  // few items (short blocks of a small batch): one item per workgroup, or the ipw items of a
+  // single workgroup would run one after the other (round 4: 16 filters x 32 samples took 63 us
+  // in one workgroup, profiles/r04/probes/breakeven.json)
+  if (ipw > 1 && items < 256u * 16u * ipw) ipw = max(1u, items / (256u * 16u));
   if (!ipw) {
     const uint32_t resident = (uint32_t)persistent_grid((const void*)k, kBlock, 0, items);
     ipw = (items + resident - 1) / resident;

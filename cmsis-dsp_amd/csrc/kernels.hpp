@@ -37,6 +37,10 @@ bool cfft_q31_r16_launch(int n, int32_t* data, uint32_t batch, const int32_t* tw
 bool cfft_q15_r16_launch(int n, int16_t* data, uint32_t batch, const int16_t* tw, uint32_t flags, hipStream_t st);
 // The same kernels with the MFCC front end fused into their load phase (PRE): forward, frame
 // maxima to maxv[frame * mstride]; false when n is not 256..2048.
+// Stores v into *dflag (a device-mapped coherent host word) after the stream's earlier work
+// (sync.hip): the drop-in calls' completion signal.
+hipError_t done_flag_launch(uint32_t* dflag, uint32_t v, hipStream_t st);
+
 // The whole MFCC q31 / q15 in one launch (front end + CFFT + back end, cfft_fixed_r16.hip);
 // n = fftLen / 2.  hipErrorNotSupported: not handled (take the two-launch schedule).
 hipError_t mfcc_q31_fused_launch(int n, const int32_t* frames, uint32_t batch, const int32_t* tw, const int32_t* win,

@@ -1,6 +1,8 @@
 // Host runtime: device table cache, staging scratch, error channel.
 #include "runtime.hpp"
 
+#include "kernels.hpp"
+
 #include <dlfcn.h>
 #include <stdlib.h>
 #include <link.h>
@@ -17,7 +19,7 @@
 #include "../../include/arm_math_mi355x.h"
 
 #ifndef MI355X_SYNC_DEFAULT
-#define MI355X_SYNC_DEFAULT 0
+#define MI355X_SYNC_DEFAULT 1
 #endif
 
 namespace mi355x {
@@ -502,10 +504,11 @@ HostIO::~HostIO() {
   if ((slot_ > 0 || zslot_ > 0) && !finished_) (void)hipStreamSynchronize(st_);
 }
 
-// Completion of a synchronous drop-in call.  kSyncSpin: a stream write of a
-// per-thread sequence number into a coherent, device-mapped host word after the call's work, and
-// the host spins on that word (bounded; then hipStreamSynchronize, which also reports errors)
-// instead of the runtime's blocking wait.  CMSISDSP_MI355X_SYNC=sync|spin overrides the default.
+// Completion of a synchronous drop-in call.  Spin mode (default): a one-lane
+// kernel after the call's work stores a per-thread sequence number into a coherent,
+// device-mapped host word (sync.hip), and the host spins on that word (bounded; then
+// hipStreamSynchronize, which also reports errors) instead of the runtime's blocking wait.
+// CMSISDSP_MI355X_SYNC=sync|spin overrides the default (MI355X_SYNC_DEFAULT).
 namespace {
 struct DoneWord { volatile uint32_t* h = nullptr; uint32_t* d = nullptr; uint32_t seq = 0; };
 thread_local std::map<int, DoneWord> t_done;
@@ -539,7 +542,7 @@ hipError_t wait_stream(hipStream_t st) {
     }
     if (w.h) {
       const uint32_t v = ++w.seq;
-      if (hipStreamWriteValue32(st, w.d, v, 0) == hipSuccess) {
+      if (done_flag_launch(w.d, v, st) == hipSuccess) {
         // spin up to ~2^22 polls (milliseconds); a slow or failed call falls through to the sync
         for (uint32_t i = 0; i < (1u << 22); ++i)
           if (__atomic_load_n(w.h, __ATOMIC_ACQUIRE) == v) return hipSuccess;

@@ -96,9 +96,6 @@
 #ifndef MI355X_FIR_F32_FMA_WAVES
 #define MI355X_FIR_F32_FMA_WAVES 4                   // FMA: + 8 coefficient and 4 tap-staging VGPRs
 #endif
-#ifndef MI355X_FIR_DB
-#define MI355X_FIR_DB 0
-#endif
 #ifndef MI355X_FIR_Q15_WAVES
 #define MI355X_FIR_Q15_WAVES 1   // minimum waves per SIMD the register allocation must allow
 #endif
@@ -148,5 +145,5 @@
 
 // ---- api.cpp
 #ifndef MI355X_MFCC_FX_MODE
-#define MI355X_MFCC_FX_MODE 2
+#define MI355X_MFCC_FX_MODE 1
 #endif
