@@ -541,6 +541,7 @@ void fir_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B, int kind) {
     memmove(zs + T1, pSrc, sb);                   // pSrc may alias pDst: read before anything
     hipError_t e = fir_run(kind, dc, taps, zs + T1, zd, B, 1, zs, st);
     if (e == hipSuccess) e = io.finish();
+    if (e == hipSuccess) hold.synced();
     if (e != hipSuccess) set_error(e, "arm_fir");
     return;
   }
@@ -567,6 +568,7 @@ void fir_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B, int kind) {
     else memcpy(S->pState + T1, pSrc, sb);     // host input, host state: the caller's words
   }
   if (e == hipSuccess) e = io.finish();
+  if (e == hipSuccess) hold.synced();
   if (e != hipSuccess) set_error(e, "arm_fir");
 }
 

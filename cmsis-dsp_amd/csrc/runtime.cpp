@@ -334,6 +334,12 @@ BlobScope::BlobScope(hipStream_t st) : st_(st), base_(t_held.size()), dev_(cur_d
 BlobScope::~BlobScope() {
   --t_scopes;
   if (t_held.size() <= base_) return;
+  if (synced_) {                            // nothing of this call is still pending
+    std::lock_guard<std::mutex> lk(g_table_mu);
+    for (size_t i = base_; i < t_held.size(); ++i) --t_held[i]->holds;
+    t_held.resize(base_);
+    return;
+  }
   // one event after everything this scope enqueued on st_, attached to every blob it held
   EvRef ev;
   {

@@ -48,6 +48,9 @@ class BlobScope {
  public:
   explicit BlobScope(hipStream_t st);
   ~BlobScope();
+  // the work this scope enqueued has completed (a synchronous call after its wait): the held
+  // blobs are released without recording an event
+  void synced() { synced_ = true; }
   BlobScope(const BlobScope&) = delete;
   BlobScope& operator=(const BlobScope&) = delete;
 
@@ -55,6 +58,7 @@ class BlobScope {
   hipStream_t st_;
   size_t base_;
   int dev_;
+  bool synced_ = false;
 };
 
 // Device permutation implementing a bit-reversal swap table of a non-canonical instance.

@@ -29,6 +29,10 @@ SPECS = {
     # two launches per step: the MFCC front end fused into the radix-16 CFFT, then post (summed)
     "mfcc_q31": ("--workload mfcc_q31 --steps 10 --warmup 3", "mfcc_q31_post|cfft_fx_r16_kernel", ""),
     "mfcc_q15": ("--workload mfcc_q15 --steps 10 --warmup 3", "mfcc_q15_post|cfft_fx_r16_kernel", ""),
+    # the one-launch schedule (variant build MI355X_MFCC_FX_MODE=2): the same bench arguments,
+    # run with CMSISDSP_MI355X_LIB=cmsis-dsp_amd/lib/variants/lib_mfcc1l.so
+    "mfcc_q31_onelaunch": ("--workload mfcc_q31 --steps 10 --warmup 3", "cfft_fx_r16_kernel", ""),
+    "mfcc_q15_onelaunch": ("--workload mfcc_q15 --steps 10 --warmup 3", "cfft_fx_r16_kernel", ""),
     "mat_mult_f32": ("--workload mat_mult_f32 --steps 6 --warmup 2", "mat_mult_f32_full", ""),
     "mat_mult_q15": ("--workload mat_mult_q15 --steps 6 --warmup 2", "mat_mult_i8v2", ""),
     "mat_mult_q31": ("--workload mat_mult_q31 --steps 6 --warmup 2", "mat_mult_i8v2", ""),
