@@ -363,6 +363,7 @@ struct MfccFxDev {
   const uint32_t* off = nullptr;
   const uint32_t* bf = nullptr;    // flat Mel coefficient g -> bin << 16 | filter
   int total = 0;
+  int kmin = 0, kcnt = 0;          // the bins some Mel filter reads: kmin .. kmin + kcnt - 1
   const int4* tw = nullptr;        // split twiddles per bin k <= fftLen/2: {A[2mk], A[2mk+1], B[2mk], B[2mk+1]}
   const int32_t* lut = nullptr;
 };
@@ -388,6 +389,13 @@ bool mfcc_fx_prepare(const Inst* S, MfccFxDev<T>& d) {
     total += len[i];
   }
   if (nm > 0xFFFFu || total > 0x7FFFFFFFull) { set_error(hipErrorInvalidValue, "mfcc: too many Mel coefficients"); return false; }
+  {
+    uint32_t lo = n, hi = 0;
+    for (uint32_t i = 0; i < nm; ++i)
+      if (len[i]) { lo = std::min(lo, pos[i]); hi = std::max(hi, pos[i] + len[i]); }
+    d.kmin = lo < hi ? (int)lo : 0;
+    d.kcnt = lo < hi ? (int)(hi - lo) : 0;
+  }
   auto up16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
   const size_t b_dct = up16(sizeof(T) * nm * nd), b_cf = up16(sizeof(T) * total), b_win = up16(sizeof(T) * n);
   const size_t b_u = up16(sizeof(uint32_t) * nm), b_bf = up16(sizeof(uint32_t) * total);
@@ -461,10 +469,10 @@ bool mfcc_fx_run(const Inst* S, const MfccFxDev<T>& d, T* x, T* y, T* dst, uint3
     hipError_t e;
     if constexpr (sizeof(T) == 4)
       e = mfcc_q31_fused_launch((int)L, x, batch, (const int32_t*)pr.tw, d.win, S->rfft.bitReverseFlagR != 0, d.tw,
-                                nm, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst, st);
+                                nm, d.coefs, d.bf, d.total, d.kmin, d.kcnt, nd, d.dct, d.lut, dst, st);
     else
       e = mfcc_q15_fused_launch((int)L, x, batch, (const int16_t*)pr.tw, d.win, S->rfft.bitReverseFlagR != 0, d.tw,
-                                nm, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst, st);
+                                nm, d.coefs, d.bf, d.total, d.kmin, d.kcnt, nd, d.dct, d.lut, dst, st);
     if (e != hipErrorNotSupported) {
       MI_CHECK(e, "mfcc fused");
       return true;
@@ -490,11 +498,11 @@ bool mfcc_fx_run(const Inst* S, const MfccFxDev<T>& d, T* x, T* y, T* dst, uint3
   }
   (void)y;
   if constexpr (sizeof(T) == 4) {
-    MI_CHECK(mfcc_q31_post_launch(n, x, d.tw, dst, nd, nm, d.pos, d.len, d.off, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst,
+    MI_CHECK(mfcc_q31_post_launch(n, x, d.tw, dst, nd, nm, d.kmin, d.kcnt, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst,
                                   batch, st),
              "mfcc q31 post");
   } else {
-    MI_CHECK(mfcc_q15_post_launch(n, x, d.tw, dst, nd, nm, d.pos, d.len, d.off, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst,
+    MI_CHECK(mfcc_q15_post_launch(n, x, d.tw, dst, nd, nm, d.kmin, d.kcnt, d.coefs, d.bf, d.total, nd, d.dct, d.lut, dst,
                                   batch, st),
              "mfcc q15 post");
   }

@@ -151,9 +151,10 @@ template <typename T> struct MqPostArgs {
   const int32_t* lut = nullptr;    // sqrt_initial_lut_q31
   T* dst = nullptr;                // [batch][nb_dct]
   int nb_mel = 0, total = 0, nb_dct = 0, stage = 0;
+  int kmin = 0, kcnt = 0;          // the bins the Mel filters read
 };
 template <typename T, int N, bool INV, bool BREV, bool SAT, bool PRE = false, bool POST = false>
-__global__ __launch_bounds__(kBlock) void cfft_fx_r16_kernel(typename R16Ops<T, INV>::C* __restrict__ data,
+__global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : 1) void cfft_fx_r16_kernel(typename R16Ops<T, INV>::C* __restrict__ data,
                                                              uint32_t batch,
                                                              const typename R16Ops<T, INV>::C* __restrict__ tw,
                                                              const typename R16Ops<T, INV>::C* __restrict__ win = nullptr,
@@ -402,8 +403,8 @@ __global__ __launch_bounds__(kBlock) void cfft_fx_r16_kernel(typename R16Ops<T, 
           const W* img = lds_all + s * PD::stride;
           auto get = [img](int i) { return O::unpack(O::from_w(img[i])); };
           if (lane == 0) mv[gn] = mvals[s];
-          mq_mel_frame<T>(op, get, pa.tw, kFrameLen, pa.nb_mel, pa.total, tb, pa.coefs, lutv, mag,
-                          acc + gn * pa.nb_mel);
+          mq_mel_frame<T>(op, get, pa.tw, kFrameLen, pa.kmin, pa.kcnt, pa.nb_mel, pa.total, tb, pa.coefs, lutv,
+                          mag, acc + gn * pa.nb_mel);
         }
         if (gn == 0) break;
         mq_finish_group(op, gn, pa.nb_mel, pa.nb_dct, acc, mv, mel, dctw, [&](int j, int r, int32_t val) {
@@ -463,7 +464,7 @@ static hipError_t launch_r16_mfcc_fused(const void* data, uint32_t batch, const 
   MqPostArgs<T> pa = pa0;
   const size_t tab = sizeof(int32_t) * (size_t)mq_tab_words(pa.total, pa.nb_mel, pa.nb_dct);
   const size_t waves = sizeof(int32_t) * 4 * (size_t)mq_wave_words(2 * N, pa.nb_mel);
-  pa.stage = waves + tab <= 32768 ? 1 : 0;
+  pa.stage = MI355X_MQF_STAGE && waves + tab <= 32768 ? 1 : 0;
   const size_t lds = waves + (pa.stage ? tab : 0);
   auto k = brev ? cfft_fx_r16_kernel<T, N, false, true, false, true, true>
                 : cfft_fx_r16_kernel<T, N, false, false, false, true, true>;
@@ -496,20 +497,20 @@ static hipError_t dispatch_r16_mfcc_fused(int n, const T* frames, uint32_t batch
 }
 hipError_t mfcc_q31_fused_launch(int n, const int32_t* frames, uint32_t batch, const int32_t* tw, const int32_t* win,
                                  bool brev, const int4* stw, int nb_mel, const int32_t* coefs, const uint32_t* bf,
-                                 int total, int nb_dct, const int32_t* dct, const int32_t* lut, int32_t* dst,
-                                 hipStream_t st) {
+                                 int total, int kmin, int kcnt, int nb_dct, const int32_t* dct, const int32_t* lut,
+                                 int32_t* dst, hipStream_t st) {
   MqPostArgs<int32_t> pa;
   pa.tw = stw; pa.coefs = coefs; pa.bf = bf; pa.dct = dct; pa.lut = lut; pa.dst = dst;
-  pa.nb_mel = nb_mel; pa.total = total; pa.nb_dct = nb_dct;
+  pa.nb_mel = nb_mel; pa.total = total; pa.nb_dct = nb_dct; pa.kmin = kmin; pa.kcnt = kcnt;
   return dispatch_r16_mfcc_fused<int32_t>(n, frames, batch, tw, win, brev, pa, st);
 }
 hipError_t mfcc_q15_fused_launch(int n, const int16_t* frames, uint32_t batch, const int16_t* tw, const int16_t* win,
                                  bool brev, const int4* stw, int nb_mel, const int16_t* coefs, const uint32_t* bf,
-                                 int total, int nb_dct, const int16_t* dct, const int32_t* lut, int16_t* dst,
-                                 hipStream_t st) {
+                                 int total, int kmin, int kcnt, int nb_dct, const int16_t* dct, const int32_t* lut,
+                                 int16_t* dst, hipStream_t st) {
   MqPostArgs<int16_t> pa;
   pa.tw = stw; pa.coefs = coefs; pa.bf = bf; pa.dct = dct; pa.lut = lut; pa.dst = dst;
-  pa.nb_mel = nb_mel; pa.total = total; pa.nb_dct = nb_dct;
+  pa.nb_mel = nb_mel; pa.total = total; pa.nb_dct = nb_dct; pa.kmin = kmin; pa.kcnt = kcnt;
   return dispatch_r16_mfcc_fused<int16_t>(n, frames, batch, tw, win, brev, pa, st);
 }
 

@@ -45,12 +45,12 @@ hipError_t done_flag_launch(uint32_t* dflag, uint32_t v, hipStream_t st);
 // n = fftLen / 2.  hipErrorNotSupported: not handled (take the two-launch schedule).
 hipError_t mfcc_q31_fused_launch(int n, const int32_t* frames, uint32_t batch, const int32_t* tw, const int32_t* win,
                                  bool brev, const int4* stw, int nb_mel, const int32_t* coefs, const uint32_t* bf,
-                                 int total, int nb_dct, const int32_t* dct, const int32_t* lut, int32_t* dst,
-                                 hipStream_t st);
+                                 int total, int kmin, int kcnt, int nb_dct, const int32_t* dct, const int32_t* lut,
+                                 int32_t* dst, hipStream_t st);
 hipError_t mfcc_q15_fused_launch(int n, const int16_t* frames, uint32_t batch, const int16_t* tw, const int16_t* win,
                                  bool brev, const int4* stw, int nb_mel, const int16_t* coefs, const uint32_t* bf,
-                                 int total, int nb_dct, const int16_t* dct, const int32_t* lut, int16_t* dst,
-                                 hipStream_t st);
+                                 int total, int kmin, int kcnt, int nb_dct, const int16_t* dct, const int32_t* lut,
+                                 int16_t* dst, hipStream_t st);
 bool cfft_q31_r16_mfcc_launch(int n, int32_t* data, uint32_t batch, const int32_t* tw, const int32_t* win,
                               int32_t* maxv, int mstride, bool brev, hipStream_t st);
 bool cfft_q15_r16_mfcc_launch(int n, int16_t* data, uint32_t batch, const int16_t* tw, const int16_t* win,
@@ -128,12 +128,12 @@ size_t mfcc_q31_post_lds(int n, int nb_mel);
 hipError_t mfcc_q15_pre_launch(int n, const int16_t* src, const int16_t* win, int16_t* x, int16_t* maxv,
                                uint32_t batch, int maxv_stride, hipStream_t st);
 hipError_t mfcc_q15_post_launch(int n, const int16_t* y, const int4* tw, const int16_t* maxv, int maxv_stride, int nb_mel,
-                                const uint32_t* pos, const uint32_t* len, const uint32_t* off, const int16_t* coefs,
+                                int kmin, int kcnt, const int16_t* coefs,
                                 const uint32_t* bf, int total, int nb_dct, const int16_t* dct, const int32_t* lut, int16_t* dst, uint32_t batch,
                                 hipStream_t st);
 
 hipError_t mfcc_q31_post_launch(int n, const int32_t* y, const int4* tw, const int32_t* maxv, int maxv_stride, int nb_mel,
-                                const uint32_t* pos, const uint32_t* len, const uint32_t* off, const int32_t* coefs,
+                                int kmin, int kcnt, const int32_t* coefs,
                                 const uint32_t* bf, int total, int nb_dct, const int32_t* dct, const int32_t* lut, int32_t* dst, uint32_t batch,
                                 hipStream_t st);
 size_t mfcc_f32_post_lds(int n, int nb_mel);

@@ -83,7 +83,7 @@ constexpr int kMqFpw = 6;   // frames per wave (two groups of 3 with the suite's
 // the group's finishes (one lane per (frame, filter)) and DCT rows (one lane per (frame, row)).
 template <typename T, typename Ops>
 __device__ __forceinline__ void mq_post_body(const Ops& op, const T* __restrict__ y, const int4* __restrict__ tw,
-                                             const T* maxv, int maxv_stride, int n, int nb_mel,
+                                             const T* maxv, int maxv_stride, int n, int kmin, int kcnt, int nb_mel,
                                              const T* __restrict__ coefs, const uint32_t* __restrict__ bf, int total,
                                              int nb_dct, const T* __restrict__ dct, const int32_t* __restrict__ lut,
                                              T* dst, uint32_t batch, int stage) {
@@ -110,7 +110,7 @@ __device__ __forceinline__ void mq_post_body(const Ops& op, const T* __restrict_
         if constexpr (sizeof(T) == 4) return reinterpret_cast<const int2*>(X)[i];
         else { const short2 v = reinterpret_cast<const short2*>(X)[i]; return make_int2(v.x, v.y); }
       };
-      mq_mel_frame<T>(op, get, tw, n, nb_mel, total, tb, coefs, lutv, mag, acc + j * nb_mel);
+      mq_mel_frame<T>(op, get, tw, n, kmin, kcnt, nb_mel, total, tb, coefs, lutv, mag, acc + j * nb_mel);
     }
     mq_finish_group(op, g, nb_mel, nb_dct, acc, mv, mel, dctw,
                     [&](int j, int r, int32_t v) { dst[(size_t)(f0 + j) * nb_dct + r] = (T)v; });
@@ -118,14 +118,14 @@ __device__ __forceinline__ void mq_post_body(const Ops& op, const T* __restrict_
 }
 
 __global__ __launch_bounds__(256) void mfcc_q31_post_kernel(const int32_t* __restrict__ y, const int4* __restrict__ tw,
-                                                            const int32_t* maxv, int maxv_stride, int n, int nb_mel,
-                                                            const int32_t* __restrict__ coefs,
+                                                            const int32_t* maxv, int maxv_stride, int n, int kmin, int kcnt,
+                                                            int nb_mel, const int32_t* __restrict__ coefs,
                                                             const uint32_t* __restrict__ bf, int total, int nb_dct,
                                                             const int32_t* __restrict__ dct,
                                                             const int32_t* __restrict__ lut, int32_t* dst,
                                                             uint32_t batch, int stage) {
-  mq_post_body<int32_t>(MqOpsQ31(n, nb_mel, nb_dct), y, tw, maxv, maxv_stride, n, nb_mel, coefs, bf, total, nb_dct, dct, lut,
-                        dst, batch, stage);
+  mq_post_body<int32_t>(MqOpsQ31(n, nb_mel, nb_dct), y, tw, maxv, maxv_stride, n, kmin, kcnt, nb_mel, coefs, bf, total, nb_dct, dct,
+                        lut, dst, batch, stage);
 }
 
 // ---------------------------------------------------------------- q15
@@ -181,14 +181,14 @@ __global__ __launch_bounds__(256) void mfcc_q15_pre_kernel(const int16_t* src, c
 }
 
 __global__ __launch_bounds__(256) void mfcc_q15_post_kernel(const int16_t* __restrict__ y, const int4* __restrict__ tw,
-                                                            const int16_t* maxv, int maxv_stride, int n, int nb_mel,
-                                                            const int16_t* __restrict__ coefs,
+                                                            const int16_t* maxv, int maxv_stride, int n, int kmin, int kcnt,
+                                                            int nb_mel, const int16_t* __restrict__ coefs,
                                                             const uint32_t* __restrict__ bf, int total, int nb_dct,
                                                             const int16_t* __restrict__ dct,
                                                             const int32_t* __restrict__ lut, int16_t* dst,
                                                             uint32_t batch, int stage) {
-  mq_post_body<int16_t>(MqOpsQ15(n, nb_mel, nb_dct), y, tw, maxv, maxv_stride, n, nb_mel, coefs, bf, total, nb_dct,
-                        dct, lut, dst, batch, stage);
+  mq_post_body<int16_t>(MqOpsQ15(n, nb_mel, nb_dct), y, tw, maxv, maxv_stride, n, kmin, kcnt, nb_mel, coefs, bf, total,
+                        nb_dct, dct, lut, dst, batch, stage);
 }
 
 hipError_t mfcc_q15_pre_launch(int n, const int16_t* src, const int16_t* win, int16_t* x, int16_t* maxv,
@@ -202,19 +202,17 @@ hipError_t mfcc_q15_pre_launch(int n, const int16_t* src, const int16_t* win, in
 }
 
 hipError_t mfcc_q15_post_launch(int n, const int16_t* y, const int4* tw, const int16_t* maxv, int maxv_stride, int nb_mel,
-                                const uint32_t* pos, const uint32_t* len, const uint32_t* off, const int16_t* coefs,
-                                const uint32_t* bf, int total, int nb_dct, const int16_t* dct, const int32_t* lut, int16_t* dst, uint32_t batch,
+                                int kmin, int kcnt, const int16_t* coefs, const uint32_t* bf, int total, int nb_dct, const int16_t* dct, const int32_t* lut, int16_t* dst, uint32_t batch,
                                 hipStream_t st) {
   if (batch == 0) return hipSuccess;
   const uint32_t grid = (batch + kMqWaves - 1) / kMqWaves;
-  (void)pos; (void)len; (void)off;
   const uint32_t grid2 = (batch + kMqFpw * kMqWaves - 1) / (kMqFpw * kMqWaves);
   const size_t tab = sizeof(int32_t) * (size_t)mq_tab_words(total, nb_mel, nb_dct);
   const int stage = mfcc_q31_post_lds(n, nb_mel) + tab <= 65536 ? 1 : 0;
   (void)grid;
   hipLaunchKernelGGL(mfcc_q15_post_kernel, dim3(grid2), dim3(64 * kMqWaves),
-                     mfcc_q31_post_lds(n, nb_mel) + (stage ? tab : 0), st, y, tw, maxv, maxv_stride, n, nb_mel, coefs,
-                     bf, total, nb_dct, dct, lut, dst, batch, stage);
+                     mfcc_q31_post_lds(n, nb_mel) + (stage ? tab : 0), st, y, tw, maxv, maxv_stride, n, kmin, kcnt, nb_mel,
+                     coefs, bf, total, nb_dct, dct, lut, dst, batch, stage);
   return hipGetLastError();
 }
 
@@ -231,19 +229,17 @@ hipError_t mfcc_q31_pre_launch(int n, const int32_t* src, const int32_t* win, in
 size_t mfcc_q31_post_lds(int n, int nb_mel) { return sizeof(int32_t) * kMqWaves * (size_t)mq_wave_words(n, nb_mel); }
 
 hipError_t mfcc_q31_post_launch(int n, const int32_t* y, const int4* tw, const int32_t* maxv, int maxv_stride, int nb_mel,
-                                const uint32_t* pos, const uint32_t* len, const uint32_t* off, const int32_t* coefs,
-                                const uint32_t* bf, int total, int nb_dct, const int32_t* dct, const int32_t* lut, int32_t* dst, uint32_t batch,
+                                int kmin, int kcnt, const int32_t* coefs, const uint32_t* bf, int total, int nb_dct, const int32_t* dct, const int32_t* lut, int32_t* dst, uint32_t batch,
                                 hipStream_t st) {
   if (batch == 0) return hipSuccess;
   const uint32_t grid = (batch + kMqWaves - 1) / kMqWaves;
-  (void)pos; (void)len; (void)off;
   const uint32_t grid2 = (batch + kMqFpw * kMqWaves - 1) / (kMqFpw * kMqWaves);
   const size_t tab = sizeof(int32_t) * (size_t)mq_tab_words(total, nb_mel, nb_dct);
   const int stage = mfcc_q31_post_lds(n, nb_mel) + tab <= 65536 ? 1 : 0;
   (void)grid;
   hipLaunchKernelGGL(mfcc_q31_post_kernel, dim3(grid2), dim3(64 * kMqWaves),
-                     mfcc_q31_post_lds(n, nb_mel) + (stage ? tab : 0), st, y, tw, maxv, maxv_stride, n, nb_mel, coefs,
-                     bf, total, nb_dct, dct, lut, dst, batch, stage);
+                     mfcc_q31_post_lds(n, nb_mel) + (stage ? tab : 0), st, y, tw, maxv, maxv_stride, n, kmin, kcnt, nb_mel,
+                     coefs, bf, total, nb_dct, dct, lut, dst, batch, stage);
   return hipGetLastError();
 }
 

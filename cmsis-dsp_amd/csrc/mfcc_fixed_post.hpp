@@ -55,6 +55,7 @@ __host__ __device__ inline int mq_group(int nb_mel) { return nb_mel >= 32 ? 1 : 
 // (G nb_mel), frame maxima (G), then the group's int64 Mel sums (G nb_mel).  mq_mpad(k) = k + k /
 // 16: the Mel sums read the magnitudes at lane strides of a slice length (often a multiple of 16
 // words), which the pad spreads over distinct banks.
+constexpr int kMqBinU = MI355X_MQ_BIN_U;   // magnitude steps in flight per wave (tuning.hpp)
 __host__ __device__ inline int mq_mpad(int k) { return k + (k >> 4); }
 __host__ __device__ inline int mq_mag_words(int n) { return mq_mpad(n / 2) + 1; }
 __host__ __device__ inline int mq_mel_off(int n, int nb_mel) { return mq_mag_words(n); }
@@ -76,28 +77,26 @@ __host__ __device__ inline int mq_wave_words(int n, int nb_mel) { return mq_acc_
 // get(i) returns CFFT bin i of the frame (the CFFT output in global memory).
 template <typename Get>
 __device__ __forceinline__ int2 mq_split_q31(Get get, int k, int L, int4 t) {
-  if (k == 0 || k == L) {
-    const int2 v = get(0);
-    return make_int2((k == 0 ? wadd(v.x, v.y) : wsub(v.x, v.y)) >> 1, 0);
-  }
-  const int2 a = get(k), b = get(L - k);
+  // branch-free (the magnitude loop is unrolled over independent bins): bins 0 and L take get(0)
+  // through the masked indices and select their own form at the end
+  const int2 a = get(k & (L - 1)), b = get((L - k) & (L - 1));
   int32_t re = mult_R(a.x, t.x), im = mult_R(a.x, t.y);
   re = multSub_R(re, a.y, t.y); im = multAcc_R(im, a.y, t.x);
   re = multSub_R(re, b.y, t.y); im = multSub_R(im, b.y, t.z);
   re = multAcc_R(re, b.x, t.z); im = multSub_R(im, b.x, t.y);
-  return make_int2(re, im);
+  const bool edge = k == 0 || k == L;
+  const int32_t ev = (k == 0 ? wadd(a.x, a.y) : wsub(a.x, a.y)) >> 1;
+  return make_int2(edge ? ev : re, edge ? 0 : im);
 }
 template <typename Get>   // get(i): bin i as int2 of sign-extended q15 words
 __device__ __forceinline__ int2 mq_split_q15(Get get, int k, int L, int4 t) {
-  if (k == 0 || k == L) {
-    const int2 v = get(0);
-    return make_int2((k == 0 ? v.x + v.y : v.x - v.y) >> 1, 0);
-  }
-  const int2 a = get(k), b = get(L - k);
+  const int2 a = get(k & (L - 1)), b = get((L - k) & (L - 1));
   auto p = [](int32_t u, int32_t v) { return (uint32_t)(u * v); };
   const int32_t re = (int32_t)(p(a.x, t.x) - p(a.y, t.y) + p(b.x, t.z) + p(b.y, t.w)) >> 16;
   const int32_t im = (int32_t)(p(b.x, t.w) - p(b.y, t.z) + p(a.y, t.x) + p(a.x, t.y)) >> 16;
-  return make_int2((int16_t)re, (int16_t)im);     // the split stores q15_t
+  const bool edge = k == 0 || k == L;
+  const int32_t ev = (k == 0 ? a.x + a.y : a.x - a.y) >> 1;
+  return make_int2(edge ? ev : (int16_t)re, edge ? 0 : (int16_t)im);     // the split stores q15_t
 }
 
 // maxv may alias dst (frame maxima carried in dst[frame][0]): read before any output store.
@@ -135,27 +134,35 @@ __device__ __forceinline__ MqTabs mq_stage_tables(int32_t* tab, const T* __restr
   return MqTabs{stage ? reinterpret_cast<const uint32_t*>(tab) : bf, tab + total, tab + 2 * total, stage != 0};
 }
 
-// One frame on one wave, from the CFFT output get(i) (i < L = n/2): |X_k| for k <= L (split +
-// magnitude) into mag, then the Mel sums into the int64 LDS totals acc[0 .. nb_mel).  mag / acc
-// are the wave's own.  Bins 0 .. L - 1 take one lane each per step; bin L (from get(0) only)
-// comes last.
+// One frame on one wave, from the CFFT output get(i) (i < L = n/2): |X_k| (split + magnitude)
+// into mag for the bins kmin .. kmin + kcnt - 1 that some Mel filter reads (the host's range of
+// the filter positions: the reference computes all L + 1 magnitudes, but only these reach its
+// output), then the Mel sums into the int64 LDS totals acc[0 .. nb_mel).  mag / acc are the
+// wave's own.  The bins take one lane each, kMqBinU steps unrolled: the steps' loads and splits
+// are independent, so their latencies overlap.
 template <typename T, typename Ops, typename Get>
-__device__ __forceinline__ void mq_mel_frame(const Ops& op, Get get, const int4* __restrict__ tw, int n, int nb_mel,
-                                             int total, const MqTabs& tb, const T* __restrict__ coefs, int32_t lutv,
-                                             int32_t* mag, int64_t* acc) {
+__device__ __forceinline__ void mq_mel_frame(const Ops& op, Get get, const int4* __restrict__ tw, int n, int kmin,
+                                             int kcnt, int nb_mel, int total, const MqTabs& tb,
+                                             const T* __restrict__ coefs, int32_t lutv, int32_t* mag, int64_t* acc) {
   const int lane = threadIdx.x & 63;
   auto coef = [&](int g) { return tb.stage ? tb.cf[g] : (int32_t)coefs[g]; };
   for (int i = lane; i < nb_mel; i += 64) acc[i] = 0;
   const int L = n >> 1;
-#pragma unroll 4
-  for (int p0 = 0; p0 < L; p0 += 64) {                 // uniform: the shuffle needs all lanes
-    const int p = p0 + lane, k = min(p, L - 1);
-    const int32_t v = op.mag(op.split(get, k, L, tw[k]), lutv);
-    if (p < L) mag[mq_mpad(k)] = v;
-  }
-  {
-    const int32_t v = op.mag(op.split(get, L, L, tw[L]), lutv);   // bin L (every lane: the shuffle)
-    if (lane == 0) mag[mq_mpad(L)] = v;
+  for (int p0 = 0; p0 < kcnt; p0 += 64 * kMqBinU) {    // uniform: the shuffle needs all lanes
+    int2 sp[kMqBinU];
+#pragma unroll
+    for (int u = 0; u < kMqBinU; ++u) {                 // past the range: a repeat of the last bin
+      const int k = kmin + min(p0 + 64 * u + lane, kcnt - 1);
+      sp[u] = op.split(get, k, L, tw[k]);
+    }
+#pragma unroll
+    for (int u = 0; u < kMqBinU; ++u) {
+      if (p0 + 64 * u < kcnt) {                         // uniform
+        const int p = p0 + 64 * u + lane;
+        const int32_t v = op.mag(sp[u], lutv);
+        if (p < kcnt) mag[mq_mpad(kmin + p)] = v;
+      }
+    }
   }
   mq_wave_sync();
   {   // the Mel sums over the flat list (lane t sums slice t, adds each filter's part to its total)

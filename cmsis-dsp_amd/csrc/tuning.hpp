@@ -143,6 +143,19 @@
 #define MI355X_FXQ15_T 8
 #endif
 
+// ---- mfcc_fixed_post.hpp: magnitude steps (64 bins each) unrolled per wave
+#ifndef MI355X_MQ_BIN_U
+#define MI355X_MQ_BIN_U 2
+#endif
+
+// ---- cfft_fixed_r16.hip: minimum workgroups per CU of the one-launch MFCC kernel (caps its VGPRs)
+#ifndef MI355X_MQF_WG
+#define MI355X_MQF_WG 1
+#endif
+#ifndef MI355X_MQF_STAGE   // stage the Mel / DCT tables in LDS when they fit 32 KiB
+#define MI355X_MQF_STAGE 1
+#endif
+
 // ---- api.cpp
 #ifndef MI355X_MFCC_FX_MODE
 #define MI355X_MFCC_FX_MODE 1

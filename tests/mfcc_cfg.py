@@ -87,3 +87,18 @@ def assert_parity(got, want, suite_tolerance=True):
         assert np.all(np.abs(g - w) <= 1e-5 + 1.2e-3 * np.abs(w)), float(np.nanmax(np.abs(g - w)))
     pytest.skip(f"host libm differs ({glibc}: logf != restated glibc 2.35 __logf_fma on {bad} sampled inputs); "
                 "suite tolerance checked, bit-exactness not assessable on this host")
+
+
+def edge_filterbanks(n, rng):
+    """Mel filter sets at the edges of the half spectrum (for the fixed-point back ends, which compute
+    only the magnitudes some filter reads): bins 0 and fftLen/2, an empty filter, a narrow range that
+    starts at an odd bin, the whole half spectrum.  Returns [(pos, len)] lists of uint32 arrays."""
+    h = n // 2
+    sets = [[(0, 3), (7, 0), (n // 4, min(40, h - n // 4)), (h - 9, 10)],
+            [(n // 4 + 3, 5), (n // 4 + 5, 7)],
+            [(h, 1), (0, 1)],
+            [(0, h + 1)]]
+    out = []
+    for s in sets:
+        out.append((np.array([p for p, _ in s], np.uint32), np.array([l for _, l in s], np.uint32)))
+    return out

@@ -79,6 +79,18 @@ def test_oracle_matches_reference_build_generated_configs(oracle, ref):
         assert oracle.mfcc_q31(cfg, x).tobytes() == ref.mfcc_q31(cfg, x).tobytes(), n
 
 
+def test_oracle_matches_reference_build_edge_filters(oracle, ref):
+    for n in (256, 1024):
+        rng = np.random.default_rng(n + 7)
+        base = make_cfg_q31(n)
+        x = frames_for(n, 6, 5 * n)
+        for pos, ln in mfcc_cfg.edge_filterbanks(n, rng):
+            cfg = dict(base, pos=pos, len=ln,
+                       coefs=rng.integers(-2**31, 2**31, int(ln.sum()), dtype=np.int64).astype(np.int32),
+                       dct=rng.integers(-2**31, 2**31, (4, len(pos)), dtype=np.int64).astype(np.int32))
+            assert oracle.mfcc_q31(cfg, x).tobytes() == ref.mfcc_q31(cfg, x).tobytes(), (n, pos, ln)
+
+
 # ------------------------------------------------------------------ GPU
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", SUITE_N)
@@ -126,3 +138,22 @@ def test_rejects_filters_beyond_half_spectrum(dsp):
     with pytest.raises(RuntimeError):
         m(np.zeros(n, np.int32))
     assert cmsisdsp_amd is dsp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", (256, 512, 1024, 4096))
+def test_gpu_filters_at_spectrum_edges(dsp, torch_gpu, ref, n):
+    """Filters on bins 0 and fftLen/2, an empty one, a narrow odd-based range, the whole half
+    spectrum: the back end computes only the magnitudes in the filters' bin range."""
+    rng = np.random.default_rng(n + 7)
+    base = make_cfg_q31(n)
+    frames = frames_for(n, 9, 3 * n)
+    for pos, ln in mfcc_cfg.edge_filterbanks(n, rng):
+        nb = len(pos)
+        cfg = dict(base, pos=pos, len=ln,
+                   coefs=rng.integers(-2**31, 2**31, int(ln.sum()), dtype=np.int64).astype(np.int32),
+                   dct=rng.integers(-2**31, 2**31, (4, nb), dtype=np.int64).astype(np.int32))
+        want = ref.mfcc_q31(cfg, frames)
+        m = dsp.MfccQ31(n, cfg["dct"], cfg["pos"], cfg["len"], cfg["coefs"], cfg["window"])
+        got = m.batch(torch_gpu.from_numpy(frames.copy()).cuda()).cpu().numpy()
+        assert got.tobytes() == want.tobytes(), (n, pos, ln, np.argwhere(got != want)[:5])
