@@ -78,6 +78,17 @@ void cfft_sync(const Inst* S, void* p1, uint8_t ifftFlag, uint8_t bitReverseFlag
     HostIO io(st);
     void* z = io.zinout(p1, bytes);
     if (!z) { set_error(hipErrorOutOfMemory, "arm_cfft staging"); return; }
+    // N = 1024 f32 (the reference example's shape): the transform's workgroup also writes the
+    // completion word, so the call is one launch (runtime.hpp done_slot)
+    uint32_t* done = nullptr;
+    uint32_t seq = 0;
+    if (kind == 0 && n == 1024 && !pr.perm && done_slot(&done, &seq) &&
+        cfft_f32_n1024_done_launch((float*)z, 1, (const float*)pr.tw, pr.perm, pr.flags, done, seq, st)) {
+      hipError_t e = hipGetLastError();
+      if (e == hipSuccess) e = io.finish(seq);
+      if (e != hipSuccess) set_error(e, "arm_cfft");
+      return;
+    }
     hipError_t e = cfft_launch(kind, n, z, 1, pr, st);
     if (e == hipSuccess) e = io.finish();
     if (e != hipSuccess) set_error(e, "arm_cfft");
@@ -547,8 +558,12 @@ void fir_sync(const Inst* S, const T* pSrc, T* pDst, uint32_t B, int kind) {
     T* zd = (T*)io.zout(pDst, sb);
     if (!zs || !zd) { set_error(hipErrorOutOfMemory, "arm_fir staging"); return; }
     memmove(zs + T1, pSrc, sb);                   // pSrc may alias pDst: read before anything
-    hipError_t e = fir_run(kind, dc, taps, zs + T1, zd, B, 1, zs, st);
-    if (e == hipSuccess) e = io.finish();
+    uint32_t* done = nullptr;
+    uint32_t seq = 0;
+    bool flagged = false;                         // the filter's workgroup wrote the completion word
+    if (!done_slot(&done, &seq)) done = nullptr;
+    hipError_t e = fir_run(kind, dc, taps, zs + T1, zd, B, 1, zs, st, done, seq, &flagged);
+    if (e == hipSuccess) e = io.finish(flagged ? seq : 0);
     if (e == hipSuccess) hold.synced();
     if (e != hipSuccess) set_error(e, "arm_fir");
     return;

@@ -130,8 +130,13 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// DONE (the synchronous drop-in, one workgroup): after its stores the workgroup writes `seq` into
+// the caller's coherent host word `done` (runtime.cpp done_slot), so the call needs no second
+// launch for its completion signal.
+template <bool DONE>
 __global__ __launch_bounds__(64 * kN1024Wpb, MI355X_N1024_WAVES) void cfft_f32_n1024_kernel(float2* __restrict__ data, uint32_t batch,
-                                                           const float2* __restrict__ tw, uint32_t flags) {
+                                                           const float2* __restrict__ tw, uint32_t flags,
+                                                           uint32_t* done, uint32_t seq) {
   __shared__ __attribute__((aligned(16))) float2 lds_all[kN1024Wpb][16 * 72];
   const int l = threadIdx.x & 63;
   float2* lds = lds_all[threadIdx.x >> 6];
@@ -238,6 +243,7 @@ __global__ __launch_bounds__(64 * kN1024Wpb, MI355X_N1024_WAVES) void cfft_f32_n
       }
     }
   }
+  if constexpr (DONE) signal_done(done, seq);
 }
 
 // ============================================================================================
@@ -590,6 +596,16 @@ static hipError_t launch_f32(float2* data, uint32_t batch, const float2* tw, con
   return hipGetLastError();
 }
 
+// The drop-in's one N = 1024 transform (the reference's own table) with its completion word
+// written by the transform's workgroup; false: not this case (the caller launches the usual way).
+bool cfft_f32_n1024_done_launch(float* data, uint32_t batch, const float* tw, const uint16_t* perm, uint32_t flags,
+                                uint32_t* done, uint32_t seq, hipStream_t st) {
+  if (perm || batch == 0 || batch > (uint32_t)((kN1024T ? kN1024T : 1) * kN1024Wpb)) return false;
+  hipLaunchKernelGGL(cfft_f32_n1024_kernel<true>, dim3(1), dim3(64 * kN1024Wpb), 0, st, reinterpret_cast<float2*>(data),
+                     batch, reinterpret_cast<const float2*>(tw), flags, done, seq);
+  return true;
+}
+
 hipError_t cfft_f32_launch(int n, float* data, uint32_t batch, const float* tw, const uint16_t* perm,
                            uint32_t flags, hipStream_t st) {
   float2* d = reinterpret_cast<float2*>(data);
@@ -615,8 +631,9 @@ hipError_t cfft_f32_launch(int n, float* data, uint32_t batch, const float* tw, 
       if (!perm) {   // the reference's own table (or no reversal): the specialist kernel
         const int per_block = (kN1024T ? kN1024T : 1) * kN1024Wpb;
         int grid = (int)((batch + per_block - 1) / per_block);
-        if (!kN1024T) grid = persistent_grid((const void*)cfft_f32_n1024_kernel, 64 * kN1024Wpb, 0, grid, 8);
-        hipLaunchKernelGGL(cfft_f32_n1024_kernel, dim3(grid), dim3(64 * kN1024Wpb), 0, st, d, batch, w, flags);
+        if (!kN1024T) grid = persistent_grid((const void*)cfft_f32_n1024_kernel<false>, 64 * kN1024Wpb, 0, grid, 8);
+        hipLaunchKernelGGL(cfft_f32_n1024_kernel<false>, dim3(grid), dim3(64 * kN1024Wpb), 0, st, d, batch, w, flags,
+                           nullptr, 0u);
         return hipGetLastError();
       }
       return launch_f32<1024>(d, batch, w, perm, flags, st);

@@ -76,4 +76,13 @@ __device__ __forceinline__ int32_t sat_shl1_q31(int32_t v) {
 }
 __device__ __forceinline__ int32_t sat_shl1_q15(int32_t v) { return ssat16(v << 1); }
 
+// End of a one-workgroup synchronous drop-in launch: every thread's stores are made visible
+// system-wide, then one lane stores seq into the caller's coherent host word (the completion
+// signal the host spins on, runtime.cpp done_slot; sync.hip does the same as its own launch).
+__device__ __forceinline__ void signal_done(uint32_t* done, uint32_t seq) {
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace mi355x

@@ -957,7 +957,8 @@ __global__ void fir_hist_kernel(const T* __restrict__ src, T* __restrict__ hist,
 constexpr int kFirSmallMax = 8192;           // T - 1 + B words of LDS
 __global__ __launch_bounds__(kBlock) void fir_f32_small_kernel(const float* __restrict__ coeffs, int T,
                                                                const float* src, float* dst, uint32_t B,
-                                                               float* hist, const float* hist_in) {
+                                                               float* hist, const float* hist_in, uint32_t* done,
+                                                               uint32_t seq) {
   __shared__ float s[kFirSmallMax];
   const int T1 = T - 1, tid = threadIdx.x;
   const uint64_t f = blockIdx.x;
@@ -969,6 +970,7 @@ __global__ __launch_bounds__(kBlock) void fir_f32_small_kernel(const float* __re
     dst[f * B + n] = acc;
   }
   for (int j = tid; j < T1; j += kBlock) hist[f * T1 + j] = s[B + j];
+  if (done) signal_done(done, seq);               // the drop-in's one filter: its completion word
 }
 
 // One f32 FIR pass over `batch` filters, outputs on the lattice `fo`.
@@ -1023,14 +1025,16 @@ hipError_t fir_f32_conv_pass(const float* c, uint64_t cstride, int T, const floa
 
 template <typename T>
 static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T* dst, uint32_t B, uint32_t batch,
-                             T* hist, hipStream_t st) {
+                             T* hist, hipStream_t st, uint32_t* done, uint32_t seq, bool* flagged) {
   if (batch == 0 || B == 0) return hipSuccess;
   if (T_ < 1) return hipErrorInvalidValue;        // numTaps > kFirMaxTaps: tap segments
   const int T1 = T_ - 1;
   if constexpr (sizeof(T) == 4) {
     if (kind == kFirF32 && batch <= 8 && (int64_t)T1 + B <= kFirSmallMax && (uint64_t)B * T_ <= (1u << 16)) {
+      uint32_t* dn = batch == 1 ? done : nullptr;  // one workgroup: it can signal the completion
       hipLaunchKernelGGL(fir_f32_small_kernel, dim3(batch), dim3(kBlock), 0, st, (const float*)coeffs, T_,
-                         (const float*)src, (float*)dst, B, (float*)hist, (const float*)hist);
+                         (const float*)src, (float*)dst, B, (float*)hist, (const float*)hist, dn, seq);
+      if (dn && flagged) *flagged = true;
       return hipGetLastError();
     }
   }
@@ -1107,23 +1111,24 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
 }
 
 hipError_t fir_run(int kind, const void* coeffs, int num_taps, const void* src, void* dst, uint32_t block_size,
-                   uint32_t batch, void* hist, hipStream_t st) {
+                   uint32_t batch, void* hist, hipStream_t st, uint32_t* done, uint32_t seq, bool* flagged) {
+  if (flagged) *flagged = false;
   switch (kind) {
     case kFirF32:
     case kFirF32Fma:
       return fir_launch<float>(kind, (const float*)coeffs, num_taps, (const float*)src, (float*)dst, block_size,
-                               batch, (float*)hist, st);
+                               batch, (float*)hist, st, done, seq, flagged);
     case kFirQ15:
     case kFirFastQ15:
       return fir_launch<int16_t>(kind, (const int16_t*)coeffs, num_taps, (const int16_t*)src, (int16_t*)dst,
-                                 block_size, batch, (int16_t*)hist, st);
+                                 block_size, batch, (int16_t*)hist, st, done, seq, flagged);
     case kFirQ31:
     case kFirFastQ31:
       return fir_launch<int32_t>(kind, (const int32_t*)coeffs, num_taps, (const int32_t*)src, (int32_t*)dst,
-                                 block_size, batch, (int32_t*)hist, st);
+                                 block_size, batch, (int32_t*)hist, st, done, seq, flagged);
     case kFirQ7:
       return fir_launch<int8_t>(kind, (const int8_t*)coeffs, num_taps, (const int8_t*)src, (int8_t*)dst,
-                                block_size, batch, (int8_t*)hist, st);
+                                block_size, batch, (int8_t*)hist, st, done, seq, flagged);
     default:
       return hipErrorInvalidValue;
   }

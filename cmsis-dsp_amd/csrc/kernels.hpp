@@ -40,6 +40,11 @@ bool cfft_q15_r16_launch(int n, int16_t* data, uint32_t batch, const int16_t* tw
 // Stores v into *dflag (a device-mapped coherent host word) after the stream's earlier work
 // (sync.hip): the drop-in calls' completion signal.
 hipError_t done_flag_launch(uint32_t* dflag, uint32_t v, hipStream_t st);
+// One arm_cfft_f32 N = 1024 call of the drop-in (the reference's table, batch within one
+// workgroup) whose workgroup stores seq into done when its stores are visible; false: not this
+// case, nothing launched.
+bool cfft_f32_n1024_done_launch(float* data, uint32_t batch, const float* tw, const uint16_t* perm, uint32_t flags,
+                                uint32_t* done, uint32_t seq, hipStream_t st);
 
 // The whole MFCC q31 / q15 in one launch (front end + CFFT + back end, cfft_fixed_r16.hip);
 // n = fftLen / 2.  hipErrorNotSupported: not handled (take the two-launch schedule).
@@ -84,8 +89,11 @@ hipError_t rfft_q15_pass_launch(bool inverse, int n, const int16_t* src, int16_t
 // the new tail).  Element type: f32 float, q15/fast_q15 int16, q31/fast_q31 int32, q7 int8.
 enum FirKind { kFirF32 = 0, kFirQ15 = 1, kFirQ31 = 2, kFirFastQ15 = 3, kFirFastQ31 = 4, kFirQ7 = 5,
                kFirF32Fma = 6 };   // kFirF32Fma: the opt-in fused-multiply-add f32 path (tolerance)
+// done / seq (the synchronous drop-in): when the pass ends in one workgroup it also stores seq into
+// the completion word done (runtime.cpp done_slot) and sets *flagged.
 hipError_t fir_run(int kind, const void* coeffs, int num_taps, const void* src, void* dst, uint32_t block_size,
-                   uint32_t batch, void* hist, hipStream_t st);
+                   uint32_t batch, void* hist, hipStream_t st, uint32_t* done = nullptr, uint32_t seq = 0,
+                   bool* flagged = nullptr);
 
 // Multirate FIR (fir.hip): `batch` independent decimators / interpolators sharing one
 // coefficient set.  Decimator: outputs [batch][blockSize / M], hist [batch][numTaps - 1].

@@ -527,42 +527,58 @@ int sync_mode() {
   }();
   return m;
 }
+
+DoneWord* done_word() {
+  const int dev = cur_dev();
+  DoneWord& w = t_done[dev];
+  if (!w.h) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+      (void)hipHostFree(p);
+      return nullptr;
+    }
+    w.h = (volatile uint32_t*)p;
+    w.d = (uint32_t*)d;
+    *w.h = 0;
+  }
+  return &w;
+}
 }  // namespace
 
+bool done_slot(uint32_t** dflag, uint32_t* seq) {
+  if (sync_mode() != 1) return false;
+  DoneWord* w = done_word();
+  if (!w) return false;
+  if (++w->seq == 0) ++w->seq;               // 0 means "no self-signalled work" (HostIO::finish)
+  *dflag = w->d;
+  *seq = w->seq;
+  return true;
+}
+
+hipError_t wait_done(hipStream_t st, uint32_t seq) {
+  DoneWord* w = done_word();
+  // spin up to ~2^22 polls (milliseconds); a slow or failed call falls through to the sync
+  if (w)
+    for (uint32_t i = 0; i < (1u << 22); ++i)
+      if (__atomic_load_n(w->h, __ATOMIC_ACQUIRE) == seq) return hipSuccess;
+  return hipStreamSynchronize(st);
+}
+
 hipError_t wait_stream(hipStream_t st) {
-  if (sync_mode() == 1) {
-    const int dev = cur_dev();
-    DoneWord& w = t_done[dev];
-    if (!w.h) {
-      void* p = nullptr;
-      if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess) {
-        void* d = nullptr;
-        if (hipHostGetDevicePointer(&d, p, 0) == hipSuccess) {
-          w.h = (volatile uint32_t*)p;
-          w.d = (uint32_t*)d;
-          *w.h = 0;
-        } else {
-          (void)hipHostFree(p);
-        }
-      }
-    }
-    if (w.h) {
-      const uint32_t v = ++w.seq;
-      if (done_flag_launch(w.d, v, st) == hipSuccess) {
-        // spin up to ~2^22 polls (milliseconds); a slow or failed call falls through to the sync
-        for (uint32_t i = 0; i < (1u << 22); ++i)
-          if (__atomic_load_n(w.h, __ATOMIC_ACQUIRE) == v) return hipSuccess;
-      } else {
-        (void)hipGetLastError();
-      }
-    }
+  uint32_t* d = nullptr;
+  uint32_t v = 0;
+  if (done_slot(&d, &v)) {
+    if (done_flag_launch(d, v, st) == hipSuccess) return wait_done(st, v);
+    (void)hipGetLastError();
   }
   return hipStreamSynchronize(st);
 }
 
-hipError_t HostIO::finish() {
+hipError_t HostIO::finish(uint32_t seq) {
   finished_ = true;
-  hipError_t e = wait_stream(st_);
+  hipError_t e = seq ? wait_done(st_, seq) : wait_stream(st_);
   if (e != hipSuccess) return e;
   for (int i = 0; i < nouts_; ++i) memcpy(outs_[i].host, outs_[i].pin, outs_[i].bytes);
   nouts_ = 0;

@@ -96,7 +96,7 @@ class HostIO {
   void* zin(const void* host, size_t bytes);                 // nullptr: allocation failed
   void* zout(void* host, size_t bytes);
   void* zinout(void* host, size_t bytes);
-  hipError_t finish();
+  hipError_t finish(uint32_t seq = 0);   // seq != 0: the work signals completion itself
 
  private:
   struct Pending { void* host; const void* pin; size_t bytes; };
@@ -110,6 +110,13 @@ class HostIO {
 // Wait for everything enqueued on st (the synchronous drop-in calls' completion): a spin on a
 // host word written by the stream, or hipStreamSynchronize (runtime.cpp, CMSISDSP_MI355X_SYNC).
 hipError_t wait_stream(hipStream_t st);
+
+// Spin mode: the calling thread's completion word on the current device and the next sequence
+// number, for a launch that signals its own completion (common.hpp signal_done) -- one launch per
+// call instead of the work plus done_flag_launch.  false in sync mode or when unavailable.
+bool done_slot(uint32_t** dflag, uint32_t* seq);
+// Wait until the completion word holds seq (bounded spin), then as wait_stream's fallback.
+hipError_t wait_done(hipStream_t st, uint32_t seq);
 
 // The internal stream used by the synchronous drop-in API on the current device.
 hipStream_t sync_stream();
