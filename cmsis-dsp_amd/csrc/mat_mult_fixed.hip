@@ -310,20 +310,39 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
     __syncthreads();
   }
 
-  // ---- epilogue: exact sums through LDS (reusing the plane buffers), int64 combine
-  int64_t* rs = reinterpret_cast<int64_t*>(lds);            // [AQ][BM]
+  // ---- epilogue: exact sums through LDS (reusing the plane buffers), int64 combine.  The
+  // partial row / column sums are reduced once (one thread per row, one per column), then every
+  // output reads its two final sums; whole tiles are staged as T in LDS and leave as 16-B
+  // stores, 16 threads per 256-B row (the per-element stores issued one 2- / 4-byte store per
+  // output, 32 lanes covering 64 / 128 B).
+  int64_t* rs = reinterpret_cast<int64_t*>(lds);            // [AQ][BM] partials
   int64_t* cs = rs + AQ * BM;                               // [NQ][BN]
+  int64_t* rfin = cs + NQ * BN;                             // [BM] final row sums
+  int64_t* cfin = rfin + BM;                                // [BN] final column sums
+  T* ct = reinterpret_cast<T*>(cfin + BN);                  // [BM][BN] output tile (FULL)
+  static_assert((AQ * BM + NQ * BN + BM + BN) * 8 + BM * BN * sizeof(T) <= 2 * BUF, "epilogue fits the planes");
   rs[(tid % AQ) * BM + ar] = my_rsum;
 #pragma unroll
   for (int c = 0; c < CW; ++c) cs[bq * BN + bg * CW + c] = my_csum[c];
+  __syncthreads();
+  for (int i = tid; i < BM + BN; i += kNT2) {
+    int64_t sum = 0;
+    if (i < BM) {
+#pragma unroll
+      for (int q = 0; q < AQ; ++q) sum += rs[q * BM + i];
+      rfin[i] = sum;
+    } else {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) sum += cs[q * BN + (i - BM)];
+      cfin[i - BM] = sum;
+    }
+  }
   __syncthreads();
   const int64_t kpad = (int64_t)nk * kKT2;   // padded k terms are zeros: the identity holds over kpad
 #pragma unroll
   for (int j = 0; j < WBN; ++j) {
     const int cc = wn * 32 * WBN + j * 32 + r;
-    int64_t csum = 0;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) csum += cs[q * BN + cc];
+    const int64_t csum = cfin[cc];
     const int gcol = col0 + cc;
 #pragma unroll
     for (int i = 0; i < WBM; ++i) {
@@ -331,20 +350,28 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
       for (int reg = 0; reg < 16; ++reg) {
         const int rr = wm * 32 * WBM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
         const int grow = row0 + rr;
-        int64_t rsum = 0;
-#pragma unroll
-        for (int q = 0; q < AQ; ++q) rsum += rs[q * BM + rr];
-        uint64_t v = (uint64_t)(C0 * (rsum + csum)) - (uint64_t)kpad * (uint64_t)(C0 * C0);
+        uint64_t v = (uint64_t)(C0 * (rfin[rr] + csum)) - (uint64_t)kpad * (uint64_t)(C0 * C0);
 #pragma unroll
         for (int s = 0; s < S; ++s) v += (uint64_t)(int64_t)acc[s][i][j][reg] << (8 * s);
-        if (FULL || (grow < M && gcol < N)) {
-          const int64_t sum = (int64_t)v;
-          // fast q15 (arm_mat_mult_fast_q15.c:356-401 host branch): q31_t modular sum, (q15)(sum >> 15)
-          if constexpr (sizeof(T) == 2)
-            C[(size_t)grow * N + gcol] = fast ? (T)((int32_t)(uint32_t)v >> 15) : (T)ssat16((int32_t)(sum >> 15));
-          else C[(size_t)grow * N + gcol] = (T)(int32_t)(sum >> 31);
-        }
+        const int64_t sum = (int64_t)v;
+        // fast q15 (arm_mat_mult_fast_q15.c:356-401 host branch): q31_t modular sum, (q15)(sum >> 15)
+        T o;
+        if constexpr (sizeof(T) == 2) o = fast ? (T)((int32_t)(uint32_t)v >> 15) : (T)ssat16((int32_t)(sum >> 15));
+        else o = (T)(int32_t)(sum >> 31);
+        if constexpr (FULL) ct[rr * BN + cc] = o;
+        else if (grow < M && gcol < N) C[(size_t)grow * N + gcol] = o;
       }
+    }
+  }
+  if constexpr (FULL) {
+    __syncthreads();
+    constexpr int VPR = BN * (int)sizeof(T) / 16;            // 16-B words per tile row
+    static_assert(VPR * 16 == BN * (int)sizeof(T), "whole 16-B words per row");
+#pragma unroll
+    for (int w = tid; w < BM * VPR; w += kNT2) {
+      const int rr = w / VPR, cw = w % VPR;
+      *reinterpret_cast<uint4*>(C + (size_t)(row0 + rr) * N + col0 + cw * (16 / (int)sizeof(T))) =
+          *reinterpret_cast<const uint4*>(ct + rr * BN + cw * (16 / (int)sizeof(T)));
     }
   }
 }
@@ -643,7 +670,7 @@ static hipError_t launch_fixed(int m, int k, int n, const T* a, const T* b, T* c
     const int tiles = ((m + G::BM - 1) / G::BM) * ((n + G::BN - 1) / G::BN);
     const bool full = m % G::BM == 0 && n % G::BN == 0 && k % G::KT == 0 &&
                       ((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0 && (k * sizeof(T)) % 16 == 0 &&
-                      (n * sizeof(T)) % 16 == 0;
+                      (n * sizeof(T)) % 16 == 0 && ((uintptr_t)c & 15) == 0;
     if (MI355X_I8_V3) {
       if (full)
         hipLaunchKernelGGL((mat_mult_i8v3_kernel<T, true>), dim3(tiles * batch), dim3(kNT2), 0, st, a, b, c, m, k, n,
