@@ -393,6 +393,33 @@ def test_mat_mult_fixed_batch(dsp, torch_gpu, ref, kind):
             assert got[i].tobytes() == ref.mat_mult_fixed(kind, a[i], b[i])[1].tobytes(), (m, i)
 
 
+@pytest.mark.parametrize("kind", ["q15", "fast_q15", "q31"])
+def test_mat_mult_fixed_many_tiles(dsp, torch_gpu, ref, kind):
+    """More whole tiles than the persistent grid (q15: workgroups walk several tiles, the next
+    tile's first K step loaded under the current epilogue): every matrix of the batch bit-exact
+    against exact int64 products (checked against the reference build on a few)."""
+    bits, dt = (15, np.int16) if kind.endswith("q15") else (31, np.int32)
+    tdt = torch_gpu.int16 if kind.endswith("q15") else torch_gpu.int32
+    rng = np.random.default_rng(21)
+    batch, m, k, n = 600, 128, 128, 128
+    a = rng.integers(-(1 << bits), 1 << bits, (batch, m, k)).astype(dt)
+    b = rng.integers(-(1 << bits), 1 << bits, (batch, k, n)).astype(dt)
+    A, B = torch_gpu.from_numpy(a).cuda(), torch_gpu.from_numpy(b).cuda()
+    Cm = torch_gpu.empty((batch, m, n), dtype=tdt, device="cuda")
+    dsp.mat_mult_batch(A, B, Cm, fast=kind.startswith("fast"))
+    got = Cm.cpu().numpy()
+    for i in (0, 1, 255, 256, 257, 511, 599):
+        assert got[i].tobytes() == ref.mat_mult_fixed(kind, a[i], b[i])[1].tobytes(), i
+    s = np.matmul(a.astype(np.int64), b.astype(np.int64))        # wraps mod 2^64 like the q63 sum
+    if kind == "q15":
+        want = np.clip(s >> 15, -32768, 32767).astype(np.int16)
+    elif kind == "fast_q15":
+        want = ((s.astype(np.uint64).astype(np.uint32).view(np.int32)) >> 15).astype(np.int16)
+    else:
+        want = (s >> 31).astype(np.int32)
+    assert got.tobytes() == want.tobytes(), np.argwhere(got != want)[:5]
+
+
 # ------------------------------------------------------------------ convolution
 def _conv_case(kind, la, lb, seed, fill=None):
     rng = np.random.default_rng(seed)

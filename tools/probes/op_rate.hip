@@ -39,8 +39,15 @@ __global__ __launch_bounds__(256) void probe(int* out, int seed) {
   if constexpr (K == 16) CHAIN8(asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(f[i]) : "s"((float)c), "v"(f[(i + 1) & 7])))
   if constexpr (K == 17) CHAIN8(asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(f[i]) : "v"((float)d), "v"(f[(i + 1) & 7])))
   if constexpr (K == 18) CHAIN8(asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(f[i]) : "s"((float)c), "v"((float)d)))
-  int s = 0;
-  for (int i = 0; i < 8; ++i) s += a[i] + (int)f[i];
+  // 64-bit products (MFCC q31 split / sqrt): 64-bit accumulator chains, carry-out to an SGPR pair
+  long long q[8];
+  for (int i = 0; i < 8; ++i) q[i] = a[i];
+  unsigned long long sc = 0;
+  if constexpr (K == 19) CHAIN8(asm volatile("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(q[i]), "=s"(sc) : "v"(c), "v"(d)))
+  if constexpr (K == 20) CHAIN8(asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(q[i]), "=s"(sc) : "v"(c), "v"(d)))
+  if constexpr (K == 21) CHAIN8(asm volatile("v_alignbit_b32 %0, %0, %1, 28" : "+v"(a[i]) : "v"(c)))
+  int s = (int)sc;
+  for (int i = 0; i < 8; ++i) s += a[i] + (int)f[i] + (int)q[i] + (int)(q[i] >> 32);
   out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
@@ -83,5 +90,8 @@ int main() {
   run<16>(out, "v_fmac_f32 s,v(acc'),acc");
   run<17>(out, "v_fmac_f32 v,v(acc'),acc");
   run<18>(out, "v_fmac_f32 s,v(const),acc");
+  run<19>(out, "v_mad_i64_i32");
+  run<20>(out, "v_mad_u64_u32");
+  run<21>(out, "v_alignbit_b32");
   return 0;
 }
