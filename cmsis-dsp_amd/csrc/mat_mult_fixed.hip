@@ -387,7 +387,14 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
 template <typename T> struct I8B3 {               // B staging geometry
   static constexpr int BN = I8Cfg<T>::BN, EB = 64 * BN / kNT2;   // elements per thread (16 q15 / 8 q31)
   static constexpr int TPR = BN / EB;                            // threads per k-row (8)
-  static constexpr int PITCH = BN + 16;                          // bytes per plane row (tr_b8 banks)
+  // bytes per plane row: a multiple of 32 that is an odd multiple of 8 dwords mod 64, so the
+  // 8 rows x 8 dwords a 32-lane group of ds_read_b64_tr_b8 touches cover the 64 banks once
+  // (MI355X_I8_V3P overrides; BN + 16 measured 8x the v2 conflicts)
+#ifdef MI355X_I8_V3P
+  static constexpr int PITCH = MI355X_I8_V3P;
+#else
+  static constexpr int PITCH = BN == 128 ? 160 : 96;
+#endif
 };
 typedef int v2i32_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ v2i32_t tr_b8(const int8_t* p) {   // p: a generic pointer into LDS
