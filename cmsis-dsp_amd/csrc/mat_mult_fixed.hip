@@ -87,6 +87,28 @@ __device__ __forceinline__ uint32_t gather4(uint32_t r0, uint32_t r1, uint32_t r
   return __builtin_amdgcn_perm(r1, r0, sel) | (__builtin_amdgcn_perm(r3, r2, sel) << 16);
 }
 
+// Diagnostic build only (MI355X_I8_STAMPS, tools/probes/i8_phases.py): thread 0 of each
+// workgroup records s_memtime after the tile decode, the prologue, the K loop, the epilogue
+// arithmetic and the copy-out, plus s_memrealtime and its HW_ID / XCC_ID, into a device buffer.
+#if MI355X_I8_STAMPS
+constexpr int kI8Stamps = 1 << 16;
+__device__ uint64_t g_i8_stamps[kI8Stamps][8];
+#define I8_STAMP(i)                                                                       \
+  do {                                                                                    \
+    if (threadIdx.x == 0 && blockIdx.x < (uint32_t)kI8Stamps) {                           \
+      g_i8_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime();                          \
+      if ((i) == 0) {                                                                     \
+        g_i8_stamps[blockIdx.x][5] = __builtin_amdgcn_s_memrealtime();                    \
+        g_i8_stamps[blockIdx.x][7] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | \
+                                     ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32); \
+      }                                                                                   \
+      if ((i) == 4) g_i8_stamps[blockIdx.x][6] = __builtin_amdgcn_s_memrealtime();        \
+    }                                                                                     \
+  } while (0)
+#else
+#define I8_STAMP(i) do { } while (0)
+#endif
+
 // FULL: M % BM == 0, N % BN == 0, K % 64 == 0 and 16-B / 8-B aligned rows -- no bounds
 // checks, so the K loop is one basic block the scheduler can interleave (loads, staging,
 // MFMAs); otherwise every load is guarded and zero-filled.
@@ -124,6 +146,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
   C += bz * (size_t)M * N;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int row0 = tm * BM, col0 = tn * BN;
+  I8_STAMP(0);
 
   // staging roles: A row ar, AK k from ak0; B k-quad bq (rows 4bq..4bq+3), columns bg*CW..+CW-1
   const int ar = tid / AQ, ak0 = AK * (tid % AQ);
@@ -182,7 +205,10 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
     }
   };
 
-  int64_t my_rsum = 0, my_csum[CW];
+  // this thread's partial row / column sums over the K steps: int32 is exact for q15 (at most
+  // 16 x 511 values of |v| <= 2^15 per partial), int64 for q31
+  using PS = typename std::conditional<sizeof(T) == 2, int32_t, int64_t>::type;
+  PS my_rsum = 0, my_csum[CW];
 #pragma unroll
   for (int c = 0; c < CW; ++c) my_csum[c] = 0;
   i32x16 acc[S][WBM][WBN];
@@ -286,6 +312,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
   stage(0);
   if (nk > 1) load(kKT2);
   __syncthreads();
+  I8_STAMP(1);
   int kt = 0;
   for (; kt + 2 < nk; ++kt) {                    // steady state: one basic block when FULL
     const int cur = kt & 1;
@@ -309,6 +336,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
     mma();
     __syncthreads();
   }
+  I8_STAMP(2);
 
   // ---- epilogue: exact sums through LDS (reusing the plane buffers), int64 combine.  The
   // partial row / column sums are reduced once (one thread per row, one per column), then every
@@ -321,9 +349,9 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
   int64_t* cfin = rfin + BM;                                // [BN] final column sums
   T* ct = reinterpret_cast<T*>(cfin + BN);                  // [BM][BN] output tile (FULL)
   static_assert((AQ * BM + NQ * BN + BM + BN) * 8 + BM * BN * sizeof(T) <= 2 * BUF, "epilogue fits the planes");
-  rs[(tid % AQ) * BM + ar] = my_rsum;
+  rs[(tid % AQ) * BM + ar] = (int64_t)my_rsum;
 #pragma unroll
-  for (int c = 0; c < CW; ++c) cs[bq * BN + bg * CW + c] = my_csum[c];
+  for (int c = 0; c < CW; ++c) cs[bq * BN + bg * CW + c] = (int64_t)my_csum[c];
   __syncthreads();
   for (int i = tid; i < BM + BN; i += kNT2) {
     int64_t sum = 0;
@@ -363,6 +391,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
       }
     }
   }
+  I8_STAMP(3);
   if constexpr (FULL) {
     __syncthreads();
     constexpr int VPR = BN * (int)sizeof(T) / 16;            // 16-B words per tile row
@@ -374,6 +403,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
           *reinterpret_cast<const uint4*>(ct + rr * BN + cw * (16 / (int)sizeof(T)));
     }
   }
+  I8_STAMP(4);
 }
 
 // ---- v3 kernel (round 4): the v2 tiling with B staged ROW-major.  B's
@@ -774,5 +804,12 @@ hipError_t mat_mult_q31_launch(int m, int k, int n, const int32_t* a, const int3
                                hipStream_t st) {
   return launch_fixed<int32_t>(m, k, n, a, b, c, batch, st);
 }
+
+#if MI355X_I8_STAMPS
+extern "C" int arm_mi355x_i8_stamps(uint64_t* out, size_t rows) {   // diagnostic builds only
+  const size_t n = rows < (size_t)kI8Stamps ? rows : (size_t)kI8Stamps;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_i8_stamps), n * 8 * sizeof(uint64_t), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 }  // namespace mi355x

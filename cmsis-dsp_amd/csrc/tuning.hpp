@@ -109,6 +109,9 @@
 #ifndef MI355X_I8_SCHED
 #define MI355X_I8_SCHED 6
 #endif
+#ifndef MI355X_I8_STAMPS    // diagnostic: per-workgroup phase timestamps (mat_mult_fixed.hip)
+#define MI355X_I8_STAMPS 0
+#endif
 #ifndef MI355X_I8_V3
 #define MI355X_I8_V3 0
 #endif

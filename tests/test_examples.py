@@ -29,12 +29,16 @@ def test_examples_compile_and_link():
 
 
 @pytest.mark.gpu
-def test_fft_bin_example_runs_on_gpu(torch_gpu):
+@pytest.mark.parametrize("sync", ["spin", "sync"])
+def test_fft_bin_example_runs_on_gpu(torch_gpu, sync):
+    """Both completion modes of the synchronous calls (CMSISDSP_MI355X_SYNC): the spin on the
+    coherent word the transform's workgroup writes, and a plain stream synchronisation."""
     exe = _build("fft_bin_dropin")
     x = np.load(os.path.join(ROOT, "tests", "golden", "reference_patterns.npz"))["kat_fftbin_input"]
     inp = os.path.join(OUT, "fftbin_input.f32")
     x.astype(np.float32).tofile(inp)
-    r = subprocess.run([exe, inp], capture_output=True, text=True, timeout=120)
+    env = dict(os.environ, CMSISDSP_MI355X_SYNC=sync)
+    r = subprocess.run([exe, inp], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0 and r.stdout.strip() == "SUCCESS 213", r.stdout + r.stderr
 
 
