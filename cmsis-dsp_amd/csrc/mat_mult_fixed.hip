@@ -73,6 +73,11 @@ template <int CW> __device__ __forceinline__ int i8_brow(int col) {
   constexpr int L = CW == 8 ? 3 : CW == 4 ? 2 : CW == 2 ? 1 : 0;
   return col ^ ((col >> L) & 1);
 }
+// B8 staging (ds_write_b64 of 8 k-bytes, 16-lane groups on consecutive column pairs, banks mod 32):
+// flipping the row parity on bit 1 of the column spreads a group over both row parities, the
+// most any 16 writes of 8 bytes into 64-byte rows can use (2-way); fragment reads keep each
+// aligned row quad, so they stay conflict free.
+__device__ __forceinline__ int i8_brow8(int col) { return col ^ ((col >> 1) & 1); }
 
 // plane p of the two q15 values in each of d0, d1: [d0.lo, d0.hi, d1.lo, d1.hi] byte p
 template <int P>
@@ -152,10 +157,18 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
   const int ar = tid / AQ, ak0 = AK * (tid % AQ);
   const int bq = tid % NQ, bg = tid / NQ;
   const int gr = row0 + ar, gc = col0 + bg * CW;
+  // B8 (q15): thread (cp, kb8) stages columns 2cp, 2cp + 1 over k-rows 8 kb8 .. 8 kb8 + 7 (eight
+  // coalesced dword loads), i.e. 8 k-bytes per column and plane: one ds_write_b64 each (4 per
+  // thread instead of v2's 16 ds_write_b32) and half the transposing v_perm work
+  constexpr bool B8 = MI355X_I8_B8 && sizeof(T) == 2;
+  constexpr int NQB = B8 ? 8 : NQ;               // column-sum partials per column
+  const int cp = tid % 64, kb8 = tid / 64;
+  const int gcp = col0 + 2 * cp;
   const bool vecA = FULL || (((K * (int)sizeof(T)) % 16) == 0 && (((uintptr_t)A) & 15) == 0);
   const bool vecB = FULL || (((N * (int)sizeof(T)) % (4 * BD)) == 0 && (((uintptr_t)B) & (4 * BD - 1)) == 0);
+  const bool vecB8 = FULL || ((N % 2) == 0 && (((uintptr_t)B) & 3) == 0);
 
-  uint32_t ad[AKD], bd[4][BD];
+  uint32_t ad[AKD], bd[4][BD], b8[8];
   auto load = [&](int k0) {
     const int ka = k0 + ak0;
     if (FULL || (vecA && gr < M && ka + AK <= K)) {
@@ -178,6 +191,19 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
         ad[d] = w;
       }
     }
+    if constexpr (B8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int kb = k0 + 8 * kb8 + i;
+        if (FULL || (vecB8 && kb < K && gcp + 2 <= N)) {
+          b8[i] = *reinterpret_cast<const uint32_t*>(B + (size_t)kb * N + gcp);
+        } else {
+          const uint32_t lo = (kb < K && gcp < N) ? (uint32_t)(uint16_t)B[(size_t)kb * N + gcp] : 0u;
+          const uint32_t hi = (kb < K && gcp + 1 < N) ? (uint32_t)(uint16_t)B[(size_t)kb * N + gcp + 1] : 0u;
+          b8[i] = lo | (hi << 16);
+        }
+      }
+    } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int kb = k0 + 4 * bq + i;
@@ -203,6 +229,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
         }
       }
     }
+    }
   };
 
   // this thread's partial row / column sums over the K steps: int32 is exact for q15 (at most
@@ -211,6 +238,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
   PS my_rsum = 0, my_csum[CW];
 #pragma unroll
   for (int c = 0; c < CW; ++c) my_csum[c] = 0;
+  int32_t bcs[2] = {0, 0};                       // B8: columns 2cp, 2cp + 1 (exact: <= 8 x 511 x 2^15)
   i32x16 acc[S][WBM][WBN];
 #pragma unroll
   for (int s = 0; s < S; ++s)
@@ -230,13 +258,21 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
 #pragma unroll
       for (int d = 0; d < AKD; ++d) ra = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2x, ad[d]), s2x{1, 1}, ra, false);
       my_rsum += ra;
+      if constexpr (B8) {
 #pragma unroll
-      for (int c = 0; c < CW; ++c) {
-        const s2x sel = (c & 1) ? s2x{0, 1} : s2x{1, 0};
-        int32_t cs = 0;
+        for (int i = 0; i < 8; ++i) {
+          bcs[0] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2x, b8[i]), s2x{1, 0}, bcs[0], false);
+          bcs[1] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2x, b8[i]), s2x{0, 1}, bcs[1], false);
+        }
+      } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) cs = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2x, bd[i][c >> 1]), sel, cs, false);
-        my_csum[c] += cs;
+        for (int c = 0; c < CW; ++c) {
+          const s2x sel = (c & 1) ? s2x{0, 1} : s2x{1, 0};
+          int32_t cs = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) cs = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2x, bd[i][c >> 1]), sel, cs, false);
+          my_csum[c] += cs;
+        }
       }
     } else {
 #pragma unroll
@@ -259,13 +295,24 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
       for (int q = 0; q < AK / 16; ++q)
         *reinterpret_cast<uint4*>(&As[p][ar][16 * i8_chunk(ar, ak0 / 16 + q)]) =
             make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+      if constexpr (B8) {
 #pragma unroll
-      for (int c = 0; c < CW; ++c) {
-        const int d = c / EPD, o = (c % EPD) * (int)sizeof(T) + p;
-        uint32_t g = gather4(bd[0][d], bd[1][d], bd[2][d], bd[3][d], o);
-        if (p != P - 1) g ^= 0x80808080u;
-        const int row = i8_brow<CW>(bg * CW + c);
-        *reinterpret_cast<uint32_t*>(&Bs[p][row][16 * i8_chunk(row, bq >> 2) + 4 * (bq & 3)]) = g;
+        for (int c = 0; c < 2; ++c) {
+          const int o = 2 * c + p;                // byte of column 2cp + c, plane p, in a dword
+          uint32_t g0 = gather4(b8[0], b8[1], b8[2], b8[3], o), g1 = gather4(b8[4], b8[5], b8[6], b8[7], o);
+          if (p != P - 1) { g0 ^= 0x80808080u; g1 ^= 0x80808080u; }
+          const int row = i8_brow8(2 * cp + c);
+          *reinterpret_cast<uint2*>(&Bs[p][row][16 * i8_chunk(row, kb8 >> 1) + 8 * (kb8 & 1)]) = make_uint2(g0, g1);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+          const int d = c / EPD, o = (c % EPD) * (int)sizeof(T) + p;
+          uint32_t g = gather4(bd[0][d], bd[1][d], bd[2][d], bd[3][d], o);
+          if (p != P - 1) g ^= 0x80808080u;
+          const int row = i8_brow<CW>(bg * CW + c);
+          *reinterpret_cast<uint32_t*>(&Bs[p][row][16 * i8_chunk(row, bq >> 2) + 4 * (bq & 3)]) = g;
+        }
       }
     }
   };
@@ -285,7 +332,8 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
         }
 #pragma unroll
         for (int j = 0; j < WBN; ++j) {
-          const int row = i8_brow<CW>(wn * 32 * WBN + j * 32 + r);
+          const int n = wn * 32 * WBN + j * 32 + r;
+          const int row = B8 ? i8_brow8(n) : i8_brow<CW>(n);
           fb[kk][p][j] = *reinterpret_cast<const i32x4*>(&Bs[p][row][16 * i8_chunk(row, 2 * kk + h)]);
         }
       }
@@ -350,8 +398,13 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
   T* ct = reinterpret_cast<T*>(cfin + BN);                  // [BM][BN] output tile (FULL)
   static_assert((AQ * BM + NQ * BN + BM + BN) * 8 + BM * BN * sizeof(T) <= 2 * BUF, "epilogue fits the planes");
   rs[(tid % AQ) * BM + ar] = (int64_t)my_rsum;
+  if constexpr (B8) {
+    cs[kb8 * BN + 2 * cp] = (int64_t)bcs[0];
+    cs[kb8 * BN + 2 * cp + 1] = (int64_t)bcs[1];
+  } else {
 #pragma unroll
-  for (int c = 0; c < CW; ++c) cs[bq * BN + bg * CW + c] = (int64_t)my_csum[c];
+    for (int c = 0; c < CW; ++c) cs[bq * BN + bg * CW + c] = (int64_t)my_csum[c];
+  }
   __syncthreads();
   for (int i = tid; i < BM + BN; i += kNT2) {
     int64_t sum = 0;
@@ -361,7 +414,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
       rfin[i] = sum;
     } else {
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) sum += cs[q * BN + (i - BM)];
+      for (int q = 0; q < NQB; ++q) sum += cs[q * BN + (i - BM)];
       cfin[i - BM] = sum;
     }
   }

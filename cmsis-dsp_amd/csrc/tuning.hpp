@@ -112,6 +112,9 @@
 #ifndef MI355X_I8_STAMPS    // diagnostic: per-workgroup phase timestamps (mat_mult_fixed.hip)
 #define MI355X_I8_STAMPS 0
 #endif
+#ifndef MI355X_I8_B8        // q15: B staged by 8-row x column-pair threads (ds_write_b64)
+#define MI355X_I8_B8 0
+#endif
 #ifndef MI355X_I8_V3
 #define MI355X_I8_V3 0
 #endif
