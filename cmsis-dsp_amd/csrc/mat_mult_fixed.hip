@@ -761,7 +761,7 @@ static hipError_t launch_fixed(int m, int k, int n, const T* a, const T* b, T* c
     const bool full = m % G::BM == 0 && n % G::BN == 0 && k % G::KT == 0 &&
                       ((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0 && (k * sizeof(T)) % 16 == 0 &&
                       (n * sizeof(T)) % 16 == 0 && ((uintptr_t)c & 15) == 0;
-    if (MI355X_I8_V3) {
+    if (MI355X_I8_V3 == 1 || (MI355X_I8_V3 == 2 && sizeof(T) == 4)) {   // 2: q31 only
       if (full)
         hipLaunchKernelGGL((mat_mult_i8v3_kernel<T, true>), dim3(tiles * batch), dim3(kNT2), 0, st, a, b, c, m, k, n,
                            fast);

@@ -113,10 +113,10 @@
 #define MI355X_I8_STAMPS 0
 #endif
 #ifndef MI355X_I8_B8        // q15: B staged by 8-row x column-pair threads (ds_write_b64)
-#define MI355X_I8_B8 0
+#define MI355X_I8_B8 1
 #endif
 #ifndef MI355X_I8_V3
-#define MI355X_I8_V3 0
+#define MI355X_I8_V3 2
 #endif
 
 // ---- mfcc_f32.hip
