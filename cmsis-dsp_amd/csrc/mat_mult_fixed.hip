@@ -352,6 +352,41 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
               acc[p + q][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kk][p][i], fb[kk][q][j], acc[p + q][i][j], 0, 0, 0);
   };
 
+  // SPLIT: the second MFMA k-step (kk = 1) of K step kt runs at the head of step kt + 1, from
+  // registers, while that step's first fragment reads are in flight (the barrier only orders the
+  // LDS; register fragments may cross it)
+  constexpr bool SPLIT = MI355X_I8_SPLIT && KS == 2;
+  i32x4 ga[P][WBM], gb[P][WBN], ha[P][WBM], hb[P][WBN];   // SPLIT: kk = 0 / kk = 1 fragments
+  auto frags_kk = [&](int buf, int kk, i32x4 (&FA)[P][WBM], i32x4 (&FB)[P][WBN]) {
+    auto As = reinterpret_cast<const int8_t (*)[BM][kPitch2]>(lds + buf * BUF);
+    auto Bs = reinterpret_cast<const int8_t (*)[BN][kPitch2]>(lds + buf * BUF + P * BM * kPitch2);
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+#pragma unroll
+      for (int i = 0; i < WBM; ++i) {
+        const int row = wm * 32 * WBM + i * 32 + r;
+        FA[p][i] = *reinterpret_cast<const i32x4*>(&As[p][row][16 * i8_chunk(row, 2 * kk + h)]);
+      }
+#pragma unroll
+      for (int j = 0; j < WBN; ++j) {
+        const int n = wn * 32 * WBN + j * 32 + r;
+        const int row = B8 ? i8_brow8(n) : i8_brow<CW>(n);
+        FB[p][j] = *reinterpret_cast<const i32x4*>(&Bs[p][row][16 * i8_chunk(row, 2 * kk + h)]);
+      }
+    }
+  };
+  auto mma_kk = [&](const i32x4 (&FA)[P][WBM], const i32x4 (&FB)[P][WBN]) {
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int i = 0; i < WBM; ++i)
+#pragma unroll
+          for (int j = 0; j < WBN; ++j)
+            acc[p + q][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[p][i], FB[q][j], acc[p + q][i][j], 0, 0, 0);
+  };
+
   // Double-buffered K loop: step kt's fragments are read from buffer kt&1 first, then step
   // kt+1's planes are staged into the other buffer and step kt+2's global loads issued, and
   // the MFMAs (register-only) can interleave with that staging work; one barrier per step.
@@ -362,7 +397,43 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
   __syncthreads();
   I8_STAMP(1);
   int kt = 0;
-  for (; kt + 2 < nk; ++kt) {                    // steady state: one basic block when FULL
+  if constexpr (SPLIT) {
+    frags_kk(0, 0, ga, gb);                      // step 0: nothing outstanding yet
+    frags_kk(0, 1, ha, hb);
+    if (nk > 1) stage(1);
+    if (nk > 2) load(2 * kKT2);
+    mma_kk(ga, gb);
+    __syncthreads();
+    kt = 1;
+    for (; kt + 2 < nk; ++kt) {                  // steady state: one basic block when FULL
+      const int cur = kt & 1;
+      frags_kk(cur, 0, ga, gb);
+      mma_kk(ha, hb);                            // step kt - 1, kk = 1
+      frags_kk(cur, 1, ha, hb);
+      stage(cur ^ 1);
+      load((kt + 2) * kKT2);
+      mma_kk(ga, gb);
+#if MI355X_I8_SCHED
+#pragma unroll
+      for (int i = 0; i < 2 * P * P * WBM * WBN; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, MI355X_I8_SCHED, 0);
+      }
+#endif
+      __syncthreads();
+    }
+    for (; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      frags_kk(cur, 0, ga, gb);
+      mma_kk(ha, hb);
+      frags_kk(cur, 1, ha, hb);
+      if (kt + 1 < nk) stage(cur ^ 1);
+      mma_kk(ga, gb);
+      __syncthreads();
+    }
+    mma_kk(ha, hb);                              // the last step's kk = 1
+  }
+  for (; !SPLIT && kt + 2 < nk; ++kt) {           // steady state: one basic block when FULL
     const int cur = kt & 1;
     frags(cur);
     stage(cur ^ 1);
@@ -377,7 +448,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
 #endif
     __syncthreads();
   }
-  for (; kt < nk; ++kt) {
+  for (; !SPLIT && kt < nk; ++kt) {
     const int cur = kt & 1;
     frags(cur);
     if (kt + 1 < nk) stage(cur ^ 1);

@@ -115,6 +115,9 @@
 #ifndef MI355X_I8_B8        // q15: B staged by 8-row x column-pair threads (ds_write_b64)
 #define MI355X_I8_B8 1
 #endif
+#ifndef MI355X_I8_SPLIT     // v2: a K step's second MFMA k-step issued under the next step's fragment reads
+#define MI355X_I8_SPLIT 1
+#endif
 #ifndef MI355X_I8_V3
 #define MI355X_I8_V3 2
 #endif
