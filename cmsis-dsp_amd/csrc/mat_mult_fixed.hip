@@ -568,7 +568,10 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v3_kernel(const T* __restrict
   constexpr int EB = GB::EB, EBD = EB / EPD, TPR = GB::TPR, BP = GB::PITCH;
   constexpr int ABUF = P * BM * kPitch2, BBUF = P * kKT2 * BP;
   constexpr int BUF = ABUF + BBUF;
-  __shared__ __attribute__((aligned(16))) int8_t lds[2 * BUF];
+  // the epilogue reuses the plane buffers: partial sums (one column partial per staged k-row),
+  // final sums and the output tile
+  constexpr int EPI = (AQ * BM + kKT2 * BN + BM + BN) * 8 + BM * BN * (int)sizeof(T);
+  __shared__ __attribute__((aligned(16))) int8_t lds[2 * BUF > EPI ? 2 * BUF : EPI];
 
   const int tilesN = (N + BN - 1) / BN, tiles = tilesN * ((M + BM - 1) / BM);
   const uint32_t total = gridDim.x;
@@ -737,13 +740,84 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v3_kernel(const T* __restrict
               acc[p + q][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kk][p][i], fb[kk][q][j], acc[p + q][i][j], 0, 0, 0);
   };
 
+  // as v2 (kk = 1 MFMAs under the next step's reads) for q15 only: with q31's four planes the two
+  // fragment sets spill
+  constexpr bool SPLIT = MI355X_I8_SPLIT && KS == 2 && sizeof(T) == 2;
+  i32x4 ga[P][WBM], gb[P][WBN], ha[P][WBM], hb[P][WBN];
+  auto frags_kk = [&](int buf, int kk, i32x4 (&FA)[P][WBM], i32x4 (&FB)[P][WBN]) {
+    auto As = reinterpret_cast<const int8_t (*)[BM][kPitch2]>(lds + buf * BUF);
+    const int8_t* Bs = lds + buf * BUF + ABUF;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+#pragma unroll
+      for (int i = 0; i < WBM; ++i) {
+        const int row = wm * 32 * WBM + i * 32 + r;
+        FA[p][i] = *reinterpret_cast<const i32x4*>(&As[p][row][16 * i8_chunk(row, 2 * kk + h)]);
+      }
+#pragma unroll
+      for (int j = 0; j < WBN; ++j) {
+        const int col = wn * 32 * WBN + j * 32 + 16 * gq + 8 * (li & 1);
+        const int8_t* b0 = Bs + (size_t)p * kKT2 * BP + (32 * kk + 16 * h + (li >> 1)) * BP + col;
+        const v2i32_t lo = tr_b8(b0), hi = tr_b8(b0 + 8 * BP);
+        FB[p][j] = i32x4{lo.x, lo.y, hi.x, hi.y};
+      }
+    }
+  };
+  auto mma_kk = [&](const i32x4 (&FA)[P][WBM], const i32x4 (&FB)[P][WBN]) {
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int i = 0; i < WBM; ++i)
+#pragma unroll
+          for (int j = 0; j < WBN; ++j)
+            acc[p + q][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[p][i], FB[q][j], acc[p + q][i][j], 0, 0, 0);
+  };
+
   const int nk = (K + kKT2 - 1) / kKT2;
   load(0);
   stage(0);
   if (nk > 1) load(kKT2);
   __syncthreads();
   int kt = 0;
-  for (; kt + 2 < nk; ++kt) {
+  if constexpr (SPLIT) {
+    frags_kk(0, 0, ga, gb);
+    frags_kk(0, 1, ha, hb);
+    if (nk > 1) stage(1);
+    if (nk > 2) load(2 * kKT2);
+    mma_kk(ga, gb);
+    __syncthreads();
+    kt = 1;
+    for (; kt + 2 < nk; ++kt) {
+      const int cur = kt & 1;
+      frags_kk(cur, 0, ga, gb);
+      mma_kk(ha, hb);
+      frags_kk(cur, 1, ha, hb);
+      stage(cur ^ 1);
+      load((kt + 2) * kKT2);
+      mma_kk(ga, gb);
+#if MI355X_I8_SCHED
+#pragma unroll
+      for (int i = 0; i < 2 * P * P * WBM * WBN; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, MI355X_I8_SCHED, 0);
+      }
+#endif
+      __syncthreads();
+    }
+    for (; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      frags_kk(cur, 0, ga, gb);
+      mma_kk(ha, hb);
+      frags_kk(cur, 1, ha, hb);
+      if (kt + 1 < nk) stage(cur ^ 1);
+      mma_kk(ga, gb);
+      __syncthreads();
+    }
+    mma_kk(ha, hb);
+  }
+  for (; !SPLIT && kt + 2 < nk; ++kt) {
     const int cur = kt & 1;
     frags(cur);
     stage(cur ^ 1);
@@ -758,7 +832,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v3_kernel(const T* __restrict
 #endif
     __syncthreads();
   }
-  for (; kt < nk; ++kt) {
+  for (; !SPLIT && kt < nk; ++kt) {
     const int cur = kt & 1;
     frags(cur);
     if (kt + 1 < nk) stage(cur ^ 1);
@@ -766,19 +840,34 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v3_kernel(const T* __restrict
     __syncthreads();
   }
 
-  // ---- epilogue: exact sums through LDS, int64 combine (as v2)
+  // ---- epilogue (as v2): partial sums reduced once, the output tile staged in LDS, 16-B stores
+  constexpr int NQB = kKT2;                                 // one column partial per staged k-row
   int64_t* rs = reinterpret_cast<int64_t*>(lds);            // [AQ][BM]
   int64_t* cs = rs + AQ * BM;                               // [64 k-rows][BN]
+  int64_t* rfin = cs + NQB * BN;
+  int64_t* cfin = rfin + BM;
+  T* ct = reinterpret_cast<T*>(cfin + BN);
   rs[(tid % AQ) * BM + ar] = my_rsum;
 #pragma unroll
   for (int c = 0; c < EB; ++c) cs[bk * BN + bc + c] = (int64_t)my_csum[c];
+  __syncthreads();
+  for (int i = tid; i < BM + BN; i += kNT2) {
+    int64_t sum = 0;
+    if (i < BM) {
+#pragma unroll
+      for (int q = 0; q < AQ; ++q) sum += rs[q * BM + i];
+      rfin[i] = sum;
+    } else {
+      for (int q = 0; q < NQB; ++q) sum += cs[q * BN + (i - BM)];
+      cfin[i - BM] = sum;
+    }
+  }
   __syncthreads();
   const int64_t kpad = (int64_t)nk * kKT2;
 #pragma unroll
   for (int j = 0; j < WBN; ++j) {
     const int cc = wn * 32 * WBN + j * 32 + r;
-    int64_t csum = 0;
-    for (int q = 0; q < kKT2; ++q) csum += cs[q * BN + cc];
+    const int64_t csum = cfin[cc];
     const int gcol = col0 + cc;
 #pragma unroll
     for (int i = 0; i < WBM; ++i) {
@@ -786,19 +875,26 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v3_kernel(const T* __restrict
       for (int reg = 0; reg < 16; ++reg) {
         const int rr = wm * 32 * WBM + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
         const int grow = row0 + rr;
-        int64_t rsum = 0;
-#pragma unroll
-        for (int q = 0; q < AQ; ++q) rsum += rs[q * BM + rr];
-        uint64_t v = (uint64_t)(C0 * (rsum + csum)) - (uint64_t)kpad * (uint64_t)(C0 * C0);
+        uint64_t v = (uint64_t)(C0 * (rfin[rr] + csum)) - (uint64_t)kpad * (uint64_t)(C0 * C0);
 #pragma unroll
         for (int s2 = 0; s2 < S; ++s2) v += (uint64_t)(int64_t)acc[s2][i][j][reg] << (8 * s2);
-        if (FULL || (grow < M && gcol < N)) {
-          const int64_t sum = (int64_t)v;
-          if constexpr (sizeof(T) == 2)
-            C[(size_t)grow * N + gcol] = fast ? (T)((int32_t)(uint32_t)v >> 15) : (T)ssat16((int32_t)(sum >> 15));
-          else C[(size_t)grow * N + gcol] = (T)(int32_t)(sum >> 31);
-        }
+        const int64_t sum = (int64_t)v;
+        T o;
+        if constexpr (sizeof(T) == 2) o = fast ? (T)((int32_t)(uint32_t)v >> 15) : (T)ssat16((int32_t)(sum >> 15));
+        else o = (T)(int32_t)(sum >> 31);
+        if constexpr (FULL) ct[rr * BN + cc] = o;
+        else if (grow < M && gcol < N) C[(size_t)grow * N + gcol] = o;
       }
+    }
+  }
+  if constexpr (FULL) {
+    __syncthreads();
+    constexpr int VPR = BN * (int)sizeof(T) / 16;
+#pragma unroll
+    for (int w = tid; w < BM * VPR; w += kNT2) {
+      const int rr = w / VPR, cw = w % VPR;
+      *reinterpret_cast<uint4*>(C + (size_t)(row0 + rr) * N + col0 + cw * (16 / (int)sizeof(T))) =
+          *reinterpret_cast<const uint4*>(ct + rr * BN + cw * (16 / (int)sizeof(T)));
     }
   }
 }
