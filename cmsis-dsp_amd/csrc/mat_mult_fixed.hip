@@ -797,11 +797,11 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v3_kernel(const T* __restrict
       stage(cur ^ 1);
       load((kt + 2) * kKT2);
       mma_kk(ga, gb);
-#if MI355X_I8_SCHED
+#if MI355X_I8_SCHED_V3
 #pragma unroll
       for (int i = 0; i < 2 * P * P * WBM * WBN; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, MI355X_I8_SCHED, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, MI355X_I8_SCHED_V3, 0);
       }
 #endif
       __syncthreads();
@@ -823,11 +823,11 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v3_kernel(const T* __restrict
     stage(cur ^ 1);
     load((kt + 2) * kKT2);
     mma();
-#if MI355X_I8_SCHED
+#if MI355X_I8_SCHED_V3
 #pragma unroll
     for (int i = 0; i < KS * P * P * WBM * WBN; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                 // one MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, MI355X_I8_SCHED, 0);   // then VALU
+      __builtin_amdgcn_sched_group_barrier(0x002, MI355X_I8_SCHED_V3, 0);   // then VALU
     }
 #endif
     __syncthreads();
