@@ -436,7 +436,13 @@ bool mfcc_fx_prepare(const Inst* S, MfccFxDev<T>& d) {
     int4* twh = reinterpret_cast<int4*>(u + 3 * b_u + b_bf);
     for (uint32_t k = 1; k < n / 2; ++k) {
       const uint32_t c = 2 * mod * k;
-      twh[k] = make_int4(ta[c], ta[c + 1], tb[c], tb[c + 1]);
+      if constexpr (sizeof(T) == 2) {   // q15: packed pairs for v_dot2 (mfcc_fixed_post.hpp mq_split_q15)
+        auto p2 = [](int32_t lo, int32_t hi) { return (int32_t)((uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16)); };
+        const int32_t a0 = ta[c], a1 = ta[c + 1], b0 = tb[c], b1 = tb[c + 1];
+        twh[k] = make_int4(p2(a0, ~a1), p2(b0, b1), p2(b1, ~b0), p2(a1, a0));
+      } else {
+        twh[k] = make_int4(ta[c], ta[c + 1], tb[c], tb[c + 1]);
+      }
     }
   }
   const uint8_t* dev = (const uint8_t*)device_blob(blob.data(), blob.size());

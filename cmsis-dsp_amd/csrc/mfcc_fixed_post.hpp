@@ -9,6 +9,8 @@
 
 namespace mi355x {
 
+typedef short s2x __attribute__((ext_vector_type(2)));
+
 // arm_sqrt_q31.c:55-125 (Newton on 1/sqrt from sqrt_initial_lut_q31, 3 iterations)
 // lutv: lane l holds sqrt_initial_lut_q31[l & 31]; the entry is fetched with a lane shuffle
 // (every lane of the wave must be active: callers run uniform loops)
@@ -90,10 +92,18 @@ __device__ __forceinline__ int2 mq_split_q31(Get get, int k, int L, int4 t) {
 }
 template <typename Get>   // get(i): bin i as int2 of sign-extended q15 words
 __device__ __forceinline__ int2 mq_split_q15(Get get, int k, int L, int4 t) {
+  // t: the packed record of bin k (mfcc_fx_prepare): {(A0, ~A1), (B0, B1), (B1, ~B0), (A1, A0)} as
+  // q15 pairs, A0 = A[2mk] ... B1 = B[2mk + 1].  A difference x*w is x*~w + x (~w = -w - 1 fits a
+  // q15 word for every w), so each output is two v_dot2_i32_i16 (int32 wrap, as the reference's
+  // uint32 sums) with the missing term as the accumulator:
+  //   re = a.x A0 - a.y A1 + b.x B0 + b.y B1,   im = b.x B1 - b.y B0 + a.y A0 + a.x A1
   const int2 a = get(k & (L - 1)), b = get((L - k) & (L - 1));
-  auto p = [](int32_t u, int32_t v) { return (uint32_t)(u * v); };
-  const int32_t re = (int32_t)(p(a.x, t.x) - p(a.y, t.y) + p(b.x, t.z) + p(b.y, t.w)) >> 16;
-  const int32_t im = (int32_t)(p(b.x, t.w) - p(b.y, t.z) + p(a.y, t.x) + p(a.x, t.y)) >> 16;
+  auto pk = [](int2 v) { return __builtin_bit_cast(s2x, __builtin_amdgcn_perm((uint32_t)v.y, (uint32_t)v.x, 0x05040100u)); };
+  const s2x A = pk(a), B = pk(b);
+  const int32_t re = __builtin_amdgcn_sdot2(B, __builtin_bit_cast(s2x, t.y),
+                                            __builtin_amdgcn_sdot2(A, __builtin_bit_cast(s2x, t.x), a.y, false), false) >> 16;
+  const int32_t im = __builtin_amdgcn_sdot2(A, __builtin_bit_cast(s2x, t.w),
+                                            __builtin_amdgcn_sdot2(B, __builtin_bit_cast(s2x, t.z), b.y, false), false) >> 16;
   const bool edge = k == 0 || k == L;
   const int32_t ev = (k == 0 ? a.x + a.y : a.x - a.y) >> 1;
   return make_int2(edge ? ev : (int16_t)re, edge ? 0 : (int16_t)im);     // the split stores q15_t
@@ -224,7 +234,9 @@ struct MqOpsQ15 : MqPre<int16_t> {
       : le((int32_t)((uint32_t)(31 - (int)mq_clz((uint32_t)n) + 12) * 0x02C5C860u)), nb_mel(nm), nb_dct(nd) {}
   template <typename Get> __device__ int2 split(Get get, int k, int L, int4 t) const { return mq_split_q15(get, k, L, t); }
   __device__ int32_t mag(int2 c, int32_t lutv) const {   // arm_cmplx_mag_q15
-    const uint32_t s2 = ((uint32_t)(c.x * c.x) + (uint32_t)(c.y * c.y)) >> 1;
+    // (uint32)(x^2 + y^2) >> 1 as one v_dot2 (the same sum mod 2^32; x, y are q15 values)
+    const s2x p = __builtin_bit_cast(s2x, __builtin_amdgcn_perm((uint32_t)c.y, (uint32_t)c.x, 0x05040100u));
+    const uint32_t s2 = (uint32_t)__builtin_amdgcn_sdot2(p, p, 0, false) >> 1;
     return mq_sqrt((int32_t)s2, lutv) >> 16;
   }
   __device__ int64_t term(int32_t a, int32_t c) const { return (int64_t)(a * c); }   // arm_dot_prod_q15
