@@ -107,10 +107,10 @@
 
 // ---- mat_mult_fixed.hip
 #ifndef MI355X_I8_SCHED
-#define MI355X_I8_SCHED 6
+#define MI355X_I8_SCHED 10
 #endif
 #ifndef MI355X_I8_SCHED_V3  // the same hint in the tr_b8 kernel (q31)
-#define MI355X_I8_SCHED_V3 MI355X_I8_SCHED
+#define MI355X_I8_SCHED_V3 6
 #endif
 #ifndef MI355X_I8_STAMPS    // diagnostic: per-workgroup phase timestamps (mat_mult_fixed.hip)
 #define MI355X_I8_STAMPS 0
