@@ -426,6 +426,17 @@ def set_table_cache_limit(nbytes):
     lib.arm_mi355x_set_table_cache_limit(C.c_size_t(nbytes))
 
 
+def release_thread_resources():
+    """Free the calling thread's drop-in streams, scratch and staging now (automatic at the exit
+    of any thread but the main one)."""
+    lib.arm_mi355x_release_thread_resources()
+
+
+def thread_resource_owners():
+    """Number of threads currently holding per-thread runtime resources."""
+    return lib.arm_mi355x_thread_resource_owners()
+
+
 def rfft_fast_batch(S, p, out, ifft, stream=None):
     batch = p.numel() // S.fftLenRFFT
     st = lib.arm_rfft_fast_f32_batch(C.byref(S), C.c_void_p(p.data_ptr()), C.c_void_p(out.data_ptr()), batch,

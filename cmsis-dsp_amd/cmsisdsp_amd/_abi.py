@@ -321,6 +321,8 @@ BATCHED = {
     "arm_mi355x_version": (C.c_char_p, []),
     "arm_mi355x_table_cache_bytes": (C.c_size_t, []),
     "arm_mi355x_set_table_cache_limit": (None, [C.c_size_t]),
+    "arm_mi355x_release_thread_resources": (None, []),
+    "arm_mi355x_thread_resource_owners": (C.c_int, []),
 }
 
 # exported data symbols (arm_const_structs.h / arm_common_tables.h)

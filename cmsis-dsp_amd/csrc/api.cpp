@@ -1056,10 +1056,14 @@ extern "C" {
 #ifndef MI355X_BUILD_DEFS
 #define MI355X_BUILD_DEFS ""
 #endif
+#ifndef MI355X_SRC_ID
+#define MI355X_SRC_ID "unknown"
+#endif
+// "src:" is the sha256-based id of the sources the library was built from (Makefile SRC_ID);
 // "[...]" lists the non-default tuning macros of the build (Makefile DEFS, build_variant.sh)
 const char* arm_mi355x_version(void) {
-  return sizeof(MI355X_BUILD_DEFS) > 1 ? "cmsisdsp-mi355x 0.2.0 gfx950 [" MI355X_BUILD_DEFS "]"
-                                       : "cmsisdsp-mi355x 0.2.0 gfx950";
+  return sizeof(MI355X_BUILD_DEFS) > 1 ? "cmsisdsp-mi355x 0.3.0 gfx950 src:" MI355X_SRC_ID " [" MI355X_BUILD_DEFS "]"
+                                       : "cmsisdsp-mi355x 0.3.0 gfx950 src:" MI355X_SRC_ID;
 }
 
 void arm_cfft_f32(const arm_cfft_instance_f32* S, float32_t* p1, uint8_t ifftFlag, uint8_t bitReverseFlag) {

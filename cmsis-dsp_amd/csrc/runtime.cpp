@@ -8,7 +8,12 @@
 #include <link.h>
 #include <string.h>
 
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -173,14 +178,66 @@ uint64_t fnv1a(const uint8_t* p, size_t n) {
   return h;
 }
 
-struct Scratch { void* p = nullptr; size_t n = 0; };
-thread_local std::map<std::pair<int, int>, Scratch> g_scratch;
-struct Pinned { void* p = nullptr; size_t n = 0; };   // kept until process exit, like Scratch
-thread_local std::map<int, Pinned> g_pinned;
-thread_local std::map<int, Pinned> g_zpinned;      // coherent, device-accessed in place
-thread_local std::map<int, hipStream_t> g_streams;
-
 int cur_dev() { int d = 0; (void)hipGetDevice(&d); return d; }
+
+// ---- per-thread resources of the synchronous drop-in path ----------------------------------
+// The reference allocates nothing (SURVEY §8b "Ownership"); this backend needs, per calling
+// thread, a non-blocking stream per device, device scratch, pinned and coherent-pinned staging
+// and a coherent completion word.  They are owned by ONE thread_local object, so a thread that
+// exits gives them back: its destructor drains and destroys the streams, then frees the scratch,
+// the staging and the completion words.  The process's main thread keeps the
+// deliberate leak at process exit -- its thread_local destructors run during static destruction,
+// when the HIP runtime may already be gone.  arm_mi355x_release_thread_resources() releases the
+// calling thread's set explicitly (thread pools that recycle threads; the main thread).
+struct Scratch { void* p = nullptr; size_t n = 0; };
+struct Pinned { void* p = nullptr; size_t n = 0; };
+struct DoneWord { volatile uint32_t* h = nullptr; uint32_t* d = nullptr; uint32_t seq = 0; };
+
+std::atomic<int> g_live_owners{0};     // threads currently holding any of the resources below
+
+bool is_main_thread() { return (pid_t)syscall(SYS_gettid) == getpid(); }
+
+struct ThreadRes {
+  std::map<std::pair<int, int>, Scratch> scratch;   // (device, slot)
+  std::map<int, Pinned> pinned;                     // slot
+  std::map<int, Pinned> zpinned;                    // slot; coherent, device-accessed in place
+  std::map<int, hipStream_t> streams;               // device
+  std::map<int, DoneWord> done;                     // device
+  bool counted = false;
+
+  void touch() {
+    if (!counted) { counted = true; g_live_owners.fetch_add(1, std::memory_order_relaxed); }
+  }
+  void release() {
+    int prev = 0;
+    const bool have_prev = hipGetDevice(&prev) == hipSuccess;
+    for (auto& kv : streams) {                      // nothing of this thread may still be in flight
+      (void)hipSetDevice(kv.first);
+      (void)hipStreamSynchronize(kv.second);
+      (void)hipStreamDestroy(kv.second);
+    }
+    streams.clear();
+    for (auto& kv : scratch) {
+      if (!kv.second.p) continue;
+      (void)hipSetDevice(kv.first.first);
+      (void)hipFree(kv.second.p);
+    }
+    scratch.clear();
+    for (auto& kv : pinned) if (kv.second.p) (void)hipHostFree(kv.second.p);
+    pinned.clear();
+    for (auto& kv : zpinned) if (kv.second.p) (void)hipHostFree(kv.second.p);
+    zpinned.clear();
+    for (auto& kv : done) if (kv.second.h) (void)hipHostFree((void*)kv.second.h);
+    done.clear();
+    if (have_prev) (void)hipSetDevice(prev);
+    (void)hipGetLastError();
+    if (counted) { counted = false; g_live_owners.fetch_sub(1, std::memory_order_relaxed); }
+  }
+  ~ThreadRes() {
+    if (counted && !is_main_thread()) release();
+  }
+};
+thread_local ThreadRes t_res;
 
 // canonical permutations the reference tables induce (verified in tests/test_tables.py):
 // f32: position holding frequency k under the mixed-radix [FIRST, 8, 8, ...] DIF
@@ -431,7 +488,8 @@ const uint16_t* device_perm(int n, const uint16_t* table, uint16_t len, int kind
 
 void* scratch(size_t bytes, int slot) {
   const int dev = cur_dev();
-  Scratch& s = g_scratch[{dev, slot}];
+  t_res.touch();
+  Scratch& s = t_res.scratch[{dev, slot}];
   if (s.n < bytes) {
     if (s.p) (void)hipFree(s.p);
     s.p = nullptr;
@@ -443,7 +501,8 @@ void* scratch(size_t bytes, int slot) {
 }
 
 void* pinned(size_t bytes, int slot) {
-  Pinned& s = g_pinned[slot];
+  t_res.touch();
+  Pinned& s = t_res.pinned[slot];
   if (s.n < bytes) {
     if (s.p) (void)hipHostFree(s.p);
     s.p = nullptr;
@@ -455,7 +514,8 @@ void* pinned(size_t bytes, int slot) {
 }
 
 static void* zpinned(size_t bytes, int slot) {
-  Pinned& s = g_zpinned[slot];
+  t_res.touch();
+  Pinned& s = t_res.zpinned[slot];
   if (s.n < bytes) {
     if (s.p) (void)hipHostFree(s.p);
     s.p = nullptr;
@@ -516,8 +576,6 @@ HostIO::~HostIO() {
 // hipStreamSynchronize, which also reports errors) instead of the runtime's blocking wait.
 // CMSISDSP_MI355X_SYNC=sync|spin overrides the default (MI355X_SYNC_DEFAULT).
 namespace {
-struct DoneWord { volatile uint32_t* h = nullptr; uint32_t* d = nullptr; uint32_t seq = 0; };
-thread_local std::map<int, DoneWord> t_done;
 int sync_mode() {
   static const int m = [] {
     const char* e = getenv("CMSISDSP_MI355X_SYNC");
@@ -530,7 +588,8 @@ int sync_mode() {
 
 DoneWord* done_word() {
   const int dev = cur_dev();
-  DoneWord& w = t_done[dev];
+  t_res.touch();
+  DoneWord& w = t_res.done[dev];
   if (!w.h) {
     void* p = nullptr;
     if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;
@@ -557,13 +616,22 @@ bool done_slot(uint32_t** dflag, uint32_t* seq) {
   return true;
 }
 
+// How long a synchronous call spins (with a pause per poll) before it blocks in
+// hipStreamSynchronize: the small calls the spin exists for finish in ~10 us; a long call
+// (a large mat_mult or FIR) blocks after this instead of burning a core.
+constexpr auto kSpinBudget = std::chrono::microseconds(200);
+
 hipError_t wait_done(hipStream_t st, uint32_t seq) {
   DoneWord* w = done_word();
-  // spin up to ~2^22 polls (milliseconds); a slow or failed call falls through to the sync
-  if (w)
-    for (uint32_t i = 0; i < (1u << 22); ++i)
+  if (w) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0;; ++i) {
       if (__atomic_load_n(w->h, __ATOMIC_ACQUIRE) == seq) return hipSuccess;
-  return hipStreamSynchronize(st);
+      __builtin_ia32_pause();
+      if ((i & 63) == 63 && std::chrono::steady_clock::now() - t0 > kSpinBudget) break;
+    }
+  }
+  return hipStreamSynchronize(st);   // a slow or failed call: block (this also reports errors)
 }
 
 hipError_t wait_stream(hipStream_t st) {
@@ -587,13 +655,17 @@ hipError_t HostIO::finish(uint32_t seq) {
 
 hipStream_t sync_stream() {
   const int dev = cur_dev();
-  auto it = g_streams.find(dev);
-  if (it != g_streams.end()) return it->second;
+  auto it = t_res.streams.find(dev);
+  if (it != t_res.streams.end()) return it->second;
   hipStream_t s = nullptr;
   if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-  g_streams[dev] = s;
+  t_res.touch();
+  t_res.streams[dev] = s;
   return s;
 }
+
+void release_thread_resources() { t_res.release(); }
+int live_thread_owners() { return g_live_owners.load(std::memory_order_relaxed); }
 
 }  // namespace mi355x
 
@@ -603,4 +675,6 @@ const char* arm_mi355x_last_error_string(void) { return mi355x::g_err_msg.c_str(
 size_t arm_mi355x_table_cache_bytes(void) { return mi355x::blob_cache_bytes(); }
 void arm_mi355x_set_table_cache_limit(size_t bytes) { mi355x::set_blob_cache_limit(bytes); }
 void arm_mi355x_clear_error(void) { mi355x::clear_error(); }
+void arm_mi355x_release_thread_resources(void) { mi355x::release_thread_resources(); }
+int arm_mi355x_thread_resource_owners(void) { return mi355x::live_thread_owners(); }
 }

@@ -121,4 +121,10 @@ hipError_t wait_done(hipStream_t st, uint32_t seq);
 // The internal stream used by the synchronous drop-in API on the current device.
 hipStream_t sync_stream();
 
+// Drain and free the calling thread's streams, scratch, staging and completion words (done
+// automatically when a thread other than the main thread exits).  The next call re-creates them.
+void release_thread_resources();
+// Number of threads currently holding per-thread runtime resources.
+int live_thread_owners();
+
 }  // namespace mi355x

