@@ -62,6 +62,7 @@ WORKLOADS = {
     "rfft_q31": ("rfftq31", 8192, 1 << 16, 16),
     "rfft_q15": ("rfftq15", 8192, 1 << 16, 8),
     "conv_f32": ("conv", 128, 1 << 16, 8),
+    "mat_mult_q7": ("matq7", 1024, 64, None),
     "mat_mult_q15": ("matq15", 1024, 64, None),
     "mat_mult_q31": ("matq31", 1024, 64, None),
     "mat_mult_fast_q31": ("matfast_q31", 1024, 64, None),
@@ -175,7 +176,7 @@ _CPU_WL = {"cfft_f32_1024": "cfft_f32", "cfft_q31_4096": "cfft_q31", "cfft_q15_4
            "fir_fast_q15": "fir_fast_q15",
            "fir_fast_q31": "fir_fast_q31", "mat_mult_f32": "mat_mult_f32", "mfcc_f32": "mfcc_f32",
            "mfcc_q31": "mfcc_q31", "mfcc_q15": "mfcc_q15",
-           "mat_mult_q15": "mat_mult_q15", "mat_mult_q31": "mat_mult_q31", "mat_mult_fast_q31": "mat_mult_fast_q31",
+           "mat_mult_q7": "mat_mult_q7", "mat_mult_q15": "mat_mult_q15", "mat_mult_q31": "mat_mult_q31", "mat_mult_fast_q31": "mat_mult_fast_q31",
            "rfft_f32": "rfft_f32", "conv_f32": "conv_f32", "rfft_q31": "rfft_q31", "rfft_q15": "rfft_q15"}
 
 
@@ -243,8 +244,8 @@ def main_rank(args):
         g.manual_seed(parallel.seed_for(rank, salt))
         if kind == "f32":
             return torch.rand(n_words, generator=g, device="cuda", dtype=torch.float32) - 0.5
-        hi = 1 << (31 if kind == "q31" else 15)
-        dt = torch.int32 if kind == "q31" else torch.int16
+        hi = 1 << {"q31": 31, "q15": 15, "q7": 7}[kind]
+        dt = {"q31": torch.int32, "q15": torch.int16, "q7": torch.int8}[kind]
         return torch.randint(-hi, hi, (n_words,), generator=g, device="cuda", dtype=torch.int64).to(dt)
 
     def synth_global(kind, n, start, count, block=4096):
@@ -580,10 +581,11 @@ def main_rank(args):
         return wall, kern_ms, {"checker": hk, "frames_checked": 64, "bit_exact": bool(got.tobytes() == want.tobytes())}
 
     def run_mat_fixed(kind, dim, batch, steps, warmup):
-        """arm_mat_mult_q15 / _q31 (byte-sliced i8 MFMA) or _fast_q31 (VALU), full-range operands,
-        bit-exact check of matrix 0 against the CPU checker."""
-        a = synth(kind[-3:], batch * dim * dim).view(batch, dim, dim)
-        b = synth(kind[-3:], batch * dim * dim, salt=3).view(batch, dim, dim)
+        """arm_mat_mult_q7 (one i8 MFMA plane), _q15 / _q31 (byte-sliced i8 MFMA) or _fast_q31 (VALU),
+        full-range operands, bit-exact check of matrix 0 against the CPU checker."""
+        base = "q7" if kind == "q7" else kind[-3:]
+        a = synth(base, batch * dim * dim).view(batch, dim, dim)
+        b = synth(base, batch * dim * dim, salt=3).view(batch, dim, dim)
         c = torch.empty_like(a)
         fast = kind.startswith("fast")
 
@@ -649,7 +651,7 @@ def main_rank(args):
         wall, kern_ms, parity = run_fir(kind[4:], n, batch, args.steps, args.warmup)
         units = batch * 4096
         algo_bytes = units * bps + batch * (n - 1) * bps  # in + out + history read/write
-    elif args.workload in ("mat_mult_q15", "mat_mult_q31", "mat_mult_fast_q31"):
+    elif args.workload in ("mat_mult_q7", "mat_mult_q15", "mat_mult_q31", "mat_mult_fast_q31"):
         wall, kern_ms, parity = run_mat_fixed(kind[3:], n, batch, args.steps, args.warmup)
         units = batch
         algo_bytes = None
@@ -699,6 +701,21 @@ def main_rank(args):
         line["roofline"] = {"bound": "valu", "achieved": round(lane_ops, 2), "peak": 39.3,
                             "unit": "T VALU lane-instr/s (256 CU x 4 SIMD x 16 lanes x 2.4 GHz)",
                             "frac": round(lane_ops / 39.3, 4), "traffic": None, "avg_kernel_ms": round(kern_ms, 4)}
+    elif args.workload == "mat_mult_q7":
+        ops = 2.0 * n * n * n * batch
+        line.update(value=round(total_units * 2.0 * n ** 3 / wall * 1e-12, 4), unit="TOPS (2*M*N*K int MAC)",
+                    dtype="q7 (int8 x int8 -> int32, one i8 MFMA plane)",
+                    config={"workload": f"arm_mat_mult_q7 {n}x{n}x{n} batch={batch}/GPU",
+                            "dims": [n, n, n], "batch_per_gpu": batch, "parallelism": f"dp{world_n} shards"})
+        i8 = ops / (kern_ms * 1e-3) * 1e-12
+        hbm = 3.0 * n * n * batch / (kern_ms * 1e-3) * 1e-9       # A, B read once, C written once
+        line["roofline"] = {"bound": "mfma", "achieved": round(i8, 2), "peak": 5000.0,
+                            "unit": "TOPS (i8 MFMA, dense)", "frac": round(i8 / 5000.0, 4),
+                            "traffic": pmc_traffic(args.workload, batch), "avg_kernel_ms": round(kern_ms, 4),
+                            "mfma_busy": pmc_field(args.workload, "mfma_busy_frac", batch),
+                            "hbm_algorithmic": {"achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                                "frac": round(hbm / HBM_PEAK_GBS, 4),
+                                                "bytes_per_matrix": 3 * n * n}}
     elif args.workload in ("mat_mult_q15", "mat_mult_q31"):
         planes = 2 if args.workload.endswith("q15") else 4
         ops = 2.0 * n * n * n * batch

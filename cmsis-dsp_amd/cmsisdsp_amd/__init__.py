@@ -22,7 +22,7 @@ from ._abi import (arm_cfft_instance_f32, arm_cfft_instance_q15, arm_cfft_instan
                    arm_fir_instance_f32, arm_fir_instance_q15, arm_fir_instance_q31, arm_fir_instance_q7,
                    arm_matrix_instance_f32,
                    arm_rfft_fast_instance_f32, arm_mfcc_instance_f32, arm_mfcc_instance_q31, arm_mfcc_instance_q15,
-                   arm_matrix_instance_q15,
+                   arm_matrix_instance_q15, arm_matrix_instance_q7,
                    arm_matrix_instance_q31, arm_rfft_instance_q31, arm_rfft_instance_q15, ARM_MATH_SUCCESS,
                    ARM_MATH_ARGUMENT_ERROR, ARM_MATH_SIZE_MISMATCH)
 
@@ -496,7 +496,7 @@ def mat_mult_batch_multi(shards):
     a0, b0, _ = shards[0]
     m, k_, n = a0.shape[1], a0.shape[2], b0.shape[2]
     kind, inst = {torch.float32: ("f32", arm_matrix_instance_f32), torch.int16: ("q15", arm_matrix_instance_q15),
-                  torch.int32: ("q31", arm_matrix_instance_q31)}[a0.dtype]
+                  torch.int32: ("q31", arm_matrix_instance_q31), torch.int8: ("q7", arm_matrix_instance_q7)}[a0.dtype]
     for d in sorted({t[0].device.index for t in shards}):
         torch.cuda.synchronize(d)
     k = len(shards)
@@ -570,11 +570,11 @@ def conv_family_batch(fn, a, b, out, first=0, num=0, stream=None):
 
 
 def arm_mat_mult_fixed(kind, a, b):
-    """(status, C) = A @ B through arm_mat_mult_q15 / _q31 / _fast_q15 / _fast_q31 (kind
-    "q15", "q31", "fast_q15", "fast_q31"; row-major)."""
-    base = kind[-3:]
-    dt = np.int16 if base == "q15" else np.int32
-    inst = arm_matrix_instance_q15 if base == "q15" else arm_matrix_instance_q31
+    """(status, C) = A @ B through arm_mat_mult_q7 / _q15 / _q31 / _fast_q15 / _fast_q31 (kind
+    "q7", "q15", "q31", "fast_q15", "fast_q31"; row-major)."""
+    base = "q7" if kind == "q7" else kind[-3:]
+    dt = {"q7": np.int8, "q15": np.int16, "q31": np.int32}[base]
+    inst = {"q7": arm_matrix_instance_q7, "q15": arm_matrix_instance_q15, "q31": arm_matrix_instance_q31}[base]
     a = np.ascontiguousarray(a, dtype=dt)
     b = np.ascontiguousarray(b, dtype=dt)
     c = np.zeros((a.shape[0], b.shape[1]), dtype=dt)
@@ -584,21 +584,23 @@ def arm_mat_mult_fixed(kind, a, b):
     init(C.byref(B), b.shape[0], b.shape[1], b.ctypes.data)
     init(C.byref(Cm), c.shape[0], c.shape[1], c.ctypes.data)
     fn = getattr(lib, f"arm_mat_mult_{kind}")
-    st = fn(C.byref(A), C.byref(B), C.byref(Cm), None) if base == "q15" else fn(C.byref(A), C.byref(B), C.byref(Cm))
+    st = fn(C.byref(A), C.byref(B), C.byref(Cm), None) if base in ("q15", "q7") else \
+        fn(C.byref(A), C.byref(B), C.byref(Cm))
     _check_void(f"arm_mat_mult_{kind}")
     return st, c
 
 
 def mat_mult_batch(a, b, c, stream=None, fast=False):
     """c[i] = a[i] @ b[i] for device tensors [batch, M, K] x [batch, K, N] -> [batch, M, N];
-    float32 -> arm_mat_mult_f32_batch, int16 -> _q15, int32 -> _q31 (fast=True: _fast_q15 /
-    _fast_q31)."""
+    float32 -> arm_mat_mult_f32_batch, int8 -> _q7, int16 -> _q15, int32 -> _q31 (fast=True:
+    _fast_q15 / _fast_q31)."""
     import torch
     batch, m, k = a.shape
     n = b.shape[2]
     kind, inst, ptr = {torch.float32: ("f32", arm_matrix_instance_f32, _abi.c_f32p),
                        torch.int16: ("q15", arm_matrix_instance_q15, _abi.c_i16p),
-                       torch.int32: ("q31", arm_matrix_instance_q31, _abi.c_i32p)}[a.dtype]
+                       torch.int32: ("q31", arm_matrix_instance_q31, _abi.c_i32p),
+                       torch.int8: ("q7", arm_matrix_instance_q7, _abi.c_i8p)}[a.dtype]
     A, B, Cm = inst(m, k, C.cast(a.data_ptr(), ptr)), inst(k, n, C.cast(b.data_ptr(), ptr)), \
         inst(m, n, C.cast(c.data_ptr(), ptr))
     fn = getattr(lib, f"arm_mat_mult_{'fast_' if fast and kind != 'f32' else ''}{kind}_batch")

@@ -10,6 +10,7 @@ import ctypes as C
 c_f32p = C.POINTER(C.c_float)
 c_i32p = C.POINTER(C.c_int32)
 c_i16p = C.POINTER(C.c_int16)
+c_i8p = C.POINTER(C.c_int8)
 c_u16p = C.POINTER(C.c_uint16)
 
 ARM_MATH_SUCCESS = 0
@@ -115,6 +116,11 @@ class arm_mfcc_instance_q15(C.Structure):
                 ("rfft", arm_rfft_instance_q15)]
 
 
+class arm_matrix_instance_q7(C.Structure):
+    # Include/dsp/matrix_functions.h:139-143
+    _fields_ = [("numRows", C.c_uint16), ("numCols", C.c_uint16), ("pData", c_i8p)]
+
+
 class arm_matrix_instance_q15(C.Structure):
     # Include/dsp/matrix_functions.h:139-144
     _fields_ = [("numRows", C.c_uint16), ("numCols", C.c_uint16), ("pData", c_i16p)]
@@ -187,7 +193,10 @@ DROPIN = {
     **{f"arm_fir_sparse_{t}": (None, [P(arm_fir_sparse_instance), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_uint32]) for t in ("q15", "q7")},
     "arm_mat_init_f32": (None, [P(arm_matrix_instance_f32), C.c_uint16, C.c_uint16, C.c_void_p]),
+    "arm_mat_init_q7": (None, [P(arm_matrix_instance_q7), C.c_uint16, C.c_uint16, C.c_void_p]),
     "arm_mat_init_q15": (None, [P(arm_matrix_instance_q15), C.c_uint16, C.c_uint16, C.c_void_p]),
+    "arm_mat_mult_q7": (C.c_int, [P(arm_matrix_instance_q7), P(arm_matrix_instance_q7),
+                                  P(arm_matrix_instance_q7), C.c_void_p]),
     "arm_mat_init_q31": (None, [P(arm_matrix_instance_q31), C.c_uint16, C.c_uint16, C.c_void_p]),
     "arm_mat_mult_q15": (C.c_int, [P(arm_matrix_instance_q15), P(arm_matrix_instance_q15),
                                    P(arm_matrix_instance_q15), C.c_void_p]),
@@ -283,6 +292,8 @@ BATCHED = {
                                                C.c_uint32, C.c_void_p, C.c_void_p]) for t in ("f32", "q31", "q15", "q7")},
     "arm_mat_mult_f32_batch": (C.c_int, [P(arm_matrix_instance_f32), P(arm_matrix_instance_f32),
                                          P(arm_matrix_instance_f32), C.c_uint32, C.c_void_p]),
+    "arm_mat_mult_q7_batch": (C.c_int, [P(arm_matrix_instance_q7), P(arm_matrix_instance_q7),
+                                        P(arm_matrix_instance_q7), C.c_uint32, C.c_void_p]),
     "arm_mat_mult_q15_batch": (C.c_int, [P(arm_matrix_instance_q15), P(arm_matrix_instance_q15),
                                          P(arm_matrix_instance_q15), C.c_uint32, C.c_void_p]),
     "arm_mat_mult_q31_batch": (C.c_int, [P(arm_matrix_instance_q31), P(arm_matrix_instance_q31),
@@ -313,7 +324,7 @@ BATCHED = {
     **{f"arm_mat_mult_{t}_batch_multi": (C.c_int, [P(inst), P(inst), P(inst), C.c_uint32, C.c_void_p, C.c_void_p,
                                                    C.c_void_p, C.c_void_p, C.c_void_p])
        for t, inst in (("f32", arm_matrix_instance_f32), ("q15", arm_matrix_instance_q15),
-                       ("q31", arm_matrix_instance_q31))},
+                       ("q31", arm_matrix_instance_q31), ("q7", arm_matrix_instance_q7))},
     "arm_mi355x_device_count": (C.c_int, []),
     "arm_mi355x_last_error": (C.c_int, []),
     "arm_mi355x_last_error_string": (C.c_char_p, []),

@@ -1021,7 +1021,9 @@ arm_status mat_mult_fixed_sync(const M* pSrcA, const M* pSrcB, M* pDst, bool fas
   if (!da) e = io.in(A, pSrcA->pData, ab);
   if (e == hipSuccess && !db) e = io.in(B, pSrcB->pData, bb);
   if (e == hipSuccess) {
-    if constexpr (sizeof(T) == 2)
+    if constexpr (sizeof(T) == 1)
+      e = mat_mult_q7_launch(m, k, n, A, B, Cd, 1, st);
+    else if constexpr (sizeof(T) == 2)
       e = fast ? mat_mult_fast_q15_launch(m, k, n, A, B, Cd, 1, st) : mat_mult_q15_launch(m, k, n, A, B, Cd, 1, st);
     else
       e = fast ? mat_mult_fast_q31_launch(m, k, n, A, B, Cd, 1, st) : mat_mult_q31_launch(m, k, n, A, B, Cd, 1, st);
@@ -1236,6 +1238,13 @@ arm_status arm_mat_mult_f32_batch_multi(const arm_matrix_instance_f32* pSrcA, co
   return mat_batch_multi<float>(pSrcA, pSrcB, pDst, nshards, devices, d_a, d_b, d_c, batch,
                                 "arm_mat_mult_f32_batch_multi", mat_mult_f32_launch);
 }
+arm_status arm_mat_mult_q7_batch_multi(const arm_matrix_instance_q7* pSrcA, const arm_matrix_instance_q7* pSrcB,
+                                       arm_matrix_instance_q7* pDst, uint32_t nshards, const int* devices,
+                                       const q7_t* const* d_a, const q7_t* const* d_b, q7_t* const* d_c,
+                                       const uint32_t* batch) {
+  return mat_batch_multi<int8_t>(pSrcA, pSrcB, pDst, nshards, devices, d_a, d_b, d_c, batch,
+                                 "arm_mat_mult_q7_batch_multi", mat_mult_q7_launch);
+}
 arm_status arm_mat_mult_q15_batch_multi(const arm_matrix_instance_q15* pSrcA, const arm_matrix_instance_q15* pSrcB,
                                         arm_matrix_instance_q15* pDst, uint32_t nshards, const int* devices,
                                         const q15_t* const* d_a, const q15_t* const* d_b, q15_t* const* d_c,
@@ -1375,7 +1384,23 @@ arm_status arm_mfcc_q15_batch(const arm_mfcc_instance_q15* S, q15_t* d_src, q15_
   return mfcc_fx_batch<int16_t>(S, d_src, d_dst, d_tmp, batch, stream);
 }
 
-// ---- matrix multiply q15 / q31 --------------------------------------------------
+// ---- matrix multiply q7 / q15 / q31 ---------------------------------------------
+// arm_mat_mult_q7.c:689-790 (scalar branch): q31_t sum of exact q7 products (never wraps for
+// uint16_t dimensions), (q7)__SSAT(sum >> 7, 8); pState (the Helium/Neon transpose buffer) unused.
+arm_status arm_mat_mult_q7(const arm_matrix_instance_q7* pSrcA, const arm_matrix_instance_q7* pSrcB,
+                           arm_matrix_instance_q7* pDst, q7_t* pState) {
+  (void)pState;
+  return mat_mult_fixed_sync<int8_t>(pSrcA, pSrcB, pDst);
+}
+arm_status arm_mat_mult_q7_batch(const arm_matrix_instance_q7* pSrcA, const arm_matrix_instance_q7* pSrcB,
+                                 arm_matrix_instance_q7* pDst, uint32_t batch, void* stream) {
+  if (!pSrcA || !pSrcB || !pDst) return ARM_MATH_ARGUMENT_ERROR;
+  if (!mat_shapes_ok(pSrcA, pSrcB, pDst)) return ARM_MATH_SIZE_MISMATCH;
+  hipError_t e = mat_mult_q7_launch(pSrcA->numRows, pSrcA->numCols, pSrcB->numCols, pSrcA->pData, pSrcB->pData,
+                                    pDst->pData, batch, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(e, "arm_mat_mult_q7_batch"); return ARM_MATH_ARGUMENT_ERROR; }
+  return ARM_MATH_SUCCESS;
+}
 arm_status arm_mat_mult_q15(const arm_matrix_instance_q15* pSrcA, const arm_matrix_instance_q15* pSrcB,
                             arm_matrix_instance_q15* pDst, q15_t* pState) {
   (void)pState;   // the reference's transpose buffer (ARM_MATH_DSP branch only)

@@ -275,7 +275,12 @@ MI_MFCC_Q15_INIT(4096)
 
 // (FIR init zeroes a state buffer that may be device memory: it lives in api.cpp.)
 
-// ---- matrix init (arm_mat_init_f32.c, arm_mat_init_q15.c, arm_mat_init_q31.c)
+// ---- matrix init (arm_mat_init_f32.c, arm_mat_init_q7.c, arm_mat_init_q15.c, arm_mat_init_q31.c)
+void arm_mat_init_q7(arm_matrix_instance_q7* S, uint16_t nRows, uint16_t nColumns, q7_t* pData) {
+  S->numRows = nRows;
+  S->numCols = nColumns;
+  S->pData = pData;
+}
 void arm_mat_init_q15(arm_matrix_instance_q15* S, uint16_t nRows, uint16_t nColumns, q15_t* pData) {
   S->numRows = nRows;
   S->numCols = nColumns;

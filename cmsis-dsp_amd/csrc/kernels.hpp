@@ -182,6 +182,10 @@ hipError_t mat_mult_q15_launch(int m, int k, int n, const int16_t* a, const int1
                                hipStream_t st);
 hipError_t mat_mult_q31_launch(int m, int k, int n, const int32_t* a, const int32_t* b, int32_t* c, uint32_t batch,
                                hipStream_t st);
+// Row-major q7 C[b] = A[b] * B[b] (arm_mat_mult_q7 semantics, bit-exact): one i8 MFMA plane
+// (mat_mult_q7.hip).
+hipError_t mat_mult_q7_launch(int m, int k, int n, const int8_t* a, const int8_t* b, int8_t* c, uint32_t batch,
+                              hipStream_t st);
 // arm_mat_mult_fast_q15 (exact i8-plane GEMM, modular q31 sum, (q15)(sum >> 15)) and
 // arm_mat_mult_fast_q31 (VALU: sum of per-product (a*b) >> 32, output << 1).
 hipError_t mat_mult_fast_q15_launch(int m, int k, int n, const int16_t* a, const int16_t* b, int16_t* c,

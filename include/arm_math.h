@@ -730,6 +730,13 @@ arm_status arm_mat_mult_f32(const arm_matrix_instance_f32 *pSrcA,
  * sum of exact products, __SSAT(sum >> 15, 16)), arm_mat_mult_q31.c:53-163 (q63 sum,
  * (q31)(sum >> 31)).  Bit-exact; pState is accepted and unused.  Size check always on. */
 void arm_mat_init_q15(arm_matrix_instance_q15 *S, uint16_t nRows, uint16_t nColumns, q15_t *pData);
+/* q7: matrix_functions.h:379-383 (arm_mat_mult_q7), :617-621 (arm_mat_init_q7); body
+ * Source/MatrixFunctions/arm_mat_mult_q7.c:689-790 (scalar branch: q31_t sum of exact products,
+ * (q7)__SSAT(sum >> 7, 8)), Source/MatrixFunctions/arm_mat_init_q7.c.  Bit-exact on one i8 MFMA
+ * plane; pState is accepted and unused. */
+void arm_mat_init_q7(arm_matrix_instance_q7 *S, uint16_t nRows, uint16_t nColumns, q7_t *pData);
+arm_status arm_mat_mult_q7(const arm_matrix_instance_q7 *pSrcA, const arm_matrix_instance_q7 *pSrcB,
+                           arm_matrix_instance_q7 *pDst, q7_t *pState);
 void arm_mat_init_q31(arm_matrix_instance_q31 *S, uint16_t nRows, uint16_t nColumns, q31_t *pData);
 arm_status arm_mat_mult_q15(const arm_matrix_instance_q15 *pSrcA, const arm_matrix_instance_q15 *pSrcB,
                             arm_matrix_instance_q15 *pDst, q15_t *pState);

@@ -208,7 +208,10 @@ arm_status arm_correlate_q7_batch(const q7_t *d_a, uint32_t srcALen, uint32_t st
  * item).  Returns ARM_MATH_SIZE_MISMATCH on incompatible shapes (arm_mat_mult_f32.c:618-630). */
 arm_status arm_mat_mult_f32_batch(const arm_matrix_instance_f32 *pSrcA, const arm_matrix_instance_f32 *pSrcB,
                                   arm_matrix_instance_f32 *pDst, uint32_t batch, void *stream);
-/* q15 / q31 analogues (bit-exact; byte-sliced planes on the i8 matrix cores). */
+/* q7 / q15 / q31 analogues (bit-exact; q7 on one i8 matrix-core plane, q15 / q31 byte-sliced
+ * planes on the i8 matrix cores). */
+arm_status arm_mat_mult_q7_batch(const arm_matrix_instance_q7 *pSrcA, const arm_matrix_instance_q7 *pSrcB,
+                                 arm_matrix_instance_q7 *pDst, uint32_t batch, void *stream);
 arm_status arm_mat_mult_q15_batch(const arm_matrix_instance_q15 *pSrcA, const arm_matrix_instance_q15 *pSrcB,
                                   arm_matrix_instance_q15 *pDst, uint32_t batch, void *stream);
 arm_status arm_mat_mult_q31_batch(const arm_matrix_instance_q31 *pSrcA, const arm_matrix_instance_q31 *pSrcB,
@@ -271,6 +274,10 @@ arm_status arm_mat_mult_f32_batch_multi(const arm_matrix_instance_f32 *pSrcA, co
                                         arm_matrix_instance_f32 *pDst, uint32_t nshards, const int *devices,
                                         const float32_t *const *d_a, const float32_t *const *d_b,
                                         float32_t *const *d_c, const uint32_t *batch);
+arm_status arm_mat_mult_q7_batch_multi(const arm_matrix_instance_q7 *pSrcA, const arm_matrix_instance_q7 *pSrcB,
+                                       arm_matrix_instance_q7 *pDst, uint32_t nshards, const int *devices,
+                                       const q7_t *const *d_a, const q7_t *const *d_b, q7_t *const *d_c,
+                                       const uint32_t *batch);
 arm_status arm_mat_mult_q15_batch_multi(const arm_matrix_instance_q15 *pSrcA, const arm_matrix_instance_q15 *pSrcB,
                                         arm_matrix_instance_q15 *pDst, uint32_t nshards, const int *devices,
                                         const q15_t *const *d_a, const q15_t *const *d_b, q15_t *const *d_c,

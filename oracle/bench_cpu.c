@@ -7,7 +7,7 @@
  * Usage: bench_xxx <workload> <n> <threads> <seconds>
  *   workload: cfft_f32 | cfft_q31 | cfft_q15 (n = fftLen), fir_f32 | fir_q15 (n = numTaps, block 4096),
  *             rfft_f32 | rfft_q31 | rfft_q15 (n = real length, forward),
- *             mat_mult_f32 (n = square dimension), mfcc_f32 / mfcc_q31 / mfcc_q15 (n = fftLen; 20 triangular
+ *             mat_mult_f32 / mat_mult_q7 / mat_mult_q15 / mat_mult_q31 (n = square dimension), mfcc_f32 / mfcc_q31 / mfcc_q15 (n = fftLen; 20 triangular
  *             Mel filters, 13 DCT outputs, Hamming window -- the suite's shape)
  * Each thread owns its own buffers (the library is reentrant) and runs until the time
  * budget is spent; in-place transforms alternate forward / inverse to stay bounded.
@@ -39,6 +39,7 @@ void oracle_arm_fir_init_q31(arm_fir_instance_q31 *S, uint16_t numTaps, const in
                              uint32_t blockSize);
 arm_status oracle_arm_fir_init_q15(arm_fir_instance_q15 *S, uint16_t numTaps, const int16_t *pCoeffs,
                                    int16_t *pState, uint32_t blockSize);
+void oracle_arm_mat_init_q7(arm_matrix_instance_q7 *S, uint16_t r, uint16_t c, int8_t *p);
 void oracle_arm_mat_init_q15(arm_matrix_instance_q15 *S, uint16_t r, uint16_t c, int16_t *p);
 void oracle_arm_mat_init_q31(arm_matrix_instance_q31 *S, uint16_t r, uint16_t c, int32_t *p);
 void oracle_arm_mat_init_f32(arm_matrix_instance_f32 *S, uint16_t r, uint16_t c, float *p);
@@ -250,6 +251,15 @@ static void *worker(void *arg) {
       samples += (double)d * d; j->flops += 2.0 * d * d * d;
     } while (now() - t0 < j->seconds);
     free(a16); free(b16); free(o16); free(st16); free(a32); free(b32); free(o32);
+  } else if (!strcmp(j->wl, "mat_mult_q7")) {
+    const int d = j->n;
+    int8_t *a = malloc((size_t)d * d), *b = malloc((size_t)d * d), *o = malloc((size_t)d * d), *st = malloc((size_t)d * d);
+    for (int i = 0; i < d * d; ++i) { a[i] = (int8_t)sm(&seed); b[i] = (int8_t)sm(&seed); }
+    arm_matrix_instance_q7 A, B, O;
+    F(arm_mat_init_q7)(&A, d, d, a); F(arm_mat_init_q7)(&B, d, d, b); F(arm_mat_init_q7)(&O, d, d, o);
+    do { F(arm_mat_mult_q7)(&A, &B, &O, st); samples += (double)d * d; j->flops += 2.0 * d * d * d; }
+    while (now() - t0 < j->seconds);
+    free(a); free(b); free(o); free(st);
   } else if (!strcmp(j->wl, "mat_mult_f32")) {
     const int d = j->n;
     float *a = malloc(sizeof(float) * d * d), *b = malloc(sizeof(float) * d * d), *o = malloc(sizeof(float) * d * d);

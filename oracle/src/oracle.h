@@ -25,6 +25,8 @@ arm_status oracle_arm_mat_mult_f32(const arm_matrix_instance_f32 *A, const arm_m
                                    arm_matrix_instance_f32 *C);
 arm_status oracle_mat_mult_f32_fmaf(const arm_matrix_instance_f32 *A, const arm_matrix_instance_f32 *B,
                                     arm_matrix_instance_f32 *Cm);
+arm_status oracle_arm_mat_mult_q7(const arm_matrix_instance_q7 *A, const arm_matrix_instance_q7 *B,
+                                  arm_matrix_instance_q7 *C, int8_t *pState);
 arm_status oracle_arm_mat_mult_q15(const arm_matrix_instance_q15 *A, const arm_matrix_instance_q15 *B,
                                    arm_matrix_instance_q15 *C, int16_t *pState);
 arm_status oracle_arm_mat_mult_q31(const arm_matrix_instance_q31 *A, const arm_matrix_instance_q31 *B,

@@ -170,6 +170,22 @@ arm_status oracle_arm_mat_mult_q15(const arm_matrix_instance_q15 *A, const arm_m
   return ARM_MATH_SUCCESS;
 }
 
+/* arm_mat_mult_q7.c:689-790 (scalar branch): q31_t sum of exact q7 products -- it cannot wrap,
+ * |sum| <= 65535 * 2^14 < 2^31 -- then (q7)__SSAT(sum >> 7, 8).  pState unused. */
+arm_status oracle_arm_mat_mult_q7(const arm_matrix_instance_q7 *A, const arm_matrix_instance_q7 *B,
+                                  arm_matrix_instance_q7 *Cm, int8_t *pState) {
+  (void)pState;
+  const uint32_t M = A->numRows, K = A->numCols, N = B->numCols;
+  for (uint32_t i = 0; i < M; ++i)
+    for (uint32_t j = 0; j < N; ++j) {
+      int32_t sum = 0;
+      for (uint32_t k = 0; k < K; ++k) sum += (int32_t)A->pData[i * K + k] * B->pData[k * N + j];
+      const int32_t v = sum >> 7;
+      Cm->pData[i * N + j] = (int8_t)(v > 127 ? 127 : v < -128 ? -128 : v);
+    }
+  return ARM_MATH_SUCCESS;
+}
+
 /* arm_mat_mult_q31.c:53-163: q63 sum of exact q31 products (wrapping), (q31)(sum >> 31). */
 arm_status oracle_arm_mat_mult_q31(const arm_matrix_instance_q31 *A, const arm_matrix_instance_q31 *B,
                                    arm_matrix_instance_q31 *Cm) {

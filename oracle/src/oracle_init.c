@@ -104,6 +104,9 @@ void oracle_arm_fir_init_q7(arm_fir_instance_q7 *S, uint16_t numTaps, const int8
   S->numTaps = numTaps; S->pCoeffs = pCoeffs; S->pState = pState;
   memset(pState, 0, (size_t)numTaps + blockSize - 1);
 }
+void oracle_arm_mat_init_q7(arm_matrix_instance_q7 *S, uint16_t r, uint16_t c, int8_t *p) {
+  S->numRows = r; S->numCols = c; S->pData = p;
+}
 void oracle_arm_mat_init_q15(arm_matrix_instance_q15 *S, uint16_t r, uint16_t c, int16_t *p) {
   S->numRows = r; S->numCols = c; S->pData = p;
 }

@@ -462,3 +462,76 @@ def test_conv_batch(dsp, torch_gpu, ref, kind, shared):
     got = out.cpu().numpy()
     for i in range(batch):
         assert got[i].tobytes() == ref.conv(kind, A[i], B[0] if shared else B[i]).tobytes(), i
+
+
+# ------------------------------------------------------------------ mat mult q7 (one i8 plane)
+def _q7_operands(rng, m, k, n, fill):
+    if fill is None:
+        return (rng.integers(-128, 127, (m, k), endpoint=True).astype(np.int8),
+                rng.integers(-128, 127, (k, n), endpoint=True).astype(np.int8))
+    if fill == "mixed":
+        vals = np.array([-128, 127, 0, -1, 1], dtype=np.int8)
+        return rng.choice(vals, (m, k)), rng.choice(vals, (k, n))
+    v = -128 if fill == "min" else 127
+    return np.full((m, k), v, np.int8), np.full((k, n), v, np.int8)
+
+
+@pytest.mark.parametrize("m,k,n,fill", [(1, 1, 1, None), (2, 3, 2, None), (5, 7, 3, None), (64, 64, 64, None),
+                                        (65, 130, 67, None), (33, 100, 31, "mixed"), (40, 64, 40, "min"),
+                                        (40, 64, 40, "max"), (300, 200, 270, None), (3, 65535, 2, "min"),
+                                        (17, 65535, 19, None), (130, 65, 129, "min"),
+                                        # whole 256 x 256 tiles, K % 64 == 0: the unguarded kernel
+                                        (256, 64, 256, None), (256, 320, 512, "mixed"), (512, 128, 256, "max"),
+                                        # K % 16 == 0 but not % 64, ragged N: vector loads with a tail
+                                        (256, 80, 272, None)])
+def test_mat_mult_q7_bitexact(dsp, torch_gpu, ref, m, k, n, fill):
+    """arm_mat_mult_q7 (arm_mat_mult_q7.c:689-790) on one i8 MFMA plane vs the reference build bit
+    for bit: extremes -128 / 127 (saturating both ways), K up to 65535 (the q31 sum at its
+    largest magnitude), ragged and whole tiles."""
+    rng = np.random.default_rng(m + 7 * k + 13 * n)
+    a, b = _q7_operands(rng, m, k, n, fill)
+    st, got = dsp.arm_mat_mult_fixed("q7", a, b)
+    st_r, want = ref.mat_mult_fixed("q7", a, b)
+    assert st == 0 and st_r == 0
+    assert got.tobytes() == want.tobytes(), np.argwhere(got != want)[:5]
+
+
+def test_mat_mult_q7_batch_and_multi(dsp, torch_gpu, ref):
+    """arm_mat_mult_q7_batch (guarded and unguarded shapes, 3 matrices) and
+    arm_mat_mult_q7_batch_multi (two ragged shards per device) against the reference build, plus a
+    1024^3 x 4 batch against exact int64 products (the bench shape)."""
+    torch = torch_gpu
+    rng = np.random.default_rng(5)
+    for (m, k, n) in ((96, 200, 80), (256, 256, 256)):
+        a = rng.integers(-128, 128, (3, m, k)).astype(np.int8)
+        b = rng.integers(-128, 128, (3, k, n)).astype(np.int8)
+        A, B = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+        Cm = torch.empty((3, m, n), dtype=torch.int8, device="cuda")
+        dsp.mat_mult_batch(A, B, Cm)
+        got = Cm.cpu().numpy()
+        for i in range(3):
+            assert got[i].tobytes() == ref.mat_mult_fixed("q7", a[i], b[i])[1].tobytes(), (m, i)
+    ndev = dsp.device_count()
+    m, k, n = 70, 90, 50
+    shards, host = [], []
+    for s in range(2 * ndev):
+        cnt = 2 + s
+        a = rng.integers(-128, 128, (cnt, m, k)).astype(np.int8)
+        b = rng.integers(-128, 128, (cnt, k, n)).astype(np.int8)
+        dev = f"cuda:{s % ndev}"
+        shards.append((torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev),
+                       torch.empty((cnt, m, n), dtype=torch.int8, device=dev)))
+        host.append((a, b))
+    dsp.mat_mult_batch_multi(shards)
+    for (a, b), (_, _, c) in zip(host, shards):
+        got = c.cpu().numpy()
+        for i in range(a.shape[0]):
+            assert got[i].tobytes() == ref.mat_mult_fixed("q7", a[i], b[i])[1].tobytes()
+    a = rng.integers(-128, 128, (4, 1024, 1024)).astype(np.int8)
+    b = rng.integers(-128, 128, (4, 1024, 1024)).astype(np.int8)
+    A, B = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+    Cm = torch.empty((4, 1024, 1024), dtype=torch.int8, device="cuda")
+    dsp.mat_mult_batch(A, B, Cm)
+    s = np.matmul(a.astype(np.int32), b.astype(np.int32))
+    want = np.clip(s >> 7, -128, 127).astype(np.int8)
+    assert Cm.cpu().numpy().tobytes() == want.tobytes()

@@ -139,11 +139,13 @@ def test_mat_mult_fmaf_oracle_is_an_exact_fma_chain(oracle, ref, m, k, n, scale)
     assert np.all(np.abs(got.astype(np.float64) - r) <= 2 * k * 2.0 ** -24 * mag + 2.0 ** -149 * k)
 
 
-@pytest.mark.parametrize("kind", ["q15", "q31"])
+@pytest.mark.parametrize("kind", ["q7", "q15", "q31"])
 @pytest.mark.parametrize("m,k,n,fill", [(1, 1, 1, None), (7, 13, 5, None), (33, 70, 17, None), (8, 64, 9, "min"),
-                                        (8, 64, 9, "max")])
+                                        (8, 64, 9, "max"), (3, 65535, 2, "min"), (2, 65535, 3, None)])
 def test_mat_mult_fixed_oracle_equals_reference(oracle, ref, kind, m, k, n, fill):
-    bits, dt = (15, np.int16) if kind == "q15" else (31, np.int32)
+    """q7 (arm_mat_mult_q7.c:689-790), q15, q31: full-range, all-minimum / all-maximum inputs and
+    K = 65535 (the largest uint16_t length: q7's q31 sum reaches -(2^14)*65535 without wrapping)."""
+    bits, dt = {"q7": (7, np.int8), "q15": (15, np.int16), "q31": (31, np.int32)}[kind]
     rng = np.random.default_rng(m * 31 + k + n)
     if fill is None:
         a = rng.integers(-(1 << bits), 1 << bits, (m, k)).astype(dt)

@@ -34,6 +34,7 @@ SPECS = {
     "mfcc_q31_onelaunch": ("--workload mfcc_q31 --steps 10 --warmup 3", "cfft_fx_r16_kernel", ""),
     "mfcc_q15_onelaunch": ("--workload mfcc_q15 --steps 10 --warmup 3", "cfft_fx_r16_kernel", ""),
     "mat_mult_f32": ("--workload mat_mult_f32 --steps 6 --warmup 2", "mat_mult_f32_full", ""),
+    "mat_mult_q7": ("--workload mat_mult_q7 --steps 10 --warmup 3", "mat_mult_q7_kernel", ""),
     "mat_mult_q15": ("--workload mat_mult_q15 --steps 6 --warmup 2", "mat_mult_i8v2", ""),
     "mat_mult_q31": ("--workload mat_mult_q31 --steps 6 --warmup 2", "mat_mult_i8v3", ""),
     "mat_mult_fast_q31": ("--workload mat_mult_fast_q31 --steps 6 --warmup 2", "mat_mult_fast_q31", ""),
