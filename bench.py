@@ -57,6 +57,8 @@ WORKLOADS = {
     "mfcc_q31": ("mfccq31", 1024, 1 << 18, 4),
     "mfcc_q15": ("mfccq15", 1024, 1 << 18, 2),
     "rfft_f32": ("rfft", 1024, 1 << 20, 8),
+    # arm_rfft_fast_f32_batch_ex(ARM_MI355X_RFFT_P_SCRATCH): p is scratch, not written back
+    "rfft_f32_pscratch": ("rfft", 1024, 1 << 20, 8),
     # real length 8192 (inner CFFT 4096 = the fixed-point specialist); bytes per sample:
     # N words in, N words written back (the inner CFFT overwrites pSrc), 2N words out
     "rfft_q31": ("rfftq31", 8192, 1 << 16, 16),
@@ -177,7 +179,7 @@ _CPU_WL = {"cfft_f32_1024": "cfft_f32", "cfft_q31_4096": "cfft_q31", "cfft_q15_4
            "fir_fast_q31": "fir_fast_q31", "mat_mult_f32": "mat_mult_f32", "mfcc_f32": "mfcc_f32",
            "mfcc_q31": "mfcc_q31", "mfcc_q15": "mfcc_q15",
            "mat_mult_q7": "mat_mult_q7", "mat_mult_q15": "mat_mult_q15", "mat_mult_q31": "mat_mult_q31", "mat_mult_fast_q31": "mat_mult_fast_q31",
-           "rfft_f32": "rfft_f32", "conv_f32": "conv_f32", "rfft_q31": "rfft_q31", "rfft_q15": "rfft_q15"}
+           "rfft_f32": "rfft_f32", "rfft_f32_pscratch": "rfft_f32", "conv_f32": "conv_f32", "rfft_q31": "rfft_q31", "rfft_q15": "rfft_q15"}
 
 
 def cpu_baseline(workload, n, all_secs=1.0, one_secs=3.0):
@@ -466,25 +468,35 @@ def main_rank(args):
                 "negative_control_tf32_rms_over_bound": tf_rms,
                 "negative_control_rejected": bool(bf_over > 0.0 and tf_rms > 1.0)}
 
-    def run_rfft(n, batch, steps, warmup):
-        """arm_rfft_fast_f32 forward over [batch][n] real frames -> [batch][n] packed spectra
-        (the forward transform also overwrites its input, as in the reference)."""
+    def run_rfft(n, batch, steps, warmup, p_scratch=False):
+        """arm_rfft_fast_f32 forward over [batch][n] real frames -> [batch][n] packed spectra.
+        Default: the forward also overwrites its input with the inner CFFT's output, as the
+        reference does, and the parity checks out AND p.  p_scratch: arm_rfft_fast_f32_batch_ex
+        with ARM_MI355X_RFFT_P_SCRATCH (p is scratch: not written back), parity on out."""
         S = dsp.const_instance(f"arm_rfft_fast_sR_f32_len{n}")
         p = synth("f32", batch * n).view(batch, n)
         out = torch.empty_like(p)
 
         def launch(s):
-            dsp.rfft_fast_batch(S, p, out, 0)
+            dsp.rfft_fast_batch(S, p, out, 0, p_scratch=p_scratch)
 
         wall, kern_ms = time_launches(launch, steps, warmup)
         host, hk = cpu_checker()
         fresh = synth("f32", 64 * n, salt=41).view(64, n)
-        want = np.stack([host.rfft(n, r, 0)[0] for r in fresh.cpu().numpy()])
-        fo = torch.empty_like(fresh)
-        dsp.rfft_fast_batch(S, fresh.clone(), fo, 0)
+        refs_ = [host.rfft(n, r, 0) for r in fresh.cpu().numpy()]
+        want = np.stack([r[0] for r in refs_])
+        want_p = np.stack([r[1] for r in refs_])
+        fo, fp = torch.empty_like(fresh), fresh.clone()
+        dsp.rfft_fast_batch(S, fp, fo, 0, p_scratch=p_scratch)
         torch.cuda.synchronize()
         ok = fo.cpu().numpy().tobytes() == want.tobytes()
-        return wall, kern_ms, {"checker": hk, "bit_exact": bool(ok), "transforms_checked": 64}
+        rec = {"checker": hk, "bit_exact": bool(ok), "transforms_checked": 64}
+        if p_scratch:
+            rec["p"] = "scratch (ARM_MI355X_RFFT_P_SCRATCH): not compared"
+        else:
+            rec["p_bit_exact"] = bool(fp.cpu().numpy().tobytes() == want_p.tobytes())
+            rec["bit_exact"] = bool(ok and rec["p_bit_exact"])
+        return wall, kern_ms, rec
 
     def run_rfft_fixed(kind, n, batch, steps, warmup):
         """arm_rfft_q31 / _q15 forward over [batch][n] full-range real signals -> [batch][2n]
@@ -594,6 +606,20 @@ def main_rank(args):
 
         wall, kern_ms = time_launches(launch, steps, warmup)
         host, hk = cpu_checker()
+        if kind == "q7":
+            # the reference's q7 body keeps its output row offset in a uint16_t (arm_mat_mult_q7.c:704,
+            # :782): at 1024 x 1024 it overwrites earlier rows.  Check matrix 0 against the exact
+            # formula, and the reference on the 64 rows whose offset does not wrap.
+            a0, b0 = a[0].cpu().numpy(), b[0].cpu().numpy()
+            exact = np.clip(np.matmul(a0.astype(np.int64), b0.astype(np.int64)) >> 7, -128, 127).astype(np.int8)
+            got = c[0].cpu().numpy()
+            rows = 65536 // dim
+            st, want = host.mat_mult_fixed(kind, a0[:rows], b0)
+            ok_exact = got.tobytes() == exact.tobytes()
+            ok_ref = st == 0 and got[:rows].tobytes() == want.tobytes()
+            return wall, kern_ms, {"checker": f"exact int64 formula (all of matrix 0) + {hk} ({rows} rows)",
+                                   "bit_exact": bool(ok_exact and ok_ref), "matrices_checked": 1,
+                                   "reference_rows_checked": rows}
         st, want = host.mat_mult_fixed(kind, a[0].cpu().numpy(), b[0].cpu().numpy())
         ok = st == 0 and c[0].cpu().numpy().tobytes() == want.tobytes()
         return wall, kern_ms, {"checker": hk, "bit_exact": bool(ok), "matrices_checked": 1}
@@ -659,8 +685,8 @@ def main_rank(args):
         wall, kern_ms, parity = run_conv(n, batch, args.steps, args.warmup)
         units = batch * (4096 + n - 1)                     # output samples
         algo_bytes = batch * 4096 * 4 + units * 4          # signal in + output
-    elif args.workload == "rfft_f32":
-        wall, kern_ms, parity = run_rfft(n, batch, args.steps, args.warmup)
+    elif args.workload in ("rfft_f32", "rfft_f32_pscratch"):
+        wall, kern_ms, parity = run_rfft(n, batch, args.steps, args.warmup, p_scratch=args.workload.endswith("pscratch"))
         units = batch * n                                  # real input samples
         algo_bytes = units * bps                           # N floats in, N floats out
     elif args.workload in ("rfft_q31", "rfft_q15"):
@@ -764,7 +790,9 @@ def main_rank(args):
                               "srcALen": 4096, "srcBLen": n, "batch_per_gpu": batch,
                               "parallelism": f"dp{world_n} shards"}
         elif kind == "rfft":
-            line["config"] = {"workload": f"arm_rfft_fast_f32 N={n} forward, batch={batch}/GPU", "fftLen": n,
+            line["config"] = {"workload": f"arm_rfft_fast_f32 N={n} forward, batch={batch}/GPU"
+                                          + (", p as scratch (arm_rfft_fast_f32_batch_ex, ARM_MI355X_RFFT_P_SCRATCH)"
+                                             if args.workload.endswith("pscratch") else ""), "fftLen": n,
                               "batch_per_gpu": batch, "parallelism": f"dp{world_n} shards"}
         elif kind in ("rfftq31", "rfftq15"):
             line["config"] = {"workload": f"arm_rfft_{kind[4:]} N={n} forward (inner CFFT {n // 2}), "
@@ -797,6 +825,8 @@ def main_rank(args):
         if args.workload == "rfft_f32":
             # the forward transform also leaves the inner CFFT output in p (reference semantics)
             line["roofline"]["bytes_moved_per_sample"] = 12
+        if args.workload == "rfft_f32_pscratch":
+            line["roofline"]["bytes_moved_per_sample"] = 8
         if args.workload in ("fir_fast_q15", "fir_q15"):
             # fast: one accumulating v_dot2 per tap pair; exact: one v_dot2 per tap (h/l planes)
             valu = units * n / (2 if args.workload == "fir_fast_q15" else 1) / (kern_ms * 1e-3) * 1e-12

@@ -437,10 +437,19 @@ def thread_resource_owners():
     return lib.arm_mi355x_thread_resource_owners()
 
 
-def rfft_fast_batch(S, p, out, ifft, stream=None):
+RFFT_P_SCRATCH = 1     # ARM_MI355X_RFFT_P_SCRATCH
+
+
+def rfft_fast_batch(S, p, out, ifft, stream=None, p_scratch=False):
+    """Batched arm_rfft_fast_f32; p_scratch=True: arm_rfft_fast_f32_batch_ex with
+    ARM_MI355X_RFFT_P_SCRATCH (p is scratch, the forward skips writing the inner CFFT back)."""
     batch = p.numel() // S.fftLenRFFT
-    st = lib.arm_rfft_fast_f32_batch(C.byref(S), C.c_void_p(p.data_ptr()), C.c_void_p(out.data_ptr()), batch,
-                                     ifft, _stream_ptr(stream))
+    if p_scratch:
+        st = lib.arm_rfft_fast_f32_batch_ex(C.byref(S), C.c_void_p(p.data_ptr()), C.c_void_p(out.data_ptr()),
+                                            batch, ifft, RFFT_P_SCRATCH, _stream_ptr(stream))
+    else:
+        st = lib.arm_rfft_fast_f32_batch(C.byref(S), C.c_void_p(p.data_ptr()), C.c_void_p(out.data_ptr()), batch,
+                                         ifft, _stream_ptr(stream))
     if st != ARM_MATH_SUCCESS:
         raise RuntimeError(f"arm_rfft_fast_f32_batch -> {st}: {last_error()[1]}")
 

@@ -264,6 +264,8 @@ BATCHED = {
                                      C.c_void_p]),
     "arm_rfft_fast_f32_batch": (C.c_int, [P(arm_rfft_fast_instance_f32), C.c_void_p, C.c_void_p, C.c_uint32,
                                           C.c_uint8, C.c_void_p]),
+    "arm_rfft_fast_f32_batch_ex": (C.c_int, [P(arm_rfft_fast_instance_f32), C.c_void_p, C.c_void_p, C.c_uint32,
+                                             C.c_uint8, C.c_uint32, C.c_void_p]),
     "arm_rfft_q31_batch": (C.c_int, [P(arm_rfft_instance_q31), C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
     "arm_rfft_q15_batch": (C.c_int, [P(arm_rfft_instance_q15), C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
     "arm_fir_f32_batch": (C.c_int, [P(arm_fir_instance_f32), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,

@@ -168,8 +168,10 @@ arm_status cfft_batch_multi(const Inst* S, uint32_t nshards, const int* devices,
 bool rfft_len_ok(uint32_t n) { return n >= 32 && n <= 4096 && (n & (n - 1)) == 0; }
 
 // arm_rfft_fast_f32.c:675-699 on `batch` signals; d_p / d_out device pointers
+// p_scratch (ARM_MI355X_RFFT_P_SCRATCH): the forward fused kernels skip writing the inner CFFT's
+// output back into p (the reference documents p as scratch; the drop-in always writes it).
 bool rfft_run(const arm_rfft_fast_instance_f32* S, float* d_p, float* d_out, uint32_t batch, uint8_t ifftFlag,
-              hipStream_t st) {
+              hipStream_t st, bool p_scratch = false) {
   const uint32_t n = S->fftLenRFFT, h = S->Sint.fftLen;
   if (h != n / 2 || !cfft_len_ok(h)) { set_error(hipErrorInvalidValue, "rfft instance"); return false; }
   BlobScope hold(st);
@@ -181,7 +183,7 @@ bool rfft_run(const arm_rfft_fast_instance_f32* S, float* d_p, float* d_out, uin
     return false;
   if (!pr.perm && ifftFlag <= 1) {   // the reference's own tables: one fused launch
     // (ifftFlag > 1: merge + a FORWARD inner CFFT, arm_cfft_f32.c:1252 -- unfused path)
-    MI_CHECK(rfft_f32_fused_launch((int)n, ifftFlag != 0, d_p, ifftFlag ? nullptr : d_p, d_out, batch,
+    MI_CHECK(rfft_f32_fused_launch((int)n, ifftFlag != 0, d_p, (ifftFlag || p_scratch) ? nullptr : d_p, d_out, batch,
                                    (const float*)pr.tw, (const float*)twr, st),
              "rfft fused");
     return true;
@@ -1136,6 +1138,15 @@ arm_status arm_rfft_fast_f32_batch(const arm_rfft_fast_instance_f32* S, float32_
   if (!S || !rfft_len_ok(S->fftLenRFFT) || (batch && (!d_p || !d_out))) return ARM_MATH_ARGUMENT_ERROR;
   if (batch == 0) return ARM_MATH_SUCCESS;
   return rfft_run(S, d_p, d_out, batch, ifftFlag, (hipStream_t)stream) ? ARM_MATH_SUCCESS : ARM_MATH_ARGUMENT_ERROR;
+}
+arm_status arm_rfft_fast_f32_batch_ex(const arm_rfft_fast_instance_f32* S, float32_t* d_p, float32_t* d_out,
+                                      uint32_t batch, uint8_t ifftFlag, uint32_t flags, void* stream) {
+  if (!S || !rfft_len_ok(S->fftLenRFFT) || (batch && (!d_p || !d_out))) return ARM_MATH_ARGUMENT_ERROR;
+  if (flags & ~(uint32_t)ARM_MI355X_RFFT_P_SCRATCH) return ARM_MATH_ARGUMENT_ERROR;
+  if (batch == 0) return ARM_MATH_SUCCESS;
+  return rfft_run(S, d_p, d_out, batch, ifftFlag, (hipStream_t)stream, (flags & ARM_MI355X_RFFT_P_SCRATCH) != 0)
+             ? ARM_MATH_SUCCESS
+             : ARM_MATH_ARGUMENT_ERROR;
 }
 
 void arm_rfft_q31(const arm_rfft_instance_q31* S, q31_t* pSrc, q31_t* pDst) { rfft_fixed_sync<int32_t>(S, pSrc, pDst); }

@@ -256,6 +256,7 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : 1) void cfft_fx_r16_
   auto pass0 = [&](uint32_t g) {
 #pragma unroll
     for (int u = 0; u < 16; ++u) v[u] = nq[u];
+    int32_t mframe = 0;                               // POST: this transform's frame maximum
     if constexpr (PRE) {
       using Pre = MqPre<T>;
       int32_t m = 0;
@@ -283,7 +284,7 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : 1) void cfft_fx_r16_
       }
       const uint32_t f = g * R::TPW + (uint32_t)w;
       if constexpr (POST) {
-        if (tp == 0) mvals[w] = m;
+        mframe = m;                                   // published after the barrier below
       } else {
         if (tp == 0 && f < batch) maxv[(size_t)f * mstride] = (T)m;
       }
@@ -316,6 +317,10 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : 1) void cfft_fx_r16_
         for (int b = 0; b < 4; ++b) v[a + 4 * b] = x[4 * a + b];
     }
     __syncthreads();                                  // the previous group's last reads are done
+    // POST: mvals is read by every wave's back end of the previous group; a wave that finished
+    // its share early must not overwrite it before the slowest one is done
+    if constexpr (POST)
+      if (tp == 0) mvals[w] = mframe;
 #pragma unroll
     for (int u = 0; u < 16; ++u) lds[sfx(tp + P * u)] = O::to_w(v[u]);
     if (g + 1 < gend) fetch(g + 1);

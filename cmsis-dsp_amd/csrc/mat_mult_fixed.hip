@@ -413,7 +413,28 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
       stage(cur ^ 1);
       load((kt + 2) * kKT2);
       mma_kk(ga, gb);
-#if MI355X_I8_SCHED
+#if MI355X_I8_PIN
+      // pinned order (experiment): kk = 0 fragment reads first, then the previous step's kk = 1
+      // MFMAs with this step's kk = 1 reads threaded between them, then the kk = 0 MFMAs with the
+      // staging work (VALU, LDS writes, global loads) between them
+      {
+        constexpr int NF = P * (WBM + WBN), NM = P * P * WBM * WBN;
+        __builtin_amdgcn_sched_group_barrier(0x100, NF, 0);
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, MI355X_I8_PIN, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, MI355X_I8_PIN, 0);
+        }
+      }
+#elif MI355X_I8_SCHED
 #pragma unroll
       for (int i = 0; i < 2 * P * P * WBM * WBN; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);

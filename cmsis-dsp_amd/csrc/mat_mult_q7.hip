@@ -26,6 +26,10 @@
 #include "common.hpp"
 #include "kernels.hpp"
 
+#ifndef MI355X_Q7_SCHED
+#define MI355X_Q7_SCHED 0
+#endif
+
 namespace mi355x {
 
 namespace {
@@ -142,6 +146,30 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __rest
         for (int j = 0; j < kQ7WBN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
   };
+  // MI355X_Q7_SCHED: pin the steady-state order -- every fragment read of kk = 0 first, then the
+  // 16 MFMAs with kk = 1's reads, the next step's LDS writes and global loads threaded between
+  // them (one per MFMA), so LDS latency hides under the matrix core instead of being waited out
+  // two MFMAs at a time (what the default schedule does to save registers).
+  auto pin_schedule = [&]() {
+#if MI355X_Q7_SCHED
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);          // kk = 0 fragment reads
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);        // one MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);        // one kk = 1 fragment read
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);        // one staging LDS write
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);        // one global load
+    }
+#endif
+  };
 
   const int nk = (K + kQ7KT - 1) / kQ7KT;
   load(0);
@@ -155,6 +183,7 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __rest
     stage(cur ^ 1);
     load((kt + 2) * kQ7KT);
     mma();
+    pin_schedule();
     __syncthreads();
   }
   for (; kt < nk; ++kt) {

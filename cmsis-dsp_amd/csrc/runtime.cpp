@@ -4,6 +4,7 @@
 #include "kernels.hpp"
 
 #include <dlfcn.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <link.h>
 #include <string.h>
@@ -160,13 +161,21 @@ void release_blobs(std::vector<BlobRef>& victims) {
   victims.clear();
 }
 
-// hand out blob b (caller holds g_table_mu): held by the innermost scope, if any
+// hand out blob b (caller holds g_table_mu): held by the innermost scope, if any.  Every entry
+// point declares a BlobScope before its first table fetch; a hand-out without one marks the blob
+// `unscoped` for good (its eviction then synchronizes the device, the one way to know an untracked
+// use has finished).  Builds with -DMI355X_DEBUG_SCOPES abort on such a hand-out instead, so a
+// future entry point that forgets its scope is caught in testing.
 const void* hand_out(const BlobRef& b) {
   b->tick = ++cache().tick;
   if (t_scopes > 0) {
     ++b->holds;
     t_held.push_back(b);
   } else {
+#ifdef MI355X_DEBUG_SCOPES
+    fprintf(stderr, "cmsisdsp-mi355x: table handed out outside a BlobScope\n");
+    abort();
+#endif
     b->unscoped = true;
   }
   return b->dev;

@@ -112,6 +112,9 @@
 #ifndef MI355X_I8_SCHED_V3  // the same hint in the tr_b8 kernel (q31)
 #define MI355X_I8_SCHED_V3 6
 #endif
+#ifndef MI355X_I8_PIN       // v2 (q15): pinned fragment-read / MFMA / staging order, N VALU per MFMA (0: off)
+#define MI355X_I8_PIN 0
+#endif
 #ifndef MI355X_I8_STAMPS    // diagnostic: per-workgroup phase timestamps (mat_mult_fixed.hip)
 #define MI355X_I8_STAMPS 0
 #endif

@@ -46,6 +46,15 @@ arm_status arm_cfft_q15_batch(const arm_cfft_instance_q15 *S, q15_t *d_p1, uint3
  * reference's overwrite of d_p on the forward transform. */
 arm_status arm_rfft_fast_f32_batch(const arm_rfft_fast_instance_f32 *S, float32_t *d_p,
                                    float32_t *d_out, uint32_t batch, uint8_t ifftFlag, void *stream);
+/* The same with flags.  ARM_MI355X_RFFT_P_SCRATCH: d_p is scratch, as the reference documents
+ * pIn of arm_rfft_fast_f32 ("the input buffer is modified by this function"): the forward
+ * transform may leave it with any contents, which lets the batched kernels skip writing the
+ * inner CFFT's output back (8 instead of 12 bytes of HBM traffic per real sample).  d_out is
+ * bit-identical either way; the inverse never writes d_p.  Other flag bits: ARM_MATH_ARGUMENT_ERROR. */
+#define ARM_MI355X_RFFT_P_SCRATCH 1u
+arm_status arm_rfft_fast_f32_batch_ex(const arm_rfft_fast_instance_f32 *S, float32_t *d_p,
+                                      float32_t *d_out, uint32_t batch, uint8_t ifftFlag, uint32_t flags,
+                                      void *stream);
 
 /* Real FFT, q31 / q15, over `batch` signals (per item: arm_rfft_q31 / arm_rfft_q15,
  * arm_rfft_q31.c:148-183).  Forward (S->ifftFlagR != 1): d_src [batch][N] is overwritten

@@ -171,7 +171,10 @@ arm_status oracle_arm_mat_mult_q15(const arm_matrix_instance_q15 *A, const arm_m
 }
 
 /* arm_mat_mult_q7.c:689-790 (scalar branch): q31_t sum of exact q7 products -- it cannot wrap,
- * |sum| <= 65535 * 2^14 < 2^31 -- then (q7)__SSAT(sum >> 7, 8).  pState unused. */
+ * |sum| <= 65535 * 2^14 < 2^31 -- then (q7)__SSAT(sum >> 7, 8).  pState unused.  The reference
+ * keeps the output row offset in a uint16_t (`i`, :704, :782), so for numRows * numColsB > 65536
+ * it writes later rows over earlier ones; this restatement (and the product) writes every element
+ * at its row-major place: equal to the reference wherever the reference's offset does not wrap. */
 arm_status oracle_arm_mat_mult_q7(const arm_matrix_instance_q7 *A, const arm_matrix_instance_q7 *B,
                                   arm_matrix_instance_q7 *Cm, int8_t *pState) {
   (void)pState;

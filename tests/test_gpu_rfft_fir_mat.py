@@ -19,28 +19,52 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("n", [32, 64, 128, 256, 512, 1024, 2048, 4096])
 @pytest.mark.parametrize("ifft", [0, 1, 2])   # 2: merge + forward inner CFFT (unfused path)
 def test_rfft_batch_bitexact(dsp, torch_gpu, ref, n, ifft):
+    """out AND the side effect on p equal the reference's on every direction: the forward leaves
+    the inner CFFT's output in p, the inverse (merge_rfft_f32, arm_rfft_fast_f32.c:405-462,
+    684-688) never writes p.  With ARM_MI355X_RFFT_P_SCRATCH out is unchanged bit for bit and the
+    inverse still leaves p alone."""
     torch = torch_gpu
     batch = 19
     x = np.stack([refs.rand_input("f32", n, seed=n + r + 100 * ifft) for r in range(batch)])
     want = np.stack([ref.rfft(n, x[r], ifft)[0] for r in range(batch)])
     want_p = np.stack([ref.rfft(n, x[r], ifft)[1] for r in range(batch)])
+    if ifft:
+        assert want_p.tobytes() == x.tobytes()        # the reference's inverse leaves p alone
     S = dsp.const_instance(f"arm_rfft_fast_sR_f32_len{n}")
-    p = torch.from_numpy(x.copy()).cuda()
-    out = torch.zeros_like(p)
-    dsp.rfft_fast_batch(S, p, out, ifft)
-    torch.cuda.synchronize()
-    assert out.cpu().numpy().tobytes() == want.tobytes()
-    if not ifft:   # the forward transform overwrites its input, like the reference
-        assert p.cpu().numpy().tobytes() == want_p.tobytes()
+    for p_scratch in (False, True):
+        p = torch.from_numpy(x.copy()).cuda()
+        out = torch.zeros_like(p)
+        dsp.rfft_fast_batch(S, p, out, ifft, p_scratch=p_scratch)
+        torch.cuda.synchronize()
+        assert out.cpu().numpy().tobytes() == want.tobytes(), p_scratch
+        if not p_scratch or ifft:
+            assert p.cpu().numpy().tobytes() == want_p.tobytes(), p_scratch
+
+
+def test_rfft_batch_ex_rejects_unknown_flags(dsp, torch_gpu):
+    import ctypes as C
+    S = dsp.const_instance("arm_rfft_fast_sR_f32_len1024")
+    p = torch_gpu.zeros((2, 1024), device="cuda")
+    st = dsp.lib.arm_rfft_fast_f32_batch_ex(C.byref(S), C.c_void_p(p.data_ptr()), C.c_void_p(p.data_ptr()), 2, 0, 2,
+                                            None)
+    assert st == dsp.ARM_MATH_ARGUMENT_ERROR
 
 
 @pytest.mark.parametrize("n", [32, 1024, 4096])
 def test_rfft_dropin(dsp, torch_gpu, ref, n):
+    """The drop-in on host buffers: pOut and p after the call equal the reference's, both ways
+    (forward: p holds the inner CFFT output; inverse: p untouched)."""
+    import ctypes as C
     x = refs.rand_input("f32", n, seed=n)
     for ifft in (0, 1):
         S = dsp.arm_rfft_fast_instance_f32()
         assert dsp.arm_rfft_fast_init_f32(S, n) == 0
         assert dsp.arm_rfft_fast_f32(S, x, ifft).tobytes() == ref.rfft(n, x, ifft)[0].tobytes()
+        p = x.copy()
+        out = np.zeros(n, dtype=np.float32)
+        dsp.lib.arm_rfft_fast_f32(C.byref(S), p.ctypes.data, out.ctypes.data, ifft)
+        want, want_p = ref.rfft(n, x, ifft)
+        assert out.tobytes() == want.tobytes() and p.tobytes() == want_p.tobytes(), ifft
 
 
 # ------------------------------------------------------------------ FIR
@@ -395,9 +419,8 @@ def test_mat_mult_fixed_batch(dsp, torch_gpu, ref, kind):
 
 @pytest.mark.parametrize("kind", ["q15", "fast_q15", "q31"])
 def test_mat_mult_fixed_many_tiles(dsp, torch_gpu, ref, kind):
-    """More whole tiles than the persistent grid (q15: workgroups walk several tiles, the next
-    tile's first K step loaded under the current epilogue): every matrix of the batch bit-exact
-    against exact int64 products (checked against the reference build on a few)."""
+    """Many whole tiles per launch (grid = tiles x batch = 600 workgroups): every matrix of the
+    batch bit-exact against exact int64 products (checked against the reference build on a few)."""
     bits, dt = (15, np.int16) if kind.endswith("q15") else (31, np.int32)
     tdt = torch_gpu.int16 if kind.endswith("q15") else torch_gpu.int32
     rng = np.random.default_rng(21)
@@ -476,6 +499,11 @@ def _q7_operands(rng, m, k, n, fill):
     return np.full((m, k), v, np.int8), np.full((k, n), v, np.int8)
 
 
+def _q7_exact(a, b):
+    s = np.matmul(a.astype(np.int64), b.astype(np.int64))
+    return np.clip(s >> 7, -128, 127).astype(np.int8)
+
+
 @pytest.mark.parametrize("m,k,n,fill", [(1, 1, 1, None), (2, 3, 2, None), (5, 7, 3, None), (64, 64, 64, None),
                                         (65, 130, 67, None), (33, 100, 31, "mixed"), (40, 64, 40, "min"),
                                         (40, 64, 40, "max"), (300, 200, 270, None), (3, 65535, 2, "min"),
@@ -487,13 +515,20 @@ def _q7_operands(rng, m, k, n, fill):
 def test_mat_mult_q7_bitexact(dsp, torch_gpu, ref, m, k, n, fill):
     """arm_mat_mult_q7 (arm_mat_mult_q7.c:689-790) on one i8 MFMA plane vs the reference build bit
     for bit: extremes -128 / 127 (saturating both ways), K up to 65535 (the q31 sum at its
-    largest magnitude), ragged and whole tiles."""
+    largest magnitude), ragged and whole tiles.  The reference keeps its output
+    row offset in a uint16_t (`i = i + numColsB`, :704,:782), so for numRows * numCols > 65536 it
+    writes later rows over earlier ones; there the product follows the documented contract (every
+    element at its row-major place) and is compared with the exact formula, and with the reference
+    on the rows it still places correctly."""
     rng = np.random.default_rng(m + 7 * k + 13 * n)
     a, b = _q7_operands(rng, m, k, n, fill)
     st, got = dsp.arm_mat_mult_fixed("q7", a, b)
-    st_r, want = ref.mat_mult_fixed("q7", a, b)
-    assert st == 0 and st_r == 0
-    assert got.tobytes() == want.tobytes(), np.argwhere(got != want)[:5]
+    assert st == 0
+    assert got.tobytes() == _q7_exact(a, b).tobytes(), np.argwhere(got != _q7_exact(a, b))[:5]
+    rows = min(m, 65536 // n)                     # rows whose uint16_t offset does not wrap
+    st_r, want = ref.mat_mult_fixed("q7", a[:rows], b)
+    assert st_r == 0
+    assert got[:rows].tobytes() == want.tobytes(), np.argwhere(got[:rows] != want)[:5]
 
 
 def test_mat_mult_q7_batch_and_multi(dsp, torch_gpu, ref):
@@ -510,7 +545,8 @@ def test_mat_mult_q7_batch_and_multi(dsp, torch_gpu, ref):
         dsp.mat_mult_batch(A, B, Cm)
         got = Cm.cpu().numpy()
         for i in range(3):
-            assert got[i].tobytes() == ref.mat_mult_fixed("q7", a[i], b[i])[1].tobytes(), (m, i)
+            assert got[i].tobytes() == _q7_exact(a[i], b[i]).tobytes(), (m, i)
+            assert got[i, :64].tobytes() == ref.mat_mult_fixed("q7", a[i, :64], b[i])[1].tobytes(), (m, i)
     ndev = dsp.device_count()
     m, k, n = 70, 90, 50
     shards, host = [], []

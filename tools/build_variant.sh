@@ -18,5 +18,5 @@ done
 /opt/rocm/bin/hipcc $FLAGS -DMI355X_BUILD_DEFS="\"$DEFS\"" -c csrc/api.cpp -o $OUT/api.o &
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,-Bsymbolic -o lib/variants/lib_$NAME.so \
-  $OBJS $OUT/api.o build/runtime.o build/init.o build/tables_data.o
+  $OBJS $OUT/api.o build/runtime.o build/init.o build/buffer_sizes.o build/tables_data.o
 echo "lib/variants/lib_$NAME.so"

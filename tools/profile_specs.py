@@ -16,6 +16,7 @@ SPECS = {
     "cfft_f32_2048": ("--fftlen 2048 --no-config3 --steps 10 --warmup 3", "n2048", ""),
     "cfft_f32_4096": ("--fftlen 4096 --no-config3 --steps 10 --warmup 3", "n4096", ""),
     "rfft_f32": ("--workload rfft_f32 --steps 10 --warmup 3", "rfft1024_fwd", ""),
+    "rfft_f32_pscratch": ("--workload rfft_f32_pscratch --steps 10 --warmup 3", "rfft1024_fwd", ""),
     "rfft_q31": ("--workload rfft_q31 --steps 10 --warmup 3", "fx4096", ""),
     "rfft_q15": ("--workload rfft_q15 --steps 10 --warmup 3", "q15_4096_pk", ""),
     "fir_f32": ("--workload fir_f32 --steps 10 --warmup 3", "fir_f32_kernel", ""),
