@@ -943,6 +943,10 @@ static hipError_t launch_fixed(int m, int k, int n, const T* a, const T* b, T* c
                                int fast = 0) {
   if (batch == 0 || m == 0 || n == 0) return hipSuccess;
   if (k == 0) return hipMemsetAsync(c, 0, sizeof(T) * (size_t)m * n * batch, st);
+  if constexpr (sizeof(T) == 2) {
+    hipError_t e = hipSuccess;
+    if (mat_mult_q15_dma_launch(m, k, n, a, b, c, batch, st, fast, &e)) return e;
+  }
   if (k <= kMatI8MaxK) {
     using G = I8Cfg<T>;
     const int tiles = ((m + G::BM - 1) / G::BM) * ((n + G::BN - 1) / G::BN);

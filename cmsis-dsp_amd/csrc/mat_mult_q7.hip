@@ -29,6 +29,15 @@
 #ifndef MI355X_Q7_SCHED
 #define MI355X_Q7_SCHED 0
 #endif
+#ifndef MI355X_Q7_DMA       // whole tiles through the LDS-DMA kernel
+#define MI355X_Q7_DMA 0
+#endif
+#ifndef MI355X_Q7_NOEPI
+#define MI355X_Q7_NOEPI 0
+#endif
+#ifndef MI355X_Q7_KT        // K bytes per LDS step: 64 or 128
+#define MI355X_Q7_KT 64
+#endif
 
 namespace mi355x {
 
@@ -37,7 +46,12 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef int v2i32 __attribute__((ext_vector_type(2)));
 
-constexpr int kQ7BM = 256, kQ7BN = 256, kQ7KT = 64, kQ7NT = 512;
+constexpr int kQ7BM = 256, kQ7BN = 256, kQ7KT = MI355X_Q7_KT, kQ7NT = 512;
+static_assert(kQ7KT == 64 || kQ7KT == 128, "K step of 64 or 128 bytes");
+constexpr int kQ7KC = kQ7KT / 16;                     // 16-B chunks per A row
+constexpr int kQ7KS = kQ7KT / 32;                     // MFMA k-steps per K step
+constexpr int kQ7NA = kQ7BM * kQ7KC / kQ7NT;          // A chunks staged per thread (2 | 4)
+constexpr int kQ7NB = kQ7KT * (kQ7BN / 16) / kQ7NT;   // B chunks staged per thread (2 | 4)
 constexpr int kQ7WM = 2, kQ7WN = 4;                   // wave grid
 constexpr int kQ7WBM = kQ7BM / (32 * kQ7WM);          // 4 row blocks of 32 per wave
 constexpr int kQ7WBN = kQ7BN / (32 * kQ7WN);          // 2 column blocks of 32 per wave
@@ -46,11 +60,57 @@ constexpr int kQ7ABUF = kQ7BM * kQ7KT, kQ7BBUF = kQ7KT * kQ7BP, kQ7BUF = kQ7ABUF
 constexpr int kQ7CP = kQ7BN + 16;                     // output tile pitch in LDS (bytes)
 static_assert(kQ7BM * kQ7CP <= 2 * kQ7BUF, "the output tile fits the plane buffers");
 
-__device__ __forceinline__ int q7_chunk(int row, int c) { return (c ^ (row >> 2)) & 3; }
+// A row swizzle: chunk c of row r at c ^ f(r).  64-B rows: f = r >> 2 (mod 4); 128-B rows (two
+// per 64-bank line): f = r >> 1 (mod 8).  Either way every 16-lane group of the fragments'
+// ds_read_b128 covers the 64 banks once and every 8-lane group of the staging ds_write_b128 the
+// 32 banks once.
+__device__ __forceinline__ int q7_chunk(int row, int c) {
+  return kQ7KC == 4 ? ((c ^ (row >> 2)) & 3) : ((c ^ (row >> 1)) & 7);
+}
 __device__ __forceinline__ v2i32 q7_tr8(const int8_t* p) {   // p: generic pointer into LDS
   return __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i32*)p);
 }
 }  // namespace
+
+// ---- epilogue (both kernels): (q7)__SSAT(sum >> 7, 8) into an LDS output tile, then 16-B row
+// stores.  Accumulator layout of a 32 x 32 block: lane l, register g holds row (g & 3) + 8 (g >> 2)
+// + 4 h, column l & 31.  The caller has passed a barrier after its last LDS read.
+template <bool FULL>
+__device__ __forceinline__ void q7_epilogue(const i32x16 (&acc)[kQ7WBM][kQ7WBN], int8_t* lds, int8_t* __restrict__ C,
+                                            int M, int N, int row0, int col0, int wm, int wn, bool vecB) {
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  int8_t* ct = lds;
+#if MI355X_Q7_NOEPI     // diagnostic only: no output (times the K loop alone)
+  if (acc[0][0][0] != 0x7fffffff) return;
+#endif
+#pragma unroll
+  for (int i = 0; i < kQ7WBM; ++i)
+#pragma unroll
+    for (int j = 0; j < kQ7WBN; ++j) {
+      const int cc = wn * 32 * kQ7WBN + 32 * j + r;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int rr = wm * 32 * kQ7WBM + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
+        ct[rr * kQ7CP + cc] = (int8_t)ssat8(acc[i][j][g] >> 7);
+      }
+    }
+  __syncthreads();
+  constexpr int VPR = kQ7BN / 16;                          // 16-B words per tile row
+  for (int w = tid; w < kQ7BM * VPR; w += kQ7NT) {
+    const int rr = w / VPR, cw = 16 * (w % VPR);
+    const int grow = row0 + rr, gcol = col0 + cw;
+    const uint4 v = *reinterpret_cast<const uint4*>(ct + rr * kQ7CP + cw);
+    if (FULL) {
+      *reinterpret_cast<uint4*>(C + (size_t)grow * N + gcol) = v;
+    } else if (grow < M) {
+      const int8_t* vb = ct + rr * kQ7CP + cw;
+      if (vecB && (((uintptr_t)C) & 15) == 0 && gcol + 16 <= N)
+        *reinterpret_cast<uint4*>(C + (size_t)grow * N + gcol) = v;
+      else
+        for (int e = 0; e < 16 && gcol + e < N; ++e) C[(size_t)grow * N + gcol + e] = vb[e];
+    }
+  }
+}
 
 template <bool FULL>
 __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __restrict__ A, const int8_t* __restrict__ B,
@@ -71,13 +131,14 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __rest
   C += bz * (size_t)M * N;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 
-  // staging roles: A rows ar and ar + 128, 16-B chunk ac; B k-rows bk and bk + 32, 16 columns at bc
-  const int ar = tid >> 2, ac = tid & 3;
+  // staging roles: A rows ar + (512 / KC) q, 16-B chunk ac; B k-rows bk + 32 q, 16 columns at bc
+  const int ar = tid / kQ7KC, ac = tid % kQ7KC;
   const int bk = tid >> 4, bc = 16 * (tid & 15);
+  constexpr int kARs = kQ7NT / kQ7KC;                  // A rows per staging pass
   const bool vecA = FULL || ((K % 16) == 0 && (((uintptr_t)A) & 15) == 0);
   const bool vecB = FULL || ((N % 16) == 0 && (((uintptr_t)B) & 15) == 0);
 
-  uint4 ra[2], rb[2];
+  uint4 ra[kQ7NA], rb[kQ7NB];
   auto load16 = [&](const int8_t* base, size_t rowoff, int colg, int collim, bool rowok, bool vec) -> uint4 {
     if (FULL || (vec && rowok && colg + 16 <= collim)) return *reinterpret_cast<const uint4*>(base + rowoff + colg);
     uint32_t w[4] = {0u, 0u, 0u, 0u};
@@ -88,9 +149,12 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __rest
   };
   auto load = [&](int k0) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int r = row0 + ar + 128 * q;
+    for (int q = 0; q < kQ7NA; ++q) {
+      const int r = row0 + ar + kARs * q;
       ra[q] = load16(A, (size_t)r * K, k0 + 16 * ac, K, r < M, vecA);
+    }
+#pragma unroll
+    for (int q = 0; q < kQ7NB; ++q) {
       const int kb = k0 + bk + 32 * q;
       rb[q] = load16(B, (size_t)kb * N, col0 + bc, N, kb < K, vecB);
     }
@@ -99,11 +163,12 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __rest
     int8_t* As = lds + buf * kQ7BUF;
     int8_t* Bs = As + kQ7ABUF;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int r = ar + 128 * q;
+    for (int q = 0; q < kQ7NA; ++q) {
+      const int r = ar + kARs * q;
       *reinterpret_cast<uint4*>(As + r * kQ7KT + 16 * q7_chunk(r, ac)) = ra[q];
-      *reinterpret_cast<uint4*>(Bs + (bk + 32 * q) * kQ7BP + bc) = rb[q];
     }
+#pragma unroll
+    for (int q = 0; q < kQ7NB; ++q) *reinterpret_cast<uint4*>(Bs + (bk + 32 * q) * kQ7BP + bc) = rb[q];
   };
 
   i32x16 acc[kQ7WBM][kQ7WBN];
@@ -118,33 +183,34 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __rest
   // B block j -> column of lane l inside the block, the same 16 k-bytes (two 8-row tr_b8 reads:
   // lane li of a 16-lane group supplies row li >> 1, columns 8 (li & 1) .. +7 of its 8 x 16 block)
   i32x4 fa[2][kQ7WBM], fb[2][kQ7WBN];
-  auto frags = [&](int buf) {
+  auto frags = [&](int buf, int pair) {           // MFMA k-steps 2 pair, 2 pair + 1
     const int8_t* As = lds + buf * kQ7BUF;
     const int8_t* Bs = As + kQ7ABUF;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kq = 0; kq < 2; ++kq) {
+      const int kk = 2 * pair + kq;
 #pragma unroll
       for (int i = 0; i < kQ7WBM; ++i) {
         const int row = wm * 32 * kQ7WBM + 32 * i + r;
-        fa[kk][i] = *reinterpret_cast<const i32x4*>(As + row * kQ7KT + 16 * q7_chunk(row, 2 * kk + h));
+        fa[kq][i] = *reinterpret_cast<const i32x4*>(As + row * kQ7KT + 16 * q7_chunk(row, 2 * kk + h));
       }
 #pragma unroll
       for (int j = 0; j < kQ7WBN; ++j) {
         const int col = wn * 32 * kQ7WBN + 32 * j + 16 * gq + 8 * (li & 1);
         const int8_t* b0 = Bs + (32 * kk + 16 * h + (li >> 1)) * kQ7BP + col;
         const v2i32 lo = q7_tr8(b0), hi = q7_tr8(b0 + 8 * kQ7BP);
-        fb[kk][j] = i32x4{lo.x, lo.y, hi.x, hi.y};
+        fb[kq][j] = i32x4{lo.x, lo.y, hi.x, hi.y};
       }
     }
   };
   auto mma = [&]() {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int kq = 0; kq < 2; ++kq)
 #pragma unroll
       for (int i = 0; i < kQ7WBM; ++i)
 #pragma unroll
         for (int j = 0; j < kQ7WBN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kq][i], fb[kq][j], acc[i][j], 0, 0, 0);
   };
   // MI355X_Q7_SCHED: pin the steady-state order -- every fragment read of kk = 0 first, then the
   // 16 MFMAs with kk = 1's reads, the next step's LDS writes and global loads threaded between
@@ -179,50 +245,193 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __rest
   int kt = 0;
   for (; kt + 2 < nk; ++kt) {                   // steady state: one basic block when FULL
     const int cur = kt & 1;
-    frags(cur);
+    frags(cur, 0);
     stage(cur ^ 1);
     load((kt + 2) * kQ7KT);
     mma();
     pin_schedule();
+#pragma unroll
+    for (int pr = 1; pr < kQ7KS / 2; ++pr) {
+      frags(cur, pr);
+      mma();
+    }
     __syncthreads();
   }
   for (; kt < nk; ++kt) {
     const int cur = kt & 1;
-    frags(cur);
+    frags(cur, 0);
     if (kt + 1 < nk) stage(cur ^ 1);
     mma();
+#pragma unroll
+    for (int pr = 1; pr < kQ7KS / 2; ++pr) {
+      frags(cur, pr);
+      mma();
+    }
     __syncthreads();
   }
 
-  // ---- epilogue: (q7)__SSAT(sum >> 7, 8) into an LDS output tile, then 16-B row stores.
-  // Accumulator layout of a 32 x 32 block: lane l, register g holds row (g & 3) + 8 (g >> 2) + 4 h,
-  // column l & 31.
-  int8_t* ct = lds;
+  q7_epilogue<FULL>(acc, lds, C, M, N, row0, col0, wm, wn, vecB);
+}
+
+// ---- LDS-DMA kernel for whole tiles (MI355X_Q7_DMA): the same tiling and fragments, but every
+// K step is moved global -> LDS by global_load_lds_dwordx4 (no staging registers, no ds_write),
+// kQ7D steps in flight in a ring of LDS buffers, one barrier per step.  A piece (one instruction)
+// fills 1 KiB of LDS lane-linearly, so the LDS swizzles are applied to the per-lane SOURCE
+// address: A rows of 64 B (16 rows per piece), chunk c of row r at c ^ ((r >> 2) & 3); B rows of
+// 256 B unpadded (4 rows per piece), chunk c of k-row k at c ^ 2 (k & 7) -- for the transposing
+// reads each 32-lane group then covers rows k0 .. k0 + 7 at chunk slots c ^ 2r and (c + 1) ^ 2r,
+// 16 distinct 16-B slots: the 64 banks once.
+constexpr int kQ7DA = kQ7BM * 64, kQ7DBUF = kQ7DA + 64 * kQ7BN;      // 16 KiB A + 16 KiB B per step
+__device__ __forceinline__ int q7_bslot(int k, int c) { return c ^ (2 * (k & 7)); }
+
+// s_waitcnt vmcnt(n) for n in {0, 4} (the other counters untouched)
+__device__ __forceinline__ void q7_wait_vm(int n) {
+  if (n >= 4) __builtin_amdgcn_s_waitcnt(0xF74);
+  else __builtin_amdgcn_s_waitcnt(0xF70);
+}
+
+// The ring is three separate LDS objects and the K loop is unrolled by three, so every access names
+// its buffer statically: the compiler's wait insertion can then tell that a fragment read of buffer
+// j does not alias the DMA pieces in flight into buffer j + 2 (with one array and a dynamic buffer
+// index it waits vmcnt(0) before every LDS read, i.e. for the just-issued prefetch).
+__global__ __launch_bounds__(kQ7NT) void mat_mult_q7_dma_kernel(const int8_t* __restrict__ A,
+                                                                const int8_t* __restrict__ B,
+                                                                int8_t* __restrict__ C, int M, int K, int N) {
+  __shared__ __attribute__((aligned(16))) int8_t ring0[kQ7DBUF];
+  __shared__ __attribute__((aligned(16))) int8_t ring1[kQ7DBUF];
+  __shared__ __attribute__((aligned(16))) int8_t ring2[kQ7DBUF];
+  const int tilesN = N / kQ7BN, tiles = tilesN * (M / kQ7BM);
+  const uint32_t total = gridDim.x;
+  uint32_t lin = blockIdx.x;
+  if (total % 8 == 0) lin = (lin % 8) * (total / 8) + lin / 8;
+  const int t = (int)(lin % (uint32_t)tiles);
+  const int row0 = (t / tilesN) * kQ7BM, col0 = (t % tilesN) * kQ7BN;
+  const size_t bz = lin / (uint32_t)tiles;
+  A += bz * (size_t)M * K;
+  B += bz * (size_t)K * N;
+  C += bz * (size_t)M * N;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+  // this wave's pieces: A pieces 2 wid, 2 wid + 1 (rows 16 g .. 16 g + 15), B pieces 2 wid,
+  // 2 wid + 1 (k-rows 4 g .. 4 g + 3)
+  const int8_t* asrc[2];
+  const int8_t* bsrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int g = 2 * wid + i;
+    const int ra = 16 * g + (lane >> 2);
+    asrc[i] = A + (size_t)(row0 + ra) * K + 16 * ((lane & 3) ^ ((ra >> 2) & 3));
+    const int kb = 4 * g + (lane >> 4);
+    bsrc[i] = B + (size_t)kb * N + col0 + 16 * q7_bslot(kb, lane & 15);
+  }
+  auto issue = [&](int kt, int8_t* base) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (size_t)kt * 64),
+                                       (__attribute__((address_space(3))) void*)(base + (2 * wid + i) * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + (size_t)kt * 64 * N),
+                                       (__attribute__((address_space(3))) void*)(base + kQ7DA + (2 * wid + i) * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  i32x16 acc[kQ7WBM][kQ7WBN];
 #pragma unroll
   for (int i = 0; i < kQ7WBM; ++i)
 #pragma unroll
-    for (int j = 0; j < kQ7WBN; ++j) {
-      const int cc = wn * 32 * kQ7WBN + 32 * j + r;
+    for (int j = 0; j < kQ7WBN; ++j) acc[i][j] = i32x16{};
+  const int wm = wid / kQ7WN, wn = wid % kQ7WN;
+  const int r = lane & 31, h = lane >> 5, li = lane & 15, gq = (lane >> 4) & 1;
+  // Fragment reads are inline asm: the compiler's wait insertion cannot separate LDS reads from
+  // the LDS-DMA pieces in flight when the read is a transposing ds_read (no memory operand), and
+  // would wait vmcnt(0) -- for the prefetch just issued -- before every step.  The asm reads are
+  // ordered by hand: each K step issues all 12 reads of its first MFMA k-step and then of its second,
+  // and waits lgkmcnt(6) / lgkmcnt(0) before the two MFMA groups; the waits take the fragment
+  // registers as operands so no MFMA can be scheduled above its wait.  The step's closing barrier is a
+// bare s_barrier after explicit waits: __syncthreads()'s fence would wait vmcnt(0), i.e. for the
+// prefetch too.
+  const uint32_t lds_base0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int8_t*)ring0;
+  (void)lds_base0;
+  auto lds_addr = [](const int8_t* p) { return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const int8_t*)p; };
+  auto step = [&](const int8_t* As) {
+    const int8_t* Bs = As + kQ7DA;
+    i32x4 fa[2][kQ7WBM], fb[2][kQ7WBN];
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int rr = wm * 32 * kQ7WBM + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
-        ct[rr * kQ7CP + cc] = (int8_t)ssat8(acc[i][j][g] >> 7);
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int i = 0; i < kQ7WBM; ++i) {
+        const int row = wm * 32 * kQ7WBM + 32 * i + r;
+        const uint32_t a = lds_addr(As + row * 64 + 16 * ((2 * kk + h) ^ ((row >> 2) & 3)));
+        asm volatile("ds_read_b128 %0, %1" : "=v"(fa[kk][i]) : "v"(a));
+      }
+#pragma unroll
+      for (int j = 0; j < kQ7WBN; ++j) {
+        const int kr = 32 * kk + 16 * h + (li >> 1);
+        const uint32_t b = lds_addr(Bs + kr * kQ7BN + 16 * q7_bslot(kr, 4 * wn + 2 * j + gq) + 8 * (li & 1));
+        v2i32 lo, hi;
+        asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(lo) : "v"(b));
+        asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(hi) : "v"(b), "i"(8 * kQ7BN));
+        fb[kk][j] = i32x4{lo.x, lo.y, hi.x, hi.y};
       }
     }
-  __syncthreads();
-  constexpr int VPR = kQ7BN / 16;                          // 16-B words per tile row
-  for (int w = tid; w < kQ7BM * VPR; w += kQ7NT) {
-    const int rr = w / VPR, cw = 16 * (w % VPR);
-    const int grow = row0 + rr, gcol = col0 + cw;
-    const uint4 v = *reinterpret_cast<const uint4*>(ct + rr * kQ7CP + cw);
-    if (FULL) {
-      *reinterpret_cast<uint4*>(C + (size_t)grow * N + gcol) = v;
-    } else if (grow < M) {
-      const int8_t* vb = ct + rr * kQ7CP + cw;
-      if (vecB && (((uintptr_t)C) & 15) == 0 && gcol + 16 <= N)
-        *reinterpret_cast<uint4*>(C + (size_t)grow * N + gcol) = v;
-      else
-        for (int e = 0; e < 16 && gcol + e < N; ++e) C[(size_t)grow * N + gcol + e] = vb[e];
+    asm volatile("s_waitcnt lgkmcnt(8)"
+                 : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fa[0][2]), "+v"(fa[0][3]), "+v"(fb[0][0]), "+v"(fb[0][1]));
+#pragma unroll
+    for (int i = 0; i < kQ7WBM; ++i)
+#pragma unroll
+      for (int j = 0; j < kQ7WBN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fa[1][2]), "+v"(fa[1][3]), "+v"(fb[1][0]), "+v"(fb[1][1]));
+#pragma unroll
+    for (int i = 0; i < kQ7WBM; ++i)
+#pragma unroll
+      for (int j = 0; j < kQ7WBN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
+  };
+
+  const int nk = K / 64;
+  issue(0, ring0);
+  if (nk > 1) issue(1, ring1);
+  q7_wait_vm(nk > 1 ? 4 : 0);                       // step 0 landed; step 1 may fly
+  __builtin_amdgcn_s_barrier();
+  // iteration kt computes ring kt % 3 and issues step kt + 2 into ring (kt + 2) % 3, which was read
+  // in iteration kt - 1 (its reads completed -- lgkmcnt(0) -- before its closing barrier)
+  auto body = [&](int kt, const int8_t* cur, int8_t* nxt) {
+    const bool more = kt + 2 < nk;
+    if (more) issue(kt + 2, nxt);
+    step(cur);
+    q7_wait_vm(more ? 4 : 0);                       // step kt + 1 landed; step kt + 2 may fly
+    __builtin_amdgcn_s_barrier();
+  };
+  for (int kt = 0; kt < nk; kt += 3) {
+    body(kt, ring0, ring2);
+    if (kt + 1 < nk) body(kt + 1, ring1, ring0);
+    if (kt + 2 < nk) body(kt + 2, ring2, ring1);
+  }
+  // epilogue: rows of wave-row group wm staged in ring wm (128 rows x 256 B each)
+  {
+#if MI355X_Q7_NOEPI
+    if (acc[0][0][0] != 0x7fffffff) return;
+#endif
+    int8_t* ct = wm ? ring1 : ring0;
+#pragma unroll
+    for (int i = 0; i < kQ7WBM; ++i)
+#pragma unroll
+      for (int j = 0; j < kQ7WBN; ++j) {
+        const int cc = wn * 32 * kQ7WBN + 32 * j + r;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const int rr = 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;          // row within the group
+          ct[rr * kQ7BN + cc] = (int8_t)ssat8(acc[i][j][g] >> 7);
+        }
+      }
+    __syncthreads();
+    for (int w = tid; w < kQ7BM * (kQ7BN / 16); w += kQ7NT) {
+      const int rr = w / (kQ7BN / 16), cw = 16 * (w % (kQ7BN / 16));
+      const int8_t* src = (rr < 128 ? ring0 : ring1) + (rr & 127) * kQ7BN + cw;
+      *reinterpret_cast<uint4*>(C + (size_t)(row0 + rr) * N + col0 + cw) = *reinterpret_cast<const uint4*>(src);
     }
   }
 }
@@ -236,7 +445,9 @@ hipError_t mat_mult_q7_launch(int m, int k, int n, const int8_t* a, const int8_t
   const bool full = m % kQ7BM == 0 && n % kQ7BN == 0 && k % kQ7KT == 0 && ((uintptr_t)a & 15) == 0 &&
                     ((uintptr_t)b & 15) == 0 && ((uintptr_t)c & 15) == 0;
   const dim3 grid((uint32_t)(tiles * batch));
-  if (full)
+  if (MI355X_Q7_DMA && full)
+    hipLaunchKernelGGL(mat_mult_q7_dma_kernel, grid, dim3(kQ7NT), 0, st, a, b, c, m, k, n);
+  else if (full)
     hipLaunchKernelGGL(mat_mult_q7_kernel<true>, grid, dim3(kQ7NT), 0, st, a, b, c, m, k, n);
   else
     hipLaunchKernelGGL(mat_mult_q7_kernel<false>, grid, dim3(kQ7NT), 0, st, a, b, c, m, k, n);

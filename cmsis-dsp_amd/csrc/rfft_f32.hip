@@ -157,7 +157,10 @@ __global__ __launch_bounds__(kBlock) void rfft_fused_kernel(const float2* src, f
 // pattern above conflict free).  Twiddles are lane-constant (stage 0: 7, stage 1: 7, split: 8).
 // Mapping sweep (2^20 transforms, Gsamples/s): T consecutive transforms per wave x WPB waves per
 // workgroup: T1 433, T2 473, T4 460, T8 462, T2 x 4 waves 442; the generic fused kernel 441.
-constexpr int kRfT = MI355X_RF1024_T, kRfWpb = MI355X_RF1024_WPB;
+// T: MI355X_RF1024_T when p receives the inner CFFT output (12 B per sample), MI355X_RF1024_TS with
+// ARM_MI355X_RFFT_P_SCRATCH (8 B per sample): round-5 sweep on one box, Gsamples/s with p as
+// scratch: T1 545, T2 606, T4 632, T8 644.
+constexpr int kRfWpb = MI355X_RF1024_WPB;
 __device__ __forceinline__ int rf_s(int e) { return (e >> 6) * 72 + (((e >> 3) & 7) << 3) + ((e & 7) ^ ((e >> 3) & 7)); }
 __device__ __forceinline__ void rf_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -169,9 +172,10 @@ __device__ __forceinline__ void rf_st(float2* p, float2 v) {
   __builtin_nontemporal_store(rf_v2f{v.x, v.y}, reinterpret_cast<rf_v2f*>(p));
 }
 
+template <int kRfT, bool KEEP_P>
 __global__ __launch_bounds__(64 * kRfWpb) void rfft1024_fwd_kernel(float2* p, float2* __restrict__ out,
                                                                    uint32_t batch, const float2* __restrict__ tw,
-                                                                   const float2* __restrict__ twr, int keep_p) {
+                                                                   const float2* __restrict__ twr) {
   __shared__ __attribute__((aligned(16))) float2 lds_all[kRfWpb][8 * 72];
   const int l = threadIdx.x & 63;
   float2* lds = lds_all[threadIdx.x >> 6];
@@ -213,7 +217,7 @@ __global__ __launch_bounds__(64 * kRfWpb) void rfft1024_fwd_kernel(float2* p, fl
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       lds[rf_s(kbin + 64 * m)] = a[m];                 // natural order for the split
-      if (keep_p) rf_st(&X[kbin + 64 * m], a[m]);      // the reference leaves the CFFT output in p
+      if (KEEP_P) rf_st(&X[kbin + 64 * m], a[m]);      // the reference leaves the CFFT output in p
     }
     rf_wave_sync();
     float2* Y = out + (size_t)t * 512;
@@ -251,9 +255,17 @@ hipError_t rfft_f32_fused_launch(int n_real, bool inverse, const float* p, float
                                  const float* tw, const float* tw_rfft, hipStream_t st) {
   if (batch == 0) return hipSuccess;
   if (MI355X_RF1024 && n_real == 1024 && !inverse && (!pcopy || pcopy == p)) {
-    const int per_block = kRfT * kRfWpb;
-    hipLaunchKernelGGL(rfft1024_fwd_kernel, dim3((batch + per_block - 1) / per_block), dim3(64 * kRfWpb), 0, st,
-                       (float2*)p, (float2*)out, batch, (const float2*)tw, (const float2*)tw_rfft, pcopy ? 1 : 0);
+    if (pcopy) {
+      constexpr int per_block = MI355X_RF1024_T * kRfWpb;
+      hipLaunchKernelGGL((rfft1024_fwd_kernel<MI355X_RF1024_T, true>), dim3((batch + per_block - 1) / per_block),
+                         dim3(64 * kRfWpb), 0, st, (float2*)p, (float2*)out, batch, (const float2*)tw,
+                         (const float2*)tw_rfft);
+    } else {
+      constexpr int per_block = MI355X_RF1024_TS * kRfWpb;
+      hipLaunchKernelGGL((rfft1024_fwd_kernel<MI355X_RF1024_TS, false>), dim3((batch + per_block - 1) / per_block),
+                         dim3(64 * kRfWpb), 0, st, (float2*)p, (float2*)out, batch, (const float2*)tw,
+                         (const float2*)tw_rfft);
+    }
     return hipGetLastError();
   }
   switch (n_real) {

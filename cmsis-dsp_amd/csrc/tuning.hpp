@@ -112,6 +112,9 @@
 #ifndef MI355X_I8_SCHED_V3  // the same hint in the tr_b8 kernel (q31)
 #define MI355X_I8_SCHED_V3 6
 #endif
+#ifndef MI355X_Q15_DMA      // q15 / fast q15 whole tiles: LDS-DMA raw tiles, planes cut in registers
+#define MI355X_Q15_DMA 0
+#endif
 #ifndef MI355X_I8_PIN       // v2 (q15): pinned fragment-read / MFMA / staging order, N VALU per MFMA (0: off)
 #define MI355X_I8_PIN 0
 #endif
@@ -136,6 +139,9 @@
 // ---- rfft_f32.hip
 #ifndef MI355X_RF1024_T
 #define MI355X_RF1024_T 2
+#endif
+#ifndef MI355X_RF1024_TS     // transforms per wave when p is scratch (ARM_MI355X_RFFT_P_SCRATCH)
+#define MI355X_RF1024_TS 8
 #endif
 #ifndef MI355X_RF1024_WPB
 #define MI355X_RF1024_WPB 8
