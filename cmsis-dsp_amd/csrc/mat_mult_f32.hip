@@ -112,6 +112,12 @@ __global__ __launch_bounds__(256) void mat_mult_f32_kernel(const float* __restri
 // transposed into a k-major LDS tile whose row pitch of 130 words puts each 32-lane group of
 // the transposing ds_write_b32 on 32 distinct banks, B written with ds_write_b128.  Half the
 // registers of the general kernel, so four workgroups fit per CU (LDS- and VGPR-wise).
+// Tile order (MI355X_MATF32_XCD): 0 = the 8 column tiles of one row band on one XCD (grid z =
+// matrix); 1 = each XCD takes a contiguous run of (matrix, tile) pairs (1-D grid), so the 64 tiles
+// of a 1024^2 matrix run together on one XCD and read its A / B panels through that XCD's L2.
+#ifndef MI355X_MATF32_XCD
+#define MI355X_MATF32_XCD 0
+#endif
 constexpr int kLdA4 = kBM + 2;
 
 __global__ __launch_bounds__(256) void mat_mult_f32_full_kernel(const float* __restrict__ A,
@@ -121,11 +127,19 @@ __global__ __launch_bounds__(256) void mat_mult_f32_full_kernel(const float* __r
   __shared__ __attribute__((aligned(16))) float Bs[2][kBK][kBN];
 
   const int tilesN = N / kBN, ntiles = tilesN * (M / kBM);
+#if MI355X_MATF32_XCD
+  const uint32_t total = gridDim.x;
+  uint32_t lin = blockIdx.x;
+  if (total % 8 == 0) lin = (lin % 8) * (total / 8) + lin / 8;
+  const int tile = (int)(lin % (uint32_t)ntiles);
+  const size_t bz = lin / (uint32_t)ntiles;
+#else
   const int orig = blockIdx.x;
   const int q = ntiles / 8, r = ntiles % 8, xcd = orig % 8;
   const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-  const int tm = tile / tilesN, tn = tile % tilesN;
   const size_t bz = blockIdx.z;
+#endif
+  const int tm = tile / tilesN, tn = tile % tilesN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int row0 = tm * kBM, col0 = tn * kBN;
@@ -210,8 +224,9 @@ hipError_t mat_mult_f32_launch(int m, int k, int n, const float* a, const float*
   const int tiles = ((m + kBM - 1) / kBM) * ((n + kBN - 1) / kBN);
   const bool full = m % kBM == 0 && n % kBN == 0 && k % kBK == 0 &&
                     ((uintptr_t)a & 15) == 0 && ((uintptr_t)b & 15) == 0;
-  if (full) {
-    hipLaunchKernelGGL(mat_mult_f32_full_kernel, dim3(tiles, 1, batch), dim3(256), 0, st, a, b, c, m, k, n);
+  if (full && (!MI355X_MATF32_XCD || (uint64_t)tiles * batch <= 0x7fffffffull)) {
+    const dim3 grid = MI355X_MATF32_XCD ? dim3((uint32_t)((uint64_t)tiles * batch)) : dim3(tiles, 1, batch);
+    hipLaunchKernelGGL(mat_mult_f32_full_kernel, grid, dim3(256), 0, st, a, b, c, m, k, n);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(mat_mult_f32_kernel, dim3(tiles, 1, batch), dim3(256), 0, st, a, b, c, m, k, n);

@@ -38,30 +38,48 @@ typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef int v2i32 __attribute__((ext_vector_type(2)));
 typedef short s2x __attribute__((ext_vector_type(2)));
 
-constexpr int kQdBM = 128, kQdBN = 128, kQdKT = 64, kQdNT = 512;
-constexpr int kQdWN = 2;                                   // 4 x 2 waves, wave tile 32 x 64
-constexpr int kQdA = kQdBM * kQdKT * 2, kQdBUF = kQdA + kQdKT * kQdBN * 2;   // 16 + 16 KiB
+// WN wave columns: WN = 2 -> 8 waves, 128 x 128 tiles, one workgroup per CU (96 KiB ring);
+// WN = 1 -> 4 waves, 128 x 64 tiles, a 72 KiB ring and TWO workgroups per CU, so the two waves
+// of a SIMD belong to different workgroups and one's barrier / fragment-read wait is covered by
+// the other's MFMAs (MI355X_Q15_DMA = 2).
+constexpr int kQdBM = 128, kQdKT = 64;
+template <int WN> struct QdCfg {
+  static constexpr int BN = 64 * WN, NT = 256 * WN, WAVES = 4 * WN;
+  static constexpr int A = kQdBM * kQdKT * 2, BUF = A + kQdKT * BN * 2;   // 16 + 8 WN KiB
+  static constexpr int APW = 16 / WAVES;                 // A pieces (1 KiB) per wave and K step
+  static constexpr int BROWS = 1024 / (2 * BN);          // k-rows per B piece
+  static constexpr int PIECES = APW + 2;                 // DMA instructions per wave and K step
+};
 constexpr int kQdMaxK = 32704;
 
 __device__ __forceinline__ uint32_t qd_lds(const void* p) {
   return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
 }
 __device__ __forceinline__ int qd_aslot(int r, int c) { return c ^ ((r >> 1) & 7); }
-__device__ __forceinline__ int qd_bslot(int k, int c) { return c ^ (4 * (k & 3)); }
+// B rows of 256 B (WN = 2): chunk c of k-row k at c ^ 4 (k & 3); rows of 128 B (WN = 1): at
+// c ^ 4 ((k >> 1) & 1).  Either way a 32-lane half of a transposing read (4 k-rows x 4 chunks)
+// meets the 64 banks once, and +4 / +32 k-rows keep the slot, so the reads' immediates stay valid.
+template <int WN> __device__ __forceinline__ int qd_bslot(int k, int c) {
+  return WN == 2 ? (c ^ (4 * (k & 3))) : (c ^ (4 * ((k >> 1) & 1)));
+}
 // plane p of the four q15 values in d0, d1 (k order): signed top byte (p = 1) or low byte - 128
 __device__ __forceinline__ int qd_plane(uint32_t d0, uint32_t d1, int p) {
   const uint32_t sel = (uint32_t)p | (uint32_t)(2 + p) << 8 | (uint32_t)(4 + p) << 16 | (uint32_t)(6 + p) << 24;
   const uint32_t w = __builtin_amdgcn_perm(d1, d0, sel);
   return (int)(p ? w : w ^ 0x80808080u);
 }
-__device__ __forceinline__ void qd_wait_vm4() { __builtin_amdgcn_s_waitcnt(0xF74); }   // vmcnt(4)
-__device__ __forceinline__ void qd_wait_vm0() { __builtin_amdgcn_s_waitcnt(0xF70); }   // vmcnt(0)
+template <int N> __device__ __forceinline__ void qd_wait_vm() {   // s_waitcnt vmcnt(N), N < 16
+  static_assert(N >= 0 && N < 16, "vmcnt");
+  __builtin_amdgcn_s_waitcnt(0xF70 | N);
+}
 }  // namespace
 
-template <bool FAST>
-__global__ __launch_bounds__(kQdNT) void mat_mult_q15_dma_kernel(const int16_t* __restrict__ A,
+template <bool FAST, int WN>
+__global__ __launch_bounds__(QdCfg<WN>::NT, WN == 1 ? 2 : 1) void mat_mult_q15_dma_kernel(const int16_t* __restrict__ A,
                                                                  const int16_t* __restrict__ B,
                                                                  int16_t* __restrict__ C, int M, int K, int N) {
+  using Cf = QdCfg<WN>;
+  constexpr int kQdBN = Cf::BN, kQdNT = Cf::NT, kQdWN = WN, kQdA = Cf::A, kQdBUF = Cf::BUF;
   __shared__ __attribute__((aligned(16))) int8_t ring0[kQdBUF];
   __shared__ __attribute__((aligned(16))) int8_t ring1[kQdBUF];
   __shared__ __attribute__((aligned(16))) int8_t ring2[kQdBUF];
@@ -78,28 +96,34 @@ __global__ __launch_bounds__(kQdNT) void mat_mult_q15_dma_kernel(const int16_t* 
   C += bz * (size_t)M * N;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 
-  // DMA pieces of this wave: A pieces 2 wid + i (rows 8 g .. 8 g + 7), B pieces 2 wid + i (k-rows
-  // 4 g .. 4 g + 3); source addresses carry the LDS swizzle
-  const int16_t* asrc[2];
+  // DMA pieces of this wave: A pieces APW wid + i (rows 8 g .. 8 g + 7), B pieces 2 wid + i (k-rows
+  // BROWS g ..); source addresses carry the LDS swizzle
+  constexpr int APW = Cf::APW, BCH = kQdBN / 8;            // B 16-B chunks per k-row
+  const int16_t* asrc[APW];
   const int16_t* bsrc[2];
+#pragma unroll
+  for (int i = 0; i < APW; ++i) {
+    const int g = APW * wid + i;
+    const int ra = 8 * g + (lane >> 3);
+    asrc[i] = A + (size_t)(row0 + ra) * K + 8 * qd_aslot(ra, lane & 7);
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int g = 2 * wid + i;
-    const int ra = 8 * g + (lane >> 3);
-    asrc[i] = A + (size_t)(row0 + ra) * K + 8 * qd_aslot(ra, lane & 7);
-    const int kb = 4 * g + (lane >> 4);
-    bsrc[i] = B + (size_t)kb * N + col0 + 8 * qd_bslot(kb, lane & 15);
+    const int kb = Cf::BROWS * g + lane / BCH;
+    bsrc[i] = B + (size_t)kb * N + col0 + 8 * qd_bslot<WN>(kb, lane % BCH);
   }
   auto issue = [&](int kt, int8_t* base) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < APW; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (size_t)kt * kQdKT),
-                                       (__attribute__((address_space(3))) void*)(base + (2 * wid + i) * 1024),
+                                       (__attribute__((address_space(3))) void*)(base + (APW * wid + i) * 1024),
                                        16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + (size_t)kt * kQdKT * N),
                                        (__attribute__((address_space(3))) void*)(base + kQdA + (2 * wid + i) * 1024),
                                        16, 0, 0);
-    }
   };
 
   const int wm = wid / kQdWN, wn = wid % kQdWN;
@@ -118,7 +142,7 @@ __global__ __launch_bounds__(kQdNT) void mat_mult_q15_dma_kernel(const int16_t* 
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int c = 8 * wn + 4 * j + 2 * gq + (p >> 1);   // 16-B chunk of columns 4p .. 4p + 3
-      boff[j] = (uint32_t)(kQdA + kr * 256 + 16 * qd_bslot(kr, c) + 8 * (p & 1));
+      boff[j] = (uint32_t)(kQdA + kr * (2 * kQdBN) + 16 * qd_bslot<WN>(kr, c) + 8 * (p & 1));
     }
   }
   const bool do_rows = wn == 0, do_cols = wm == 0;        // wave-uniform
@@ -142,10 +166,11 @@ __global__ __launch_bounds__(kQdNT) void mat_mult_q15_dma_kernel(const int16_t* 
       for (int j = 0; j < 2; ++j) {
         v2i32 x0, x1, x2, x3;
         const uint32_t ba = b0 + boff[j];
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(x0) : "v"(ba), "i"(8192 * kk));
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(x1) : "v"(ba), "i"(8192 * kk + 1024));
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(x2) : "v"(ba), "i"(8192 * kk + 2048));
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(x3) : "v"(ba), "i"(8192 * kk + 3072));
+        constexpr int R4 = 4 * 2 * kQdBN;                 // 4 k-rows in bytes
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(x0) : "v"(ba), "i"(8 * R4 * kk));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(x1) : "v"(ba), "i"(8 * R4 * kk + R4));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(x2) : "v"(ba), "i"(8 * R4 * kk + 2 * R4));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(x3) : "v"(ba), "i"(8 * R4 * kk + 3 * R4));
         rb[kk][j][0] = i32x4{x0.x, x0.y, x1.x, x1.y};
         rb[kk][j][1] = i32x4{x2.x, x2.y, x3.x, x3.y};
       }
@@ -206,13 +231,13 @@ __global__ __launch_bounds__(kQdNT) void mat_mult_q15_dma_kernel(const int16_t* 
   const int nk = K / kQdKT;
   issue(0, ring0);
   if (nk > 1) issue(1, ring1);
-  if (nk > 1) qd_wait_vm4(); else qd_wait_vm0();
+  if (nk > 1) qd_wait_vm<Cf::PIECES>(); else qd_wait_vm<0>();
   __builtin_amdgcn_s_barrier();
   auto body = [&](int kt, const int8_t* cur, int8_t* nxt) {
     const bool more = kt + 2 < nk;
     if (more) issue(kt + 2, nxt);
     step(cur);
-    if (more) qd_wait_vm4(); else qd_wait_vm0();     // step kt + 1 landed (kt + 2 may fly)
+    if (more) qd_wait_vm<Cf::PIECES>(); else qd_wait_vm<0>();   // step kt + 1 landed (kt + 2 may fly)
     __builtin_amdgcn_s_barrier();
   };
   for (int kt = 0; kt < nk; kt += 3) {
@@ -231,7 +256,7 @@ __global__ __launch_bounds__(kQdNT) void mat_mult_q15_dma_kernel(const int16_t* 
     for (int j = 0; j < 2; ++j) csp[h * kQdBN + wn * 64 + 32 * j + r] = csum[j];
   }
   __syncthreads();
-  int16_t* ct = reinterpret_cast<int16_t*>(ring0);          // [128][128]
+  int16_t* ct = reinterpret_cast<int16_t*>(ring0);          // [128][BN]
   const int64_t C0 = 128;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -257,20 +282,26 @@ __global__ __launch_bounds__(kQdNT) void mat_mult_q15_dma_kernel(const int16_t* 
   }
 }
 
-// Whole tiles only (M, N multiples of 128, K of 64, 16-B aligned operands, K <= 32704); returns
-// false when the shape is not one (the caller takes the general kernels).
+// Whole tiles only (M multiple of 128, N of 128 / 64, K of 64, 16-B aligned operands, K <= 32704);
+// returns false when the shape is not one (the caller takes the general kernels).
+template <int WN>
+static void qd_launch(int m, int k, int n, const int16_t* a, const int16_t* b, int16_t* c, uint32_t grid, hipStream_t st,
+                      int fast) {
+  if (fast)
+    hipLaunchKernelGGL((mat_mult_q15_dma_kernel<true, WN>), dim3(grid), dim3(QdCfg<WN>::NT), 0, st, a, b, c, m, k, n);
+  else
+    hipLaunchKernelGGL((mat_mult_q15_dma_kernel<false, WN>), dim3(grid), dim3(QdCfg<WN>::NT), 0, st, a, b, c, m, k, n);
+}
 bool mat_mult_q15_dma_launch(int m, int k, int n, const int16_t* a, const int16_t* b, int16_t* c, uint32_t batch,
                              hipStream_t st, int fast, hipError_t* err) {
   if (!MI355X_Q15_DMA) return false;
-  if (m % kQdBM || n % kQdBN || k % kQdKT || k > kQdMaxK || k == 0) return false;
+  constexpr int WN = MI355X_Q15_DMA == 2 ? 1 : 2;
+  constexpr int BN = QdCfg<WN>::BN;
+  if (m % kQdBM || n % BN || k % kQdKT || k > kQdMaxK || k == 0) return false;
   if (((uintptr_t)a & 15) || ((uintptr_t)b & 15) || ((uintptr_t)c & 15)) return false;
-  const uint64_t tiles = (uint64_t)(m / kQdBM) * (n / kQdBN);
+  const uint64_t tiles = (uint64_t)(m / kQdBM) * (n / BN);
   if (tiles * batch > 0x7fffffffull || batch == 0) return false;
-  const dim3 grid((uint32_t)(tiles * batch));
-  if (fast)
-    hipLaunchKernelGGL(mat_mult_q15_dma_kernel<true>, grid, dim3(kQdNT), 0, st, a, b, c, m, k, n);
-  else
-    hipLaunchKernelGGL(mat_mult_q15_dma_kernel<false>, grid, dim3(kQdNT), 0, st, a, b, c, m, k, n);
+  qd_launch<WN>(m, k, n, a, b, c, (uint32_t)(tiles * batch), st, fast);
   *err = hipGetLastError();
   return true;
 }

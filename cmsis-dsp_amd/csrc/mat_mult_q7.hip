@@ -273,67 +273,88 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __rest
   q7_epilogue<FULL>(acc, lds, C, M, N, row0, col0, wm, wn, vecB);
 }
 
-// ---- LDS-DMA kernel for whole tiles (MI355X_Q7_DMA): the same tiling and fragments, but every
-// K step is moved global -> LDS by global_load_lds_dwordx4 (no staging registers, no ds_write),
-// kQ7D steps in flight in a ring of LDS buffers, one barrier per step.  A piece (one instruction)
-// fills 1 KiB of LDS lane-linearly, so the LDS swizzles are applied to the per-lane SOURCE
-// address: A rows of 64 B (16 rows per piece), chunk c of row r at c ^ ((r >> 2) & 3); B rows of
-// 256 B unpadded (4 rows per piece), chunk c of k-row k at c ^ 2 (k & 7) -- for the transposing
-// reads each 32-lane group then covers rows k0 .. k0 + 7 at chunk slots c ^ 2r and (c + 1) ^ 2r,
-// 16 distinct 16-B slots: the 64 banks once.
-constexpr int kQ7DA = kQ7BM * 64, kQ7DBUF = kQ7DA + 64 * kQ7BN;      // 16 KiB A + 16 KiB B per step
-__device__ __forceinline__ int q7_bslot(int k, int c) { return c ^ (2 * (k & 7)); }
+// ---- LDS-DMA kernel for whole tiles (MI355X_Q7_DMA): the same fragments, but every K step is
+// moved global -> LDS by global_load_lds_dwordx4 (no staging registers, no ds_write), two steps in
+// flight in a ring of three LDS buffers, one barrier per step.  A piece (one instruction) fills
+// 1 KiB of LDS lane-linearly, so the LDS swizzles are applied to the per-lane SOURCE address: A
+// rows of 64 B (16 rows per piece), chunk c of row r at c ^ ((r >> 2) & 3); B rows unpadded.
+// WN wave columns: MI355X_Q7_DMA = 1 -> 8 waves (2 x 4), 256 x 256 tiles, one workgroup per CU
+// (96 KiB ring); = 2 -> 4 waves (2 x 2), 256 x 128 tiles, a 72 KiB ring and TWO workgroups per CU,
+// so the two waves of a SIMD belong to different workgroups and one's barrier / fragment-read wait
+// is covered by the other's MFMAs.
+template <int WN> struct Q7D {
+  static constexpr int BN = 64 * WN, NT = 128 * WN, WAVES = 2 * WN;
+  static constexpr int DA = kQ7BM * 64, DBUF = DA + 64 * BN;     // 16 KiB A + 64 BN B per step
+  static constexpr int APW = 16 / WAVES;                           // A pieces per wave and step
+  static constexpr int BROWS = 1024 / BN;                          // k-rows per B piece
+  static constexpr int PIECES = APW + 2;
+};
+// B slot of 16-B chunk c in k-row k: 256-B rows c ^ 2 (k & 7); 128-B rows c ^ 2 ((k >> 1) & 3).  The
+// 32-lane half of a transposing read takes 8 k-rows x 2 chunks: 16 distinct 16-B slots, the 64 banks
+// once; +8 / +16 / +32 k-rows keep the slot, so the reads' immediates stay valid.
+template <int WN> __device__ __forceinline__ int q7_bslot(int k, int c) {
+  return WN == 4 ? (c ^ (2 * (k & 7))) : (c ^ (2 * ((k >> 1) & 3)));
+}
 
-// s_waitcnt vmcnt(n) for n in {0, 4} (the other counters untouched)
-__device__ __forceinline__ void q7_wait_vm(int n) {
-  if (n >= 4) __builtin_amdgcn_s_waitcnt(0xF74);
-  else __builtin_amdgcn_s_waitcnt(0xF70);
+// s_waitcnt vmcnt(n), n < 16 (the other counters untouched)
+template <int N> __device__ __forceinline__ void q7_wait_vm() {
+  static_assert(N >= 0 && N < 16, "vmcnt");
+  __builtin_amdgcn_s_waitcnt(0xF70 | N);
 }
 
 // The ring is three separate LDS objects and the K loop is unrolled by three, so every access names
 // its buffer statically: the compiler's wait insertion can then tell that a fragment read of buffer
 // j does not alias the DMA pieces in flight into buffer j + 2 (with one array and a dynamic buffer
 // index it waits vmcnt(0) before every LDS read, i.e. for the just-issued prefetch).
-__global__ __launch_bounds__(kQ7NT) void mat_mult_q7_dma_kernel(const int8_t* __restrict__ A,
+template <int WN>
+__global__ __launch_bounds__(Q7D<WN>::NT, WN == 2 ? 2 : 1) void mat_mult_q7_dma_kernel(const int8_t* __restrict__ A,
                                                                 const int8_t* __restrict__ B,
                                                                 int8_t* __restrict__ C, int M, int K, int N) {
-  __shared__ __attribute__((aligned(16))) int8_t ring0[kQ7DBUF];
-  __shared__ __attribute__((aligned(16))) int8_t ring1[kQ7DBUF];
-  __shared__ __attribute__((aligned(16))) int8_t ring2[kQ7DBUF];
-  const int tilesN = N / kQ7BN, tiles = tilesN * (M / kQ7BM);
+  using D = Q7D<WN>;
+  constexpr int BN = D::BN, NT = D::NT, DA = D::DA, APW = D::APW;
+  __shared__ __attribute__((aligned(16))) int8_t ring0[D::DBUF];
+  __shared__ __attribute__((aligned(16))) int8_t ring1[D::DBUF];
+  __shared__ __attribute__((aligned(16))) int8_t ring2[D::DBUF];
+  const int tilesN = N / BN, tiles = tilesN * (M / kQ7BM);
   const uint32_t total = gridDim.x;
   uint32_t lin = blockIdx.x;
   if (total % 8 == 0) lin = (lin % 8) * (total / 8) + lin / 8;
   const int t = (int)(lin % (uint32_t)tiles);
-  const int row0 = (t / tilesN) * kQ7BM, col0 = (t % tilesN) * kQ7BN;
+  const int row0 = (t / tilesN) * kQ7BM, col0 = (t % tilesN) * BN;
   const size_t bz = lin / (uint32_t)tiles;
   A += bz * (size_t)M * K;
   B += bz * (size_t)K * N;
   C += bz * (size_t)M * N;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 
-  // this wave's pieces: A pieces 2 wid, 2 wid + 1 (rows 16 g .. 16 g + 15), B pieces 2 wid,
-  // 2 wid + 1 (k-rows 4 g .. 4 g + 3)
-  const int8_t* asrc[2];
+  // this wave's pieces: A pieces APW wid + i (rows 16 g .. 16 g + 15), B pieces 2 wid + i (k-rows
+  // BROWS g ..)
+  constexpr int BCH = BN / 16;                         // 16-B chunks per B k-row
+  const int8_t* asrc[APW];
   const int8_t* bsrc[2];
+#pragma unroll
+  for (int i = 0; i < APW; ++i) {
+    const int g = APW * wid + i;
+    const int ra = 16 * g + (lane >> 2);
+    asrc[i] = A + (size_t)(row0 + ra) * K + 16 * ((lane & 3) ^ ((ra >> 2) & 3));
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int g = 2 * wid + i;
-    const int ra = 16 * g + (lane >> 2);
-    asrc[i] = A + (size_t)(row0 + ra) * K + 16 * ((lane & 3) ^ ((ra >> 2) & 3));
-    const int kb = 4 * g + (lane >> 4);
-    bsrc[i] = B + (size_t)kb * N + col0 + 16 * q7_bslot(kb, lane & 15);
+    const int kb = D::BROWS * g + lane / BCH;
+    bsrc[i] = B + (size_t)kb * N + col0 + 16 * q7_bslot<WN>(kb, lane % BCH);
   }
   auto issue = [&](int kt, int8_t* base) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < APW; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (size_t)kt * 64),
-                                       (__attribute__((address_space(3))) void*)(base + (2 * wid + i) * 1024),
+                                       (__attribute__((address_space(3))) void*)(base + (APW * wid + i) * 1024),
                                        16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + (size_t)kt * 64 * N),
-                                       (__attribute__((address_space(3))) void*)(base + kQ7DA + (2 * wid + i) * 1024),
+                                       (__attribute__((address_space(3))) void*)(base + DA + (2 * wid + i) * 1024),
                                        16, 0, 0);
-    }
   };
 
   i32x16 acc[kQ7WBM][kQ7WBN];
@@ -341,21 +362,19 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_dma_kernel(const int8_t* __
   for (int i = 0; i < kQ7WBM; ++i)
 #pragma unroll
     for (int j = 0; j < kQ7WBN; ++j) acc[i][j] = i32x16{};
-  const int wm = wid / kQ7WN, wn = wid % kQ7WN;
+  const int wm = wid / WN, wn = wid % WN;
   const int r = lane & 31, h = lane >> 5, li = lane & 15, gq = (lane >> 4) & 1;
   // Fragment reads are inline asm: the compiler's wait insertion cannot separate LDS reads from
   // the LDS-DMA pieces in flight when the read is a transposing ds_read (no memory operand), and
   // would wait vmcnt(0) -- for the prefetch just issued -- before every step.  The asm reads are
   // ordered by hand: each K step issues all 12 reads of its first MFMA k-step and then of its second,
-  // and waits lgkmcnt(6) / lgkmcnt(0) before the two MFMA groups; the waits take the fragment
+  // and waits lgkmcnt(8) / lgkmcnt(0) before the two MFMA groups; the waits take the fragment
   // registers as operands so no MFMA can be scheduled above its wait.  The step's closing barrier is a
-// bare s_barrier after explicit waits: __syncthreads()'s fence would wait vmcnt(0), i.e. for the
-// prefetch too.
-  const uint32_t lds_base0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int8_t*)ring0;
-  (void)lds_base0;
+  // bare s_barrier after explicit waits: __syncthreads()'s fence would wait vmcnt(0), i.e. for the
+  // prefetch too.
   auto lds_addr = [](const int8_t* p) { return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const int8_t*)p; };
   auto step = [&](const int8_t* As) {
-    const int8_t* Bs = As + kQ7DA;
+    const int8_t* Bs = As + DA;
     i32x4 fa[2][kQ7WBM], fb[2][kQ7WBN];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -368,10 +387,10 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_dma_kernel(const int8_t* __
 #pragma unroll
       for (int j = 0; j < kQ7WBN; ++j) {
         const int kr = 32 * kk + 16 * h + (li >> 1);
-        const uint32_t b = lds_addr(Bs + kr * kQ7BN + 16 * q7_bslot(kr, 4 * wn + 2 * j + gq) + 8 * (li & 1));
+        const uint32_t b = lds_addr(Bs + kr * BN + 16 * q7_bslot<WN>(kr, 4 * wn + 2 * j + gq) + 8 * (li & 1));
         v2i32 lo, hi;
         asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(lo) : "v"(b));
-        asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(hi) : "v"(b), "i"(8 * kQ7BN));
+        asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(hi) : "v"(b), "i"(8 * BN));
         fb[kk][j] = i32x4{lo.x, lo.y, hi.x, hi.y};
       }
     }
@@ -394,7 +413,7 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_dma_kernel(const int8_t* __
   const int nk = K / 64;
   issue(0, ring0);
   if (nk > 1) issue(1, ring1);
-  q7_wait_vm(nk > 1 ? 4 : 0);                       // step 0 landed; step 1 may fly
+  if (nk > 1) q7_wait_vm<D::PIECES>(); else q7_wait_vm<0>();   // step 0 landed; step 1 may fly
   __builtin_amdgcn_s_barrier();
   // iteration kt computes ring kt % 3 and issues step kt + 2 into ring (kt + 2) % 3, which was read
   // in iteration kt - 1 (its reads completed -- lgkmcnt(0) -- before its closing barrier)
@@ -402,7 +421,7 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_dma_kernel(const int8_t* __
     const bool more = kt + 2 < nk;
     if (more) issue(kt + 2, nxt);
     step(cur);
-    q7_wait_vm(more ? 4 : 0);                       // step kt + 1 landed; step kt + 2 may fly
+    if (more) q7_wait_vm<D::PIECES>(); else q7_wait_vm<0>();   // step kt + 1 landed; kt + 2 may fly
     __builtin_amdgcn_s_barrier();
   };
   for (int kt = 0; kt < nk; kt += 3) {
@@ -410,7 +429,7 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_dma_kernel(const int8_t* __
     if (kt + 1 < nk) body(kt + 1, ring1, ring0);
     if (kt + 2 < nk) body(kt + 2, ring2, ring1);
   }
-  // epilogue: rows of wave-row group wm staged in ring wm (128 rows x 256 B each)
+  // epilogue: rows of wave-row group wm staged in ring wm (128 rows x BN bytes each)
   {
 #if MI355X_Q7_NOEPI
     if (acc[0][0][0] != 0x7fffffff) return;
@@ -424,13 +443,13 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_dma_kernel(const int8_t* __
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
           const int rr = 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;          // row within the group
-          ct[rr * kQ7BN + cc] = (int8_t)ssat8(acc[i][j][g] >> 7);
+          ct[rr * BN + cc] = (int8_t)ssat8(acc[i][j][g] >> 7);
         }
       }
     __syncthreads();
-    for (int w = tid; w < kQ7BM * (kQ7BN / 16); w += kQ7NT) {
-      const int rr = w / (kQ7BN / 16), cw = 16 * (w % (kQ7BN / 16));
-      const int8_t* src = (rr < 128 ? ring0 : ring1) + (rr & 127) * kQ7BN + cw;
+    for (int w = tid; w < kQ7BM * (BN / 16); w += NT) {
+      const int rr = w / (BN / 16), cw = 16 * (w % (BN / 16));
+      const int8_t* src = (rr < 128 ? ring0 : ring1) + (rr & 127) * BN + cw;
       *reinterpret_cast<uint4*>(C + (size_t)(row0 + rr) * N + col0 + cw) = *reinterpret_cast<const uint4*>(src);
     }
   }
@@ -445,9 +464,16 @@ hipError_t mat_mult_q7_launch(int m, int k, int n, const int8_t* a, const int8_t
   const bool full = m % kQ7BM == 0 && n % kQ7BN == 0 && k % kQ7KT == 0 && ((uintptr_t)a & 15) == 0 &&
                     ((uintptr_t)b & 15) == 0 && ((uintptr_t)c & 15) == 0;
   const dim3 grid((uint32_t)(tiles * batch));
-  if (MI355X_Q7_DMA && full)
-    hipLaunchKernelGGL(mat_mult_q7_dma_kernel, grid, dim3(kQ7NT), 0, st, a, b, c, m, k, n);
-  else if (full)
+  constexpr int kDWN = MI355X_Q7_DMA == 2 ? 2 : 4;
+  if (MI355X_Q7_DMA && m % kQ7BM == 0 && n % Q7D<kDWN>::BN == 0 && k % 64 == 0 && ((uintptr_t)a & 15) == 0 &&
+      ((uintptr_t)b & 15) == 0 && ((uintptr_t)c & 15) == 0) {
+    const uint64_t dt = (uint64_t)(m / kQ7BM) * (n / Q7D<kDWN>::BN) * batch;
+    if (dt <= 0x7fffffffull) {
+      hipLaunchKernelGGL(mat_mult_q7_dma_kernel<kDWN>, dim3((uint32_t)dt), dim3(Q7D<kDWN>::NT), 0, st, a, b, c, m, k, n);
+      return hipGetLastError();
+    }
+  }
+  if (full)
     hipLaunchKernelGGL(mat_mult_q7_kernel<true>, grid, dim3(kQ7NT), 0, st, a, b, c, m, k, n);
   else
     hipLaunchKernelGGL(mat_mult_q7_kernel<false>, grid, dim3(kQ7NT), 0, st, a, b, c, m, k, n);

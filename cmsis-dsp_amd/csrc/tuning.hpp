@@ -173,6 +173,9 @@
 #ifndef MI355X_MQF_WG
 #define MI355X_MQF_WG 1
 #endif
+#ifndef MI355X_MQF_TWRELOAD  // one-launch MFCC: CFFT twiddles re-read per group, not held through the back end
+#define MI355X_MQF_TWRELOAD 0
+#endif
 #ifndef MI355X_MQF_STAGE   // stage the Mel / DCT tables in LDS when they fit 32 KiB
 #define MI355X_MQF_STAGE 1
 #endif
