@@ -27,8 +27,14 @@
 // the per-lane source addresses.  LDS reads are inline asm with hand-counted lgkmcnt waits: the
 // compiler cannot tell a transposing read from the DMA writes in flight and would otherwise wait
 // for every outstanding piece before each read (see mat_mult_q7.hip).
+#include <type_traits>
+
 #include "common.hpp"
 #include "kernels.hpp"
+
+#ifndef MI355X_Q15_PIPE      // fragments of step kt + 1 read under step kt's MFMAs
+#define MI355X_Q15_PIPE 0
+#endif
 
 namespace mi355x {
 
@@ -229,6 +235,135 @@ __global__ __launch_bounds__(QdCfg<WN>::NT, WN == 1 ? 2 : 1) void mat_mult_q15_d
   };
 
   const int nk = K / kQdKT;
+#if MI355X_Q15_PIPE
+  // Software-pipelined K loop (as mat_mult_q7.hip MI355X_Q7_PIPE): the raw fragments of step kt + 1
+  // are read into the other register set between step kt's two k-steps, so the first k-step's
+  // plane split and MFMAs cover the barrier and the second the reads' latency; ring slot kt % 3 is
+  // refilled with step kt + 3 right after the barrier that follows every wave's last read of it.
+  // Reads: six per-lane base VGPRs (A chunk (kk, e), B block j) plus immediates (slot, k-rows).
+  i32x4 pra[2][2][2], prb[2][2][2][2];                   // [set][kk][e], [set][kk][j][t pair]
+  const uint32_t lb = qd_lds(ring0);
+  const bool contiguous = qd_lds(ring1) == lb + kQdBUF && qd_lds(ring2) == lb + 2 * kQdBUF;
+  constexpr int R4 = 4 * 2 * kQdBN;                     // 4 k-rows in bytes
+  constexpr bool kHi = 2 * kQdBUF + kQdA + 8 * R4 + 3 * R4 + 8 > 65535;   // slot 2 from raised bases
+  static_assert(kQdBUF + kQdA + 8 * R4 + 3 * R4 + 8 <= 65535, "ds_read immediate offsets");
+  uint32_t aB[2][2][2], bB[2][2];                       // [lo/hi][kk][e], [lo/hi][j]
+#pragma unroll
+  for (int hb = 0; hb < 2; ++hb) {
+    const uint32_t add = (hb && kHi) ? (uint32_t)kQdBUF : 0u;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) aB[hb][kk][e] = lb + aoff[kk][e] + add;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bB[hb][j] = lb + boff[j] + add;
+  }
+#define QDA(dst, base, off) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(off))
+#define QDB(dst, base, off) asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(off))
+  auto rd = [&](auto SLOT, i32x4 (&ra)[2][2], i32x4 (&rb)[2][2][2]) {
+    constexpr bool hi = kHi && decltype(SLOT)::value == 2;
+    constexpr int so = (hi ? 1 : decltype(SLOT)::value) * kQdBUF;
+    constexpr int hb = hi ? 1 : 0;
+    QDA(ra[0][0], aB[hb][0][0], so); QDA(ra[0][1], aB[hb][0][1], so);
+    v2i32 x0, x1, x2, x3, y0, y1, y2, y3;
+    QDB(x0, bB[hb][0], so); QDB(x1, bB[hb][0], so + R4); QDB(x2, bB[hb][0], so + 2 * R4); QDB(x3, bB[hb][0], so + 3 * R4);
+    QDB(y0, bB[hb][1], so); QDB(y1, bB[hb][1], so + R4); QDB(y2, bB[hb][1], so + 2 * R4); QDB(y3, bB[hb][1], so + 3 * R4);
+    rb[0][0][0] = i32x4{x0.x, x0.y, x1.x, x1.y}; rb[0][0][1] = i32x4{x2.x, x2.y, x3.x, x3.y};
+    rb[0][1][0] = i32x4{y0.x, y0.y, y1.x, y1.y}; rb[0][1][1] = i32x4{y2.x, y2.y, y3.x, y3.y};
+    QDA(ra[1][0], aB[hb][1][0], so); QDA(ra[1][1], aB[hb][1][1], so);
+    v2i32 z0, z1, z2, z3, w0, w1, w2, w3;
+    QDB(z0, bB[hb][0], so + 8 * R4); QDB(z1, bB[hb][0], so + 9 * R4); QDB(z2, bB[hb][0], so + 10 * R4); QDB(z3, bB[hb][0], so + 11 * R4);
+    QDB(w0, bB[hb][1], so + 8 * R4); QDB(w1, bB[hb][1], so + 9 * R4); QDB(w2, bB[hb][1], so + 10 * R4); QDB(w3, bB[hb][1], so + 11 * R4);
+    rb[1][0][0] = i32x4{z0.x, z0.y, z1.x, z1.y}; rb[1][0][1] = i32x4{z2.x, z2.y, z3.x, z3.y};
+    rb[1][1][0] = i32x4{w0.x, w0.y, w1.x, w1.y}; rb[1][1][1] = i32x4{w2.x, w2.y, w3.x, w3.y};
+  };
+#undef QDA
+#undef QDB
+  auto wait_set = [&](i32x4 (&ra)[2][2], i32x4 (&rb)[2][2][2]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ra[0][0]), "+v"(ra[0][1]), "+v"(rb[0][0][0]), "+v"(rb[0][0][1]),
+                 "+v"(rb[0][1][0]), "+v"(rb[0][1][1]));
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ra[1][0]), "+v"(ra[1][1]), "+v"(rb[1][0][0]), "+v"(rb[1][0][1]),
+                 "+v"(rb[1][1][0]), "+v"(rb[1][1][1]));
+  };
+  // one k-step from raw fragments: the exact row / column sums, the byte planes, 8 MFMAs
+  auto kstep = [&](const i32x4 (&ra)[2], const i32x4 (&rb)[2][2]) {
+    uint32_t ad[8], bd[2][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      ad[u] = (uint32_t)ra[0][u];
+      ad[4 + u] = (uint32_t)ra[1][u];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bd[j][u] = (uint32_t)rb[j][0][u];
+        bd[j][4 + u] = (uint32_t)rb[j][1][u];
+      }
+    }
+    if (do_rows) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) rsum = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2x, ad[u]), s2x{1, 1}, rsum, false);
+    }
+    if (do_cols) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          csum[j] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2x, bd[j][u]), s2x{1, 1}, csum[j], false);
+    }
+    i32x4 fa[2], fb[2][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      fa[p] = i32x4{qd_plane(ad[0], ad[1], p), qd_plane(ad[2], ad[3], p), qd_plane(ad[4], ad[5], p),
+                    qd_plane(ad[6], ad[7], p)};
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        fb[p][j] = i32x4{qd_plane(bd[j][0], bd[j][1], p), qd_plane(bd[j][2], bd[j][3], p),
+                         qd_plane(bd[j][4], bd[j][5], p), qd_plane(bd[j][6], bd[j][7], p)};
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[p + q][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[p], fb[q][j], acc[p + q][j], 0, 0, 0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  auto ring = [&](auto SLOT) -> int8_t* { return SLOT.value == 0 ? ring0 : (SLOT.value == 1 ? ring1 : ring2); };
+  if (!contiguous) __builtin_trap();                    // layout assumption
+  issue(0, ring0);
+  if (nk > 1) issue(1, ring1);
+  if (nk > 2) issue(2, ring2);
+  if (nk > 2) qd_wait_vm<2 * Cf::PIECES>(); else if (nk > 1) qd_wait_vm<Cf::PIECES>(); else qd_wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+  rd(I0{}, pra[0], prb[0]);
+  auto body = [&](int kt, auto CUR, auto NXT, auto SET) {
+    constexpr int cs = decltype(SET)::value;
+    wait_set(pra[cs], prb[cs]);
+    __builtin_amdgcn_sched_barrier(0);
+    kstep(pra[cs][0], prb[cs][0]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 1 < nk) {
+      if (kt + 2 < nk) qd_wait_vm<Cf::PIECES>(); else qd_wait_vm<0>();   // step kt + 1 landed
+      __builtin_amdgcn_s_barrier();                   // ... for every wave; slot CUR read by all
+      if (kt + 3 < nk) issue(kt + 3, ring(CUR));
+      rd(NXT, pra[cs ^ 1], prb[cs ^ 1]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    kstep(pra[cs][1], prb[cs][1]);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int k0 = 0; k0 < nk; k0 += 6) {
+    body(k0, I0{}, I1{}, I0{});
+    if (k0 + 1 < nk) body(k0 + 1, I1{}, I2{}, I1{});
+    if (k0 + 2 < nk) body(k0 + 2, I2{}, I0{}, I0{});
+    if (k0 + 3 < nk) body(k0 + 3, I0{}, I1{}, I1{});
+    if (k0 + 4 < nk) body(k0 + 4, I1{}, I2{}, I0{});
+    if (k0 + 5 < nk) body(k0 + 5, I2{}, I0{}, I1{});
+  }
+  __syncthreads();                                       // every wave's reads done before the epilogue
+#else
   issue(0, ring0);
   if (nk > 1) issue(1, ring1);
   if (nk > 1) qd_wait_vm<Cf::PIECES>(); else qd_wait_vm<0>();
@@ -245,6 +380,8 @@ __global__ __launch_bounds__(QdCfg<WN>::NT, WN == 1 ? 2 : 1) void mat_mult_q15_d
     if (kt + 1 < nk) body(kt + 1, ring1, ring0);
     if (kt + 2 < nk) body(kt + 2, ring2, ring1);
   }
+
+#endif
 
   // ---- epilogue: the two k-halves of the row / column sums meet in LDS (ring1), the int64 combine,
   // the output tile staged in ring0 as q15 and written as 16-B rows
