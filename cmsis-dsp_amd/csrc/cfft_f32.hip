@@ -596,11 +596,98 @@ static hipError_t launch_f32(float2* data, uint32_t batch, const float2* tw, con
   return hipGetLastError();
 }
 
+// ============================================================================================
+// N = 1024, ONE transform, latency-shaped (the synchronous drop-in's batch-1 call; MI355X_N1024_LAT).
+// The batched kernel gives a transform one wave, so a lone call waits for that wave to run both
+// 512-point halves.  After the radix8by2 pre-pass the halves are independent (stages 0-2 of the
+// radix-8 core work inside a half), so here wave h of a 2-wave workgroup runs half h alone: both
+// waves load the same 16 words per lane (the pre-pass pairs x[k] with x[k + 512]), wave 0 keeps the
+// sums (half 0), wave 1 the twiddled differences (half 1), and from there each wave runs the
+// batched kernel's phases A-C on its own half of the LDS image with wave-level ordering only —
+// the same operations in the same order, so the words are the batched kernel's (bit-exact to the
+// reference).  Half 0's outputs are the even bins, half 1's the odd ones (phase C's mapping), so
+// each lane stores 8-byte words.  Then the workgroup writes the caller's completion word.
+__global__ __launch_bounds__(128) void cfft_f32_n1024_lat_kernel(float2* __restrict__ X, const float2* __restrict__ tw,
+                                                                 uint32_t flags, uint32_t* done, uint32_t seq) {
+  __shared__ __attribute__((aligned(16))) float2 lds[16 * 72];
+  const int l = threadIdx.x & 63, h = threadIdx.x >> 6;    // lane, half
+  const bool ifft = flags & kIfft;
+  const bool brev = flags & kBitrev;
+  const float invL = 1.0f / 1024.0f;
+  float2 wb[4], w0[7], w1[7];
+  if (h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wb[i] = tw[l + 64 * i];
+  }
+#pragma unroll
+  for (int m = 0; m < 7; ++m) w0[m] = tw[2 * (m + 1) * l];
+  const int j1 = l & 7;
+#pragma unroll
+  for (int m = 0; m < 7; ++m) w1[m] = tw[16 * (m + 1) * j1];
+
+  float2 p[8], q[8], v[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) { p[m] = X[l + 64 * m]; q[m] = X[512 + l + 64 * m]; }
+  if (ifft) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) { p[m].y = -p[m].y; q[m].y = -q[m].y; }
+  }
+  if (h == 0) {                                        // radix8by2 sums (arm_cfft_f32.c:867-951)
+#pragma unroll
+    for (int m = 0; m < 8; ++m) v[m] = make_float2(p[m].x + q[m].x, p[m].y + q[m].y);
+  } else {                                             // ... and twiddled differences
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const float2 w = wb[m];
+      const float2 t2 = make_float2(p[m].x - q[m].x, p[m].y - q[m].y);
+      v[m] = make_float2(t2.x * w.x + t2.y * w.y, t2.y * w.x - t2.x * w.y);
+      const float2 t4 = make_float2(q[m + 4].x - p[m + 4].x, q[m + 4].y - p[m + 4].y);
+      v[m + 4] = make_float2(t4.x * w.y - t4.y * w.x, t4.y * w.y + t4.x * w.x);
+    }
+  }
+  const int hb = 512 * h;
+  r8_sel(v, w0, l != 0);                               // stage 0
+#pragma unroll
+  for (int m = 0; m < 8; ++m) lds[s1024(hb + l + 64 * m)] = v[m];
+  wave_sync();
+  {                                                    // stage 1
+    const int base = hb + 64 * (l >> 3) + j1;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) v[m] = lds[s1024(base + 8 * m)];
+    r8_sel(v, w1, j1 != 0);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) lds[s1024(base + 8 * m)] = v[m];
+  }
+  wave_sync();
+#pragma unroll
+  for (int m = 0; m < 8; ++m) v[m] = lds[s1024(hb + 8 * l + m)];   // stage 2
+  r8_core(v);
+  if (ifft) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) v[m] = make_float2(v[m].x * invL, -v[m].y * invL);
+  }
+  if (brev) {
+    const int kl = 2 * (l >> 3) + 16 * (l & 7) + h;    // bin of (p = l + 64 h, m = 0)
+#pragma unroll
+    for (int m = 0; m < 8; ++m) X[kl + 128 * m] = v[m];
+  } else {
+    float4* Y = reinterpret_cast<float4*>(X + hb + 8 * l);
+#pragma unroll
+    for (int m = 0; m < 8; m += 2) Y[m >> 1] = make_float4(v[m].x, v[m].y, v[m + 1].x, v[m + 1].y);
+  }
+  signal_done(done, seq);
+}
+
 // The drop-in's one N = 1024 transform (the reference's own table) with its completion word
 // written by the transform's workgroup; false: not this case (the caller launches the usual way).
 bool cfft_f32_n1024_done_launch(float* data, uint32_t batch, const float* tw, const uint16_t* perm, uint32_t flags,
                                 uint32_t* done, uint32_t seq, hipStream_t st) {
   if (perm || batch == 0 || batch > (uint32_t)((kN1024T ? kN1024T : 1) * kN1024Wpb)) return false;
+  if (MI355X_N1024_LAT && batch == 1) {
+    hipLaunchKernelGGL(cfft_f32_n1024_lat_kernel, dim3(1), dim3(128), 0, st, reinterpret_cast<float2*>(data),
+                       reinterpret_cast<const float2*>(tw), flags, done, seq);
+    return true;
+  }
   hipLaunchKernelGGL(cfft_f32_n1024_kernel<true>, dim3(1), dim3(64 * kN1024Wpb), 0, st, reinterpret_cast<float2*>(data),
                      batch, reinterpret_cast<const float2*>(tw), flags, done, seq);
   return true;

@@ -118,9 +118,6 @@ __global__ __launch_bounds__(256) void mat_mult_f32_kernel(const float* __restri
 #ifndef MI355X_MATF32_XCD
 #define MI355X_MATF32_XCD 1
 #endif
-#ifndef MI355X_MATF32_STAGGER   // s_sleep units (64 cycles) per residency slot; 0: off
-#define MI355X_MATF32_STAGGER 0
-#endif
 constexpr int kLdA4 = kBM + 2;
 
 __global__ __launch_bounds__(256) void mat_mult_f32_full_kernel(const float* __restrict__ A,
@@ -146,15 +143,6 @@ __global__ __launch_bounds__(256) void mat_mult_f32_full_kernel(const float* __r
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int row0 = tm * kBM, col0 = tn * kBN;
-#if MI355X_MATF32_STAGGER
-  // The four workgroups of a CU start together and, being identical, reach their barriers together,
-  // idling the SIMD's matrix core at once; the first wave of workgroups starts staggered by a
-  // quarter K step per residency slot (blockIdx / 256 mod 4 under the round-robin dispatch).
-  if (blockIdx.x < 1024u) {
-    const int slot = (int)((blockIdx.x >> 8) & 3);
-    for (int i = 0; i < slot; ++i) __builtin_amdgcn_s_sleep(MI355X_MATF32_STAGGER);
-  }
-#endif
 
   // this thread's float4 slots: A rows (tid>>2) and 64 + (tid>>2), k quad (tid&3);
   // B rows k = tid>>5 and 8 + (tid>>5), column quad (tid&31)

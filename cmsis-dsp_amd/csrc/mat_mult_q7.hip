@@ -37,6 +37,9 @@
 #ifndef MI355X_Q7_PIPE      // DMA kernel: fragments of step kt + 1 read under step kt's MFMAs
 #define MI355X_Q7_PIPE 0
 #endif
+#ifndef MI355X_Q7_TEPI      // transposed accumulators: the epilogue packs 4 outputs per LDS dword
+#define MI355X_Q7_TEPI 0
+#endif
 #ifndef MI355X_Q7_NOEPI
 #define MI355X_Q7_NOEPI 0
 #endif
@@ -87,6 +90,49 @@ __device__ __forceinline__ void q7_epilogue(const i32x16 (&acc)[kQ7WBM][kQ7WBN],
   int8_t* ct = lds;
 #if MI355X_Q7_NOEPI     // diagnostic only: no output (times the K loop alone)
   if (acc[0][0][0] != 0x7fffffff) return;
+#endif
+#if MI355X_Q7_TEPI
+  // Transposed accumulators (the K loop swaps the MFMA operands): lane l holds output row l & 31
+  // of a block and, in registers 4q .. 4q + 3, the four consecutive columns 8q + 4h .. + 3, so the
+  // saturated bytes pack into one dword per 4 outputs -- 32 ds_write_b32 per lane instead of 128
+  // byte stores.  Rows sit 264 B apart (66 dwords: the 32 rows of a store group fall on 16 banks,
+  // 2-way, which costs nothing for ds_write_b32) and are read back as 8-B pieces.
+  constexpr int CPT = kQ7BN + 8;
+  static_assert(kQ7BM * CPT <= 2 * kQ7BUF, "the output tile fits the plane buffers");
+#pragma unroll
+  for (int i = 0; i < kQ7WBM; ++i)
+#pragma unroll
+    for (int j = 0; j < kQ7WBN; ++j) {
+      const int rr = wm * 32 * kQ7WBM + 32 * i + r;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int cc = wn * 32 * kQ7WBN + 32 * j + 8 * q + 4 * h;
+        const uint32_t w = (uint32_t)(uint8_t)ssat8(acc[i][j][4 * q] >> 7) |
+                           (uint32_t)(uint8_t)ssat8(acc[i][j][4 * q + 1] >> 7) << 8 |
+                           (uint32_t)(uint8_t)ssat8(acc[i][j][4 * q + 2] >> 7) << 16 |
+                           (uint32_t)(uint8_t)ssat8(acc[i][j][4 * q + 3] >> 7) << 24;
+        *reinterpret_cast<uint32_t*>(ct + rr * CPT + cc) = w;
+      }
+    }
+  __syncthreads();
+  constexpr int VPRT = kQ7BN / 16;
+  for (int w = tid; w < kQ7BM * VPRT; w += kQ7NT) {
+    const int rr = w / VPRT, cw = 16 * (w % VPRT);
+    const int grow = row0 + rr, gcol = col0 + cw;
+    const uint2 lo = *reinterpret_cast<const uint2*>(ct + rr * CPT + cw);
+    const uint2 hi = *reinterpret_cast<const uint2*>(ct + rr * CPT + cw + 8);
+    const uint4 v = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    if (FULL) {
+      *reinterpret_cast<uint4*>(C + (size_t)grow * N + gcol) = v;
+    } else if (grow < M) {
+      const int8_t* vb = ct + rr * CPT + cw;
+      if (vecB && (((uintptr_t)C) & 15) == 0 && gcol + 16 <= N)
+        *reinterpret_cast<uint4*>(C + (size_t)grow * N + gcol) = v;
+      else
+        for (int e = 0; e < 16 && gcol + e < N; ++e) C[(size_t)grow * N + gcol + e] = vb[e];
+    }
+  }
+  return;
 #endif
 #pragma unroll
   for (int i = 0; i < kQ7WBM; ++i)
@@ -215,7 +261,8 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __rest
       for (int i = 0; i < kQ7WBM; ++i)
 #pragma unroll
         for (int j = 0; j < kQ7WBN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kq][i], fb[kq][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = MI355X_Q7_TEPI ? __builtin_amdgcn_mfma_i32_32x32x32_i8(fb[kq][j], fa[kq][i], acc[i][j], 0, 0, 0)
+                                     : __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kq][i], fb[kq][j], acc[i][j], 0, 0, 0);
   };
   // MI355X_Q7_SCHED: pin the steady-state order -- every fragment read of kk = 0 first, then the
   // 16 MFMAs with kk = 1's reads, the next step's LDS writes and global loads threaded between
