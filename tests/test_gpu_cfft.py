@@ -60,9 +60,11 @@ def test_cfft_fixed_wrap_saturation(dsp, torch_gpu, ref, kind, n, dist):
 @pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("n", [16, 256, 1024, 4096])
 def test_cfft_dropin_host_pointer(dsp, torch_gpu, ref, kind, n):
-    """The synchronous drop-in API on host memory (staged through the device)."""
+    """The synchronous drop-in API on host memory (staged through the device; f32 N = 1024 one
+    transform runs the 2-wave latency kernel, cfft_f32.hip cfft_f32_n1024_lat_kernel): every
+    (ifftFlag, bitReverseFlag) pair, ifftFlag 2 = forward as in arm_cfft_f32.c:1252."""
     x = refs.rand_input(kind, 2 * n, seed=5 + n)
-    for ifft, bitrev in [(0, 1), (1, 1), (0, 0)]:
+    for ifft, bitrev in [(0, 1), (1, 1), (0, 0), (1, 0), (2, 1)]:
         S = getattr(dsp, f"arm_cfft_instance_{kind}")()
         assert getattr(dsp, f"arm_cfft_init_{kind}")(S, n) == 0
         got = getattr(dsp, f"arm_cfft_{kind}")(S, x, ifft, bitrev)
