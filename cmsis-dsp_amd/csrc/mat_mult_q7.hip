@@ -38,7 +38,7 @@
 #define MI355X_Q7_PIPE 0
 #endif
 #ifndef MI355X_Q7_TEPI      // transposed accumulators: the epilogue packs 4 outputs per LDS dword
-#define MI355X_Q7_TEPI 0
+#define MI355X_Q7_TEPI 1
 #endif
 #ifndef MI355X_Q7_NOEPI
 #define MI355X_Q7_NOEPI 0

@@ -133,6 +133,9 @@
 #ifndef MI355X_I8_V3
 #define MI355X_I8_V3 2
 #endif
+#ifndef MI355X_I8_RSDOT     // q31 (tr_b8 kernel): row sums by v_dot4 over the cut planes
+#define MI355X_I8_RSDOT 0
+#endif
 
 // ---- mfcc_f32.hip
 #ifndef MI355X_MFCC_UNROLL
