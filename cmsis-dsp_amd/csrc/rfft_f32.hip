@@ -168,7 +168,6 @@ __device__ __forceinline__ void rf_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 typedef float rf_v2f __attribute__((ext_vector_type(2)));
-typedef float rf_v4f __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void rf_st(float2* p, float2 v) {
   __builtin_nontemporal_store(rf_v2f{v.x, v.y}, reinterpret_cast<rf_v2f*>(p));
 }
@@ -186,10 +185,8 @@ __global__ __launch_bounds__(64 * kRfWpb) void rfft1024_fwd_kernel(float2* p, fl
   const int j1 = l & 7;
 #pragma unroll
   for (int m = 0; m < 7; ++m) { w0[m] = tw[(m + 1) * l]; w1[m] = tw[8 * (m + 1) * j1]; }
-  // split bins of lane l: k = l + 64 m (8-B stores), or with MI355X_RF1024_ST16 the pairs
-  // k = 2 l + 128 m' + e (m = 2 m' + e), so every output store is one 16-B word
 #pragma unroll
-  for (int m = 0; m < 8; ++m) ws[m] = twr[MI355X_RF1024_ST16 ? 2 * l + 128 * (m >> 1) + (m & 1) : l + 64 * m];
+  for (int m = 0; m < 8; ++m) ws[m] = twr[l + 64 * m];
   const int kbin = 8 * (l & 7) + (l >> 3);            // stage-2 output m of lane l is bin kbin + 64 m
   for (uint32_t t = t_begin; t < t_end; ++t) {
     float2* X = p + (size_t)t * 512;
@@ -224,10 +221,9 @@ __global__ __launch_bounds__(64 * kRfWpb) void rfft1024_fwd_kernel(float2* p, fl
     }
     rf_wave_sync();
     float2* Y = out + (size_t)t * 512;
-    float2 ov[8];
 #pragma unroll
     for (int m = 0; m < 8; ++m) {                      // stage_rfft_f32, arm_rfft_fast_f32.c:316-402
-      const int k = MI355X_RF1024_ST16 ? 2 * l + 128 * (m >> 1) + (m & 1) : l + 64 * m;
+      const int k = l + 64 * m;
       float2 o;
       if (k == 0) {
         const float2 x0 = lds[rf_s(0)];
@@ -239,14 +235,7 @@ __global__ __launch_bounds__(64 * kRfWpb) void rfft1024_fwd_kernel(float2* p, fl
         const float p0 = w.x * t1a, p1 = w.y * t1a, p2 = w.x * t1b, p3 = w.y * t1b;
         o = make_float2(0.5f * (A.x + B.x + p0 + p3), 0.5f * (A.y - B.y + p1 - p2));
       }
-      if (MI355X_RF1024_ST16) ov[m] = o;
-      else rf_st(&Y[k], o);
-    }
-    if (MI355X_RF1024_ST16) {
-#pragma unroll
-      for (int m = 0; m < 8; m += 2)
-        __builtin_nontemporal_store(rf_v4f{ov[m].x, ov[m].y, ov[m + 1].x, ov[m + 1].y},
-                                    reinterpret_cast<rf_v4f*>(&Y[2 * l + 64 * m]));
+      rf_st(&Y[k], o);
     }
   }
 }

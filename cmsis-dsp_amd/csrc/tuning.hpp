@@ -149,9 +149,6 @@
 #ifndef MI355X_RF1024_TS     // transforms per wave when p is scratch (ARM_MI355X_RFFT_P_SCRATCH)
 #define MI355X_RF1024_TS 8
 #endif
-#ifndef MI355X_RF1024_ST16   // split outputs as bin pairs: 16-B stores instead of 8-B
-#define MI355X_RF1024_ST16 0
-#endif
 #ifndef MI355X_RF1024_WPB
 #define MI355X_RF1024_WPB 8
 #endif
