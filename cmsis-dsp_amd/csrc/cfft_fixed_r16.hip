@@ -179,53 +179,44 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : 1) void cfft_fx_r16_
   const int h = R::BY2 ? (tp & 1) : 0;                // by2 half of the later passes
   const int tq = R::BY2 ? (tp >> 1) : tp;             // thread within that radix-4 transform
 
-  // ---- twiddles, lane-constant for the kernel's life.  POST with MI355X_MQF_TWRELOAD: re-read
-  // (L1 / L2 hits) at the head of every group instead, so the ~64 VGPRs they take are free during
-  // the back end (the opaque pointer update keeps the compiler from hoisting the loads out of the
-  // group loop).
-  constexpr bool kTwReload = POST && MI355X_MQF_TWRELOAD;
-  const C* twr = tw;
+  // ---- twiddles, lane-constant for the kernel's life
   // first pass: non-by2 stage 1 (j = tp + P a) and stage 2 (j = tp); by2 pre-pass (i = tp + P u)
   // and stage 1 of the halves (j = tp + P c, c < 2)
   constexpr int NA0 = R::BY2 ? 2 : 4;
   Tw tw0a[NA0][3], tw0b[3];
   C twpre[R::BY2 ? 8 : 1];
+#pragma unroll
+  for (int a = 0; a < NA0; ++a)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) tw0a[a][k] = O::tw(tw, (k + 1) * (tp + P * a) * R::MOD0);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) tw0b[k] = O::tw(tw, (k + 1) * tp * 4 * R::MOD0);
+  if constexpr (R::BY2) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) twpre[u] = tw[tp + P * u];
+  }
   // middle pass (stages S_MID, S_MID + 1): j = tq mod d2
   constexpr int LM = M / pow4(R::S_MID - 1), D1M = LM / 4, D2M = LM / 16;
   constexpr int MODM = R::MOD0 * pow4(R::S_MID - 1);
   Tw twma[4][3], twmb[3];
+  if constexpr (R::HAS_MID) {
+    const int j = tq % D2M;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) twma[a][k] = O::tw(tw, (k + 1) * (j + D2M * a) * MODM);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) twmb[k] = O::tw(tw, (k + 1) * j * 4 * MODM);
+  }
   // two-stage last pass: stage K-1 twiddles depend on a only
   constexpr int MODL = R::MOD0 * pow4(K - 2);
   Tw twl[4][3];
-  auto load_tw = [&]() {
-    if constexpr (kTwReload) __asm__ volatile("" : "+s"(twr));
+  if constexpr (R::LAST2) {
 #pragma unroll
-    for (int a = 0; a < NA0; ++a)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) tw0a[a][k] = O::tw(twr, (k + 1) * (tp + P * a) * R::MOD0);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) tw0b[k] = O::tw(twr, (k + 1) * tp * 4 * R::MOD0);
-    if constexpr (R::BY2) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) twpre[u] = twr[tp + P * u];
-    }
-    if constexpr (R::HAS_MID) {
-      const int j = tq % D2M;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) twma[a][k] = O::tw(twr, (k + 1) * (j + D2M * a) * MODM);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) twmb[k] = O::tw(twr, (k + 1) * j * 4 * MODM);
-    }
-    if constexpr (R::LAST2) {
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) twl[a][k] = O::tw(twr, (k + 1) * a * MODL);
-    }
-  };
-  if constexpr (!kTwReload) load_tw();
+      for (int k = 0; k < 3; ++k) twl[a][k] = O::tw(tw, (k + 1) * a * MODL);
+  }
 
   // ---- work: groups of TPW transforms; workgroup b takes MI355X_FXR_T consecutive groups
   const uint32_t ngroups = (batch + R::TPW - 1) / R::TPW;
@@ -263,7 +254,6 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : 1) void cfft_fx_r16_
   __shared__ int32_t mvals[POST ? R::TPW : 1];        // POST: the group's frame maxima
   // first pass from nq, then the next group's loads (they fly under the later passes)
   auto pass0 = [&](uint32_t g) {
-    if constexpr (kTwReload) load_tw();
 #pragma unroll
     for (int u = 0; u < 16; ++u) v[u] = nq[u];
     int32_t mframe = 0;                               // POST: this transform's frame maximum

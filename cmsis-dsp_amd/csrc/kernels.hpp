@@ -180,9 +180,6 @@ hipError_t fir_f32_conv_pass(const float* c, uint64_t cstride, int T, const floa
 // byte-sliced planes on the i8 matrix cores (mat_mult_fixed.hip).
 hipError_t mat_mult_q15_launch(int m, int k, int n, const int16_t* a, const int16_t* b, int16_t* c, uint32_t batch,
                                hipStream_t st);
-// Whole-tile q15 GEMM with LDS-DMA staging (mat_mult_q15_dma.hip); false: shape not eligible.
-bool mat_mult_q15_dma_launch(int m, int k, int n, const int16_t* a, const int16_t* b, int16_t* c, uint32_t batch,
-                             hipStream_t st, int fast, hipError_t* err);
 hipError_t mat_mult_q31_launch(int m, int k, int n, const int32_t* a, const int32_t* b, int32_t* c, uint32_t batch,
                                hipStream_t st);
 // Row-major q7 C[b] = A[b] * B[b] (arm_mat_mult_q7 semantics, bit-exact): one i8 MFMA plane

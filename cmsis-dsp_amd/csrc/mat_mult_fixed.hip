@@ -413,28 +413,7 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v2_kernel(const T* __restrict
       stage(cur ^ 1);
       load((kt + 2) * kKT2);
       mma_kk(ga, gb);
-#if MI355X_I8_PIN
-      // pinned order (experiment): kk = 0 fragment reads first, then the previous step's kk = 1
-      // MFMAs with this step's kk = 1 reads threaded between them, then the kk = 0 MFMAs with the
-      // staging work (VALU, LDS writes, global loads) between them
-      {
-        constexpr int NF = P * (WBM + WBN), NM = P * P * WBM * WBN;
-        __builtin_amdgcn_sched_group_barrier(0x100, NF, 0);
-#pragma unroll
-        for (int i = 0; i < NM; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, MI355X_I8_PIN, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < NM; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, MI355X_I8_PIN, 0);
-        }
-      }
-#elif MI355X_I8_SCHED
+#if MI355X_I8_SCHED
 #pragma unroll
       for (int i = 0; i < 2 * P * P * WBM * WBN; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -661,10 +640,6 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v3_kernel(const T* __restrict
   };
 
   int64_t my_rsum = 0;
-  constexpr bool kRsDot = MI355X_I8_RSDOT && sizeof(T) == 4;
-  int32_t rsp[P];                                         // per-plane byte sums (kRsDot)
-#pragma unroll
-  for (int p = 0; p < P; ++p) rsp[p] = 0;
   // column sums of the k-rows this thread stages (at most K / 64 <= 511 of them): exact in int32
   // for q15 (|v| <= 2^15), int64 for q31
   using CS = typename std::conditional<sizeof(T) == 2, int32_t, int64_t>::type;
@@ -695,10 +670,8 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v3_kernel(const T* __restrict
         my_csum[2 * d + 1] += (int16_t)(bd[d] >> 16);
       }
     } else {
-      if constexpr (!kRsDot) {
 #pragma unroll
-        for (int d = 0; d < AKD; ++d) my_rsum += (int32_t)ad[d];
-      }
+      for (int d = 0; d < AKD; ++d) my_rsum += (int32_t)ad[d];
 #pragma unroll
       for (int d = 0; d < EBD; ++d) my_csum[d] += (int32_t)bd[d];
     }
@@ -709,10 +682,6 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v3_kernel(const T* __restrict
       for (int q = 0; q < AK / 4; ++q) {
         if constexpr (sizeof(T) == 2) w[q] = plane_q15<P>(ad[2 * q], ad[2 * q + 1], p);
         else w[q] = plane4<P>(ad[4 * q], ad[4 * q + 1], ad[4 * q + 2], ad[4 * q + 3], p);
-        // MI355X_I8_RSDOT (q31): the row sums from the byte planes just cut, one v_dot4 per 4
-        // values and plane into int32 (|sum| <= 128 * 16 * 511), instead of a sign extension and
-        // a 64-bit add per value
-        if constexpr (kRsDot) rsp[p] = __builtin_amdgcn_sdot4((int)w[q], 0x01010101, rsp[p], false);
       }
 #pragma unroll
       for (int q = 0; q < AK / 16; ++q)
@@ -878,12 +847,6 @@ __global__ __launch_bounds__(kNT2) void mat_mult_i8v3_kernel(const T* __restrict
   int64_t* rfin = cs + NQB * BN;
   int64_t* cfin = rfin + BM;
   T* ct = reinterpret_cast<T*>(cfin + BN);
-  if constexpr (kRsDot) {   // sum v = sum_p 256^p sum t_p + (values staged) * C0, pads included (each 0)
-    int64_t s2 = (int64_t)AK * nk * C0;
-#pragma unroll
-    for (int p = 0; p < P; ++p) s2 += (int64_t)rsp[p] << (8 * p);
-    my_rsum = s2;
-  }
   rs[(tid % AQ) * BM + ar] = my_rsum;
 #pragma unroll
   for (int c = 0; c < EB; ++c) cs[bk * BN + bc + c] = (int64_t)my_csum[c];
@@ -959,10 +922,6 @@ static hipError_t launch_fixed(int m, int k, int n, const T* a, const T* b, T* c
                                int fast = 0) {
   if (batch == 0 || m == 0 || n == 0) return hipSuccess;
   if (k == 0) return hipMemsetAsync(c, 0, sizeof(T) * (size_t)m * n * batch, st);
-  if constexpr (sizeof(T) == 2) {
-    hipError_t e = hipSuccess;
-    if (mat_mult_q15_dma_launch(m, k, n, a, b, c, batch, st, fast, &e)) return e;
-  }
   if (k <= kMatI8MaxK) {
     using G = I8Cfg<T>;
     const int tiles = ((m + G::BM - 1) / G::BM) * ((n + G::BN - 1) / G::BN);

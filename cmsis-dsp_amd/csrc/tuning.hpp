@@ -115,12 +115,6 @@
 #ifndef MI355X_I8_SCHED_V3  // the same hint in the tr_b8 kernel (q31)
 #define MI355X_I8_SCHED_V3 6
 #endif
-#ifndef MI355X_Q15_DMA      // q15 / fast q15 whole tiles: LDS-DMA raw tiles, planes cut in registers
-#define MI355X_Q15_DMA 0
-#endif
-#ifndef MI355X_I8_PIN       // v2 (q15): pinned fragment-read / MFMA / staging order, N VALU per MFMA (0: off)
-#define MI355X_I8_PIN 0
-#endif
 #ifndef MI355X_I8_STAMPS    // diagnostic: per-workgroup phase timestamps (mat_mult_fixed.hip)
 #define MI355X_I8_STAMPS 0
 #endif
@@ -132,9 +126,6 @@
 #endif
 #ifndef MI355X_I8_V3
 #define MI355X_I8_V3 2
-#endif
-#ifndef MI355X_I8_RSDOT     // q31 (tr_b8 kernel): row sums by v_dot4 over the cut planes
-#define MI355X_I8_RSDOT 0
 #endif
 
 // ---- mfcc_f32.hip
@@ -178,9 +169,6 @@
 // ---- cfft_fixed_r16.hip: minimum workgroups per CU of the one-launch MFCC kernel (caps its VGPRs)
 #ifndef MI355X_MQF_WG
 #define MI355X_MQF_WG 1
-#endif
-#ifndef MI355X_MQF_TWRELOAD  // one-launch MFCC: CFFT twiddles re-read per group, not held through the back end
-#define MI355X_MQF_TWRELOAD 0
 #endif
 #ifndef MI355X_MQF_STAGE   // stage the Mel / DCT tables in LDS when they fit 32 KiB
 #define MI355X_MQF_STAGE 1

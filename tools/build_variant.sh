@@ -15,7 +15,8 @@ for src in csrc/*.hip; do
   /opt/rocm/bin/hipcc $FLAGS $EXTRA -c $src -o $OUT/$f.o &
   OBJS="$OBJS $OUT/$f.o"
 done
-/opt/rocm/bin/hipcc $FLAGS -DMI355X_BUILD_DEFS="\"$DEFS\"" -c csrc/api.cpp -o $OUT/api.o &
+SRC_ID=$(cat build/srcid.stamp 2>/dev/null || echo unknown)
+/opt/rocm/bin/hipcc $FLAGS -DMI355X_BUILD_DEFS="\"$DEFS\"" -DMI355X_SRC_ID="\"$SRC_ID\"" -c csrc/api.cpp -o $OUT/api.o &
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,-Bsymbolic -o lib/variants/lib_$NAME.so \
   $OBJS $OUT/api.o build/runtime.o build/init.o build/buffer_sizes.o build/tables_data.o
