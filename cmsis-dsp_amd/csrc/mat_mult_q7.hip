@@ -27,7 +27,7 @@
 #include "kernels.hpp"
 
 #ifndef MI355X_Q7_SCHED     // pinned fragment-read / MFMA / staging order in the steady K step
-#define MI355X_Q7_SCHED 0
+#define MI355X_Q7_SCHED 1
 #endif
 #ifndef MI355X_Q7_KT        // K bytes per LDS step: 64 or 128
 #define MI355X_Q7_KT 64
