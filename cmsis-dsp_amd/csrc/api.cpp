@@ -228,6 +228,15 @@ bool rfft_fixed_run(const RInst* S, T* d_src, T* d_dst, uint32_t batch, hipStrea
     MI_CHECK(pass(d_src, d_dst), "rfft merge");
     pr.flags |= kSatShl1;
     MI_CHECK(cfft_launch(kind, L, d_dst, batch, pr, st), "rfft cfft");
+  } else if (kind == 1 && L == 4096 && !pr.perm && (pr.flags & kBitrev) && MI355X_RFFT_Q31_FUSED) {
+    // one launch: the inner CFFT-4096 with the split fused into its last pass (cfft_fixed.hip)
+    MI_CHECK(rfft_q31_8192_fused_launch((int32_t*)d_src, (int32_t*)d_dst, batch, (const int32_t*)pr.tw,
+                                        (const int32_t*)ta, (const int32_t*)tb, S->twidCoefRModifier, st),
+             "rfft q31 fused");
+  } else if (kind == 2 && L == 4096 && !pr.perm && (pr.flags & kBitrev) && MI355X_RFFT_Q15_FUSED && MI355X_FX_Q15_PACKED) {
+    MI_CHECK(rfft_q15_8192_fused_launch((int16_t*)d_src, (int16_t*)d_dst, batch, (const int16_t*)pr.tw,
+                                        (const int16_t*)ta, (const int16_t*)tb, S->twidCoefRModifier, st),
+             "rfft q15 fused");
   } else {
     MI_CHECK(cfft_launch(kind, L, d_src, batch, pr, st), "rfft cfft");
     MI_CHECK(pass(d_src, d_dst), "rfft split");

@@ -15,6 +15,7 @@
 #include "common.hpp"
 #include "kernels.hpp"
 #include "cfft_fixed_core.hpp"
+#include "rfft_fixed_split.hpp"
 
 namespace mi355x {
 
@@ -129,9 +130,21 @@ template <typename C> constexpr int kFxSlots = sizeof(C) == 8 ? MI355X_FX_Q31_SL
 // BREV / SAT are the bitReverseFlag and the RFFT inverse's saturating <<1 (kSatShl1) as
 // template parameters: as run-time flags the compiler if-converted them into selects on
 // every output word and address.
-template <typename T, bool INV, bool BREV, bool SAT>
+// RSPLIT (the forward arm_rfft_q31 of N = 8192, whose inner CFFT this is): after pass 3 the
+// transform's bins also go to LDS in natural order, and the workgroup runs the RFFT's split on
+// them (rfft_fixed_split.hpp, arm_rfft_q31.c:256-341) straight into the 2N-word spectrum row --
+// the CFFT output is still stored to `data`, as the reference leaves pSrc, but never read back.
+template <typename T> struct RfSplitArgs {
+  T* dst = nullptr;                 // [batch][2 * 8192] spectrum rows
+  const T* ta = nullptr;            // realCoefA / B (device copies)
+  const T* tb = nullptr;
+  uint32_t mod = 0;                 // twidCoefRModifier
+};
+template <typename T, bool INV, bool BREV, bool SAT, bool RSPLIT = false>
 __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typename Fx<T>::C* __restrict__ data, uint32_t batch,
-                                                          const typename Fx<T>::C* __restrict__ tw) {
+                                                          const typename Fx<T>::C* __restrict__ tw,
+                                                          RfSplitArgs<T> rs = {}) {
+  static_assert(!RSPLIT || (!INV && BREV && !SAT), "the fused split follows the forward, bit-reversed CFFT");
   using F = Fx<T>;
   using C = typename F::C;
   using IO = FxIO<C>;
@@ -272,6 +285,16 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 #pragma unroll
       for (int u = 0; u < 16; ++u) IO::st(rx, 16 * q3 * kC, u * kC, o[u]);
     }
+    if constexpr (RSPLIT) {
+      __syncthreads();                  // every thread's pass-3 LDS reads are done
+#pragma unroll
+      for (int u = 0; u < 16; ++u) F::st(lds + sfx<C>((int)(__brev((uint32_t)u) >> 28) * 256 + t), v[u]);
+      __syncthreads();
+      T* y = rs.dst + (size_t)tr * (2 * 8192);
+      auto get = [&](int i) { return F::ld(lds + sfx<C>(i)); };
+#pragma unroll 2
+      for (int i = 0; i < 8; ++i) rfft_split_pair<T>(get, y, t + 256 * i, 8192, rs.ta, rs.tb, rs.mod);
+    }                                   // (the next pass 1 starts with a barrier before its LDS writes)
   };
   for (;;) {
 #pragma unroll
@@ -301,9 +324,12 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 // MI355X_FXQ15_TW34_LDS = 1: the stage-3/4 twiddle pairs (functions of t % 16 only) live in
 // LDS tables (1.5 KiB + 384 B) instead of 30 VGPRs; MI355X_FXQ15_WAVES = the minimum waves per
 // SIMD the register allocation must allow.
-template <bool INV, bool BREV, bool SAT>
+// RSPLIT: the forward arm_rfft_q15 of N = 8192 fused as in cfft_fx4096_kernel.
+template <bool INV, bool BREV, bool SAT, bool RSPLIT = false>
 __global__ __launch_bounds__(256, MI355X_FXQ15_WAVES) void cfft_q15_4096_pk_kernel(short2* __restrict__ data, uint32_t batch,
-                                                                    const short2* __restrict__ tw) {
+                                                                    const short2* __restrict__ tw,
+                                                                    RfSplitArgs<int16_t> rs) {
+  static_assert(!RSPLIT || (!INV && BREV && !SAT), "the fused split follows the forward, bit-reversed CFFT");
   __shared__ __attribute__((aligned(16))) uint32_t lds[MI355X_FXQ15_SLOTS];
   const int t = threadIdx.x;
   const int q2 = t >> 4, j2 = t & 15;
@@ -420,6 +446,19 @@ __global__ __launch_bounds__(256, MI355X_FXQ15_WAVES) void cfft_q15_4096_pk_kern
 #pragma unroll
       for (int u = 0; u < 16; ++u) __builtin_amdgcn_raw_buffer_store_b32((int)upk(v[u]), rx, 64 * q3, 4 * u, MI355X_FX_NT);
     }
+    if constexpr (RSPLIT) {
+      __syncthreads();                  // every thread's pass-3 LDS reads are done
+#pragma unroll
+      for (int u = 0; u < 16; ++u) lds[s4096((int)(__brev((uint32_t)u) >> 28) * 256 + t)] = upk(v[u]);
+      __syncthreads();
+      int16_t* y = rs.dst + (size_t)tr * (2 * 8192);
+      auto get = [&](int i) {
+        const uint32_t w = lds[s4096(i)];
+        return make_int2((int)(int16_t)(w & 0xffffu), (int)(int16_t)(w >> 16));
+      };
+#pragma unroll 2
+      for (int i = 0; i < 8; ++i) rfft_split_pair<int16_t>(get, y, t + 256 * i, 8192, rs.ta, rs.tb, rs.mod);
+    }                                   // (the next pass 1 starts with a barrier before its LDS writes)
   };
   for (;;) {
 #pragma unroll
@@ -441,17 +480,41 @@ __global__ __launch_bounds__(256, MI355X_FXQ15_WAVES) void cfft_q15_4096_pk_kern
 // of LDS per wave and 128 data VGPRs, leaving no room for the next transform's loads
 // (profiles/r02/variants_fx4096w/).  Removed in round 3.
 
+// The forward arm_rfft_q31 of N = 8192 in one launch: the inner CFFT-4096 (bit-reversed, pSrc
+// overwritten as the reference leaves it) with the split fused into its last pass.
+hipError_t rfft_q31_8192_fused_launch(int32_t* src, int32_t* dst, uint32_t batch, const int32_t* tw, const int32_t* ta,
+                                      const int32_t* tb, uint32_t mod, hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  auto k = cfft_fx4096_kernel<int32_t, false, true, false, true>;
+  const int grid = fx_grid<MI355X_FX_T>((const void*)k, batch);
+  RfSplitArgs<int32_t> rs;
+  rs.dst = dst; rs.ta = ta; rs.tb = tb; rs.mod = mod;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (int2*)src, batch, (const int2*)tw, rs);
+  return hipGetLastError();
+}
+
+hipError_t rfft_q15_8192_fused_launch(int16_t* src, int16_t* dst, uint32_t batch, const int16_t* tw, const int16_t* ta,
+                                      const int16_t* tb, uint32_t mod, hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  auto k = cfft_q15_4096_pk_kernel<false, true, false, true>;
+  const int grid = fx_grid<MI355X_FXQ15_T>((const void*)k, batch);
+  RfSplitArgs<int16_t> rs;
+  rs.dst = dst; rs.ta = ta; rs.tb = tb; rs.mod = mod;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (short2*)src, batch, (const short2*)tw, rs);
+  return hipGetLastError();
+}
+
 template <typename T, bool INV, bool BREV, bool SAT>
 static void launch_fx4096_t(void* data, uint32_t batch, const void* tw, hipStream_t st) {
   using C = typename Fx<T>::C;
   if constexpr (sizeof(T) == 2 && MI355X_FX_Q15_PACKED) {
     auto k = cfft_q15_4096_pk_kernel<INV, BREV, SAT>;
     const int grid = fx_grid<MI355X_FXQ15_T>((const void*)k, batch);
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (short2*)data, batch, (const short2*)tw);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (short2*)data, batch, (const short2*)tw, RfSplitArgs<int16_t>{});
   } else {
     auto k = cfft_fx4096_kernel<T, INV, BREV, SAT>;
     const int grid = fx_grid<MI355X_FX_T>((const void*)k, batch);
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (C*)data, batch, (const C*)tw);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (C*)data, batch, (const C*)tw, RfSplitArgs<T>{});
   }
 }
 

@@ -79,6 +79,11 @@ hipError_t rfft_f32_merge_launch(int n_real, const float* p, float* out, uint32_
 // RFFT q31 / q15 split (forward: src = [batch][N] CFFT(N/2) output -> dst [batch][2N]
 // spectrum) or merge (inverse: src = [batch][2N] spectrum rows -> dst [batch][N] inverse
 // CFFT input) pass.  ta / tb: device realCoef{A,B}; mod = the instance's modifier.
+// forward arm_rfft_q31, N = 8192 (reference tables), inner CFFT + split in one launch (cfft_fixed.hip)
+hipError_t rfft_q31_8192_fused_launch(int32_t* src, int32_t* dst, uint32_t batch, const int32_t* tw, const int32_t* ta,
+                                      const int32_t* tb, uint32_t mod, hipStream_t st);
+hipError_t rfft_q15_8192_fused_launch(int16_t* src, int16_t* dst, uint32_t batch, const int16_t* tw, const int16_t* ta,
+                                      const int16_t* tb, uint32_t mod, hipStream_t st);
 hipError_t rfft_q31_pass_launch(bool inverse, int n, const int32_t* src, int32_t* dst, uint32_t batch,
                                 const int32_t* ta, const int32_t* tb, uint32_t mod, hipStream_t st);
 hipError_t rfft_q15_pass_launch(bool inverse, int n, const int16_t* src, int16_t* dst, uint32_t batch,

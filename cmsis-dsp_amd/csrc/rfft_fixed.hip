@@ -16,31 +16,11 @@
 // Twiddle c = 2*modifier*k into realCoef{A,B} (shared 8192-entry tables, L2-resident).
 #include "common.hpp"
 #include "kernels.hpp"
+#include "rfft_fixed_split.hpp"
 
 namespace mi355x {
 
 namespace {
-
-// ((q63)x*y + 2^31) >> 32 forms of none.h:184-194 (SMMULR / SMMLAR / SMMLSR) -> common.hpp
-__device__ __forceinline__ int32_t wneg(int32_t a) { return (int32_t)(0u - (uint32_t)a); }
-// q15 x q15 product as a wrapping int32 term
-__device__ __forceinline__ uint32_t p16(int32_t a, int32_t b) { return (uint32_t)(a * b); }
-
-template <typename T> struct Cx;
-template <> struct Cx<int32_t> {
-  using C = int2;
-  __device__ static int2 ld(const int32_t* p) { return *reinterpret_cast<const int2*>(p); }
-  __device__ static void st(int32_t* p, int32_t re, int32_t im) { *reinterpret_cast<int2*>(p) = make_int2(re, im); }
-};
-template <> struct Cx<int16_t> {
-  __device__ static int2 ld(const int16_t* p) {
-    const short2 s = *reinterpret_cast<const short2*>(p);
-    return make_int2(s.x, s.y);
-  }
-  __device__ static void st(int16_t* p, int32_t re, int32_t im) {
-    *reinterpret_cast<short2*>(p) = make_short2((short)re, (short)im);
-  }
-};
 
 // Work mapping: a workgroup takes kper = min(L, 256) consecutive k for R signals at a time
 // (256 / kper signals side by side); each thread loads its k's twiddles once — a strided
@@ -117,29 +97,9 @@ __global__ __launch_bounds__(256) void rfft_fx_split_kernel(const T* __restrict_
   }
 }
 
-// Paired forward split: bins k and L - k read the same two CFFT bins (x[k], x[L-k]), so one
-// thread forms both (j in [1, L/2): bins j and L - j; j = 0: bins 0, L and L/2) and every
-// CFFT word is read once instead of twice.  Same arithmetic per bin as rfft_fx_split_kernel.
-template <typename T>
-__device__ __forceinline__ int2 rfft_split_bin(int2 a, int2 b, int32_t a1, int32_t a2, int32_t b1, int32_t b2) {
-  if constexpr (sizeof(T) == 4) {
-    int32_t re = mult_R(a.x, a1), im = mult_R(a.x, a2);
-    re = multSub_R(re, a.y, a2); im = multAcc_R(im, a.y, a1);
-    re = multSub_R(re, b.y, a2); im = multSub_R(im, b.y, b1);
-    re = multAcc_R(re, b.x, b1); im = multSub_R(im, b.x, a2);
-    return make_int2(re, im);
-  } else {
-    const int32_t re = (int32_t)(p16(a.x, a1) - p16(a.y, a2) + p16(b.x, b1) + p16(b.y, b2)) >> 16;
-    const int32_t im = (int32_t)(p16(b.x, b2) - p16(b.y, b1) + p16(a.y, a1) + p16(a.x, a2)) >> 16;
-    return make_int2(re, im);
-  }
-}
-template <typename T>
-__device__ __forceinline__ void rfft_st_pair(T* y, int k, int n, int2 v) {   // bin k and its mirror 2n - 2k
-  Cx<T>::st(y + 2 * k, v.x, v.y);
-  if constexpr (sizeof(T) == 4) Cx<T>::st(y + 2 * n - 2 * k, v.x, wneg(v.y));
-  else Cx<T>::st(y + 2 * n - 2 * k, v.x, -v.y);
-}
+// Paired forward split (rfft_fixed_split.hpp): bins k and L - k read the same two CFFT bins
+// (x[k], x[L-k]), so one thread forms both (j in [1, L/2): bins j and L - j; j = 0: bins 0, L and
+// L/2) and every CFFT word is read once instead of twice.
 template <typename T>
 __global__ __launch_bounds__(256) void rfft_fx_split2_kernel(const T* __restrict__ src, T* __restrict__ dst,
                                                              uint64_t rows, int n, const T* __restrict__ ta,

@@ -175,6 +175,12 @@
 #endif
 
 // ---- api.cpp
+#ifndef MI355X_RFFT_Q31_FUSED   // forward arm_rfft_q31 N = 8192: split fused into the inner CFFT's last pass
+#define MI355X_RFFT_Q31_FUSED 1
+#endif
+#ifndef MI355X_RFFT_Q15_FUSED   // ... and arm_rfft_q15
+#define MI355X_RFFT_Q15_FUSED 1
+#endif
 #ifndef MI355X_MFCC_FX_MODE
 #define MI355X_MFCC_FX_MODE 1
 #endif
