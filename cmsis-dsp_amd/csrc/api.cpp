@@ -209,15 +209,24 @@ bool rfft_fixed_run(const RInst* S, T* d_src, T* d_dst, uint32_t batch, hipStrea
   const auto* in = S->pCfft;
   if (!in || in->fftLen != L || !cfft_len_ok(L) || n > 8192) { set_error(hipErrorInvalidValue, "rfft instance"); return false; }
   BlobScope hold(st);
-  // the split reads realCoef[2*mod*k + 1] for k < L: mod * N words cover it
-  const size_t words = std::max<size_t>(2, (size_t)S->twidCoefRModifier * n);
-  const T* ta = (const T*)device_table(S->pTwiddleAReal, sizeof(T) * words);
-  const T* tb = (const T*)device_table(S->pTwiddleBReal, sizeof(T) * words);
-  if (!ta || !tb) return false;
   const bool inv = S->ifftFlagR == 1u;
   CfftPrep pr;
   if (!cfft_prepare(L, in->pTwiddle, in->pBitRevTable, in->bitRevLength, kind, inv ? 1 : 0, S->bitReverseFlagR, pr))
     return false;
+  // forward, the reference's own bit reversal, bitReverseFlag 1: the split runs inside the CFFT
+  // launch (cfft_fixed.hip L = 4096 from the tables as they are; cfft_fixed_r16.hip L = 256 .. 2048
+  // from packed per-bin records)
+  const bool fuse = !inv && !pr.perm && (pr.flags & kBitrev) &&
+                    (L == 4096 ? (kind == 1 ? MI355X_RFFT_Q31_FUSED : MI355X_RFFT_Q15_FUSED && MI355X_FX_Q15_PACKED)
+                               : L >= 256 && L <= 2048 && MI355X_RFFT_FX_R16_FUSED);
+  // the split / merge pass reads realCoef[2*mod*k + 1] for k < L: mod * N words cover it
+  const T *ta = nullptr, *tb = nullptr;
+  if (!fuse || L == 4096) {
+    const size_t words = std::max<size_t>(2, (size_t)S->twidCoefRModifier * n);
+    ta = (const T*)device_table(S->pTwiddleAReal, sizeof(T) * words);
+    tb = (const T*)device_table(S->pTwiddleBReal, sizeof(T) * words);
+    if (!ta || !tb) return false;
+  }
   auto pass = [&](const T* a, T* b) {
     if constexpr (kind == 1)
       return rfft_q31_pass_launch(inv, (int)n, a, b, batch, ta, tb, S->twidCoefRModifier, st);
@@ -228,15 +237,22 @@ bool rfft_fixed_run(const RInst* S, T* d_src, T* d_dst, uint32_t batch, hipStrea
     MI_CHECK(pass(d_src, d_dst), "rfft merge");
     pr.flags |= kSatShl1;
     MI_CHECK(cfft_launch(kind, L, d_dst, batch, pr, st), "rfft cfft");
-  } else if (kind == 1 && L == 4096 && !pr.perm && (pr.flags & kBitrev) && MI355X_RFFT_Q31_FUSED) {
-    // one launch: the inner CFFT-4096 with the split fused into its last pass (cfft_fixed.hip)
-    MI_CHECK(rfft_q31_8192_fused_launch((int32_t*)d_src, (int32_t*)d_dst, batch, (const int32_t*)pr.tw,
-                                        (const int32_t*)ta, (const int32_t*)tb, S->twidCoefRModifier, st),
-             "rfft q31 fused");
-  } else if (kind == 2 && L == 4096 && !pr.perm && (pr.flags & kBitrev) && MI355X_RFFT_Q15_FUSED && MI355X_FX_Q15_PACKED) {
-    MI_CHECK(rfft_q15_8192_fused_launch((int16_t*)d_src, (int16_t*)d_dst, batch, (const int16_t*)pr.tw,
-                                        (const int16_t*)ta, (const int16_t*)tb, S->twidCoefRModifier, st),
-             "rfft q15 fused");
+  } else if (fuse) {
+    if (L == 4096) {
+      MI_CHECK(kind == 1 ? rfft_q31_8192_fused_launch((int32_t*)d_src, (int32_t*)d_dst, batch, (const int32_t*)pr.tw,
+                                                      (const int32_t*)ta, (const int32_t*)tb, S->twidCoefRModifier, st)
+                         : rfft_q15_8192_fused_launch((int16_t*)d_src, (int16_t*)d_dst, batch, (const int16_t*)pr.tw,
+                                                      (const int16_t*)ta, (const int16_t*)tb, S->twidCoefRModifier, st),
+               "rfft fused");
+    } else {
+      const void* rec = device_split_records(S->pTwiddleAReal, S->pTwiddleBReal, S->twidCoefRModifier, L, (int)sizeof(T));
+      if (!rec) return false;
+      const bool done = kind == 1
+          ? rfft_q31_r16_fused_launch((int)L, (int32_t*)d_src, (int32_t*)d_dst, batch, (const int32_t*)pr.tw, rec, st)
+          : rfft_q15_r16_fused_launch((int)L, (int16_t*)d_src, (int16_t*)d_dst, batch, (const int16_t*)pr.tw, rec, st);
+      if (!done) { set_error(hipErrorInvalidValue, "rfft fused length"); return false; }
+      MI_CHECK(hipGetLastError(), "rfft fused");
+    }
   } else {
     MI_CHECK(cfft_launch(kind, L, d_src, batch, pr, st), "rfft cfft");
     MI_CHECK(pass(d_src, d_dst), "rfft split");

@@ -134,12 +134,6 @@ template <typename C> constexpr int kFxSlots = sizeof(C) == 8 ? MI355X_FX_Q31_SL
 // transform's bins also go to LDS in natural order, and the workgroup runs the RFFT's split on
 // them (rfft_fixed_split.hpp, arm_rfft_q31.c:256-341) straight into the 2N-word spectrum row --
 // the CFFT output is still stored to `data`, as the reference leaves pSrc, but never read back.
-template <typename T> struct RfSplitArgs {
-  T* dst = nullptr;                 // [batch][2 * 8192] spectrum rows
-  const T* ta = nullptr;            // realCoefA / B (device copies)
-  const T* tb = nullptr;
-  uint32_t mod = 0;                 // twidCoefRModifier
-};
 template <typename T, bool INV, bool BREV, bool SAT, bool RSPLIT = false>
 __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typename Fx<T>::C* __restrict__ data, uint32_t batch,
                                                           const typename Fx<T>::C* __restrict__ tw,
@@ -292,8 +286,9 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
       __syncthreads();
       T* y = rs.dst + (size_t)tr * (2 * 8192);
       auto get = [&](int i) { return F::ld(lds + sfx<C>(i)); };
+      const SplitStridedTab<T> tab{rs.ta, rs.tb, rs.mod};
 #pragma unroll 2
-      for (int i = 0; i < 8; ++i) rfft_split_pair<T>(get, y, t + 256 * i, 8192, rs.ta, rs.tb, rs.mod);
+      for (int i = 0; i < 8; ++i) rfft_split_pair<T>(get, y, t + 256 * i, 8192, tab);
     }                                   // (the next pass 1 starts with a barrier before its LDS writes)
   };
   for (;;) {
@@ -456,8 +451,9 @@ __global__ __launch_bounds__(256, MI355X_FXQ15_WAVES) void cfft_q15_4096_pk_kern
         const uint32_t w = lds[s4096(i)];
         return make_int2((int)(int16_t)(w & 0xffffu), (int)(int16_t)(w >> 16));
       };
+      const SplitStridedTab<int16_t> tab{rs.ta, rs.tb, rs.mod};
 #pragma unroll 2
-      for (int i = 0; i < 8; ++i) rfft_split_pair<int16_t>(get, y, t + 256 * i, 8192, rs.ta, rs.tb, rs.mod);
+      for (int i = 0; i < 8; ++i) rfft_split_pair<int16_t>(get, y, t + 256 * i, 8192, tab);
     }                                   // (the next pass 1 starts with a barrier before its LDS writes)
   };
   for (;;) {

@@ -30,6 +30,7 @@
 #include "cfft_fixed_core.hpp"
 #include "mfcc_fixed_ops.hpp"
 #include "mfcc_fixed_post.hpp"
+#include "rfft_fixed_split.hpp"
 
 namespace mi355x {
 
@@ -153,14 +154,19 @@ template <typename T> struct MqPostArgs {
   int nb_mel = 0, total = 0, nb_dct = 0, stage = 0;
   int kmin = 0, kcnt = 0;          // the bins the Mel filters read
 };
-template <typename T, int N, bool INV, bool BREV, bool SAT, bool PRE = false, bool POST = false>
+// RSPLIT (round 5): the forward arm_rfft_q31 / _q15 of fftLenReal = 2N in one launch, as
+// cfft_fx4096_kernel's RSPLIT: after the bit-reversed CFFT store (pSrc keeps the CFFT output, as
+// the reference leaves it) the bins go to the LDS image in natural order and the transform's P
+// threads run the split on them (8 bin pairs each) straight into its 4N-word spectrum row.
+template <typename T, int N, bool INV, bool BREV, bool SAT, bool PRE = false, bool POST = false, bool RSPLIT = false>
 __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : 1) void cfft_fx_r16_kernel(typename R16Ops<T, INV>::C* __restrict__ data,
                                                              uint32_t batch,
                                                              const typename R16Ops<T, INV>::C* __restrict__ tw,
                                                              const typename R16Ops<T, INV>::C* __restrict__ win = nullptr,
                                                              T* __restrict__ maxv = nullptr, int mstride = 0,
-                                                             MqPostArgs<T> pa = {}) {
+                                                             MqPostArgs<T> pa = {}, RfSplitArgs<T> rs = {}) {
   static_assert(!POST || (PRE && !INV && !SAT), "the fused MFCC runs the forward front end");
+  static_assert(!RSPLIT || (!PRE && !POST && !INV && BREV && !SAT), "the fused split follows the forward, bit-reversed CFFT");
   using R = R16<N>;
   using O = R16Ops<T, INV>;
   using V = typename O::V;
@@ -424,6 +430,20 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : 1) void cfft_fx_r16_
       if constexpr (BREV) O::st(rx, vin, bin[u] * kC, v[u]);
       else O::st(rx, (w * N + epos[u]) * kC, 0, v[u]);
     }
+    if constexpr (RSPLIT) {
+      __syncthreads();                                // every thread is done reading the image
+#pragma unroll
+      for (int u = 0; u < 16; ++u) lds[tp + bin[u]] = O::to_w(v[u]);   // natural bin order, unpadded
+      __syncthreads();
+      const uint32_t f = g * R::TPW + (uint32_t)w;
+      if (f < batch) {
+        T* y = rs.dst + (size_t)f * (4 * N);
+        auto get = [&](int i) { return O::unpack(O::from_w(lds[i])); };
+        const SplitRecTab<T> tab{rs.rec};
+#pragma unroll MI355X_RFFT_SPLIT_UNROLL
+        for (int i = 0; i < 8; ++i) rfft_split_pair<T>(get, y, tp + P * i, 2 * N, tab);
+      }
+    }                                                 // (the next pass 0 starts with a barrier)
     }
     if (++g >= gend) return;
     pass0(g);
@@ -436,7 +456,7 @@ static void launch_r16_t(void* data, uint32_t batch, const void* tw, hipStream_t
   const uint32_t ngroups = (batch + R16<N>::TPW - 1) / R16<N>::TPW;
   const uint32_t grid = (ngroups + MI355X_FXR_T - 1) / MI355X_FXR_T;
   hipLaunchKernelGGL((cfft_fx_r16_kernel<T, N, INV, BREV, SAT>), dim3(grid), dim3(kBlock), 0, st, (C*)data, batch,
-                     (const C*)tw, (const C*)nullptr, (T*)nullptr, 0, MqPostArgs<T>{});
+                     (const C*)tw, (const C*)nullptr, (T*)nullptr, 0, MqPostArgs<T>{}, RfSplitArgs<T>{});
 }
 
 template <typename T, int N>
@@ -459,7 +479,7 @@ static void launch_r16_mfcc(void* data, uint32_t batch, const void* tw, const vo
   const uint32_t grid = (ngroups + MI355X_FXR_T - 1) / MI355X_FXR_T;
   auto k = brev ? cfft_fx_r16_kernel<T, N, false, true, false, true> : cfft_fx_r16_kernel<T, N, false, false, false, true>;
   hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, st, (C*)data, batch, (const C*)tw, (const C*)win, maxv, mstride,
-                     MqPostArgs<T>{});
+                     MqPostArgs<T>{}, RfSplitArgs<T>{});
 }
 
 template <typename T, int N>
@@ -481,7 +501,7 @@ static hipError_t launch_r16_mfcc_fused(const void* data, uint32_t batch, const 
   const uint32_t ngroups = (batch + R16<N>::TPW - 1) / R16<N>::TPW;
   const uint32_t grid = (ngroups + MI355X_FXR_T - 1) / MI355X_FXR_T;
   hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), lds, st, (C*)data, batch, (const C*)tw, (const C*)win, (T*)nullptr,
-                     0, pa);
+                     0, pa, RfSplitArgs<T>{});
   return hipGetLastError();
 }
 
@@ -539,6 +559,39 @@ bool cfft_q31_r16_mfcc_launch(int n, int32_t* data, uint32_t batch, const int32_
 bool cfft_q15_r16_mfcc_launch(int n, int16_t* data, uint32_t batch, const int16_t* tw, const int16_t* win,
                               int16_t* maxv, int mstride, bool brev, hipStream_t st) {
   return dispatch_r16_mfcc<int16_t>(n, data, batch, tw, win, maxv, mstride, brev, st);
+}
+
+// The forward arm_rfft_q31 / _q15 of fftLenReal = 2n in one launch (n = 256 .. 2048, the
+// reference's own bit-reversal table, bitReverseFlag 1); false: not handled here.
+template <typename T, int N>
+static void launch_r16_rfft(T* src, T* dst, uint32_t batch, const T* tw, const void* rec, hipStream_t st) {
+  using C = typename R16Ops<T, false>::C;
+  const uint32_t ngroups = (batch + R16<N>::TPW - 1) / R16<N>::TPW;
+  const uint32_t grid = (ngroups + MI355X_FXR_T - 1) / MI355X_FXR_T;
+  RfSplitArgs<T> rs;
+  rs.dst = dst;
+  rs.rec = (const typename SplitRec<T>::R*)rec;
+  hipLaunchKernelGGL((cfft_fx_r16_kernel<T, N, false, true, false, false, false, true>), dim3(grid), dim3(kBlock), 0, st,
+                     (C*)src, batch, (const C*)tw, (const C*)nullptr, (T*)nullptr, 0, MqPostArgs<T>{}, rs);
+}
+template <typename T>
+static bool dispatch_r16_rfft(int n, T* src, T* dst, uint32_t batch, const T* tw, const void* rec, hipStream_t st) {
+  if (batch == 0 && n >= 256 && n <= 2048) return true;
+  switch (n) {
+    case 256:  launch_r16_rfft<T, 256>(src, dst, batch, tw, rec, st); return true;
+    case 512:  launch_r16_rfft<T, 512>(src, dst, batch, tw, rec, st); return true;
+    case 1024: launch_r16_rfft<T, 1024>(src, dst, batch, tw, rec, st); return true;
+    case 2048: launch_r16_rfft<T, 2048>(src, dst, batch, tw, rec, st); return true;
+    default:   return false;
+  }
+}
+bool rfft_q31_r16_fused_launch(int n, int32_t* src, int32_t* dst, uint32_t batch, const int32_t* tw, const void* rec,
+                               hipStream_t st) {
+  return dispatch_r16_rfft<int32_t>(n, src, dst, batch, tw, rec, st);
+}
+bool rfft_q15_r16_fused_launch(int n, int16_t* src, int16_t* dst, uint32_t batch, const int16_t* tw, const void* rec,
+                               hipStream_t st) {
+  return dispatch_r16_rfft<int16_t>(n, src, dst, batch, tw, rec, st);
 }
 
 // Returns true if N is handled here (the reference's own bit-reversal table only).

@@ -80,6 +80,13 @@ hipError_t rfft_f32_merge_launch(int n_real, const float* p, float* out, uint32_
 // spectrum) or merge (inverse: src = [batch][2N] spectrum rows -> dst [batch][N] inverse
 // CFFT input) pass.  ta / tb: device realCoef{A,B}; mod = the instance's modifier.
 // forward arm_rfft_q31, N = 8192 (reference tables), inner CFFT + split in one launch (cfft_fixed.hip)
+// forward arm_rfft_q31 / _q15 of fftLenReal = 2n, n = 256 .. 2048, in one launch (false: other n);
+// rec = device_split_records(A, B, mod, n, sizeof word)
+bool rfft_q31_r16_fused_launch(int n, int32_t* src, int32_t* dst, uint32_t batch, const int32_t* tw, const void* rec,
+                               hipStream_t st);
+bool rfft_q15_r16_fused_launch(int n, int16_t* src, int16_t* dst, uint32_t batch, const int16_t* tw, const void* rec,
+                               hipStream_t st);
+// ... and fftLenReal = 8192 (the CFFT-4096 specialists), from the instance's realCoefA / B
 hipError_t rfft_q31_8192_fused_launch(int32_t* src, int32_t* dst, uint32_t batch, const int32_t* tw, const int32_t* ta,
                                       const int32_t* tb, uint32_t mod, hipStream_t st);
 hipError_t rfft_q15_8192_fused_launch(int16_t* src, int16_t* dst, uint32_t batch, const int16_t* tw, const int16_t* ta,

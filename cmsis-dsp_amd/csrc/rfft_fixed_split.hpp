@@ -1,6 +1,7 @@
 // The fixed-point RFFT's forward split per bin (arm_split_rfft_q31, arm_rfft_q31.c:256-341;
 // arm_split_rfft_q15, the scalar branch of arm_rfft_q15.c), shared by the split pass
-// (rfft_fixed.hip) and the fused N = 8192 forward RFFT (cfft_fixed.hip).
+// (rfft_fixed.hip) and the fused forward RFFTs (cfft_fixed.hip N = 8192, cfft_fixed_r16.hip
+// N = 512 .. 4096).
 #pragma once
 #include "common.hpp"
 
@@ -50,16 +51,53 @@ __device__ __forceinline__ void rfft_st_pair(T* y, int k, int n, int2 v) {   // 
   if constexpr (sizeof(T) == 4) Cx<T>::st(y + 2 * n - 2 * k, v.x, wneg(v.y));
   else Cx<T>::st(y + 2 * n - 2 * k, v.x, -v.y);
 }
+// The split's twiddle record of bin k, (A0, A1, B0, B1) = (A[2 mod k], A[2 mod k + 1], B[2 mod k],
+// B[2 mod k + 1]) (arm_rfft_q31.c:293-326 index), from one of two sources:
+//  * SplitRecTab: packed per-bin records (device_split_records, runtime.hpp; int4 for q31, 8-B
+//    short4 for q15), one load per bin -- the radix-16 fused RFFTs, whose mod = 8192 / N >= 2
+//    would otherwise read four words at a stride of 2 mod;
+//  * SplitStridedTab: the instance's tables as they are -- the N = 8192 fused RFFTs (mod = 1, the
+//    words of a bin are adjacent): measured faster there than the records (q15 610 vs 564-567
+//    Gsamples/s on one box, profiles/r05/ab_o2; q31 equal).
+template <typename T> struct SplitRec;
+template <> struct SplitRec<int32_t> { using R = int4; };
+template <> struct SplitRec<int16_t> { using R = short4; };
+template <typename T> struct SplitRecTab {
+  const typename SplitRec<T>::R* rec;
+  __device__ int4 operator()(int k) const {
+    const auto r = rec[k];
+    return make_int4(r.x, r.y, r.z, r.w);
+  }
+};
+template <typename T> struct SplitStridedTab {
+  const T* ta;
+  const T* tb;
+  uint32_t mod;
+  __device__ int4 operator()(int k) const {
+    const uint32_t c = 2u * mod * (uint32_t)k;
+    return make_int4(ta[c], ta[c + 1], tb[c], tb[c + 1]);
+  }
+};
+
+// Arguments of a CFFT kernel that runs the split on its own output (the fused forward RFFT)
+template <typename T> struct RfSplitArgs {
+  T* dst = nullptr;                                  // [batch][2 * fftLenReal] spectrum rows
+  const typename SplitRec<T>::R* rec = nullptr;      // SplitRecTab
+  const T* ta = nullptr;                             // SplitStridedTab
+  const T* tb = nullptr;
+  uint32_t mod = 0;
+};
+
 // Paired split unit j of one row (j in [0, L/2)): bins j and L - j with their mirrors (j = 0: bins
-// 0, L and L/2), from get(i) = CFFT bin i of the row; y = the row's 2N-word spectrum.
-template <typename T, typename Get>
-__device__ __forceinline__ void rfft_split_pair(Get get, T* __restrict__ y, int j, int n, const T* __restrict__ ta,
-                                                const T* __restrict__ tb, uint32_t mod) {
+// 0, L and L/2), from get(i) = CFFT bin i of the row and tab(k) = the record of bin k; y = the
+// row's 2N-word spectrum.
+template <typename T, typename Get, typename Tab>
+__device__ __forceinline__ void rfft_split_pair(Get get, T* __restrict__ y, int j, int n, const Tab& tab) {
   const int L = n >> 1, H = L >> 1;
   const int k2 = j == 0 ? H : L - j;
-  const uint32_t c1 = 2u * mod * (uint32_t)j, c2 = 2u * mod * (uint32_t)k2;
   const int2 a = get(j), b = get(k2);
-  const int2 v2 = rfft_split_bin<T>(b, j == 0 ? b : a, ta[c2], ta[c2 + 1], tb[c2], tb[c2 + 1]);
+  const int4 r2 = tab(k2);
+  const int2 v2 = rfft_split_bin<T>(b, j == 0 ? b : a, r2.x, r2.y, r2.z, r2.w);
   if (j == 0) {
     if constexpr (sizeof(T) == 4) {
       Cx<T>::st(y + n, wsub(a.x, a.y) >> 1, 0);
@@ -69,7 +107,8 @@ __device__ __forceinline__ void rfft_split_pair(Get get, T* __restrict__ y, int 
       Cx<T>::st(y, (a.x + a.y) >> 1, 0);
     }
   } else {
-    rfft_st_pair<T>(y, j, n, rfft_split_bin<T>(a, b, ta[c1], ta[c1 + 1], tb[c1], tb[c1 + 1]));
+    const int4 r1 = tab(j);
+    rfft_st_pair<T>(y, j, n, rfft_split_bin<T>(a, b, r1.x, r1.y, r1.z, r1.w));
   }
   rfft_st_pair<T>(y, k2, n, v2);
 }

@@ -374,6 +374,59 @@ const void* device_blob(const void* host, size_t bytes) {
   return hand_out(b);
 }
 
+const void* device_split_records(const void* A, const void* B, uint32_t mod, uint32_t L, int elem) {
+  if (!A || !B || !mod || !L || (elem != 2 && elem != 4)) {
+    set_error(hipErrorInvalidValue, "split records");
+    return nullptr;
+  }
+  const int dev = cur_dev();
+  const bool lib = is_library_addr(A) && is_library_addr(B);
+  using Key = std::tuple<int, const void*, const void*, uint32_t, uint32_t, int>;
+  static std::map<Key, void*>* built = new std::map<Key, void*>;   // library tables: never freed
+  const Key key{dev, A, B, mod, L, elem};
+  if (lib) {
+    std::lock_guard<std::mutex> lk(g_table_mu);
+    auto it = built->find(key);
+    if (it != built->end()) return it->second;
+  }
+  // the words read: A/B[2 mod k + {0, 1}] for k < L
+  const size_t words = 2 * (size_t)mod * (L - 1) + 2, wb = words * (size_t)elem;
+  std::vector<uint8_t> ha(wb), hb(wb);
+  for (int s = 0; s < 2; ++s) {
+    const void* src = s ? B : A;
+    uint8_t* dst = s ? hb.data() : ha.data();
+    if (is_device_ptr(src)) {
+      if (hipMemcpy(dst, src, wb, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error(hipErrorInvalidValue, "split records: table copy");
+        return nullptr;
+      }
+    } else {
+      memcpy(dst, src, wb);
+    }
+  }
+  std::vector<uint8_t> rec((size_t)L * 4 * elem);
+  for (uint32_t k = 0; k < L; ++k) {
+    const size_t c = 2 * (size_t)mod * k * elem;
+    uint8_t* r = rec.data() + (size_t)k * 4 * elem;
+    memcpy(r, ha.data() + c, 2 * (size_t)elem);
+    memcpy(r + 2 * elem, hb.data() + c, 2 * (size_t)elem);
+  }
+  const size_t rb = rec.size();
+  if (!lib) return device_blob(rec.data(), rb);
+  void* d = nullptr;
+  hipError_t e = hipMalloc(&d, rb);
+  if (e == hipSuccess) e = hipMemcpy(d, rec.data(), rb, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    set_error(e, "split records: upload");
+    if (d) (void)hipFree(d);
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lk(g_table_mu);
+  auto ins = built->emplace(key, d);
+  if (!ins.second) { (void)hipFree(d); return ins.first->second; }   // another thread built it first
+  return d;
+}
+
 size_t blob_cache_bytes() {
   std::lock_guard<std::mutex> lk(g_table_mu);
   size_t s = 0;
@@ -400,10 +453,18 @@ BlobScope::BlobScope(hipStream_t st) : st_(st), base_(t_held.size()), dev_(cur_d
 BlobScope::~BlobScope() {
   --t_scopes;
   if (t_held.size() <= base_) return;
+  // Insertions made while every other blob was held may have left the cache over its limit
+  // (held blobs are never evicted); the scope that drops the last hold trims it back, so the
+  // limit holds again whenever no call is live.
+  std::vector<BlobRef> victims;
   if (synced_) {                            // nothing of this call is still pending
-    std::lock_guard<std::mutex> lk(g_table_mu);
-    for (size_t i = base_; i < t_held.size(); ++i) --t_held[i]->holds;
+    {
+      std::lock_guard<std::mutex> lk(g_table_mu);
+      for (size_t i = base_; i < t_held.size(); ++i) --t_held[i]->holds;
+      if (cache().bytes[dev_] > cache().limit) victims = evict_locked(dev_, 0);
+    }
     t_held.resize(base_);
+    release_blobs(victims);
     return;
   }
   // one event after everything this scope enqueued on st_, attached to every blob it held
@@ -438,8 +499,10 @@ BlobScope::~BlobScope() {
       else b.unscoped = true;                // untracked use: release after a device sync
       --b.holds;
     }
+    if (cache().bytes[dev_] > cache().limit) victims = evict_locked(dev_, 0);
   }
   t_held.resize(base_);
+  release_blobs(victims);
 }
 
 const uint16_t* device_perm(int n, const uint16_t* table, uint16_t len, int kind, bool* canonical, bool* ok) {

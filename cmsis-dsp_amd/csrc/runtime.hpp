@@ -37,6 +37,13 @@ const void* device_table(const void* host, size_t bytes);
 // until the work enqueued before that scope ended has completed.  Returns nullptr on failure.
 const void* device_blob(const void* host, size_t bytes);
 size_t blob_cache_bytes();
+
+// Device table of the fixed-point RFFT split's per-bin twiddle records, bin k < L:
+// {A[2 mod k], A[2 mod k + 1], B[2 mod k], B[2 mod k + 1]} (arm_rfft_q31.c:293-326 index), `elem`
+// bytes per word (4: int4 records, 2: 8-B records), so that a split reads one record per bin
+// instead of four words at a stride of 2 mod (rfft_fixed_split.hpp SplitRecTab).  The library's own tables: built once per (device,
+// A, B, mod, L); any other (host or device) table: rebuilt per call and cached by content.
+const void* device_split_records(const void* A, const void* B, uint32_t mod, uint32_t L, int elem);
 void set_blob_cache_limit(size_t bytes);   // per device
 
 // Pins every blob device_blob / device_table / device_perm hand out on this thread while the

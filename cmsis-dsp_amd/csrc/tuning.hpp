@@ -178,6 +178,12 @@
 #ifndef MI355X_RFFT_Q31_FUSED   // forward arm_rfft_q31 N = 8192: split fused into the inner CFFT's last pass
 #define MI355X_RFFT_Q31_FUSED 1
 #endif
+#ifndef MI355X_RFFT_FX_R16_FUSED   // forward arm_rfft_q31 / _q15 N = 512 .. 4096: split fused into the radix-16 CFFT
+#define MI355X_RFFT_FX_R16_FUSED 1
+#endif
+#ifndef MI355X_RFFT_SPLIT_UNROLL   // fused radix-16 split: bin pairs per unrolled step
+#define MI355X_RFFT_SPLIT_UNROLL 2
+#endif
 #ifndef MI355X_RFFT_Q15_FUSED   // ... and arm_rfft_q15
 #define MI355X_RFFT_Q15_FUSED 1
 #endif

@@ -112,12 +112,13 @@ def test_rfft_fixed_batch_bitexact(dsp, torch_gpu, ref, kind, n, ifft):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["q31", "q15"])
-def test_rfft_fixed_extremes_and_large_batch(dsp, torch_gpu, ref, kind):
+@pytest.mark.parametrize("n", [512, 2048, 4096, 8192])
+def test_rfft_fixed_extremes_and_large_batch(dsp, torch_gpu, ref, kind, n):
     """All-extreme words (wrap in the split sums, saturation in the inverse shift) and a
-    batch above one launch's persistent grid at N = 8192 (the inner CFFT is the 4096
-    specialist)."""
+    batch above one launch's persistent grid (N = 8192: the inner CFFT is the 4096
+    specialist; N = 512 .. 4096 the radix-16 kernel; both run the forward split fused)."""
     torch = torch_gpu
-    n, batch = 8192, 1100
+    batch = 1100
     for ifft in (0, 1):
         words = 2 * n if ifft else n
         x = np.stack([refs.rand_input(kind, words, seed=r, dist="extreme" if r % 2 else "uniform")

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-5 GPU step O: same-box A/B of the packed-record fused RFFT q31/q15 (default: N = 512 ..
+# 8192 fused) against the previous commit's library (lib_prev: N = 8192 fused with strided
+# table reads, other N two launches), alternating repetitions (o1: 3 with 8-B q15 records; o2: the
+# q15 records in v_dot2 pairs, after the RFFT / MFCC / runtime GPU tests).
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/${STEP:-o2}; mkdir -p $O
+step() { local t=$1; shift; timeout -k 10 $t "$@"; local rc=$?; [ $rc -eq 0 ] || { echo "step rc=$rc: $*"; exit $rc; }; }
+show() { python -c "import json;d=json.load(open('$1'));p=d['parity'];print('$2',d['value'],d['roofline']['frac'],d['roofline']['avg_kernel_ms'],p.get('bit_exact',p) if isinstance(p,dict) else p)"; }
+lib() { [ $1 = default ] && echo cmsis-dsp_amd/lib/libcmsisdsp_mi355x.so || echo cmsis-dsp_amd/lib/variants/lib_$1.so; }
+PT="-x -q --timeout 120 --timeout-method thread -p no:cacheprovider"
+step 400 python -u -m pytest tests/test_rfft_fixed.py tests/test_gpu_runtime.py tests/test_mfcc_q31.py tests/test_mfcc_q15.py -m gpu $PT > $O/t_fused.log 2>&1
+echo "fused tests: $(tail -1 $O/t_fused.log)"
+for rep in 1 2; do
+for v in default prev; do
+  for w in rfft_q31 rfft_q15; do
+    for n in 1024 4096 8192; do
+      CMSISDSP_MI355X_LIB=$(lib $v) step 200 python -u bench.py --workload $w --fftlen $n --no-cpu-baseline > $O/${w}_${n}_${v}_$rep.json 2> $O/${w}_${n}_${v}_$rep.err
+      show $O/${w}_${n}_${v}_$rep.json ${w}_${n}_$v
+    done
+  done
+done
+done
+echo all-ok
