@@ -158,7 +158,14 @@ template <typename T> struct MqPostArgs {
 // cfft_fx4096_kernel's RSPLIT: after the bit-reversed CFFT store (pSrc keeps the CFFT output, as
 // the reference leaves it) the bins go to the LDS image in natural order and the transform's P
 // threads run the split on them (8 bin pairs each) straight into its 4N-word spectrum row.
-template <typename T, int N, bool INV, bool BREV, bool SAT, bool PRE = false, bool POST = false, bool RSPLIT = false>
+// RMERGE (round 5): the inverse arm_rfft_q31 / _q15 of fftLenReal = 2N in one launch.  The first
+// pass's loads read spectrum bins X[e] and X[N - e] of the input row (rs.spec, 4N words per row)
+// instead of the CFFT input, and the merge (rfft_merge_bin, arm_rfft_q31.c:397-476) forms element
+// e in registers from them and the bin's record (staged once per workgroup in LDS) before the
+// butterflies; the CFFT (inverse, the final arm_shift(+1) folded into the store) then writes the
+// output rows in place of `data`.  The merge pass's write and the CFFT's re-read disappear.
+template <typename T, int N, bool INV, bool BREV, bool SAT, bool PRE = false, bool POST = false, bool RSPLIT = false,
+          bool RMERGE = false>
 __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : 1) void cfft_fx_r16_kernel(typename R16Ops<T, INV>::C* __restrict__ data,
                                                              uint32_t batch,
                                                              const typename R16Ops<T, INV>::C* __restrict__ tw,
@@ -167,6 +174,7 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : 1) void cfft_fx_r16_
                                                              MqPostArgs<T> pa = {}, RfSplitArgs<T> rs = {}) {
   static_assert(!POST || (PRE && !INV && !SAT), "the fused MFCC runs the forward front end");
   static_assert(!RSPLIT || (!PRE && !POST && !INV && BREV && !SAT), "the fused split follows the forward, bit-reversed CFFT");
+  static_assert(!RMERGE || (!PRE && !POST && !RSPLIT && INV && SAT), "the fused merge precedes the inverse CFFT");
   using R = R16<N>;
   using O = R16Ops<T, INV>;
   using V = typename O::V;
@@ -250,10 +258,31 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : 1) void cfft_fx_r16_
   };
   const int vin = (w * N + tp) * kC;                  // byte offset of the thread's first word
   V nq[16];
+  V nq2[RMERGE ? 16 : 1];                             // RMERGE: bins X[N - e]
+  using Rec = typename SplitRec<T>::R;
+  __shared__ Rec recl[RMERGE ? N : 1];                // RMERGE: the merge records of bins 0 .. N-1
+  if constexpr (RMERGE) {
+    for (int i = t; i < N; i += kBlock) recl[i] = rs.rec[i];
+    __syncthreads();
+  }
+  // RMERGE: spectrum row f at rs.spec + f * 4N words (2N complex); X[e] at complex e, X[N - e]
+  // at complex N - tp - P u = (P - tp) + P (15 - u), a non-negative immediate per u
+  const int vsa = (w * 2 * N + tp) * kC, vsb = (w * 2 * N + P - tp) * kC;
   auto fetch = [&](uint32_t g) {
-    const __amdgpu_buffer_rsrc_t r = group_rsrc(g);
+    if constexpr (RMERGE) {
+      const uint32_t first = g * R::TPW;
+      const uint32_t valid = min((uint32_t)R::TPW, batch - first);
+      const __amdgpu_buffer_rsrc_t r = fx_rsrc((const C*)(rs.spec + (size_t)first * 4 * N), valid * 2 * N * kC);
 #pragma unroll
-    for (int u = 0; u < 16; ++u) nq[u] = O::ld(r, vin, P * u * kC);   // e = tp + P u
+      for (int u = 0; u < 16; ++u) {
+        nq[u] = O::ld(r, vsa, P * u * kC);
+        nq2[u] = O::ld(r, vsb, P * (15 - u) * kC);
+      }
+    } else {
+      const __amdgpu_buffer_rsrc_t r = group_rsrc(g);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) nq[u] = O::ld(r, vin, P * u * kC);   // e = tp + P u
+    }
   };
   V v[16];
   __shared__ int32_t red[PRE && P > 64 ? 2 * R::TPW : 1];
@@ -262,6 +291,25 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : 1) void cfft_fx_r16_
   auto pass0 = [&](uint32_t g) {
 #pragma unroll
     for (int u = 0; u < 16; ++u) v[u] = nq[u];
+    if constexpr (RMERGE) {
+      // The records are the same for every group: an opaque index keeps their LDS reads here
+      // (hoisted out of the group loop they held 64 VGPRs for the kernel's life), in blocks of
+      // MI355X_RFFT_MERGE_BLK elements read and merged before the next block's.
+      int ri = tp;
+      asm volatile("" : "+v"(ri));
+#pragma unroll
+      for (int u0 = 0; u0 < 16; u0 += MI355X_RFFT_MERGE_BLK) {
+        Rec rc[MI355X_RFFT_MERGE_BLK];
+#pragma unroll
+        for (int u = 0; u < MI355X_RFFT_MERGE_BLK; ++u) rc[u] = recl[ri + P * (u0 + u)];
+#pragma unroll
+        for (int u = 0; u < MI355X_RFFT_MERGE_BLK; ++u) {
+          const int2 m = rfft_merge_bin<T>(O::unpack(v[u0 + u]), O::unpack(nq2[u0 + u]), rc[u].x, rc[u].y, rc[u].z, rc[u].w);
+          v[u0 + u] = O::pack(m.x, m.y);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
     int32_t mframe = 0;                               // POST: this transform's frame maximum
     if constexpr (PRE) {
       using Pre = MqPre<T>;
@@ -585,6 +633,40 @@ static bool dispatch_r16_rfft(int n, T* src, T* dst, uint32_t batch, const T* tw
     default:   return false;
   }
 }
+// The inverse arm_rfft_q31 / _q15 of fftLenReal = 2n in one launch (n = 256 .. 2048, the
+// reference's own bit-reversal table, bitReverseFlag 1): spec [batch][4n] spectrum rows (bins 0..n
+// read), dst [batch][2n]; false: not handled here.
+template <typename T, int N>
+static void launch_r16_irfft(const T* spec, T* dst, uint32_t batch, const T* tw, const void* rec, hipStream_t st) {
+  using C = typename R16Ops<T, true>::C;
+  const uint32_t ngroups = (batch + R16<N>::TPW - 1) / R16<N>::TPW;
+  const uint32_t grid = (ngroups + MI355X_FXR_T - 1) / MI355X_FXR_T;
+  RfSplitArgs<T> rs;
+  rs.spec = spec;
+  rs.rec = (const typename SplitRec<T>::R*)rec;
+  hipLaunchKernelGGL((cfft_fx_r16_kernel<T, N, true, true, true, false, false, false, true>), dim3(grid), dim3(kBlock), 0,
+                     st, (C*)dst, batch, (const C*)tw, (const C*)nullptr, (T*)nullptr, 0, MqPostArgs<T>{}, rs);
+}
+template <typename T>
+static bool dispatch_r16_irfft(int n, const T* spec, T* dst, uint32_t batch, const T* tw, const void* rec, hipStream_t st) {
+  if (batch == 0 && n >= 256 && n <= 2048) return true;
+  switch (n) {
+    case 256:  launch_r16_irfft<T, 256>(spec, dst, batch, tw, rec, st); return true;
+    case 512:  launch_r16_irfft<T, 512>(spec, dst, batch, tw, rec, st); return true;
+    case 1024: launch_r16_irfft<T, 1024>(spec, dst, batch, tw, rec, st); return true;
+    case 2048: launch_r16_irfft<T, 2048>(spec, dst, batch, tw, rec, st); return true;
+    default:   return false;
+  }
+}
+bool rfft_q31_r16_inv_fused_launch(int n, const int32_t* spec, int32_t* dst, uint32_t batch, const int32_t* tw,
+                                   const void* rec, hipStream_t st) {
+  return dispatch_r16_irfft<int32_t>(n, spec, dst, batch, tw, rec, st);
+}
+bool rfft_q15_r16_inv_fused_launch(int n, const int16_t* spec, int16_t* dst, uint32_t batch, const int16_t* tw,
+                                   const void* rec, hipStream_t st) {
+  return dispatch_r16_irfft<int16_t>(n, spec, dst, batch, tw, rec, st);
+}
+
 bool rfft_q31_r16_fused_launch(int n, int32_t* src, int32_t* dst, uint32_t batch, const int32_t* tw, const void* rec,
                                hipStream_t st) {
   return dispatch_r16_rfft<int32_t>(n, src, dst, batch, tw, rec, st);

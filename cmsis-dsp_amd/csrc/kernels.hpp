@@ -86,6 +86,12 @@ bool rfft_q31_r16_fused_launch(int n, int32_t* src, int32_t* dst, uint32_t batch
                                hipStream_t st);
 bool rfft_q15_r16_fused_launch(int n, int16_t* src, int16_t* dst, uint32_t batch, const int16_t* tw, const void* rec,
                                hipStream_t st);
+// inverse arm_rfft_q31 / _q15 of fftLenReal = 2n, n = 256 .. 2048, in one launch (merge fused into
+// the radix-16 CFFT's first pass; false: other n); spec [batch][4n], dst [batch][2n]
+bool rfft_q31_r16_inv_fused_launch(int n, const int32_t* spec, int32_t* dst, uint32_t batch, const int32_t* tw,
+                                   const void* rec, hipStream_t st);
+bool rfft_q15_r16_inv_fused_launch(int n, const int16_t* spec, int16_t* dst, uint32_t batch, const int16_t* tw,
+                                   const void* rec, hipStream_t st);
 // ... and fftLenReal = 8192 (the CFFT-4096 specialists), from the instance's realCoefA / B
 hipError_t rfft_q31_8192_fused_launch(int32_t* src, int32_t* dst, uint32_t batch, const int32_t* tw, const int32_t* ta,
                                       const int32_t* tb, uint32_t mod, hipStream_t st);

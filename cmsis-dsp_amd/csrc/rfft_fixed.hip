@@ -182,21 +182,6 @@ __global__ __launch_bounds__(256) void rfft_fx_merge_kernel(const T* __restrict_
 // Paired inverse merge: bins k and L - k of the N-word CFFT input read the same two spectrum
 // bins (X[k], X[L-k]); j in [1, L/2) forms both, j = 0 forms bin 0 (X[0], X[L]) and bin L/2.
 template <typename T>
-__device__ __forceinline__ int2 rfft_merge_bin(int2 a, int2 b, int32_t a1, int32_t a2, int32_t b1, int32_t b2) {
-  if constexpr (sizeof(T) == 4) {
-    // arm_rfft_q31.c:430-466
-    int32_t re = mult_R(a.x, a1), im = mult_R(a.x, wneg(a2));
-    re = multAcc_R(re, a.y, a2); im = multAcc_R(im, a.y, a1);
-    re = multAcc_R(re, b.y, a2); im = multSub_R(im, b.y, b1);
-    re = multAcc_R(re, b.x, b1); im = multAcc_R(im, b.x, a2);
-    return make_int2(re, im);
-  } else {
-    const int32_t re = (int32_t)(p16(b.x, b1) - p16(b.y, b2) + p16(a.x, a1) + p16(a.y, a2)) >> 16;
-    const int32_t im = (int32_t)(p16(a.y, a1) - p16(a.x, a2) - p16(b.x, b2) - p16(b.y, b1)) >> 16;
-    return make_int2(re, im);
-  }
-}
-template <typename T>
 __global__ __launch_bounds__(256) void rfft_fx_merge2_kernel(const T* __restrict__ src, T* __restrict__ dst,
                                                              uint64_t rows, int n, const T* __restrict__ ta,
                                                              const T* __restrict__ tb, uint32_t mod) {

@@ -1,7 +1,8 @@
 // The fixed-point RFFT's forward split per bin (arm_split_rfft_q31, arm_rfft_q31.c:256-341;
 // arm_split_rfft_q15, the scalar branch of arm_rfft_q15.c), shared by the split pass
 // (rfft_fixed.hip) and the fused forward RFFTs (cfft_fixed.hip N = 8192, cfft_fixed_r16.hip
-// N = 512 .. 4096).
+// N = 512 .. 4096); the inverse's merge per bin (arm_split_rifft_q31, arm_rfft_q31.c:397-476; the
+// q15 scalar branch), shared by the merge pass and the fused inverse (cfft_fixed_r16.hip).
 #pragma once
 #include "common.hpp"
 
@@ -45,6 +46,22 @@ __device__ __forceinline__ int2 rfft_split_bin(int2 a, int2 b, int32_t a1, int32
     return make_int2(re, im);
   }
 }
+// CFFT input element k of the inverse from spectrum bins a = X[k], b = X[L - k] and the k-th record
+template <typename T>
+__device__ __forceinline__ int2 rfft_merge_bin(int2 a, int2 b, int32_t a1, int32_t a2, int32_t b1, int32_t b2) {
+  if constexpr (sizeof(T) == 4) {
+    // arm_rfft_q31.c:430-466
+    int32_t re = mult_R(a.x, a1), im = mult_R(a.x, wneg(a2));
+    re = multAcc_R(re, a.y, a2); im = multAcc_R(im, a.y, a1);
+    re = multAcc_R(re, b.y, a2); im = multSub_R(im, b.y, b1);
+    re = multAcc_R(re, b.x, b1); im = multAcc_R(im, b.x, a2);
+    return make_int2(re, im);
+  } else {
+    const int32_t re = (int32_t)(p16(b.x, b1) - p16(b.y, b2) + p16(a.x, a1) + p16(a.y, a2)) >> 16;
+    const int32_t im = (int32_t)(p16(a.y, a1) - p16(a.x, a2) - p16(b.x, b2) - p16(b.y, b1)) >> 16;
+    return make_int2(re, im);
+  }
+}
 template <typename T>
 __device__ __forceinline__ void rfft_st_pair(T* y, int k, int n, int2 v) {   // bin k and its mirror 2n - 2k
   Cx<T>::st(y + 2 * k, v.x, v.y);
@@ -82,7 +99,8 @@ template <typename T> struct SplitStridedTab {
 // Arguments of a CFFT kernel that runs the split on its own output (the fused forward RFFT)
 template <typename T> struct RfSplitArgs {
   T* dst = nullptr;                                  // [batch][2 * fftLenReal] spectrum rows
-  const typename SplitRec<T>::R* rec = nullptr;      // SplitRecTab
+  const typename SplitRec<T>::R* rec = nullptr;      // SplitRecTab (split and merge)
+  const T* spec = nullptr;                           // the fused inverse's input spectrum rows
   const T* ta = nullptr;                             // SplitStridedTab
   const T* tb = nullptr;
   uint32_t mod = 0;

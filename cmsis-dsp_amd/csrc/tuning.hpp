@@ -181,6 +181,12 @@
 #ifndef MI355X_RFFT_FX_R16_FUSED   // forward arm_rfft_q31 / _q15 N = 512 .. 4096: split fused into the radix-16 CFFT
 #define MI355X_RFFT_FX_R16_FUSED 1
 #endif
+#ifndef MI355X_RFFT_FX_R16_INV_FUSED   // inverse arm_rfft_q31 / _q15 N = 512 .. 4096: merge fused into the radix-16 CFFT
+#define MI355X_RFFT_FX_R16_INV_FUSED 1
+#endif
+#ifndef MI355X_RFFT_MERGE_BLK   // fused inverse: merged elements per pinned block
+#define MI355X_RFFT_MERGE_BLK 4
+#endif
 #ifndef MI355X_RFFT_SPLIT_UNROLL   // fused radix-16 split: bin pairs per unrolled step
 #define MI355X_RFFT_SPLIT_UNROLL 2
 #endif
