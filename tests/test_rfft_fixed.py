@@ -143,3 +143,46 @@ def test_rfft_fixed_dropin(dsp, torch_gpu, ref, kind, n):
         S = _instance(dsp, kind, n, ifft, 1)
         got = getattr(dsp, f"arm_rfft_{kind}")(S, x)
         assert got.tobytes() == ref.rfft_fixed(kind, n, x, ifft, 1)[0].tobytes(), ifft
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["q31", "q15"])
+@pytest.mark.parametrize("n", [1024, 4096, 8192])
+@pytest.mark.parametrize("where", ["host", "device"])
+def test_rfft_fixed_user_tables(dsp, torch_gpu, ref, kind, n, where):
+    """realCoefA / B that are not the library's own (host or device buffers, contents changed):
+    the fused kernels' packed per-bin records (device_split_records) must be built from them, per
+    call, forward and inverse, bit-exact against the reference on the same tables."""
+    import ctypes as C
+    torch = torch_gpu
+    dt = DT[kind]
+    ptr_t = C.POINTER(C.c_int32 if kind == "q31" else C.c_int16)
+    rng = np.random.default_rng(n + (kind == "q15"))
+    batch = 9
+    for ifft in (0, 1):
+        S = _instance(dsp, kind, n, ifft, 1)
+        Sr = (refs._abi.arm_rfft_instance_q31 if kind == "q31" else refs._abi.arm_rfft_instance_q15)()
+        assert ref.fn(f"arm_rfft_init_{kind}")(C.byref(Sr), n, ifft, 1) == 0
+        words = S.twidCoefRModifier * n
+        tabs = []
+        for name in ("pTwiddleAReal", "pTwiddleBReal"):
+            t = np.ctypeslib.as_array(C.cast(getattr(S, name), ptr_t), (words,)).copy()
+            t[::7] = rng.integers(np.iinfo(dt).min, np.iinfo(dt).max, t[::7].size, dtype=dt)   # not the library's
+            tabs.append(t)
+            setattr(Sr, name, t.ctypes.data_as(ptr_t))
+        keep = [torch.from_numpy(t).cuda() for t in tabs] if where == "device" else tabs
+        for name, t in zip(("pTwiddleAReal", "pTwiddleBReal"), keep):
+            setattr(S, name, C.cast(C.c_void_p(t.data_ptr() if where == "device" else t.ctypes.data), ptr_t))
+        words_in = 2 * n if ifft else n
+        x = np.stack([refs.rand_input(kind, words_in, seed=3 * n + r + ifft, dist="uniform") for r in range(batch)])
+        want = []
+        for r in range(batch):
+            src = x[r].copy()
+            out = np.zeros(n if ifft else 2 * n, dtype=dt)
+            ref.fn(f"arm_rfft_{kind}")(C.byref(Sr), src.ctypes.data, out.ctypes.data)
+            want.append(out)
+        s = torch.from_numpy(x.copy()).cuda()
+        d = torch.zeros((batch, n if ifft else 2 * n), dtype=s.dtype, device="cuda")
+        dsp.rfft_fixed_batch(S, s, d)
+        torch.cuda.synchronize()
+        assert d.cpu().numpy().tobytes() == np.stack(want).tobytes(), (ifft, where)
