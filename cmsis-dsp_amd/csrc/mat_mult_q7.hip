@@ -32,6 +32,9 @@
 #ifndef MI355X_Q7_KT        // K bytes per LDS step: 64 or 128
 #define MI355X_Q7_KT 64
 #endif
+#ifndef MI355X_Q7_BN        // tile columns: 256 (8 waves, one workgroup per CU) or 128 (4 waves, two per CU)
+#define MI355X_Q7_BN 256
+#endif
 
 namespace mi355x {
 
@@ -40,13 +43,15 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef int v2i32 __attribute__((ext_vector_type(2)));
 
-constexpr int kQ7BM = 256, kQ7BN = 256, kQ7KT = MI355X_Q7_KT, kQ7NT = 512;
+constexpr int kQ7BM = 256, kQ7BN = MI355X_Q7_BN, kQ7KT = MI355X_Q7_KT, kQ7NT = 2 * kQ7BN;
+static_assert(kQ7BN == 256 || kQ7BN == 128, "tile columns 256 or 128");
 static_assert(kQ7KT == 64 || kQ7KT == 128, "K step of 64 or 128 bytes");
 constexpr int kQ7KC = kQ7KT / 16;                     // 16-B chunks per A row
 constexpr int kQ7KS = kQ7KT / 32;                     // MFMA k-steps per K step
 constexpr int kQ7NA = kQ7BM * kQ7KC / kQ7NT;          // A chunks staged per thread (2 | 4)
 constexpr int kQ7NB = kQ7KT * (kQ7BN / 16) / kQ7NT;   // B chunks staged per thread (2 | 4)
-constexpr int kQ7WM = 2, kQ7WN = 4;                   // wave grid
+constexpr int kQ7WM = 2, kQ7WN = kQ7BN / 64;         // wave grid (wave tiles of 128 x 64)
+constexpr int kQ7BTR = kQ7BN / 16;                    // staging threads per B row
 constexpr int kQ7WBM = kQ7BM / (32 * kQ7WM);          // 4 row blocks of 32 per wave
 constexpr int kQ7WBN = kQ7BN / (32 * kQ7WN);          // 2 column blocks of 32 per wave
 constexpr int kQ7BP = kQ7BN + 32;                     // B row pitch: 72 dwords = 8 x odd mod 64
@@ -116,7 +121,7 @@ __device__ __forceinline__ void q7_epilogue(const i32x16 (&acc)[kQ7WBM][kQ7WBN],
 }
 
 template <bool FULL>
-__global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __restrict__ A, const int8_t* __restrict__ B,
+__global__ __launch_bounds__(kQ7NT, kQ7BN == 128 ? 2 : 1) void mat_mult_q7_kernel(const int8_t* __restrict__ A, const int8_t* __restrict__ B,
                                                             int8_t* __restrict__ C, int M, int K, int N) {
   __shared__ __attribute__((aligned(16))) int8_t lds[2 * kQ7BUF];
 
@@ -134,9 +139,10 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __rest
   C += bz * (size_t)M * N;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 
-  // staging roles: A rows ar + (512 / KC) q, 16-B chunk ac; B k-rows bk + 32 q, 16 columns at bc
+  // staging roles: A rows ar + (NT / KC) q, 16-B chunk ac; B k-rows bk + 32 q, 16 columns at bc
   const int ar = tid / kQ7KC, ac = tid % kQ7KC;
-  const int bk = tid >> 4, bc = 16 * (tid & 15);
+  const int bk = tid / kQ7BTR, bc = 16 * (tid % kQ7BTR);
+  constexpr int kBRs = kQ7NT / kQ7BTR;                 // B k-rows per staging pass
   constexpr int kARs = kQ7NT / kQ7KC;                  // A rows per staging pass
   const bool vecA = FULL || ((K % 16) == 0 && (((uintptr_t)A) & 15) == 0);
   const bool vecB = FULL || ((N % 16) == 0 && (((uintptr_t)B) & 15) == 0);
@@ -158,7 +164,7 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __rest
     }
 #pragma unroll
     for (int q = 0; q < kQ7NB; ++q) {
-      const int kb = k0 + bk + 32 * q;
+      const int kb = k0 + bk + kBRs * q;
       rb[q] = load16(B, (size_t)kb * N, col0 + bc, N, kb < K, vecB);
     }
   };
@@ -171,7 +177,7 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __rest
       *reinterpret_cast<uint4*>(As + r * kQ7KT + 16 * q7_chunk(r, ac)) = ra[q];
     }
 #pragma unroll
-    for (int q = 0; q < kQ7NB; ++q) *reinterpret_cast<uint4*>(Bs + (bk + 32 * q) * kQ7BP + bc) = rb[q];
+    for (int q = 0; q < kQ7NB; ++q) *reinterpret_cast<uint4*>(Bs + (bk + kBRs * q) * kQ7BP + bc) = rb[q];
   };
 
   i32x16 acc[kQ7WBM][kQ7WBN];
@@ -227,15 +233,26 @@ __global__ __launch_bounds__(kQ7NT) void mat_mult_q7_kernel(const int8_t* __rest
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);        // one MFMA
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);        // one kk = 1 fragment read
     }
+    if constexpr (kQ7NA + kQ7NB == 4) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);        // one staging LDS write
-    }
+      for (int i = 0; i < 4; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);      // one staging LDS write
+      }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);        // one global load
+      for (int i = 0; i < 4; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);      // one global load
+      }
+    } else {                                                    // BN = 128: 6 writes, 6 loads
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (i < kQ7NA + kQ7NB) {
+          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+      }
     }
 #endif
   };
