@@ -19,6 +19,9 @@ SPECS = {
     "rfft_f32_pscratch": ("--workload rfft_f32_pscratch --steps 10 --warmup 3", "rfft1024_fwd", ""),
     "rfft_q31": ("--workload rfft_q31 --steps 10 --warmup 3", "fx4096", ""),
     "rfft_q15": ("--workload rfft_q15 --steps 10 --warmup 3", "q15_4096_pk", ""),
+    # fftLenReal 1024: the split fused into the radix-16 CFFT-512 (round 5)
+    "rfft_q31_1024": ("--workload rfft_q31 --fftlen 1024 --steps 10 --warmup 3", "cfft_fx_r16_kernel", ""),
+    "rfft_q15_1024": ("--workload rfft_q15 --fftlen 1024 --steps 10 --warmup 3", "cfft_fx_r16_kernel", ""),
     "fir_f32": ("--workload fir_f32 --steps 10 --warmup 3", "fir_f32_kernel", ""),
     "fir_f32_fma": ("--workload fir_f32_fma --steps 10 --warmup 3", "fir_f32_kernel", ""),
     "fir_q15": ("--workload fir_q15 --steps 10 --warmup 3", "fir_q15_kernel", ""),

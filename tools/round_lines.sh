@@ -7,7 +7,7 @@ set -e -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/lines_${1:-cur}; mkdir -p $O
 timeout -k 10 400 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err
-for wl in fir_f32 mat_mult_f32 fir_f32_fma fir_q15 mfcc_f32 mfcc_q31 mfcc_q15 rfft_f32 rfft_q31 rfft_q15 conv_f32 mat_mult_q15 mat_mult_q31; do
+for wl in fir_f32 mat_mult_f32 fir_f32_fma fir_q15 fir_q31 fir_fast_q15 fir_fast_q31 mfcc_f32 mfcc_q31 mfcc_q15 rfft_f32 rfft_f32_pscratch rfft_q31 rfft_q15 conv_f32 mat_mult_q7 mat_mult_q15 mat_mult_q31 mat_mult_fast_q31; do
   cb="--no-cpu-baseline"
   case $wl in fir_f32|mat_mult_f32) cb="";; esac
   timeout -k 10 300 python -u bench.py --workload $wl $cb > $O/$wl.json 2> $O/$wl.err
