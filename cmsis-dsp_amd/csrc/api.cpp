@@ -219,11 +219,13 @@ bool rfft_fixed_run(const RInst* S, T* d_src, T* d_dst, uint32_t batch, hipStrea
   const bool fuse = !inv && !pr.perm && (pr.flags & kBitrev) &&
                     (L == 4096 ? (kind == 1 ? MI355X_RFFT_Q31_FUSED : MI355X_RFFT_Q15_FUSED && MI355X_FX_Q15_PACKED)
                                : L >= 256 && L <= 2048 && MI355X_RFFT_FX_R16_FUSED);
-  // inverse, same conditions, L = 256 .. 2048: the merge runs in the CFFT's first pass
-  const bool ifuse = inv && !pr.perm && (pr.flags & kBitrev) && L >= 256 && L <= 2048 && MI355X_RFFT_FX_R16_INV_FUSED;
+  // inverse, same conditions, L = 256 .. 2048 (and q15 L = 4096): the merge runs in the CFFT's first pass
+  const bool ifuse = inv && !pr.perm && (pr.flags & kBitrev) &&
+                     (L == 4096 ? kind == 2 && MI355X_RFFT_Q15_INV_FUSED && MI355X_FX_Q15_PACKED
+                                : L >= 256 && L <= 2048 && MI355X_RFFT_FX_R16_INV_FUSED);
   // the split / merge pass reads realCoef[2*mod*k + 1] for k < L: mod * N words cover it
   const T *ta = nullptr, *tb = nullptr;
-  if ((!fuse && !ifuse) || L == 4096) {
+  if ((!fuse && !ifuse) || (fuse && L == 4096)) {
     const size_t words = std::max<size_t>(2, (size_t)S->twidCoefRModifier * n);
     ta = (const T*)device_table(S->pTwiddleAReal, sizeof(T) * words);
     tb = (const T*)device_table(S->pTwiddleBReal, sizeof(T) * words);
@@ -238,6 +240,11 @@ bool rfft_fixed_run(const RInst* S, T* d_src, T* d_dst, uint32_t batch, hipStrea
   if (ifuse) {
     const void* rec = device_split_records(S->pTwiddleAReal, S->pTwiddleBReal, S->twidCoefRModifier, L, (int)sizeof(T));
     if (!rec) return false;
+    if (L == 4096) {
+      MI_CHECK(rfft_q15_8192_inv_fused_launch((const int16_t*)d_src, (int16_t*)d_dst, batch, (const int16_t*)pr.tw, rec, st),
+               "rfft q15 inverse fused");
+      return true;
+    }
     const bool done = kind == 1
         ? rfft_q31_r16_inv_fused_launch((int)L, (const int32_t*)d_src, (int32_t*)d_dst, batch, (const int32_t*)pr.tw, rec, st)
         : rfft_q15_r16_inv_fused_launch((int)L, (const int16_t*)d_src, (int16_t*)d_dst, batch, (const int16_t*)pr.tw, rec, st);

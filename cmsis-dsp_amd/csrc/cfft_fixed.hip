@@ -320,11 +320,16 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
 // LDS tables (1.5 KiB + 384 B) instead of 30 VGPRs; MI355X_FXQ15_WAVES = the minimum waves per
 // SIMD the register allocation must allow.
 // RSPLIT: the forward arm_rfft_q15 of N = 8192 fused as in cfft_fx4096_kernel.
-template <bool INV, bool BREV, bool SAT, bool RSPLIT = false>
-__global__ __launch_bounds__(256, MI355X_FXQ15_WAVES) void cfft_q15_4096_pk_kernel(short2* __restrict__ data, uint32_t batch,
+// RMERGE: the inverse arm_rfft_q15 of N = 8192 in one launch (as cfft_fx_r16_kernel's RMERGE): the
+// prefetch reads spectrum bins X[e] and X[4096 - e] of the input row (rs.spec), pass 1 forms the
+// merge from them and the bin's record (32 KiB of short4 records in LDS, staged once), and the
+// inverse CFFT's saturating <<1 store writes the output row to `data`.
+template <bool INV, bool BREV, bool SAT, bool RSPLIT = false, bool RMERGE = false>
+__global__ __launch_bounds__(256, RMERGE ? 3 : MI355X_FXQ15_WAVES) void cfft_q15_4096_pk_kernel(short2* __restrict__ data, uint32_t batch,
                                                                     const short2* __restrict__ tw,
                                                                     RfSplitArgs<int16_t> rs) {
   static_assert(!RSPLIT || (!INV && BREV && !SAT), "the fused split follows the forward, bit-reversed CFFT");
+  static_assert(!RMERGE || (!RSPLIT && INV && BREV && SAT), "the fused merge precedes the inverse CFFT");
   __shared__ __attribute__((aligned(16))) uint32_t lds[MI355X_FXQ15_SLOTS];
   const int t = threadIdx.x;
   const int q2 = t >> 4, j2 = t & 15;
@@ -332,59 +337,93 @@ __global__ __launch_bounds__(256, MI355X_FXQ15_WAVES) void cfft_q15_4096_pk_kern
   const FxWalk wk = fx_walk<MI355X_FXQ15_T>(batch);
   const uint32_t tr0 = wk.begin, tend = wk.end, step = wk.step;
   TwP tw1[4][3], tw2[3], tw5[4][3];
-#if MI355X_FXQ15_TW34_LDS
-  __shared__ TwP tw3l[64 * 3], tw4l[16 * 3];
-  if (t < 192) tw3l[t] = twp<INV>(tw[(t % 3 + 1) * (t / 3) * 16]);    // visible after the loop's barriers
-  else if (t < 240) tw4l[t - 192] = twp<INV>(tw[((t - 192) % 3 + 1) * 64 * ((t - 192) / 3)]);
-#define TW3Q(a, k) tw3l[(j2 + 16 * (a)) * 3 + (k)]
-#define TW4Q(k) tw4l[j2 * 3 + (k)]
-#else
+  // RMERGE keeps the stage-3/4 twiddles in LDS too: its X[4096 - e] prefetch words need the 30
+  // VGPRs to stay at three waves per SIMD (172 -> 142)
+  constexpr bool kTwL = MI355X_FXQ15_TW34_LDS || RMERGE;
+  __shared__ TwP tw3l[kTwL ? 64 * 3 : 1], tw4l[kTwL ? 16 * 3 : 1];
   TwP tw3[4][3], tw4[3];
-#define TW3Q(a, k) tw3[a][k]
-#define TW4Q(k) tw4[k]
-#endif
+  if constexpr (kTwL) {
+    if (t < 192) tw3l[t] = twp<INV>(tw[(t % 3 + 1) * (t / 3) * 16]);    // visible after the loop's barriers
+    else if (t < 240) tw4l[t - 192] = twp<INV>(tw[((t - 192) % 3 + 1) * 64 * ((t - 192) / 3)]);
+  }
+  auto TW3Q = [&](int a, int k) -> TwP {
+    if constexpr (kTwL) return tw3l[(j2 + 16 * a) * 3 + k];
+    else return tw3[a][k];
+  };
+  auto TW4Q = [&](int k) -> TwP {
+    if constexpr (kTwL) return tw4l[j2 * 3 + k];
+    else return tw4[k];
+  };
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       tw1[a][k] = twp<INV>(tw[(k + 1) * (t + 256 * a)]);
-#if !MI355X_FXQ15_TW34_LDS
-      tw3[a][k] = twp<INV>(tw[(k + 1) * (j2 + 16 * a) * 16]);
-#endif
+      if constexpr (!kTwL) tw3[a][k] = twp<INV>(tw[(k + 1) * (j2 + 16 * a) * 16]);
       tw5[a][k] = twp<INV>(tw[(k + 1) * a * 256]);
     }
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     tw2[k] = twp<INV>(tw[(k + 1) * 4 * t]);
-#if !MI355X_FXQ15_TW34_LDS
-    tw4[k] = twp<INV>(tw[(k + 1) * 64 * j2]);
-#endif
+    if constexpr (!kTwL) tw4[k] = twp<INV>(tw[(k + 1) * 64 * j2]);
   }
   const TwP z{};
+  __shared__ short4 recl[RMERGE ? 4096 : 1];               // RMERGE: the merge records of bins 0 .. 4095
+  if constexpr (RMERGE) {
+    for (int i = t; i < 4096; i += 256) recl[i] = rs.rec[i];
+    __syncthreads();
+  }
 
   s16x2 v[16];
   const int vin = t * 4;                                   // byte offset of element t
-  auto fetch = [&](uint32_t (&dst)[16], uint32_t tr) {
-    const __amdgpu_buffer_rsrc_t r = fx_rsrc(data + (size_t)tr * 4096, 4096 * 4);
+  auto fetch = [&](uint32_t (&dst)[16], uint32_t (&dst2)[16], uint32_t tr) {
+    if constexpr (RMERGE) {
+      // spectrum row tr: 8192 complex words; X[e] at e = t + 256 a + 1024 b, X[4096 - e] at
+      // (256 - t) + 256 (3 - a) + 1024 (3 - b): non-negative immediates
+      const __amdgpu_buffer_rsrc_t r = fx_rsrc(rs.spec + (size_t)tr * 16384, 8192 * 4);
+      const int vneg = (256 - t) * 4;
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b)
-        dst[4 * a + b] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, vin, (256 * a + 1024 * b) * 4, MI355X_FX_NT);
+        for (int b = 0; b < 4; ++b) {
+          dst[4 * a + b] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, vin, (256 * a + 1024 * b) * 4, MI355X_FX_NT);
+          dst2[4 * a + b] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, vneg, (256 * (3 - a) + 1024 * (3 - b)) * 4,
+                                                                           MI355X_FX_NT);
+        }
+    } else {
+      const __amdgpu_buffer_rsrc_t r = fx_rsrc(data + (size_t)tr * 4096, 4096 * 4);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          dst[4 * a + b] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, vin, (256 * a + 1024 * b) * 4, MI355X_FX_NT);
+    }
   };
   // Register prefetch MI355X_FX_Q15_PFD transforms deep: nq[d] holds transform tr + (d+1)*step.
   // q15 moves 4 B per load, so at the workgroups a CU holds one transform of look-ahead
   // (16 KiB per workgroup) does not cover the HBM latency; two measured +8.5 %.
   constexpr int PFD = MI355X_FX_Q15_PFD;
-  uint32_t nq[PFD][16];
+  uint32_t nq[PFD][16], nq2[PFD][16];                     // nq2: RMERGE's X[4096 - e] words
 #pragma unroll
   for (int d = 0; d < PFD; ++d)
-    if (tr0 + d * step < tend) fetch(nq[d], tr0 + d * step);
+    if (tr0 + d * step < tend) fetch(nq[d], nq2[d], tr0 + d * step);
   // Loop entered after pass 1, as in cfft_fx4096_kernel: the wait for the prefetched words
   // then covers only the older loads (vmcnt = the younger stores + deeper prefetches).
-  auto pass1 = [&](uint32_t (&buf)[16], uint32_t tr) {
+  auto pass1 = [&](uint32_t (&buf)[16], uint32_t (&buf2)[16], uint32_t tr) {
 #pragma unroll
     for (int u = 0; u < 16; ++u) v[u] = pk(buf[u]);
+    if constexpr (RMERGE) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int u = 4 * a + b;
+          const short4 rc = recl[t + 256 * a + 1024 * b];
+          const s16x2 y = pk(buf2[u]);
+          const int2 m = rfft_merge_bin<int16_t>(make_int2(v[u].x, v[u].y), make_int2(y.x, y.y), rc.x, rc.y, rc.z, rc.w);
+          v[u] = s16x2{(short)m.x, (short)m.y};
+        }
+    }
 #pragma unroll
     for (int a = 0; a < 4; ++a)
       bfly_pk<INV, 0>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], tw1[a][0], tw1[a][1], tw1[a][2]);
@@ -395,11 +434,11 @@ __global__ __launch_bounds__(256, MI355X_FXQ15_WAVES) void cfft_q15_4096_pk_kern
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) lds[s4096(t + 256 * a + 1024 * b)] = upk(v[4 * a + b]);
-    if (tr + PFD * step < tend) fetch(buf, tr + PFD * step);
+    if (tr + PFD * step < tend) fetch(buf, buf2, tr + PFD * step);
     __syncthreads();
   };
   if (tr0 >= tend) return;
-  pass1(nq[0], tr0);
+  pass1(nq[0], nq2[0], tr0);
   uint32_t tr = tr0;
   auto pass23 = [&]() {
     const __amdgpu_buffer_rsrc_t rx = fx_rsrc(data + (size_t)tr * 4096, 4096 * 4);
@@ -462,13 +501,11 @@ __global__ __launch_bounds__(256, MI355X_FXQ15_WAVES) void cfft_q15_4096_pk_kern
       pass23();
       tr += step;
       if (tr >= tend) return;
-      pass1(nq[(d + 1) % PFD], tr);
+      pass1(nq[(d + 1) % PFD], nq2[(d + 1) % PFD], tr);
     }
   }
 }
 
-#undef TW3Q
-#undef TW4Q
 
 // ============================================================================================
 // A one-wave-per-transform q31 N = 4096 kernel (the one-wave f32 pattern; lane l holds x[l + 64m],
@@ -497,6 +534,20 @@ hipError_t rfft_q15_8192_fused_launch(int16_t* src, int16_t* dst, uint32_t batch
   RfSplitArgs<int16_t> rs;
   rs.dst = dst; rs.ta = ta; rs.tb = tb; rs.mod = mod;
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (short2*)src, batch, (const short2*)tw, rs);
+  return hipGetLastError();
+}
+
+// The inverse arm_rfft_q15 of N = 8192 in one launch: spec [batch][16384] spectrum rows (bins
+// 0..4096 read), dst [batch][8192]; rec = device_split_records(A, B, mod, 4096, 2).
+hipError_t rfft_q15_8192_inv_fused_launch(const int16_t* spec, int16_t* dst, uint32_t batch, const int16_t* tw,
+                                          const void* rec, hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  auto k = cfft_q15_4096_pk_kernel<true, true, true, false, true>;
+  const int grid = fx_grid<MI355X_FXQ15_T>((const void*)k, batch);
+  RfSplitArgs<int16_t> rs;
+  rs.spec = spec;
+  rs.rec = (const short4*)rec;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (short2*)dst, batch, (const short2*)tw, rs);
   return hipGetLastError();
 }
 
