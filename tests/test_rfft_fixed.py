@@ -186,3 +186,30 @@ def test_rfft_fixed_user_tables(dsp, torch_gpu, ref, kind, n, where):
         dsp.rfft_fixed_batch(S, s, d)
         torch.cuda.synchronize()
         assert d.cpu().numpy().tobytes() == np.stack(want).tobytes(), (ifft, where)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["q31", "q15"])
+@pytest.mark.parametrize("n", [512, 2048, 8192])
+def test_rfft_fixed_fused_ragged_batches(dsp, torch_gpu, ref, kind, n):
+    """The fused forward split / inverse merge at batch sizes around the radix-16 kernel's group of
+    256 / (N/32) transforms and the specialist's walk (1, 2, 3, 17, 257 signals): rows past the
+    batch are out of the buffer ranges (zero loads, dropped stores), every row bit-exact."""
+    torch = torch_gpu
+    for batch in (1, 2, 3, 17, 257):
+        for ifft in (0, 1):
+            words = 2 * n if ifft else n
+            x = np.stack([refs.rand_input(kind, words, seed=7 * batch + r + 100 * ifft, dist="extreme" if r % 3 == 0 else "uniform")
+                          for r in range(batch)])
+            S = _instance(dsp, kind, n, ifft, 1)
+            src = torch.from_numpy(x.copy()).cuda()
+            dst = torch.zeros((batch, n if ifft else 2 * n), dtype=src.dtype, device="cuda")
+            dsp.rfft_fixed_batch(S, src, dst)
+            torch.cuda.synchronize()
+            got = dst.cpu().numpy()
+            rows = range(batch) if batch <= 17 else [0, 1, 127, 128, batch - 2, batch - 1]
+            for r in rows:
+                want, wsrc = ref.rfft_fixed(kind, n, x[r], ifft, 1)
+                assert got[r].tobytes() == want.tobytes(), (batch, ifft, r)
+                if not ifft:
+                    assert src[r].cpu().numpy().tobytes() == wsrc.tobytes(), (batch, r)
