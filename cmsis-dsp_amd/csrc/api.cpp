@@ -219,10 +219,19 @@ bool rfft_fixed_run(const RInst* S, T* d_src, T* d_dst, uint32_t batch, hipStrea
   const bool fuse = !inv && !pr.perm && (pr.flags & kBitrev) &&
                     (L == 4096 ? (kind == 1 ? MI355X_RFFT_Q31_FUSED : MI355X_RFFT_Q15_FUSED && MI355X_FX_Q15_PACKED)
                                : L >= 256 && L <= 2048 && MI355X_RFFT_FX_R16_FUSED);
-  // inverse, same conditions, L = 256 .. 2048 (and q15 L = 4096): the merge runs in the CFFT's first pass
-  const bool ifuse = inv && !pr.perm && (pr.flags & kBitrev) &&
-                     (L == 4096 ? kind == 2 && MI355X_RFFT_Q15_INV_FUSED && MI355X_FX_Q15_PACKED
-                                : L >= 256 && L <= 2048 && MI355X_RFFT_FX_R16_INV_FUSED);
+  // inverse, same conditions: the merge runs in the CFFT's first pass (cfft_fixed_r16.hip L = 256 ..
+  // 2048, cfft_fixed.hip L = 4096 -- q31 there stages half the records, so only for tables whose
+  // records are symmetric, as the reference's realCoefAQ31 / BQ31 are)
+  bool ifuse = inv && !pr.perm && (pr.flags & kBitrev) &&
+               (L == 4096 ? (kind == 1 ? MI355X_RFFT_Q31_INV_FUSED : MI355X_RFFT_Q15_INV_FUSED && MI355X_FX_Q15_PACKED)
+                          : L >= 256 && L <= 2048 && MI355X_RFFT_FX_R16_INV_FUSED);
+  const void* irec = nullptr;
+  if (ifuse) {
+    bool sym = false;
+    irec = device_split_records(S->pTwiddleAReal, S->pTwiddleBReal, S->twidCoefRModifier, L, (int)sizeof(T), &sym);
+    if (!irec) return false;
+    if (kind == 1 && L == 4096 && !sym) ifuse = false;
+  }
   // the split / merge pass reads realCoef[2*mod*k + 1] for k < L: mod * N words cover it
   const T *ta = nullptr, *tb = nullptr;
   if ((!fuse && !ifuse) || (fuse && L == 4096)) {
@@ -238,16 +247,15 @@ bool rfft_fixed_run(const RInst* S, T* d_src, T* d_dst, uint32_t batch, hipStrea
       return rfft_q15_pass_launch(inv, (int)n, a, b, batch, ta, tb, S->twidCoefRModifier, st);
   };
   if (ifuse) {
-    const void* rec = device_split_records(S->pTwiddleAReal, S->pTwiddleBReal, S->twidCoefRModifier, L, (int)sizeof(T));
-    if (!rec) return false;
     if (L == 4096) {
-      MI_CHECK(rfft_q15_8192_inv_fused_launch((const int16_t*)d_src, (int16_t*)d_dst, batch, (const int16_t*)pr.tw, rec, st),
-               "rfft q15 inverse fused");
+      MI_CHECK(kind == 1 ? rfft_q31_8192_inv_fused_launch((const int32_t*)d_src, (int32_t*)d_dst, batch, (const int32_t*)pr.tw, irec, st)
+                         : rfft_q15_8192_inv_fused_launch((const int16_t*)d_src, (int16_t*)d_dst, batch, (const int16_t*)pr.tw, irec, st),
+               "rfft inverse fused 8192");
       return true;
     }
     const bool done = kind == 1
-        ? rfft_q31_r16_inv_fused_launch((int)L, (const int32_t*)d_src, (int32_t*)d_dst, batch, (const int32_t*)pr.tw, rec, st)
-        : rfft_q15_r16_inv_fused_launch((int)L, (const int16_t*)d_src, (int16_t*)d_dst, batch, (const int16_t*)pr.tw, rec, st);
+        ? rfft_q31_r16_inv_fused_launch((int)L, (const int32_t*)d_src, (int32_t*)d_dst, batch, (const int32_t*)pr.tw, irec, st)
+        : rfft_q15_r16_inv_fused_launch((int)L, (const int16_t*)d_src, (int16_t*)d_dst, batch, (const int16_t*)pr.tw, irec, st);
     if (!done) { set_error(hipErrorInvalidValue, "rfft inverse fused length"); return false; }
     MI_CHECK(hipGetLastError(), "rfft inverse fused");
   } else if (inv) {

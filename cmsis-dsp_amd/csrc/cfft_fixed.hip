@@ -134,16 +134,20 @@ template <typename C> constexpr int kFxSlots = sizeof(C) == 8 ? MI355X_FX_Q31_SL
 // transform's bins also go to LDS in natural order, and the workgroup runs the RFFT's split on
 // them (rfft_fixed_split.hpp, arm_rfft_q31.c:256-341) straight into the 2N-word spectrum row --
 // the CFFT output is still stored to `data`, as the reference leaves pSrc, but never read back.
-template <typename T, bool INV, bool BREV, bool SAT, bool RSPLIT = false>
-__global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typename Fx<T>::C* __restrict__ data, uint32_t batch,
+// RMERGE (q31): the inverse arm_rfft_q31 of N = 8192 in one launch, as cfft_q15_4096_pk_kernel's
+// RMERGE, from half the records (the tables' symmetry) and the minimal image: two workgroups per CU.
+template <typename T, bool INV, bool BREV, bool SAT, bool RSPLIT = false, bool RMERGE = false>
+__global__ __launch_bounds__(256, RMERGE ? 2 : MI355X_FX_WAVES) void cfft_fx4096_kernel(typename Fx<T>::C* __restrict__ data, uint32_t batch,
                                                           const typename Fx<T>::C* __restrict__ tw,
                                                           RfSplitArgs<T> rs = {}) {
   static_assert(!RSPLIT || (!INV && BREV && !SAT), "the fused split follows the forward, bit-reversed CFFT");
+  static_assert(!RMERGE || (sizeof(T) == 4 && !RSPLIT && INV && BREV && SAT), "the fused merge precedes the inverse CFFT");
   using F = Fx<T>;
   using C = typename F::C;
   using IO = FxIO<C>;
   constexpr int kC = (int)sizeof(C);
-  __shared__ __attribute__((aligned(16))) C lds[kFxSlots<C>];
+  // RMERGE: the minimal image (4112 slots) beside 32 KiB of records, so two workgroups share a CU
+  __shared__ __attribute__((aligned(16))) C lds[RMERGE ? 4112 : kFxSlots<C>];
   const int t = threadIdx.x;
   const int q2 = t >> 4, j2 = t & 15;
   const int q3 = (int)(__brev((uint32_t)t) >> 24);        // rev8(t)
@@ -153,58 +157,92 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
   // Lane-constant twiddles (stored in the table's word type).  (w1, w2, w3) = table[ia],
   // table[2ia], table[3ia] of the butterfly's index ia.
   C tw1[4][3], tw2[3], tw5[4][3];
-#if MI355X_FX_TW3_LDS
-  __shared__ __attribute__((aligned(16))) C tw3l[64 * 3];
-  if (t < 192) tw3l[t] = tw[(t % 3 + 1) * (t / 3) * 16];        // visible after the loop's barriers
-#define TW3(a, k) tw3l[(j2 + 16 * (a)) * 3 + (k)]
-#else
-  C tw3[4][3];
-#define TW3(a, k) tw3[a][k]
-#endif
-#if MI355X_FX_TW4_LDS
-  __shared__ __attribute__((aligned(16))) C tw4l[16 * 3];
-  if (t < 48) tw4l[t] = tw[(t % 3 + 1) * 64 * (t / 3)];
-#define TW4(k) tw4l[j2 * 3 + (k)]
-#else
-  C tw4[3];
-#define TW4(k) tw4[k]
-#endif
+  // RMERGE keeps the stage-3/4 twiddles in LDS tables (30 VGPRs) to stay at two waves per SIMD
+  constexpr bool kTw3L = MI355X_FX_TW3_LDS || RMERGE, kTw4L = MI355X_FX_TW4_LDS || RMERGE;
+  __shared__ __attribute__((aligned(16))) C tw3l[kTw3L ? 64 * 3 : 1];
+  __shared__ __attribute__((aligned(16))) C tw4l[kTw4L ? 16 * 3 : 1];
+  C tw3[4][3], tw4[3];
+  if constexpr (kTw3L)
+    if (t < 192) tw3l[t] = tw[(t % 3 + 1) * (t / 3) * 16];        // visible after the loop's barriers
+  if constexpr (kTw4L)
+    if (t < 48) tw4l[t] = tw[(t % 3 + 1) * 64 * (t / 3)];
+  auto TW3 = [&](int a, int k) -> C {
+    if constexpr (kTw3L) return tw3l[(j2 + 16 * a) * 3 + k];
+    else return tw3[a][k];
+  };
+  auto TW4 = [&](int k) -> C {
+    if constexpr (kTw4L) return tw4l[j2 * 3 + k];
+    else return tw4[k];
+  };
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       tw1[a][k] = tw[(k + 1) * (t + 256 * a)];
-#if !MI355X_FX_TW3_LDS
-      tw3[a][k] = tw[(k + 1) * (j2 + 16 * a) * 16];
-#endif
+      if constexpr (!kTw3L) tw3[a][k] = tw[(k + 1) * (j2 + 16 * a) * 16];
       tw5[a][k] = tw[(k + 1) * a * 256];
     }
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     tw2[k] = tw[(k + 1) * 4 * t];
-#if !MI355X_FX_TW4_LDS
-    tw4[k] = tw[(k + 1) * 64 * j2];
-#endif
+    if constexpr (!kTw4L) tw4[k] = tw[(k + 1) * 64 * j2];
   }
   auto W = [](C c) { return make_int2(c.x, c.y); };
+  // RMERGE: the records of bins 0 .. 2048 only -- the caller checked that its tables are symmetric
+  // (record 4096 - e = record e with A1, B1 negated, true of the reference's realCoefAQ31 / BQ31)
+  __shared__ int4 recl[RMERGE ? 2049 : 1];
+  if constexpr (RMERGE) {
+    for (int i = t; i <= 2048; i += 256) recl[i] = reinterpret_cast<const int4*>(rs.rec)[i];
+    __syncthreads();
+  }
 
   // walk: nq[d] holds transform tr + (d + 1) * step (FxWalk)
   constexpr int PFD = MI355X_FX_PF > 0 ? MI355X_FX_PF : 1;
   const int vin = t * kC;                                    // byte offset of element t
-  auto fetch = [&](C (&dst)[16], uint32_t tr) {
-    const __amdgpu_buffer_rsrc_t r = fx_rsrc(data + (size_t)tr * 4096, 4096 * kC);
+  auto fetch = [&](C (&dst)[16], C (&dst2)[16], uint32_t tr) {
+    if constexpr (RMERGE) {
+      // spectrum row tr: 8192 complex words; X[e] at e = t + 256 a + 1024 b, X[4096 - e] at
+      // (256 - t) + 256 (3 - a) + 1024 (3 - b)
+      const __amdgpu_buffer_rsrc_t r = fx_rsrc(rs.spec + (size_t)tr * 16384, 8192 * kC);
+      const int vneg = (256 - t) * kC;
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) dst[4 * a + b] = IO::ld(r, vin, (256 * a + 1024 * b) * kC);
+        for (int b = 0; b < 4; ++b) {
+          dst[4 * a + b] = IO::ld(r, vin, (256 * a + 1024 * b) * kC);
+          dst2[4 * a + b] = IO::ld(r, vneg, (256 * (3 - a) + 1024 * (3 - b)) * kC);
+        }
+    } else {
+      const __amdgpu_buffer_rsrc_t r = fx_rsrc(data + (size_t)tr * 4096, 4096 * kC);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) dst[4 * a + b] = IO::ld(r, vin, (256 * a + 1024 * b) * kC);
+    }
   };
   int2 v[16];
-  C nq[PFD][16];
+  C nq[PFD][16], nq2[PFD][16];                              // nq2: RMERGE's X[4096 - e] words
   // Pass 1 of transform tr from nq[0]; then the prefetch of transform tr + PFD * step.
-  auto pass1 = [&](C (&buf)[16], uint32_t tr) {
+  auto pass1 = [&](C (&buf)[16], C (&buf2)[16], uint32_t tr) {
 #pragma unroll
     for (int u = 0; u < 16; ++u) v[u] = W(buf[u]);
+    if constexpr (RMERGE) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int u = 4 * a + b;
+          int4 rc;
+          if (b < 2) {
+            rc = recl[t + 256 * a + 1024 * b];
+          } else {                                           // e >= 2048: mirrored record
+            const int4 r = recl[4096 - (t + 256 * a + 1024 * b)];
+            rc = make_int4(r.x, wneg(r.y), r.z, wneg(r.w));
+          }
+          v[u] = rfft_merge_bin<T>(v[u], W(buf2[u]), rc.x, rc.y, rc.z, rc.w);
+        }
+    }
 #pragma unroll
     for (int a = 0; a < 4; ++a)
       bfly<T, INV, 0>(v[4 * a], v[4 * a + 1], v[4 * a + 2], v[4 * a + 3], W(tw1[a][0]), W(tw1[a][1]), W(tw1[a][2]));
@@ -215,7 +253,7 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) F::st(lds + sfx<C>(t + 256 * a + 1024 * b), v[4 * a + b]);
-    if (tr + PFD * step < tend) fetch(buf, tr + PFD * step);   // flies under passes 2-3
+    if (tr + PFD * step < tend) fetch(buf, buf2, tr + PFD * step);   // flies under passes 2-3
     __syncthreads();
   };
   // The loop is entered after pass 1, so that at the point where pass 1 of the next
@@ -229,8 +267,8 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
   if (tr0 >= tend) return;
 #pragma unroll
   for (int d = 0; d < PFD; ++d)
-    if (tr0 + d * step < tend) fetch(nq[d], tr0 + d * step);
-  pass1(nq[0], tr0);
+    if (tr0 + d * step < tend) fetch(nq[d], nq2[d], tr0 + d * step);
+  pass1(nq[0], nq2[0], tr0);
   uint32_t tr = tr0;
   auto pass23 = [&]() {
     const __amdgpu_buffer_rsrc_t rx = fx_rsrc(data + (size_t)tr * 4096, 4096 * kC);
@@ -297,13 +335,11 @@ __global__ __launch_bounds__(256, MI355X_FX_WAVES) void cfft_fx4096_kernel(typen
       pass23();
       tr += step;
       if (tr >= tend) return;
-      pass1(nq[(d + 1) % PFD], tr);
+      pass1(nq[(d + 1) % PFD], nq2[(d + 1) % PFD], tr);
     }
   }
 }
 
-#undef TW3
-#undef TW4
 
 // ============================================================================================
 // q15 N = 4096 on packed 16-bit math: one VGPR holds a complex sample {re, im} and every
@@ -534,6 +570,20 @@ hipError_t rfft_q15_8192_fused_launch(int16_t* src, int16_t* dst, uint32_t batch
   RfSplitArgs<int16_t> rs;
   rs.dst = dst; rs.ta = ta; rs.tb = tb; rs.mod = mod;
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (short2*)src, batch, (const short2*)tw, rs);
+  return hipGetLastError();
+}
+
+// The inverse arm_rfft_q31 of N = 8192 in one launch: spec [batch][16384] spectrum rows (bins
+// 0..4096 read), dst [batch][8192]; rec = device_split_records(A, B, mod, 4096, 4).
+hipError_t rfft_q31_8192_inv_fused_launch(const int32_t* spec, int32_t* dst, uint32_t batch, const int32_t* tw,
+                                          const void* rec, hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  auto k = cfft_fx4096_kernel<int32_t, true, true, true, false, true>;
+  const int grid = fx_grid<MI355X_FX_T>((const void*)k, batch);
+  RfSplitArgs<int32_t> rs;
+  rs.spec = spec;
+  rs.rec = (const int4*)rec;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, (int2*)dst, batch, (const int2*)tw, rs);
   return hipGetLastError();
 }
 

@@ -95,6 +95,8 @@ bool rfft_q15_r16_inv_fused_launch(int n, const int16_t* spec, int16_t* dst, uin
 // ... and fftLenReal = 8192 (the CFFT-4096 specialists), from the instance's realCoefA / B
 hipError_t rfft_q31_8192_fused_launch(int32_t* src, int32_t* dst, uint32_t batch, const int32_t* tw, const int32_t* ta,
                                       const int32_t* tb, uint32_t mod, hipStream_t st);
+hipError_t rfft_q31_8192_inv_fused_launch(const int32_t* spec, int32_t* dst, uint32_t batch, const int32_t* tw,
+                                          const void* rec, hipStream_t st);
 hipError_t rfft_q15_8192_inv_fused_launch(const int16_t* spec, int16_t* dst, uint32_t batch, const int16_t* tw,
                                           const void* rec, hipStream_t st);
 hipError_t rfft_q15_8192_fused_launch(int16_t* src, int16_t* dst, uint32_t batch, const int16_t* tw, const int16_t* ta,

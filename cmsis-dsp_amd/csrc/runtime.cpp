@@ -374,7 +374,8 @@ const void* device_blob(const void* host, size_t bytes) {
   return hand_out(b);
 }
 
-const void* device_split_records(const void* A, const void* B, uint32_t mod, uint32_t L, int elem) {
+const void* device_split_records(const void* A, const void* B, uint32_t mod, uint32_t L, int elem, bool* symmetric) {
+  if (symmetric) *symmetric = false;
   if (!A || !B || !mod || !L || (elem != 2 && elem != 4)) {
     set_error(hipErrorInvalidValue, "split records");
     return nullptr;
@@ -382,12 +383,16 @@ const void* device_split_records(const void* A, const void* B, uint32_t mod, uin
   const int dev = cur_dev();
   const bool lib = is_library_addr(A) && is_library_addr(B);
   using Key = std::tuple<int, const void*, const void*, uint32_t, uint32_t, int>;
-  static std::map<Key, void*>* built = new std::map<Key, void*>;   // library tables: never freed
+  struct Built { void* d; bool sym; };
+  static std::map<Key, Built>* built = new std::map<Key, Built>;   // library tables: never freed
   const Key key{dev, A, B, mod, L, elem};
   if (lib) {
     std::lock_guard<std::mutex> lk(g_table_mu);
     auto it = built->find(key);
-    if (it != built->end()) return it->second;
+    if (it != built->end()) {
+      if (symmetric) *symmetric = it->second.sym;
+      return it->second.d;
+    }
   }
   // the words read: A/B[2 mod k + {0, 1}] for k < L
   const size_t words = 2 * (size_t)mod * (L - 1) + 2, wb = words * (size_t)elem;
@@ -412,6 +417,22 @@ const void* device_split_records(const void* A, const void* B, uint32_t mod, uin
     memcpy(r + 2 * elem, hb.data() + c, 2 * (size_t)elem);
   }
   const size_t rb = rec.size();
+  // record L - k = record k with A1, B1 negated (mod 2^32 / 2^16), for every k in 1 .. L - 1: the
+  // fused N = 8192 q31 inverse then stages records 0 .. L/2 only
+  bool sym = true;
+  for (uint32_t k = 1; k < L && sym; ++k) {
+    const uint8_t* r1 = rec.data() + (size_t)k * 4 * elem;
+    const uint8_t* r2 = rec.data() + (size_t)(L - k) * 4 * elem;
+    for (int w = 0; w < 4 && sym; ++w) {
+      int64_t x = 0, y = 0;
+      if (elem == 4) { int32_t a, b; memcpy(&a, r1 + 4 * w, 4); memcpy(&b, r2 + 4 * w, 4); x = a; y = b; }
+      else { int16_t a, b; memcpy(&a, r1 + 2 * w, 2); memcpy(&b, r2 + 2 * w, 2); x = a; y = b; }
+      const int64_t m = elem == 4 ? (int64_t(1) << 32) : (int64_t(1) << 16);
+      const int64_t want = (w & 1) ? ((-x) % m + m) % m : (x % m + m) % m;
+      sym = ((y % m + m) % m) == want;
+    }
+  }
+  if (symmetric) *symmetric = sym;
   if (!lib) return device_blob(rec.data(), rb);
   void* d = nullptr;
   hipError_t e = hipMalloc(&d, rb);
@@ -422,8 +443,8 @@ const void* device_split_records(const void* A, const void* B, uint32_t mod, uin
     return nullptr;
   }
   std::lock_guard<std::mutex> lk(g_table_mu);
-  auto ins = built->emplace(key, d);
-  if (!ins.second) { (void)hipFree(d); return ins.first->second; }   // another thread built it first
+  auto ins = built->emplace(key, Built{d, sym});
+  if (!ins.second) { (void)hipFree(d); return ins.first->second.d; }   // another thread built it first
   return d;
 }
 

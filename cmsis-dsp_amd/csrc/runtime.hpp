@@ -43,7 +43,10 @@ size_t blob_cache_bytes();
 // bytes per word (4: int4 records, 2: 8-B records), so that a split reads one record per bin
 // instead of four words at a stride of 2 mod (rfft_fixed_split.hpp SplitRecTab).  The library's own tables: built once per (device,
 // A, B, mod, L); any other (host or device) table: rebuilt per call and cached by content.
-const void* device_split_records(const void* A, const void* B, uint32_t mod, uint32_t L, int elem);
+// *symmetric (optional): record L - k equals record k with A1 and B1 negated for every k (true of the
+// reference's realCoefA/B tables), which the fused N = 8192 q31 inverse relies on.
+const void* device_split_records(const void* A, const void* B, uint32_t mod, uint32_t L, int elem,
+                                 bool* symmetric = nullptr);
 void set_blob_cache_limit(size_t bytes);   // per device
 
 // Pins every blob device_blob / device_table / device_perm hand out on this thread while the

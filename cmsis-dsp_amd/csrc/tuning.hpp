@@ -184,6 +184,9 @@
 #ifndef MI355X_RFFT_FX_R16_INV_FUSED   // inverse arm_rfft_q31 / _q15 N = 512 .. 4096: merge fused into the radix-16 CFFT
 #define MI355X_RFFT_FX_R16_INV_FUSED 1
 #endif
+#ifndef MI355X_RFFT_Q31_INV_FUSED   // inverse arm_rfft_q31 N = 8192: merge fused into the CFFT-4096 (one workgroup per CU)
+#define MI355X_RFFT_Q31_INV_FUSED 1
+#endif
 #ifndef MI355X_RFFT_Q15_INV_FUSED   // inverse arm_rfft_q15 N = 8192: merge fused into the packed CFFT-4096
 #define MI355X_RFFT_Q15_INV_FUSED 1
 #endif

@@ -149,10 +149,13 @@ def test_rfft_fixed_dropin(dsp, torch_gpu, ref, kind, n):
 @pytest.mark.parametrize("kind", ["q31", "q15"])
 @pytest.mark.parametrize("n", [1024, 4096, 8192])
 @pytest.mark.parametrize("where", ["host", "device"])
-def test_rfft_fixed_user_tables(dsp, torch_gpu, ref, kind, n, where):
-    """realCoefA / B that are not the library's own (host or device buffers, contents changed):
-    the fused kernels' packed per-bin records (device_split_records) must be built from them, per
-    call, forward and inverse, bit-exact against the reference on the same tables."""
+@pytest.mark.parametrize("altered", [True, False])
+def test_rfft_fixed_user_tables(dsp, torch_gpu, ref, kind, n, where, altered):
+    """realCoefA / B that are not the library's own (host or device buffers, contents changed or
+    copied as they are): the fused kernels' packed per-bin records (device_split_records) must be
+    built from them, per call, forward and inverse, bit-exact against the reference on the same
+    tables.  Altered tables are not symmetric, so the q31 N = 8192 inverse takes merge + CFFT; the
+    unaltered copies keep the fused kernel, with records from the content cache."""
     import ctypes as C
     torch = torch_gpu
     dt = DT[kind]
@@ -167,7 +170,8 @@ def test_rfft_fixed_user_tables(dsp, torch_gpu, ref, kind, n, where):
         tabs = []
         for name in ("pTwiddleAReal", "pTwiddleBReal"):
             t = np.ctypeslib.as_array(C.cast(getattr(S, name), ptr_t), (words,)).copy()
-            t[::7] = rng.integers(np.iinfo(dt).min, np.iinfo(dt).max, t[::7].size, dtype=dt)   # not the library's
+            if altered:
+                t[::7] = rng.integers(np.iinfo(dt).min, np.iinfo(dt).max, t[::7].size, dtype=dt)   # not the library's
             tabs.append(t)
             setattr(Sr, name, t.ctypes.data_as(ptr_t))
         keep = [torch.from_numpy(t).cuda() for t in tabs] if where == "device" else tabs
