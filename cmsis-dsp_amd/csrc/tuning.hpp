@@ -190,6 +190,9 @@
 #ifndef MI355X_RFFT_Q15_INV_FUSED   // inverse arm_rfft_q15 N = 8192: merge fused into the packed CFFT-4096
 #define MI355X_RFFT_Q15_INV_FUSED 1
 #endif
+#ifndef MI355X_RFFT_MERGE_WAVES   // fused radix-16 inverse: minimum waves per SIMD its registers must allow
+#define MI355X_RFFT_MERGE_WAVES 1
+#endif
 #ifndef MI355X_RFFT_MERGE_BLK   // fused inverse: merged elements per pinned block
 #define MI355X_RFFT_MERGE_BLK 4
 #endif
