@@ -167,7 +167,8 @@ template <typename T> struct MqPostArgs {
 template <typename T, int N, bool INV, bool BREV, bool SAT, bool PRE = false, bool POST = false, bool RSPLIT = false,
           bool RMERGE = false>
 // (RMERGE at N = 256: registers capped at two waves per SIMD -- q31 spills 12 VGPRs -- 470 against
-// 435 Gsamples/s at one wave; at N = 1024 the cap spills 60 and loses, 294 against 388: ab_u1)
+// 435 Gsamples/s at one wave; at N = 1024 the cap spills 60 and loses, 294 against 388: ab_u1;
+// RSPLIT at N = 1024 capped at three waves spills 4 and loses too, 307 against 320: ab_v1)
 __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : RMERGE ? (N == 256 ? 2 : MI355X_RFFT_MERGE_WAVES) : 1) void cfft_fx_r16_kernel(typename R16Ops<T, INV>::C* __restrict__ data,
                                                              uint32_t batch,
                                                              const typename R16Ops<T, INV>::C* __restrict__ tw,
