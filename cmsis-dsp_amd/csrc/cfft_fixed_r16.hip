@@ -166,10 +166,11 @@ template <typename T> struct MqPostArgs {
 // output rows in place of `data`.  The merge pass's write and the CFFT's re-read disappear.
 template <typename T, int N, bool INV, bool BREV, bool SAT, bool PRE = false, bool POST = false, bool RSPLIT = false,
           bool RMERGE = false>
-// (RMERGE at N = 256: registers capped at two waves per SIMD -- q31 spills 12 VGPRs -- 470 against
-// 435 Gsamples/s at one wave; at N = 1024 the cap spills 60 and loses, 294 against 388: ab_u1;
-// RSPLIT at N = 1024 capped at three waves spills 4 and loses too, 307 against 320: ab_v1)
-__global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : RMERGE ? (N == 256 ? 2 : MI355X_RFFT_MERGE_WAVES) : 1) void cfft_fx_r16_kernel(typename R16Ops<T, INV>::C* __restrict__ data,
+// (RMERGE: registers capped at two waves per SIMD, MI355X_RFFT_MERGE_WAVES.  With the lane exchange
+// (MI355X_RFFT_MERGE_XCH) q31 N = 1024 then spills 21 VGPRs and still runs 464-476 against 414-416
+// at one wave (ab_w1); without it the cap had spilled 60 there and lost, 294 against 388 (ab_u1).
+// RSPLIT at N = 1024 capped at three waves spills 4 and loses, 307 against 320: ab_v1)
+__global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : RMERGE ? MI355X_RFFT_MERGE_WAVES : 1) void cfft_fx_r16_kernel(typename R16Ops<T, INV>::C* __restrict__ data,
                                                              uint32_t batch,
                                                              const typename R16Ops<T, INV>::C* __restrict__ tw,
                                                              const typename R16Ops<T, INV>::C* __restrict__ win = nullptr,
@@ -261,7 +262,13 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : RMERGE ? (N == 256 ?
   };
   const int vin = (w * N + tp) * kC;                  // byte offset of the thread's first word
   V nq[16];
-  V nq2[RMERGE ? 16 : 1];                             // RMERGE: bins X[N - e]
+  // RMERGE, P > 64: bins X[N - e] prefetched too.  P <= 64 (MI355X_RFFT_MERGE_XCH): a transform's
+  // lanes sit in one wave and X[N - e] = X[(P - tp) + P (15 - u)] is lane P - tp's own word u' =
+  // 15 - u (lane tp = 0: its own word 16 - u, and X[N], loaded once) -- a ds_bpermute instead of a
+  // second set of loads and 16-32 prefetch VGPRs.
+  constexpr bool kXch = RMERGE && MI355X_RFFT_MERGE_XCH && P <= 64;
+  V nq2[RMERGE && !kXch ? 16 : 1];
+  V nqN{};                                            // kXch: X[N] of the lane's transform
   using Rec = typename SplitRec<T>::R;
   __shared__ Rec recl[RMERGE ? N : 1];                // RMERGE: the merge records of bins 0 .. N-1
   if constexpr (RMERGE) {
@@ -279,8 +286,9 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : RMERGE ? (N == 256 ?
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         nq[u] = O::ld(r, vsa, P * u * kC);
-        nq2[u] = O::ld(r, vsb, P * (15 - u) * kC);
+        if constexpr (!kXch) nq2[u] = O::ld(r, vsb, P * (15 - u) * kC);
       }
+      if constexpr (kXch) nqN = O::ld(r, (w * 2 * N + N) * kC, 0);
     } else {
       const __amdgpu_buffer_rsrc_t r = group_rsrc(g);
 #pragma unroll
@@ -300,6 +308,13 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : RMERGE ? (N == 256 ?
       // MI355X_RFFT_MERGE_BLK elements read and merged before the next block's.
       int ri = tp;
       asm volatile("" : "+v"(ri));
+      const int xsrc = ((t & 63) + P - 2 * tp) * 4;  // kXch: byte index of lane P - tp of this transform
+      auto xch = [&](V x) -> V {
+        if constexpr (sizeof(T) == 4)
+          return make_int2(__builtin_amdgcn_ds_bpermute(xsrc, x.x), __builtin_amdgcn_ds_bpermute(xsrc, x.y));
+        else
+          return __builtin_bit_cast(V, __builtin_amdgcn_ds_bpermute(xsrc, __builtin_bit_cast(int, x)));
+      };
 #pragma unroll
       for (int u0 = 0; u0 < 16; u0 += MI355X_RFFT_MERGE_BLK) {
         Rec rc[MI355X_RFFT_MERGE_BLK];
@@ -307,7 +322,15 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : RMERGE ? (N == 256 ?
         for (int u = 0; u < MI355X_RFFT_MERGE_BLK; ++u) rc[u] = recl[ri + P * (u0 + u)];
 #pragma unroll
         for (int u = 0; u < MI355X_RFFT_MERGE_BLK; ++u) {
-          const int2 m = rfft_merge_bin<T>(O::unpack(v[u0 + u]), O::unpack(nq2[u0 + u]), rc[u].x, rc[u].y, rc[u].z, rc[u].w);
+          const int uu = u0 + u;
+          V bm;
+          if constexpr (kXch) {
+            bm = xch(nq[15 - uu]);
+            if (tp == 0) bm = uu == 0 ? nqN : nq[(16 - uu) & 15];
+          } else {
+            bm = nq2[uu];
+          }
+          const int2 m = rfft_merge_bin<T>(O::unpack(v[uu]), O::unpack(bm), rc[u].x, rc[u].y, rc[u].z, rc[u].w);
           v[u0 + u] = O::pack(m.x, m.y);
         }
         __builtin_amdgcn_sched_barrier(0);

@@ -191,7 +191,10 @@
 #define MI355X_RFFT_Q15_INV_FUSED 1
 #endif
 #ifndef MI355X_RFFT_MERGE_WAVES   // fused radix-16 inverse: minimum waves per SIMD its registers must allow
-#define MI355X_RFFT_MERGE_WAVES 1
+#define MI355X_RFFT_MERGE_WAVES 2
+#endif
+#ifndef MI355X_RFFT_MERGE_XCH   // fused radix-16 inverse, N <= 1024: X[N - e] by lane exchange instead of loads
+#define MI355X_RFFT_MERGE_XCH 1
 #endif
 #ifndef MI355X_RFFT_MERGE_BLK   // fused inverse: merged elements per pinned block
 #define MI355X_RFFT_MERGE_BLK 4
