@@ -267,8 +267,11 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : RMERGE ? MI355X_RFFT
   // 15 - u (lane tp = 0: its own word 16 - u, and X[N], loaded once) -- a ds_bpermute instead of a
   // second set of loads and 16-32 prefetch VGPRs.
   constexpr bool kXch = RMERGE && MI355X_RFFT_MERGE_XCH && P <= 64;
-  V nq2[RMERGE && !kXch ? 16 : 1];
-  V nqN{};                                            // kXch: X[N] of the lane's transform
+  // P = 128 (MI355X_RFFT_MERGE_LDSX): the transform spans two waves, so the raw words go through the
+  // transform's LDS image instead (two extra barriers per group)
+  constexpr bool kLdsX = RMERGE && MI355X_RFFT_MERGE_LDSX && P > 64;
+  V nq2[RMERGE && !kXch && !kLdsX ? 16 : 1];
+  V nqN{};                                            // kXch / kLdsX: X[N] of the lane's transform
   using Rec = typename SplitRec<T>::R;
   __shared__ Rec recl[RMERGE ? N : 1];                // RMERGE: the merge records of bins 0 .. N-1
   if constexpr (RMERGE) {
@@ -286,9 +289,9 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : RMERGE ? MI355X_RFFT
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         nq[u] = O::ld(r, vsa, P * u * kC);
-        if constexpr (!kXch) nq2[u] = O::ld(r, vsb, P * (15 - u) * kC);
+        if constexpr (!kXch && !kLdsX) nq2[u] = O::ld(r, vsb, P * (15 - u) * kC);
       }
-      if constexpr (kXch) nqN = O::ld(r, (w * 2 * N + N) * kC, 0);
+      if constexpr (kXch || kLdsX) nqN = O::ld(r, (w * 2 * N + N) * kC, 0);
     } else {
       const __amdgpu_buffer_rsrc_t r = group_rsrc(g);
 #pragma unroll
@@ -306,6 +309,12 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : RMERGE ? MI355X_RFFT
       // The records are the same for every group: an opaque index keeps their LDS reads here
       // (hoisted out of the group loop they held 64 VGPRs for the kernel's life), in blocks of
       // MI355X_RFFT_MERGE_BLK elements read and merged before the next block's.
+      if constexpr (kLdsX) {
+        __syncthreads();                              // the previous group's last-pass reads are done
+#pragma unroll
+        for (int u = 0; u < 16; ++u) lds[tp + P * u] = O::to_w(nq[u]);   // natural order, unpadded
+        __syncthreads();
+      }
       int ri = tp;
       asm volatile("" : "+v"(ri));
       const int xsrc = ((t & 63) + P - 2 * tp) * 4;  // kXch: byte index of lane P - tp of this transform
@@ -327,6 +336,9 @@ __global__ __launch_bounds__(kBlock, POST ? MI355X_MQF_WG : RMERGE ? MI355X_RFFT
           if constexpr (kXch) {
             bm = xch(nq[15 - uu]);
             if (tp == 0) bm = uu == 0 ? nqN : nq[(16 - uu) & 15];
+          } else if constexpr (kLdsX) {
+            bm = O::from_w(lds[(N - tp - P * uu) & (N - 1)]);
+            if (uu == 0 && tp == 0) bm = nqN;
           } else {
             bm = nq2[uu];
           }

@@ -196,6 +196,9 @@
 #ifndef MI355X_RFFT_MERGE_XCH   // fused radix-16 inverse, N <= 1024: X[N - e] by lane exchange instead of loads
 #define MI355X_RFFT_MERGE_XCH 1
 #endif
+#ifndef MI355X_RFFT_MERGE_LDSX   // fused radix-16 inverse, N = 2048: X[N - e] through LDS instead of loads
+#define MI355X_RFFT_MERGE_LDSX 1
+#endif
 #ifndef MI355X_RFFT_MERGE_BLK   // fused inverse: merged elements per pinned block
 #define MI355X_RFFT_MERGE_BLK 4
 #endif
