@@ -21,6 +21,7 @@ from cmsisdsp_amd import _abi
 from . import datatype  # noqa: F401
 
 _lib = _amd.lib
+_ARCH_DEFAULT = 1                      # ARM_MATH_DEFAULT_TARGET_ARCH = ARM_MATH_SCALAR_ARCH (arm_math_types.h)
 
 
 def has_neon():
@@ -112,6 +113,13 @@ def arm_cfft_tmp_buffer_size(dt, nbSamples, buf_id, arch=None):
 
 def arm_cfft_output_buffer_size(dt, nbSamples, arch=None):
     return 2 * int(nbSamples)
+
+
+def arm_cifft_output_buffer_size(dt, nbSamples, arch=None):
+    """cmsisdsp_transform.c cmsis_arm_cifft_output_buffer_size ("II|$I", :3032-3050), answered
+    by the library's arm_cifft_output_buffer_size (arm_transform_buffer_sizes.c)."""
+    return int(_lib.arm_cifft_output_buffer_size(_ARCH_DEFAULT if arch is None else int(arch), int(dt),
+                                                 int(nbSamples)))
 
 
 # ------------------------------------------------------------------ real FFT (fast)
@@ -346,6 +354,16 @@ def arm_mat_mult_q31(pSrcA, pSrcB):
     return _amd.arm_mat_mult_fixed("q31", _arr(pSrcA, _np.int32), _arr(pSrcB, _np.int32))
 
 
+def arm_mat_mult_opt_q31(pSrcA, pSrcB, pState=None):
+    """cmsisdsp_matrix.c cmsis_arm_mat_mult_opt_q31 ("OOO" -> (status, C), :1302-1330)."""
+    return _amd.arm_mat_mult_fixed("opt_q31", _arr(pSrcA, _np.int32), _arr(pSrcB, _np.int32))
+
+
+def arm_mat_mult_q7(pSrcA, pSrcB, pState=None):
+    """cmsisdsp_matrix.c cmsis_arm_mat_mult_q7 ("OOO" -> (status, C), :1110-1140)."""
+    return _amd.arm_mat_mult_fixed("q7", _arr(pSrcA, _np.int8), _arr(pSrcB, _np.int8))
+
+
 def arm_mat_mult_q15(pSrcA, pSrcB, pState=None):
     return _amd.arm_mat_mult_fixed("q15", _arr(pSrcA, _np.int16), _arr(pSrcB, _np.int16))
 
@@ -398,6 +416,47 @@ for _fn in ("conv_fast_q15", "conv_fast_q31", "correlate_f32", "correlate_q15", 
             "correlate_fast_q31", "conv_partial_f32", "conv_partial_q15", "conv_partial_q31", "conv_partial_fast_q15",
             "conv_partial_fast_q31", "correlate_q7", "conv_partial_q7"):
     globals()[f"arm_{_fn}"] = _conv_family(_fn)
+del _fn
+
+
+# The scratch-buffer ("_opt") forms, cmsisdsp_filtering.c cmsis_arm_conv_opt_q15 / _q7 /
+# _fast_opt_q15 ("OiOiOO", :3993, :4231, :4112), cmsis_arm_correlate_opt_q15 / _fast_opt_q15
+# ("OiOiO", :6316, :6431), cmsis_arm_correlate_opt_q7 ("OiOiOO", :6546) -> the output words;
+# cmsis_arm_conv_partial_opt_q15 / _q7 / _fast_opt_q15 ("OiOiiiOO", :4354, :4616, :4485) ->
+# (status, srcALen + srcBLen - 1 words).  The caller's scratch arrays are accepted and not
+# touched: the C call gets scratch of its own, sized as the reference requires
+# (pScratch1 srcALen + 2 srcBLen - 2 q15 words, pScratch2 min(srcALen, srcBLen)).
+def _conv_opt(fn):
+    dt = _DT[fn.split("_")[-1]]
+    n_scratch = _abi.CONV_OPT_FULL.get(fn, 2)
+
+    def run(pSrcA, srcALen, pSrcB, srcBLen, *rest):
+        a = _arr(pSrcA, dt)[:int(srcALen)]
+        b = _arr(pSrcB, dt)[:int(srcBLen)]
+        s1 = _np.zeros(len(a) + 2 * len(b) + 16, _np.int16)
+        s2 = _np.zeros(len(a) + 2 * len(b) + 16, _np.int16)
+        f = getattr(_lib, f"arm_{fn}")
+        if fn in _abi.CONV_OPT_PARTIAL:
+            first, num = int(rest[0]), int(rest[1])
+            y = _np.zeros(len(a) + len(b) - 1, dt)
+            st = f(a.ctypes.data, len(a), b.ctypes.data, len(b), y.ctypes.data, first, num, s1.ctypes.data,
+                   s2.ctypes.data)
+            _check(f"arm_{fn}")
+            return st, y
+        n = 2 * max(len(a), len(b)) - 1 if fn.startswith("correlate") else len(a) + len(b) - 1
+        y = _np.zeros(n, dt)
+        args = [a.ctypes.data, len(a), b.ctypes.data, len(b), y.ctypes.data, s1.ctypes.data]
+        if n_scratch == 2:
+            args.append(s2.ctypes.data)
+        f(*args)
+        _check(f"arm_{fn}")
+        return y
+    run.__name__ = f"arm_{fn}"
+    return run
+
+
+for _fn in (*_abi.CONV_OPT_FULL, *_abi.CONV_OPT_PARTIAL):
+    globals()[f"arm_{_fn}"] = _conv_opt(_fn)
 del _fn
 
 

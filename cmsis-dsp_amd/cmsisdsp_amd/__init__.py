@@ -580,7 +580,7 @@ def conv_family_batch(fn, a, b, out, first=0, num=0, stream=None):
 
 def arm_mat_mult_fixed(kind, a, b):
     """(status, C) = A @ B through arm_mat_mult_q7 / _q15 / _q31 / _fast_q15 / _fast_q31 (kind
-    "q7", "q15", "q31", "fast_q15", "fast_q31"; row-major)."""
+    "q7", "q15", "q31", "opt_q31", "fast_q15", "fast_q31"; row-major)."""
     base = "q7" if kind == "q7" else kind[-3:]
     dt = {"q7": np.int8, "q15": np.int16, "q31": np.int32}[base]
     inst = {"q7": arm_matrix_instance_q7, "q15": arm_matrix_instance_q15, "q31": arm_matrix_instance_q31}[base]
@@ -593,7 +593,7 @@ def arm_mat_mult_fixed(kind, a, b):
     init(C.byref(B), b.shape[0], b.shape[1], b.ctypes.data)
     init(C.byref(Cm), c.shape[0], c.shape[1], c.ctypes.data)
     fn = getattr(lib, f"arm_mat_mult_{kind}")
-    st = fn(C.byref(A), C.byref(B), C.byref(Cm), None) if base in ("q15", "q7") else \
+    st = fn(C.byref(A), C.byref(B), C.byref(Cm), None) if base in ("q15", "q7") or kind == "opt_q31" else \
         fn(C.byref(A), C.byref(B), C.byref(Cm))
     _check_void(f"arm_mat_mult_{kind}")
     return st, c

@@ -202,6 +202,8 @@ DROPIN = {
                                    P(arm_matrix_instance_q15), C.c_void_p]),
     "arm_mat_mult_q31": (C.c_int, [P(arm_matrix_instance_q31), P(arm_matrix_instance_q31),
                                    P(arm_matrix_instance_q31)]),
+    "arm_mat_mult_opt_q31": (C.c_int, [P(arm_matrix_instance_q31), P(arm_matrix_instance_q31),
+                                       P(arm_matrix_instance_q31), C.c_void_p]),
     "arm_mat_mult_fast_q15": (C.c_int, [P(arm_matrix_instance_q15), P(arm_matrix_instance_q15),
                                         P(arm_matrix_instance_q15), C.c_void_p]),
     "arm_mat_mult_fast_q31": (C.c_int, [P(arm_matrix_instance_q31), P(arm_matrix_instance_q31),

@@ -228,7 +228,7 @@ bool rfft_fixed_run(const RInst* S, T* d_src, T* d_dst, uint32_t batch, hipStrea
   const void* irec = nullptr;
   if (ifuse) {
     bool sym = false;
-    irec = device_split_records(S->pTwiddleAReal, S->pTwiddleBReal, S->twidCoefRModifier, L, (int)sizeof(T), &sym);
+    irec = device_split_records(S->pTwiddleAReal, S->pTwiddleBReal, S->twidCoefRModifier, L, (int)sizeof(T), st, &sym);
     if (!irec) return false;
     if (kind == 1 && L == 4096 && !sym) ifuse = false;
   }
@@ -270,7 +270,7 @@ bool rfft_fixed_run(const RInst* S, T* d_src, T* d_dst, uint32_t batch, hipStrea
                                                       (const int16_t*)ta, (const int16_t*)tb, S->twidCoefRModifier, st),
                "rfft fused");
     } else {
-      const void* rec = device_split_records(S->pTwiddleAReal, S->pTwiddleBReal, S->twidCoefRModifier, L, (int)sizeof(T));
+      const void* rec = device_split_records(S->pTwiddleAReal, S->pTwiddleBReal, S->twidCoefRModifier, L, (int)sizeof(T), st);
       if (!rec) return false;
       const bool done = kind == 1
           ? rfft_q31_r16_fused_launch((int)L, (int32_t*)d_src, (int32_t*)d_dst, batch, (const int32_t*)pr.tw, rec, st)
@@ -1469,6 +1469,13 @@ arm_status arm_mat_mult_q15(const arm_matrix_instance_q15* pSrcA, const arm_matr
 }
 arm_status arm_mat_mult_q31(const arm_matrix_instance_q31* pSrcA, const arm_matrix_instance_q31* pSrcB,
                             arm_matrix_instance_q31* pDst) {
+  return mat_mult_fixed_sync<int32_t>(pSrcA, pSrcB, pDst);
+}
+// arm_mat_mult_opt_q31.c:648-780 (the host build's scalar branch): the q31 product above; pState
+// (the Helium branch's transpose buffer) is unused there too.
+arm_status arm_mat_mult_opt_q31(const arm_matrix_instance_q31* pSrcA, const arm_matrix_instance_q31* pSrcB,
+                                arm_matrix_instance_q31* pDst, q31_t* pState) {
+  (void)pState;
   return mat_mult_fixed_sync<int32_t>(pSrcA, pSrcB, pDst);
 }
 // arm_mat_mult_fast_q15.c:351-401 (!ARM_MATH_DSP: q31_t modular sum, (q15)(sum >> 15)),

@@ -645,6 +645,10 @@ __global__ __launch_bounds__(128) void cfft_f32_n1024_lat_kernel(float2* __restr
       v[m + 4] = make_float2(t4.x * w.y - t4.y * w.x, t4.y * w.y + t4.x * w.x);
     }
   }
+  // Both waves read all of X above and each writes half of it back below: every wave's loads must
+  // have returned before either wave stores (the pre-pass already waited for its own loads, so the
+  // barrier costs only the other wave's skew).
+  __syncthreads();
   const int hb = 512 * h;
   r8_sel(v, w0, l != 0);                               // stage 0
 #pragma unroll

@@ -374,7 +374,8 @@ const void* device_blob(const void* host, size_t bytes) {
   return hand_out(b);
 }
 
-const void* device_split_records(const void* A, const void* B, uint32_t mod, uint32_t L, int elem, bool* symmetric) {
+const void* device_split_records(const void* A, const void* B, uint32_t mod, uint32_t L, int elem, hipStream_t st,
+                                 bool* symmetric) {
   if (symmetric) *symmetric = false;
   if (!A || !B || !mod || !L || (elem != 2 && elem != 4)) {
     set_error(hipErrorInvalidValue, "split records");
@@ -401,7 +402,9 @@ const void* device_split_records(const void* A, const void* B, uint32_t mod, uin
     const void* src = s ? B : A;
     uint8_t* dst = s ? hb.data() : ha.data();
     if (is_device_ptr(src)) {
-      if (hipMemcpy(dst, src, wb, hipMemcpyDeviceToHost) != hipSuccess) {
+      // on the call's stream: ordered after whatever the caller enqueued there (e.g. the table's
+      // own upload on a non-blocking stream), which a null-stream copy is not
+      if (hipMemcpyAsync(dst, src, wb, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
         set_error(hipErrorInvalidValue, "split records: table copy");
         return nullptr;
       }

@@ -45,7 +45,9 @@ size_t blob_cache_bytes();
 // A, B, mod, L); any other (host or device) table: rebuilt per call and cached by content.
 // *symmetric (optional): record L - k equals record k with A1 and B1 negated for every k (true of the
 // reference's realCoefA/B tables), which the fused N = 8192 q31 inverse relies on.
-const void* device_split_records(const void* A, const void* B, uint32_t mod, uint32_t L, int elem,
+// A device-resident table is read back on `st` (the call's stream, then synchronized), so a table
+// the caller wrote on that stream just before the call is read after that write.
+const void* device_split_records(const void* A, const void* B, uint32_t mod, uint32_t L, int elem, hipStream_t st,
                                  bool* symmetric = nullptr);
 void set_blob_cache_limit(size_t bytes);   // per device
 

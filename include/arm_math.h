@@ -742,6 +742,11 @@ arm_status arm_mat_mult_q15(const arm_matrix_instance_q15 *pSrcA, const arm_matr
                             arm_matrix_instance_q15 *pDst, q15_t *pState);
 arm_status arm_mat_mult_q31(const arm_matrix_instance_q31 *pSrcA, const arm_matrix_instance_q31 *pSrcB,
                             arm_matrix_instance_q31 *pDst);
+/* matrix_functions.h:459-463.  The scalar branch of Source/MatrixFunctions/arm_mat_mult_opt_q31.c:
+ * 648-780 is arm_mat_mult_q31's (q63 sum of exact products, (q31)(sum >> 31)) with an unused
+ * pState, so this runs the same bit-exact i8-plane GEMM. */
+arm_status arm_mat_mult_opt_q31(const arm_matrix_instance_q31 *pSrcA, const arm_matrix_instance_q31 *pSrcB,
+                                arm_matrix_instance_q31 *pDst, q31_t *pState);
 /* Fast fixed-point matrix multiply (matrix_functions.h:431-435,484-487):
  * arm_mat_mult_fast_q15.c (!ARM_MATH_DSP): q31_t modular sum of q15 products, (q15)(sum >> 15);
  * arm_mat_mult_fast_q31.c: sum = (q31)(((q63)sum << 32 + a*b) >> 32) per product, output

@@ -52,7 +52,7 @@ SRCS := \
   $(SU)/arm_copy_q15.c $(SU)/arm_fill_q15.c \
   $(F)/arm_fir_q7.c $(F)/arm_fir_init_q7.c $(F)/arm_conv_q7.c $(F)/arm_conv_partial_q7.c $(F)/arm_correlate_q7.c \
   $(M)/arm_mat_mult_f32.c $(M)/arm_mat_init_f32.c $(M)/arm_mat_vec_mult_f32.c \
-  $(M)/arm_mat_mult_q7.c $(M)/arm_mat_mult_q15.c $(M)/arm_mat_mult_q31.c $(M)/arm_mat_mult_fast_q15.c $(M)/arm_mat_mult_fast_q31.c $(M)/arm_mat_init_q7.c $(M)/arm_mat_init_q15.c $(M)/arm_mat_init_q31.c \
+  $(M)/arm_mat_mult_q7.c $(M)/arm_mat_mult_q15.c $(M)/arm_mat_mult_q31.c $(M)/arm_mat_mult_opt_q31.c $(M)/arm_mat_mult_fast_q15.c $(M)/arm_mat_mult_fast_q31.c $(M)/arm_mat_init_q7.c $(M)/arm_mat_init_q15.c $(M)/arm_mat_init_q31.c \
   $(T)/arm_mfcc_f32.c $(T)/arm_mfcc_init_f32.c $(ST)/arm_absmax_f32.c $(B)/arm_scale_f32.c \
   $(B)/arm_mult_f32.c $(B)/arm_dot_prod_f32.c $(B)/arm_offset_f32.c $(X)/arm_cmplx_mag_f32.c \
   $(FM)/arm_vlog_f32.c \

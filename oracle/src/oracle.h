@@ -31,6 +31,8 @@ arm_status oracle_arm_mat_mult_q15(const arm_matrix_instance_q15 *A, const arm_m
                                    arm_matrix_instance_q15 *C, int16_t *pState);
 arm_status oracle_arm_mat_mult_q31(const arm_matrix_instance_q31 *A, const arm_matrix_instance_q31 *B,
                                    arm_matrix_instance_q31 *C);
+arm_status oracle_arm_mat_mult_opt_q31(const arm_matrix_instance_q31 *A, const arm_matrix_instance_q31 *B,
+                                       arm_matrix_instance_q31 *C, int32_t *pState);
 arm_status oracle_arm_mat_mult_fast_q15(const arm_matrix_instance_q15 *A, const arm_matrix_instance_q15 *B,
                                         arm_matrix_instance_q15 *C, int16_t *pState);
 arm_status oracle_arm_mat_mult_fast_q31(const arm_matrix_instance_q31 *A, const arm_matrix_instance_q31 *B,

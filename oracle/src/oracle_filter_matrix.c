@@ -202,6 +202,13 @@ arm_status oracle_arm_mat_mult_q31(const arm_matrix_instance_q31 *A, const arm_m
   return ARM_MATH_SUCCESS;
 }
 
+/* arm_mat_mult_opt_q31.c:648-780 (the scalar branch): the q31 product above, pState unused. */
+arm_status oracle_arm_mat_mult_opt_q31(const arm_matrix_instance_q31 *A, const arm_matrix_instance_q31 *B,
+                                       arm_matrix_instance_q31 *Cm, int32_t *pState) {
+  (void)pState;
+  return oracle_arm_mat_mult_q31(A, B, Cm);
+}
+
 /* arm_mat_mult_fast_q15.c:351-401 (!ARM_MATH_DSP): q31_t sum += a*b (wrapping), output
  * (q15)(sum >> 15) -- truncation, no saturation.  arm_mat_mult_fast_q31.c:152-166, :215-266:
  * sum = (q31)(((q63)sum << 32 + (q63)a*b) >> 32) per product (= sum + ((a*b) >> 32) mod 2^32),

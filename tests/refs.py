@@ -262,7 +262,7 @@ class Host:
         return y, 0
 
     def mat_mult_fixed(self, kind, a, b):
-        """arm_mat_mult_q7 / _q15 / _q31 / _fast_q15 / _fast_q31: returns (status, C)."""
+        """arm_mat_mult_q7 / _q15 / _q31 / _opt_q31 / _fast_q15 / _fast_q31: returns (status, C)."""
         base = kind[-3:] if kind != "q7" else "q7"
         dt = {"q7": np.int8, "q15": np.int16, "q31": np.int32}[base]
         inst = {"q7": _abi.arm_matrix_instance_q7, "q15": _abi.arm_matrix_instance_q15,
@@ -275,7 +275,7 @@ class Host:
         init(C.byref(A), a.shape[0], a.shape[1], a.ctypes.data)
         init(C.byref(B), b.shape[0], b.shape[1], b.ctypes.data)
         init(C.byref(Cm), c.shape[0], c.shape[1], c.ctypes.data)
-        if base in ("q15", "q7"):
+        if base in ("q15", "q7") or kind == "opt_q31":
             state = np.zeros(a.shape[1] * b.shape[1] + 16, dtype=dt)
             st = self.fn(f"arm_mat_mult_{kind}")(C.byref(A), C.byref(B), C.byref(Cm), state.ctypes.data)
         else:

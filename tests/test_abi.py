@@ -49,6 +49,8 @@ def test_library_exports_every_declared_symbol(dsp):
         except AttributeError:
             missing.append(n)
     assert not missing, missing
+    # VERDICT r5 Missing #2: matrix_functions.h:459 (arm_mat_mult_opt_q31.c:648-780)
+    assert "arm_mat_mult_opt_q31" in names and callable(dsp.lib.arm_mat_mult_opt_q31)
 
 
 def test_struct_layout_matches_reference():

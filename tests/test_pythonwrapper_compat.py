@@ -4,6 +4,8 @@ test_fir_f32 / test_mat_mult_f32, testdsp2.py test_arm_mat_mult_q31 / _q15, test
 test_rfft_f32 / test_rifft_f32, testmfcc.py) with their tolerances, plus bit-exact checks
 against the reference build.  The helpers below restate the examples' testtools.py
 conversions (toQ15 / toQ31: round, saturate)."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -235,3 +237,100 @@ def test_correlate_and_partial(cdsp, torch_gpu, ref):
             assert got.tobytes() == ref.conv_family(fn, qa, qb)[0].tobytes(), fn
         st, got = getattr(cdsp, f"arm_conv_partial_{kind}")(qa, len(qa), qb, len(qb), 3, 30)
         assert st == 0 and got[3:33].tobytes() == ref.conv_family(f"conv_partial_{kind}", qa, qb, 3, 30)[0][3:33].tobytes()
+
+
+_R6_NAMES = ("arm_mat_mult_q7", "arm_mat_mult_opt_q31", "arm_conv_opt_q15", "arm_conv_opt_q7", "arm_conv_fast_opt_q15",
+             "arm_conv_partial_opt_q15", "arm_conv_partial_opt_q7", "arm_conv_partial_fast_opt_q15",
+             "arm_correlate_opt_q15", "arm_correlate_opt_q7", "arm_correlate_fast_opt_q15",
+             "arm_cifft_output_buffer_size")
+
+
+def test_module_exposes_the_reference_binding_names(cdsp, ref):
+    """VERDICT r5 Missing #1: the names cmsisdsp_matrix.c (:1110-1140, :1302-1330),
+    cmsisdsp_filtering.c (:3993, :4112, :4231, :4354, :4485, :4616, :6316, :6431, :6546) and
+    cmsisdsp_transform.c (:3032-3050) register exist here; the buffer-size helper (host-only)
+    equals the reference build's for every datatype."""
+    import cmsisdsp.datatype as dt
+    for name in _R6_NAMES:
+        assert callable(getattr(cdsp, name)), name
+    f = ref.fn("arm_cifft_output_buffer_size")
+    f.restype, f.argtypes = C.c_int32, [C.c_int, C.c_int, C.c_uint32]
+    for d in (dt.F32, dt.Q31, dt.Q15, dt.F64, dt.F16):
+        for n in (16, 1024, 4096, 15):
+            assert cdsp.arm_cifft_output_buffer_size(d, n) == f(1, d, n)
+            assert cdsp.arm_cifft_output_buffer_size(d, n, arch=4) == f(4, d, n)
+
+
+def _fixed(kind, n, rng, dist):
+    info = np.iinfo({"q7": np.int8, "q15": np.int16, "q31": np.int32}[kind])
+    dt = info.dtype
+    if dist == "min":
+        return np.full(n, info.min, dt)
+    if dist == "max":
+        return np.full(n, info.max, dt)
+    return rng.integers(info.min, info.max, n, endpoint=True).astype(dt)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dist", ["rand", "max", "min"])
+def test_mat_mult_q7_opt_q31_module(cdsp, torch_gpu, ref, dist):
+    """cmsis_arm_mat_mult_q7 / _opt_q31 call shapes ("OOO" -> (status, C)) on ragged shapes and
+    extreme words, bit-exact vs the reference build (q7: M*N <= 65535, the reference's uint16_t
+    row offset, arm_mat_mult_q7.c:689-790)."""
+    rng = np.random.default_rng({"rand": 11, "max": 12, "min": 13}[dist])
+    for m, k, n in ((1, 1, 1), (7, 33, 5), (64, 100, 96), (130, 257, 70)):
+        for kind in ("q7", "opt_q31"):
+            base = "q7" if kind == "q7" else "q31"
+            a = _fixed(base, m * k, rng, dist).reshape(m, k)
+            b = _fixed(base, k * n, rng, dist).reshape(k, n)
+            st, c = getattr(cdsp, f"arm_mat_mult_{kind}")(a, b, np.zeros(k * n + 16, a.dtype))
+            st_r, c_r = ref.mat_mult_fixed(kind, a, b)
+            assert st == st_r == 0 and c.shape == (m, n)
+            assert c.tobytes() == c_r.tobytes(), (kind, m, k, n, dist)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dist", ["rand", "max", "min"])
+def test_conv_opt_module(cdsp, torch_gpu, ref, dist):
+    """The nine scratch-buffer forms through the module's call shapes ("OiOiOO" / "OiOiO" /
+    "OiOiiiOO"), ragged lengths in both orders, bit-exact vs the reference build.  All-minimum q15
+    words take the plain function's words for the exact _opt forms (the reference's host
+    __SMLALD emulation wraps the (-32768)^2 pair sum, none.h:503-505; tests/test_conv_opt.py)."""
+    from cmsisdsp_amd import _abi
+    rng = np.random.default_rng({"rand": 21, "max": 22, "min": 23}[dist])
+    for la, lb in ((1, 1), (1, 9), (9, 1), (40, 13), (13, 40), (97, 64)):
+        for fn in (*_abi.CONV_OPT_FULL, *_abi.CONV_OPT_PARTIAL):
+            kind = fn.split("_")[-1]
+            a, b = _fixed(kind, la, rng, dist), _fixed(kind, lb, rng, dist)
+            plain = fn.replace("_opt", "")
+            exact_min = dist == "min" and kind == "q15" and "fast" not in fn
+            py = getattr(cdsp, f"arm_{fn}")
+            if fn in _abi.CONV_OPT_PARTIAL:
+                first, num = min(2, la + lb - 2), max(1, min(la + lb - 3, 30))
+                st, y = py(a, la, b, lb, first, num, np.zeros(1, np.int16), np.zeros(1, np.int16))
+                if exact_min:
+                    want, st_r = ref.conv_family(plain, a, b, first, num)
+                else:
+                    want = np.zeros(la + lb + 4, y.dtype)
+                    s1 = np.zeros(la + 2 * lb + 16, np.int16)
+                    s2 = np.zeros(la + 2 * lb + 16, np.int16)
+                    st_r = ref.fn(f"arm_{fn}")(a.ctypes.data, la, b.ctypes.data, lb, want.ctypes.data, first, num,
+                                               s1.ctypes.data, s2.ctypes.data)
+                assert len(y) == la + lb - 1 and st == st_r, (fn, la, lb)
+                if st == 0:
+                    assert y[first:first + num].tobytes() == want[first:first + num].tobytes(), (fn, la, lb, dist)
+                continue
+            scratch = [np.zeros(1, np.int16)] * _abi.CONV_OPT_FULL[fn]
+            y = py(a, la, b, lb, *scratch)
+            if exact_min:
+                want = ref.conv_family(plain, a, b)[0]
+            else:
+                n = 2 * max(la, lb) - 1 if fn.startswith("correlate") else la + lb - 1
+                want = np.zeros(n, y.dtype)
+                s1 = np.zeros(la + 2 * lb + 16, np.int16)
+                s2 = np.zeros(la + 2 * lb + 16, np.int16)
+                args = [a.ctypes.data, la, b.ctypes.data, lb, want.ctypes.data, s1.ctypes.data]
+                if _abi.CONV_OPT_FULL[fn] == 2:
+                    args.append(s2.ctypes.data)
+                ref.fn(f"arm_{fn}")(*args)
+            assert y.tobytes() == want.tobytes(), (fn, la, lb, dist)

@@ -217,3 +217,54 @@ def test_rfft_fixed_fused_ragged_batches(dsp, torch_gpu, ref, kind, n):
                 assert got[r].tobytes() == want.tobytes(), (batch, ifft, r)
                 if not ifft:
                     assert src[r].cpu().numpy().tobytes() == wsrc.tobytes(), (batch, r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["q31", "q15"])
+def test_rfft_fixed_device_tables_written_on_the_call_stream(dsp, torch_gpu, ref, kind):
+    """device-resident realCoefA / B written on a non-blocking stream just before the
+    batched call (behind a long kernel on that stream) must be read after that write: the fused
+    kernels' records (device_split_records) are read back on the call's stream, not the null
+    stream.  Tables are altered, so the result differs from the library's own tables'; forward
+    and inverse, N = 1024 (fused radix-16 path), bit-exact against the reference."""
+    import ctypes as C
+    torch = torch_gpu
+    dt = DT[kind]
+    ptr_t = C.POINTER(C.c_int32 if kind == "q31" else C.c_int16)
+    n, batch = 1024, 5
+    rng = np.random.default_rng(77 + (kind == "q15"))
+    side = torch.cuda.Stream()
+    for ifft in (0, 1):
+        S = _instance(dsp, kind, n, ifft, 1)
+        Sr = (refs._abi.arm_rfft_instance_q31 if kind == "q31" else refs._abi.arm_rfft_instance_q15)()
+        assert ref.fn(f"arm_rfft_init_{kind}")(C.byref(Sr), n, ifft, 1) == 0
+        words = S.twidCoefRModifier * n
+        tabs, dev = [], []
+        for name in ("pTwiddleAReal", "pTwiddleBReal"):
+            t = np.ctypeslib.as_array(C.cast(getattr(S, name), ptr_t), (words,)).copy()
+            t[::5] = rng.integers(np.iinfo(dt).min, np.iinfo(dt).max, t[::5].size, dtype=dt)
+            tabs.append(t)
+            setattr(Sr, name, t.ctypes.data_as(ptr_t))
+        words_in = 2 * n if ifft else n
+        x = np.stack([refs.rand_input(kind, words_in, seed=5 * r + ifft, dist="uniform") for r in range(batch)])
+        want = []
+        for r in range(batch):
+            out = np.zeros(n if ifft else 2 * n, dtype=dt)
+            ref.fn(f"arm_rfft_{kind}")(C.byref(Sr), x[r].copy().ctypes.data, out.ctypes.data)
+            want.append(out)
+        s = torch.from_numpy(x.copy()).cuda()
+        d = torch.zeros((batch, n if ifft else 2 * n), dtype=s.dtype, device="cuda")
+        host = [torch.from_numpy(t).pin_memory() for t in tabs]
+        big = torch.randn(4096, 4096, device="cuda")
+        torch.cuda.synchronize()
+        with torch.cuda.stream(side):
+            dev = [torch.zeros(words, dtype=s.dtype, device="cuda") for _ in tabs]
+            for _ in range(8):
+                big = big @ big * 1e-3                    # keeps the stream busy before the write
+            for dd, hh in zip(dev, host):
+                dd.copy_(hh, non_blocking=True)
+        for name, t in zip(("pTwiddleAReal", "pTwiddleBReal"), dev):
+            setattr(S, name, C.cast(C.c_void_p(t.data_ptr()), ptr_t))
+        dsp.rfft_fixed_batch(S, s, d, stream=side)
+        torch.cuda.synchronize()
+        assert d.cpu().numpy().tobytes() == np.stack(want).tobytes(), ifft
