@@ -1,0 +1,266 @@
+// Batched arm_fir_q15 on the i8 matrix cores — MI355X, bit-exact.
+//
+// Replaces the host scalar path of Source/FilteringFunctions/arm_fir_q15.c:458-726 (the
+// ARM_MATH_LOOPUNROLL, !ARM_MATH_DSP branch): with s = [history (T - 1) ; block] and the taps in
+// the reference's order, y[n] = __SSAT(acc >> 15, 16) where acc is a q63 sum over tap PAIRS of the
+// __SMLALD pair sums (int32-wrapped, none.h:497-506) for the unrolled outputs and of exact products
+// for the blockSize % 4 tail (:649-681).  A pair sum wraps only for a coefficient pair (-32768,
+// -32768) times a sample pair (-32768, -32768); for any other taps both branches are the exact sum
+// of products, an integer GEMM, which this kernel runs on v_mfma_i32_32x32x32_i8.  Taps holding
+// such a pair take the exact pair-wise VALU path of the same kernel (it needs two consecutive
+// coefficients of -32768).
+//
+// FIR as a GEMM: a block of 32 consecutive outputs n0 .. n0 + 31 is y[n0 + i] = sum_k Tc[i][k]
+// w[k] over a window w of the state, with the banded Toeplitz matrix Tc[i][k] = c[k - d - i]
+// (0 <= k - d - i < T; d in {0, 1} is the window's start one sample early, so that its source
+// words are 4-byte aligned).  32 such blocks (1024 outputs) are one 32 x 32 MFMA tile: MFMA A
+// operand = Tc (32 outputs x K), B operand = the 32 blocks' windows (K x 32 blocks, column j =
+// w[32 j + k]: consecutive blocks' windows overlap, all read from one staged window in LDS),
+// D[i][j] = y[n0 + 32 j + i] -- the accumulator layout gives a lane four consecutive outputs per
+// register quad.  K = 32 KS >= T + 32.
+//
+// Exact i8 planes: samples x = 256 xh + xl' + 128 (xh = x >> 8, xl' = (x & 255) - 128, signed
+// bytes); coefficients WITHOUT an offset, c = 2^14 a + 2^7 b + c0 (b, c0 in 0 .. 127, a = c >> 14
+// in -2 .. 1, carried as a' = 64 a), so the only correction is the constant 128 sum(c):
+//   sum x c = 2^16 (xh.a') + 2^15 (xh.b) + 2^8 (xh.c0 + xl'.a') + 2^7 (xl'.b) + (xl'.c0) + 128 sum c
+// six plane products per K step into five int32 accumulators (each exact: |class sum| < 2^24 for
+// K <= 192), formed in int64 for the output.  The three coefficient planes of Tc, as the MFMA's A
+// operand wants them lane by lane, are built once per call by fir_q15_coef_image_kernel (for both
+// window shifts d) and read by every workgroup from L2.
+//
+// Geometry: persistent workgroups of 4 waves walk the items = (filter, chunk of 4096 outputs); wave
+// w takes the 32 blocks of outputs 1024 w .. + 1023.  The window (count + T samples) is staged into
+// two LDS byte planes (xh, xl') in 256-B rows whose 16-B slots are XOR-swizzled by the row's parity
+// (slot ^ (row & 1)), so the B-operand reads (ds_read_b128, lane j at byte 32 j + 32 ks + 16 h) hit
+// 16 distinct slots in every 16-lane group.  The next item's window words are loaded into
+// registers while the current item is multiplied.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace mi355x {
+
+namespace {
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kFmChunk = 4096;                 // outputs per item (4 waves x 32 blocks x 32)
+constexpr int kFmMaxKS = 6;                    // K steps: T + 32 <= 192 -> T <= 160
+constexpr int kFmWords = (kFmChunk + 32 * kFmMaxKS) / 2;   // window words staged per item (>= count + T + 1 samples)
+constexpr int kFmPer = (kFmWords + 255) / 256;             // words per thread
+constexpr int kFmPlane = 2 * kFmWords + 256;               // plane bytes (whole rows + look-ahead)
+
+__device__ __forceinline__ int fm_swz(int m) {  // byte m of a plane -> LDS byte (16-B slots XORed by row parity)
+  return (m & ~255) | ((((m >> 4) & 15) ^ ((m >> 8) & 1)) << 4) | (m & 15);
+}
+}  // namespace
+
+// Coefficient planes of Tc for both window shifts d, lane by lane: image[d][ks][plane][lane] = the
+// 16 bytes lane L = (i = L & 31, h = L >> 5) passes as the MFMA A operand at K step ks, i.e. the
+// plane bytes of c[32 ks + 16 h + e - d - i], e = 0 .. 15 (0 outside the taps).  Also [2] words:
+// sum(c) and whether a (-32768, -32768) tap pair is present.
+__global__ __launch_bounds__(64) void fir_q15_coef_image_kernel(const int16_t* __restrict__ coeffs, int T, int KS,
+                                                                uint4* __restrict__ image, int* __restrict__ info) {
+  const int L = threadIdx.x, i = L & 31, h = L >> 5;
+  for (int d = 0; d < 2; ++d)
+    for (int ks = 0; ks < KS; ++ks) {
+      uint32_t w[3][4] = {};
+      for (int e = 0; e < 16; ++e) {
+        const int ci = 32 * ks + 16 * h + e - d - i;
+        const int32_t c = (ci >= 0 && ci < T) ? coeffs[ci] : 0;
+        w[0][e >> 2] |= (uint32_t)(uint8_t)(int8_t)(64 * (c >> 14)) << (8 * (e & 3));
+        w[1][e >> 2] |= (uint32_t)((c >> 7) & 127) << (8 * (e & 3));
+        w[2][e >> 2] |= (uint32_t)(c & 127) << (8 * (e & 3));
+      }
+      for (int p = 0; p < 3; ++p)
+        image[((d * KS + ks) * 3 + p) * 64 + L] = make_uint4(w[p][0], w[p][1], w[p][2], w[p][3]);
+    }
+  if (L == 0) {
+    int sum = 0, wrap = 0;
+    for (int k = 0; k < T; ++k) sum += coeffs[k];
+    for (int m = 0; m + 1 < T; m += 2) wrap |= coeffs[m] == -32768 && coeffs[m + 1] == -32768;
+    info[0] = sum;
+    info[1] = wrap;
+  }
+}
+
+template <int KS>
+__global__ __launch_bounds__(256, 2) void fir_q15_mfma_kernel(const int16_t* __restrict__ coeffs, int T,
+                                                              const int16_t* __restrict__ src, int16_t* __restrict__ dst,
+                                                              uint32_t B, const int16_t* __restrict__ hist,
+                                                              uint32_t nchunks, uint32_t items,
+                                                              const uint4* __restrict__ image,
+                                                              const int* __restrict__ info) {
+  __shared__ __attribute__((aligned(16))) uint8_t ph[kFmPlane];
+  __shared__ __attribute__((aligned(16))) uint8_t pl[kFmPlane];
+  const int tid = threadIdx.x, L = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T1 = T - 1;
+  const bool wrap = info[1] != 0;
+  const int64_t corr = 128 * (int64_t)info[0];
+
+  // window word u (samples 2u, 2u + 1 of w) of item `it`, w[m] = s[n0 - d + m], d = parity of the
+  // block-input offset so that the words of the block input are 4-byte aligned
+  struct Item { uint32_t f; int n0, count, d; };
+  auto item_of = [&](uint32_t it) {
+    Item x;
+    x.f = it / nchunks;
+    x.n0 = (int)(it - x.f * nchunks) * kFmChunk;
+    x.count = min((int)B - x.n0, kFmChunk);
+    x.d = (int)(((uint64_t)x.f * B + (uint32_t)x.n0 - (uint32_t)T1) & 1u);   // s index n0 - d + m -> src f B + n0 - d + m - T1
+    return x;
+  };
+  auto sample = [&](const Item& x, int m) -> uint32_t {   // w[m] as 16 bits (0 outside the state)
+    const int sidx = x.n0 - x.d + m;
+    if (sidx < 0 || sidx - T1 >= (int)B) return 0u;     // outside the state [history ; block]
+    return (uint16_t)(sidx < T1 ? hist[(uint64_t)x.f * T1 + sidx] : src[(uint64_t)x.f * B + (sidx - T1)]);
+  };
+  uint32_t wv[kFmPer];
+  auto load_window = [&](const Item& x) {
+    // block-input words: aligned dword loads; the history part (first item of a filter only) and
+    // the edges sample by sample
+    const int64_t base = (int64_t)x.f * B + x.n0 - x.d - T1;               // src index of w[0] (even)
+#pragma unroll
+    for (int q = 0; q < kFmPer; ++q) {
+      const int u = tid + 256 * q, m = 2 * u;
+      if (u >= kFmWords) { wv[q] = 0u; continue; }
+      const int sidx = x.n0 - x.d + m;
+      const bool whole = sidx >= T1 && base + m + 1 < (int64_t)(x.f + 1) * B;
+      if (whole) {
+        wv[q] = *reinterpret_cast<const uint32_t*>(src + base + m);
+      } else {
+        wv[q] = sample(x, m) | (sample(x, m + 1) << 16);
+      }
+    }
+  };
+  auto stage_window = [&]() {                            // registers -> the two byte planes
+#pragma unroll
+    for (int q = 0; q < kFmPer; ++q) {
+      const int u = tid + 256 * q;
+      if (u >= kFmWords) continue;
+      const uint32_t v = wv[q];
+      const uint32_t hi = ((v >> 8) & 0xFFu) | ((v >> 16) & 0xFF00u);
+      const uint32_t lo = ((v & 0xFFu) | ((v >> 8) & 0xFF00u)) ^ 0x8080u;   // (x & 255) - 128 per byte
+      const int a = fm_swz(2 * u);
+      *reinterpret_cast<uint16_t*>(ph + a) = (uint16_t)hi;
+      *reinterpret_cast<uint16_t*>(pl + a) = (uint16_t)lo;
+    }
+  };
+
+  uint32_t it = blockIdx.x;
+  if (it >= items) return;
+  Item cur = item_of(it);
+  load_window(cur);
+  const int i = L & 31, h = L >> 5;
+  for (;;) {
+    __syncthreads();                                     // the previous item's reads are done
+    stage_window();
+    __syncthreads();
+    const uint32_t nxt = it + gridDim.x;
+    const Item next = item_of(nxt < items ? nxt : it);
+    if (nxt < items) load_window(next);                  // in flight under this item's MFMAs
+
+    if (wrap) {
+      // exact pair-wise path (arm_fir_q15.c:482-640 unrolled outputs with the __SMLALD pair wrap,
+      // :649-681 tail outputs with exact products), from the planes
+      const int unrolled_end = (int)(B - (B & 3u));
+      auto xs = [&](int m) -> int32_t {
+        const int a = fm_swz(m);
+        return (int32_t)(int16_t)(uint16_t)(((uint32_t)ph[a] << 8) | (uint32_t)(pl[a] ^ 0x80u));
+      };
+      for (int o = tid; o < cur.count; o += 256) {
+        const int n = cur.n0 + o, m0 = o + cur.d;       // y[n] = sum_t s[n + t] c[t] = sum_t w[o + d + t] c[t]
+        int64_t acc = 0;
+        for (int m = 0; m < T / 2; ++m) {
+          const int64_t p0 = (int64_t)xs(m0 + 2 * m) * coeffs[2 * m], p1 = (int64_t)xs(m0 + 2 * m + 1) * coeffs[2 * m + 1];
+          acc += n < unrolled_end ? (int64_t)(int32_t)(uint32_t)(uint64_t)(p0 + p1) : p0 + p1;
+        }
+        dst[(uint64_t)cur.f * B + n] = (int16_t)ssat16((int32_t)(acc >> 15));
+      }
+    } else if (1024 * wid < cur.count) {
+      const uint4* img = image + (size_t)cur.d * KS * 3 * 64 + L;
+      i32x16 a16 = {}, a15 = {}, a8 = {}, a7 = {}, a0 = {};
+      const int mb = 1024 * wid + 32 * i + 16 * h;      // window byte of this lane at ks = 0 (column j = i)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const uint4 ua = img[(ks * 3 + 0) * 64], ub = img[(ks * 3 + 1) * 64], uc = img[(ks * 3 + 2) * 64];
+        const i32x4 ca = i32x4{(int)ua.x, (int)ua.y, (int)ua.z, (int)ua.w};
+        const i32x4 cb = i32x4{(int)ub.x, (int)ub.y, (int)ub.z, (int)ub.w};
+        const i32x4 cc = i32x4{(int)uc.x, (int)uc.y, (int)uc.z, (int)uc.w};
+        const int a = fm_swz(mb + 32 * ks);
+        const i32x4 xh = *reinterpret_cast<const i32x4*>(ph + a);
+        const i32x4 xl = *reinterpret_cast<const i32x4*>(pl + a);
+        a16 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ca, xh, a16, 0, 0, 0);
+        a15 = __builtin_amdgcn_mfma_i32_32x32x32_i8(cb, xh, a15, 0, 0, 0);
+        a8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(cc, xh, a8, 0, 0, 0);
+        a8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ca, xl, a8, 0, 0, 0);
+        a7 = __builtin_amdgcn_mfma_i32_32x32x32_i8(cb, xl, a7, 0, 0, 0);
+        a0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(cc, xl, a0, 0, 0, 0);
+      }
+      // lane (j = L & 31, h), register 4q + e -> output 8q + 4h + e of block j
+      const int j = L & 31;
+      int16_t* yb = dst + (uint64_t)cur.f * B + cur.n0 + 1024 * wid + 32 * j + 4 * h;
+      const int ob = 1024 * wid + 32 * j + 4 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        int16_t y[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int g = 4 * q + e;
+          const int64_t S = ((int64_t)a16[g] << 16) + ((int64_t)a15[g] << 15) + ((int64_t)a8[g] << 8) +
+                            ((int64_t)a7[g] << 7) + (int64_t)a0[g] + corr;
+          y[e] = (int16_t)ssat16((int32_t)(S >> 15));
+        }
+        const int o = ob + 8 * q;
+        if (o + 4 <= cur.count && ((((uintptr_t)(yb + 8 * q)) & 7) == 0)) {
+          *reinterpret_cast<uint2*>(yb + 8 * q) = *reinterpret_cast<const uint2*>(y);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (o + e < cur.count) yb[8 * q + e] = y[e];
+        }
+      }
+    }
+    if (nxt >= items) break;
+    it = nxt;
+    cur = next;
+  }
+}
+
+// true: launched (numTaps even, 2 .. 160, enough work to fill the chip); false: not this path
+bool fir_q15_mfma_launch(const int16_t* coeffs, int T, const int16_t* src, int16_t* dst, uint32_t B,
+                         uint32_t batch, const int16_t* hist_in, hipStream_t st) {
+  if (!MI355X_FIR_Q15_MFMA || T < 2 || (T & 1) || T > 32 * kFmMaxKS - 32 || B == 0 || batch == 0) return false;
+  const uint32_t nchunks = (B + kFmChunk - 1) / kFmChunk;
+  const uint64_t items = (uint64_t)nchunks * batch;
+  if (items < 256 || items > 0x7fffffffull) return false;
+  const int ks = (T + 32 + 31) / 32;
+  // the coefficient image (2 shifts x KS steps x 3 planes x 64 lanes x 16 B) and [sum, wrap]
+  const size_t img_bytes = (size_t)2 * ks * 3 * 64 * 16;
+  void* buf = nullptr;
+  if (hipMallocAsync(&buf, img_bytes + 16, st) != hipSuccess) return false;
+  uint4* img = (uint4*)buf;
+  int* info = (int*)((char*)buf + img_bytes);
+  hipLaunchKernelGGL(fir_q15_coef_image_kernel, dim3(1), dim3(64), 0, st, coeffs, T, ks, img, info);
+#define FM_CASE(K)                                                                                              \
+  case K: {                                                                                                     \
+    const int g = persistent_grid((const void*)fir_q15_mfma_kernel<K>, 256, 0, items);                         \
+    hipLaunchKernelGGL(fir_q15_mfma_kernel<K>, dim3(g), dim3(256), 0, st, coeffs, T, src, dst, B, hist_in,       \
+                       nchunks, (uint32_t)items, (const uint4*)img, (const int*)info);                          \
+    break;                                                                                                      \
+  }
+  switch (ks) {
+    FM_CASE(2)
+    FM_CASE(3)
+    FM_CASE(4)
+    FM_CASE(5)
+    FM_CASE(6)
+    default:
+      (void)hipFreeAsync(buf, st);
+      return false;
+  }
+#undef FM_CASE
+  (void)hipFreeAsync(buf, st);
+  return true;
+}
+
+}  // namespace mi355x

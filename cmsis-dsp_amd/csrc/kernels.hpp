@@ -113,6 +113,10 @@ enum FirKind { kFirF32 = 0, kFirQ15 = 1, kFirQ31 = 2, kFirFastQ15 = 3, kFirFastQ
                kFirF32Fma = 6 };   // kFirF32Fma: the opt-in fused-multiply-add f32 path (tolerance)
 // done / seq (the synchronous drop-in): when the pass ends in one workgroup it also stores seq into
 // the completion word done (runtime.cpp done_slot) and sets *flagged.
+// arm_fir_q15 on the i8 matrix cores (fir_mfma.hip): false when the shape is not its (the caller
+// then runs fir_q15_kernel)
+bool fir_q15_mfma_launch(const int16_t* coeffs, int T, const int16_t* src, int16_t* dst, uint32_t B, uint32_t batch,
+                         const int16_t* hist_in, hipStream_t st);
 hipError_t fir_run(int kind, const void* coeffs, int num_taps, const void* src, void* dst, uint32_t block_size,
                    uint32_t batch, void* hist, hipStream_t st, uint32_t* done = nullptr, uint32_t seq = 0,
                    bool* flagged = nullptr);

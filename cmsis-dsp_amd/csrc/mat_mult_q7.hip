@@ -293,6 +293,279 @@ __global__ __launch_bounds__(kQ7NT, kQ7BN == 128 ? 2 : 1) void mat_mult_q7_kerne
   q7_epilogue<FULL>(acc, lds, C, M, N, row0, col0, wm, wn, vecB);
 }
 
+// ============================================================================================
+// Whole tiles (M, N multiples of 256, K of 64, 16-B aligned): the ping-pong K loop.
+//
+// The kernel above keeps all 8 waves in lockstep -- every wave reads its fragments, then every wave
+// issues its MFMAs, then all meet at the barrier -- so on each SIMD the two waves wait for LDS at
+// the same time and the matrix core idles while they do (MFMA busy 0.37-0.39).  Here the
+// waves form two groups (waves 0-3 and 4-7: one of each on every SIMD, cdna_hip_programming.md
+// "The 256² 8-phase template") that run one barrier apart: between two consecutive workgroup
+// barriers one group issues the 16 MFMAs of its current K chunk while the other reads the next
+// chunk's fragments and issues the LDS-DMA of a later chunk, then they swap.  So each SIMD always
+// has one wave feeding its matrix core while the other waits on LDS, and the barrier never drains
+// the DMA in flight (raw s_barrier; vmcnt counted by hand, never 0 inside the loop).
+//
+// Data: K in chunks of 64 bytes; a ring of FOUR chunk slots (4 x 32 KiB = the whole 128 KiB LDS
+// array), slot = A (256 rows x 64 B, 16-B chunk c of row r at c ^ ((r >> 2) & 3), as above) + B (64
+// k-rows x 256 B, chunk c of k-row k at c ^ 2 (k & 7): every 32-lane half of a transposing read
+// takes 8 k-rows x 2 chunks = the 64 banks once).  global_load_lds_dwordx4 fills 1 KiB of LDS
+// lane-linearly per wave instruction, so both swizzles are applied to the per-lane SOURCE address
+// (16 rows x 64 B per A piece, 4 k-rows x 256 B per B piece; 2 + 2 pieces per wave and chunk).
+//
+// Phase p (chunk p, slot p & 3), per group: L_p = 16 fragment reads of chunk p (inline asm: the
+// compiler neither sees nor waits for them) + the DMA of chunk p + 2 into slot (p + 2) & 3 + a wait
+// until chunk p + 1 has landed (vmcnt(4): chunk p + 2's four pieces may still fly) + barrier;
+// M_p = lgkmcnt(0) (tied to the fragment registers, so no MFMA moves above it) + 16 MFMAs at
+// priority 1 + barrier.  Group 1 starts one barrier late, so barrier-interval 2p + 1 holds group 0's
+// M_p and group 1's L_p, and interval 2p + 2 group 0's L_{p+1} and group 1's M_p.  Ordering:
+//  * RAW: chunk p + 1 is read in L_{p+1} (intervals 2p + 2 / 2p + 3); every wave that loaded a piece
+//    of it waited for it in L_p (intervals 2p / 2p + 1), before barrier 2p + 1, which both readers
+//    pass afterwards -- the wait-then-barrier the LDS-DMA needs (MI355X_MICROARCH.md item 7);
+//  * WAR: slot (p + 2) & 3 last held chunk p - 2, whose reads were issued by interval 2p - 3 and
+//    retired by each reader's lgkmcnt(0) at the start of its M_{p-2} (interval 2p - 2 at the latest);
+//    the refill is issued in L_p, after barrier 2p - 1.
+// Group 0 adds one closing barrier, so both groups have passed the same number when the epilogue
+// reuses the array (every read retired, vmcnt(0) after the last chunk).
+#ifndef MI355X_Q7_PP
+#define MI355X_Q7_PP 1
+#endif
+#ifndef MI355X_Q7_DIAG      // diagnostics (wrong results): 1 = no DMA in the loop, 2 = no fragment reads, 3 = neither
+#define MI355X_Q7_DIAG 0
+#endif
+#ifndef MI355X_Q7_STAMP     // diagnostic: s_memtime stamps (q7_stamp_buf, tools/probes/q7_stamps.hip)
+#define MI355X_Q7_STAMP 0
+#endif
+#ifndef MI355X_Q7_NOEPI
+#define MI355X_Q7_NOEPI 0
+#endif
+#ifndef MI355X_Q7_WGPC      // persistent workgroups per CU (1: the LDS ring takes the whole array)
+#define MI355X_Q7_WGPC 1
+#endif
+
+namespace {
+constexpr int kPPSlot = 32768, kPPB = 16384;           // slot bytes; B region offset in a slot
+__device__ __forceinline__ uint32_t q7_lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+template <int N> __device__ __forceinline__ void q7_wait_vm() {   // s_waitcnt vmcnt(N), N < 16
+  static_assert(N >= 0 && N < 16, "vmcnt");
+  __builtin_amdgcn_s_waitcnt(0xF70 | N);
+}
+}  // namespace
+
+#if MI355X_Q7_STAMP   // diagnostic: s_memtime at every barrier of waves 0 and 4 of workgroups 0-63
+__device__ unsigned long long q7_stamp_buf[64][2][160];
+__device__ unsigned long long q7_stamp_real[64][2][2];   // s_memrealtime (100 MHz) at start / end
+#endif
+
+// Persistent: gridDim.x workgroups (a multiple of 8, at most one per CU) walk the tiles, and the
+// chunk stream runs on across tile boundaries -- the DMA of the next tile's first chunks is in
+// flight under the current tile's last MFMAs, and a tile's output leaves from registers (below)
+// while the other group computes -- so no workgroup start, prologue burst or LDS epilogue sits
+// between two tiles.  Tile order: XCD x (= workgroup % 8) takes the contiguous tile run
+// [x T / 8, (x + 1) T / 8) (T % 8 == 0; else round robin), its G / 8 workgroups striding through it,
+// so the tiles of one matrix run together in one L2 (as the kernel above).
+//
+// Epilogue from registers: block (i, j) of the C^T accumulators leaves lane (r, h) with rows r,
+// columns 8q + 4h .. + 3 in register group q; four saturated bytes pack into one dword D_q, and two
+// v_permlane32_swap (D0 <-> D2, D1 <-> D3: lanes 32-63 of the first with lanes 0-31 of the
+// second) leave lane (r, h) with columns 16h .. 16h + 15 of row r, one 16-B store.  The stores count
+// in vmcnt: every counted wait below names the LOADS allowed in flight, which stays correct with
+// stores outstanding (they only add to the count).
+__global__ __launch_bounds__(512, 1) void mat_mult_q7_pp_kernel(const int8_t* __restrict__ A, const int8_t* __restrict__ B,
+                                                                int8_t* __restrict__ C, int M, int K, int N,
+                                                                uint32_t T) {
+  __shared__ __attribute__((aligned(1024))) int8_t lds[4 * kPPSlot];
+  const int tilesN = N / 256, tpm = tilesN * (M / 256);
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  // this workgroup's tiles: first, stride, count
+  uint32_t t_first, t_stride, n_t;
+  if (T % 8 == 0 && G % 8 == 0) {
+    const uint32_t per = T / 8, j = b / 8, gx = G / 8;
+    t_first = (b % 8) * per + j;
+    t_stride = gx;
+    n_t = j < per ? (per - j + gx - 1) / gx : 0;
+  } else {
+    t_first = b;
+    t_stride = G;
+    n_t = b < T ? (T - b + G - 1) / G : 0;
+  }
+  const int tid = threadIdx.x, L = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: SGPR arithmetic, scalar branches
+  const int wm = wid >> 2, wn = wid & 3;                // wave tile: rows 128 wm .., cols 64 wn ..
+  const int r = L & 31, h = L >> 5, li = L & 15, gq = (L >> 4) & 1;
+#if MI355X_Q7_STAMP
+  const bool stamp = b < 64 && (wid == 0 || wid == 4) && L == 0;
+  int ns = 0;
+  auto STAMP = [&]() {
+    if (stamp && ns < 160) q7_stamp_buf[b][wid >> 2][ns] = __builtin_amdgcn_s_memtime();
+    ++ns;
+  };
+#else
+  auto STAMP = [&]() {};
+#endif
+
+  // ---- per-lane DMA offsets (the tile base is added per issue) and LDS destinations
+  const size_t aLane = (size_t)(32 * wid + (L >> 2)) * K + 16 * ((L & 3) ^ ((L >> 4) & 3));
+  const size_t aPiece = (size_t)16 * K;                 // piece 2w + 1: 16 rows further, same swizzle
+  const size_t bLane0 = (size_t)(8 * wid + (L >> 4)) * N + 16 * ((L & 15) ^ (2 * (L >> 4)));
+  const size_t bLane1 = (size_t)(8 * wid + 4 + (L >> 4)) * N + 16 * ((L & 15) ^ (2 * (4 + (L >> 4))));
+  const int nc = K / 64;
+  const uint32_t total = n_t * (uint32_t)nc;            // chunks this workgroup streams
+  // issue cursor: chunk `ic` of tile number `it` (0-based within this workgroup's list)
+  uint32_t it = 0;
+  int ic = 0;
+  const int8_t* aTile = nullptr;
+  const int8_t* bTile = nullptr;
+  auto tile_bases = [&](uint32_t k) {                    // k-th tile of this workgroup
+    const uint32_t t = t_first + k * t_stride;
+    const uint32_t bz = t / (uint32_t)tpm, tt = t % (uint32_t)tpm;
+    const int row0 = (int)(tt / (uint32_t)tilesN) * 256, col0 = (int)(tt % (uint32_t)tilesN) * 256;
+    aTile = A + (size_t)bz * M * K + (size_t)row0 * K;
+    bTile = B + (size_t)bz * K * N + col0;
+  };
+  auto piece = [&](uint32_t g, int q) {                 // DMA piece q (A 0, A 1, B 0, B 1) of chunk g
+#if MI355X_Q7_DIAG == 1 || MI355X_Q7_DIAG >= 3          // diagnostic only: no DMA past the prologue
+    if (g > 2) return;
+#endif
+    if (ic == 0 && q == 0) tile_bases(it);
+    int8_t* sl = lds + (g & 3) * kPPSlot + (q < 2 ? 0 : kPPB) + 2048 * wid + 1024 * (q & 1);
+    const int8_t* src = q < 2 ? aTile + (size_t)64 * ic + aLane + (q ? aPiece : 0)
+                              : bTile + (size_t)64 * ic * N + (q == 2 ? bLane0 : bLane1);
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)sl, 16, 0, 0);
+    if (q == 3 && ++ic == nc) { ic = 0; ++it; }
+  };
+  auto issue_next = [&](uint32_t g) {                   // chunk g of the stream into slot g & 3
+    piece(g, 0); piece(g, 1); piece(g, 2); piece(g, 3);
+  };
+
+  // ---- fragment read bases (slot 0): A block i adds 2048 i, B k-step kk adds 8192 kk, the hi
+  // 8 k-rows of a transposing read 2048
+  const uint32_t lb = q7_lds_addr(lds);
+  const int arow = 128 * wm + r;
+  const uint32_t aK0 = lb + arow * 64 + 16 * ((0 + h) ^ ((r >> 2) & 3));
+  const uint32_t aK1 = lb + arow * 64 + 16 * ((2 + h) ^ ((r >> 2) & 3));
+  const int bkr = 16 * h + (li >> 1);
+  const uint32_t bJ0 = lb + kPPB + bkr * 256 + 16 * ((4 * wn + 0 + gq) ^ (2 * (bkr & 7))) + 8 * (li & 1);
+  const uint32_t bJ1 = lb + kPPB + bkr * 256 + 16 * ((4 * wn + 2 + gq) ^ (2 * (bkr & 7))) + 8 * (li & 1);
+
+  i32x16 acc[4][2];
+  i32x4 fa[2][4] = {};
+  v2i32 fl[2][2] = {}, fh[2][2] = {};                   // B fragments: [kk][j] lo / hi 8 k-rows
+
+#define Q7A(dst, base, off) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(off))
+#define Q7B(dst, base, off) asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(off))
+  auto read_frags = [&](uint32_t so) {
+#if MI355X_Q7_DIAG >= 2                                 // diagnostic only: no fragment reads
+    return;
+#endif
+    const uint32_t a0 = aK0 + so, a1 = aK1 + so, b0 = bJ0 + so, b1 = bJ1 + so;
+    Q7A(fa[0][0], a0, 0); Q7A(fa[0][1], a0, 2048); Q7A(fa[0][2], a0, 4096); Q7A(fa[0][3], a0, 6144);
+    Q7B(fl[0][0], b0, 0); Q7B(fh[0][0], b0, 2048); Q7B(fl[0][1], b1, 0); Q7B(fh[0][1], b1, 2048);
+    Q7A(fa[1][0], a1, 0); Q7A(fa[1][1], a1, 2048); Q7A(fa[1][2], a1, 4096); Q7A(fa[1][3], a1, 6144);
+    Q7B(fl[1][0], b0, 8192); Q7B(fh[1][0], b0, 10240); Q7B(fl[1][1], b1, 8192); Q7B(fh[1][1], b1, 10240);
+  };
+#undef Q7A
+#undef Q7B
+  auto wait_frags = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fa[0][2]), "+v"(fa[0][3]), "+v"(fa[1][0]), "+v"(fa[1][1]),
+                   "+v"(fa[1][2]), "+v"(fa[1][3]), "+v"(fl[0][0]), "+v"(fh[0][0]), "+v"(fl[0][1]), "+v"(fh[0][1]),
+                   "+v"(fl[1][0]), "+v"(fh[1][0]), "+v"(fl[1][1]), "+v"(fh[1][1]));
+  };
+  auto fb = [&](int kk, int j) { return i32x4{fl[kk][j].x, fl[kk][j].y, fh[kk][j].x, fh[kk][j].y}; };
+  auto mma = [&](bool first) {
+    if (first) {                                        // a tile's first chunk: C operand 0
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb(0, j), fa[0][i], i32x16{}, 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb(0, j), fa[0][i], acc[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb(1, j), fa[1][i], acc[i][j], 0, 0, 0);
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    STAMP();
+  };
+  auto store_tile = [&](uint32_t k) {                   // (q7)__SSAT(acc >> 7, 8), from registers
+#if MI355X_Q7_NOEPI                                     // diagnostic only: no output stores
+    if (acc[0][0][0] != 0x7fffffff) return;
+#endif
+    const uint32_t t = t_first + k * t_stride;
+    const uint32_t bz = t / (uint32_t)tpm, tt = t % (uint32_t)tpm;
+    const int row0 = (int)(tt / (uint32_t)tilesN) * 256, col0 = (int)(tt % (uint32_t)tilesN) * 256;
+    int8_t* c = C + (size_t)bz * M * N + (size_t)(row0 + 128 * wm + r) * N + col0 + 64 * wn + 16 * h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        // (q7)__SSAT(x >> 7, 8) = high byte of sat16(2x): |x| < 2^30 (K <= 65535), so 2x does not
+        // wrap; in [-2^14, 2^14) the high byte of 2x is x >> 7, above / below it sat16 gives 0x7fff /
+        // 0x8000.  v_cvt_pk_i16_i32 saturates two words, one v_perm_b32 takes the four high bytes.
+        uint32_t d[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const auto lo = __builtin_amdgcn_cvt_pk_i16(acc[i][j][4 * q] << 1, acc[i][j][4 * q + 1] << 1);
+          const auto hi = __builtin_amdgcn_cvt_pk_i16(acc[i][j][4 * q + 2] << 1, acc[i][j][4 * q + 3] << 1);
+          d[q] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi), __builtin_bit_cast(uint32_t, lo), 0x07050301u);
+        }
+        const auto s02 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+        const auto s13 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+        *reinterpret_cast<uint4*>(c + (size_t)(32 * i) * N + 32 * j) = make_uint4(s02[0], s02[1], s13[0], s13[1]);
+      }
+  };
+
+  if (total == 0) return;                               // (uniform per workgroup: no barrier skipped)
+#if MI355X_Q7_STAMP
+  if (stamp) q7_stamp_real[b][wid >> 2][0] = __builtin_amdgcn_s_memrealtime();
+#endif
+  STAMP();
+  issue_next(0);
+  if (total > 1) { issue_next(1); q7_wait_vm<4>(); } else q7_wait_vm<0>();
+  barrier();                                            // chunk 0 landed for every wave
+  if (wm) barrier();                                    // group 1 runs one barrier behind
+  uint32_t k = 0;                                       // tile being computed
+  int p = 0;                                            // its chunk
+  for (uint32_t g = 0; g < total; ++g) {
+    read_frags((uint32_t)((g & 3) * kPPSlot));
+    if (g + 2 < total) {
+      issue_next(g + 2);
+      q7_wait_vm<4>();                                  // chunk g + 1 landed (g + 2 may fly)
+    } else {
+      q7_wait_vm<0>();
+    }
+    barrier();
+    wait_frags();
+    __builtin_amdgcn_s_setprio(1);
+    mma(p == 0);
+#if MI355X_Q7_DIAG == 4                                 // diagnostic only: 32 MFMAs per segment
+    mma(false);
+#endif
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    if (++p == nc) {                                    // the tile's last chunk: its output leaves
+      store_tile(k);
+      p = 0;
+      ++k;
+    }
+  }
+  if (!wm) barrier();                                   // both groups: the same barrier count
+#if MI355X_Q7_STAMP
+  if (stamp) q7_stamp_real[b][wid >> 2][1] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
+
 hipError_t mat_mult_q7_launch(int m, int k, int n, const int8_t* a, const int8_t* b, int8_t* c, uint32_t batch,
                               hipStream_t st) {
   if (batch == 0 || m == 0 || n == 0) return hipSuccess;
@@ -302,6 +575,21 @@ hipError_t mat_mult_q7_launch(int m, int k, int n, const int8_t* a, const int8_t
   const bool full = m % kQ7BM == 0 && n % kQ7BN == 0 && k % kQ7KT == 0 && ((uintptr_t)a & 15) == 0 &&
                     ((uintptr_t)b & 15) == 0 && ((uintptr_t)c & 15) == 0;
   const dim3 grid((uint32_t)(tiles * batch));
+  if (MI355X_Q7_PP && kQ7BN == 256 && m % 256 == 0 && n % 256 == 0 && k % 64 == 0 && ((uintptr_t)a & 15) == 0 &&
+      ((uintptr_t)b & 15) == 0 && ((uintptr_t)c & 15) == 0 && ((size_t)n & 15) == 0) {
+    // one persistent workgroup per CU (128 KiB of LDS each), a multiple of 8 so every XCD gets
+    // the same number; never more than the tiles
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      int v = 0;
+      if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
+    }
+    const uint64_t T = tiles * batch;
+    uint32_t g = (uint32_t)std::min<uint64_t>(T, (uint64_t)(cus / 8) * 8 * MI355X_Q7_WGPC);
+    if (g >= 8) g -= g % 8;
+    hipLaunchKernelGGL(mat_mult_q7_pp_kernel, dim3(g), dim3(512), 0, st, a, b, c, m, k, n, (uint32_t)T);
+    return hipGetLastError();
+  }
   if (full)
     hipLaunchKernelGGL(mat_mult_q7_kernel<true>, grid, dim3(kQ7NT), 0, st, a, b, c, m, k, n);
   else

@@ -121,6 +121,42 @@ def test_fir_batch_bitexact_two_calls(dsp, torch_gpu, ref, kind, taps, block):
         assert hist[f].tobytes() == state[:taps - 1].tobytes()
 
 
+@pytest.mark.parametrize("taps,block,fill", [(128, 4096, None), (2, 4096, None), (8, 1000, "min"), (64, 4100, "mixed"),
+                                             (130, 2049, None), (158, 4096, "max"), (160, 8195, None),
+                                             (128, 4096, "min"), (16, 4096, "wrap")])
+def test_fir_q15_mfma_path(dsp, torch_gpu, ref, taps, block, fill):
+    """arm_fir_q15 through the i8-MFMA kernel (fir_mfma.hip: even numTaps <= 160 and >= 256
+    (filter, 4096-output chunk) items per call): 260 filters, two calls each (state carry), every
+    word of 12 filters against the reference build -- random full range, all -32768 / 32767 (the
+    plane sums at their extremes, the output saturating), mixed extremes, and taps holding a
+    (-32768, -32768) pair over all -32768 input (the __SMLALD pair wrap: the kernel's exact pair-wise
+    path)."""
+    rng = np.random.default_rng(taps * 31 + block)
+    batch = 260
+    if fill == "min" or fill == "wrap":
+        coeffs = rng.integers(-32768, 32767, taps, endpoint=True).astype(np.int16)
+        if fill == "wrap":
+            coeffs[4:6] = -32768
+        mk = lambda: np.full(block, -32768, np.int16)
+    elif fill == "max":
+        coeffs = np.full(taps, 32767, np.int16)
+        mk = lambda: np.full(block, 32767, np.int16)
+    elif fill == "mixed":
+        vals = np.array([-32768, 32767, 0, -1, 1], np.int16)
+        coeffs = rng.choice(vals, taps)
+        mk = lambda: rng.choice(vals, block)
+    else:
+        coeffs = rng.integers(-32768, 32767, taps, endpoint=True).astype(np.int16)
+        mk = lambda: rng.integers(-32768, 32767, block, endpoint=True).astype(np.int16)
+    blocks = [[mk() for _ in range(2)] for _ in range(batch)]
+    got, hist = _fir_batched(dsp, torch_gpu, "q15", coeffs, blocks)
+    for f in (0, 1, 7, 63, 64, 100, 128, 129, 200, 255, 258, 259):
+        want, state = ref.fir("q15", coeffs, blocks[f])
+        for k in range(2):
+            assert got[k][f].tobytes() == want[k].tobytes(), (f, k, np.argwhere(got[k][f] != want[k])[:4])
+        assert hist[f].tobytes() == state[:taps - 1].tobytes()
+
+
 def test_fir_q15_pairwrap_extreme(dsp, torch_gpu, ref):
     """All -32768 input and taps: the __SMLALD pair sum wraps in int32 on the unrolled
     outputs but not on the blockSize%4 tail (arm_fir_q15.c:482-640 vs :649-681)."""
@@ -510,6 +546,10 @@ def _q7_exact(a, b):
                                         (17, 65535, 19, None), (130, 65, 129, "min"),
                                         # whole 256 x 256 tiles, K % 64 == 0: the unguarded kernel
                                         (256, 64, 256, None), (256, 320, 512, "mixed"), (512, 128, 256, "max"),
+                                        # the ping-pong kernel: 1, 2, 3 chunks (prologue / ring edges), a
+                                        # deep ring, extremes through every slot
+                                        (256, 192, 256, None), (768, 4096, 512, None), (512, 4032, 256, "min"), (256, 256, 512, "min"),
+                                        (256, 1216, 768, "max"),
                                         # K % 16 == 0 but not % 64, ragged N: vector loads with a tail
                                         (256, 80, 272, None)])
 def test_mat_mult_q7_bitexact(dsp, torch_gpu, ref, m, k, n, fill):
@@ -571,3 +611,25 @@ def test_mat_mult_q7_batch_and_multi(dsp, torch_gpu, ref):
     s = np.matmul(a.astype(np.int32), b.astype(np.int32))
     want = np.clip(s >> 7, -128, 127).astype(np.int8)
     assert Cm.cpu().numpy().tobytes() == want.tobytes()
+
+
+def test_mat_mult_q7_pingpong_repeatable(dsp, torch_gpu):
+    """The ping-pong kernel's LDS ordering (DMA wait + barrier before a read, refill two phases
+    after the last read) screened by repetition: 1024^3 x 16 (one workgroup per CU) run six times
+    must give the same words every time, and two of the matrices the exact int64 products."""
+    torch = torch_gpu
+    rng = np.random.default_rng(61)
+    a = rng.integers(-128, 128, (16, 1024, 1024)).astype(np.int8)
+    b = rng.integers(-128, 128, (16, 1024, 1024)).astype(np.int8)
+    A, B = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+    Cm = torch.empty((16, 1024, 1024), dtype=torch.int8, device="cuda")
+    dsp.mat_mult_batch(A, B, Cm)
+    first = Cm.clone()
+    for _ in range(5):
+        Cm.fill_(0)
+        dsp.mat_mult_batch(A, B, Cm)
+        assert torch.equal(Cm, first)
+    got = first.cpu().numpy()
+    for i in (0, 11):
+        s = np.matmul(a[i].astype(np.int32), b[i].astype(np.int32))
+        assert got[i].tobytes() == np.clip(s >> 7, -128, 127).astype(np.int8).tobytes(), i

@@ -250,7 +250,8 @@ def test_rfft_fixed_device_tables_written_on_the_call_stream(dsp, torch_gpu, ref
         want = []
         for r in range(batch):
             out = np.zeros(n if ifft else 2 * n, dtype=dt)
-            ref.fn(f"arm_rfft_{kind}")(C.byref(Sr), x[r].copy().ctypes.data, out.ctypes.data)
+            src = x[r].copy()                             # alive for the call
+            ref.fn(f"arm_rfft_{kind}")(C.byref(Sr), src.ctypes.data, out.ctypes.data)
             want.append(out)
         s = torch.from_numpy(x.copy()).cuda()
         d = torch.zeros((batch, n if ifft else 2 * n), dtype=s.dtype, device="cuda")
