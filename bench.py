@@ -827,11 +827,19 @@ def main_rank(args):
             line["roofline"]["bytes_moved_per_sample"] = 12
         if args.workload == "rfft_f32_pscratch":
             line["roofline"]["bytes_moved_per_sample"] = 8
-        if args.workload in ("fir_fast_q15", "fir_q15"):
-            # fast: one accumulating v_dot2 per tap pair; exact: one v_dot2 per tap (h/l planes)
-            valu = units * n / (2 if args.workload == "fir_fast_q15" else 1) / (kern_ms * 1e-3) * 1e-12
-            line["roofline"]["valu_tops_dot2"] = {"achieved": round(valu, 2), "peak": FP32_NOFMA_TFLOPS,
-                                                  "frac": round(valu / FP32_NOFMA_TFLOPS, 4)}
+        if args.workload == "fir_fast_q15":
+            # one accumulating v_dot2 per tap pair per output; v_dot2_i32_i16 issues at half rate:
+            # 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T lane-instr/s (op_rate.txt measures 36.4)
+            valu = units * n / 2 / (kern_ms * 1e-3) * 1e-12
+            line["roofline"]["valu_dot2"] = {"achieved": round(valu, 2), "peak": 39.3, "unit": "T v_dot2 lane-instr/s",
+                                             "frac": round(valu / 39.3, 4)}
+        if args.workload == "fir_q15":
+            # fir_mfma.hip: per 1024 outputs 6 i8 plane products of a 32 x 32 x (32 KS) MFMA tile, KS =
+            # ceil((numTaps + 32) / 32): the i8 MFMA work the kernel issues against the 5 POPS dense peak
+            ks = (n + 32 + 31) // 32
+            i8 = units / 1024 * 6 * 2 * 32 * 32 * 32 * ks / (kern_ms * 1e-3) * 1e-12
+            line["roofline"]["mfma_i8"] = {"achieved": round(i8, 2), "peak": 5000.0, "unit": "TOPS (i8 MFMA issued)",
+                                           "frac": round(i8 / 5000.0, 4), "k_steps": ks, "plane_products": 6}
         if args.workload == "fir_f32":
             valu = units * n * 2 / (kern_ms * 1e-3) * 1e-12
             line["roofline"]["valu_tflops_nofma"] = {"achieved": round(valu, 2), "peak": FP32_NOFMA_TFLOPS,

@@ -37,6 +37,10 @@
 #include "common.hpp"
 #include "kernels.hpp"
 
+#ifndef MI355X_FIR_Q15_MFMA_WG     // workgroups per CU the register allocation must allow
+#define MI355X_FIR_Q15_MFMA_WG 3
+#endif
+
 namespace mi355x {
 
 namespace {
@@ -84,7 +88,7 @@ __global__ __launch_bounds__(64) void fir_q15_coef_image_kernel(const int16_t* _
 }
 
 template <int KS>
-__global__ __launch_bounds__(256, 2) void fir_q15_mfma_kernel(const int16_t* __restrict__ coeffs, int T,
+__global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kernel(const int16_t* __restrict__ coeffs, int T,
                                                               const int16_t* __restrict__ src, int16_t* __restrict__ dst,
                                                               uint32_t B, const int16_t* __restrict__ hist,
                                                               uint32_t nchunks, uint32_t items,
@@ -92,11 +96,13 @@ __global__ __launch_bounds__(256, 2) void fir_q15_mfma_kernel(const int16_t* __r
                                                               const int* __restrict__ info) {
   __shared__ __attribute__((aligned(16))) uint8_t ph[kFmPlane];
   __shared__ __attribute__((aligned(16))) uint8_t pl[kFmPlane];
+  __shared__ __attribute__((aligned(16))) uint4 imgl[2 * KS * 3 * 64];   // the coefficient image, once per workgroup
   const int tid = threadIdx.x, L = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T1 = T - 1;
   const bool wrap = info[1] != 0;
   const int64_t corr = 128 * (int64_t)info[0];
+  for (int u = tid; u < 2 * KS * 3 * 64; u += 256) imgl[u] = image[u];   // visible after the loop's first barrier
 
   // window word u (samples 2u, 2u + 1 of w) of item `it`, w[m] = s[n0 - d + m], d = parity of the
   // block-input offset so that the words of the block input are 4-byte aligned
@@ -177,7 +183,7 @@ __global__ __launch_bounds__(256, 2) void fir_q15_mfma_kernel(const int16_t* __r
         dst[(uint64_t)cur.f * B + n] = (int16_t)ssat16((int32_t)(acc >> 15));
       }
     } else if (1024 * wid < cur.count) {
-      const uint4* img = image + (size_t)cur.d * KS * 3 * 64 + L;
+      const uint4* img = imgl + cur.d * KS * 3 * 64 + L;
       i32x16 a16 = {}, a15 = {}, a8 = {}, a7 = {}, a0 = {};
       const int mb = 1024 * wid + 32 * i + 16 * h;      // window byte of this lane at ks = 0 (column j = i)
 #pragma unroll
@@ -205,10 +211,12 @@ __global__ __launch_bounds__(256, 2) void fir_q15_mfma_kernel(const int16_t* __r
         int16_t y[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
+          // S = 2^15 X + R with X = 2 a16 + a15 (|X| < 2^23, int32) and R = 2^7 (2 a8 + a7) + a0 +
+          // 128 sum c (int64); S >> 15 = X + (R >> 15) exactly (floor division by 2^15)
           const int g = 4 * q + e;
-          const int64_t S = ((int64_t)a16[g] << 16) + ((int64_t)a15[g] << 15) + ((int64_t)a8[g] << 8) +
-                            ((int64_t)a7[g] << 7) + (int64_t)a0[g] + corr;
-          y[e] = (int16_t)ssat16((int32_t)(S >> 15));
+          const int32_t X = 2 * a16[g] + a15[g];
+          const int64_t R = (int64_t)(2 * a8[g] + a7[g]) * 128 + a0[g] + corr;
+          y[e] = (int16_t)ssat16(X + (int32_t)(R >> 15));
         }
         const int o = ob + 8 * q;
         if (o + 4 <= cur.count && ((((uintptr_t)(yb + 8 * q)) & 7) == 0)) {
