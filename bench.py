@@ -727,6 +727,9 @@ def main_rank(args):
         line["roofline"] = {"bound": "valu", "achieved": round(lane_ops, 2), "peak": 39.3,
                             "unit": "T VALU lane-instr/s (256 CU x 4 SIMD x 16 lanes x 2.4 GHz)",
                             "frac": round(lane_ops / 39.3, 4), "traffic": None, "avg_kernel_ms": round(kern_ms, 4)}
+        vi = valu_issue(args.workload, batch, kern_ms)
+        if vi:
+            line["roofline"]["valu_issue"] = vi
     elif args.workload == "mat_mult_q7":
         ops = 2.0 * n * n * n * batch
         line.update(value=round(total_units * 2.0 * n ** 3 / wall * 1e-12, 4), unit="TOPS (2*M*N*K int MAC)",
@@ -840,6 +843,10 @@ def main_rank(args):
             i8 = units / 1024 * 6 * 2 * 32 * 32 * 32 * ks / (kern_ms * 1e-3) * 1e-12
             line["roofline"]["mfma_i8"] = {"achieved": round(i8, 2), "peak": 5000.0, "unit": "TOPS (i8 MFMA issued)",
                                            "frac": round(i8 / 5000.0, 4), "k_steps": ks, "plane_products": 6}
+        if args.workload in ("fir_q15", "fir_q31", "fir_fast_q15", "fir_fast_q31", "mfcc_q31", "mfcc_q15"):
+            vi = valu_issue(prof, batch, kern_ms)
+            if vi:
+                line["roofline"]["valu_issue"] = vi
         if args.workload == "fir_f32":
             valu = units * n * 2 / (kern_ms * 1e-3) * 1e-12
             line["roofline"]["valu_tflops_nofma"] = {"achieved": round(valu, 2), "peak": FP32_NOFMA_TFLOPS,
@@ -875,6 +882,10 @@ def main_rank(args):
                                                   "algorithmic_bytes_per_launch": biggest * 4096 * qbps,
                                                   "avg_kernel_ms": round(k2, 4)},
                       "parity": p2}
+            if args.global_batch == 1 << 20:
+                vi = valu_issue(f"cfft_{qk}_4096_strong1M", biggest, k2)
+                if vi:
+                    c3[qk]["roofline"]["valu_issue"] = vi
         if args.scatter:
             for qk in ("q31", "q15"):
                 c3[qk]["scatter"] = run_scatter(qk, 4096)
@@ -952,6 +963,23 @@ def pmc_field(name, field, launch_items=None):
     if launch_items is not None and items != launch_items:
         return None
     return rec.get(field)
+
+
+def valu_issue(name, launch_items, kern_ms):
+    """Compute roofline of a VALU-issue-bound kernel from the committed PMC record `name`:
+    SQ_INSTS_VALU per launch x the kernel's issue cycles per VALU instruction (full rate 2, half
+    rate 4, transcendental 8 cycles per wave64 instruction, classes from its hottest loop's ISA,
+    tools/profile_collect.py) against 256 CU x 4 SIMD x 2.4 GHz issue cycles per second, over
+    this run's live kernel time."""
+    cyc = pmc_field(name, "valu_issue_cycles_per_launch", launch_items)
+    if cyc is None or not kern_ms:
+        return None
+    peak = 256 * 4 * 2.4e9
+    ach = cyc / (kern_ms * 1e-3)
+    return {"valu_insts_per_launch": pmc_field(name, "valu_insts_per_launch", launch_items),
+            "issue_cycles_per_launch": round(cyc), "achieved": round(ach * 1e-12, 4), "peak": round(peak * 1e-12, 4),
+            "unit": "T SIMD issue cycles/s (256 CU x 4 SIMD x 2.4 GHz)", "frac": round(ach / peak, 4),
+            "source": pmc_field(name, "source", launch_items)}
 
 
 def pmc_traffic(name, launch_items=None):

@@ -159,7 +159,13 @@ __global__ __launch_bounds__(kBlock) void rfft_fused_kernel(const float2* src, f
 // workgroup: T1 433, T2 473, T4 460, T8 462, T2 x 4 waves 442; the generic fused kernel 441.
 // T: MI355X_RF1024_T when p receives the inner CFFT output (12 B per sample), MI355X_RF1024_TS with
 // ARM_MI355X_RFFT_P_SCRATCH (8 B per sample): round-5 sweep on one box, Gsamples/s with p as
-// scratch: T1 545, T2 606, T4 632, T8 644.
+// scratch: T1 545, T2 606, T4 632, T8 644 (twiddles in 44 registers: 110-128 VGPRs, 4 waves per SIMD).
+// Round 6: an out-of-place 4 KiB-record stream runs 6.0 TB/s with ONE transform per wave and 5.1 with
+// eight (tools/probes/hbm_oop.hip, profiles/r06/probe_hbm_oop.txt); with the twiddles read from a
+// workgroup LDS copy at each use (MI355X_RF1024_TWLDS: 77-88 VGPRs, 5 waves per SIMD) short waves pay
+// no per-wave register preload.  Sweep on one box (Gsamples/s, P_SCRATCH / p kept), WPB x TS/T:
+// registers 8 x 8/2 650/469; LDS 8 x 8/2 640/458, 4 x 8/2 650/469, 2 x 8/2 651/484, 8 x 1/1 727/426,
+// 4 x 1/1 727/477, 4 x 2/2 744/461, 4 x 2/2 strided 737/467, 2 x 1/1 645/489, 16 x 1/1 644/440.
 constexpr int kRfWpb = MI355X_RF1024_WPB;
 __device__ __forceinline__ int rf_s(int e) { return (e >> 6) * 72 + (((e >> 3) & 7) << 3) + ((e & 7) ^ ((e >> 3) & 7)); }
 __device__ __forceinline__ void rf_wave_sync() {
@@ -173,22 +179,40 @@ __device__ __forceinline__ void rf_st(float2* p, float2 v) {
 }
 
 template <int kRfT, bool KEEP_P>
-__global__ __launch_bounds__(64 * kRfWpb) void rfft1024_fwd_kernel(float2* p, float2* __restrict__ out,
+#if MI355X_RF1024_WPE
+#define MI355X_RF1024_ATTR __attribute__((amdgpu_waves_per_eu(MI355X_RF1024_WPE)))
+#else
+#define MI355X_RF1024_ATTR
+#endif
+__global__ __launch_bounds__(64 * kRfWpb) MI355X_RF1024_ATTR void rfft1024_fwd_kernel(float2* p, float2* __restrict__ out,
                                                                    uint32_t batch, const float2* __restrict__ tw,
                                                                    const float2* __restrict__ twr) {
   __shared__ __attribute__((aligned(16))) float2 lds_all[kRfWpb][8 * 72];
   const int l = threadIdx.x & 63;
   float2* lds = lds_all[threadIdx.x >> 6];
-  const uint32_t wave = blockIdx.x * kRfWpb + (threadIdx.x >> 6);
-  const uint32_t t_begin = wave * kRfT, t_end = min(batch, t_begin + kRfT);
-  float2 w0[7], w1[7], ws[8];
+  const uint32_t wave = blockIdx.x * kRfWpb + (threadIdx.x >> 6), n_waves = gridDim.x * kRfWpb;
   const int j1 = l & 7;
+#if MI355X_RF1024_TWLDS
+  // twiddles read from a per-workgroup LDS copy at each use (tw[0, 448): stage 0 and 1, twr[0, 512):
+  // the split) instead of 44 lane-constant registers held across the loop: 110-128 -> fewer VGPRs,
+  // more resident waves and more 4 KiB records in flight per CU
+  __shared__ float2 tw_l[448 + 512];
+  for (int i = threadIdx.x; i < 448 + 512; i += 64 * kRfWpb) tw_l[i] = i < 448 ? tw[i] : twr[i - 448];
+  __syncthreads();
+#else
+  float2 w0[7], w1[7], ws[8];
 #pragma unroll
   for (int m = 0; m < 7; ++m) { w0[m] = tw[(m + 1) * l]; w1[m] = tw[8 * (m + 1) * j1]; }
 #pragma unroll
   for (int m = 0; m < 8; ++m) ws[m] = twr[l + 64 * m];
+#endif
   const int kbin = 8 * (l & 7) + (l >> 3);            // stage-2 output m of lane l is bin kbin + 64 m
-  for (uint32_t t = t_begin; t < t_end; ++t) {
+  for (uint32_t k = 0; k < (uint32_t)kRfT; ++k) {
+    // MI355X_RF1024_STRIDE: wave w takes transforms w, w + W, w + 2W ... (W waves in the grid), so
+    // the waves resident at one time stream neighbouring 4 KiB records (tools/probes/hbm_oop.hip);
+    // else kRfT consecutive transforms per wave
+    const uint32_t t = MI355X_RF1024_STRIDE ? wave + k * n_waves : wave * kRfT + k;
+    if (t >= batch) break;
     float2* X = p + (size_t)t * 512;
     float2 a[8];
 #pragma unroll
@@ -196,6 +220,13 @@ __global__ __launch_bounds__(64 * kRfWpb) void rfft1024_fwd_kernel(float2* p, fl
       const rf_v2f v = __builtin_nontemporal_load(reinterpret_cast<const rf_v2f*>(&X[l + 64 * m]));
       a[m] = make_float2(v.x, v.y);
     }
+#if MI355X_RF1024_TWLDS
+    int lo = l;                                        // opaque per transform: the reads stay in the loop
+    asm volatile("" : "+v"(lo));
+    float2 w0[7], w1[7];
+#pragma unroll
+    for (int m = 0; m < 7; ++m) { w0[m] = tw_l[(m + 1) * lo]; w1[m] = tw_l[8 * (m + 1) * (lo & 7)]; }
+#endif
     r8_sel(a, w0, l != 0);                             // stage 0, arm_cfft_radix8_f32.c:152-174
     rf_wave_sync();                                    // the previous transform's split reads are done
 #pragma unroll
@@ -230,7 +261,11 @@ __global__ __launch_bounds__(64 * kRfWpb) void rfft1024_fwd_kernel(float2* p, fl
         const float t1a = x0.x + x0.x, t1b = x0.y + x0.y;
         o = make_float2(0.5f * (t1a + t1b), 0.5f * (t1a - t1b));
       } else {
+#if MI355X_RF1024_TWLDS
+        const float2 A = lds[rf_s(k)], B = lds[rf_s(512 - k)], w = tw_l[448 + (lo + 64 * m)];
+#else
         const float2 A = lds[rf_s(k)], B = lds[rf_s(512 - k)], w = ws[m];
+#endif
         const float t1a = B.x - A.x, t1b = B.y + A.y;
         const float p0 = w.x * t1a, p1 = w.y * t1a, p2 = w.x * t1b, p3 = w.y * t1b;
         o = make_float2(0.5f * (A.x + B.x + p0 + p3), 0.5f * (A.y - B.y + p1 - p2));

@@ -138,13 +138,22 @@
 
 // ---- rfft_f32.hip
 #ifndef MI355X_RF1024_T
-#define MI355X_RF1024_T 2
+#define MI355X_RF1024_T 1
+#endif
+#ifndef MI355X_RF1024_STRIDE // 1: a wave's transforms are W apart (W = waves in the grid), 0: consecutive
+#define MI355X_RF1024_STRIDE 0
+#endif
+#ifndef MI355X_RF1024_TWLDS  // 1: twiddles from a workgroup LDS copy at each use, 0: held in registers
+#define MI355X_RF1024_TWLDS 1
+#endif
+#ifndef MI355X_RF1024_WPE    // >0: amdgpu_waves_per_eu floor (register budget) of the rfft1024 kernel
+#define MI355X_RF1024_WPE 0
 #endif
 #ifndef MI355X_RF1024_TS     // transforms per wave when p is scratch (ARM_MI355X_RFFT_P_SCRATCH)
-#define MI355X_RF1024_TS 8
+#define MI355X_RF1024_TS 2
 #endif
 #ifndef MI355X_RF1024_WPB
-#define MI355X_RF1024_WPB 8
+#define MI355X_RF1024_WPB 4
 #endif
 #ifndef MI355X_RF1024
 #define MI355X_RF1024 1

@@ -12,7 +12,12 @@ Per workload:
     reads at half, MI355X_MICROARCH.md §HBM, cross-checked with TCC_EA0_RDREQ x 128; write
     = WRITE_SIZE), the effective clock (GRBM_GUI_ACTIVE per XCD over the kernel time) and,
     for MFMA kernels, MFMA busy cycles as a fraction of the SIMD cycles of the launch;
-  * run_kernel_stats.csv — rocprofv3's own --stats summary (all dispatches).
+  * run_kernel_stats.csv — rocprofv3's own --stats summary (all dispatches);
+  * for names whose spec lists source units, a valu_issue record: SQ_INSTS_VALU per launch of each
+    kernel times its issue cycles per VALU instruction, weighted by the instruction classes of
+    that kernel's hottest loop in its device assembly (tools/valu_mix.py on
+    `make -C cmsis-dsp_amd build/<unit>.s`; full rate 2, half rate 4, transcendental 8 cycles per
+    wave64 instruction per SIMD, profiles/r04/probes/op_rate.txt; MFMA issue counted 0).
 pmc_traffic.json keys: the profile name; bench.py uses a record only when its recorded
 bench config equals the line's config.
 Usage: profile_collect.py <round> [name ...]
@@ -22,12 +27,14 @@ import glob
 import json
 import os
 import shutil
+import subprocess
 import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from profile_specs import SPECS  # noqa: E402
+import valu_mix  # noqa: E402
 
 N_XCD, N_SIMD = 8, 1024
 
@@ -102,6 +109,57 @@ def pmc_summary(d, ksub):
     return {name: sum(v) / len(v) for name, v in acc.items()}, gmax
 
 
+_ASM = {}
+
+
+def kernel_asm(unit, kernel_name):
+    """(mangled symbol, body lines) of the kernel whose demangled name (as the trace prints it)
+    is kernel_name, from cmsis-dsp_amd/build/<unit>.s (built on demand)."""
+    if unit not in _ASM:
+        path = os.path.join(ROOT, "cmsis-dsp_amd", "build", f"{unit}.s")
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "cmsis-dsp_amd"), f"build/{unit}.s"], check=True,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        syms = [l.split(":")[0] for l in open(path) if l.startswith("_Z") and ":" in l.split()[0]]
+        dem = subprocess.run(["c++filt"], input="\n".join(syms), capture_output=True, text=True, check=True).stdout
+        _ASM[unit] = (path, dict(zip(dem.strip().split("\n"), syms)))
+    path, table = _ASM[unit]
+    sym = table.get(kernel_name)
+    return (sym, valu_mix.kernel_lines(path, sym)) if sym else (None, None)
+
+
+def valu_issue(d, ksub, units, tr):
+    """Issue cycles of the VALU instructions one launch executes (see the module docstring)."""
+    parts, uparts = ksub.split("|"), units.split("|")
+    out = {"by_kernel": {}, "valu_insts_per_launch": 0.0, "issue_cycles_per_launch": 0.0,
+           "weighting": "hottest-loop instruction classes of the kernel's device assembly: full 2, half 4, "
+                        "trans 8 cycles per wave64 VALU instruction, MFMA 0 (op_rate.txt)"}
+    for part, unit in zip(parts, uparts):
+        pm = pmc_summary(d, part)
+        cand = [k for k in tr if part in k]
+        if not pm or "SQ_INSTS_VALU" not in pm[0] or not cand:
+            return None
+        kname = max(cand, key=lambda k: tr[k]["timed_avg_ms"] * tr[k]["timed_dispatches"])
+        sym, body = kernel_asm(unit, kname)
+        if not body:
+            return None
+        ls = valu_mix.loops(body)
+        whole = valu_mix.mix([l.strip() for l in body if l.startswith("\t")])
+        if ls:
+            pick = max(ls, key=lambda k: sum(1 for t in ls[k] if t.startswith("v_")))
+            mx = valu_mix.mix(ls[pick])
+        else:
+            pick, mx = None, whole
+        nv = mx["full"] + mx["half"] + mx["trans"] + mx["mfma"]
+        cpi = mx["issue_cycles_per_wave"] / nv if nv else 2.0
+        insts = pm[0]["SQ_INSTS_VALU"]
+        out["by_kernel"][kname] = {"symbol": sym, "unit": unit, "loop": pick, "loop_mix": mx,
+                                   "whole_kernel_mix": whole, "cycles_per_valu_inst": round(cpi, 4),
+                                   "valu_insts_per_launch": insts, "issue_cycles_per_launch": insts * cpi}
+        out["valu_insts_per_launch"] += insts
+        out["issue_cycles_per_launch"] += insts * cpi
+    return out
+
+
 def main():
     rnd = sys.argv[1]
     src = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
@@ -155,12 +213,19 @@ def main():
                 p["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cycles
             if line and line.get("roofline", {}).get("algorithmic_bytes_per_launch") and "hbm_bytes_per_launch" in p:
                 p["traffic_over_algorithmic"] = p["hbm_bytes_per_launch"] / line["roofline"]["algorithmic_bytes_per_launch"]
+            units = SPECS[name][2] if len(SPECS[name]) > 2 else ""
+            if units:
+                vi = valu_issue(d, ksub, units, tr)
+                if vi:
+                    p["valu_issue"] = vi
             json.dump(p, open(os.path.join(dest, "pmc.json"), "w"), indent=1)
             rec["pmc"] = {k: v for k, v in p.items() if k != "counters_per_dispatch"}
             if "hbm_bytes_per_launch" in p or "mfma_busy_frac" in p:
                 traffic[name] = {"hbm_bytes_per_launch": round(p.get("hbm_bytes_per_launch", 0)) or None,
                                  "read_bytes": round(p.get("read_bytes", 0)), "write_bytes": round(p.get("write_bytes", 0)),
                                  "mfma_busy_frac": p.get("mfma_busy_frac"), "kernel": rec.get("dominant_kernel", ksub),
+                                 "valu_insts_per_launch": p.get("valu_issue", {}).get("valu_insts_per_launch"),
+                                 "valu_issue_cycles_per_launch": p.get("valu_issue", {}).get("issue_cycles_per_launch"),
                                  "avg_kernel_ms_trace": ms, "bench_config": rec["bench_config"], "round": rnd,
                                  "source": f"profiles/{rnd}/{name}/pmc.json"}
         index[name] = {k: rec.get(k) for k in ("dominant_kernel", "trace_timed_avg_ms", "bench_hip_event_avg_ms",

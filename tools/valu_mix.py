@@ -57,6 +57,8 @@ def loops(body):
         if re.match(r"^\.LBB\w+:", l) or re.match(r"^; %bb", l):
             mm = re.search(r"in Loop: Header=(\w+)", l)
             cur = ("." + "LBB" + mm.group(1)[2:]) if mm else None
+            if cur:
+                out.setdefault(cur, [])   # a loop block laid out before its header
             continue
         if cur and l.startswith("\t") and not l.strip().startswith((";", ".")):
             out[cur].append(l.strip())
