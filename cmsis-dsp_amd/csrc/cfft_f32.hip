@@ -152,14 +152,25 @@ __global__ __launch_bounds__(64 * kN1024Wpb, MI355X_N1024_WAVES) void cfft_f32_n
   const float invL = 1.0f / 1024.0f;
 
   // lane-constant twiddles (arm_cfft_f32.c:909-933; arm_cfft_radix8_f32.c:152-174)
+  const int j1 = l & 7;
+#if MI355X_N1024_TWLDS
+  // read from a workgroup LDS copy of tw[0, 883) at each use instead of 36 registers held across
+  // the loop (the rfft1024 measurement: fewer VGPRs -> more resident waves -> more records in flight).
+  // Here it does not pay (round 6, one box, Gsamples/s / HBM frac): registers 8 waves x T4 381 / 0.764;
+  // LDS 16 x T1 368, 16 x T2 375, 16 x T4 355, 4 x T1 360, 4 x T4 351 -- the 9 KiB per-wave image
+  // already bounds residency (125 VGPRs: 16 waves per CU either way)
+  __shared__ float2 tw_l[896];
+  for (int i = threadIdx.x; i < 896; i += 64 * kN1024Wpb) tw_l[i] = tw[i];
+  __syncthreads();
+#else
   float2 wb[4], w0[7], w1[7];
 #pragma unroll
   for (int i = 0; i < 4; ++i) wb[i] = tw[l + 64 * i];
 #pragma unroll
   for (int m = 0; m < 7; ++m) w0[m] = tw[2 * (m + 1) * l];          // stage 0: j = l, modifier 2
-  const int j1 = l & 7;
 #pragma unroll
   for (int m = 0; m < 7; ++m) w1[m] = tw[16 * (m + 1) * j1];        // stage 1: j = l%8, modifier 16
+#endif
 
 // MI355X_NT: non-temporal loads/stores (the batch is streamed once; -13% without).  A
 // software-pipelined variant (the next transform's loads under phases B/C) was +4% under the
@@ -173,6 +184,17 @@ __global__ __launch_bounds__(64 * kN1024Wpb, MI355X_N1024_WAVES) void cfft_f32_n
   float2 a[8], b[8];
   for (uint32_t t = t_begin; t < t_end; t += t_step) {
     float2* X = data + (size_t)t * 1024;
+#if MI355X_N1024_TWLDS
+    int lo = l;                          // opaque per transform: the table reads stay in the loop
+    asm volatile("" : "+v"(lo));
+    float2 wb[4], w0[7], w1[7];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wb[i] = tw_l[lo + 64 * i];
+#pragma unroll
+    for (int m = 0; m < 7; ++m) w0[m] = tw_l[2 * (m + 1) * lo];
+#pragma unroll
+    for (int m = 0; m < 7; ++m) w1[m] = tw_l[16 * (m + 1) * (lo & 7)];
+#endif
     // ---------------- phase A
 #pragma unroll
     for (int m = 0; m < 8; ++m) { a[m] = LD(&X[l + 64 * m]); b[m] = LD(&X[512 + l + 64 * m]); }

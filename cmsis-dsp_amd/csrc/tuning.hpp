@@ -9,6 +9,9 @@
 #ifndef MI355X_N1024_WAVES
 #define MI355X_N1024_WAVES 1
 #endif
+#ifndef MI355X_N1024_TWLDS  // 1: stage twiddles from a workgroup LDS copy at each use, 0: in registers
+#define MI355X_N1024_TWLDS 0
+#endif
 #ifndef MI355X_N1024_T
 #define MI355X_N1024_T 4
 #endif
