@@ -76,6 +76,23 @@ def trace_summary(d, steps=None):
     return out
 
 
+def merged_timed(d, sub, steps):
+    """Mean duration (ms) of the last `steps` largest-grid dispatches of ALL kernels whose name
+    contains `sub`, in dispatch order: the timed region when one step alternates template
+    instances (configs[3]: forward / inverse), which the per-kernel `steps` cut would mix with
+    warmup dispatches."""
+    v = []
+    for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if sub in row["Kernel_Name"]:
+                v.append((_grid(row), int(row["End_Timestamp"]) - int(row["Start_Timestamp"]), int(row["Start_Timestamp"])))
+    if not v or not steps:
+        return None
+    g = max(x[0] for x in v)
+    big = sorted((x for x in v if x[0] == g), key=lambda x: x[2])[-steps:]
+    return sum(x[1] for x in big) / len(big) * 1e-6
+
+
 def pmc_summary(d, ksub):
     """Per-dispatch counter averages of the kernel(s) matching ksub; "a|b" sums the kernels of a
     multi-launch step (e.g. the MFCC front-end CFFT + post), each averaged over its timed grid."""
@@ -187,9 +204,14 @@ def main():
             pipe = [q for q in tr if "mi355x::" in q and steps and tr[q]["largest_grid_dispatches"] >= steps]
             rec["trace_pipeline_kernels"] = pipe
             rec["trace_pipeline_avg_ms"] = sum(tr[q]["timed_avg_ms"] for q in pipe) if pipe else None
+            if len(dom) > 1 and steps:
+                rec["trace_timed_avg_ms_all_instances"] = merged_timed(d, ksub.split("|")[0], steps)
             if line and line.get("roofline", {}).get("avg_kernel_ms"):
                 rec["bench_hip_event_avg_ms"] = line["roofline"]["avg_kernel_ms"]
                 rec["trace_over_hip_event"] = tr[k]["timed_avg_ms"] / line["roofline"]["avg_kernel_ms"]
+                if rec.get("trace_timed_avg_ms_all_instances"):
+                    rec["trace_all_instances_over_hip_event"] = (rec["trace_timed_avg_ms_all_instances"]
+                                                                 / line["roofline"]["avg_kernel_ms"])
                 if rec["trace_pipeline_avg_ms"]:
                     rec["pipeline_over_hip_event"] = rec["trace_pipeline_avg_ms"] / line["roofline"]["avg_kernel_ms"]
         for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True):
@@ -229,7 +251,8 @@ def main():
                                  "avg_kernel_ms_trace": ms, "bench_config": rec["bench_config"], "round": rnd,
                                  "source": f"profiles/{rnd}/{name}/pmc.json"}
         index[name] = {k: rec.get(k) for k in ("dominant_kernel", "trace_timed_avg_ms", "bench_hip_event_avg_ms",
-                                               "trace_over_hip_event", "trace_pipeline_avg_ms",
+                                               "trace_over_hip_event", "trace_timed_avg_ms_all_instances",
+                                               "trace_all_instances_over_hip_event", "trace_pipeline_avg_ms",
                                                "pipeline_over_hip_event")}
         index[name].update({k: rec.get("pmc", {}).get(k) for k in ("hbm_bytes_per_launch", "traffic_over_algorithmic",
                                                                    "effective_clock_ghz", "mfma_busy_frac")})
