@@ -1094,6 +1094,9 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
       break;
     }
     default: {
+      if (kind == kFirQ31 && fir_q31_mfma_launch((const int32_t*)coeffs, T_, (const int32_t*)src, (int32_t*)dst, B,
+                                                 batch, (const int32_t*)hist_in, st))
+        break;
       auto k = kind == kFirQ31 ? (T_ > kFirMaxTaps ? fir_q31_kernel<false, true> : fir_q31_kernel<false, false>)
                                : (T_ > kFirMaxTaps ? fir_q31_kernel<true, true> : fir_q31_kernel<true, false>);
       hipLaunchKernelGGL(k, dim3(items), dim3(kBlock), 0, st, (const int32_t*)coeffs, T_, (const int32_t*)src,

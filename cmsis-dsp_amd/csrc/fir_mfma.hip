@@ -336,4 +336,282 @@ bool fir_q15_mfma_launch(const int16_t* coeffs, int T, const int16_t* src, int16
   return true;
 }
 
+// =============================================================================================
+// Batched arm_fir_q31 on the i8 matrix cores (round 6), bit-exact.  Replaces the scalar path of
+// Source/FilteringFunctions/arm_fir_q31.c (the q63 accumulator of exact q31 x q31 products,
+// y = (q31)(acc >> 31), :880-1000 LOOPUNROLL and tail alike): acc wraps mod 2^64 in the reference
+// build and y keeps its bits 31 .. 62, so any exact sum order gives the reference's words.
+//
+// Same banded-Toeplitz GEMM as the q15 kernel (d = 0: q31 samples are 4-byte words), with four
+// byte planes per operand:
+//   samples  x = 2^24 x3 + 2^16 x2' + 2^8 x1' + x0' + beta, xi' = byte i - 128 (i < 3), x3 the
+//            signed top byte, beta = 128 (2^16 + 2^8 + 1);
+//   taps     c' = 2^24 d3 + 2^16 d2 + 2^8 d1 + d0, balanced signed digits (each -128 .. 127), which
+//            covers c' in [-2^31, 0x7F7F7F7F]; a tap above that ("big", within 2^-7.98 of +1.0) is
+//            carried as c' = c - 2^31, and 2^31 x (the difference) adds exactly x to y = S >> 31.
+// sum_t x c = sum_{i,j} 2^{8 (i + j)} (x_i' . d_j) + beta sum c'  (+ 2^31 sum over big taps of x):
+// 16 plane products per K step into seven int32 accumulators by shift class i + j (each exact:
+// at most 4 products of |.| <= 128 x 128 x 192), combined in int64 mod 2^64 for the output.
+// Up to kQ31MaxBig big taps are corrected per output from the planes; more take an exact
+// per-output VALU path in the same kernel.
+constexpr int kQ31Words = kFmChunk + 32 * kFmMaxKS;            // window samples staged per item (4288)
+constexpr int kQ31Groups = (kQ31Words + 1023) / 1024;          // 4-sample groups per thread
+constexpr int kQ31Plane = kQ31Words + 256;                     // plane bytes (whole rows + look-ahead)
+constexpr int kQ31MaxBig = 4;
+constexpr int64_t kQ31Beta = 128 * (65536 + 256 + 1);
+
+__device__ __forceinline__ int64_t q31_tap_carried(int32_t c) {   // c' of the tap
+  return c > 0x7F7F7F7F ? (int64_t)c - (int64_t)0x80000000LL : (int64_t)c;
+}
+
+// image[ks][digit][lane]: the 16 digit bytes lane L = (i = L & 31, h = L >> 5) passes as the A operand
+// at K step ks (taps c'[32 ks + 16 h + e - i]); info: [0, 1] sum c' (int64), [2] number of big taps,
+// [3 ..] their indices (first kQ31MaxBig)
+__global__ __launch_bounds__(256) void fir_q31_coef_image_kernel(const int32_t* __restrict__ coeffs, int T, int KS,
+                                                                 uint4* __restrict__ image, int* __restrict__ info) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g < KS * 64) {
+    const int L = g & 63, ks = g >> 6, i = L & 31, h = L >> 5;
+    uint32_t w[4][4] = {};
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int ci = 32 * ks + 16 * h + e - i;
+      int64_t v = (ci >= 0 && ci < T) ? q31_tap_carried(coeffs[ci]) : 0;
+#pragma unroll
+      for (int dgt = 0; dgt < 4; ++dgt) {
+        const int64_t dd = dgt < 3 ? ((v + 128) & 255) - 128 : v;   // balanced digit
+        v = (v - dd) >> 8;
+        w[dgt][e >> 2] |= (uint32_t)(uint8_t)(int8_t)dd << (8 * (e & 3));
+      }
+    }
+#pragma unroll
+    for (int dgt = 0; dgt < 4; ++dgt) image[(ks * 4 + dgt) * 64 + L] = make_uint4(w[dgt][0], w[dgt][1], w[dgt][2], w[dgt][3]);
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x < 64) {   // one wave: sum c' and the big taps in order
+    const int l = threadIdx.x;
+    int64_t sum = 0;
+    int nbig = 0;
+    for (int k0 = 0; k0 < T; k0 += 64) {
+      const int k = k0 + l;
+      const int32_t c = k < T ? coeffs[k] : 0;
+      sum += q31_tap_carried(c);
+      const bool big = c > 0x7F7F7F7F;
+      const uint64_t mask = __ballot(big);
+      if (big) {
+        const int r = nbig + __popcll(mask & ((1ull << l) - 1));
+        if (r < kQ31MaxBig) info[3 + r] = k;
+      }
+      nbig += __popcll(mask);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    if (l == 0) {
+      info[0] = (int)(uint32_t)(uint64_t)sum;
+      info[1] = (int)(uint32_t)((uint64_t)sum >> 32);
+      info[2] = nbig;
+    }
+  }
+}
+
+template <int KS>
+__global__ __launch_bounds__(256, 2) void fir_q31_mfma_kernel(const int32_t* __restrict__ coeffs, int T,
+                                                              const int32_t* __restrict__ src, int32_t* __restrict__ dst,
+                                                              uint32_t B, const int32_t* __restrict__ hist,
+                                                              uint32_t nchunks, uint32_t items,
+                                                              const uint4* __restrict__ image,
+                                                              const int* __restrict__ info) {
+  __shared__ __attribute__((aligned(16))) uint8_t pq[4][kQ31Plane];
+  __shared__ __attribute__((aligned(16))) uint4 imgl[KS * 4 * 64];
+  const int tid = threadIdx.x, L = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T1 = T - 1;
+  const uint64_t k0 = (uint64_t)kQ31Beta * ((uint64_t)(uint32_t)info[0] | ((uint64_t)(uint32_t)info[1] << 32));
+  const int nbig = info[2];
+  int big[kQ31MaxBig];
+#pragma unroll
+  for (int b = 0; b < kQ31MaxBig; ++b) big[b] = b < nbig ? info[3 + b] : 0;
+  for (int u = tid; u < KS * 4 * 64; u += 256) imgl[u] = image[u];   // visible after the loop's first barrier
+
+  struct Item { uint32_t f; int n0, count; };
+  auto item_of = [&](uint32_t it) {
+    Item x;
+    x.f = it / nchunks;
+    x.n0 = (int)(it - x.f * nchunks) * kFmChunk;
+    x.count = min((int)B - x.n0, kFmChunk);
+    return x;
+  };
+  // window sample m = s[n0 + m] (state = [history T1 ; block B], 0 past it): thread tid takes the
+  // four samples 4 (tid + 256 q) + e, each one aligned dword from a clamped, always-valid address
+  uint32_t wv[4 * kQ31Groups];
+  auto load_window = [&](const Item& x) {
+    const int32_t* blk = src + (uint64_t)x.f * B + x.n0 - T1;     // window sample m of the block input: blk[m]
+#pragma unroll
+    for (int q = 0; q < kQ31Groups; ++q) {
+      const int m0 = 4 * (tid + 256 * q), j0 = x.n0 + m0;
+      if (j0 >= T1 && j0 + 3 - T1 < (int)B && m0 + 3 < kQ31Words) {   // the four samples in the block input
+#pragma unroll
+        for (int e = 0; e < 4; ++e) wv[4 * q + e] = (uint32_t)blk[m0 + e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + e, j = j0 + e;
+          const bool in_h = j < T1, in_b = j >= T1 && j - T1 < (int)B;
+          const int32_t* p = in_h ? hist + (uint64_t)x.f * T1 + j : (in_b ? src + (uint64_t)x.f * B + (j - T1) : src);
+          const uint32_t v = (uint32_t)*p;
+          wv[4 * q + e] = (m < kQ31Words && (in_h || in_b)) ? v : 0u;
+        }
+      }
+    }
+  };
+  auto stage_window = [&]() {                            // 4 samples -> one 4-byte word per plane
+#pragma unroll
+    for (int q = 0; q < kQ31Groups; ++q) {
+      const int m = 4 * (tid + 256 * q);
+      if (m >= kQ31Words) continue;
+      const uint32_t s0 = wv[4 * q], s1 = wv[4 * q + 1], s2 = wv[4 * q + 2], s3 = wv[4 * q + 3];
+      const uint32_t u01 = __builtin_amdgcn_perm(s1, s0, 0x05010400u), u23 = __builtin_amdgcn_perm(s3, s2, 0x05010400u);
+      const uint32_t v01 = __builtin_amdgcn_perm(s1, s0, 0x07030602u), v23 = __builtin_amdgcn_perm(s3, s2, 0x07030602u);
+      const int a = fm_swz(m);
+      *reinterpret_cast<uint32_t*>(&pq[0][a]) = __builtin_amdgcn_perm(u23, u01, 0x05040100u) ^ 0x80808080u;
+      *reinterpret_cast<uint32_t*>(&pq[1][a]) = __builtin_amdgcn_perm(u23, u01, 0x07060302u) ^ 0x80808080u;
+      *reinterpret_cast<uint32_t*>(&pq[2][a]) = __builtin_amdgcn_perm(v23, v01, 0x05040100u) ^ 0x80808080u;
+      *reinterpret_cast<uint32_t*>(&pq[3][a]) = __builtin_amdgcn_perm(v23, v01, 0x07060302u);
+    }
+  };
+  auto xs = [&](int m) -> int32_t {                      // window sample m from the planes
+    const int a = fm_swz(m);
+    return (int32_t)(((uint32_t)pq[3][a] << 24) | ((uint32_t)(pq[2][a] ^ 0x80u) << 16) |
+                     ((uint32_t)(pq[1][a] ^ 0x80u) << 8) | (uint32_t)(pq[0][a] ^ 0x80u));
+  };
+
+  uint32_t it = blockIdx.x;
+  if (it >= items) return;
+  Item cur = item_of(it);
+  load_window(cur);
+  for (;;) {
+    __syncthreads();                                     // the previous item's reads are done
+    stage_window();
+    __syncthreads();
+    const uint32_t nxt = it + gridDim.x;
+    const Item next = item_of(nxt < items ? nxt : it);
+    if (nxt < items) load_window(next);                  // in flight under this item's MFMAs
+    int32_t* yf = dst + (uint64_t)cur.f * B + cur.n0;
+    if (nbig > kQ31MaxBig) {
+      // exact per-output path (arm_fir_q31.c: q63 sum of exact products, y = acc >> 31)
+      for (int o = tid; o < cur.count; o += 256) {
+        uint64_t acc = 0;
+        for (int t = 0; t < T; ++t) acc += (uint64_t)((int64_t)xs(o + t) * coeffs[t]);
+        yf[o] = (int32_t)(uint32_t)(acc >> 31);
+      }
+    } else if (1024 * wid < cur.count) {
+      const int i = L & 31, h = L >> 5;
+      const uint4* img = imgl + L;
+      i32x16 c0 = {}, c1 = {}, c2 = {}, c3 = {}, c4 = {}, c5 = {}, c6 = {};
+      const int mb = 1024 * wid + 32 * i + 16 * h;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        i32x4 D[4], P[4];
+        const int a = fm_swz(mb + 32 * ks);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint4 u = img[(ks * 4 + r) * 64];
+          D[r] = i32x4{(int)u.x, (int)u.y, (int)u.z, (int)u.w};
+          P[r] = *reinterpret_cast<const i32x4*>(&pq[r][a]);
+        }
+        c3 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[0], P[3], c3, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[0], P[2], c2, 0, 0, 0);
+        c4 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[1], P[3], c4, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[0], P[1], c1, 0, 0, 0);
+        c3 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[1], P[2], c3, 0, 0, 0);
+        c5 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[2], P[3], c5, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[1], P[1], c2, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[0], P[0], c0, 0, 0, 0);
+        c4 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[2], P[2], c4, 0, 0, 0);
+        c3 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[2], P[1], c3, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[1], P[0], c1, 0, 0, 0);
+        c6 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[3], P[3], c6, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[2], P[0], c2, 0, 0, 0);
+        c5 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[3], P[2], c5, 0, 0, 0);
+        c4 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[3], P[1], c4, 0, 0, 0);
+        c3 = __builtin_amdgcn_mfma_i32_32x32x32_i8(D[3], P[0], c3, 0, 0, 0);
+      }
+      // lane (j = L & 31, h), register 4q + e -> output 8q + 4h + e of block j
+      const int j = L & 31;
+      const int ob = 1024 * wid + 32 * j + 4 * h;
+      int32_t y[16];
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        // S = sum_s 2^{8 s} c_s + beta sum c' (mod 2^64, Horner in int64); y = bits 31 .. 62
+        uint64_t S = (uint64_t)(int64_t)c6[g];
+        S = (S << 8) + (uint64_t)(int64_t)c5[g];
+        S = (S << 8) + (uint64_t)(int64_t)c4[g];
+        S = (S << 8) + (uint64_t)(int64_t)c3[g];
+        S = (S << 8) + (uint64_t)(int64_t)c2[g];
+        S = (S << 8) + (uint64_t)(int64_t)c1[g];
+        S = (S << 8) + (uint64_t)(int64_t)c0[g];
+        y[g] = (int32_t)(uint32_t)((S + k0) >> 31);
+      }
+      if (nbig) {
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const int o = ob + 8 * (g >> 2) + (g & 3);
+          for (int b = 0; b < nbig; ++b) y[g] += xs(o + big[b]);   // mod 2^32, as the reference's (q31_t) cast
+        }
+      }
+      int32_t* yb = yf + ob;
+      if (cur.count == kFmChunk && ((((uintptr_t)yf) & 15) == 0)) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<uint4*>(yb + 8 * q) = make_uint4(y[4 * q], y[4 * q + 1], y[4 * q + 2], y[4 * q + 3]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (ob + 8 * q + e < cur.count) yb[8 * q + e] = y[4 * q + e];
+      }
+    }
+    if (nxt >= items) break;
+    it = nxt;
+    cur = next;
+  }
+}
+
+// true: launched (numTaps 1 .. 161, enough work to fill the chip); false: not this path
+bool fir_q31_mfma_launch(const int32_t* coeffs, int T, const int32_t* src, int32_t* dst, uint32_t B,
+                         uint32_t batch, const int32_t* hist_in, hipStream_t st) {
+  if (!MI355X_FIR_Q31_MFMA || T < 1 || T > 32 * kFmMaxKS - 31 || B == 0 || batch == 0) return false;
+  const uint32_t nchunks = (B + kFmChunk - 1) / kFmChunk;
+  const uint64_t items = (uint64_t)nchunks * batch;
+  if (items < 256 || items > 0x7fffffffull) return false;
+  const int ks = (T + 31 + 31) / 32;
+  const size_t img_bytes = (size_t)ks * 4 * 64 * 16;
+  void* buf = nullptr;
+  if (hipMallocAsync(&buf, img_bytes + 32, st) != hipSuccess) return false;
+  uint4* img = (uint4*)buf;
+  int* info = (int*)((char*)buf + img_bytes);
+  hipLaunchKernelGGL(fir_q31_coef_image_kernel, dim3((ks * 64 + 255) / 256), dim3(256), 0, st, coeffs, T, ks, img, info);
+#define FQ_CASE(K)                                                                                              \
+  case K: {                                                                                                     \
+    const int g = persistent_grid((const void*)fir_q31_mfma_kernel<K>, 256, 0, items);                         \
+    hipLaunchKernelGGL(fir_q31_mfma_kernel<K>, dim3(g), dim3(256), 0, st, coeffs, T, src, dst, B, hist_in,       \
+                       nchunks, (uint32_t)items, (const uint4*)img, (const int*)info);                          \
+    break;                                                                                                      \
+  }
+  switch (ks) {
+    FQ_CASE(1)
+    FQ_CASE(2)
+    FQ_CASE(3)
+    FQ_CASE(4)
+    FQ_CASE(5)
+    FQ_CASE(6)
+    default:
+      (void)hipFreeAsync(buf, st);
+      return false;
+  }
+#undef FQ_CASE
+  (void)hipFreeAsync(buf, st);
+  return true;
+}
+
 }  // namespace mi355x

@@ -157,6 +157,44 @@ def test_fir_q15_mfma_path(dsp, torch_gpu, ref, taps, block, fill):
         assert hist[f].tobytes() == state[:taps - 1].tobytes()
 
 
+@pytest.mark.parametrize("taps,block,fill", [(128, 4096, None), (1, 4096, None), (161, 4096, None), (64, 4100, "mixed"),
+                                             (130, 2049, None), (127, 4096, "big1"), (31, 4096, "big4"),
+                                             (64, 4096, "big7"), (128, 4096, "min"), (128, 4096, "max"),
+                                             (160, 8195, None), (33, 1000, "big2")])
+def test_fir_q31_mfma_path(dsp, torch_gpu, ref, taps, block, fill):
+    """arm_fir_q31 through the i8-MFMA kernel (fir_mfma.hip: numTaps <= 161 and >= 256 (filter,
+    4096-output chunk) items per call): 260 filters, two calls each (state carry), every word of 12
+    filters against the reference build -- random full range, all INT_MIN / INT_MAX (the class sums
+    at their extremes, the q63 sum wrapping), mixed extremes, and taps above 0x7F7F7F7F (no
+    balanced 4-digit form: 1, 2 and 4 of them corrected per output, 7 taking the exact
+    per-output path)."""
+    rng = np.random.default_rng(taps * 37 + block)
+    batch = 260
+    lo, hi = -(1 << 31), (1 << 31) - 1
+    coeffs = rng.integers(lo, hi, taps, endpoint=True).astype(np.int32)
+    mk = lambda: rng.integers(lo, hi, block, endpoint=True).astype(np.int32)
+    if fill == "min":
+        mk = lambda: np.full(block, lo, np.int32)
+    elif fill == "max":
+        coeffs = np.full(taps, hi, np.int32)
+        mk = lambda: np.full(block, hi, np.int32)
+    elif fill == "mixed":
+        vals = np.array([lo, hi, 0, -1, 1, 0x7F7F7F7F, 0x7F7F7F80], np.int32)
+        coeffs = rng.choice(vals, taps)
+        mk = lambda: rng.choice(vals, block)
+    elif fill and fill.startswith("big"):
+        coeffs = np.clip(coeffs, lo, 0x7F7F7F7F).astype(np.int32)
+        idx = rng.choice(taps, int(fill[3:]), replace=False)
+        coeffs[idx] = rng.integers(0x7F7F7F80, hi, len(idx), endpoint=True)
+    blocks = [[mk() for _ in range(2)] for _ in range(batch)]
+    got, hist = _fir_batched(dsp, torch_gpu, "q31", coeffs, blocks)
+    for f in (0, 1, 7, 63, 64, 100, 128, 129, 200, 255, 258, 259):
+        want, state = ref.fir("q31", coeffs, blocks[f])
+        for k in range(2):
+            assert got[k][f].tobytes() == want[k].tobytes(), (f, k, np.argwhere(got[k][f] != want[k])[:4])
+        assert hist[f].tobytes() == state[:taps - 1].tobytes()
+
+
 def test_fir_q15_pairwrap_extreme(dsp, torch_gpu, ref):
     """All -32768 input and taps: the __SMLALD pair sum wraps in int32 on the unrolled
     outputs but not on the blockSize%4 tail (arm_fir_q15.c:482-640 vs :649-681)."""
