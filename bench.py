@@ -830,19 +830,20 @@ def main_rank(args):
             line["roofline"]["bytes_moved_per_sample"] = 12
         if args.workload == "rfft_f32_pscratch":
             line["roofline"]["bytes_moved_per_sample"] = 8
-        if args.workload == "fir_fast_q15":
-            # one accumulating v_dot2 per tap pair per output; v_dot2_i32_i16 issues at half rate:
-            # 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T lane-instr/s (op_rate.txt measures 36.4)
-            valu = units * n / 2 / (kern_ms * 1e-3) * 1e-12
-            line["roofline"]["valu_dot2"] = {"achieved": round(valu, 2), "peak": 39.3, "unit": "T v_dot2 lane-instr/s",
-                                             "frac": round(valu / 39.3, 4)}
-        if args.workload == "fir_q15":
+        if args.workload in ("fir_q15", "fir_fast_q15"):
             # fir_mfma.hip: per 1024 outputs 6 i8 plane products of a 32 x 32 x (32 KS) MFMA tile, KS =
             # ceil((numTaps + 32) / 32): the i8 MFMA work the kernel issues against the 5 POPS dense peak
+            # (arm_fir_fast_q15 runs the same kernel with the modular epilogue)
             ks = (n + 32 + 31) // 32
             i8 = units / 1024 * 6 * 2 * 32 * 32 * 32 * ks / (kern_ms * 1e-3) * 1e-12
             line["roofline"]["mfma_i8"] = {"achieved": round(i8, 2), "peak": 5000.0, "unit": "TOPS (i8 MFMA issued)",
                                            "frac": round(i8 / 5000.0, 4), "k_steps": ks, "plane_products": 6}
+        if args.workload == "fir_q31":
+            # fir_mfma.hip: 16 i8 plane products (4 sample x 4 tap planes) per K step, KS = ceil((numTaps + 31) / 32)
+            ks = (n + 31 + 31) // 32
+            i8 = units / 1024 * 16 * 2 * 32 * 32 * 32 * ks / (kern_ms * 1e-3) * 1e-12
+            line["roofline"]["mfma_i8"] = {"achieved": round(i8, 2), "peak": 5000.0, "unit": "TOPS (i8 MFMA issued)",
+                                           "frac": round(i8 / 5000.0, 4), "k_steps": ks, "plane_products": 16}
         if args.workload in ("fir_q15", "fir_q31", "fir_fast_q15", "fir_fast_q31", "mfcc_q31", "mfcc_q15"):
             vi = valu_issue(prof, batch, kern_ms)
             if vi:

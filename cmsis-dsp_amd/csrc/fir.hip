@@ -1078,9 +1078,9 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
     }
     case kFirQ15:
     case kFirFastQ15: {
-      if (kind == kFirQ15 && T_ <= kFirMaxTaps &&
+      if (T_ <= kFirMaxTaps &&
           fir_q15_mfma_launch((const int16_t*)coeffs, T_, (const int16_t*)src, (int16_t*)dst, B, batch,
-                              (const int16_t*)hist_in, st))
+                              (const int16_t*)hist_in, st, kind == kFirFastQ15))
         break;
       auto k = kind == kFirQ15 ? (T_ > kFirMaxTaps ? fir_q15_kernel<false, true> : fir_q15_kernel<false, false>)
                                : (T_ > kFirMaxTaps ? fir_q15_kernel<true, true> : fir_q15_kernel<true, false>);

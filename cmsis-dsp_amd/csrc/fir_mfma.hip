@@ -128,7 +128,7 @@ __device__ __forceinline__ void fm_wrap_item(const uint8_t* ph, const uint8_t* p
   }
 }
 
-template <int KS>
+template <int KS, bool FAST>
 __device__ __forceinline__ void fm_tile_y(const uint4* __restrict__ imgd, const uint8_t* ph, const uint8_t* pl, int wid,
                                           int L, int32_t sumc, uint32_t (&y)[8]) {
   const int i = L & 31, h = L >> 5;
@@ -157,8 +157,17 @@ __device__ __forceinline__ void fm_tile_y(const uint4* __restrict__ imgd, const 
     // W = Y + sum c + (a0 >> 7): R = 2^7 W + (a0 & 127), so R >> 15 = W >> 8 (floor division),
     // every term int32 (|Y| < 2^26, |sum c| < 2^23)
     const int32_t X = 2 * a16[g] + a15[g];
-    const int32_t W = 2 * a8[g] + a7[g] + sumc + (a0[g] >> 7);
-    const uint32_t v = (uint16_t)(int16_t)ssat16(X + (W >> 8));
+    uint32_t v;
+    if constexpr (FAST) {
+      // arm_fir_fast_q15: the q31_t accumulator wraps mod 2^32 (every __SMLAD and tail product),
+      // so the exact sum's low word is the reference's accumulator: S mod 2^32 in uint32 arithmetic
+      const uint32_t S = ((uint32_t)X << 15) + ((uint32_t)(2 * a8[g] + a7[g]) << 7) + (uint32_t)a0[g] +
+                         ((uint32_t)sumc << 7);
+      v = (uint16_t)(int16_t)ssat16((int32_t)S >> 15);
+    } else {
+      const int32_t W = 2 * a8[g] + a7[g] + sumc + (a0[g] >> 7);
+      v = (uint16_t)(int16_t)ssat16(X + (W >> 8));
+    }
     y[g >> 1] = (g & 1) ? (y[g >> 1] | (v << 16)) : v;
   }
 }
@@ -183,15 +192,17 @@ __device__ __forceinline__ void fm_tile_store(const uint32_t (&y)[8], int wid, i
 
 // One wave's 32 x 32 output tile of an item (outputs 1024 wid .. + 1023) from the staged planes:
 // 6 plane products per K step into five int32 accumulators, then the exact output.
-template <int KS>
+template <int KS, bool FAST>
 __device__ __forceinline__ void fm_tile(const uint4* __restrict__ imgd, const uint8_t* ph, const uint8_t* pl, int wid,
                                         int L, int count, int16_t* __restrict__ yrow, int32_t sumc) {
   uint32_t y[8];
-  fm_tile_y<KS>(imgd, ph, pl, wid, L, sumc, y);
+  fm_tile_y<KS, FAST>(imgd, ph, pl, wid, L, sumc, y);
   fm_tile_store(y, wid, L, count, yrow);
 }
 
-template <int KS>
+// FAST: arm_fir_fast_q15 (arm_fir_fast_q15.c: the same products summed in a wrapping q31_t, no
+// pair-wrap special case since everything is mod 2^32)
+template <int KS, bool FAST>
 __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kernel(const int16_t* __restrict__ coeffs, int T,
                                                               const int16_t* __restrict__ src, int16_t* __restrict__ dst,
                                                               uint32_t B, const int16_t* __restrict__ hist,
@@ -204,7 +215,7 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
   const int tid = threadIdx.x, L = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T1 = T - 1;
-  const bool wrap = info[1] != 0;
+  const bool wrap = !FAST && info[1] != 0;
   const int32_t sumc = info[0];                          // |sum c| <= 160 * 2^15
   for (int u = tid; u < 2 * KS * 3 * 64; u += 256) imgl[u] = image[u];   // visible after the loop's first barrier
 
@@ -291,7 +302,7 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
     if (wrap) {
       fm_wrap_item(ph, pl, coeffs, T, B, cur.n0, cur.d, cur.count, tid, dst + (uint64_t)cur.f * B);
     } else if (1024 * wid < cur.count) {
-      fm_tile<KS>(imgl + cur.d * KS * 3 * 64, ph, pl, wid, L, cur.count, dst + (uint64_t)cur.f * B + cur.n0, sumc);
+      fm_tile<KS, FAST>(imgl + cur.d * KS * 3 * 64, ph, pl, wid, L, cur.count, dst + (uint64_t)cur.f * B + cur.n0, sumc);
     }
     if (nxt >= items) break;
     it = nxt;
@@ -301,8 +312,8 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
 
 // true: launched (numTaps even, 2 .. 160, enough work to fill the chip); false: not this path
 bool fir_q15_mfma_launch(const int16_t* coeffs, int T, const int16_t* src, int16_t* dst, uint32_t B,
-                         uint32_t batch, const int16_t* hist_in, hipStream_t st) {
-  if (!MI355X_FIR_Q15_MFMA || T < 2 || (T & 1) || T > 32 * kFmMaxKS - 32 || B == 0 || batch == 0) return false;
+                         uint32_t batch, const int16_t* hist_in, hipStream_t st, bool fast) {
+  if (!(fast ? MI355X_FIR_FAST_Q15_MFMA : MI355X_FIR_Q15_MFMA) || T < 2 || (T & 1) || T > 32 * kFmMaxKS - 32 || B == 0 || batch == 0) return false;
   const uint32_t nchunks = (B + kFmChunk - 1) / kFmChunk;
   const uint64_t items = (uint64_t)nchunks * batch;
   if (items < 256 || items > 0x7fffffffull) return false;
@@ -316,9 +327,10 @@ bool fir_q15_mfma_launch(const int16_t* coeffs, int T, const int16_t* src, int16
   hipLaunchKernelGGL(fir_q15_coef_image_kernel, dim3((2 * ks * 64 + 255) / 256), dim3(256), 0, st, coeffs, T, ks, img, info);
 #define FM_CASE(K)                                                                                              \
   case K: {                                                                                                     \
-    const int g = persistent_grid((const void*)fir_q15_mfma_kernel<K>, 256, 0, items);                         \
-    hipLaunchKernelGGL(fir_q15_mfma_kernel<K>, dim3(g), dim3(256), 0, st, coeffs, T, src, dst, B, hist_in,       \
-                       nchunks, (uint32_t)items, (const uint4*)img, (const int*)info);                          \
+    auto kern = fast ? fir_q15_mfma_kernel<K, true> : fir_q15_mfma_kernel<K, false>;                            \
+    const int g = persistent_grid((const void*)kern, 256, 0, items);                                            \
+    hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, st, coeffs, T, src, dst, B, hist_in, nchunks,              \
+                       (uint32_t)items, (const uint4*)img, (const int*)info);                                   \
     break;                                                                                                      \
   }
   switch (ks) {

@@ -105,6 +105,9 @@
 #ifndef MI355X_FIR_Q31_MFMA     // arm_fir_q31 (numTaps <= 161, >= 256 items) on the i8 MFMA (fir_mfma.hip)
 #define MI355X_FIR_Q31_MFMA 1
 #endif
+#ifndef MI355X_FIR_FAST_Q15_MFMA   // arm_fir_fast_q15 on the same kernel (modular epilogue)
+#define MI355X_FIR_FAST_Q15_MFMA 1
+#endif
 #ifndef MI355X_FIR_Q15_MFMA     // arm_fir_q15 (even numTaps <= 160, >= 256 items) on the i8 MFMA (fir_mfma.hip)
 #define MI355X_FIR_Q15_MFMA 1
 #endif

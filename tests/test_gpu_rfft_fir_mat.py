@@ -124,13 +124,14 @@ def test_fir_batch_bitexact_two_calls(dsp, torch_gpu, ref, kind, taps, block):
 @pytest.mark.parametrize("taps,block,fill", [(128, 4096, None), (2, 4096, None), (8, 1000, "min"), (64, 4100, "mixed"),
                                              (130, 2049, None), (158, 4096, "max"), (160, 8195, None),
                                              (128, 4096, "min"), (16, 4096, "wrap")])
-def test_fir_q15_mfma_path(dsp, torch_gpu, ref, taps, block, fill):
+@pytest.mark.parametrize("kind", ["q15", "fast_q15"])
+def test_fir_q15_mfma_path(dsp, torch_gpu, ref, taps, block, fill, kind):
     """arm_fir_q15 through the i8-MFMA kernel (fir_mfma.hip: even numTaps <= 160 and >= 256
     (filter, 4096-output chunk) items per call): 260 filters, two calls each (state carry), every
     word of 12 filters against the reference build -- random full range, all -32768 / 32767 (the
     plane sums at their extremes, the output saturating), mixed extremes, and taps holding a
     (-32768, -32768) pair over all -32768 input (the __SMLALD pair wrap: the kernel's exact pair-wise
-    path)."""
+    path).  arm_fir_fast_q15 runs the same kernel with the modular (q31_t wrap) epilogue."""
     rng = np.random.default_rng(taps * 31 + block)
     batch = 260
     if fill == "min" or fill == "wrap":
@@ -149,9 +150,9 @@ def test_fir_q15_mfma_path(dsp, torch_gpu, ref, taps, block, fill):
         coeffs = rng.integers(-32768, 32767, taps, endpoint=True).astype(np.int16)
         mk = lambda: rng.integers(-32768, 32767, block, endpoint=True).astype(np.int16)
     blocks = [[mk() for _ in range(2)] for _ in range(batch)]
-    got, hist = _fir_batched(dsp, torch_gpu, "q15", coeffs, blocks)
+    got, hist = _fir_batched(dsp, torch_gpu, kind, coeffs, blocks)
     for f in (0, 1, 7, 63, 64, 100, 128, 129, 200, 255, 258, 259):
-        want, state = ref.fir("q15", coeffs, blocks[f])
+        want, state = ref.fir(kind, coeffs, blocks[f])
         for k in range(2):
             assert got[k][f].tobytes() == want[k].tobytes(), (f, k, np.argwhere(got[k][f] != want[k])[:4])
         assert hist[f].tobytes() == state[:taps - 1].tobytes()

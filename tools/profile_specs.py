@@ -27,7 +27,7 @@ SPECS = {
     "fir_f32_fma": ("--workload fir_f32_fma --steps 10 --warmup 3", "fir_f32_kernel", ""),
     "fir_q15": ("--workload fir_q15 --steps 10 --warmup 3", "fir_q15_mfma", "fir_mfma"),
     "fir_q31": ("--workload fir_q31 --steps 10 --warmup 3", "fir_q31_mfma", "fir_mfma"),
-    "fir_fast_q15": ("--workload fir_fast_q15 --steps 10 --warmup 3", "fir_q15_kernel", "fir"),
+    "fir_fast_q15": ("--workload fir_fast_q15 --steps 10 --warmup 3", "fir_q15_mfma", "fir_mfma"),
     "fir_fast_q31": ("--workload fir_fast_q31 --steps 10 --warmup 3", "fir_q31_kernel", "fir"),
     "conv_f32": ("--workload conv_f32 --steps 10 --warmup 3", "fir_f32_kernel", ""),
     "mfcc_f32": ("--workload mfcc_f32 --steps 10 --warmup 3", "mfcc_fused", ""),
