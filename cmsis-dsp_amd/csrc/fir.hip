@@ -1089,6 +1089,9 @@ static hipError_t fir_launch(int kind, const T* coeffs, int T_, const T* src, T*
       break;
     }
     case kFirQ7: {
+      if (fir_q7_mfma_launch((const int8_t*)coeffs, T_, (const int8_t*)src, (int8_t*)dst, B, batch,
+                             (const int8_t*)hist_in, st))
+        break;
       hipLaunchKernelGGL(T_ > kFirMaxTaps ? fir_q7_kernel<true> : fir_q7_kernel<false>, dim3(items), dim3(kBlock), 0, st, (const int8_t*)coeffs, T_,
                          (const int8_t*)src, (int8_t*)dst, B, (const int8_t*)hist_in, nchunks);
       break;

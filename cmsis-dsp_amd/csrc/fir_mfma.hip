@@ -626,4 +626,168 @@ bool fir_q31_mfma_launch(const int32_t* coeffs, int T, const int32_t* src, int32
   return true;
 }
 
+// =============================================================================================
+// Batched arm_fir_q7 on the i8 matrix cores (round 6), bit-exact.  The reference
+// (Source/FilteringFunctions/arm_fir_q7.c:446-560 and the tail) sums (q15_t)(x * c) -- exact, |x c|
+// <= 2^14 -- in a q31_t and stores (q7_t)__SSAT(acc >> 7, 8); with numTaps <= 161 the sum is exact
+// in int32, so the whole filter is ONE i8 plane product per K step: the samples and the taps are
+// already the MFMA's i8 operands.  Same Toeplitz tiling as above; the window starts d = 0 .. 3
+// samples early so that its block-input words are 4-byte aligned (one coefficient image per d).
+constexpr int kQ7Words = (kFmChunk + 32 * kFmMaxKS) / 4;      // window words (4 samples) per item: 1072
+constexpr int kQ7Per = (kQ7Words + 255) / 256;                // words per thread
+constexpr int kQ7Plane = 4 * kQ7Words + 256;
+
+// image[d][ks][lane]: taps c[32 ks + 16 h + e - d - i] as the A operand (lane L: i = L & 31, h = L >> 5)
+__global__ __launch_bounds__(256) void fir_q7_coef_image_kernel(const int8_t* __restrict__ coeffs, int T, int KS,
+                                                                uint4* __restrict__ image) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= 4 * KS * 64) return;
+  const int L = g & 63, ks = (g >> 6) % KS, d = (g >> 6) / KS, i = L & 31, h = L >> 5;
+  uint32_t w[4] = {};
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int ci = 32 * ks + 16 * h + e - d - i;
+    w[e >> 2] |= (uint32_t)(uint8_t)((ci >= 0 && ci < T) ? coeffs[ci] : 0) << (8 * (e & 3));
+  }
+  image[(d * KS + ks) * 64 + L] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <int KS>
+__global__ __launch_bounds__(256) void fir_q7_mfma_kernel(int T, const int8_t* __restrict__ src, int8_t* __restrict__ dst,
+                                                          uint32_t B, const int8_t* __restrict__ hist, uint32_t nchunks,
+                                                          uint32_t items, const uint4* __restrict__ image) {
+  __shared__ __attribute__((aligned(16))) uint8_t pw[kQ7Plane];
+  __shared__ __attribute__((aligned(16))) uint4 imgl[4 * KS * 64];
+  const int tid = threadIdx.x, L = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T1 = T - 1;
+  for (int u = tid; u < 4 * KS * 64; u += 256) imgl[u] = image[u];   // visible after the loop's first barrier
+
+  struct Item { uint32_t f; int n0, count, d; };
+  auto item_of = [&](uint32_t it) {
+    Item x;
+    x.f = it / nchunks;
+    x.n0 = (int)(it - x.f * nchunks) * kFmChunk;
+    x.count = min((int)B - x.n0, kFmChunk);
+    x.d = (int)(((uint64_t)x.f * B + (uint32_t)x.n0 - (uint32_t)T1) & 3u);   // w[m] = s[n0 - d + m]
+    return x;
+  };
+  uint32_t wv[kQ7Per];
+  auto load_window = [&](const Item& x) {
+    const int8_t* blk = src + ((int64_t)x.f * B + x.n0 - x.d - T1);      // w[m] of the block input: blk[m] (aligned)
+#pragma unroll
+    for (int q = 0; q < kQ7Per; ++q) {
+      const int u = tid + 256 * q, j0 = x.n0 - x.d + 4 * u;
+      if (u >= kQ7Words) {
+        wv[q] = 0u;
+      } else if (j0 >= T1 && j0 + 3 - T1 < (int)B) {                     // four samples in the block input
+        wv[q] = *reinterpret_cast<const uint32_t*>(blk + 4 * u);
+      } else {
+        uint32_t r = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = j0 + e;
+          const bool in_h = j >= 0 && j < T1, in_b = j >= T1 && j - T1 < (int)B;
+          const int8_t* p = in_h ? hist + (uint64_t)x.f * T1 + j : (in_b ? src + (uint64_t)x.f * B + (j - T1) : src);
+          const uint32_t v = (uint8_t)*p;
+          r |= ((in_h || in_b) ? v : 0u) << (8 * e);
+        }
+        wv[q] = r;
+      }
+    }
+  };
+  auto stage_window = [&]() {
+#pragma unroll
+    for (int q = 0; q < kQ7Per; ++q) {
+      const int u = tid + 256 * q;
+      if (u < kQ7Words) *reinterpret_cast<uint32_t*>(pw + fm_swz(4 * u)) = wv[q];
+    }
+  };
+
+  uint32_t it = blockIdx.x;
+  if (it >= items) return;
+  Item cur = item_of(it);
+  load_window(cur);
+  for (;;) {
+    __syncthreads();                                     // the previous item's reads are done
+    stage_window();
+    __syncthreads();
+    const uint32_t nxt = it + gridDim.x;
+    const Item next = item_of(nxt < items ? nxt : it);
+    if (nxt < items) load_window(next);                  // in flight under this item's MFMAs
+    if (1024 * wid < cur.count) {
+      const int i = L & 31, h = L >> 5;
+      const uint4* img = imgl + cur.d * KS * 64 + L;
+      i32x16 acc = {};
+      const int mb = 1024 * wid + 32 * i + 16 * h;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const uint4 u = img[ks * 64];
+        const i32x4 c = i32x4{(int)u.x, (int)u.y, (int)u.z, (int)u.w};
+        const i32x4 x = *reinterpret_cast<const i32x4*>(pw + fm_swz(mb + 32 * ks));
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(c, x, acc, 0, 0, 0);
+      }
+      // lane (j = L & 31, h), register 4q + e -> output 8q + 4h + e of block j
+      const int j = L & 31, ob = 1024 * wid + 32 * j + 4 * h;
+      int8_t* yf = dst + (uint64_t)cur.f * B + cur.n0;
+      uint32_t y[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v |= (uint32_t)(uint8_t)(int8_t)ssat8(acc[4 * q + e] >> 7) << (8 * e);
+        y[q] = v;
+      }
+      if (cur.count == kFmChunk && ((((uintptr_t)yf) & 3) == 0)) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<uint32_t*>(yf + ob + 8 * q) = y[q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (ob + 8 * q + e < cur.count) yf[ob + 8 * q + e] = (int8_t)(y[q] >> (8 * e));
+      }
+    }
+    if (nxt >= items) break;
+    it = nxt;
+    cur = next;
+  }
+}
+
+// true: launched (numTaps 1 .. 157, enough work to fill the chip); false: not this path
+bool fir_q7_mfma_launch(const int8_t* coeffs, int T, const int8_t* src, int8_t* dst, uint32_t B, uint32_t batch,
+                        const int8_t* hist_in, hipStream_t st) {
+  if (!MI355X_FIR_Q7_MFMA || T < 1 || T > 32 * kFmMaxKS - 35 || B == 0 || batch == 0) return false;
+  const uint32_t nchunks = (B + kFmChunk - 1) / kFmChunk;
+  const uint64_t items = (uint64_t)nchunks * batch;
+  if (items < 256 || items > 0x7fffffffull) return false;
+  const int ks = (T + 34 + 31) / 32;                     // K >= numTaps - 1 + 31 + d (d <= 3) + 1
+  const size_t img_bytes = (size_t)4 * ks * 64 * 16;
+  void* buf = nullptr;
+  if (hipMallocAsync(&buf, img_bytes, st) != hipSuccess) return false;
+  uint4* img = (uint4*)buf;
+  hipLaunchKernelGGL(fir_q7_coef_image_kernel, dim3((4 * ks * 64 + 255) / 256), dim3(256), 0, st, coeffs, T, ks, img);
+#define F7_CASE(K)                                                                                              \
+  case K: {                                                                                                     \
+    const int g = persistent_grid((const void*)fir_q7_mfma_kernel<K>, 256, 0, items);                          \
+    hipLaunchKernelGGL(fir_q7_mfma_kernel<K>, dim3(g), dim3(256), 0, st, T, src, dst, B, hist_in, nchunks,     \
+                       (uint32_t)items, (const uint4*)img);                                                     \
+    break;                                                                                                      \
+  }
+  switch (ks) {
+    F7_CASE(2)
+    F7_CASE(3)
+    F7_CASE(4)
+    F7_CASE(5)
+    F7_CASE(6)
+    default:
+      (void)hipFreeAsync(buf, st);
+      return false;
+  }
+#undef F7_CASE
+  (void)hipFreeAsync(buf, st);
+  return true;
+}
+
 }  // namespace mi355x

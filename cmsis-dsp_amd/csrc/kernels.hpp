@@ -117,6 +117,9 @@ enum FirKind { kFirF32 = 0, kFirQ15 = 1, kFirQ31 = 2, kFirFastQ15 = 3, kFirFastQ
 // then runs fir_q15_kernel)
 bool fir_q15_mfma_launch(const int16_t* coeffs, int T, const int16_t* src, int16_t* dst, uint32_t B, uint32_t batch,
                          const int16_t* hist_in, hipStream_t st, bool fast = false);   // fast: arm_fir_fast_q15
+// arm_fir_q7 likewise (numTaps <= 157)
+bool fir_q7_mfma_launch(const int8_t* coeffs, int T, const int8_t* src, int8_t* dst, uint32_t B, uint32_t batch,
+                        const int8_t* hist_in, hipStream_t st);
 // arm_fir_q31 likewise (numTaps <= 161)
 bool fir_q31_mfma_launch(const int32_t* coeffs, int T, const int32_t* src, int32_t* dst, uint32_t B, uint32_t batch,
                          const int32_t* hist_in, hipStream_t st);

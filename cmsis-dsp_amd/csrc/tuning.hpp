@@ -102,6 +102,9 @@
 #ifndef MI355X_FIR_F32_FMA_WAVES
 #define MI355X_FIR_F32_FMA_WAVES 4                   // FMA: + 8 coefficient and 4 tap-staging VGPRs
 #endif
+#ifndef MI355X_FIR_Q7_MFMA      // arm_fir_q7 (numTaps <= 157, >= 256 items) on the i8 MFMA (fir_mfma.hip)
+#define MI355X_FIR_Q7_MFMA 1
+#endif
 #ifndef MI355X_FIR_Q31_MFMA     // arm_fir_q31 (numTaps <= 161, >= 256 items) on the i8 MFMA (fir_mfma.hip)
 #define MI355X_FIR_Q31_MFMA 1
 #endif

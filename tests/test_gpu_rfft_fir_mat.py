@@ -196,6 +196,37 @@ def test_fir_q31_mfma_path(dsp, torch_gpu, ref, taps, block, fill):
         assert hist[f].tobytes() == state[:taps - 1].tobytes()
 
 
+@pytest.mark.parametrize("taps,block,fill", [(128, 4096, None), (1, 4096, None), (157, 4096, None), (64, 4100, "mixed"),
+                                             (130, 2049, None), (33, 1001, None), (128, 4096, "min"),
+                                             (128, 4096, "max"), (100, 8195, None)])
+def test_fir_q7_mfma_path(dsp, torch_gpu, ref, taps, block, fill):
+    """arm_fir_q7 through the i8-MFMA kernel (fir_mfma.hip: numTaps <= 157 and >= 256 (filter,
+    4096-output chunk) items per call; ragged blocks give every filter its own window shift d):
+    260 filters, two calls each (state carry), every word of 12 filters against the reference
+    build -- random full range, all -128 / 127 (the output saturating both ways), mixed extremes."""
+    rng = np.random.default_rng(taps * 41 + block)
+    batch = 260
+    coeffs = rng.integers(-128, 127, taps, endpoint=True).astype(np.int8)
+    mk = lambda: rng.integers(-128, 127, block, endpoint=True).astype(np.int8)
+    if fill == "min":
+        coeffs = np.full(taps, -128, np.int8)
+        mk = lambda: np.full(block, -128, np.int8)
+    elif fill == "max":
+        coeffs = np.full(taps, 127, np.int8)
+        mk = lambda: np.full(block, -128, np.int8)
+    elif fill == "mixed":
+        vals = np.array([-128, 127, 0, -1, 1], np.int8)
+        coeffs = rng.choice(vals, taps)
+        mk = lambda: rng.choice(vals, block)
+    blocks = [[mk() for _ in range(2)] for _ in range(batch)]
+    got, hist = _fir_batched(dsp, torch_gpu, "q7", coeffs, blocks)
+    for f in (0, 1, 7, 63, 64, 100, 128, 129, 200, 255, 258, 259):
+        want, state = ref.fir("q7", coeffs, blocks[f])
+        for k in range(2):
+            assert got[k][f].tobytes() == want[k].tobytes(), (f, k, np.argwhere(got[k][f] != want[k])[:4])
+        assert hist[f].tobytes() == state[:taps - 1].tobytes()
+
+
 def test_fir_q15_pairwrap_extreme(dsp, torch_gpu, ref):
     """All -32768 input and taps: the __SMLALD pair sum wraps in int32 on the unrolled
     outputs but not on the blockSize%4 tail (arm_fir_q15.c:482-640 vs :649-681)."""
