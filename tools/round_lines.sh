@@ -13,3 +13,5 @@ for wl in fir_f32 mat_mult_f32 fir_f32_fma fir_q15 fir_q31 fir_fast_q15 fir_fast
   timeout -k 10 300 python -u bench.py --workload $wl $cb > $O/$wl.json 2> $O/$wl.err
   python -c "import json;d=json.load(open('$O/$wl.json'));print('$wl',d['value'],d['unit'],d['roofline'].get('frac'),d['parity'].get('bit_exact'),(d.get('cpu_baseline') or {}).get('value'))"
 done
+timeout -k 10 200 python -u tools/bench_filters.py fir_q7 > $O/fir_q7.json 2> $O/fir_q7.err
+python -c "import json;d=json.loads(open('$O/fir_q7.json').read().splitlines()[0]);print('fir_q7',d['input_gsamples_per_s'],d['bit_exact'])"
