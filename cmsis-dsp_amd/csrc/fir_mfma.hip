@@ -47,11 +47,24 @@
 #define MI355X_FIR_Q15_MFMA_WG 3
 #endif
 
+#ifndef MI355X_FIR_STAMP
+#define MI355X_FIR_STAMP 0
+#endif
 #ifndef MI355X_FIR_Q15_DIAG        // 1: diagnostic only -- no window loads after the first item (wrong output)
 #define MI355X_FIR_Q15_DIAG 0
 #endif
 
 namespace mi355x {
+
+#if MI355X_FIR_STAMP   // diagnostic: s_memtime per phase of the first 64 items of workgroups 0-63 (wave 0)
+__device__ unsigned long long fir_stamp_buf[64][64][8];
+#define FM_STAMP(k, e)                                                                              \
+  do {                                                                                              \
+    if (blockIdx.x < 64 && tid == 0 && (k) < 64) fir_stamp_buf[blockIdx.x][(k)][(e)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define FM_STAMP(k, e) do { } while (0)
+#endif
 
 namespace {
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -172,32 +185,37 @@ __device__ __forceinline__ void fm_tile_y(const uint4* __restrict__ imgd, const 
   }
 }
 
-// lane (j = L & 31, h), register 4q + e -> output 8q + 4h + e of block j
+// lane (j = L & 31, h), register 4q + e -> output 8q + 4h + e of block j.  A whole tile goes out
+// through the wave's 2 KiB LDS slot otw: each lane writes its four 8-B pieces (16-B chunk c = 4 j + q
+// of the tile, half h), then reads chunks L and 64 + L back, so each global store instruction
+// writes 1 KiB of consecutive outputs -- stored straight from the accumulator layout, every lane
+// wrote 8 B into its own 64-B segment and the store phase took ~1,100 of an item's ~6,900 ticks
+// (tools/probes/fir_stamps.hip).  Chunks are XOR-swizzled (c ^ ((c >> 4) & 3)) so that the writes
+// spread over the 16 four-bank groups.
+__device__ __forceinline__ int fm_ochunk(int c) { return c ^ ((c >> 4) & 3); }
 __device__ __forceinline__ void fm_tile_store(const uint32_t (&y)[8], int wid, int L, int count,
-                                              int16_t* __restrict__ yrow) {
+                                              int16_t* __restrict__ yrow, uint4* otw) {
   const int j = L & 31, h = L >> 5;
-  int16_t* yb = yrow + 1024 * wid + 32 * j + 4 * h;
-  const int ob = 1024 * wid + 32 * j + 4 * h;
-  if (count == kFmChunk && ((((uintptr_t)yrow) & 7) == 0)) {
+  if (count == kFmChunk && ((((uintptr_t)yrow) & 15) == 0)) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) *reinterpret_cast<uint2*>(yb + 8 * q) = make_uint2(y[2 * q], y[2 * q + 1]);
+    for (int q = 0; q < 4; ++q) reinterpret_cast<uint2*>(otw + fm_ochunk(4 * j + q))[h] = make_uint2(y[2 * q], y[2 * q + 1]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int c = 64 * r + L;
+      *reinterpret_cast<uint4*>(yrow + 1024 * wid + 8 * c) = otw[fm_ochunk(c)];
+    }
   } else {
+    int16_t* yb = yrow + 1024 * wid + 32 * j + 4 * h;
+    const int ob = 1024 * wid + 32 * j + 4 * h;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         if (ob + 8 * q + e < count) yb[8 * q + e] = (int16_t)(y[2 * q + (e >> 1)] >> (16 * (e & 1)));
   }
-}
-
-// One wave's 32 x 32 output tile of an item (outputs 1024 wid .. + 1023) from the staged planes:
-// 6 plane products per K step into five int32 accumulators, then the exact output.
-template <int KS, bool FAST>
-__device__ __forceinline__ void fm_tile(const uint4* __restrict__ imgd, const uint8_t* ph, const uint8_t* pl, int wid,
-                                        int L, int count, int16_t* __restrict__ yrow, int32_t sumc) {
-  uint32_t y[8];
-  fm_tile_y<KS, FAST>(imgd, ph, pl, wid, L, sumc, y);
-  fm_tile_store(y, wid, L, count, yrow);
 }
 
 // FAST: arm_fir_fast_q15 (arm_fir_fast_q15.c: the same products summed in a wrapping q31_t, no
@@ -212,6 +230,8 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
   __shared__ __attribute__((aligned(16))) uint8_t ph[kFmPlane];
   __shared__ __attribute__((aligned(16))) uint8_t pl[kFmPlane];
   __shared__ __attribute__((aligned(16))) uint4 imgl[2 * KS * 3 * 64];   // the coefficient image, once per workgroup
+  __shared__ uint32_t hd[256];                           // head samples (and [192]: the tail sample) of the next window
+  __shared__ __attribute__((aligned(16))) uint4 ot[4][128];   // per wave: the output tile on its way out
   const int tid = threadIdx.x, L = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T1 = T - 1;
@@ -231,28 +251,30 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
     return x;
   };
   // Window words in PAIRS: thread tid takes words 2 (tid + 256 q) and + 1 (4 samples, one 4-byte
-  // write per plane), then single words 512 kFmPer2 + tid + 256 q.  Words whose two samples both lie in the block input (u_lo <= u < u_hi, wave-
-  // uniform bounds) are aligned dword loads; the rest (history of a filter's first item, the
-  // zero tail past the block) sample by sample from a clamped, always-valid address.
-  uint32_t wv[2 * kFmPer2 + kFmPer1];
-  auto word_slow = [&](const Item& x, int u) -> uint32_t {
-    uint32_t r = 0;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int j = x.n0 - x.d + 2 * u + e;              // state index
-      const bool in_h = j >= 0 && j < T1, in_b = j >= T1 && j - T1 < (int)B;
-      const int16_t* p = in_h ? hist + (uint64_t)x.f * T1 + j : (in_b ? src + (uint64_t)x.f * B + (j - T1) : src);
-      const uint32_t v = (uint16_t)*p;
-      r |= ((in_h || in_b) ? v : 0u) << (16 * e);
-    }
-    return r;
-  };
-  auto load_window = [&](const Item& x) {
-    const int64_t base = (int64_t)x.f * B + x.n0 - x.d - T1;               // src index of w[0] (even)
+  // write per plane), then single words 512 kFmPer2 + tid + 256 q.
+  // Window words: every word is loaded as one aligned dword from a CLAMPED block-input address with no
+  // branch and no select, so nothing in the load phase waits for a load (a per-lane "block word or
+  // per-sample path" select put the wave behind its own loads -- the result register's join made
+  // the compiler wait there; phase stamps, tools/probes/fir_stamps.hip, had the load phase at 53 % of
+  // an item).  The words before u_lo (a filter's first item: the history) come from per-sample head
+  // samples and a block ending mid-word (odd blockSize) from the tail sample, both landed in LDS by
+  // DMA; they are combined when the window is staged.
+  struct Win { int u_lo, u_hi; bool straddle; };
+  auto win_of = [&](const Item& x) {
+    Win w;
     const int lo_num = T1 - x.n0 + x.d, hi_num = T1 + (int)B - 2 - x.n0 + x.d;
-    const int u_lo = lo_num > 0 ? (lo_num + 1) >> 1 : 0, u_hi = hi_num >= 0 ? (hi_num >> 1) + 1 : 0;
+    w.u_lo = lo_num > 0 ? (lo_num + 1) >> 1 : 0;
+    w.u_hi = hi_num >= 0 ? (hi_num >> 1) + 1 : 0;
+    w.straddle = x.n0 - x.d + 2 * w.u_hi == T1 + (int)B - 1 && w.u_hi < kFmWords;   // word u_hi = (last sample, 0)
+    return w;
+  };
+  uint32_t wv[2 * kFmPer2 + kFmPer1];
+  auto load_window = [&](const Item& x) {
+    const Win w = win_of(x);
+    const int64_t base = (int64_t)x.f * B + x.n0 - x.d - T1;               // src index of w[0] (even)
     auto word = [&](int u) -> uint32_t {
-      return (u >= u_lo && u < u_hi) ? *reinterpret_cast<const uint32_t*>(src + base + 2 * u) : word_slow(x, u);
+      const int uc = min(max(u, w.u_lo), w.u_hi - 1);
+      return *reinterpret_cast<const uint32_t*>(src + base + 2 * uc);
     };
 #pragma unroll
     for (int q = 0; q < kFmPer2; ++q) {
@@ -260,17 +282,30 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
       for (int e = 0; e < 2; ++e) wv[2 * q + e] = word(2 * (tid + 256 * q) + e);
     }
 #pragma unroll
-    for (int q = 0; q < kFmPer1; ++q) {
-      const int u = 512 * kFmPer2 + tid + 256 * q;
-      wv[2 * kFmPer2 + q] = u < kFmWords ? word(u) : 0u;
+    for (int q = 0; q < kFmPer1; ++q) wv[2 * kFmPer2 + q] = word(min(512 * kFmPer2 + tid + 256 * q, kFmWords - 1));
+    // The head samples and the tail sample go to LDS by DMA (one zero-extended dword per lane,
+    // tools/probes/lds_dma_sub.hip): waves 0-2 samples 64 w + lane, wave 3 the block's last sample.
+    // No register receives them, so nothing here waits; barrier A's vmcnt(0) lands them.
+    {
+      const int j = x.n0 - x.d + 64 * wid + L;            // state index (2 u_lo <= T1 + 2 <= 161 samples)
+      const bool in_h = j >= 0 && j < T1;
+      const uint64_t ph_ = (uint64_t)(uintptr_t)(hist + (uint64_t)x.f * T1 + (in_h ? j : 0));
+      const uint64_t pb_ = (uint64_t)(uintptr_t)(src + (uint64_t)x.f * B + (wid == 3 ? (int)B - 1 : min(max(j - T1, 0), (int)B - 1)));
+      const uint64_t pa = (wid < 3 && in_h) ? ph_ : pb_;
+      __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)pa, (__attribute__((address_space(3))) void*)(hd + 64 * wid),
+                                       2, 0, 0);
     }
   };
-  auto stage_window = [&]() {                            // registers -> the two byte planes
+  auto stage_window = [&](const Item& x) {               // registers -> the two byte planes
+    const Win w = win_of(x);
+    auto val = [&](int u, uint32_t v) -> uint32_t {      // word u from its block load, the tail, or 0
+      return u < w.u_hi ? v : (u == w.u_hi && w.straddle ? hd[192] : 0u);
+    };
 #pragma unroll
     for (int q = 0; q < kFmPer1; ++q) {
       const int u = 512 * kFmPer2 + tid + 256 * q;
       if (u >= kFmWords) continue;
-      const uint32_t v = wv[2 * kFmPer2 + q];
+      const uint32_t v = val(u, wv[2 * kFmPer2 + q]);
       const int a = fm_swz(2 * u);
       *reinterpret_cast<uint16_t*>(ph + a) = (uint16_t)(((v >> 8) & 0xFFu) | ((v >> 16) & 0xFF00u));
       *reinterpret_cast<uint16_t*>(pl + a) = (uint16_t)(((v & 0xFFu) | ((v >> 8) & 0xFF00u)) ^ 0x8080u);
@@ -278,7 +313,14 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
 #pragma unroll
     for (int q = 0; q < kFmPer2; ++q) {
       const int u = 2 * (tid + 256 * q);
-      const uint32_t v0 = wv[2 * q], v1 = wv[2 * q + 1];
+      uint32_t v0 = val(u, wv[2 * q]), v1 = val(u + 1, wv[2 * q + 1]);
+      if (q == 0 && u < w.u_lo) {                        // head words: the per-sample loads (0 before the state)
+        uint32_t hs[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hs[e] = x.n0 - x.d + 4 * tid + e >= 0 ? hd[4 * tid + e] : 0u;   // j < T1 + B here
+        v0 = hs[0] | (hs[1] << 16);
+        if (u + 1 < w.u_lo) v1 = hs[2] | (hs[3] << 16);
+      }
       const uint32_t hi = __builtin_amdgcn_perm(v1, v0, 0x07050301u);               // x >> 8 per sample
       const uint32_t lo = __builtin_amdgcn_perm(v1, v0, 0x06040200u) ^ 0x80808080u;  // (x & 255) - 128
       const int a = fm_swz(2 * u);
@@ -291,18 +333,27 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
   if (it >= items) return;
   Item cur = item_of(it);
   load_window(cur);
-  for (;;) {
+  for (int kk = 0;; ++kk) {
+    FM_STAMP(kk, 0);
     __syncthreads();                                     // the previous item's reads are done
-    stage_window();
+    FM_STAMP(kk, 1);
+    stage_window(cur);
+    FM_STAMP(kk, 2);
     __syncthreads();
+    FM_STAMP(kk, 3);
     const uint32_t nxt = it + gridDim.x;
     const Item next = item_of(nxt < items ? nxt : it);
     if (nxt < items && !MI355X_FIR_Q15_DIAG) load_window(next);   // in flight under this item's MFMAs
+    FM_STAMP(kk, 4);
 
     if (wrap) {
       fm_wrap_item(ph, pl, coeffs, T, B, cur.n0, cur.d, cur.count, tid, dst + (uint64_t)cur.f * B);
     } else if (1024 * wid < cur.count) {
-      fm_tile<KS, FAST>(imgl + cur.d * KS * 3 * 64, ph, pl, wid, L, cur.count, dst + (uint64_t)cur.f * B + cur.n0, sumc);
+      uint32_t y[8];
+      fm_tile_y<KS, FAST>(imgl + cur.d * KS * 3 * 64, ph, pl, wid, L, sumc, y);
+      FM_STAMP(kk, 5);
+      fm_tile_store(y, wid, L, cur.count, dst + (uint64_t)cur.f * B + cur.n0, ot[wid]);
+      FM_STAMP(kk, 6);
     }
     if (nxt >= items) break;
     it = nxt;
@@ -313,7 +364,9 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
 // true: launched (numTaps even, 2 .. 160, enough work to fill the chip); false: not this path
 bool fir_q15_mfma_launch(const int16_t* coeffs, int T, const int16_t* src, int16_t* dst, uint32_t B,
                          uint32_t batch, const int16_t* hist_in, hipStream_t st, bool fast) {
-  if (!(fast ? MI355X_FIR_FAST_Q15_MFMA : MI355X_FIR_Q15_MFMA) || T < 2 || (T & 1) || T > 32 * kFmMaxKS - 32 || B == 0 || batch == 0) return false;
+  if (!(fast ? MI355X_FIR_FAST_Q15_MFMA : MI355X_FIR_Q15_MFMA) || T < 2 || (T & 1) || T > 32 * kFmMaxKS - 32 || B < 64 ||
+      batch == 0)
+    return false;
   const uint32_t nchunks = (B + kFmChunk - 1) / kFmChunk;
   const uint64_t items = (uint64_t)nchunks * batch;
   if (items < 256 || items > 0x7fffffffull) return false;
