@@ -487,6 +487,8 @@ __global__ __launch_bounds__(256, 2) void fir_q31_mfma_kernel(const int32_t* __r
                                                               const int* __restrict__ info) {
   __shared__ __attribute__((aligned(16))) uint8_t pq[4][kQ31Plane];
   __shared__ __attribute__((aligned(16))) uint4 imgl[KS * 4 * 64];
+  __shared__ uint32_t hd[192];                           // the next window's history head (DMA)
+  __shared__ __attribute__((aligned(16))) uint4 ot[4][256];   // per wave: the output tile on its way out
   const int tid = threadIdx.x, L = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T1 = T - 1;
@@ -507,33 +509,40 @@ __global__ __launch_bounds__(256, 2) void fir_q31_mfma_kernel(const int32_t* __r
   };
   // window sample m = s[n0 + m] (state = [history T1 ; block B], 0 past it): thread tid takes the
   // four samples 4 (tid + 256 q) + e, each one aligned dword from a clamped, always-valid address
+  // Window samples m = 4 (tid + 256 q) + e: one dword each from a CLAMPED block-input index with no
+  // branch (as in the q15 kernel: a per-lane select between the block load and a per-sample path
+  // made the wave wait for its own loads); the history head of a filter's first item (m < T1 - n0 <=
+  // 160, wave 0's first group) lands in LDS by DMA from waves 0-2 and is merged at staging.
   uint32_t wv[4 * kQ31Groups];
   auto load_window = [&](const Item& x) {
-    const int32_t* blk = src + (uint64_t)x.f * B + x.n0 - T1;     // window sample m of the block input: blk[m]
+    const int m_lo = max(T1 - x.n0, 0), m_hi = min(T1 + (int)B - x.n0, kQ31Words);   // block samples [m_lo, m_hi)
+    const int32_t* blk = src + ((int64_t)x.f * B + x.n0 - T1);      // window sample m of the block input: blk[m]
 #pragma unroll
-    for (int q = 0; q < kQ31Groups; ++q) {
-      const int m0 = 4 * (tid + 256 * q), j0 = x.n0 + m0;
-      if (j0 >= T1 && j0 + 3 - T1 < (int)B && m0 + 3 < kQ31Words) {   // the four samples in the block input
+    for (int q = 0; q < kQ31Groups; ++q)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) wv[4 * q + e] = (uint32_t)blk[m0 + e];
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = m0 + e, j = j0 + e;
-          const bool in_h = j < T1, in_b = j >= T1 && j - T1 < (int)B;
-          const int32_t* p = in_h ? hist + (uint64_t)x.f * T1 + j : (in_b ? src + (uint64_t)x.f * B + (j - T1) : src);
-          const uint32_t v = (uint32_t)*p;
-          wv[4 * q + e] = (m < kQ31Words && (in_h || in_b)) ? v : 0u;
-        }
+      for (int e = 0; e < 4; ++e) {
+        const int m = min(max(4 * (tid + 256 * q) + e, m_lo), m_hi - 1);
+        wv[4 * q + e] = (uint32_t)blk[m];
       }
-    }
+    const int j = x.n0 + 64 * wid + L;                     // head sample 64 w + lane (waves 0-2)
+    // (numTaps 1: no history at all -- any valid address, never read)
+    const int32_t* hp = T1 > 0 ? hist + (uint64_t)x.f * T1 + min(j, T1 - 1) : src + (uint64_t)x.f * B;
+    if (wid < 3)
+      __builtin_amdgcn_global_load_lds((const void*)hp, (__attribute__((address_space(3))) void*)(hd + 64 * wid), 4, 0, 0);
   };
-  auto stage_window = [&]() {                            // 4 samples -> one 4-byte word per plane
+  auto stage_window = [&](const Item& x) {               // 4 samples -> one 4-byte word per plane
+    const int m_lo = max(T1 - x.n0, 0), m_hi = min(T1 + (int)B - x.n0, kQ31Words);
 #pragma unroll
     for (int q = 0; q < kQ31Groups; ++q) {
       const int m = 4 * (tid + 256 * q);
       if (m >= kQ31Words) continue;
-      const uint32_t s0 = wv[4 * q], s1 = wv[4 * q + 1], s2 = wv[4 * q + 2], s3 = wv[4 * q + 3];
+      uint32_t sv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int me = m + e;
+        sv[e] = me < m_lo ? (q == 0 ? hd[me] : 0u) : (me < m_hi ? wv[4 * q + e] : 0u);
+      }
+      const uint32_t s0 = sv[0], s1 = sv[1], s2 = sv[2], s3 = sv[3];
       const uint32_t u01 = __builtin_amdgcn_perm(s1, s0, 0x05010400u), u23 = __builtin_amdgcn_perm(s3, s2, 0x05010400u);
       const uint32_t v01 = __builtin_amdgcn_perm(s1, s0, 0x07030602u), v23 = __builtin_amdgcn_perm(s3, s2, 0x07030602u);
       const int a = fm_swz(m);
@@ -554,8 +563,8 @@ __global__ __launch_bounds__(256, 2) void fir_q31_mfma_kernel(const int32_t* __r
   Item cur = item_of(it);
   load_window(cur);
   for (;;) {
-    __syncthreads();                                     // the previous item's reads are done
-    stage_window();
+    __syncthreads();                                     // the previous item's reads (and the head DMA's landing)
+    stage_window(cur);
     __syncthreads();
     const uint32_t nxt = it + gridDim.x;
     const Item next = item_of(nxt < items ? nxt : it);
@@ -625,9 +634,22 @@ __global__ __launch_bounds__(256, 2) void fir_q31_mfma_kernel(const int32_t* __r
       }
       int32_t* yb = yf + ob;
       if (cur.count == kFmChunk && ((((uintptr_t)yf) & 15) == 0)) {
+        // through the wave's 4 KiB LDS slot (16-B chunk c = 8 j + 2 q + h, XOR-swizzled), then four
+        // coalesced 1 KiB stores
+        uint4* otw = ot[wid];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          *reinterpret_cast<uint4*>(yb + 8 * q) = make_uint4(y[4 * q], y[4 * q + 1], y[4 * q + 2], y[4 * q + 3]);
+        for (int q = 0; q < 4; ++q) {
+          const int c = 8 * j + 2 * q + h;
+          otw[c ^ ((c >> 4) & 7)] = make_uint4(y[4 * q], y[4 * q + 1], y[4 * q + 2], y[4 * q + 3]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 64 * r + L;
+          *reinterpret_cast<uint4*>(yf + 1024 * wid + 4 * c) = otw[c ^ ((c >> 4) & 7)];
+        }
       } else {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -711,6 +733,8 @@ __global__ __launch_bounds__(256) void fir_q7_mfma_kernel(int T, const int8_t* _
                                                           uint32_t items, const uint4* __restrict__ image) {
   __shared__ __attribute__((aligned(16))) uint8_t pw[kQ7Plane];
   __shared__ __attribute__((aligned(16))) uint4 imgl[4 * KS * 64];
+  __shared__ uint32_t hd[256];                           // the next window's head samples [0, 192) and tail word samples [192, 196)
+  __shared__ __attribute__((aligned(16))) uint32_t ot[4][256];   // per wave: the output tile on its way out
   const int tid = threadIdx.x, L = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T1 = T - 1;
@@ -725,35 +749,54 @@ __global__ __launch_bounds__(256) void fir_q7_mfma_kernel(int T, const int8_t* _
     x.d = (int)(((uint64_t)x.f * B + (uint32_t)x.n0 - (uint32_t)T1) & 3u);   // w[m] = s[n0 - d + m]
     return x;
   };
+  // Window words (4 samples) from CLAMPED aligned block-input words, no branch; the words not wholly
+  // in the block input -- the history head of a filter's first item and the block's last partial
+  // word -- from per-sample LDS DMA (ubyte, zero-extended to a dword per lane): waves 0-2 head samples
+  // 64 w + lane, wave 3 (lanes 0-3) the four samples of word u_hi.  As in the q15 kernel.
+  struct Win { int u_lo, u_hi; };
+  auto win_of = [&](const Item& x) {
+    Win w;
+    const int lo_num = T1 - x.n0 + x.d, hi_num = T1 + (int)B - 4 - x.n0 + x.d;
+    w.u_lo = lo_num > 0 ? (lo_num + 3) >> 2 : 0;
+    w.u_hi = hi_num >= 0 ? (hi_num >> 2) + 1 : 0;
+    return w;
+  };
   uint32_t wv[kQ7Per];
   auto load_window = [&](const Item& x) {
+    const Win w = win_of(x);
     const int8_t* blk = src + ((int64_t)x.f * B + x.n0 - x.d - T1);      // w[m] of the block input: blk[m] (aligned)
+    // clamped to the aligned dwords inside this filter's block (never empty: blockSize >= 64)
+    const uintptr_t lo_a = ((uintptr_t)(src + (uint64_t)x.f * B) + 3) & ~(uintptr_t)3;
+    const uintptr_t hi_a = ((uintptr_t)(src + (uint64_t)(x.f + 1) * B) & ~(uintptr_t)3) - 4;
 #pragma unroll
     for (int q = 0; q < kQ7Per; ++q) {
-      const int u = tid + 256 * q, j0 = x.n0 - x.d + 4 * u;
-      if (u >= kQ7Words) {
-        wv[q] = 0u;
-      } else if (j0 >= T1 && j0 + 3 - T1 < (int)B) {                     // four samples in the block input
-        wv[q] = *reinterpret_cast<const uint32_t*>(blk + 4 * u);
-      } else {
-        uint32_t r = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int j = j0 + e;
-          const bool in_h = j >= 0 && j < T1, in_b = j >= T1 && j - T1 < (int)B;
-          const int8_t* p = in_h ? hist + (uint64_t)x.f * T1 + j : (in_b ? src + (uint64_t)x.f * B + (j - T1) : src);
-          const uint32_t v = (uint8_t)*p;
-          r |= ((in_h || in_b) ? v : 0u) << (8 * e);
-        }
-        wv[q] = r;
-      }
+      const uintptr_t ad = (uintptr_t)(blk + 4 * (tid + 256 * q));
+      wv[q] = *reinterpret_cast<const uint32_t*>(ad < lo_a ? lo_a : (ad > hi_a ? hi_a : ad));
     }
+    const int m = wid < 3 ? 64 * wid + L : 4 * w.u_hi + min(L, 3);
+    const int j = x.n0 - x.d + m;                          // state index of window sample m
+    const bool in_h = j >= 0 && j < T1;
+    const int8_t* p = in_h ? hist + (uint64_t)x.f * T1 + j : src + (uint64_t)x.f * B + min(max(j - T1, 0), (int)B - 1);
+    __builtin_amdgcn_global_load_lds((const void*)p, (__attribute__((address_space(3))) void*)(hd + 64 * wid), 1, 0, 0);
   };
-  auto stage_window = [&]() {
+  auto stage_window = [&](const Item& x) {
+    const Win w = win_of(x);
 #pragma unroll
     for (int q = 0; q < kQ7Per; ++q) {
       const int u = tid + 256 * q;
-      if (u < kQ7Words) *reinterpret_cast<uint32_t*>(pw + fm_swz(4 * u)) = wv[q];
+      if (u >= kQ7Words) continue;
+      uint32_t v = wv[q];
+      if (u < w.u_lo || u >= w.u_hi) {                   // per-sample: head (hd[m]) or the tail word (hd[192 + e])
+        v = 0u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = x.n0 - x.d + 4 * u + e;
+          const bool valid = j >= 0 && j - T1 < (int)B;
+          const uint32_t sm = u < w.u_lo ? hd[min(4 * u + e, 191)] : (u == w.u_hi ? hd[192 + e] : 0u);
+          v |= (valid ? (sm & 255u) : 0u) << (8 * e);
+        }
+      }
+      *reinterpret_cast<uint32_t*>(pw + fm_swz(4 * u)) = v;
     }
   };
 
@@ -762,8 +805,8 @@ __global__ __launch_bounds__(256) void fir_q7_mfma_kernel(int T, const int8_t* _
   Item cur = item_of(it);
   load_window(cur);
   for (;;) {
-    __syncthreads();                                     // the previous item's reads are done
-    stage_window();
+    __syncthreads();                                     // the previous item's reads (and the DMA's landing)
+    stage_window(cur);
     __syncthreads();
     const uint32_t nxt = it + gridDim.x;
     const Item next = item_of(nxt < items ? nxt : it);
@@ -791,9 +834,24 @@ __global__ __launch_bounds__(256) void fir_q7_mfma_kernel(int T, const int8_t* _
         for (int e = 0; e < 4; ++e) v |= (uint32_t)(uint8_t)(int8_t)ssat8(acc[4 * q + e] >> 7) << (8 * e);
         y[q] = v;
       }
-      if (cur.count == kFmChunk && ((((uintptr_t)yf) & 3) == 0)) {
+      if (cur.count == kFmChunk && ((((uintptr_t)yf) & 15) == 0)) {
+        // through the wave's 1 KiB LDS slot (dword 8 j + 2 q + h), then one coalesced 1 KiB store
+        uint32_t* otw = ot[wid];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) *reinterpret_cast<uint32_t*>(yf + ob + 8 * q) = y[q];
+        for (int q = 0; q < 4; ++q) {
+          const int c = 8 * j + 2 * q + h;
+          otw[c ^ (((c >> 5) & 7) << 2)] = y[q];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t r[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 4 * L + e;
+          r[e] = otw[c ^ (((c >> 5) & 7) << 2)];
+        }
+        *reinterpret_cast<uint4*>(yf + 1024 * wid + 16 * L) = make_uint4(r[0], r[1], r[2], r[3]);
       } else {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -811,7 +869,7 @@ __global__ __launch_bounds__(256) void fir_q7_mfma_kernel(int T, const int8_t* _
 // true: launched (numTaps 1 .. 157, enough work to fill the chip); false: not this path
 bool fir_q7_mfma_launch(const int8_t* coeffs, int T, const int8_t* src, int8_t* dst, uint32_t B, uint32_t batch,
                         const int8_t* hist_in, hipStream_t st) {
-  if (!MI355X_FIR_Q7_MFMA || T < 1 || T > 32 * kFmMaxKS - 35 || B == 0 || batch == 0) return false;
+  if (!MI355X_FIR_Q7_MFMA || T < 1 || T > 32 * kFmMaxKS - 35 || B < 64 || batch == 0) return false;
   const uint32_t nchunks = (B + kFmChunk - 1) / kFmChunk;
   const uint64_t items = (uint64_t)nchunks * batch;
   if (items < 256 || items > 0x7fffffffull) return false;
