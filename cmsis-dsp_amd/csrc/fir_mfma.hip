@@ -47,6 +47,9 @@
 #define MI355X_FIR_Q15_MFMA_WG 3
 #endif
 
+#ifndef MI355X_FIR_Q31_ALN        // fir_q31: the 16-B aligned window mode when the shapes allow it
+#define MI355X_FIR_Q31_ALN 1
+#endif
 #ifndef MI355X_FIR_STAMP
 #define MI355X_FIR_STAMP 0
 #endif
@@ -432,7 +435,7 @@ __device__ __forceinline__ int64_t q31_tap_carried(int32_t c) {   // c' of the t
 // image[ks][digit][lane]: the 16 digit bytes lane L = (i = L & 31, h = L >> 5) passes as the A operand
 // at K step ks (taps c'[32 ks + 16 h + e - i]); info: [0, 1] sum c' (int64), [2] number of big taps,
 // [3 ..] their indices (first kQ31MaxBig)
-__global__ __launch_bounds__(256) void fir_q31_coef_image_kernel(const int32_t* __restrict__ coeffs, int T, int KS,
+__global__ __launch_bounds__(256) void fir_q31_coef_image_kernel(const int32_t* __restrict__ coeffs, int T, int KS, int d,
                                                                  uint4* __restrict__ image, int* __restrict__ info) {
   const int g = blockIdx.x * 256 + threadIdx.x;
   if (g < KS * 64) {
@@ -440,7 +443,7 @@ __global__ __launch_bounds__(256) void fir_q31_coef_image_kernel(const int32_t* 
     uint32_t w[4][4] = {};
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int ci = 32 * ks + 16 * h + e - i;
+      const int ci = 32 * ks + 16 * h + e - d - i;      // window shifted d samples early (aligned mode)
       int64_t v = (ci >= 0 && ci < T) ? q31_tap_carried(coeffs[ci]) : 0;
 #pragma unroll
       for (int dgt = 0; dgt < 4; ++dgt) {
@@ -478,8 +481,12 @@ __global__ __launch_bounds__(256) void fir_q31_coef_image_kernel(const int32_t* 
   }
 }
 
-template <int KS>
-__global__ __launch_bounds__(256, 2) void fir_q31_mfma_kernel(const int32_t* __restrict__ coeffs, int T,
+// ALN: blockSize % 4 == 0 and 16-B aligned data -- the window starts d = (-T1) mod 4 samples early so
+// that its history / block / tail regions all begin on 16-B boundaries, and it is loaded as dwordx4
+// (five instructions per thread and item instead of twenty dword loads: vector-memory instruction
+// issue, ~40-100 cycles each under this load, was a large share of an item; MI355X_MICROARCH.md).
+template <int KS, bool ALN>
+__global__ __launch_bounds__(256, 2) void fir_q31_mfma_kernel(const int32_t* __restrict__ coeffs, int T, int d,
                                                               const int32_t* __restrict__ src, int32_t* __restrict__ dst,
                                                               uint32_t B, const int32_t* __restrict__ hist,
                                                               uint32_t nchunks, uint32_t items,
@@ -515,23 +522,33 @@ __global__ __launch_bounds__(256, 2) void fir_q31_mfma_kernel(const int32_t* __r
   // 160, wave 0's first group) lands in LDS by DMA from waves 0-2 and is merged at staging.
   uint32_t wv[4 * kQ31Groups];
   auto load_window = [&](const Item& x) {
-    const int m_lo = max(T1 - x.n0, 0), m_hi = min(T1 + (int)B - x.n0, kQ31Words);   // block samples [m_lo, m_hi)
-    const int32_t* blk = src + ((int64_t)x.f * B + x.n0 - T1);      // window sample m of the block input: blk[m]
+    const int m_lo = max(T1 - x.n0 + d, 0), m_hi = min(T1 + (int)B - x.n0 + d, kQ31Words);   // block samples [m_lo, m_hi)
+    const int32_t* blk = src + ((int64_t)x.f * B + x.n0 - d - T1);  // window sample m of the block input: blk[m]
 #pragma unroll
-    for (int q = 0; q < kQ31Groups; ++q)
+    for (int q = 0; q < kQ31Groups; ++q) {
+      if constexpr (ALN) {                                 // m_lo, m_hi, blk: multiples of 4 samples / 16 B
+        const int m = min(max(4 * (tid + 256 * q), m_lo), m_hi - 4);
+        const uint4 v = *reinterpret_cast<const uint4*>(blk + m);
+        wv[4 * q] = v.x;
+        wv[4 * q + 1] = v.y;
+        wv[4 * q + 2] = v.z;
+        wv[4 * q + 3] = v.w;
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int m = min(max(4 * (tid + 256 * q) + e, m_lo), m_hi - 1);
-        wv[4 * q + e] = (uint32_t)blk[m];
+        for (int e = 0; e < 4; ++e) {
+          const int m = min(max(4 * (tid + 256 * q) + e, m_lo), m_hi - 1);
+          wv[4 * q + e] = (uint32_t)blk[m];
+        }
       }
-    const int j = x.n0 + 64 * wid + L;                     // head sample 64 w + lane (waves 0-2)
+    }
+    const int j = x.n0 - d + 64 * wid + L;                 // head sample 64 w + lane (waves 0-2)
     // (numTaps 1: no history at all -- any valid address, never read)
-    const int32_t* hp = T1 > 0 ? hist + (uint64_t)x.f * T1 + min(j, T1 - 1) : src + (uint64_t)x.f * B;
+    const int32_t* hp = T1 > 0 ? hist + (uint64_t)x.f * T1 + min(max(j, 0), T1 - 1) : src + (uint64_t)x.f * B;
     if (wid < 3)
       __builtin_amdgcn_global_load_lds((const void*)hp, (__attribute__((address_space(3))) void*)(hd + 64 * wid), 4, 0, 0);
   };
   auto stage_window = [&](const Item& x) {               // 4 samples -> one 4-byte word per plane
-    const int m_lo = max(T1 - x.n0, 0), m_hi = min(T1 + (int)B - x.n0, kQ31Words);
+    const int m_lo = max(T1 - x.n0 + d, 0), m_hi = min(T1 + (int)B - x.n0 + d, kQ31Words);
 #pragma unroll
     for (int q = 0; q < kQ31Groups; ++q) {
       const int m = 4 * (tid + 256 * q);
@@ -539,8 +556,8 @@ __global__ __launch_bounds__(256, 2) void fir_q31_mfma_kernel(const int32_t* __r
       uint32_t sv[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int me = m + e;
-        sv[e] = me < m_lo ? (q == 0 ? hd[me] : 0u) : (me < m_hi ? wv[4 * q + e] : 0u);
+        const int me = m + e;                            // head: 0 before the state (j < 0)
+        sv[e] = me < m_lo ? (q == 0 && me >= d - x.n0 ? hd[me] : 0u) : (me < m_hi ? wv[4 * q + e] : 0u);
       }
       const uint32_t s0 = sv[0], s1 = sv[1], s2 = sv[2], s3 = sv[3];
       const uint32_t u01 = __builtin_amdgcn_perm(s1, s0, 0x05010400u), u23 = __builtin_amdgcn_perm(s3, s2, 0x05010400u);
@@ -574,7 +591,7 @@ __global__ __launch_bounds__(256, 2) void fir_q31_mfma_kernel(const int32_t* __r
       // exact per-output path (arm_fir_q31.c: q63 sum of exact products, y = acc >> 31)
       for (int o = tid; o < cur.count; o += 256) {
         uint64_t acc = 0;
-        for (int t = 0; t < T; ++t) acc += (uint64_t)((int64_t)xs(o + t) * coeffs[t]);
+        for (int t = 0; t < T; ++t) acc += (uint64_t)((int64_t)xs(o + d + t) * coeffs[t]);
         yf[o] = (int32_t)(uint32_t)(acc >> 31);
       }
     } else if (1024 * wid < cur.count) {
@@ -629,7 +646,7 @@ __global__ __launch_bounds__(256, 2) void fir_q31_mfma_kernel(const int32_t* __r
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
           const int o = ob + 8 * (g >> 2) + (g & 3);
-          for (int b = 0; b < nbig; ++b) y[g] += xs(o + big[b]);   // mod 2^32, as the reference's (q31_t) cast
+          for (int b = 0; b < nbig; ++b) y[g] += xs(o + d + big[b]);   // mod 2^32, as the reference's (q31_t) cast
         }
       }
       int32_t* yb = yf + ob;
@@ -672,17 +689,23 @@ bool fir_q31_mfma_launch(const int32_t* coeffs, int T, const int32_t* src, int32
   const uint64_t items = (uint64_t)nchunks * batch;
   if (items < 256 || items > 0x7fffffffull) return false;
   const int ks = (T + 31 + 31) / 32;
+  // aligned mode: the shift d = (-T1) mod 4 puts every region of every window on a 16-B boundary;
+  // taken when blockSize % 4 == 0, the pointers are 16-B aligned and the shift costs no K step
+  const int d4 = (4 - (T - 1) % 4) % 4;
+  const bool aln = MI355X_FIR_Q31_ALN && B % 4 == 0 && ((uintptr_t)src & 15) == 0 && (T + 31 + d4 + 31) / 32 == ks;
+  const int d = aln ? d4 : 0;
   const size_t img_bytes = (size_t)ks * 4 * 64 * 16;
   void* buf = nullptr;
   if (hipMallocAsync(&buf, img_bytes + 32, st) != hipSuccess) return false;
   uint4* img = (uint4*)buf;
   int* info = (int*)((char*)buf + img_bytes);
-  hipLaunchKernelGGL(fir_q31_coef_image_kernel, dim3((ks * 64 + 255) / 256), dim3(256), 0, st, coeffs, T, ks, img, info);
+  hipLaunchKernelGGL(fir_q31_coef_image_kernel, dim3((ks * 64 + 255) / 256), dim3(256), 0, st, coeffs, T, ks, d, img, info);
 #define FQ_CASE(K)                                                                                              \
   case K: {                                                                                                     \
-    const int g = persistent_grid((const void*)fir_q31_mfma_kernel<K>, 256, 0, items);                         \
-    hipLaunchKernelGGL(fir_q31_mfma_kernel<K>, dim3(g), dim3(256), 0, st, coeffs, T, src, dst, B, hist_in,       \
-                       nchunks, (uint32_t)items, (const uint4*)img, (const int*)info);                          \
+    auto kern = aln ? fir_q31_mfma_kernel<K, true> : fir_q31_mfma_kernel<K, false>;                             \
+    const int g = persistent_grid((const void*)kern, 256, 0, items);                                            \
+    hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, st, coeffs, T, d, src, dst, B, hist_in, nchunks,            \
+                       (uint32_t)items, (const uint4*)img, (const int*)info);                                   \
     break;                                                                                                      \
   }
   switch (ks) {
