@@ -47,6 +47,9 @@
 #define MI355X_FIR_Q15_MFMA_WG 3
 #endif
 
+#ifndef MI355X_FIR_Q15_ALN        // fir_q15 / fast_q15: the 16-B aligned window mode when the shapes allow it
+#define MI355X_FIR_Q15_ALN 1
+#endif
 #ifndef MI355X_FIR_Q31_ALN        // fir_q31: the 16-B aligned window mode when the shapes allow it
 #define MI355X_FIR_Q31_ALN 1
 #endif
@@ -90,7 +93,7 @@ __device__ __forceinline__ int fm_swz(int m) {  // byte m of a plane -> LDS byte
 // plane bytes of c[32 ks + 16 h + e - d - i], e = 0 .. 15 (0 outside the taps).  Also [2] words:
 // sum(c) and whether a (-32768, -32768) tap pair is present.
 __global__ __launch_bounds__(256) void fir_q15_coef_image_kernel(const int16_t* __restrict__ coeffs, int T, int KS,
-                                                                 uint4* __restrict__ image, int* __restrict__ info) {
+                                                                 int d_base, uint4* __restrict__ image, int* __restrict__ info) {
   // one thread per (d, ks, lane): 2 KS x 64 threads, each the three planes' 16 bytes; the last
   // workgroup's first wave also reduces sum(c) and the wrap flag
   const int g = blockIdx.x * 256 + threadIdx.x;
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(256) void fir_q15_coef_image_kernel(const int16_t* 
     uint32_t w[3][4] = {};
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int ci = 32 * ks + 16 * h + e - d - i;
+      const int ci = 32 * ks + 16 * h + e - (d_base + d) - i;   // slot d holds window shift d_base + d
       const int32_t c = (ci >= 0 && ci < T) ? coeffs[ci] : 0;
       w[0][e >> 2] |= (uint32_t)(uint8_t)(int8_t)(64 * (c >> 14)) << (8 * (e & 3));
       w[1][e >> 2] |= (uint32_t)((c >> 7) & 127) << (8 * (e & 3));
@@ -223,8 +226,11 @@ __device__ __forceinline__ void fm_tile_store(const uint32_t (&y)[8], int wid, i
 
 // FAST: arm_fir_fast_q15 (arm_fir_fast_q15.c: the same products summed in a wrapping q31_t, no
 // pair-wrap special case since everything is mod 2^32)
-template <int KS, bool FAST>
-__global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kernel(const int16_t* __restrict__ coeffs, int T,
+// ALN: blockSize % 8 == 0 and 16-B aligned data -- every window starts d_base = (-T1) mod 8 samples early,
+// so its history / block regions begin on 16-B boundaries and it is loaded as three dwordx4 per
+// thread instead of nine dword loads (the image's slot 0 is that shift).
+template <int KS, bool FAST, bool ALN>
+__global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kernel(const int16_t* __restrict__ coeffs, int T, int d_base,
                                                               const int16_t* __restrict__ src, int16_t* __restrict__ dst,
                                                               uint32_t B, const int16_t* __restrict__ hist,
                                                               uint32_t nchunks, uint32_t items,
@@ -250,7 +256,7 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
     x.f = it / nchunks;
     x.n0 = (int)(it - x.f * nchunks) * kFmChunk;
     x.count = min((int)B - x.n0, kFmChunk);
-    x.d = (int)(((uint64_t)x.f * B + (uint32_t)x.n0 - (uint32_t)T1) & 1u);   // s index n0 - d + m -> src f B + n0 - d + m - T1
+    x.d = ALN ? d_base : (int)(((uint64_t)x.f * B + (uint32_t)x.n0 - (uint32_t)T1) & 1u);   // s index n0 - d + m -> src f B + n0 - d + m - T1
     return x;
   };
   // Window words in PAIRS: thread tid takes words 2 (tid + 256 q) and + 1 (4 samples, one 4-byte
@@ -271,10 +277,27 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
     w.straddle = x.n0 - x.d + 2 * w.u_hi == T1 + (int)B - 1 && w.u_hi < kFmWords;   // word u_hi = (last sample, 0)
     return w;
   };
-  uint32_t wv[2 * kFmPer2 + kFmPer1];
+  uint32_t wv[ALN ? 12 : 2 * kFmPer2 + kFmPer1];
+  auto aln_bounds = [&](const Item& x, int& m_lo, int& m_hi) {   // block samples of the window (multiples of 8)
+    m_lo = max(T1 - x.n0 + x.d, 0);
+    m_hi = min(T1 + (int)B - x.n0 + x.d, 2 * kFmWords);
+  };
   auto load_window = [&](const Item& x) {
     const Win w = win_of(x);
     const int64_t base = (int64_t)x.f * B + x.n0 - x.d - T1;               // src index of w[0] (even)
+    if constexpr (ALN) {
+      int m_lo, m_hi;
+      aln_bounds(x, m_lo, m_hi);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int m = min(max(8 * (tid + 256 * q), m_lo), m_hi - 8);
+        const uint4 v = *reinterpret_cast<const uint4*>(src + base + m);
+        wv[4 * q] = v.x;
+        wv[4 * q + 1] = v.y;
+        wv[4 * q + 2] = v.z;
+        wv[4 * q + 3] = v.w;
+      }
+    } else {
     auto word = [&](int u) -> uint32_t {
       const int uc = min(max(u, w.u_lo), w.u_hi - 1);
       return *reinterpret_cast<const uint32_t*>(src + base + 2 * uc);
@@ -286,6 +309,7 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
     }
 #pragma unroll
     for (int q = 0; q < kFmPer1; ++q) wv[2 * kFmPer2 + q] = word(min(512 * kFmPer2 + tid + 256 * q, kFmWords - 1));
+    }
     // The head samples and the tail sample go to LDS by DMA (one zero-extended dword per lane,
     // tools/probes/lds_dma_sub.hip): waves 0-2 samples 64 w + lane, wave 3 the block's last sample.
     // No register receives them, so nothing here waits; barrier A's vmcnt(0) lands them.
@@ -297,6 +321,36 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
       const uint64_t pa = (wid < 3 && in_h) ? ph_ : pb_;
       __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)pa, (__attribute__((address_space(3))) void*)(hd + 64 * wid),
                                        2, 0, 0);
+    }
+  };
+  auto stage_window_aln = [&](const Item& x) {           // ALN: 8 samples -> 8 bytes per plane
+    int m_lo, m_hi;
+    aln_bounds(x, m_lo, m_hi);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int m0 = 8 * (tid + 256 * q);
+      if (m0 >= 2 * kFmWords) continue;
+      uint32_t w4[4];
+      if (m0 < m_lo) {                                   // history head (wave 0): the DMA'd samples, 0 before the state
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int m = m0 + 2 * k;
+          const uint32_t s0 = x.n0 - x.d + m >= 0 ? hd[m] : 0u, s1 = x.n0 - x.d + m + 1 >= 0 ? hd[m + 1] : 0u;
+          w4[k] = s0 | (s1 << 16);
+        }
+      } else if (m0 < m_hi) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w4[k] = wv[4 * q + k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w4[k] = 0u;
+      }
+      const uint32_t h0 = __builtin_amdgcn_perm(w4[1], w4[0], 0x07050301u), h1 = __builtin_amdgcn_perm(w4[3], w4[2], 0x07050301u);
+      const uint32_t l0 = __builtin_amdgcn_perm(w4[1], w4[0], 0x06040200u) ^ 0x80808080u;
+      const uint32_t l1 = __builtin_amdgcn_perm(w4[3], w4[2], 0x06040200u) ^ 0x80808080u;
+      const int a = fm_swz(m0);
+      *reinterpret_cast<uint2*>(ph + a) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(pl + a) = make_uint2(l0, l1);
     }
   };
   auto stage_window = [&](const Item& x) {               // registers -> the two byte planes
@@ -340,7 +394,7 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
     FM_STAMP(kk, 0);
     __syncthreads();                                     // the previous item's reads are done
     FM_STAMP(kk, 1);
-    stage_window(cur);
+    if constexpr (ALN) stage_window_aln(cur); else stage_window(cur);
     FM_STAMP(kk, 2);
     __syncthreads();
     FM_STAMP(kk, 3);
@@ -353,7 +407,7 @@ __global__ __launch_bounds__(256, MI355X_FIR_Q15_MFMA_WG) void fir_q15_mfma_kern
       fm_wrap_item(ph, pl, coeffs, T, B, cur.n0, cur.d, cur.count, tid, dst + (uint64_t)cur.f * B);
     } else if (1024 * wid < cur.count) {
       uint32_t y[8];
-      fm_tile_y<KS, FAST>(imgl + cur.d * KS * 3 * 64, ph, pl, wid, L, sumc, y);
+      fm_tile_y<KS, FAST>(imgl + (cur.d - d_base) * KS * 3 * 64, ph, pl, wid, L, sumc, y);
       FM_STAMP(kk, 5);
       fm_tile_store(y, wid, L, cur.count, dst + (uint64_t)cur.f * B + cur.n0, ot[wid]);
       FM_STAMP(kk, 6);
@@ -374,18 +428,25 @@ bool fir_q15_mfma_launch(const int16_t* coeffs, int T, const int16_t* src, int16
   const uint64_t items = (uint64_t)nchunks * batch;
   if (items < 256 || items > 0x7fffffffull) return false;
   const int ks = (T + 32 + 31) / 32;
+  // aligned mode: shift d8 = (-T1) mod 8 when blockSize % 8 == 0, the data is 16-B aligned and the
+  // shift costs no K step (K >= numTaps - 1 + d8 + 31 + 1)
+  const int d8 = (8 - (T - 1) % 8) % 8;
+  const bool aln = MI355X_FIR_Q15_ALN && B % 8 == 0 && ((uintptr_t)src & 15) == 0 && (T + d8 + 31 + 31) / 32 <= ks;
+  const int d_base = aln ? d8 : 0;
   // the coefficient image (2 shifts x KS steps x 3 planes x 64 lanes x 16 B) and [sum, wrap]
   const size_t img_bytes = (size_t)2 * ks * 3 * 64 * 16;
   void* buf = nullptr;
   if (hipMallocAsync(&buf, img_bytes + 16, st) != hipSuccess) return false;
   uint4* img = (uint4*)buf;
   int* info = (int*)((char*)buf + img_bytes);
-  hipLaunchKernelGGL(fir_q15_coef_image_kernel, dim3((2 * ks * 64 + 255) / 256), dim3(256), 0, st, coeffs, T, ks, img, info);
+  hipLaunchKernelGGL(fir_q15_coef_image_kernel, dim3((2 * ks * 64 + 255) / 256), dim3(256), 0, st, coeffs, T, ks, d_base,
+                     img, info);
 #define FM_CASE(K)                                                                                              \
   case K: {                                                                                                     \
-    auto kern = fast ? fir_q15_mfma_kernel<K, true> : fir_q15_mfma_kernel<K, false>;                            \
+    auto kern = fast ? (aln ? fir_q15_mfma_kernel<K, true, true> : fir_q15_mfma_kernel<K, true, false>)          \
+                     : (aln ? fir_q15_mfma_kernel<K, false, true> : fir_q15_mfma_kernel<K, false, false>);      \
     const int g = persistent_grid((const void*)kern, 256, 0, items);                                            \
-    hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, st, coeffs, T, src, dst, B, hist_in, nchunks,              \
+    hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, st, coeffs, T, d_base, src, dst, B, hist_in, nchunks,      \
                        (uint32_t)items, (const uint4*)img, (const int*)info);                                   \
     break;                                                                                                      \
   }
