@@ -50,6 +50,9 @@
 #ifndef MI355X_FIR_Q15_ALN        // fir_q15 / fast_q15: the 16-B aligned window mode when the shapes allow it
 #define MI355X_FIR_Q15_ALN 1
 #endif
+#ifndef MI355X_FIR_Q7_ALN         // fir_q7: the 16-B aligned window mode when the shapes allow it
+#define MI355X_FIR_Q7_ALN 1
+#endif
 #ifndef MI355X_FIR_Q31_ALN        // fir_q31: the 16-B aligned window mode when the shapes allow it
 #define MI355X_FIR_Q31_ALN 1
 #endif
@@ -798,21 +801,23 @@ constexpr int kQ7Plane = 4 * kQ7Words + 256;
 
 // image[d][ks][lane]: taps c[32 ks + 16 h + e - d - i] as the A operand (lane L: i = L & 31, h = L >> 5)
 __global__ __launch_bounds__(256) void fir_q7_coef_image_kernel(const int8_t* __restrict__ coeffs, int T, int KS,
-                                                                uint4* __restrict__ image) {
+                                                                int d_base, uint4* __restrict__ image) {
   const int g = blockIdx.x * 256 + threadIdx.x;
   if (g >= 4 * KS * 64) return;
   const int L = g & 63, ks = (g >> 6) % KS, d = (g >> 6) / KS, i = L & 31, h = L >> 5;
   uint32_t w[4] = {};
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    const int ci = 32 * ks + 16 * h + e - d - i;
+    const int ci = 32 * ks + 16 * h + e - (d_base + d) - i;   // slot d holds window shift d_base + d
     w[e >> 2] |= (uint32_t)(uint8_t)((ci >= 0 && ci < T) ? coeffs[ci] : 0) << (8 * (e & 3));
   }
   image[(d * KS + ks) * 64 + L] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-template <int KS>
-__global__ __launch_bounds__(256) void fir_q7_mfma_kernel(int T, const int8_t* __restrict__ src, int8_t* __restrict__ dst,
+// ALN: blockSize % 16 == 0 and 16-B aligned data -- the window starts d_base = (-T1) mod 16 samples
+// early (image slot 0), every region begins on a 16-B boundary, two dwordx4 loads per thread.
+template <int KS, bool ALN>
+__global__ __launch_bounds__(256) void fir_q7_mfma_kernel(int T, int d_base, const int8_t* __restrict__ src, int8_t* __restrict__ dst,
                                                           uint32_t B, const int8_t* __restrict__ hist, uint32_t nchunks,
                                                           uint32_t items, const uint4* __restrict__ image) {
   __shared__ __attribute__((aligned(16))) uint8_t pw[kQ7Plane];
@@ -830,7 +835,7 @@ __global__ __launch_bounds__(256) void fir_q7_mfma_kernel(int T, const int8_t* _
     x.f = it / nchunks;
     x.n0 = (int)(it - x.f * nchunks) * kFmChunk;
     x.count = min((int)B - x.n0, kFmChunk);
-    x.d = (int)(((uint64_t)x.f * B + (uint32_t)x.n0 - (uint32_t)T1) & 3u);   // w[m] = s[n0 - d + m]
+    x.d = ALN ? d_base : (int)(((uint64_t)x.f * B + (uint32_t)x.n0 - (uint32_t)T1) & 3u);   // w[m] = s[n0 - d + m]
     return x;
   };
   // Window words (4 samples) from CLAMPED aligned block-input words, no branch; the words not wholly
@@ -845,10 +850,27 @@ __global__ __launch_bounds__(256) void fir_q7_mfma_kernel(int T, const int8_t* _
     w.u_hi = hi_num >= 0 ? (hi_num >> 2) + 1 : 0;
     return w;
   };
-  uint32_t wv[kQ7Per];
+  uint32_t wv[ALN ? 8 : kQ7Per];
+  auto aln_bounds = [&](const Item& x, int& m_lo, int& m_hi) {   // block samples of the window (multiples of 16)
+    m_lo = max(T1 - x.n0 + x.d, 0);
+    m_hi = min(T1 + (int)B - x.n0 + x.d, 4 * kQ7Words);
+  };
   auto load_window = [&](const Item& x) {
     const Win w = win_of(x);
     const int8_t* blk = src + ((int64_t)x.f * B + x.n0 - x.d - T1);      // w[m] of the block input: blk[m] (aligned)
+    if constexpr (ALN) {
+      int m_lo, m_hi;
+      aln_bounds(x, m_lo, m_hi);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int m = min(max(16 * (tid + 256 * q), m_lo), m_hi - 16);
+        const uint4 v = *reinterpret_cast<const uint4*>(blk + m);
+        wv[4 * q] = v.x;
+        wv[4 * q + 1] = v.y;
+        wv[4 * q + 2] = v.z;
+        wv[4 * q + 3] = v.w;
+      }
+    } else {
     // clamped to the aligned dwords inside this filter's block (never empty: blockSize >= 64)
     const uintptr_t lo_a = ((uintptr_t)(src + (uint64_t)x.f * B) + 3) & ~(uintptr_t)3;
     const uintptr_t hi_a = ((uintptr_t)(src + (uint64_t)(x.f + 1) * B) & ~(uintptr_t)3) - 4;
@@ -857,11 +879,41 @@ __global__ __launch_bounds__(256) void fir_q7_mfma_kernel(int T, const int8_t* _
       const uintptr_t ad = (uintptr_t)(blk + 4 * (tid + 256 * q));
       wv[q] = *reinterpret_cast<const uint32_t*>(ad < lo_a ? lo_a : (ad > hi_a ? hi_a : ad));
     }
+    }
     const int m = wid < 3 ? 64 * wid + L : 4 * w.u_hi + min(L, 3);
     const int j = x.n0 - x.d + m;                          // state index of window sample m
     const bool in_h = j >= 0 && j < T1;
     const int8_t* p = in_h ? hist + (uint64_t)x.f * T1 + j : src + (uint64_t)x.f * B + min(max(j - T1, 0), (int)B - 1);
     __builtin_amdgcn_global_load_lds((const void*)p, (__attribute__((address_space(3))) void*)(hd + 64 * wid), 1, 0, 0);
+  };
+  auto stage_window_aln = [&](const Item& x) {           // ALN: 16 samples -> one 16-B slot
+    int m_lo, m_hi;
+    aln_bounds(x, m_lo, m_hi);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int m0 = 16 * (tid + 256 * q);
+      if (m0 >= 4 * kQ7Words) continue;
+      uint32_t w4[4];
+      if (m0 < m_lo) {                                   // history head (wave 0): the DMA'd samples, 0 before the state
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          uint32_t v = 0u;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int m = m0 + 4 * k + e;
+            v |= (x.n0 - x.d + m >= 0 ? (hd[m] & 255u) : 0u) << (8 * e);
+          }
+          w4[k] = v;
+        }
+      } else if (m0 < m_hi) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w4[k] = wv[4 * q + k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w4[k] = 0u;
+      }
+      *reinterpret_cast<uint4*>(pw + fm_swz(m0)) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
   };
   auto stage_window = [&](const Item& x) {
     const Win w = win_of(x);
@@ -890,14 +942,14 @@ __global__ __launch_bounds__(256) void fir_q7_mfma_kernel(int T, const int8_t* _
   load_window(cur);
   for (;;) {
     __syncthreads();                                     // the previous item's reads (and the DMA's landing)
-    stage_window(cur);
+    if constexpr (ALN) stage_window_aln(cur); else stage_window(cur);
     __syncthreads();
     const uint32_t nxt = it + gridDim.x;
     const Item next = item_of(nxt < items ? nxt : it);
     if (nxt < items) load_window(next);                  // in flight under this item's MFMAs
     if (1024 * wid < cur.count) {
       const int i = L & 31, h = L >> 5;
-      const uint4* img = imgl + cur.d * KS * 64 + L;
+      const uint4* img = imgl + (cur.d - d_base) * KS * 64 + L;
       i32x16 acc = {};
       const int mb = 1024 * wid + 32 * i + 16 * h;
 #pragma unroll
@@ -957,16 +1009,23 @@ bool fir_q7_mfma_launch(const int8_t* coeffs, int T, const int8_t* src, int8_t* 
   const uint32_t nchunks = (B + kFmChunk - 1) / kFmChunk;
   const uint64_t items = (uint64_t)nchunks * batch;
   if (items < 256 || items > 0x7fffffffull) return false;
-  const int ks = (T + 34 + 31) / 32;                     // K >= numTaps - 1 + 31 + d (d <= 3) + 1
+  // aligned mode: shift d16 = (-T1) mod 16 (blockSize % 16 == 0, 16-B aligned data), K >= numTaps + d16 + 31;
+  // otherwise the window shift d <= 3 per item, K >= numTaps + 34
+  const int d16 = (16 - (T - 1) % 16) % 16;
+  const int ks_aln = (T + d16 + 31 + 31) / 32;
+  const bool aln = MI355X_FIR_Q7_ALN && B % 16 == 0 && ((uintptr_t)src & 15) == 0 && ks_aln <= kFmMaxKS;
+  const int ks = aln ? ks_aln : (T + 34 + 31) / 32;
+  const int d_base = aln ? d16 : 0;
   const size_t img_bytes = (size_t)4 * ks * 64 * 16;
   void* buf = nullptr;
   if (hipMallocAsync(&buf, img_bytes, st) != hipSuccess) return false;
   uint4* img = (uint4*)buf;
-  hipLaunchKernelGGL(fir_q7_coef_image_kernel, dim3((4 * ks * 64 + 255) / 256), dim3(256), 0, st, coeffs, T, ks, img);
+  hipLaunchKernelGGL(fir_q7_coef_image_kernel, dim3((4 * ks * 64 + 255) / 256), dim3(256), 0, st, coeffs, T, ks, d_base, img);
 #define F7_CASE(K)                                                                                              \
   case K: {                                                                                                     \
-    const int g = persistent_grid((const void*)fir_q7_mfma_kernel<K>, 256, 0, items);                          \
-    hipLaunchKernelGGL(fir_q7_mfma_kernel<K>, dim3(g), dim3(256), 0, st, T, src, dst, B, hist_in, nchunks,     \
+    auto kern = aln ? fir_q7_mfma_kernel<K, true> : fir_q7_mfma_kernel<K, false>;                               \
+    const int g = persistent_grid((const void*)kern, 256, 0, items);                                            \
+    hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, st, T, d_base, src, dst, B, hist_in, nchunks,               \
                        (uint32_t)items, (const uint4*)img);                                                     \
     break;                                                                                                      \
   }
