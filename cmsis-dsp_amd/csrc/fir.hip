@@ -942,8 +942,16 @@ __global__ void fir_hist_kernel(const T* __restrict__ src, T* __restrict__ hist,
                                 uint32_t B, int T1, uint32_t batch, uint32_t start) {
   const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (g >= (uint64_t)batch * T1) return;
-  const uint64_t f = g / T1;
-  const int j = (int)(g % T1);
+  uint64_t f;
+  int j;
+  if ((uint64_t)batch * T1 <= 0xffffffffull) {      // 32-bit division (the 64-bit one was most of the kernel)
+    const uint32_t g32 = (uint32_t)g;
+    f = g32 / (uint32_t)T1;
+    j = (int)(g32 - (uint32_t)f * (uint32_t)T1);
+  } else {
+    f = g / T1;
+    j = (int)(g % T1);
+  }
   const int64_t sidx = (int64_t)start + j;          // index into s of the new history word j
   hist[g] = sidx < T1 ? hist_in[f * T1 + sidx] : src[f * B + (sidx - T1)];
 }
