@@ -348,9 +348,9 @@ constexpr int kPPSlot = 32768, kPPB = 16384;           // slot bytes; B region o
 __device__ __forceinline__ uint32_t q7_lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
-template <int N> __device__ __forceinline__ void q7_wait_vm() {   // s_waitcnt vmcnt(N), N < 16
-  static_assert(N >= 0 && N < 16, "vmcnt");
-  __builtin_amdgcn_s_waitcnt(0xF70 | N);
+template <int N> __device__ __forceinline__ void q7_wait_vm() {   // s_waitcnt vmcnt(N), N < 64
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt(0xF70 | (N & 15) | ((N >> 4) << 14));
 }
 }  // namespace
 
@@ -566,6 +566,503 @@ __global__ __launch_bounds__(512, 1) void mat_mult_q7_pp_kernel(const int8_t* __
 #endif
 }
 
+// ============================================================================================
+// K a multiple of 128: the same ping-pong with 128-deep chunks (round 6, second pass).
+//
+// The stamps of the kernel above put a floor of ≈ 660 cycles under an interval of 16 MFMAs (512
+// cycles of matrix core): ≈ 148 cycles of every barrier interval are the hand-over between the
+// groups, whatever the interval holds (32 MFMAs per interval: 1,172 cycles, MI355X_Q7_DIAG=4).
+// So here a chunk is 128 k-bytes and an interval holds 32 MFMAs per wave (4 k-steps x 4 x 2
+// blocks; 96 fragment VGPRs, 128 accumulators).  A 128-deep chunk is 64 KiB (A 2 x 16 KiB, one
+// half per group, + B 32 KiB) and the whole 160 KiB array is the ring:
+//   A0 (group 0's 128 rows) 2 slots [0, 32K), A1 2 slots [32K, 64K), B 3 slots [64K, 160K); chunk
+//   s in A slot s & 1 and B slot s % 3.  A rows of 128 B, 16-B chunk c of row r at c ^ ((r >> 1) & 7)
+//   (every 16-lane group of a ds_read_b128 covers the 64 banks once); B k-rows of 256 B, chunk c of
+//   k-row k at c ^ 2 (k & 7) (as above).
+// Barrier interval 2s: group 0 reads chunk s (L_s) while group 1 runs M_{s-1}; interval 2s + 1:
+// group 1 reads chunk s, group 0 runs M_s.  Refills (8 DMA pieces per wave and L segment): group 0
+// in L_s issues A1(s + 1) and the first half of B(s + 2); group 1 in L_s issues A0(s + 2) and the
+// second half of B(s + 2).  An L segment ends with vmcnt(its own pieces): everything the group
+// issued one L segment earlier has landed; M segments wait for nothing.
+//  * RAW: A1(s + 1) (issued interval 2s) is waited at the end of interval 2s + 2, first read in
+//    2s + 3; B(s + 2) halves (2s, 2s + 1) at the end of 2s + 2 / 2s + 3, first read 2s + 4; A0(s + 2)
+//    (2s + 1) at the end of 2s + 3, first read 2s + 4.  Issue to wait: about three intervals (the
+//    two-slot B ring of the first version waited after two, and that wait cost ≈ 400 cycles a
+//    step: tools/probes/q7_stamps, MI355X_Q7_DIAG=5).
+//  * WAR: an L segment retires its fragment reads (lgkmcnt(0)) before its closing barrier; B(s + 2)
+//    refills B(s - 1)'s slot (last read in 2s - 1), A1(s + 1) A1(s - 1)'s (2s - 1), A0(s + 2) A0(s)'s
+//    (2s), each issued after that barrier.
+// Epilogue: a tile's output leaves in the group's NEXT L segment, after its waits (the first MFMAs
+// of the next tile take C = 0 and come after it), so the stores are older than the loads of the L
+// segment after that and the counted wait there still holds (loads return in order; a store only
+// adds to the count).
+#ifndef MI355X_Q7_PP2
+#define MI355X_Q7_PP2 1
+#endif
+#ifndef MI355X_Q7_CSTORE
+#define MI355X_Q7_CSTORE 0
+#endif
+#ifndef MI355X_Q7_LDSEPI    // epilogue stores through a wave's LDS scratch (16 rows x 64 B per store)
+#define MI355X_Q7_LDSEPI 1
+#endif
+#ifndef MI355X_Q7_MDMA      // DMA pieces issued between the MFMAs of the M segments (not in the L segments)
+#define MI355X_Q7_MDMA 1
+#endif
+#ifndef MI355X_Q7_DMA_FIRST // L segment order: the DMA pieces before the fragment reads
+#define MI355X_Q7_DMA_FIRST 0
+#endif
+#if MI355X_Q7_DIAG == 5                                 // diagnostic only: no counted waits in the loop
+#define PP2_WAIT(n) ((void)0)
+#else
+#define PP2_WAIT(n) q7_wait_vm<n>()
+#endif
+
+// (q7)__SSAT(acc >> 7, 8) of a wave's 128 x 64 C^T accumulator tile, from registers (see the
+// comment above mat_mult_q7_pp_kernel); c = the lane's first output byte (block i = 0, j = 0).
+// The doubling is one 64-bit shift per register pair: the high word gains the low word's sign bit
+// as its bit 0, which never moves the high byte of sat16 (2 x_hi is even: 2 x_hi + 1 stays inside
+// the int16 range exactly when 2 x_hi does, and saturates the same way outside it).
+__device__ __forceinline__ void q7_store_regs(const i32x16 (&acc)[4][2], int8_t* c, int N) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      uint32_t d[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint64_t w0, w1;
+        asm("v_lshlrev_b64 %0, 1, %1" : "=v"(w0) : "v"(__builtin_bit_cast(uint64_t, v2i32{acc[i][j][4 * q], acc[i][j][4 * q + 1]})));
+        asm("v_lshlrev_b64 %0, 1, %1" : "=v"(w1) : "v"(__builtin_bit_cast(uint64_t, v2i32{acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]})));
+        const auto lo = __builtin_amdgcn_cvt_pk_i16((int)(uint32_t)w0, (int)(uint32_t)(w0 >> 32));
+        const auto hi = __builtin_amdgcn_cvt_pk_i16((int)(uint32_t)w1, (int)(uint32_t)(w1 >> 32));
+        d[q] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi), __builtin_bit_cast(uint32_t, lo), 0x07050301u);
+      }
+      const auto s02 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+      const auto s13 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+#if MI355X_Q7_CSTORE                                    // diagnostic only (wrong places): 1 KiB contiguous per store
+      *reinterpret_cast<uint4*>(c - (size_t)(threadIdx.x & 31) * N - 16 * ((threadIdx.x >> 5) & 1) - 64 * ((threadIdx.x >> 6) & 3) +
+                                8192 * ((threadIdx.x >> 6) & 3) + 1024 * (2 * i + j) + 16 * (threadIdx.x & 63)) =
+          make_uint4(s02[0], s02[1], s13[0], s13[1]);
+#else
+      *reinterpret_cast<uint4*>(c + (size_t)(32 * i) * N + 32 * j) = make_uint4(s02[0], s02[1], s13[0], s13[1]);
+#endif
+    }
+}
+
+__global__ __launch_bounds__(512, 1) void mat_mult_q7_pp2_kernel(const int8_t* __restrict__ A, const int8_t* __restrict__ B,
+                                                                 int8_t* __restrict__ C, int M, int K, int N,
+                                                                 uint32_t T) {
+  constexpr uint32_t kGrpA = 32768, kSlotA = 16384, kB0 = 65536, kSlotB = 32768;
+  __shared__ __attribute__((aligned(1024))) int8_t lds[163840];
+  const int tilesN = N / 256, tpm = tilesN * (M / 256);
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  uint32_t t_first, t_stride, n_t;                      // this workgroup's tiles (as above)
+  if (T % 8 == 0 && G % 8 == 0) {
+    const uint32_t per = T / 8, j = b / 8, gx = G / 8;
+    t_first = (b % 8) * per + j;
+    t_stride = gx;
+    n_t = j < per ? (per - j + gx - 1) / gx : 0;
+  } else {
+    t_first = b;
+    t_stride = G;
+    n_t = b < T ? (T - b + G - 1) / G : 0;
+  }
+  const int tid = threadIdx.x, L = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3, wq = wid & 3;
+  const int r = L & 31, h = L >> 5, li = L & 15, gq = (L >> 4) & 1;
+#if MI355X_Q7_STAMP == 1
+  const bool stamp = b < 64 && (wid == 0 || wid == 4) && L == 0;
+  int ns = 0;
+  auto STAMP = [&]() {
+    if (stamp && ns < 160) q7_stamp_buf[b][wid >> 2][ns] = __builtin_amdgcn_s_memtime();
+    ++ns;
+  };
+#else
+  auto STAMP = [&]() {};
+#endif
+#if MI355X_Q7_STAMP == 2    // diagnostic: s_memtime ticks per loop phase, written once at the end
+  uint32_t ph[8] = {};
+  auto cyc = [&]() -> uint32_t {
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t v = (uint32_t)__builtin_amdgcn_s_memtime();   // (SMEM: only at points with no LDS read in flight)
+    __builtin_amdgcn_sched_barrier(0);
+    return v;
+  };
+  uint32_t tc = cyc();
+  auto PH = [&](int k) { const uint32_t t = cyc(); ph[k] += t - tc; tc = t; };
+#else
+  auto PH = [&](int) {};
+#endif
+  const int nc = K / 128;
+  const uint32_t total = n_t * (uint32_t)nc;
+
+  auto tile_origin = [&](uint32_t k, int& row0, int& col0) -> uint32_t {   // k-th tile: matrix index
+    const uint32_t t = t_first + k * t_stride;
+    const uint32_t bz = t / (uint32_t)tpm, tt = t % (uint32_t)tpm;
+    row0 = (int)(tt / (uint32_t)tilesN) * 256;
+    col0 = (int)(tt % (uint32_t)tilesN) * 256;
+    return bz;
+  };
+  auto chunk_src = [&](uint32_t g, const int8_t*& aT, const int8_t*& bT) {   // stream chunk g
+    const uint32_t kt = g / (uint32_t)nc;
+    const int ic = (int)(g - kt * (uint32_t)nc);
+    int row0, col0;
+    const uint32_t bz = tile_origin(kt, row0, col0);
+    aT = A + (size_t)bz * M * K + (size_t)row0 * K + 128 * ic;
+    bT = B + (size_t)bz * K * N + (size_t)(128 * ic) * N + col0;
+  };
+  // per-lane DMA sources (the swizzles applied to the source address; LDS lane-linear)
+  // (32-bit: < 16 rows of at most 65535 bytes)
+  const uint32_t aLane0 = (uint32_t)((L >> 3) * K + 16 * ((L & 7) ^ (L >> 4)));
+  const uint32_t aLane1 = (uint32_t)((8 + (L >> 3)) * K + 16 * ((L & 7) ^ (4 + (L >> 4))));
+  const uint32_t bLane0 = (uint32_t)((L >> 4) * N + 16 * ((L & 15) ^ (2 * (L >> 4))));
+  const uint32_t bLane1 = (uint32_t)((4 + (L >> 4)) * N + 16 * ((L & 15) ^ (2 * (4 + (L >> 4)))));
+  auto dma = [&](const int8_t* src, int8_t* dst) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  };
+  auto issue_B = [&](uint32_t g, int half, int slot) {  // B(g) k-rows 64 half + 16 wq .. + 15: 4 pieces
+    const int8_t *aT, *bT;
+    chunk_src(g, aT, bT);
+    int8_t* d = lds + kB0 + slot * kSlotB + 16384 * half + 4096 * wq;
+    const int8_t* s = bT + (size_t)(64 * half + 16 * wq) * N;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dma(s + (size_t)(8 * (q >> 1)) * N + (q & 1 ? bLane1 : bLane0), d + 1024 * q);
+  };
+  auto issue_A = [&](uint32_t g, int grp) {             // A(g) rows 128 grp + 32 wq .. + 31: 4 pieces
+    const int8_t *aT, *bT;
+    chunk_src(g, aT, bT);
+    int8_t* d = lds + grp * kGrpA + (g & 1) * kSlotA + 4096 * wq;
+    const int8_t* s = aT + (size_t)(128 * grp + 32 * wq) * K;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dma(s + (size_t)(16 * (q >> 1)) * K + (q & 1 ? aLane1 : aLane0), d + 1024 * q);
+  };
+
+  // single pieces (MI355X_Q7_MDMA: issued between the MFMAs): q-th piece of a 4-piece A or B group
+  auto src_A = [&](uint32_t g, int grp, const int8_t*& s, int8_t*& d) {
+    const int8_t *aT, *bT;
+    chunk_src(g, aT, bT);
+    d = lds + grp * kGrpA + (g & 1) * kSlotA + 4096 * wq;
+    s = aT + (size_t)(128 * grp + 32 * wq) * K;
+  };
+  auto src_B = [&](uint32_t g, int half, int slot, const int8_t*& s, int8_t*& d) {
+    const int8_t *aT, *bT;
+    chunk_src(g, aT, bT);
+    d = lds + kB0 + slot * kSlotB + 16384 * half + 4096 * wq;
+    s = bT + (size_t)(64 * half + 16 * wq) * N;
+  };
+  auto piece_A = [&](const int8_t* s, int8_t* d, int q) { dma(s + (size_t)(16 * (q >> 1)) * K + (q & 1 ? aLane1 : aLane0), d + 1024 * q); };
+  auto piece_B = [&](const int8_t* s, int8_t* d, int q) { dma(s + (size_t)(8 * (q >> 1)) * N + (q & 1 ? bLane1 : bLane0), d + 1024 * q); };
+
+  // fragment bases (slot 0): A k-step kk of block i at aK[kk] + 4096 i; B as the kernel above
+  const uint32_t lb = q7_lds_addr(lds);
+  const uint32_t aRow = lb + wm * kGrpA + r * 128;
+  const int fr = (r >> 1) & 7;
+  const uint32_t aK0 = aRow + 16 * ((0 + h) ^ fr), aK1 = aRow + 16 * ((2 + h) ^ fr);
+  const uint32_t aK2 = aRow + 16 * ((4 + h) ^ fr), aK3 = aRow + 16 * ((6 + h) ^ fr);
+  const int bkr = 16 * h + (li >> 1);
+  const uint32_t bJ0 = lb + kB0 + bkr * 256 + 16 * ((4 * wn + 0 + gq) ^ (2 * (bkr & 7))) + 8 * (li & 1);
+  const uint32_t bJ1 = lb + kB0 + bkr * 256 + 16 * ((4 * wn + 2 + gq) ^ (2 * (bkr & 7))) + 8 * (li & 1);
+
+  i32x16 acc[4][2];
+  i32x4 fa[4][4] = {};
+  v2i32 fl[4][2] = {}, fh[4][2] = {};                   // B fragments: [kk][j] lo / hi 8 k-rows
+#define Q7A(dst, base, off) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(off))
+#define Q7B(dst, base, off) asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(off))
+#define Q7KK(kk, aK)                                                                                  \
+  {                                                                                                   \
+    const uint32_t a_ = aK + sa;                                                                      \
+    Q7A(fa[kk][0], a_, 0); Q7A(fa[kk][1], a_, 4096); Q7A(fa[kk][2], a_, 8192); Q7A(fa[kk][3], a_, 12288); \
+    Q7B(fl[kk][0], b0, 8192 * kk); Q7B(fh[kk][0], b0, 8192 * kk + 2048);                              \
+    Q7B(fl[kk][1], b1, 8192 * kk); Q7B(fh[kk][1], b1, 8192 * kk + 2048);                              \
+  }
+  auto read_frags = [&](uint32_t sa, uint32_t sb) {     // slot offsets of A and B
+#if MI355X_Q7_DIAG == 2 || MI355X_Q7_DIAG == 3         // diagnostic only: no fragment reads
+    return;
+#endif
+    const uint32_t b0 = bJ0 + sb, b1 = bJ1 + sb;
+    Q7KK(0, aK0) Q7KK(1, aK1) Q7KK(2, aK2) Q7KK(3, aK3)
+  };
+#undef Q7KK
+#undef Q7A
+#undef Q7B
+  auto wait_frags = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fa[0][2]), "+v"(fa[0][3]), "+v"(fa[1][0]), "+v"(fa[1][1]),
+                   "+v"(fa[1][2]), "+v"(fa[1][3]), "+v"(fa[2][0]), "+v"(fa[2][1]), "+v"(fa[2][2]), "+v"(fa[2][3]),
+                   "+v"(fa[3][0]), "+v"(fa[3][1]), "+v"(fa[3][2]), "+v"(fa[3][3]));
+    asm volatile(""
+                 : "+v"(fl[0][0]), "+v"(fh[0][0]), "+v"(fl[0][1]), "+v"(fh[0][1]), "+v"(fl[1][0]), "+v"(fh[1][0]),
+                   "+v"(fl[1][1]), "+v"(fh[1][1]), "+v"(fl[2][0]), "+v"(fh[2][0]), "+v"(fl[2][1]), "+v"(fh[2][1]),
+                   "+v"(fl[3][0]), "+v"(fh[3][0]), "+v"(fl[3][1]), "+v"(fh[3][1]));
+  };
+  auto fb = [&](int kk, int j) { return i32x4{fl[kk][j].x, fl[kk][j].y, fh[kk][j].x, fh[kk][j].y}; };
+  auto mma = [&](bool first) {
+    if (first) {                                        // a tile's first chunk: C operand 0
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb(0, j), fa[0][i], i32x16{}, 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb(0, j), fa[0][i], acc[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int kk = 1; kk < 4; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb(kk, j), fa[kk][i], acc[i][j], 0, 0, 0);
+  };
+  auto mma4 = [&](int kk, int i0, bool first) {         // 4 of the 32 MFMAs: k-step kk, blocks i0, i0 + 1
+#pragma unroll
+    for (int i = i0; i < i0 + 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = first ? __builtin_amdgcn_mfma_i32_32x32x32_i8(fb(kk, j), fa[kk][i], i32x16{}, 0, 0, 0)
+                          : __builtin_amdgcn_mfma_i32_32x32x32_i8(fb(kk, j), fa[kk][i], acc[i][j], 0, 0, 0);
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    STAMP();
+  };
+  // sc: the wave's 4 KiB of scratch (its share of the group's A slot that this L segment has just
+  // read and retired, refilled only after the next barrier)
+  auto store_tile = [&](uint32_t k, int8_t* sc) {
+#if MI355X_Q7_NOEPI                                     // diagnostic only: no output stores
+    if (acc[0][0][0] != 0x7fffffff) return;
+#endif
+    int row0, col0;
+    const uint32_t bz = tile_origin(k, row0, col0);
+#if MI355X_Q7_LDSEPI
+    // through LDS: each store covers 16 rows x 64 B (four lanes per row) instead of 32 rows x 32 B.
+    // Scratch rows of 64 B, 16-B chunk c of row rho at c ^ ((rho >> 1) & 3): conflict-free for the
+    // 8-lane groups of ds_write_b128 and the 16-lane groups of ds_read_b128.  The scratch accesses
+    // are inline asm: the compiler would otherwise order them behind the LDS-DMA in flight
+    // (vmcnt(0)), which targets other slots.  Buffer stores: the wave's output rows as a buffer
+    // resource (SGPRs) + a 32-bit lane offset, the uniform row offset in soffset.
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t cb = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(C + (size_t)bz * M * N + (size_t)(row0 + 128 * wm) * N + col0 + 64 * wn), (short)0, 0x7fffffff, 0x00020000);
+    const int wr = L >> 2, wc = (L & 3) ^ ((wr >> 1) & 3);
+    const uint32_t co = (uint32_t)(wr * N + 16 * (L & 3));
+    const uint32_t sb = q7_lds_addr(sc), rda = sb + wr * 64 + 16 * wc;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = 2 * half + ii;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          uint32_t d[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            uint64_t w0, w1;
+            asm("v_lshlrev_b64 %0, 1, %1" : "=v"(w0) : "v"(__builtin_bit_cast(uint64_t, v2i32{acc[i][j][4 * q], acc[i][j][4 * q + 1]})));
+            asm("v_lshlrev_b64 %0, 1, %1" : "=v"(w1) : "v"(__builtin_bit_cast(uint64_t, v2i32{acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]})));
+            const auto lo = __builtin_amdgcn_cvt_pk_i16((int)(uint32_t)w0, (int)(uint32_t)(w0 >> 32));
+            const auto hi = __builtin_amdgcn_cvt_pk_i16((int)(uint32_t)w1, (int)(uint32_t)(w1 >> 32));
+            d[q] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi), __builtin_bit_cast(uint32_t, lo), 0x07050301u);
+          }
+          const auto s02 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+          const auto s13 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+          const int rho = 32 * ii + r, c = 2 * j + h;                  // scratch row, 16-B chunk
+          const uint32_t wa = sb + rho * 64 + 16 * (c ^ ((rho >> 1) & 3));
+          asm volatile("ds_write_b128 %0, %1" ::"v"(wa), "v"(u32x4{s02[0], s02[1], s13[0], s13[1]}) : "memory");
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; t += 2) {                                 // rows 16 t + (L >> 2) of this half
+        u32x4 v0, v1;
+        asm volatile("ds_read_b128 %0, %2 offset:%3\n\tds_read_b128 %1, %2 offset:%4\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(v0), "=v"(v1) : "v"(rda), "i"(1024 * t), "i"(1024 * (t + 1)) : "memory");
+        __builtin_amdgcn_raw_buffer_store_b128(v0, cb, (int)co, (64 * half + 16 * t) * N, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v1, cb, (int)co, (64 * half + 16 * t + 16) * N, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#else
+    (void)sc;
+    q7_store_regs(acc, C + (size_t)bz * M * N + (size_t)(row0 + 128 * wm + r) * N + col0 + 64 * wn + 16 * h, N);
+#endif
+  };
+
+  if (total == 0) return;                               // (uniform per workgroup)
+#if MI355X_Q7_STAMP == 1
+  if (stamp) q7_stamp_real[b][wid >> 2][0] = __builtin_amdgcn_s_memrealtime();
+#endif
+  STAMP();
+#if MI355X_Q7_MDMA
+  // prologue: B(0), B(1), B(2) second half, A0(0), A0(1), A1(0), A1(1)
+  if (wm == 0) {
+    issue_B(0, 0, 0);
+    issue_B(0, 1, 0);
+    issue_A(0, 0);
+    if (total > 1) issue_A(1, 0);
+  } else {
+    issue_A(0, 1);
+    if (total > 1) {
+      issue_B(1, 0, 1);
+      issue_B(1, 1, 1);
+      issue_A(1, 1);
+    }
+    if (total > 2) issue_B(2, 1, 2);
+  }
+#else
+  if (wm == 0) {
+    issue_B(0, 0, 0);
+    issue_B(0, 1, 0);
+    issue_A(0, 0);
+    if (total > 1) issue_A(1, 0);
+  } else {
+    issue_A(0, 1);
+    if (total > 1) {
+      issue_B(1, 0, 1);
+      issue_B(1, 1, 1);
+    }
+  }
+#endif
+  // vmcnt(0) lgkmcnt(0): also retires the kernel-argument loads here, so that the waitcnt pass
+  // does not leave an lgkmcnt(0) on the argument pointers inside the loop (where it would wait for
+  // the inline-asm fragment reads too)
+  __builtin_amdgcn_s_waitcnt(0x0070);
+  barrier();
+  if (wm) barrier();                                    // group 1 runs one barrier behind
+  uint32_t k = 0;                                       // tile being computed
+  int p = 0;                                            // its chunk
+  bool pend = false;                                    // tile k - 1's output still in acc
+  int rs = 0, is = 2;                                   // B slots of chunk g and of chunk g + 2
+#if MI355X_Q7_MDMA
+  // DMA in the M segments: group 0 in M_g issues A0(g + 2) and B(g + 2)'s first half, group 1 in
+  // M_g A1(g + 2) and B(g + 3)'s second half, one piece after every 4 MFMAs; an M segment ends with
+  // vmcnt(its own pieces + the stores of the L segment before it): everything the group issued in
+  // its previous M segment has landed (vmcnt counts loads, stores and LDS-DMA in issue order).
+  for (uint32_t g = 0; g < total; ++g) {
+    PH(7);
+    read_frags((g & 1) * kSlotA, rs * kSlotB);
+    const int8_t *pa = nullptr, *pb = nullptr;
+    int8_t *da = nullptr, *db = nullptr;
+    const bool ha = g + 2 < total, hb = wm == 0 ? g + 2 < total : g + 3 < total;
+    if (ha) src_A(g + 2, wm, pa, da);
+    if (hb) src_B(wm == 0 ? g + 2 : g + 3, wm, wm == 0 ? is : rs, pb, db);
+    wait_frags();
+    PH(3);
+    const bool st = pend;
+    if (pend) {
+      store_tile(k - 1, lds + wm * kGrpA + (g & 1) * kSlotA + 4096 * wq);
+      pend = false;
+    }
+#if MI355X_Q7_MDMA == 2                                 // the A pieces here (this slot's reads have retired)
+    if (ha) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) piece_A(pa, da, q);
+    }
+#endif
+    PH(4);
+    barrier();
+    PH(5);
+    __builtin_amdgcn_s_setprio(1);
+    const bool first = p == 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {                       // 8 x (4 MFMAs, one piece)
+      if (e < 2 && first)                               // a tile's first chunk: C operand 0 (a branch, not selects)
+        mma4(0, 2 * e, true);
+      else
+        mma4(e >> 1, 2 * (e & 1), false);
+      __builtin_amdgcn_sched_barrier(0);
+#if MI355X_Q7_MDMA == 2                                 // the B pieces: one after every 8 MFMAs
+      if ((e & 1) && hb) piece_B(pb, db, e >> 1);
+#else
+      if (e < 4) {
+        if (ha) piece_A(pa, da, e);
+      } else {
+        if (hb) piece_B(pb, db, e - 4);
+      }
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    const int nv = (ha ? 4 : 0) + (hb ? 4 : 0) + (st ? 8 : 0);
+    if (nv == 16) PP2_WAIT(16); else if (nv == 12) PP2_WAIT(12); else if (nv == 8) PP2_WAIT(8);
+    else if (nv == 4) PP2_WAIT(4); else PP2_WAIT(0);
+    PH(6);
+    barrier();
+    if (++p == nc) {
+      p = 0;
+      ++k;
+      pend = true;
+    }
+    rs = rs == 2 ? 0 : rs + 1;
+    is = is == 2 ? 0 : is + 1;
+  }
+#else
+  for (uint32_t g = 0; g < total; ++g) {
+    PH(7);
+#if !MI355X_Q7_DMA_FIRST
+    read_frags((g & 1) * kSlotA, rs * kSlotB);          // (aRow holds the group's region)
+#endif
+    uint32_t nvm = 0;                                   // pieces issued in this L segment
+#if MI355X_Q7_DIAG == 1 || MI355X_Q7_DIAG == 3         // diagnostic only: no DMA past the prologue
+    if (false) {
+#else
+    if (true) {
+#endif
+      if (wm == 0) {
+        if (g + 1 < total) { issue_A(g + 1, 1); nvm += 4; }
+        if (g + 2 < total) { issue_B(g + 2, 0, is); nvm += 4; }
+      } else if (g + 2 < total) {
+        issue_A(g + 2, 0);
+        issue_B(g + 2, 1, is);
+        nvm = 8;
+      }
+    }
+#if MI355X_Q7_DMA_FIRST
+    read_frags((g & 1) * kSlotA, rs * kSlotB);          // (aRow holds the group's region)
+#endif
+    // everything this group issued one L segment earlier has landed (nvm is wave-uniform)
+    if (nvm == 8) PP2_WAIT(8); else if (nvm == 4) PP2_WAIT(4); else PP2_WAIT(0);
+    wait_frags();                                       // this slot's reads retired before the barrier
+    PH(3);
+    if (pend) {                                         // the previous tile's output, after the waits
+      store_tile(k - 1, lds + wm * kGrpA + (g & 1) * kSlotA + 4096 * wq);
+      pend = false;
+    }
+    PH(4);
+    barrier();
+    PH(5);
+    __builtin_amdgcn_s_setprio(1);
+#if MI355X_Q7_DIAG != 6                                 // diagnostic only: no MFMAs (data movement alone)
+    mma(p == 0);
+#endif
+    __builtin_amdgcn_s_setprio(0);
+    PH(6);
+    barrier();
+    if (++p == nc) {
+      p = 0;
+      ++k;
+      pend = true;
+    }
+    rs = rs == 2 ? 0 : rs + 1;
+    is = is == 2 ? 0 : is + 1;
+  }
+#endif
+  if (pend) {                                           // (no DMA in flight any more)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7");       // the last MFMAs' results (the asm reads hide them from the hazard pass)
+    store_tile(k - 1, lds + wm * kGrpA + 4096 * wq);
+  }
+  if (!wm) barrier();                                   // both groups: the same barrier count
+#if MI355X_Q7_STAMP == 1
+  if (stamp) q7_stamp_real[b][wid >> 2][1] = __builtin_amdgcn_s_memrealtime();
+#elif MI355X_Q7_STAMP == 2
+  if (b < 64 && (wid == 0 || wid == 4) && L == 0)
+    for (int e = 0; e < 8; ++e) q7_stamp_buf[b][wid >> 2][e] = ph[e];
+#endif
+}
+
 hipError_t mat_mult_q7_launch(int m, int k, int n, const int8_t* a, const int8_t* b, int8_t* c, uint32_t batch,
                               hipStream_t st) {
   if (batch == 0 || m == 0 || n == 0) return hipSuccess;
@@ -575,6 +1072,7 @@ hipError_t mat_mult_q7_launch(int m, int k, int n, const int8_t* a, const int8_t
   const bool full = m % kQ7BM == 0 && n % kQ7BN == 0 && k % kQ7KT == 0 && ((uintptr_t)a & 15) == 0 &&
                     ((uintptr_t)b & 15) == 0 && ((uintptr_t)c & 15) == 0;
   const dim3 grid((uint32_t)(tiles * batch));
+  const bool pp2 = MI355X_Q7_PP2 && k % 128 == 0;
   if (MI355X_Q7_PP && kQ7BN == 256 && m % 256 == 0 && n % 256 == 0 && k % 64 == 0 && ((uintptr_t)a & 15) == 0 &&
       ((uintptr_t)b & 15) == 0 && ((uintptr_t)c & 15) == 0 && ((size_t)n & 15) == 0) {
     // one persistent workgroup per CU (128 KiB of LDS each), a multiple of 8 so every XCD gets
@@ -587,7 +1085,10 @@ hipError_t mat_mult_q7_launch(int m, int k, int n, const int8_t* a, const int8_t
     const uint64_t T = tiles * batch;
     uint32_t g = (uint32_t)std::min<uint64_t>(T, (uint64_t)(cus / 8) * 8 * MI355X_Q7_WGPC);
     if (g >= 8) g -= g % 8;
-    hipLaunchKernelGGL(mat_mult_q7_pp_kernel, dim3(g), dim3(512), 0, st, a, b, c, m, k, n, (uint32_t)T);
+    if (pp2)
+      hipLaunchKernelGGL(mat_mult_q7_pp2_kernel, dim3(g), dim3(512), 0, st, a, b, c, m, k, n, (uint32_t)T);
+    else
+      hipLaunchKernelGGL(mat_mult_q7_pp_kernel, dim3(g), dim3(512), 0, st, a, b, c, m, k, n, (uint32_t)T);
     return hipGetLastError();
   }
   if (full)

@@ -620,6 +620,10 @@ def _q7_exact(a, b):
                                         # deep ring, extremes through every slot
                                         (256, 192, 256, None), (768, 4096, 512, None), (512, 4032, 256, "min"), (256, 256, 512, "min"),
                                         (256, 1216, 768, "max"),
+                                        # K % 128 == 0: the 128-deep ping-pong (two-slot ring): 1, 2, 3,
+                                        # 9 chunks, extremes through both slots of every region
+                                        (256, 128, 256, "mixed"), (256, 384, 256, None), (512, 1152, 256, "min"),
+                                        (256, 2048, 256, "max"),
                                         # K % 16 == 0 but not % 64, ragged N: vector loads with a tail
                                         (256, 80, 272, None)])
 def test_mat_mult_q7_bitexact(dsp, torch_gpu, ref, m, k, n, fill):
@@ -703,3 +707,22 @@ def test_mat_mult_q7_pingpong_repeatable(dsp, torch_gpu):
     for i in (0, 11):
         s = np.matmul(a[i].astype(np.int32), b[i].astype(np.int32))
         assert got[i].tobytes() == np.clip(s >> 7, -128, 127).astype(np.int8).tobytes(), i
+
+
+@pytest.mark.parametrize("batch,m,k,n", [(1, 4608, 256, 4096), (81, 512, 512, 512)])
+def test_mat_mult_q7_pp2_multitile(dsp, torch_gpu, batch, m, k, n):
+    """The 128-deep ping-pong kernel with several tiles per persistent workgroup, so the chunk
+    stream (and its refills: B one chunk ahead, A0 two) runs across tile boundaries: 288 tiles
+    (XCD-contiguous runs, tiles % 8 == 0) and 81 x 4 = 324 tiles (round robin), against exact
+    products (float64 matmul: |sum| < 2^53)."""
+    torch = torch_gpu
+    rng = np.random.default_rng(batch + m + k)
+    a = rng.integers(-128, 128, (batch, m, k)).astype(np.int8)
+    b = rng.integers(-128, 128, (batch, k, n)).astype(np.int8)
+    A, B = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+    Cm = torch.empty((batch, m, n), dtype=torch.int8, device="cuda")
+    dsp.mat_mult_batch(A, B, Cm)
+    s = np.matmul(a.astype(np.float64), b.astype(np.float64)).astype(np.int64)
+    want = np.clip(s >> 7, -128, 127).astype(np.int8)
+    got = Cm.cpu().numpy()
+    assert got.tobytes() == want.tobytes(), np.argwhere(got != want)[:5]
