@@ -606,7 +606,7 @@ __global__ __launch_bounds__(512, 1) void mat_mult_q7_pp_kernel(const int8_t* __
 #define MI355X_Q7_LDSEPI 1
 #endif
 #ifndef MI355X_Q7_MDMA      // DMA pieces issued between the MFMAs of the M segments (not in the L segments)
-#define MI355X_Q7_MDMA 1
+#define MI355X_Q7_MDMA 2
 #endif
 #ifndef MI355X_Q7_DMA_FIRST // L segment order: the DMA pieces before the fragment reads
 #define MI355X_Q7_DMA_FIRST 0

@@ -1,7 +1,8 @@
 // In-kernel timestamps of the persistent ping-pong q7 GEMM (mat_mult_q7.hip, MI355X_Q7_STAMP):
 // s_memtime at every barrier of waves 0 (group 0) and 4 (group 1) of workgroups 0-63, for the
 // bench shape 1024^3 x 64.  Prints one JSON object: {"stamps": [[wg][group][k] ...]} (shader
-// clock ticks), analysed by tools/probes/q7_stamps.py.
+// clock ticks), analysed by tools/probes/q7_stamps.py.  With -DMI355X_Q7_STAMP=2 (the 128-deep
+// kernel) the same buffer holds per-segment tick sums instead (q7_stamps.py --phases).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DMI355X_Q7_STAMP=1 \
 //          tools/probes/q7_stamps.hip -o tools/probes/q7_stamps
 #include "../../cmsis-dsp_amd/csrc/mat_mult_q7.hip"

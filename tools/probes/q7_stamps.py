@@ -3,7 +3,11 @@
 s_memtime stamps at every barrier; the intervals between consecutive barriers are the ping-pong
 half-phases (one group's MFMA segment beside the other's read / DMA segment).
 
-usage: python tools/probes/q7_stamps.py stamps.json [more.json ...]
+A build with -DMI355X_Q7_STAMP=2 (the 128-deep kernel only) writes, instead, per workgroup and
+group the s_memtime ticks summed per loop segment (entries 3..7: L segment, epilogue, barrier after
+L, MFMA segment, barrier after M); `--phases` prints their means per step.
+
+usage: python tools/probes/q7_stamps.py [--phases] stamps.json [more.json ...]
 """
 import json
 import sys
@@ -33,6 +37,19 @@ def summary(path):
     return out
 
 
+def phases(path, steps=32):
+    d = json.load(open(path))
+    st = np.array(d["stamps"], dtype=np.int64)[:, :, :8]
+    names = ["L_segment", "epilogue", "barrier_after_L", "mfma_segment", "barrier_after_M"]
+    out = {"file": path, "launch_ms": d["ms"]}
+    for g in (0, 1):
+        m = st[:, g, :].mean(axis=0) / steps
+        out[f"group{g}"] = {n: round(float(v)) for n, v in zip(names, m[3:8])}
+    return out
+
+
 if __name__ == "__main__":
-    for p in sys.argv[1:]:
-        print(json.dumps(summary(p)))
+    args = sys.argv[1:]
+    ph = args and args[0] == "--phases"
+    for p in args[1:] if ph else args:
+        print(json.dumps(phases(p) if ph else summary(p)))
