@@ -580,22 +580,25 @@ __global__ __launch_bounds__(512, 1) void mat_mult_q7_pp_kernel(const int8_t* __
 //   (every 16-lane group of a ds_read_b128 covers the 64 banks once); B k-rows of 256 B, chunk c of
 //   k-row k at c ^ 2 (k & 7) (as above).
 // Barrier interval 2s: group 0 reads chunk s (L_s) while group 1 runs M_{s-1}; interval 2s + 1:
-// group 1 reads chunk s, group 0 runs M_s.  Refills (8 DMA pieces per wave and L segment): group 0
-// in L_s issues A1(s + 1) and the first half of B(s + 2); group 1 in L_s issues A0(s + 2) and the
-// second half of B(s + 2).  An L segment ends with vmcnt(its own pieces): everything the group
-// issued one L segment earlier has landed; M segments wait for nothing.
-//  * RAW: A1(s + 1) (issued interval 2s) is waited at the end of interval 2s + 2, first read in
-//    2s + 3; B(s + 2) halves (2s, 2s + 1) at the end of 2s + 2 / 2s + 3, first read 2s + 4; A0(s + 2)
-//    (2s + 1) at the end of 2s + 3, first read 2s + 4.  Issue to wait: about three intervals (the
-//    two-slot B ring of the first version waited after two, and that wait cost ≈ 400 cycles a
-//    step: tools/probes/q7_stamps, MI355X_Q7_DIAG=5).
-//  * WAR: an L segment retires its fragment reads (lgkmcnt(0)) before its closing barrier; B(s + 2)
-//    refills B(s - 1)'s slot (last read in 2s - 1), A1(s + 1) A1(s - 1)'s (2s - 1), A0(s + 2) A0(s)'s
-//    (2s), each issued after that barrier.
-// Epilogue: a tile's output leaves in the group's NEXT L segment, after its waits (the first MFMAs
-// of the next tile take C = 0 and come after it), so the stores are older than the loads of the L
-// segment after that and the counted wait there still holds (loads return in order; a store only
-// adds to the count).
+// group 1 reads chunk s, group 0 runs M_s.  L segments retire their fragment reads (lgkmcnt(0))
+// before their closing barrier, so a slot is free for a refill right after its last reader's
+// barrier.  Refill placement (MI355X_Q7_MDMA; the stamps of DESIGN §4 price each):
+//  * 2 (default): in L_s, after its reads retire, each group refills its own A half for chunk
+//    s + 2 (the slot it has just read); in M_s, one piece after every 8 MFMAs, group 0 issues the
+//    first half of B(s + 2), group 1 the second half of B(s + 3).  An M segment ends with
+//    vmcnt(the pieces and stores issued since the group's previous M segment): everything issued
+//    before that has landed.  RAW: A_g(s + 2) (L_s) and B(s + 2) (M_s / M_{s-1}) are waited at the
+//    end of M_{s+1} / M_s, before their first reader two or more intervals later; WAR: A_g(s + 2)
+//    refills the slot of A_g(s), read in L_s itself; B(s + 3) (group 1, M_s = interval 2s + 2) and
+//    B(s + 2) (group 0, M_s = 2s + 1) refill B(s)'s / B(s - 1)'s slot, last read in 2s + 1 / 2s - 1.
+//  * 1: all eight pieces between the MFMAs (group 0: A0(s + 2), B(s + 2) first half; group 1:
+//    A1(s + 2), B(s + 3) second half), the same waits.
+//  * 0: all pieces in the L segment after the reads (group 0: A1(s + 1), B(s + 2) first half; group
+//    1: A0(s + 2), B(s + 2) second half), each L segment ending with vmcnt(its own pieces).
+// Epilogue: a tile's output leaves in the group's NEXT L segment, after its reads retire (the first
+// MFMAs of the next tile take C = 0 and come after it), through the A slot it has just read; vmcnt
+// counts loads, stores and LDS-DMA in issue order, so the counted waits stay exact with stores in
+// flight (each counts the stores issued after the pieces it waits for).
 #ifndef MI355X_Q7_PP2
 #define MI355X_Q7_PP2 1
 #endif
